@@ -1,0 +1,13 @@
+// Temporary registration stubs (filled in by later milestones).
+#include "decoders/decoders.h"
+#include "elements/elements.h"
+
+namespace nnsx {
+void register_tensor_stream_elements() {}
+void register_extra_elements() {}
+void register_comm_elements() {}
+void register_bbox_decoder() {}
+void register_segment_decoder() {}
+void register_pose_decoder() {}
+void register_serial_decoders() {}
+}  // namespace nnsx

@@ -1,0 +1,656 @@
+// tensor_converter: media (video/audio/text/octet/flexible tensors/custom)
+// -> other/tensors.  Behaviour follows gst/nnstreamer/elements/
+// gsttensor_converter.c (chain :1015-1312, parse_* :1422-1833, timestamps
+// :783-841, chunking :946-1013).
+//
+// MI355X path (nnsx extension, property `device`): frames are uploaded into
+// stream-ordered device memory right here -- padded video rows are stripped by
+// hipMemcpy2DAsync during the H2D copy (K7), and `frames-per-tensor` batches
+// are assembled directly in one device block (K8) -- so everything
+// downstream stays HBM-resident.
+#include <cstring>
+#include <deque>
+
+#include "core/log.h"
+#include "elements/elements.h"
+#include "elements/tensor_common.h"
+#include "runtime/pipeline.h"
+#include "runtime/plugin_api.h"
+#include "runtime/video.h"
+
+namespace nnsx {
+
+namespace {
+
+Caps converter_sink_templ() {
+  return Caps::from_string(
+      "video/x-raw, format=(string){ RGB, BGR, RGBx, BGRx, xRGB, xBGR, RGBA, BGRA, ARGB, ABGR, GRAY8 }, "
+      "width=(int)[ 1, 2147483647 ], height=(int)[ 1, 2147483647 ], framerate=(fraction)[ 0/1, 2147483647/1 ]; "
+      "audio/x-raw, format=(string){ S8, U8, S16LE, U16LE, S32LE, U32LE, F32LE, F64LE }, "
+      "rate=(int)[ 1, 2147483647 ], channels=(int)[ 1, 2147483647 ], layout=(string)interleaved; "
+      "text/x-raw, format=(string)utf8; application/octet-stream; "
+      "other/tensors, format=(string)flexible, framerate=(fraction)[ 0/1, 2147483647/1 ]");
+}
+
+class TensorConverter : public Element {
+ public:
+  explicit TensorConverter(const std::string& name) : Element("tensor_converter", name) {
+    add_template("sink", PadDirection::SINK, PadPresence::ALWAYS, Caps::Any());
+    add_template("src", PadDirection::SRC, PadPresence::ALWAYS,
+                 Caps::from_string(tensor_caps_template_static() + "; " + tensor_caps_template_flexible()));
+    prop_string("input-dim", &input_dim_, "Input tensor dimension from inner array, up to 8 dimensions (text/octet)", [this] {
+      prop_info_.parse_dimensions(input_dim_);
+      unsigned n = static_cast<unsigned>(split_any(input_dim_, ",.").size());
+      if (prop_info_.num_tensors < n) prop_info_.num_tensors = n;
+    });
+    prop_string("input-type", &input_type_, "Type of each element of the input tensor (octet)", [this] {
+      prop_info_.parse_types(input_type_);
+      unsigned n = static_cast<unsigned>(split_any(input_type_, ",.").size());
+      if (prop_info_.num_tensors < n) prop_info_.num_tensors = n;
+    });
+    prop_uint("frames-per-tensor", &frames_per_tensor_, "The number of frames in output tensor");
+    prop_bool("set-timestamp", &set_timestamp_, "The flag to set timestamp when received a buffer with invalid timestamp");
+    prop_string("mode", &mode_, "Converter mode: custom-code:<registered callback> or custom-script:<python script>", [this] { parse_mode(); });
+    prop_readonly("sub-plugins", [] { return join(Registry::get().names(SubpluginKind::CONVERTER), ","); },
+                  "Registrable sub-plugins list");
+    prop_int("device", &device_, "nnsx: -1 keep tensors on the host, N upload into GPU N's HBM (zero-copy downstream)");
+  }
+
+  bool start() override {
+    configured_ = false;
+    adapter_.clear();
+    avail_ = 0;
+    old_pts_ = -1;
+    need_segment_ = true;
+    return true;
+  }
+
+  Caps query_caps(Pad* pad, const Caps* filter) override {
+    if (pad->direction() == PadDirection::SINK) {
+      Caps t = converter_sink_templ();
+      if (!mode_.empty() || !Registry::get().names(SubpluginKind::CONVERTER).empty()) t = Caps::Any();
+      if (filter) t = t.intersect(*filter);
+      return t;
+    }
+    Caps c = pad->template_caps();
+    if (configured_) c = caps_from_config(config_);
+    return filter ? c.intersect(*filter) : c;
+  }
+
+  bool sink_event(Pad* pad, Event& ev) override {
+    (void)pad;
+    switch (ev.type) {
+      case EventType::CAPS:
+        if (!parse_caps(ev.caps)) {
+          post_error("not-negotiated: tensor_converter cannot handle " + ev.caps.to_string());
+          return false;
+        }
+        return update_src_caps();
+      case EventType::SEGMENT:
+        in_segment_ = ev.segment;
+        need_segment_ = true;
+        return true;  // re-sent in TIME format at the next buffer
+      case EventType::EOS: {
+        // flush a partial chunk? the reference drops incomplete frames-per-tensor chunks
+        return forward_event_downstream(ev);
+      }
+      case EventType::FLUSH_STOP:
+        adapter_.clear();
+        avail_ = 0;
+        return forward_event_downstream(ev);
+      default:
+        return forward_event_downstream(ev);
+    }
+  }
+
+  FlowReturn chain(Pad*, BufferPtr buf) override {
+    try {
+      return do_chain(std::move(buf));
+    } catch (const std::exception& e) {
+      post_error(e.what());
+      return FlowReturn::ERROR;
+    }
+  }
+
+ private:
+  void parse_mode() {
+    custom_fn_ = nullptr;
+    external_.reset();
+    if (mode_.empty()) return;
+    auto parts = split(mode_, ':', 2);
+    if (parts.size() != 2) throw Error("invalid mode " + mode_);
+    if (parts[0] == "custom-code") {
+      auto fn = Registry::get().find_as<ConverterCustomFn>(SubpluginKind::CUSTOM_CONVERTER, parts[1], false);
+      if (!fn) throw Error("custom-code converter '" + parts[1] + "' is not registered");
+      custom_fn_ = *fn;
+    } else if (parts[0] == "custom-script") {
+      external_ = make_script_converter(parts[1]);
+      if (!external_) throw Error("cannot load converter script " + parts[1]);
+    } else {
+      throw Error("unknown converter mode " + parts[0]);
+    }
+  }
+
+  bool parse_caps(const Caps& caps) {
+    if (caps.size() == 0) return false;
+    const Structure& st = caps.at(0);
+    media_ = structure_media_type(st);
+    TensorsConfig cfg;
+    remove_padding_ = false;
+    if (custom_fn_ || external_) {
+      media_ = MediaType::ANY;
+    }
+    switch (media_) {
+      case MediaType::VIDEO: {
+        if (!vinfo_.from_structure(st) || !vinfo_.packed() || vinfo_.format == "YUY2" || vinfo_.format == "GRAY16_LE") {
+          NNSX_LOGE(name(), "unsupported video caps ", caps.to_string());
+          return false;
+        }
+        cfg.info.resize(1);
+        auto& t = cfg.info.at(0);
+        t.type = DType::UINT8;
+        t.dim = make_dims({static_cast<uint32_t>(vinfo_.channels), static_cast<uint32_t>(vinfo_.width),
+                           static_cast<uint32_t>(vinfo_.height), frames_per_tensor_});
+        cfg.rate_n = vinfo_.fps_n;
+        cfg.rate_d = vinfo_.fps_d;
+        size_t row = static_cast<size_t>(vinfo_.width) * vinfo_.channels;
+        remove_padding_ = (row % 4) != 0;
+        frame_size_ = row * vinfo_.height;  // tensor bytes per frame (padding stripped)
+        in_frame_size_ = vinfo_.size;
+        break;
+      }
+      case MediaType::AUDIO: {
+        AudioInfo ai;
+        if (!ai.from_structure(st)) return false;
+        static const std::map<std::string, DType> fmt = {
+            {"S8", DType::INT8},     {"U8", DType::UINT8},     {"S16LE", DType::INT16},   {"U16LE", DType::UINT16},
+            {"S32LE", DType::INT32}, {"U32LE", DType::UINT32}, {"F32LE", DType::FLOAT32}, {"F64LE", DType::FLOAT64}};
+        auto it = fmt.find(ai.format);
+        if (it == fmt.end()) return false;
+        cfg.info.resize(1);
+        cfg.info.at(0).type = it->second;
+        cfg.info.at(0).dim = make_dims({static_cast<uint32_t>(ai.channels), frames_per_tensor_});
+        cfg.rate_n = ai.rate;
+        cfg.rate_d = 1;
+        frame_size_ = in_frame_size_ = ai.bpf;
+        break;
+      }
+      case MediaType::TEXT: {
+        uint32_t text_size = prop_info_.num_tensors > 0 ? prop_info_.at(0).dim[0] : 0;
+        if (text_size == 0) {
+          NNSX_LOGE(name(), "tensor_converter: set input-dim for text streams (e.g. input-dim=30)");
+          return false;
+        }
+        std::string f;
+        if (st.get_string("format", &f) && lower(f) != "utf8") return false;
+        cfg.info.resize(1);
+        cfg.info.at(0).type = DType::UINT8;
+        cfg.info.at(0).dim = make_dims({text_size, frames_per_tensor_});
+        if (!st.get_fraction("framerate", &cfg.rate_n, &cfg.rate_d)) {
+          cfg.rate_n = 0;
+          cfg.rate_d = 1;
+        }
+        frame_size_ = in_frame_size_ = text_size;
+        break;
+      }
+      case MediaType::OCTET: {
+        Caps peer = src_pad()->peer_query_caps(nullptr);
+        TensorsConfig pc;
+        bool peer_flex = peer.size() > 0 && config_from_structure(peer.at(0), &pc) && pc.is_flexible() &&
+                         peer.at(0).get("format") && peer.at(0).get("format")->is_fixed();
+        bool configured = prop_info_.num_tensors > 0 && prop_info_.valid();
+        if (!configured && peer.size() > 0 && config_from_structure(peer.at(0), &pc) && pc.info.valid() &&
+            peer.is_fixed()) {
+          prop_info_ = pc.info;
+          configured = true;
+        }
+        if (peer_flex || !configured) {
+          cfg.info.format = Format::FLEXIBLE;
+          cfg.info.resize(1);
+          cfg.info.at(0).type = DType::UINT8;
+          cfg.info.at(0).dim = make_dims({1});
+          frame_size_ = in_frame_size_ = 0;
+        } else {
+          cfg.info = prop_info_;
+          if (frames_per_tensor_ > 1 && cfg.info.num_tensors == 1) {
+            int r = cfg.info.at(0).rank();
+            if (r < kRankLimit) cfg.info.at(0).dim[r] = frames_per_tensor_;
+          }
+          frame_size_ = in_frame_size_ = prop_info_.size();
+        }
+        if (!st.get_fraction("framerate", &cfg.rate_n, &cfg.rate_d)) {
+          cfg.rate_n = 0;
+          cfg.rate_d = 1;
+        }
+        break;
+      }
+      case MediaType::TENSOR: {
+        // flexible -> static: config comes from the first buffer's headers
+        TensorsConfig in;
+        config_from_structure(st, &in);
+        cfg = in;
+        cfg.info.format = Format::STATIC;
+        cfg.info.num_tensors = 0;
+        if (prop_info_.num_tensors > 0) cfg.info = prop_info_;
+        frame_size_ = in_frame_size_ = 0;
+        break;
+      }
+      default: {
+        if (!custom_fn_ && !external_) {
+          external_ = find_converter_for_caps(caps);
+          if (!external_) {
+            NNSX_LOGE(name(), "no converter sub-plugin for ", caps.to_string());
+            return false;
+          }
+        }
+        media_ = MediaType::ANY;
+        if (external_ && external_->get_out_config(caps, &cfg)) {
+          // known in advance
+        } else {
+          cfg.info.num_tensors = 0;
+        }
+        int n = 0, d = 1;
+        if (st.get_fraction("framerate", &n, &d)) {
+          cfg.rate_n = n;
+          cfg.rate_d = d;
+        } else {
+          cfg.rate_n = 0;
+          cfg.rate_d = 1;
+        }
+        break;
+      }
+    }
+    config_ = cfg;
+    configured_ = true;
+    return true;
+  }
+
+  bool update_src_caps() {
+    if (config_.is_static() && config_.info.num_tensors == 0) return true;  // decided at first buffer
+    Caps c = tensor_src_caps(src_pad(), config_, device_ >= 0);
+    out_flexible_ = c.size() > 0 && c.at(0).get_string_or("format", "static") == "flexible";
+    return src_pad()->push_event(Event::make_caps(c));
+  }
+
+  void push_segment() {
+    if (!need_segment_) return;
+    Segment seg;
+    bool have_fr = config_.rate_n > 0 && config_.rate_d > 0;
+    if (have_fr && in_segment_.start > 0 && frame_size_ > 0 && media_ == MediaType::AUDIO) {
+      int64_t start = in_segment_.start * config_.rate_d * kSecond / (static_cast<int64_t>(frame_size_) * config_.rate_n);
+      seg.start = seg.time = start;
+    } else {
+      seg = in_segment_;
+    }
+    out_segment_ = seg;
+    need_segment_ = false;
+    src_pad()->push_event(Event::make_segment(seg));
+  }
+
+  void set_timestamp(Buffer& b, unsigned frames_in) {
+    if (set_timestamp_) {
+      bool have_fr = config_.rate_n > 0 && config_.rate_d > 0;
+      if (b.duration < 0 && have_fr)
+        b.duration = static_cast<int64_t>(frames_in) * config_.rate_d * kSecond / config_.rate_n;
+      if (b.pts < 0) {
+        int64_t pts = out_segment_.start;
+        if (have_fr) {
+          if (old_pts_ >= 0) pts = old_pts_ + (b.duration > 0 ? b.duration : 0);
+        } else {
+          pts = running_time();
+          if (pts < 0) pts = 0;
+        }
+        b.pts = pts;
+      }
+    }
+    old_pts_ = b.pts;
+  }
+
+  // strip row padding (K7) and optionally upload (device path: one 2D H2D copy)
+  MemoryPtr video_frame(const MemoryPtr& m, int dev, hipStream_t s) {
+    size_t row = static_cast<size_t>(vinfo_.width) * vinfo_.channels;
+    if (!remove_padding_) {
+      if (dev >= 0 && frames_per_tensor_ == 1) {
+        auto out = Memory::alloc_device(frame_size_, dev, s);
+        if (m->on_device()) {
+          m->wait_ready(s);
+          hip::check(hipMemcpyAsync(out->data(), m->data(), frame_size_, hipMemcpyDeviceToDevice, s), "D2D");
+        } else {
+          hip::check(hipMemcpyAsync(out->data(), m->data(), frame_size_, hipMemcpyHostToDevice, s), "H2D frame");
+        }
+        m->record_use(s, dev);
+        out->mark_ready(s);
+        return out;
+      }
+      return m->size() == frame_size_ ? m : Memory::view(m, 0, frame_size_);
+    }
+    size_t stride = vinfo_.stride[0];
+    if (dev >= 0 && frames_per_tensor_ == 1 && !m->on_device()) {
+      auto out = Memory::alloc_device(frame_size_, dev, s);
+      hip::check(hipMemcpy2DAsync(out->data(), row, m->data(), stride, row, vinfo_.height, hipMemcpyHostToDevice, s),
+                 "H2D 2D frame");
+      m->record_use(s, dev);
+      out->mark_ready(s);
+      return out;
+    }
+    const uint8_t* src = static_cast<const uint8_t*>(m->map_host());
+    auto out = Memory::alloc_host(frame_size_);
+    uint8_t* dst = static_cast<uint8_t*>(out->data());
+    for (int y = 0; y < vinfo_.height; ++y) std::memcpy(dst + y * row, src + y * stride, row);
+    return out;
+  }
+
+  struct Piece {
+    MemoryPtr mem;
+    size_t off;
+    int64_t pts, dts;
+  };
+
+  // take `size` bytes from the adapter: zero-copy view when inside one piece,
+  // otherwise gathered into one block (on the device when uploading)
+  MemoryPtr adapter_take(size_t size, int dev, hipStream_t s, int64_t* pts, int64_t* dts, size_t* pts_dist) {
+    Piece& f = adapter_.front();
+    *pts = f.pts;
+    *dts = f.dts;
+    *pts_dist = f.off;
+    MemoryPtr out;
+    if (f.mem->size() - f.off >= size && dev < 0) {
+      out = Memory::view(f.mem, f.off, size);
+      f.off += size;
+      if (f.off == f.mem->size()) adapter_.pop_front();
+      avail_ -= size;
+      return out;
+    }
+    out = dev >= 0 ? Memory::alloc_device(size, dev, s) : Memory::alloc_host(size);
+    size_t done = 0;
+    while (done < size) {
+      Piece& p = adapter_.front();
+      size_t n = std::min(size - done, p.mem->size() - p.off);
+      char* dst = static_cast<char*>(out->data()) + done;
+      const char* srcp = static_cast<const char*>(p.mem->data()) + p.off;
+      if (dev >= 0) {
+        if (p.mem->on_device()) p.mem->wait_ready(s);
+        hip::check(hipMemcpyAsync(dst, srcp, n, p.mem->on_device() ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s),
+                   "adapter copy");
+        p.mem->record_use(s, dev);
+      } else {
+        std::memcpy(dst, static_cast<const char*>(p.mem->map_host()) + p.off, n);
+      }
+      done += n;
+      p.off += n;
+      if (p.off == p.mem->size()) adapter_.pop_front();
+    }
+    if (dev >= 0) out->mark_ready(s);
+    avail_ -= size;
+    return out;
+  }
+
+  FlowReturn push_out(BufferPtr b) {
+    // octet: split one memory into N static tensors (zero-copy views)
+    if (media_ == MediaType::OCTET && !config_.is_flexible() && config_.info.num_tensors > 1 && b->n_memory() == 1) {
+      auto nb = make_buffer();
+      nb->copy_metadata_from(*b);
+      size_t off = 0;
+      for (unsigned i = 0; i < config_.info.num_tensors; ++i) {
+        size_t sz = config_.info.size(static_cast<int>(i));
+        nb->mems.push_back(Memory::view(b->mems[0], off, sz));
+        off += sz;
+      }
+      b = nb;
+    }
+    if (out_flexible_ && !skip_header_) {
+      auto nb = make_buffer();
+      nb->copy_metadata_from(*b);
+      for (size_t i = 0; i < b->n_memory(); ++i) {
+        TensorInfo ti = config_.info.at(static_cast<unsigned>(i));
+        if (config_.is_flexible() && media_ == MediaType::OCTET) {
+          ti.type = DType::UINT8;
+          ti.dim = make_dims({static_cast<uint32_t>(b->mems[i]->size())});
+        }
+        MediaType mt = (media_ == MediaType::VIDEO || media_ == MediaType::AUDIO || media_ == MediaType::TEXT ||
+                        media_ == MediaType::OCTET)
+                           ? media_
+                           : MediaType::TENSOR;
+        nb->mems.push_back(make_flexible(b->mems[i], MetaInfo::from_info(ti, Format::FLEXIBLE, mt)));
+      }
+      b = nb;
+    }
+    return src_pad()->push(std::move(b));
+  }
+
+  FlowReturn do_chain(BufferPtr buf) {
+    if (!configured_) {
+      post_error("tensor_converter: buffer before caps");
+      return FlowReturn::NOT_NEGOTIATED;
+    }
+    size_t buf_size = buf->total_size();
+    if (buf_size == 0 && media_ != MediaType::ANY) return FlowReturn::OK;
+    int dev = device_ >= 0 && hip::available() ? device_ : -1;
+    hipStream_t s = dev >= 0 ? streams_.get(dev) : nullptr;
+    unsigned frames_out = frames_per_tensor_;
+    unsigned frames_in = 1;
+    size_t frame_size = frame_size_;
+    BufferPtr in = buf;
+    skip_header_ = false;
+
+    switch (media_) {
+      case MediaType::VIDEO: {
+        if (buf->n_memory() != 1) {
+          auto m = Memory::alloc_host(buf_size);
+          size_t off = 0;
+          for (auto& mm : buf->mems) {
+            std::memcpy(static_cast<char*>(m->data()) + off, mm->map_host(), mm->size());
+            off += mm->size();
+          }
+          buf = make_buffer();
+          buf->copy_metadata_from(*in);
+          buf->mems.push_back(m);
+        }
+        if (buf_size < in_frame_size_) {
+          post_error(strfmt("video buffer too small: ", buf_size, " < ", in_frame_size_));
+          return FlowReturn::ERROR;
+        }
+        auto nb = make_buffer();
+        nb->copy_metadata_from(*buf);
+        nb->mems.push_back(video_frame(buf->mems[0], dev, s));
+        in = nb;
+        break;
+      }
+      case MediaType::AUDIO:
+        frames_in = static_cast<unsigned>(buf_size / frame_size_);
+        break;
+      case MediaType::TEXT:
+        if (buf_size != frame_size_) {
+          auto m = Memory::alloc_host(frame_size_);
+          std::memset(m->data(), 0, frame_size_);
+          size_t off = 0;
+          for (auto& mm : buf->mems) {
+            size_t n = std::min(mm->size(), frame_size_ - off);
+            std::memcpy(static_cast<char*>(m->data()) + off, mm->map_host(), n);
+            off += n;
+            if (off >= frame_size_) break;
+          }
+          in = make_buffer();
+          in->copy_metadata_from(*buf);
+          in->mems.push_back(m);
+        }
+        break;
+      case MediaType::OCTET:
+        if (config_.is_flexible()) {
+          frame_size = buf_size;
+        } else {
+          if (frame_size_ == 0 || buf_size % frame_size_ != 0) {
+            post_error(strfmt("octet stream size ", buf_size, " is not a multiple of the tensor size ", frame_size_));
+            return FlowReturn::ERROR;
+          }
+          frames_in = static_cast<unsigned>(buf_size / frame_size_);
+        }
+        break;
+      case MediaType::TENSOR: {
+        // flexible -> static: strip headers, check against configured info
+        TensorsConfig tmp;
+        tmp.rate_n = config_.rate_n;
+        tmp.rate_d = config_.rate_d;
+        tmp.info.format = Format::FLEXIBLE;
+        BufferPtr fb;
+        if (!buffer_from_config(buf, tmp, &fb)) {
+          post_error("invalid flexible tensor buffer");
+          return FlowReturn::ERROR;
+        }
+        auto nb = make_buffer();
+        nb->copy_metadata_from(*buf);
+        tmp.info.format = Format::STATIC;
+        tmp.info.resize(static_cast<unsigned>(fb->n_memory()));
+        for (size_t i = 0; i < fb->n_memory(); ++i) {
+          MetaInfo meta;
+          MemoryPtr payload;
+          if (!parse_flexible(fb->mems[i], &meta, &payload) || !meta.to_info(&tmp.info.at(static_cast<unsigned>(i)))) {
+            post_error("invalid flexible header");
+            return FlowReturn::ERROR;
+          }
+          if (payload->size() != tmp.info.at(static_cast<unsigned>(i)).size()) {
+            post_error(strfmt("flexible->static: data size ", payload->size(), " != expected ",
+                              tmp.info.at(static_cast<unsigned>(i)).size()));
+            return FlowReturn::ERROR;
+          }
+          if (dev >= 0 && !payload->on_device()) {
+            auto d = Memory::alloc_device(payload->size(), dev, s);
+            hip::check(hipMemcpyAsync(d->data(), payload->data(), payload->size(), hipMemcpyHostToDevice, s), "H2D");
+            payload->record_use(s, dev);
+            d->mark_ready(s);
+            payload = d;
+          }
+          nb->mems.push_back(payload);
+        }
+        if (!(tmp.info == config_.info)) {
+          if (prop_info_.num_tensors > 0 && prop_info_.valid()) {
+            post_error("incoming flexible buffer does not match the given input-dim/input-type");
+            return FlowReturn::ERROR;
+          }
+          config_ = tmp;
+          update_src_caps();
+        }
+        push_segment();
+        set_timestamp(*nb, 1);
+        return push_out(nb);
+      }
+      case MediaType::ANY: {
+        TensorsConfig nc = config_;
+        BufferPtr out;
+        if (custom_fn_)
+          out = custom_fn_(buf, &nc);
+        else if (external_)
+          out = external_->convert(buf, &nc);
+        if (!out) {
+          post_error("converter returned no buffer");
+          return FlowReturn::ERROR;
+        }
+        out->copy_metadata_from(*buf);
+        skip_header_ = nc.is_flexible();
+        if (!(nc == config_) || !src_pad()->has_current_caps()) {
+          config_ = nc;
+          update_src_caps();
+        }
+        if (dev >= 0) {
+          for (auto& m : out->mems) {
+            if (m->on_device()) continue;
+            auto d = Memory::alloc_device(m->size(), dev, s);
+            hip::check(hipMemcpyAsync(d->data(), m->data(), m->size(), hipMemcpyHostToDevice, s), "H2D");
+            m->record_use(s, dev);
+            d->mark_ready(s);
+            m = d;
+          }
+        }
+        push_segment();
+        set_timestamp(*out, 1);
+        return push_out(out);
+      }
+      default:
+        post_error("tensor_converter: unknown media type");
+        return FlowReturn::ERROR;
+    }
+
+    push_segment();
+    set_timestamp(*in, frames_in);
+
+    if (frames_in == frames_out) {
+      if (dev >= 0) {
+        auto nb = make_buffer();
+        nb->copy_metadata_from(*in);
+        for (auto& m : in->mems) {
+          if (m->on_device()) {
+            nb->mems.push_back(m);
+            continue;
+          }
+          auto d = Memory::alloc_device(m->size(), dev, s);
+          hip::check(hipMemcpyAsync(d->data(), m->data(), m->size(), hipMemcpyHostToDevice, s), "H2D");
+          m->record_use(s, dev);
+          d->mark_ready(s);
+          nb->mems.push_back(d);
+        }
+        in = nb;
+      }
+      return push_out(in);
+    }
+
+    // chunking through the adapter (frames-per-tensor)
+    int64_t duration = in->duration;
+    if (duration >= 0) duration = duration * frames_out / std::max(1u, frames_in);
+    for (auto& m : in->mems) {
+      adapter_.push_back(Piece{m, 0, in->pts, in->dts});
+      avail_ += m->size();
+      // only the first memory carries the timestamp
+      in->pts = -1;
+      in->dts = -1;
+    }
+    size_t out_size = static_cast<size_t>(frames_out) * frame_size;
+    FlowReturn ret = FlowReturn::OK;
+    bool have_fr = config_.rate_n > 0 && config_.rate_d > 0;
+    while (avail_ >= out_size && flow_ok(ret)) {
+      int64_t pts, dts;
+      size_t dist;
+      auto m = adapter_take(out_size, dev, s, &pts, &dts, &dist);
+      if (frames_in > 1 && have_fr && frame_size > 0) {
+        if (pts >= 0) pts += static_cast<int64_t>(dist) * config_.rate_d * kSecond / (config_.rate_n * static_cast<int64_t>(frame_size));
+        if (dts >= 0) dts += static_cast<int64_t>(dist) * config_.rate_d * kSecond / (config_.rate_n * static_cast<int64_t>(frame_size));
+      }
+      auto ob = make_buffer();
+      ob->pts = pts;
+      ob->dts = dts;
+      ob->duration = duration;
+      ob->mems.push_back(m);
+      ret = push_out(ob);
+    }
+    return ret;
+  }
+
+  std::string input_dim_, input_type_, mode_;
+  TensorsInfo prop_info_;
+  unsigned frames_per_tensor_ = 1;
+  bool set_timestamp_ = true;
+  int device_ = -1;
+  bool configured_ = false;
+  TensorsConfig config_;
+  MediaType media_ = MediaType::INVALID;
+  VideoInfo vinfo_;
+  bool remove_padding_ = false;
+  size_t frame_size_ = 0, in_frame_size_ = 0;
+  bool out_flexible_ = false, skip_header_ = false;
+  int64_t old_pts_ = -1;
+  bool need_segment_ = true;
+  Segment in_segment_, out_segment_;
+  std::deque<Piece> adapter_;
+  size_t avail_ = 0;
+  ConverterCustomFn custom_fn_;
+  std::shared_ptr<ConverterSubplugin> external_;
+  StreamSet streams_;
+};
+
+}  // namespace
+
+void register_tensor_converter() {
+  register_element("tensor_converter", "Converter/Tensor", "Converts audio/video/text/octet streams to tensors",
+                   [](const std::string& n) { return std::make_unique<TensorConverter>(n); });
+}
+
+}  // namespace nnsx

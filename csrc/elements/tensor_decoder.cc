@@ -1,0 +1,181 @@
+// tensor_decoder: dispatches `mode=` to a decoder sub-plugin; option1..9 are
+// forwarded through set_option(idx).  Reference: gst/nnstreamer/elements/
+// gsttensor_decoder.c (registry :133-200, props :286-397, transform :666-742,
+// caps :750-907, custom register :936-974).
+#include "core/log.h"
+#include "elements/elements.h"
+#include "elements/tensor_common.h"
+#include "runtime/base.h"
+#include "runtime/pipeline.h"
+#include "runtime/plugin_api.h"
+
+namespace nnsx {
+
+namespace {
+
+class CustomCodeDecoder : public DecoderInstance {
+ public:
+  explicit CustomCodeDecoder(DecoderCustomFn fn) : fn_(std::move(fn)) {}
+  Caps get_out_caps(const TensorsConfig& config) override {
+    (void)config;
+    return Caps::Any();
+  }
+  FlowReturn decode(const TensorsConfig& config, const std::vector<MemoryPtr>& in, Buffer* out,
+                    InvokeContext&) override {
+    return fn_(in, config, out);
+  }
+
+ private:
+  DecoderCustomFn fn_;
+};
+
+class TensorDecoder : public BaseTransform {
+ public:
+  explicit TensorDecoder(const std::string& name)
+      : BaseTransform("tensor_decoder", name, Caps::from_string(tensor_caps_template_all()), Caps::Any()) {
+    prop_string("mode", &mode_, "Decoder mode", [this] { load_mode(); });
+    for (int i = 0; i < 9; ++i) {
+      prop_string("option" + std::to_string(i + 1), &options_[i], "Option " + std::to_string(i + 1) + " of the decoder mode",
+                  [this, i] {
+                    if (inst_ && !inst_->set_option(i, options_[i]))
+                      throw Error("decoder " + mode_ + " rejected option" + std::to_string(i + 1) + "=" + options_[i]);
+                  });
+    }
+    prop_readonly("sub-plugins", [] { return join(Registry::get().names(SubpluginKind::DECODER), ","); },
+                  "Registrable sub-plugins list");
+    prop_string("config-file", &config_file_, "Path to a config file holding option1..9 (key=value lines)", [this] {
+      load_config_file();
+    });
+    prop_int("device", &device_, "nnsx: -2 follow input placement, -1 CPU, N run post-processing kernels on GPU N");
+  }
+
+ protected:
+  void load_mode() {
+    inst_.reset();
+    auto parts = split(mode_, ':', 2);
+    if (parts.size() == 2 && parts[0] == "custom-code") {
+      auto fn = Registry::get().find_as<DecoderCustomFn>(SubpluginKind::CUSTOM_DECODER, parts[1], false);
+      if (!fn) throw Error("custom-code decoder '" + parts[1] + "' is not registered");
+      inst_ = std::make_unique<CustomCodeDecoder>(*fn);
+      return;
+    }
+    auto d = find_decoder(mode_);
+    if (!d) throw Error("tensor_decoder: mode '" + mode_ + "' is not available");
+    inst_ = d->create();
+    for (int i = 0; i < 9; ++i)
+      if (!options_[i].empty() && !inst_->set_option(i, options_[i]))
+        throw Error("decoder " + mode_ + " rejected option" + std::to_string(i + 1));
+  }
+
+  void load_config_file() {
+    // "option1=...\noption2=..." style file
+    FILE* f = fopen(config_file_.c_str(), "r");
+    if (!f) throw Error("cannot open config-file " + config_file_);
+    char line[4096];
+    while (fgets(line, sizeof(line), f)) {
+      std::string t = strip(line);
+      auto eq = t.find('=');
+      if (eq == std::string::npos) continue;
+      std::string k = strip(t.substr(0, eq));
+      if (k == "mode")
+        set_property("mode", strip(t.substr(eq + 1)));
+      else if (starts_with(k, "option"))
+        set_property(k, strip(t.substr(eq + 1)));
+    }
+    fclose(f);
+  }
+
+  Caps transform_caps(PadDirection dir, const Caps& caps, const Caps* filter) override {
+    if (dir == PadDirection::SRC) {
+      Caps r = sink_pad()->template_caps();
+      return filter ? r.intersect(*filter) : r;
+    }
+    Caps r;
+    for (size_t i = 0; i < caps.size(); ++i) {
+      TensorsConfig cfg;
+      if (!inst_ || !config_from_structure(caps.at(i), &cfg)) {
+        r = Caps::Any();
+        break;
+      }
+      if (cfg.is_static() && (cfg.info.num_tensors == 0 || !cfg.info.valid())) {
+        r = Caps::Any();
+        break;
+      }
+      Caps o = inst_->get_out_caps(cfg);
+      if (o.is_empty()) continue;
+      r.append(o);
+      if (o.is_any()) break;
+    }
+    if (filter) r = r.intersect(*filter);
+    return r;
+  }
+
+  Caps fixate_caps(PadDirection, const Caps& caps, Caps othercaps) override {
+    (void)caps;
+    if (othercaps.is_any()) return othercaps;
+    return othercaps.fixate();
+  }
+
+  bool set_caps(const Caps& incaps, const Caps& outcaps) override {
+    (void)outcaps;
+    if (!inst_) {
+      NNSX_LOGE(name(), "tensor_decoder: mode is not set");
+      return false;
+    }
+    return tensor_config_from_caps(incaps, &config_);
+  }
+
+  FlowReturn transform(const BufferPtr& inbuf, BufferPtr* outbuf) override {
+    BufferPtr in;
+    if (!buffer_from_config(inbuf, config_, &in)) {
+      post_error("tensor_decoder: buffer does not match the negotiated caps");
+      return FlowReturn::ERROR;
+    }
+    TensorsConfig cfg = config_;
+    std::vector<MemoryPtr> mems;
+    if (config_.is_flexible()) {
+      cfg.info.format = Format::STATIC;
+      cfg.info.resize(static_cast<unsigned>(in->n_memory()));
+      for (size_t i = 0; i < in->n_memory(); ++i) {
+        MetaInfo meta;
+        MemoryPtr payload;
+        if (!parse_flexible(in->mems[i], &meta, &payload)) return FlowReturn::ERROR;
+        meta.to_info(&cfg.info.at(static_cast<unsigned>(i)));
+        mems.push_back(payload);
+      }
+    } else {
+      mems = in->mems;
+    }
+    InvokeContext ctx;
+    ctx.device = inst_->supports_device() ? resolve_device(device_, *in) : -1;
+    ctx.stream = ctx.device >= 0 ? streams_.get(ctx.device) : nullptr;
+    hip::DeviceGuard g(ctx.device);
+    auto out = make_buffer();
+    out->copy_metadata_from(*in);
+    FlowReturn r = inst_->decode(cfg, mems, out.get(), ctx);
+    if (r != FlowReturn::OK) {
+      if (r == FlowReturn::CUSTOM_SUCCESS) return r;
+      post_error("tensor_decoder: decode failed (" + mode_ + ")");
+      return r;
+    }
+    if (ctx.device >= 0)
+      for (auto& m : mems) m->record_use(ctx.stream, ctx.device);
+    *outbuf = out;
+    return FlowReturn::OK;
+  }
+
+  std::string mode_, options_[9], config_file_;
+  int device_ = -2;
+  std::unique_ptr<DecoderInstance> inst_;
+  TensorsConfig config_;
+  StreamSet streams_;
+};
+
+}  // namespace
+
+void register_tensor_decoder() {
+  register_element("tensor_decoder", "Converter/Tensor", "Converts tensors to media streams via decoder sub-plugins",
+                   [](const std::string& n) { return std::make_unique<TensorDecoder>(n); });
+}
+
+}  // namespace nnsx

@@ -1,0 +1,578 @@
+// tensor_filter: runs a framework sub-plugin on every buffer.
+// Reference: gst/nnstreamer/tensor_filter/tensor_filter.c (validate :558-626,
+// transform :632-894, statistics :354-495, configure :903-1086,
+// transform_caps :1099-1215, latency query :1314-1376, model update event
+// :1414-1446, QoS throttle :1455-1485) and tensor_filter_common.c
+// (properties :899-1017, combinations :1815-1885, shared models :2911-3076,
+// accelerator grammar :2495-2800).
+//
+// nnsx: frameworks receive Memory objects plus the element's HIP stream and
+// device; GPU frameworks consume device memories in place and return
+// device-resident, allocate-in-invoke outputs (no per-frame PCIe copies).
+#include <algorithm>
+#include <deque>
+
+#include "core/log.h"
+#include "elements/elements.h"
+#include "elements/tensor_common.h"
+#include "runtime/base.h"
+#include "runtime/pipeline.h"
+#include "runtime/plugin_api.h"
+
+namespace nnsx {
+
+namespace {
+
+// shared-tensor-filter-key table (tensor_filter_common.c:2911-3076)
+struct SharedModel {
+  std::shared_ptr<FilterInstance> inst;
+  std::mutex invoke_mu;
+  int refs = 0;
+};
+std::mutex g_shared_mu;
+std::map<std::string, std::shared_ptr<SharedModel>> g_shared;
+
+std::vector<int> parse_ranks(const std::string& s) {
+  std::vector<int> v;
+  for (auto& x : split(s, ','))
+    if (!strip(x).empty()) v.push_back(static_cast<int>(to_int(x)));
+  return v;
+}
+
+class TensorFilter : public BaseTransform {
+ public:
+  explicit TensorFilter(const std::string& name)
+      : BaseTransform("tensor_filter", name, Caps::from_string(tensor_caps_template_all()),
+                      Caps::from_string(tensor_caps_template_all())) {
+    prop_string("framework", &fw_name_, "Neural network framework", [this] { on_framework_set(); });
+    prop_string("model", &model_str_, "File path to the model file. Separated with ',' in case of multiple model files",
+                [this] { on_model_set(); });
+    prop_string("input", &input_str_, "Input tensor dimension from inner array, up to 8 dimensions ?", [this] {
+      unsigned n = props_.input_info.parse_dimensions(input_str_);
+      props_.input_info.num_tensors = std::max(props_.input_info.num_tensors, n);
+    });
+    prop_string("inputtype", &inputtype_str_, "Type of each element of the input tensor ?", [this] {
+      unsigned n = props_.input_info.parse_types(inputtype_str_);
+      props_.input_info.num_tensors = std::max(props_.input_info.num_tensors, n);
+    });
+    prop_string("inputname", &inputname_str_, "The Name of Input Tensor", [this] { props_.input_info.parse_names(inputname_str_); });
+    prop_string("inputlayout", &props_.input_layout, "Set channel first (NCHW) or channel last layout (NHWC) or None for input data");
+    prop_string("inputranks", &inputranks_str_, "The Rank of the Input Tensor", [this] { props_.input_ranks = parse_ranks(inputranks_str_); });
+    prop_string("output", &output_str_, "Output tensor dimension from inner array, up to 8 dimensions ?", [this] {
+      unsigned n = props_.output_info.parse_dimensions(output_str_);
+      props_.output_info.num_tensors = std::max(props_.output_info.num_tensors, n);
+    });
+    prop_string("outputtype", &outputtype_str_, "Type of each element of the output tensor ?", [this] {
+      unsigned n = props_.output_info.parse_types(outputtype_str_);
+      props_.output_info.num_tensors = std::max(props_.output_info.num_tensors, n);
+    });
+    prop_string("outputname", &outputname_str_, "The Name of Output Tensor", [this] { props_.output_info.parse_names(outputname_str_); });
+    prop_string("outputlayout", &props_.output_layout, "Set channel first (NCHW) or channel last layout (NHWC) or None for output data");
+    prop_string("outputranks", &outputranks_str_, "The Rank of the Out Tensor", [this] { props_.output_ranks = parse_ranks(outputranks_str_); });
+    prop_string("custom", &props_.custom_properties, "Custom properties for subplugins ?");
+    prop_readonly("sub-plugins", [] { return join(Registry::get().names(SubpluginKind::FILTER), ","); },
+                  "Registrable sub-plugins list");
+    prop_string("accelerator", &props_.accl_str, "Set accelerator for the subplugin with format (true/false):(comma separated ACCELERATOR(s)). true/false determines if accelerator is to be used. list of accelerators determines the backend (ignored with false). Example, if GPU, NPU can be used but not CPU - true:npu,gpu,!cpu.");
+    prop_bool("is-updatable", &props_.is_updatable, "Indicate whether a given model to this tensor filter is updatable in runtime. (e.g., with on-device training)");
+    {
+      PropSpec s;
+      s.name = "latency";
+      s.type = PropType::INT;
+      s.blurb = "The average latency over the recent 10 inferences in microseconds (write 1 to enable, 0 to disable; -1 when disabled)";
+      s.set = [this](const std::string& v) { latency_mode_ = static_cast<int>(to_int(v)); };
+      s.get = [this] { return std::to_string(latency_mode_ > 0 ? avg_latency_us() : -1); };
+      add_prop(s);
+    }
+    {
+      PropSpec s;
+      s.name = "throughput";
+      s.type = PropType::INT;
+      s.blurb = "The average throughput in frames per second x 1000 (write 1 to enable, 0 to disable; -1 when disabled)";
+      s.set = [this](const std::string& v) { throughput_mode_ = static_cast<int>(to_int(v)); };
+      s.get = [this] { return std::to_string(throughput_mode_ > 0 ? throughput_milli_fps() : -1); };
+      add_prop(s);
+    }
+    prop_string("input-combination", &input_comb_str_, "Select the input tensor(s) to invoke the models", [this] {
+      input_comb_.clear();
+      for (auto& x : split(input_comb_str_, ','))
+        if (!strip(x).empty()) input_comb_.push_back(static_cast<int>(to_int(x)));
+    });
+    prop_string("output-combination", &output_comb_str_, "Select the output tensor(s) in the input tensor(s) and/or model output (e.g. i0,o0,o1)",
+                [this] { parse_output_combination(); });
+    prop_string("shared-tensor-filter-key", &props_.shared_key, "Multiple element instances of tensor-filter in a pipeline may share a single resource instance if they share the same framework (subplugin) and neural network model. Designate \"shared-tensor-filter-key\" for such elements.");
+    prop_bool("latency-report", &latency_report_, "Report the latency of tensor filter to the pipeline bus (LATENCY message)");
+    prop_int("invoke-dynamic", &props_.invoke_dynamic, "Flexible tensors whose shape can change per invoke (output caps become flexible)");
+    prop_int("device", &device_prop_, "nnsx: GPU index for GPU frameworks (-2 = follow input placement, else LOCAL_RANK or 0)");
+    prop_string("config-file", &config_file_, "Path to a key=value file setting any of the properties", [this] { load_config_file(); });
+  }
+
+  ~TensorFilter() override { close_fw(); }
+
+ protected:
+  // ------------------------------------------------------------ properties ----
+  void on_framework_set() {
+    if (inst_) close_fw();
+    fw_.reset();
+  }
+
+  void on_model_set() {
+    std::vector<std::string> models;
+    for (auto& m : split(model_str_, ','))
+      if (!strip(m).empty()) models.push_back(strip(m));
+    bool reload = inst_ && props_.is_updatable && models != props_.model_files;
+    props_.model_files = models;
+    if (reload) {
+      FilterProperties np = props_;
+      if (!inst_->reload_model(np)) post_error("tensor_filter: model reload failed");
+    }
+  }
+
+  void load_config_file() {
+    FILE* f = fopen(config_file_.c_str(), "r");
+    if (!f) throw Error("cannot open config-file " + config_file_);
+    char line[8192];
+    while (fgets(line, sizeof(line), f)) {
+      std::string t = strip(line);
+      if (t.empty() || t[0] == '#') continue;
+      auto eq = t.find('=');
+      if (eq == std::string::npos) continue;
+      set_property(strip(t.substr(0, eq)), strip(t.substr(eq + 1)));
+    }
+    fclose(f);
+  }
+
+  void parse_output_combination() {
+    out_comb_.clear();
+    for (auto& x : split(output_comb_str_, ',')) {
+      std::string t = strip(x);
+      if (t.empty()) continue;
+      if (t[0] != 'i' && t[0] != 'o') throw Error("output-combination: invalid token " + t);
+      out_comb_.emplace_back(t[0] == 'i', static_cast<int>(to_int(t.substr(1))));
+    }
+  }
+
+  // -------------------------------------------------------------- framework ----
+  bool ensure_open() {
+    if (inst_) return true;
+    std::lock_guard<std::mutex> lk(open_mu_);
+    if (inst_) return true;
+    std::string fwn = fw_name_;
+    if (fwn.empty() || fwn == "auto") {
+      fwn = detect_framework(props_.model_files);
+      if (fwn.empty()) {
+        NNSX_LOGE(name(), "tensor_filter: cannot detect the framework for model '", model_str_, "'");
+        return false;
+      }
+    }
+    fw_ = find_filter_framework(fwn);
+    if (!fw_) {
+      NNSX_LOGE(name(), "tensor_filter: framework '", fwn, "' is not available");
+      return false;
+    }
+    props_.fwname = fw_->name();
+    if (props_.model_files.empty() && !fw_->run_without_model()) {
+      NNSX_LOGE(name(), "tensor_filter: model property is not set");
+      return false;
+    }
+    bool use_accl = false;
+    props_.accl = parse_accelerator(props_.accl_str, fw_->accelerators(), &use_accl);
+    props_.device = -1;
+    if ((props_.accl == Accelerator::GPU || props_.accl == Accelerator::AUTO ||
+         (props_.accl == Accelerator::DEFAULT && fw_->accelerators().find("gpu") != std::string::npos &&
+          Config::get().custom_bool("pytorch", "enable_use_gpu", true))) &&
+        hip::available() && fw_->check_availability(Accelerator::GPU)) {
+      int dev = device_prop_;
+      if (dev < 0) {
+        const char* lr = getenv("LOCAL_RANK");
+        dev = lr ? static_cast<int>(to_int(lr)) % hip::device_count() : 0;
+      }
+      props_.device = dev;
+    }
+    if (!props_.shared_key.empty()) {
+      std::lock_guard<std::mutex> lk2(g_shared_mu);
+      auto it = g_shared.find(props_.shared_key);
+      if (it != g_shared.end()) {
+        shared_ = it->second;
+        shared_->refs++;
+        inst_ = shared_->inst;
+        return true;
+      }
+    }
+    try {
+      inst_ = std::shared_ptr<FilterInstance>(fw_->open(props_).release());
+    } catch (const std::exception& e) {
+      NNSX_LOGE(name(), "tensor_filter: failed to open framework ", fwn, ": ", e.what());
+      inst_.reset();
+      return false;
+    }
+    if (!inst_) return false;
+    if (!props_.shared_key.empty()) {
+      std::lock_guard<std::mutex> lk2(g_shared_mu);
+      auto sm = std::make_shared<SharedModel>();
+      sm->inst = inst_;
+      sm->refs = 1;
+      g_shared[props_.shared_key] = sm;
+      shared_ = sm;
+    }
+    load_model_info();
+    return true;
+  }
+
+  void close_fw() {
+    if (shared_) {
+      std::lock_guard<std::mutex> lk(g_shared_mu);
+      if (--shared_->refs == 0) g_shared.erase(props_.shared_key);
+      shared_.reset();
+    }
+    inst_.reset();
+  }
+
+  void load_model_info() {
+    TensorsInfo in, out;
+    model_info_known_ = inst_->get_model_info(&in, &out);
+    if (model_info_known_) {
+      // properties given by the user must agree with the model (gst_tensor_filter_load_tensor_info)
+      if (props_.input_info.num_tensors > 0 && props_.input_info.valid() && !(in == props_.input_info)) {
+        NNSX_LOGW(name(), "input property (", props_.input_info.to_string(), ") differs from model (", in.to_string(), ")");
+      }
+      model_in_ = in;
+      model_out_ = out;
+    } else {
+      model_in_ = props_.input_info;
+      model_out_ = props_.output_info;
+    }
+  }
+
+  // -------------------------------------------------------------------- caps ----
+  TensorsInfo combined_in(const TensorsInfo& full) const {
+    if (input_comb_.empty()) return full;
+    TensorsInfo r;
+    r.format = full.format;
+    r.resize(static_cast<unsigned>(input_comb_.size()));
+    for (size_t i = 0; i < input_comb_.size(); ++i) r.at(static_cast<unsigned>(i)) = full.at(static_cast<unsigned>(input_comb_[i]));
+    return r;
+  }
+
+  bool output_info_for(const TensorsConfig& in, TensorsInfo* out) {
+    TensorsInfo min = combined_in(in.info);
+    TensorsInfo mout;
+    if (model_info_known_ && (model_in_ == min || min.format != Format::STATIC)) {
+      mout = model_out_;
+    } else {
+      if (!inst_->set_input_info(min, &mout)) {
+        if (model_info_known_) {
+          NNSX_LOGE(name(), "tensor_filter: input ", min.to_string(), " does not match model input ", model_in_.to_string());
+          return false;
+        }
+        if (props_.output_info.num_tensors > 0 && props_.output_info.valid()) {
+          mout = props_.output_info;
+        } else {
+          NNSX_LOGE(name(), "tensor_filter: cannot determine output info for ", min.to_string());
+          return false;
+        }
+      }
+    }
+    if (out_comb_.empty()) {
+      *out = mout;
+      return true;
+    }
+    TensorsInfo r;
+    r.resize(static_cast<unsigned>(out_comb_.size()));
+    for (size_t i = 0; i < out_comb_.size(); ++i) {
+      const auto& c = out_comb_[i];
+      r.at(static_cast<unsigned>(i)) = c.first ? in.info.at(static_cast<unsigned>(c.second)) : mout.at(static_cast<unsigned>(c.second));
+    }
+    *out = r;
+    return true;
+  }
+
+  Caps transform_caps(PadDirection dir, const Caps& caps, const Caps* filter) override {
+    if (!ensure_open()) return Caps();
+    Caps r;
+    if (dir == PadDirection::SRC) {
+      TensorsConfig c;
+      c.info = model_in_;
+      if (model_in_.num_tensors > 0 && model_in_.valid() && input_comb_.empty()) {
+        for (size_t i = 0; i < caps.size(); ++i) {
+          TensorsConfig oc;
+          if (config_from_structure(caps.at(i), &oc) && oc.rate_n >= 0) {
+            c.rate_n = oc.rate_n;
+            c.rate_d = oc.rate_d;
+          }
+        }
+        r = caps_from_config(c);
+        r.append(Caps::from_string(tensor_caps_template_flexible()));
+      } else {
+        r = Caps::from_string(tensor_caps_template_all());
+      }
+    } else {
+      for (size_t i = 0; i < caps.size(); ++i) {
+        TensorsConfig in;
+        if (!config_from_structure(caps.at(i), &in)) continue;
+        if (in.is_static() && (in.info.num_tensors == 0 || !in.info.valid())) {
+          r.append(Caps::from_string(tensor_caps_template_all()));
+          continue;
+        }
+        TensorsInfo out;
+        if (in.is_flexible() && !model_info_known_) {
+          r.append(Caps::from_string(tensor_caps_template_flexible()));
+          continue;
+        }
+        if (!output_info_for(in, &out)) continue;
+        TensorsConfig oc;
+        oc.info = out;
+        oc.rate_n = in.rate_n;
+        oc.rate_d = in.rate_d;
+        if (props_.invoke_dynamic) oc.info.format = Format::FLEXIBLE;
+        r.append(caps_from_config(oc, props_.device >= 0));
+        if (!props_.invoke_dynamic) {
+          TensorsConfig fc = oc;
+          fc.info.format = Format::FLEXIBLE;
+          r.append(caps_from_config(fc));
+        }
+      }
+    }
+    if (filter) r = r.intersect(*filter);
+    return r;
+  }
+
+  Caps fixate_caps(PadDirection, const Caps& caps, Caps othercaps) override {
+    TensorsConfig in;
+    if (caps.size() && config_from_structure(caps.at(0), &in) && othercaps.size() > 0) {
+      TensorsConfig oc;
+      if (config_from_structure(othercaps.at(0), &oc)) {
+        Caps peer = src_pad()->peer_query_caps(nullptr);
+        return pad_caps_from_config(oc, &peer, props_.device >= 0);
+      }
+    }
+    return othercaps.fixate();
+  }
+
+  bool set_caps(const Caps& incaps, const Caps& outcaps) override {
+    if (!ensure_open()) return false;
+    if (!tensor_config_from_caps(incaps, &in_config_) || !tensor_config_from_caps(outcaps, &out_config_)) return false;
+    in_flexible_ = in_config_.is_flexible();
+    out_flexible_ = out_config_.is_flexible();
+    if (in_flexible_ && out_flexible_ && !model_info_known_ && props_.input_info.num_tensors == 0 &&
+        !props_.invoke_dynamic) {
+      NNSX_LOGE(name(), "tensor_filter: flexible -> flexible needs the model I/O or input/output properties");
+      return false;
+    }
+    if (!in_flexible_) {
+      TensorsInfo out;
+      if (!output_info_for(in_config_, &out)) return false;
+      model_out_runtime_ = out;
+    } else {
+      model_out_runtime_ = model_out_;
+    }
+    configured_ = true;
+    return true;
+  }
+
+  // ------------------------------------------------------------------ events ----
+  bool handle_sink_event(Event& ev) override {
+    if (ev.type == EventType::CUSTOM_DOWNSTREAM && ev.data.name() == "evt_update_model") {
+      std::string m = ev.data.get_string_or("model", "");
+      if (!m.empty() && inst_) {
+        props_.model_files = split(m, ',');
+        model_str_ = m;
+        if (!inst_->reload_model(props_)) post_error("tensor_filter: failed to update the model");
+      }
+      return false;  // consumed
+    }
+    return true;
+  }
+
+  bool handle_src_event(Event& ev) override {
+    if (ev.type == EventType::QOS && ev.qos_type == "throttle") {
+      throttle_delay_ = ev.diff > 0 ? ev.diff : 0;
+      return true;  // keep propagating upstream like the reference
+    }
+    return true;
+  }
+
+  int64_t own_latency() const override { return latency_mode_ > 0 ? avg_latency_us() * 1000 : 0; }
+
+  // ---------------------------------------------------------------- transform ----
+  FlowReturn transform(const BufferPtr& inbuf, BufferPtr* outbuf) override {
+    if (!configured_ || !inst_) {
+      post_error("tensor_filter: not configured");
+      return FlowReturn::NOT_NEGOTIATED;
+    }
+    // QoS throttling drop (tensor_filter.c:501-552)
+    if (throttle_delay_ > 0 && inbuf->pts >= 0) {
+      if (prev_ts_ >= 0 && inbuf->pts - prev_ts_ < throttle_delay_) return FlowReturn::CUSTOM_SUCCESS;
+      prev_ts_ = inbuf->pts;
+    }
+    BufferPtr in;
+    if (!buffer_from_config(inbuf, in_config_, &in)) {
+      post_error("tensor_filter: input buffer does not match the negotiated caps");
+      return FlowReturn::ERROR;
+    }
+    std::vector<MemoryPtr> all_in;
+    if (in_flexible_) {
+      for (auto& m : in->mems) {
+        MetaInfo meta;
+        MemoryPtr payload;
+        if (!parse_flexible(m, &meta, &payload)) return FlowReturn::ERROR;
+        all_in.push_back(payload);
+      }
+    } else {
+      all_in = in->mems;
+    }
+    std::vector<MemoryPtr> model_in;
+    if (input_comb_.empty()) {
+      model_in = all_in;
+    } else {
+      for (int i : input_comb_) {
+        if (i < 0 || static_cast<size_t>(i) >= all_in.size()) return FlowReturn::ERROR;
+        model_in.push_back(all_in[i]);
+      }
+    }
+    InvokeContext ctx;
+    ctx.device = props_.device;
+    if (device_prop_ == -2 && ctx.device >= 0) {
+      int d = resolve_device(-2, *in);
+      if (d >= 0) ctx.device = d;
+    }
+    ctx.stream = ctx.device >= 0 ? streams_.get(ctx.device) : nullptr;
+    TensorsInfo dyn_out;
+    ctx.out_info = &dyn_out;
+    std::vector<MemoryPtr> outs;
+    int64_t t0 = now_ns();
+    int ret;
+    {
+      hip::DeviceGuard g(ctx.device);
+      if (shared_) {
+        std::lock_guard<std::mutex> lk(shared_->invoke_mu);
+        ret = inst_->invoke(model_in, &outs, ctx);
+      } else {
+        ret = inst_->invoke(model_in, &outs, ctx);
+      }
+    }
+    int64_t t1 = now_ns();
+    record_stats(t1 - t0, t1);
+    if (ret > 0) return FlowReturn::CUSTOM_SUCCESS;  // drop this frame (tensor_filter.c:811-813)
+    if (ret < 0) {
+      post_error(strfmt("tensor_filter: invoke failed (", ret, ")"));
+      return FlowReturn::ERROR;
+    }
+    auto out = make_buffer();
+    out->copy_metadata_from(*in);
+    auto add = [&](const MemoryPtr& m, const TensorInfo* ti) {
+      if (out_flexible_) {
+        TensorInfo info = ti ? *ti : TensorInfo();
+        if (!ti || !dimension_valid(info.dim)) {
+          info.type = DType::UINT8;
+          info.dim = make_dims({static_cast<uint32_t>(m->size())});
+        }
+        out->mems.push_back(make_flexible(m, MetaInfo::from_info(info)));
+      } else {
+        out->mems.push_back(m);
+      }
+    };
+    const TensorsInfo& oinfo = dyn_out.num_tensors ? dyn_out : model_out_;
+    if (out_comb_.empty()) {
+      for (size_t i = 0; i < outs.size(); ++i) add(outs[i], i < oinfo.num_tensors ? &oinfo.at(static_cast<unsigned>(i)) : nullptr);
+    } else {
+      for (const auto& c : out_comb_) {
+        if (c.first) {
+          if (static_cast<size_t>(c.second) >= all_in.size()) return FlowReturn::ERROR;
+          const TensorInfo* ti = in_flexible_ ? nullptr : &in_config_.info.at(static_cast<unsigned>(c.second));
+          add(all_in[c.second], ti);
+        } else {
+          if (static_cast<size_t>(c.second) >= outs.size()) return FlowReturn::ERROR;
+          add(outs[c.second], static_cast<unsigned>(c.second) < oinfo.num_tensors ? &oinfo.at(static_cast<unsigned>(c.second)) : nullptr);
+        }
+      }
+    }
+    *outbuf = out;
+    return FlowReturn::OK;
+  }
+
+  // ---------------------------------------------------------------- stats ----
+  void record_stats(int64_t dur_ns, int64_t now) {
+    if (latency_mode_ <= 0 && throughput_mode_ <= 0 && !latency_report_) return;
+    std::lock_guard<std::mutex> lk(stat_mu_);
+    ++total_invoke_;
+    if (total_invoke_ <= kWarmup) return;  // ignore warm-up samples
+    lat_.push_back(dur_ns);
+    if (lat_.size() > 10) lat_.pop_front();
+    stamps_.push_back(now);
+    if (stamps_.size() > 10) stamps_.pop_front();
+    if (latency_report_) {
+      int64_t avg = 0;
+      for (auto v : lat_) avg += v;
+      avg /= static_cast<int64_t>(lat_.size());
+      if (reported_ <= 0 || avg > reported_ * 125 / 100 || avg < reported_ * 75 / 100) {
+        reported_ = avg;
+        Structure s("latency");
+        s.set("latency-ns", Value::Int(avg * 105 / 100));  // +5% headroom like the reference
+        post_latency();
+      }
+    }
+  }
+
+  int64_t avg_latency_us() const {
+    std::lock_guard<std::mutex> lk(stat_mu_);
+    if (lat_.empty()) return 0;
+    int64_t s = 0;
+    for (auto v : lat_) s += v;
+    return s / static_cast<int64_t>(lat_.size()) / 1000;
+  }
+
+  int64_t throughput_milli_fps() const {
+    std::lock_guard<std::mutex> lk(stat_mu_);
+    if (stamps_.size() < 2) return 0;
+    int64_t span = stamps_.back() - stamps_.front();
+    if (span <= 0) return 0;
+    return static_cast<int64_t>((stamps_.size() - 1) * 1000.0 * 1e9 / static_cast<double>(span));
+  }
+
+  bool start() override {
+    prev_ts_ = -1;
+    throttle_delay_ = 0;
+    {
+      std::lock_guard<std::mutex> lk(stat_mu_);
+      lat_.clear();
+      stamps_.clear();
+      total_invoke_ = 0;
+    }
+    return ensure_open();
+  }
+  bool stop() override { return true; }
+  void close() override { close_fw(); }
+
+ private:
+  static constexpr int64_t kWarmup = 0;
+  std::string fw_name_, model_str_, input_str_, inputtype_str_, inputname_str_, inputranks_str_, output_str_,
+      outputtype_str_, outputname_str_, outputranks_str_, input_comb_str_, output_comb_str_, config_file_;
+  FilterProperties props_;
+  std::vector<int> input_comb_;
+  std::vector<std::pair<bool, int>> out_comb_;
+  bool latency_report_ = false;
+  int latency_mode_ = 0, throughput_mode_ = 0;
+  int device_prop_ = -1;
+  std::shared_ptr<FilterFramework> fw_;
+  std::shared_ptr<FilterInstance> inst_;
+  std::shared_ptr<SharedModel> shared_;
+  std::mutex open_mu_;
+  bool model_info_known_ = false;
+  TensorsInfo model_in_, model_out_, model_out_runtime_;
+  TensorsConfig in_config_, out_config_;
+  bool in_flexible_ = false, out_flexible_ = false, configured_ = false;
+  int64_t throttle_delay_ = 0, prev_ts_ = -1;
+  mutable std::mutex stat_mu_;
+  std::deque<int64_t> lat_, stamps_;
+  int64_t total_invoke_ = 0, reported_ = 0;
+  StreamSet streams_;
+};
+
+}  // namespace
+
+void register_tensor_filter() {
+  register_element("tensor_filter", "Filter/Tensor", "Handles NN Frameworks (e.g., pytorch) as Media Filters with other/tensor type stream",
+                   [](const std::string& n) { return std::make_unique<TensorFilter>(n); });
+}
+
+}  // namespace nnsx

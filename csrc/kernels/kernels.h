@@ -1,0 +1,60 @@
+// Host-side launch API of the hand-written CDNA4 (gfx950) kernels.
+// Every launcher is asynchronous on the given stream, allocation-free and
+// graph-capturable (no hipMalloc / sync inside).
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "core/types.h"
+
+namespace nnsx {
+namespace kernels {
+
+// --------------------------------------------------------------- transform ----
+enum ArithKind : int { OP_ADD = 0, OP_MUL = 1, OP_DIV = 2, OP_CLAMP = 3 };
+
+struct ArithOp {
+  int kind;          // ArithKind
+  double fval;       // operand as double (floats)
+  int64_t ival;      // operand as int64 (integer compute types)
+  double fval2;      // clamp max
+  int ch;            // -1 = all channels
+};
+
+constexpr int kMaxArithOps = 16;
+
+struct ArithParams {
+  int nops = 0;
+  ArithOp ops[kMaxArithOps];
+  // per-channel: channel = (i / ch_size) % ch_count ; ch_count = 0 disables
+  uint64_t ch_size = 1;
+  uint32_t ch_count = 0;
+};
+
+// out[i] = ops(cast<out_t>(in[i]))   (tensor_transform typecast / arithmetic / clamp)
+void arith(const void* in, DType in_t, void* out, DType out_t, uint64_t n, const ArithParams& p,
+           hipStream_t s);
+
+// Generic permutation of up to 8 axes: out.dim[k] = in.dim[perm[k]]
+// (tensor_transform transpose / dimchg).  dims are innermost-first.
+void permute(const void* in, void* out, size_t elem_size, const uint32_t in_dim[8], const int perm[8],
+             hipStream_t s);
+
+// Standardisation (tensor_transform stand): two-pass, fp64 statistics.
+// mode 0 = default |x-mean|/std, 1 = dc-average x-mean; per_channel reduces over d0.
+// `ws` must hold at least stand_workspace_bytes(ch) bytes.
+size_t stand_workspace_bytes(uint32_t channels);
+void stand(const void* in, DType in_t, void* out, DType out_t, uint64_t n, uint32_t channels, int mode,
+           bool per_channel, void* ws, hipStream_t s);
+
+// ------------------------------------------------------------------ decode ----
+// Global argmax over n elements (first max wins).  out_index: int32 on device.
+void argmax(const void* in, DType t, uint64_t n, int32_t* out_index, hipStream_t s);
+// Batched argmax: rows of `n` elements, `batch` rows -> out_index[batch]
+void argmax_rows(const void* in, DType t, uint64_t n, uint32_t batch, int32_t* out_index, hipStream_t s);
+
+}  // namespace kernels
+}  // namespace nnsx

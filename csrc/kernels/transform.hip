@@ -1,0 +1,382 @@
+// tensor_transform kernels for gfx950.
+//
+// * arith: fused typecast + add/mul/div chain (+ per-channel operands, clamp)
+//   in one pass over HBM -- the reference needs one ORC pass per operator
+//   (gst/nnstreamer/elements/gsttensor_transform.c:1241-1412).  Semantics
+//   follow the reference's C path: every operator runs in the output type
+//   with the operand cast to it first (integer ops wrap, integer div
+//   truncates), half types round after each op.
+// * permute: transpose / dimchg as one gather pass with coalesced writes.
+// * stand: fp64 two-pass mean / population std (tensor_data.c:315-493).
+//
+// Memory-bound: 8 elements per lane, 256-thread blocks, grid capped at
+// 8 blocks per CU x 256 CUs with a grid-stride loop (cdna_hip_programming.md G11).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <type_traits>
+
+#include "kernels/dtype.cuh"
+#include "kernels/kernels.h"
+
+namespace nnsx {
+namespace kernels {
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kVec = 8;
+
+inline unsigned grid_for(uint64_t work_items) {
+  uint64_t g = (work_items + kBlock - 1) / kBlock;
+  return static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(g, 2048)));
+}
+
+template <typename T>
+__device__ __forceinline__ T apply_op(T v, const ArithOp& op) {
+  if constexpr (is_intlike<T>::value) {
+    using W = typename std::conditional<is_unsigned_int<T>::value, uint64_t, int64_t>::type;
+    if (op.kind == OP_CLAMP) {
+      double d = static_cast<double>(v);
+      d = d < op.fval ? op.fval : (d > op.fval2 ? op.fval2 : d);
+      return static_cast<T>(d);
+    }
+    W a = static_cast<W>(v);
+    W b = static_cast<W>(static_cast<T>(op.ival));
+    switch (op.kind) {
+      case OP_ADD: return static_cast<T>(a + b);
+      case OP_MUL: return static_cast<T>(a * b);
+      default: return b == 0 ? static_cast<T>(0) : static_cast<T>(a / b);
+    }
+  } else if constexpr (std::is_same<T, f16s>::value || std::is_same<T, bf16s>::value) {
+    float a = to_f32(v);
+    float b = static_cast<float>(op.fval);
+    float r;
+    switch (op.kind) {
+      case OP_ADD: r = a + to_f32(Num<T>::from(b)); break;
+      case OP_MUL: r = a * to_f32(Num<T>::from(b)); break;
+      case OP_DIV: r = a / to_f32(Num<T>::from(b)); break;
+      default: r = a < op.fval ? static_cast<float>(op.fval) : (a > op.fval2 ? static_cast<float>(op.fval2) : a); break;
+    }
+    return Num<T>::from(r);
+  } else {
+    T b = static_cast<T>(op.fval);
+    switch (op.kind) {
+      case OP_ADD: return v + b;
+      case OP_MUL: return v * b;
+      case OP_DIV: return v / b;
+      default: {
+        double d = static_cast<double>(v);
+        d = d < op.fval ? op.fval : (d > op.fval2 ? op.fval2 : d);
+        return static_cast<T>(d);
+      }
+    }
+  }
+}
+
+template <typename InT, typename OutT>
+__device__ __forceinline__ OutT eval(InT x, const ArithParams& p, uint64_t idx) {
+  OutT v = Num<OutT>::from(x);
+  if (p.ch_count) {
+    int ch = static_cast<int>((idx / p.ch_size) % p.ch_count);
+    for (int k = 0; k < p.nops; ++k)
+      if (p.ops[k].ch < 0 || p.ops[k].ch == ch) v = apply_op<OutT>(v, p.ops[k]);
+  } else {
+    for (int k = 0; k < p.nops; ++k) v = apply_op<OutT>(v, p.ops[k]);
+  }
+  return v;
+}
+
+template <typename T, int N>
+struct alignas(sizeof(T) * N) VecT {
+  T v[N];
+};
+
+// Vector path: n is a multiple of kVec and both pointers are aligned.
+template <typename InT, typename OutT>
+__global__ void __launch_bounds__(kBlock) arith_vec_kernel(const InT* __restrict__ in, OutT* __restrict__ out,
+                                                           uint64_t nvec, ArithParams p) {
+  const auto* vin = reinterpret_cast<const VecT<InT, kVec>*>(in);
+  auto* vout = reinterpret_cast<VecT<OutT, kVec>*>(out);
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < nvec;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    VecT<InT, kVec> a = vin[i];
+    VecT<OutT, kVec> b;
+#pragma unroll
+    for (int k = 0; k < kVec; ++k) b.v[k] = eval<InT, OutT>(a.v[k], p, i * kVec + k);
+    vout[i] = b;
+  }
+}
+
+template <typename InT, typename OutT>
+__global__ void __launch_bounds__(kBlock) arith_scalar_kernel(const InT* __restrict__ in, OutT* __restrict__ out,
+                                                              uint64_t begin, uint64_t n, ArithParams p) {
+  for (uint64_t i = begin + blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    out[i] = eval<InT, OutT>(in[i], p, i);
+}
+
+template <typename InT, typename OutT>
+void launch_arith(const void* in, void* out, uint64_t n, const ArithParams& p, hipStream_t s) {
+  const InT* a = static_cast<const InT*>(in);
+  OutT* b = static_cast<OutT*>(out);
+  bool aligned = (reinterpret_cast<uintptr_t>(in) % (sizeof(InT) * kVec) == 0) &&
+                 (reinterpret_cast<uintptr_t>(out) % (sizeof(OutT) * kVec) == 0);
+  uint64_t done = 0;
+  if (aligned && n >= kVec) {
+    uint64_t nvec = n / kVec;
+    hipLaunchKernelGGL((arith_vec_kernel<InT, OutT>), dim3(grid_for(nvec)), dim3(kBlock), 0, s, a, b, nvec, p);
+    done = nvec * kVec;
+  }
+  if (done < n)
+    hipLaunchKernelGGL((arith_scalar_kernel<InT, OutT>), dim3(grid_for(n - done)), dim3(kBlock), 0, s, a, b, done,
+                       n, p);
+}
+
+template <typename InT>
+void dispatch_out(DType out_t, const void* in, void* out, uint64_t n, const ArithParams& p, hipStream_t s) {
+#define NNSX_OUT(T) launch_arith<InT, T>(in, out, n, p, s)
+  NNSX_DTYPE_CASES(out_t, NNSX_OUT)
+#undef NNSX_OUT
+}
+
+// ------------------------------------------------------------------ permute ----
+struct PermParams {
+  int rank;
+  uint64_t out_dim[8];
+  uint64_t in_stride_for_out[8];  // input stride (elements) of the axis that becomes out axis k
+  uint64_t total;
+};
+
+template <typename E>
+__global__ void __launch_bounds__(kBlock) permute_kernel(const E* __restrict__ in, E* __restrict__ out, PermParams p) {
+  for (uint64_t o = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; o < p.total;
+       o += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    uint64_t rem = o, src = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k >= p.rank) break;
+      uint64_t c = rem % p.out_dim[k];
+      rem /= p.out_dim[k];
+      src += c * p.in_stride_for_out[k];
+    }
+    out[o] = in[src];
+  }
+}
+
+// HWC->CHW style transpose of the two innermost "super axes" through an LDS
+// tile (32 x 33 pad: conflict-free column reads).  in: [B][R][C] -> out: [B][C][R]
+template <typename E>
+__global__ void __launch_bounds__(kBlock) transpose2d_kernel(const E* __restrict__ in, E* __restrict__ out,
+                                                             uint64_t R, uint64_t C) {
+  __shared__ E tile[32][33];
+  const uint64_t b = blockIdx.z;
+  const uint64_t r0 = static_cast<uint64_t>(blockIdx.y) * 32, c0 = static_cast<uint64_t>(blockIdx.x) * 32;
+  const E* src = in + b * R * C;
+  E* dst = out + b * R * C;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8 threads
+  for (int k = ty; k < 32; k += 8) {
+    uint64_t r = r0 + k, c = c0 + tx;
+    if (r < R && c < C) tile[k][tx] = src[r * C + c];
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    uint64_t c = c0 + k, r = r0 + tx;
+    if (r < R && c < C) dst[c * R + r] = tile[tx][k];
+  }
+}
+
+// -------------------------------------------------------------------- stand ----
+template <typename InT>
+__global__ void __launch_bounds__(kBlock) stand_sum_kernel(const InT* __restrict__ in, uint64_t n, uint32_t C,
+                                                           bool per_channel, const double* __restrict__ mean,
+                                                           double* __restrict__ acc, int pass) {
+  // grid.y = channel (per-channel) ; pass 0 sums x, pass 1 sums (x-mean)^2
+  const uint32_t ch = per_channel ? blockIdx.y : 0;
+  const uint64_t stride = per_channel ? C : 1;
+  const uint64_t count = per_channel ? n / C : n;
+  const double m = pass ? mean[ch] : 0.0;
+  double local = 0.0;
+  for (uint64_t j = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; j < count;
+       j += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    double x = Num<InT>::as_double(in[j * stride + ch]);
+    local += pass ? (x - m) * (x - m) : x;
+  }
+  // wave64 reduction, then one LDS slot per wave
+  for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
+  __shared__ double part[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = local;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0;
+    for (int w = 0; w < kBlock / 64; ++w) s += part[w];
+    atomicAdd(&acc[ch], s);
+  }
+}
+
+__global__ void stand_finish_kernel(double* mean_or_std, uint32_t C, uint64_t count, int pass) {
+  uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  if (pass == 0) {
+    mean_or_std[c] /= static_cast<double>(count);
+  } else {
+    double v = mean_or_std[c] / static_cast<double>(count);
+    mean_or_std[c] = v != 0.0 ? sqrt(v) : 1e-10;
+  }
+}
+
+template <typename InT, typename OutT>
+__global__ void __launch_bounds__(kBlock) stand_apply_kernel(const InT* __restrict__ in, OutT* __restrict__ out,
+                                                             uint64_t n, uint32_t C, bool per_channel, int mode,
+                                                             const double* __restrict__ mean,
+                                                             const double* __restrict__ stdv) {
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    uint32_t ch = per_channel ? static_cast<uint32_t>(i % C) : 0;
+    double x = Num<InT>::as_double(in[i]);
+    double r = mode == 0 ? fabs((x - mean[ch]) / stdv[ch]) : x - mean[ch];
+    out[i] = Num<OutT>::from(r);
+  }
+}
+
+template <typename InT>
+void launch_stand(const void* in, DType out_t, void* out, uint64_t n, uint32_t C, int mode, bool per_channel,
+                  void* ws, hipStream_t s) {
+  uint32_t nch = per_channel ? C : 1;
+  double* mean = static_cast<double*>(ws);
+  double* stdv = mean + nch;
+  (void)hipMemsetAsync(ws, 0, sizeof(double) * 2 * nch, s);
+  uint64_t count = per_channel ? n / C : n;
+  dim3 grid(std::min<unsigned>(grid_for(count), 512), nch);
+  const InT* a = static_cast<const InT*>(in);
+  hipLaunchKernelGGL((stand_sum_kernel<InT>), grid, dim3(kBlock), 0, s, a, n, C, per_channel, mean, mean, 0);
+  hipLaunchKernelGGL(stand_finish_kernel, dim3((nch + 63) / 64), dim3(64), 0, s, mean, nch, count, 0);
+  if (mode == 0) {
+    hipLaunchKernelGGL((stand_sum_kernel<InT>), grid, dim3(kBlock), 0, s, a, n, C, per_channel, mean, stdv, 1);
+    hipLaunchKernelGGL(stand_finish_kernel, dim3((nch + 63) / 64), dim3(64), 0, s, stdv, nch, count, 1);
+  }
+#define NNSX_OUT(T)                                                                                          \
+  hipLaunchKernelGGL((stand_apply_kernel<InT, T>), dim3(grid_for(n)), dim3(kBlock), 0, s, a,               \
+                     static_cast<T*>(out), n, C, per_channel, mode, mean, stdv)
+  NNSX_DTYPE_CASES(out_t, NNSX_OUT)
+#undef NNSX_OUT
+}
+
+}  // namespace
+
+void arith(const void* in, DType in_t, void* out, DType out_t, uint64_t n, const ArithParams& p, hipStream_t s) {
+  if (n == 0) return;
+#define NNSX_IN(T) dispatch_out<T>(out_t, in, out, n, p, s)
+  NNSX_DTYPE_CASES(in_t, NNSX_IN)
+#undef NNSX_IN
+}
+
+void permute(const void* in, void* out, size_t elem_size, const uint32_t in_dim[8], const int perm[8],
+             hipStream_t s) {
+  uint64_t in_stride[8];
+  uint64_t acc = 1;
+  for (int k = 0; k < 8; ++k) {
+    in_stride[k] = acc;
+    acc *= in_dim[k];
+  }
+  PermParams p{};
+  p.rank = 8;
+  p.total = acc;
+  for (int k = 0; k < 8; ++k) {
+    p.out_dim[k] = in_dim[perm[k]];
+    p.in_stride_for_out[k] = in_stride[perm[k]];
+  }
+  // trim trailing unit axes for a cheaper index computation
+  while (p.rank > 1 && p.out_dim[p.rank - 1] == 1) --p.rank;
+  if (acc == 0) return;
+
+  // Special case: a pure 2-D transpose of super-axes [A][B] -> [B][A] with a
+  // batch above (e.g. HWC -> CHW: A = W*H, B = C).  Detect: out = (in axes
+  // j..r-1, then 0..j-1) for some split j, rest identity.
+  int r = 8;
+  while (r > 1 && in_dim[r - 1] == 1 && perm[r - 1] == r - 1) --r;
+  for (int j = 1; j < r; ++j) {
+    bool ok = true;
+    for (int k = 0; k < r; ++k) {
+      int expect = k < r - j ? k + j : k - (r - j);
+      if (perm[k] != expect) {
+        ok = false;
+        break;
+      }
+    }
+    // batch = outermost axis kept in place is handled by the generic path
+    if (ok) {
+      uint64_t B = 1, A = 1;
+      for (int k = 0; k < j; ++k) B *= in_dim[k];  // innermost block of the input
+      for (int k = j; k < r; ++k) A *= in_dim[k];
+      // in viewed as [A rows][B cols] -> out [B rows][A cols]
+      dim3 grid(static_cast<unsigned>((B + 31) / 32), static_cast<unsigned>((A + 31) / 32), 1);
+      if (grid.y <= 65535 && A >= 32 && B >= 32) {
+        switch (elem_size) {
+          case 1: hipLaunchKernelGGL(transpose2d_kernel<uint8_t>, grid, dim3(256), 0, s, (const uint8_t*)in, (uint8_t*)out, A, B); return;
+          case 2: hipLaunchKernelGGL(transpose2d_kernel<uint16_t>, grid, dim3(256), 0, s, (const uint16_t*)in, (uint16_t*)out, A, B); return;
+          case 4: hipLaunchKernelGGL(transpose2d_kernel<uint32_t>, grid, dim3(256), 0, s, (const uint32_t*)in, (uint32_t*)out, A, B); return;
+          case 8: hipLaunchKernelGGL(transpose2d_kernel<uint64_t>, grid, dim3(256), 0, s, (const uint64_t*)in, (uint64_t*)out, A, B); return;
+          default: break;
+        }
+      }
+      break;
+    }
+  }
+  // transpose with the outermost axis kept (HWC->CHW with N frames): batch over the last kept axis
+  {
+    int rr = r;
+    if (rr >= 2 && perm[rr - 1] == rr - 1) {
+      int r2 = rr - 1;
+      for (int j = 1; j < r2; ++j) {
+        bool ok = true;
+        for (int k = 0; k < r2; ++k) {
+          int expect = k < r2 - j ? k + j : k - (r2 - j);
+          if (perm[k] != expect) {
+            ok = false;
+            break;
+          }
+        }
+        if (ok) {
+          uint64_t Bc = 1, A = 1;
+          for (int k = 0; k < j; ++k) Bc *= in_dim[k];
+          for (int k = j; k < r2; ++k) A *= in_dim[k];
+          uint64_t batch = in_dim[rr - 1];
+          dim3 grid(static_cast<unsigned>((Bc + 31) / 32), static_cast<unsigned>((A + 31) / 32),
+                    static_cast<unsigned>(batch));
+          if (grid.y <= 65535 && batch <= 65535 && A >= 32 && Bc >= 32) {
+            switch (elem_size) {
+              case 1: hipLaunchKernelGGL(transpose2d_kernel<uint8_t>, grid, dim3(256), 0, s, (const uint8_t*)in, (uint8_t*)out, A, Bc); return;
+              case 2: hipLaunchKernelGGL(transpose2d_kernel<uint16_t>, grid, dim3(256), 0, s, (const uint16_t*)in, (uint16_t*)out, A, Bc); return;
+              case 4: hipLaunchKernelGGL(transpose2d_kernel<uint32_t>, grid, dim3(256), 0, s, (const uint32_t*)in, (uint32_t*)out, A, Bc); return;
+              case 8: hipLaunchKernelGGL(transpose2d_kernel<uint64_t>, grid, dim3(256), 0, s, (const uint64_t*)in, (uint64_t*)out, A, Bc); return;
+              default: break;
+            }
+          }
+          break;
+        }
+      }
+    }
+  }
+  unsigned g = grid_for(acc);
+  switch (elem_size) {
+    case 1: hipLaunchKernelGGL(permute_kernel<uint8_t>, dim3(g), dim3(kBlock), 0, s, (const uint8_t*)in, (uint8_t*)out, p); break;
+    case 2: hipLaunchKernelGGL(permute_kernel<uint16_t>, dim3(g), dim3(kBlock), 0, s, (const uint16_t*)in, (uint16_t*)out, p); break;
+    case 4: hipLaunchKernelGGL(permute_kernel<uint32_t>, dim3(g), dim3(kBlock), 0, s, (const uint32_t*)in, (uint32_t*)out, p); break;
+    case 8: hipLaunchKernelGGL(permute_kernel<uint64_t>, dim3(g), dim3(kBlock), 0, s, (const uint64_t*)in, (uint64_t*)out, p); break;
+    default: break;
+  }
+}
+
+size_t stand_workspace_bytes(uint32_t channels) { return sizeof(double) * 2 * (channels ? channels : 1); }
+
+void stand(const void* in, DType in_t, void* out, DType out_t, uint64_t n, uint32_t channels, int mode,
+           bool per_channel, void* ws, hipStream_t s) {
+  if (n == 0) return;
+#define NNSX_IN(T) launch_stand<T>(in, out_t, out, n, channels, mode, per_channel, ws, s)
+  NNSX_DTYPE_CASES(in_t, NNSX_IN)
+#undef NNSX_IN
+}
+
+}  // namespace kernels
+}  // namespace nnsx

@@ -1,0 +1,209 @@
+#include "runtime/hip_util.h"
+
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <thread>
+
+#include "core/util.h"
+
+namespace nnsx {
+namespace hip {
+
+int device_count() {
+  static int count = [] {
+    if (const char* e = std::getenv("NNSX_DISABLE_GPU")) {
+      if (to_bool(e)) return 0;
+    }
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+      (void)hipGetLastError();
+      return 0;
+    }
+    return n;
+  }();
+  return count;
+}
+
+bool available() { return device_count() > 0; }
+
+std::string device_arch(int dev) {
+  if (!available()) return "";
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return "";
+  return prop.gcnArchName;
+}
+
+void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) {
+    throw Error(strfmt("HIP error ", hipGetErrorName(e), " (", hipGetErrorString(e), ") at ", what));
+  }
+}
+
+DeviceGuard::DeviceGuard(int dev) {
+  if (dev < 0 || !available()) return;
+  if (hipGetDevice(&prev_) != hipSuccess) prev_ = -1;
+  if (prev_ != dev) {
+    check(hipSetDevice(dev), "hipSetDevice");
+    changed_ = true;
+  }
+}
+
+DeviceGuard::~DeviceGuard() {
+  if (changed_ && prev_ >= 0) (void)hipSetDevice(prev_);
+}
+
+namespace {
+struct EventPool {
+  std::mutex mu;
+  std::unordered_map<int, std::vector<hipEvent_t>> free;
+};
+EventPool& event_pool() {
+  static EventPool* p = new EventPool();  // leaked on purpose: outlives static dtors
+  return *p;
+}
+}  // namespace
+
+hipEvent_t event_get(int dev) {
+  auto& pool = event_pool();
+  {
+    std::lock_guard<std::mutex> lk(pool.mu);
+    auto& v = pool.free[dev];
+    if (!v.empty()) {
+      hipEvent_t e = v.back();
+      v.pop_back();
+      return e;
+    }
+  }
+  DeviceGuard g(dev);
+  hipEvent_t e;
+  check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreateWithFlags");
+  return e;
+}
+
+void event_put(int dev, hipEvent_t ev) {
+  if (!ev) return;
+  auto& pool = event_pool();
+  std::lock_guard<std::mutex> lk(pool.mu);
+  pool.free[dev].push_back(ev);
+}
+
+hipStream_t stream_create(int dev, int priority) {
+  DeviceGuard g(dev);
+  hipStream_t s;
+  check(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority), "hipStreamCreateWithPriority");
+  return s;
+}
+
+void stream_destroy(int dev, hipStream_t s) {
+  if (!s) return;
+  DeviceGuard g(dev);
+  (void)hipStreamSynchronize(s);
+  (void)hipStreamDestroy(s);
+}
+
+hipStream_t release_stream(int dev) {
+  static std::mutex mu;
+  static std::map<int, hipStream_t>* streams = new std::map<int, hipStream_t>();
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = streams->find(dev);
+  if (it != streams->end()) return it->second;
+  hipStream_t s = stream_create(dev);
+  (*streams)[dev] = s;
+  return s;
+}
+
+hipStream_t thread_copy_stream(int dev) {
+  thread_local std::map<int, hipStream_t> streams;  // leaked at thread exit (driver reclaims at exit)
+  auto it = streams.find(dev);
+  if (it != streams.end()) return it->second;
+  hipStream_t s = stream_create(dev);
+  streams[dev] = s;
+  return s;
+}
+
+namespace {
+std::once_flag g_pool_once[64];
+void configure_pool(int dev) {
+  std::call_once(g_pool_once[dev & 63], [dev] {
+    DeviceGuard g(dev);
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+      uint64_t thr = UINT64_MAX;  // keep everything cached: 288 GB of HBM per GPU
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+    }
+    (void)hipGetLastError();
+  });
+}
+}  // namespace
+
+void* device_alloc(int dev, size_t bytes, hipStream_t s) {
+  configure_pool(dev);
+  DeviceGuard g(dev);
+  void* p = nullptr;
+  check(hipMallocAsync(&p, bytes ? bytes : 1, s), "hipMallocAsync");
+  return p;
+}
+
+void device_free(int dev, void* p, hipStream_t s) {
+  if (!p) return;
+  DeviceGuard g(dev);
+  (void)hipFreeAsync(p, s);
+}
+
+namespace {
+struct PinnedPool {
+  std::mutex mu;
+  std::map<size_t, std::vector<void*>> free;  // bucket size -> blocks
+};
+PinnedPool& pinned_pool() {
+  static PinnedPool* p = new PinnedPool();
+  return *p;
+}
+size_t bucket(size_t n) {
+  size_t b = 256;
+  while (b < n) b <<= 1;
+  return b;
+}
+}  // namespace
+
+void* pinned_alloc(size_t bytes) {
+  if (!available()) return host_alloc(bytes);
+  size_t b = bucket(bytes);
+  auto& pool = pinned_pool();
+  {
+    std::lock_guard<std::mutex> lk(pool.mu);
+    auto& v = pool.free[b];
+    if (!v.empty()) {
+      void* p = v.back();
+      v.pop_back();
+      return p;
+    }
+  }
+  void* p = nullptr;
+  check(hipHostMalloc(&p, b, hipHostMallocDefault), "hipHostMalloc");
+  return p;
+}
+
+void pinned_free(void* p, size_t bytes) {
+  if (!p) return;
+  if (!available()) {
+    host_free(p);
+    return;
+  }
+  auto& pool = pinned_pool();
+  std::lock_guard<std::mutex> lk(pool.mu);
+  pool.free[bucket(bytes)].push_back(p);
+}
+
+void* host_alloc(size_t bytes) {
+  void* p = nullptr;
+  size_t n = (bytes + 63) & ~static_cast<size_t>(63);
+  if (posix_memalign(&p, 64, n ? n : 64) != 0) throw Error("host_alloc: out of memory");
+  return p;
+}
+
+void host_free(void* p) { std::free(p); }
+
+}  // namespace hip
+}  // namespace nnsx

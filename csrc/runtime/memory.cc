@@ -1,0 +1,337 @@
+#include "runtime/memory.h"
+
+#include <cstring>
+
+#include "core/util.h"
+#include "runtime/hip_util.h"
+
+namespace nnsx {
+
+Memory::Memory(void* data, size_t size, MemPlace place, int device, Release release)
+    : data_(data), size_(size), place_(place), device_(device), release_(std::move(release)) {}
+
+Memory::~Memory() {
+  if (release_) release_(this);
+  if (ready_) hip::event_put(ready_dev_, ready_);
+  for (auto& u : uses_) hip::event_put(u.first, u.second);
+}
+
+MemoryPtr Memory::alloc_host(size_t size) {
+  void* p = hip::host_alloc(size);
+  return std::make_shared<Memory>(p, size, MemPlace::HOST, -1, [](Memory* m) { hip::host_free(m->data()); });
+}
+
+MemoryPtr Memory::alloc_pinned(size_t size) {
+  if (!hip::available()) return alloc_host(size);
+  void* p = hip::pinned_alloc(size);
+  return std::make_shared<Memory>(p, size, MemPlace::PINNED, -1, [](Memory* m) {
+    // a pending H2D may still read this block: wait for recorded readers
+    m->sync_uses();
+    hip::pinned_free(m->data(), m->size());
+  });
+}
+
+MemoryPtr Memory::alloc_device(size_t size, int dev, hipStream_t stream) {
+  void* p = hip::device_alloc(dev, size, stream);
+  return std::make_shared<Memory>(p, size, MemPlace::DEVICE, dev, [dev](Memory* m) {
+    // the block returns to the stream-ordered pool only after the producer and
+    // every recorded reader: the free is ordered on a process-lifetime stream
+    hipStream_t rs = hip::release_stream(dev);
+    m->wait_ready(rs);
+    m->wait_uses(rs);
+    hip::device_free(dev, m->data(), rs);
+  });
+}
+
+MemoryPtr Memory::wrap(void* data, size_t size, MemPlace place, int device, Release release) {
+  return std::make_shared<Memory>(data, size, place, device, std::move(release));
+}
+
+MemoryPtr Memory::view(const MemoryPtr& parent, size_t offset, size_t size) {
+  if (offset + size > parent->size()) throw Error("Memory::view out of range");
+  auto m = std::make_shared<Memory>(static_cast<char*>(parent->data()) + offset, size, parent->place(),
+                                    parent->device(), nullptr);
+  m->parent_ = parent;
+  return m;
+}
+
+MemoryPtr Memory::from_bytes(const void* src, size_t size) {
+  auto m = alloc_host(size);
+  if (size) std::memcpy(m->data(), src, size);
+  return m;
+}
+
+void Memory::mark_ready(hipStream_t stream) {
+  Memory* r = root();
+  if (r->place_ == MemPlace::HOST) return;
+  int dev = r->device_ >= 0 ? r->device_ : 0;
+  std::lock_guard<std::mutex> lk(r->ev_mu_);
+  if (!r->ready_) {
+    r->ready_ = hip::event_get(dev);
+    r->ready_dev_ = dev;
+  }
+  hip::check(hipEventRecord(r->ready_, stream), "hipEventRecord(ready)");
+}
+
+void Memory::wait_ready(hipStream_t stream) const {
+  const Memory* r = root();
+  std::lock_guard<std::mutex> lk(r->ev_mu_);
+  if (r->ready_) hip::check(hipStreamWaitEvent(stream, r->ready_, 0), "hipStreamWaitEvent(ready)");
+}
+
+void Memory::sync_ready() const {
+  const Memory* r = root();
+  hipEvent_t e;
+  {
+    std::lock_guard<std::mutex> lk(r->ev_mu_);
+    e = r->ready_;
+  }
+  if (e) hip::check(hipEventSynchronize(e), "hipEventSynchronize(ready)");
+}
+
+void Memory::record_use(hipStream_t stream, int dev) {
+  Memory* r = root();
+  hipEvent_t e = hip::event_get(dev);
+  hip::check(hipEventRecord(e, stream), "hipEventRecord(use)");
+  std::lock_guard<std::mutex> lk(r->ev_mu_);
+  r->uses_.emplace_back(dev, e);
+  // bound the list: a long-lived memory read by many frames keeps the tail only
+  if (r->uses_.size() > 64) {
+    hip::event_put(r->uses_.front().first, r->uses_.front().second);
+    r->uses_.erase(r->uses_.begin());
+  }
+}
+
+void Memory::wait_uses(hipStream_t stream) const {
+  const Memory* r = root();
+  std::lock_guard<std::mutex> lk(r->ev_mu_);
+  for (auto& u : r->uses_) (void)hipStreamWaitEvent(stream, u.second, 0);
+}
+
+void Memory::sync_uses() const {
+  const Memory* r = root();
+  std::lock_guard<std::mutex> lk(r->ev_mu_);
+  for (auto& u : r->uses_) (void)hipEventSynchronize(u.second);
+}
+
+const void* Memory::map_host() {
+  if (place_ != MemPlace::DEVICE) {
+    if (place_ == MemPlace::PINNED) sync_ready();  // a D2H may be landing here
+    return data_;
+  }
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!host_mirror_) {
+    auto mirror = alloc_pinned(size_);
+    hip::DeviceGuard g(device_);
+    hipStream_t s = hip::thread_copy_stream(device_);
+    wait_ready(s);  // producer first, then copy, then block: the caller wants bytes now
+    if (size_) hip::check(hipMemcpyAsync(mirror->data(), data_, size_, hipMemcpyDeviceToHost, s), "D2H");
+    hip::check(hipStreamSynchronize(s), "hipStreamSynchronize(map_host)");
+    host_mirror_ = mirror;
+  }
+  return host_mirror_->data();
+}
+
+const void* Memory::map_device(int dev, hipStream_t stream) {
+  if (place_ == MemPlace::DEVICE && device_ == dev) {
+    wait_ready(stream);
+    return data_;
+  }
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = dev_mirror_.find(dev);
+  if (it != dev_mirror_.end()) {
+    it->second->wait_ready(stream);
+    return it->second->data();
+  }
+  auto mirror = alloc_device(size_, dev, stream);
+  hip::DeviceGuard g(dev);
+  if (place_ == MemPlace::DEVICE) {
+    wait_ready(stream);  // peer copy over xGMI after the producer
+    if (size_) hip::check(hipMemcpyPeerAsync(mirror->data(), dev, data_, device_, size_, stream), "P2P");
+    record_use(stream, dev);
+  } else {
+    if (size_) hip::check(hipMemcpyAsync(mirror->data(), data_, size_, hipMemcpyHostToDevice, stream), "H2D");
+    // a pinned source is read asynchronously: it must not be recycled before the copy ran
+    if (place_ == MemPlace::PINNED) record_use(stream, dev);
+  }
+  mirror->mark_ready(stream);
+  dev_mirror_[dev] = mirror;
+  return mirror->data();
+}
+
+// ------------------------------------------------------------ helpers ----
+
+bool buffer_from_config(const BufferPtr& in, const TensorsConfig& config, BufferPtr* out) {
+  auto b = make_buffer();
+  b->copy_metadata_from(*in);
+  if (config.is_static()) {
+    unsigned n = config.info.num_tensors;
+    if (in->n_memory() == n) {
+      b->mems = in->mems;
+      for (unsigned i = 0; i < n; ++i)
+        if (in->mems[i]->size() != config.info.at(i).size()) return false;
+    } else if (in->n_memory() >= 1) {
+      // one (or more) contiguous chunk(s): concatenate views across memories
+      size_t total = in->total_size();
+      if (total != config.info.size()) return false;
+      size_t mi = 0, moff = 0;
+      for (unsigned i = 0; i < n; ++i) {
+        size_t need = config.info.at(i).size();
+        if (mi >= in->n_memory()) return false;
+        if (moff + need <= in->mems[mi]->size()) {
+          b->mems.push_back(Memory::view(in->mems[mi], moff, need));
+          moff += need;
+          if (moff == in->mems[mi]->size()) {
+            ++mi;
+            moff = 0;
+          }
+        } else {
+          return false;  // tensor straddles memories: unsupported
+        }
+      }
+    } else {
+      return false;
+    }
+  } else {
+    // flexible/sparse: one tensor per memory, or headers walked inside one memory
+    for (auto& m : in->mems) {
+      if (m->has_meta()) {
+        b->mems.push_back(m);
+        continue;
+      }
+      const uint8_t* p = static_cast<const uint8_t*>(m->map_host());
+      size_t off = 0;
+      while (off < m->size()) {
+        MetaInfo meta;
+        if (!MetaInfo::parse(p + off, m->size() - off, &meta)) return false;
+        size_t sz = meta.header_size() + meta.data_size();
+        if (off + sz > m->size()) return false;
+        b->mems.push_back(Memory::view(m, off, sz));
+        off += sz;
+      }
+    }
+  }
+  *out = b;
+  return true;
+}
+
+MemoryPtr make_flexible(const MemoryPtr& mem, const MetaInfo& meta) {
+  if (mem->on_device()) {
+    auto v = Memory::view(mem, 0, mem->size());
+    v->set_meta(meta);
+    return v;
+  }
+  auto m = Memory::alloc_host(kMetaHeaderSize + mem->size());
+  meta.write(m->data());
+  if (mem->size()) std::memcpy(static_cast<char*>(m->data()) + kMetaHeaderSize, mem->map_host(), mem->size());
+  return m;
+}
+
+bool parse_flexible(const MemoryPtr& mem, MetaInfo* meta, MemoryPtr* payload) {
+  if (mem->has_meta()) {
+    *meta = mem->meta();
+    if (payload) *payload = mem;
+    return meta->valid();
+  }
+  if (mem->size() < kMetaHeaderSize) return false;
+  const void* p = mem->on_device() ? nullptr : mem->map_host();
+  MetaInfo m;
+  if (p) {
+    if (!MetaInfo::parse(p, mem->size(), &m)) return false;
+  } else {
+    // device memory with in-band header: read the 128 bytes only
+    uint8_t hdr[kMetaHeaderSize];
+    hip::DeviceGuard g(mem->device());
+    hipStream_t s = hip::thread_copy_stream(mem->device());
+    mem->wait_ready(s);
+    hip::check(hipMemcpyAsync(hdr, mem->data(), kMetaHeaderSize, hipMemcpyDeviceToHost, s), "D2H hdr");
+    hip::check(hipStreamSynchronize(s), "sync hdr");
+    if (!MetaInfo::parse(hdr, kMetaHeaderSize, &m)) return false;
+  }
+  size_t hs = m.header_size();
+  size_t ds = m.data_size();
+  if (hs + ds > mem->size()) return false;
+  *meta = m;
+  if (payload) *payload = Memory::view(mem, hs, ds);
+  return true;
+}
+
+std::vector<uint8_t> serialize_with_header(const MemoryPtr& mem) {
+  std::vector<uint8_t> out;
+  const uint8_t* p = static_cast<const uint8_t*>(mem->map_host());
+  if (mem->has_meta()) {
+    out.resize(kMetaHeaderSize + mem->size());
+    mem->meta().write(out.data());
+    std::memcpy(out.data() + kMetaHeaderSize, p, mem->size());
+  } else {
+    out.assign(p, p + mem->size());
+  }
+  return out;
+}
+
+namespace {
+struct ExtraHeader {
+  uint32_t magic;
+  uint32_t version;
+  uint32_t num_extra;
+  uint32_t pad;
+  uint64_t reserved;  // size of the 16th tensor
+};
+struct ExtraEntry {
+  uint32_t type;
+  uint32_t dim[kRankLimit];
+};
+constexpr size_t kExtraInfoSize = sizeof(ExtraHeader) + sizeof(ExtraEntry) * kSizeExtraLimit;
+}  // namespace
+
+std::vector<MemoryPtr> pack_extra(const std::vector<MemoryPtr>& mems, const TensorsInfo& info) {
+  if (mems.size() <= static_cast<size_t>(kSizeLimit)) return mems;
+  std::vector<MemoryPtr> out(mems.begin(), mems.begin() + (kSizeLimit - 1));
+  size_t total = kExtraInfoSize;
+  for (size_t i = kSizeLimit - 1; i < mems.size(); ++i) total += mems[i]->size();
+  auto blk = Memory::alloc_host(total);
+  std::memset(blk->data(), 0, kExtraInfoSize);
+  auto* h = static_cast<ExtraHeader*>(blk->data());
+  h->magic = kExtraMagic;
+  h->num_extra = static_cast<uint32_t>(mems.size() - kSizeLimit);
+  h->reserved = mems[kSizeLimit - 1]->size();
+  auto* ent = reinterpret_cast<ExtraEntry*>(h + 1);
+  for (size_t i = kSizeLimit; i < mems.size(); ++i) {
+    const auto& ti = info.at(static_cast<unsigned>(i));
+    ent[i - kSizeLimit].type = static_cast<uint32_t>(ti.type);
+    for (int d = 0; d < kRankLimit; ++d) ent[i - kSizeLimit].dim[d] = ti.dim[d];
+  }
+  size_t off = kExtraInfoSize;
+  for (size_t i = kSizeLimit - 1; i < mems.size(); ++i) {
+    std::memcpy(static_cast<char*>(blk->data()) + off, mems[i]->map_host(), mems[i]->size());
+    off += mems[i]->size();
+  }
+  out.push_back(blk);
+  return out;
+}
+
+std::vector<MemoryPtr> unpack_extra(const std::vector<MemoryPtr>& mems, TensorsInfo* info) {
+  if (mems.size() != static_cast<size_t>(kSizeLimit)) return mems;
+  const auto& last = mems.back();
+  if (last->size() < kExtraInfoSize) return mems;
+  const auto* h = static_cast<const ExtraHeader*>(last->map_host());
+  if (h->magic != kExtraMagic) return mems;
+  std::vector<MemoryPtr> out(mems.begin(), mems.end() - 1);
+  size_t off = kExtraInfoSize;
+  out.push_back(Memory::view(last, off, h->reserved));
+  off += h->reserved;
+  const auto* ent = reinterpret_cast<const ExtraEntry*>(h + 1);
+  for (uint32_t i = 0; i < h->num_extra; ++i) {
+    TensorInfo ti;
+    ti.type = static_cast<DType>(ent[i].type);
+    for (int d = 0; d < kRankLimit; ++d) ti.dim[d] = ent[i].dim[d];
+    size_t sz = ti.size();
+    out.push_back(Memory::view(last, off, sz));
+    off += sz;
+    if (info) info->at(kSizeLimit + i) = ti;
+  }
+  if (info && info->num_tensors < out.size()) info->num_tensors = static_cast<unsigned>(out.size());
+  return out;
+}
+
+}  // namespace nnsx

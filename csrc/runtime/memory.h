@@ -1,0 +1,180 @@
+// Memory / Buffer: the payload model that replaces GstMemory / GstBuffer.
+//
+// A Memory is one tensor chunk.  It lives on the host (plain or pinned) or on
+// a GPU.  Device memories carry a `ready` event recorded on the producer's
+// stream: consumers make their own stream wait on it (never a host sync), and
+// record `uses` so the block is only recycled once every reader finished.
+// `map_host` / `map_device` are the caps-boundary copies: a host<->device
+// transfer happens only where a host-only element meets device data (or the
+// reverse); adjacent GPU elements exchange device pointers zero-copy.
+//
+// Reference: gst_tensor_buffer_from_config / append/get nth memory
+// (gst/nnstreamer/nnstreamer_plugin_api_impl.c:452-556,1477-1768).
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <atomic>
+#include <cstdint>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "core/types.h"
+
+namespace nnsx {
+
+enum class MemPlace { HOST = 0, PINNED = 1, DEVICE = 2 };
+
+class Memory;
+using MemoryPtr = std::shared_ptr<Memory>;
+
+class Memory : public std::enable_shared_from_this<Memory> {
+ public:
+  using Release = std::function<void(Memory*)>;
+
+  Memory(void* data, size_t size, MemPlace place, int device, Release release);
+  ~Memory();
+  Memory(const Memory&) = delete;
+  Memory& operator=(const Memory&) = delete;
+
+  static MemoryPtr alloc_host(size_t size);
+  static MemoryPtr alloc_pinned(size_t size);
+  static MemoryPtr alloc_device(size_t size, int dev, hipStream_t stream);
+  // Wrap external memory.  `release` runs when the last reference drops.
+  static MemoryPtr wrap(void* data, size_t size, MemPlace place, int device, Release release = nullptr);
+  // Sub-view sharing the parent's storage (zero-copy slice / split / demux).
+  static MemoryPtr view(const MemoryPtr& parent, size_t offset, size_t size);
+  // Host copy of bytes.
+  static MemoryPtr from_bytes(const void* src, size_t size);
+
+  void* data() const { return data_; }
+  size_t size() const { return size_; }
+  MemPlace place() const { return place_; }
+  int device() const { return device_; }
+  bool on_device() const { return place_ == MemPlace::DEVICE; }
+  bool host_accessible() const { return place_ != MemPlace::DEVICE; }
+
+  // --- producer side (device memories) ---
+  // Record the ready event on `stream` (after the producing work is enqueued).
+  void mark_ready(hipStream_t stream);
+  // --- consumer side ---
+  // Make `stream` wait until the producer's writes are visible.
+  void wait_ready(hipStream_t stream) const;
+  // Host wait for the producer (map paths).
+  void sync_ready() const;
+  // Record that work enqueued on `stream` reads this memory.
+  void record_use(hipStream_t stream, int dev);
+  // Events of every recorded reader (used when releasing the block).
+  void wait_uses(hipStream_t stream) const;
+  void sync_uses() const;
+
+  // Host-visible pointer.  Device memories are copied into a cached pinned
+  // mirror (one D2H per memory, however many host readers).
+  const void* map_host();
+  // Device pointer on `dev`, ordered on `stream`.  Host memories are uploaded
+  // into a cached device mirror (one H2D per memory and device).
+  const void* map_device(int dev, hipStream_t stream);
+
+  // Typed metadata carried per memory.
+  std::map<std::string, int64_t>& tags() { return tags_; }
+
+  // Flexible/sparse meta attached out-of-band (device memories keep the
+  // 128-byte header off the payload so no payload copy is needed; host
+  // memories carry it in-band like the reference).
+  bool has_meta() const { return has_meta_; }
+  const MetaInfo& meta() const { return meta_; }
+  void set_meta(const MetaInfo& m) { meta_ = m; has_meta_ = true; }
+
+  Memory* root() { return parent_ ? parent_->root() : this; }
+  const Memory* root() const { return parent_ ? parent_->root() : this; }
+
+ private:
+  void* data_;
+  size_t size_;
+  MemPlace place_;
+  int device_;
+  Release release_;
+  MemoryPtr parent_;  // for views
+  hipEvent_t ready_ = nullptr;
+  int ready_dev_ = 0;
+  mutable std::mutex ev_mu_;  // ready_ / uses_ (only the root's is used)
+  mutable std::mutex mu_;     // mirrors
+  std::vector<std::pair<int, hipEvent_t>> uses_;
+  MemoryPtr host_mirror_;
+  std::map<int, MemoryPtr> dev_mirror_;
+  std::map<std::string, int64_t> tags_;
+  MetaInfo meta_;
+  bool has_meta_ = false;
+};
+
+// Meta a buffer carries across elements.
+struct BufferMeta {
+  int64_t client_id = -1;  // GstMetaQuery client id (tensor_query routing)
+  std::map<std::string, std::string> extra;
+};
+
+enum BufferFlags : uint32_t {
+  BUF_FLAG_NONE = 0,
+  BUF_FLAG_DISCONT = 1u << 0,
+  BUF_FLAG_GAP = 1u << 1,
+  BUF_FLAG_DELTA = 1u << 2,
+};
+
+struct Buffer {
+  std::vector<MemoryPtr> mems;
+  int64_t pts = -1;
+  int64_t dts = -1;
+  int64_t duration = -1;
+  int64_t offset = -1;
+  int64_t offset_end = -1;
+  uint32_t flags = 0;
+  BufferMeta meta;
+
+  size_t n_memory() const { return mems.size(); }
+  MemoryPtr& mem(size_t i) { return mems.at(i); }
+  size_t total_size() const {
+    size_t s = 0;
+    for (auto& m : mems) s += m->size();
+    return s;
+  }
+  void copy_metadata_from(const Buffer& o) {
+    pts = o.pts;
+    dts = o.dts;
+    duration = o.duration;
+    offset = o.offset;
+    offset_end = o.offset_end;
+    flags = o.flags;
+    meta = o.meta;
+  }
+};
+using BufferPtr = std::shared_ptr<Buffer>;
+
+inline BufferPtr make_buffer() { return std::make_shared<Buffer>(); }
+
+// ---- tensor <-> buffer helpers ----
+// Split one contiguous memory into per-tensor chunks of a static config, or walk
+// flexible headers.  Views share storage (zero-copy).
+bool buffer_from_config(const BufferPtr& in, const TensorsConfig& config, BufferPtr* out);
+// Make a flexible-format memory: host memories get the 128B header prepended
+// (byte-compatible with the reference); device memories get it attached.
+MemoryPtr make_flexible(const MemoryPtr& mem, const MetaInfo& meta);
+// Read the meta of a flexible memory and return the payload (zero-copy view).
+bool parse_flexible(const MemoryPtr& mem, MetaInfo* meta, MemoryPtr* payload);
+// Serialize a memory to host bytes with an in-band header when it carries meta.
+std::vector<uint8_t> serialize_with_header(const MemoryPtr& mem);
+// nnsx buffers are not limited to 16 memories (no GstBuffer memory cap), so
+// >16 tensors are held as plain extra memories.  For wire/file formats that
+// must stay within 16 chunks the reference's "extra tensors" packing
+// (nnstreamer_plugin_api_impl.c:1477-1768) is available explicitly:
+// memories [15..] are concatenated behind an ExtraInfo header.
+std::vector<MemoryPtr> pack_extra(const std::vector<MemoryPtr>& mems, const TensorsInfo& info);
+std::vector<MemoryPtr> unpack_extra(const std::vector<MemoryPtr>& mems, TensorsInfo* info);
+
+// "Extra tensors" header in the 16th memory (magic 0xf00dc0de).
+constexpr uint32_t kExtraMagic = 0xf00dc0deu;
+
+}  // namespace nnsx
