@@ -422,6 +422,8 @@ PYBIND11_MODULE(_C, m) {
         return v;
       })
       .def("dot", &Pipeline::dot)
+      .def("running_time", [](Pipeline& p) { return now_ns() - p.base_time_ns(); },
+           "Pipeline running time (ns): the clock buffer PTS are compared against")
       .def("stop", [](Pipeline& p) {
         py::gil_scoped_release r;
         p.set_state(State::NULL_);

@@ -590,7 +590,9 @@ class VideoTestSrc : public BaseSrc {
       b->pts = produced_ * kSecond * info_.fps_d / info_.fps_n;
       b->duration = kSecond * info_.fps_d / info_.fps_n;
     } else {
-      b->pts = is_live_ ? running_time() : 0;
+      // no framerate: stamp the capture time (running time) so sinks can
+      // measure per-frame end-to-end latency
+      b->pts = running_time();
       b->duration = -1;
     }
     b->offset = produced_;

@@ -32,6 +32,15 @@ struct SharedModel {
 std::mutex g_shared_mu;
 std::map<std::string, std::shared_ptr<SharedModel>> g_shared;
 
+std::vector<int> field_ranks(const std::string& dims) {
+  std::vector<int> v;
+  for (auto& d : split_any(dims, ",.")) {
+    Dims tmp{};
+    v.push_back(static_cast<int>(parse_dimension(d, tmp)));
+  }
+  return v;
+}
+
 std::vector<int> parse_ranks(const std::string& s) {
   std::vector<int> v;
   for (auto& x : split(s, ','))
@@ -50,6 +59,8 @@ class TensorFilter : public BaseTransform {
     prop_string("input", &input_str_, "Input tensor dimension from inner array, up to 8 dimensions ?", [this] {
       unsigned n = props_.input_info.parse_dimensions(input_str_);
       props_.input_info.num_tensors = std::max(props_.input_info.num_tensors, n);
+      // the rank of each tensor is the number of fields written (tensor_filter_common.c:1490-1505)
+      if (inputranks_str_.empty()) props_.input_ranks = field_ranks(input_str_);
     });
     prop_string("inputtype", &inputtype_str_, "Type of each element of the input tensor ?", [this] {
       unsigned n = props_.input_info.parse_types(inputtype_str_);
@@ -61,6 +72,7 @@ class TensorFilter : public BaseTransform {
     prop_string("output", &output_str_, "Output tensor dimension from inner array, up to 8 dimensions ?", [this] {
       unsigned n = props_.output_info.parse_dimensions(output_str_);
       props_.output_info.num_tensors = std::max(props_.output_info.num_tensors, n);
+      if (outputranks_str_.empty()) props_.output_ranks = field_ranks(output_str_);
     });
     prop_string("outputtype", &outputtype_str_, "Type of each element of the output tensor ?", [this] {
       unsigned n = props_.output_info.parse_types(outputtype_str_);

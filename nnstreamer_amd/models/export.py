@@ -1,0 +1,98 @@
+"""Export random-init model families as TorchScript files for
+`tensor_filter framework=pytorch model=<file>.pt` (no checkpoints or
+datasets are available offline; weights are seeded random init).
+
+    python -m nnstreamer_amd.models.export mobilenet_v2 /tmp/mbv2.pt
+"""
+from __future__ import annotations
+
+import argparse
+import os
+
+import torch
+
+from .mobilenet_v2 import mobilenet_v2
+
+
+class NCHWWrapper(torch.nn.Module):
+    """Accepts the NNStreamer-ordered float tensor as the pytorch filter builds
+    it (dims reversed: [N, C, H, W] for `224:224:3:N`)."""
+
+    def __init__(self, model: torch.nn.Module):
+        super().__init__()
+        self.model = model
+
+    def forward(self, x):
+        return self.model(x)
+
+
+class NHWCWrapper(torch.nn.Module):
+    """Accepts `3:W:H:N` (NNStreamer video order == NHWC) float input."""
+
+    def __init__(self, model: torch.nn.Module):
+        super().__init__()
+        self.model = model
+
+    def forward(self, x):
+        return self.model(x.permute(0, 3, 1, 2))
+
+
+def build_model(name: str, seed: int = 0, layout: str = "nchw", num_classes: int = 1000):
+    name = name.lower().replace("-", "_")
+    if name in ("mobilenet_v2", "mbv2"):
+        m = mobilenet_v2(num_classes=num_classes, seed=seed)
+    elif name in ("mobilenet_v2_fused", "mbv2_fused"):
+        from .fused import FusedMobileNetV2
+
+        return FusedMobileNetV2.from_reference(mobilenet_v2(num_classes=num_classes, seed=seed)).eval()
+    elif name in ("ssd_mobilenet", "ssd"):
+        from .ssd import ssd_mobilenet
+
+        return ssd_mobilenet(seed=seed).eval()
+    elif name in ("deeplabv3", "deeplab"):
+        from .deeplab import deeplabv3
+
+        return deeplabv3(seed=seed).eval()
+    elif name in ("posenet", "pose"):
+        from .posenet import posenet
+
+        return posenet(seed=seed).eval()
+    else:
+        raise ValueError(f"unknown model {name}")
+    return (NHWCWrapper(m) if layout == "nhwc" else NCHWWrapper(m)).eval()
+
+
+def export(name: str, path: str, seed: int = 0, layout: str = "nchw", example_shape=None, trace: bool = False) -> str:
+    model = build_model(name, seed=seed, layout=layout)
+    with torch.no_grad():
+        if trace:
+            shape = example_shape or ((1, 3, 224, 224) if layout == "nchw" else (1, 224, 224, 3))
+            sm = torch.jit.trace(model, torch.zeros(shape))
+        else:
+            sm = torch.jit.script(model)
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    sm.save(path)
+    return path
+
+
+def write_labels(path: str, n: int = 1000) -> str:
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    with open(path, "w") as f:
+        for i in range(n):
+            f.write(f"class_{i}\n")
+    return path
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("model")
+    ap.add_argument("path")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--layout", default="nchw", choices=["nchw", "nhwc"])
+    ap.add_argument("--trace", action="store_true")
+    a = ap.parse_args()
+    print(export(a.model, a.path, a.seed, a.layout, trace=a.trace))
+
+
+if __name__ == "__main__":
+    main()
