@@ -41,8 +41,8 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("NNSX_BENCH_BATCH", "64")))
-    ap.add_argument("--model", default=os.environ.get("NNSX_BENCH_MODEL", "mobilenet_v2"),
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("NNSX_BENCH_BATCH", "128")))
+    ap.add_argument("--model", default=os.environ.get("NNSX_BENCH_MODEL", "mobilenet_v2_fused"),
                     help="mobilenet_v2 (plain torch) | mobilenet_v2_fused (nnsx CDNA4 kernels)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="CPU reference path (device=-1, torch CPU)")

@@ -1,0 +1,132 @@
+// torch.ops.nnsx.* -- the CDNA4 kernels exposed as PyTorch operators so that
+// TorchScript models (loaded by tensor_filter framework=pytorch) run them,
+// and hipGraph capture records them like any other kernel.  CPU
+// implementations are the fp32 numerics reference.
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <torch/library.h>
+
+#include "kernels/mbv2.h"
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+at::Tensor act_ref(at::Tensor v, int64_t act) {
+  if (act == 1) return v.clamp(0, 6);
+  if (act == 2) return v.clamp_min(0);
+  return v;
+}
+
+// ------------------------------------------------------------ pw_conv ----
+at::Tensor pw_conv_cuda(const at::Tensor& x, const at::Tensor& wt, const at::Tensor& bias,
+                        const c10::optional<at::Tensor>& res, int64_t N, int64_t act, bool out_f32) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "pw_conv: x must be contiguous bf16 cuda");
+  TORCH_CHECK(wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() && wt.dim() == 2, "pw_conv: wt [Npad,Kpad] bf16");
+  TORCH_CHECK(bias.scalar_type() == at::kFloat && bias.numel() >= N, "pw_conv: bias f32 [N]");
+  const int64_t K = x.size(-1);
+  const int64_t M = x.numel() / K;
+  const int64_t Kpad = wt.size(1);
+  TORCH_CHECK(K % 8 == 0 && N % 8 == 0 && Kpad % 32 == 0 && Kpad >= K && wt.size(0) >= ((N + 63) / 64) * 64,
+              "pw_conv: shape constraints (K%8, N%8, Kpad%32, wt rows padded to 64)");
+  auto sizes = x.sizes().vec();
+  sizes.back() = N;
+  at::Tensor y = at::empty(sizes, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  const void* r = nullptr;
+  if (res.has_value() && res->defined()) {
+    TORCH_CHECK(res->scalar_type() == at::kBFloat16 && res->is_contiguous() && res->numel() == M * N, "pw_conv: residual");
+    r = res->data_ptr();
+  }
+  nnsx::kernels::pw_gemm(x.data_ptr(), wt.data_ptr(), bias.data_ptr<float>(), r, y.data_ptr(), static_cast<int>(M),
+                         static_cast<int>(N), static_cast<int>(K), static_cast<int>(Kpad), static_cast<int>(act), out_f32,
+                         cur_stream());
+  return y;
+}
+
+at::Tensor pw_conv_cpu(const at::Tensor& x, const at::Tensor& wt, const at::Tensor& bias,
+                       const c10::optional<at::Tensor>& res, int64_t N, int64_t act, bool out_f32) {
+  const int64_t K = x.size(-1);
+  at::Tensor w = wt.slice(0, 0, N).slice(1, 0, K).to(at::kFloat);
+  at::Tensor v = at::matmul(x.to(at::kFloat), w.t()) + bias.slice(0, 0, N);
+  if (res.has_value() && res->defined()) v = v + res->to(at::kFloat);
+  v = act_ref(v, act);
+  return v.to(out_f32 ? at::kFloat : at::kBFloat16);
+}
+
+// ------------------------------------------------------------ dw_conv ----
+at::Tensor dw_conv_cuda(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int64_t stride, int64_t act) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() == 4, "dw_conv: x [B,H,W,C] bf16");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(C % 8 == 0 && w.numel() == 9 * C && w.scalar_type() == at::kBFloat16, "dw_conv: w [9,C] bf16, C%8==0");
+  const int64_t Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  at::Tensor y = at::empty({B, Ho, Wo, C}, x.options());
+  nnsx::kernels::dw3x3(x.data_ptr(), w.data_ptr(), bias.data_ptr<float>(), y.data_ptr(), static_cast<int>(B),
+                       static_cast<int>(H), static_cast<int>(W), static_cast<int>(C), static_cast<int>(stride),
+                       static_cast<int>(act), cur_stream());
+  return y;
+}
+
+at::Tensor dw_conv_cpu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int64_t stride, int64_t act) {
+  const int64_t C = x.size(3);
+  at::Tensor xf = x.to(at::kFloat).permute({0, 3, 1, 2});
+  at::Tensor wf = w.to(at::kFloat).view({3, 3, C}).permute({2, 0, 1}).unsqueeze(1).contiguous();
+  at::Tensor v = at::conv2d(xf, wf, bias, {stride, stride}, {1, 1}, {1, 1}, C);
+  return act_ref(v, act).permute({0, 2, 3, 1}).contiguous().to(at::kBFloat16);
+}
+
+// --------------------------------------------------------------- stem ----
+at::Tensor stem_conv_cuda(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int64_t act) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 4 && x.size(3) == 3,
+              "stem_conv: x [B,H,W,3] f32");
+  TORCH_CHECK(w.numel() == 27 * 32 && w.scalar_type() == at::kFloat, "stem_conv: w [3,3,3,32] f32");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2);
+  const int64_t Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  at::Tensor y = at::empty({B, Ho, Wo, 32}, x.options().dtype(at::kBFloat16));
+  nnsx::kernels::stem3x3(x.data_ptr<float>(), w.data_ptr<float>(), bias.data_ptr<float>(), y.data_ptr(),
+                         static_cast<int>(B), static_cast<int>(H), static_cast<int>(W), static_cast<int>(act), cur_stream());
+  return y;
+}
+
+at::Tensor stem_conv_cpu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int64_t act) {
+  at::Tensor xf = x.to(at::kFloat).permute({0, 3, 1, 2});
+  at::Tensor wf = w.view({3, 3, 3, 32}).permute({3, 2, 0, 1}).contiguous();
+  at::Tensor v = at::conv2d(xf, wf, bias, {2, 2}, {1, 1});
+  return act_ref(v, act).permute({0, 2, 3, 1}).contiguous().to(at::kBFloat16);
+}
+
+// ------------------------------------------------------------ avgpool ----
+at::Tensor avgpool_cuda(const at::Tensor& x) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() == 4, "avgpool: x [B,H,W,C] bf16");
+  const int64_t B = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  TORCH_CHECK(C % 8 == 0, "avgpool: C % 8");
+  at::Tensor y = at::empty({B, C}, x.options());
+  nnsx::kernels::avgpool(x.data_ptr(), y.data_ptr(), static_cast<int>(B), static_cast<int>(HW), static_cast<int>(C),
+                         cur_stream());
+  return y;
+}
+
+at::Tensor avgpool_cpu(const at::Tensor& x) { return x.to(at::kFloat).mean({1, 2}).to(at::kBFloat16); }
+
+}  // namespace
+
+TORCH_LIBRARY(nnsx, m) {
+  m.def("pw_conv(Tensor x, Tensor wt, Tensor bias, Tensor? res, int N, int act, bool out_f32) -> Tensor");
+  m.def("dw_conv(Tensor x, Tensor w, Tensor bias, int stride, int act) -> Tensor");
+  m.def("stem_conv(Tensor x, Tensor w, Tensor bias, int act) -> Tensor");
+  m.def("avgpool(Tensor x) -> Tensor");
+}
+
+TORCH_LIBRARY_IMPL(nnsx, CUDA, m) {
+  m.impl("pw_conv", pw_conv_cuda);
+  m.impl("dw_conv", dw_conv_cuda);
+  m.impl("stem_conv", stem_conv_cuda);
+  m.impl("avgpool", avgpool_cuda);
+}
+
+TORCH_LIBRARY_IMPL(nnsx, CPU, m) {
+  m.impl("pw_conv", pw_conv_cpu);
+  m.impl("dw_conv", dw_conv_cpu);
+  m.impl("stem_conv", stem_conv_cpu);
+  m.impl("avgpool", avgpool_cpu);
+}

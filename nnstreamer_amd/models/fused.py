@@ -1,0 +1,129 @@
+"""FusedMobileNetV2: the inference form of MobileNetV2 that runs on the
+hand-written CDNA4 kernels (csrc/kernels/mbv2.hip) through torch.ops.nnsx.*.
+
+* BatchNorm folded into conv weight + bias (fp32 fold, then bf16 weights).
+* NHWC bf16 activations end to end; the input is the NNStreamer video tensor
+  `3:224:224:B` (NHWC float32 after tensor_transform) -- no transpose needed.
+* 1x1 convs (expand / project / head / classifier) are MFMA GEMMs with
+  bias + ReLU6 + residual fused in the epilogue; depthwise 3x3 and the stem are
+  bandwidth kernels; global average pool is its own small kernel.
+
+The module is TorchScript-scriptable so `tensor_filter framework=pytorch` can
+load it from a .pt file (the ops resolve because the filter lives in the same
+native library that registers them).
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+
+from .mobilenet_v2 import ConvBNReLU, InvertedResidual, MobileNetV2
+
+
+def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d):
+    w = conv.weight.detach().double()
+    scale = bn.weight.detach().double() / torch.sqrt(bn.running_var.detach().double() + bn.eps)
+    w = w * scale.view(-1, 1, 1, 1)
+    b = bn.bias.detach().double() - bn.running_mean.detach().double() * scale
+    return w.float(), b.float()
+
+
+def _pw_weight(w: torch.Tensor):
+    """[N, K, 1, 1] fp32 -> zero-padded [ceil64(N), ceil32(K)] bf16 (K contiguous)."""
+    n, k = w.shape[0], w.shape[1]
+    npad = (n + 63) // 64 * 64
+    kpad = (k + 31) // 32 * 32
+    out = torch.zeros(npad, kpad, dtype=torch.float32)
+    out[:n, :k] = w.reshape(n, k)
+    return out.to(torch.bfloat16)
+
+
+class PW(nn.Module):
+    def __init__(self, w: torch.Tensor, b: torch.Tensor, act: int, out_f32: bool = False):
+        super().__init__()
+        self.register_buffer("wt", _pw_weight(w))
+        bias = torch.zeros(self.wt.shape[0], dtype=torch.float32)
+        bias[: b.numel()] = b
+        self.register_buffer("bias", bias)
+        self.n = int(w.shape[0])
+        self.act = int(act)
+        self.out_f32 = bool(out_f32)
+
+    def forward(self, x: torch.Tensor, res: Optional[torch.Tensor] = None) -> torch.Tensor:
+        return torch.ops.nnsx.pw_conv(x, self.wt, self.bias, res, self.n, self.act, self.out_f32)
+
+
+class DW(nn.Module):
+    def __init__(self, w: torch.Tensor, b: torch.Tensor, stride: int):
+        super().__init__()
+        c = w.shape[0]
+        self.register_buffer("w", w.reshape(c, 9).t().contiguous().to(torch.bfloat16))  # [9, C]
+        self.register_buffer("bias", b.contiguous())
+        self.stride = int(stride)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return torch.ops.nnsx.dw_conv(x, self.w, self.bias, self.stride, 1)
+
+
+class Block(nn.Module):
+    def __init__(self, ir: InvertedResidual):
+        super().__init__()
+        layers = list(ir.conv)
+        self.has_expand = ir.expand != 1
+        idx = 0
+        if self.has_expand:
+            e: ConvBNReLU = layers[0]
+            self.expand = PW(*_fold(e[0], e[1]), act=1)
+            idx = 1
+        else:
+            self.expand = PW(torch.zeros(8, 8, 1, 1), torch.zeros(8), act=0)  # unused placeholder
+        d: ConvBNReLU = layers[idx]
+        self.dw = DW(*_fold(d[0], d[1]), stride=ir.stride)
+        p: ConvBNReLU = layers[idx + 1]
+        self.project = PW(*_fold(p[0], p[1]), act=0)
+        self.use_res = bool(ir.use_res)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        h = self.expand(x) if self.has_expand else x
+        h = self.dw(h)
+        if self.use_res:
+            return self.project(h, x)
+        return self.project(h)
+
+
+class FusedMobileNetV2(nn.Module):
+    """Input: [B, H, W, 3] float32 NHWC (NNStreamer `3:W:H:B`).  Output: [B, classes] fp32 logits."""
+
+    def __init__(self):
+        super().__init__()
+
+    @classmethod
+    def from_reference(cls, m: MobileNetV2) -> "FusedMobileNetV2":
+        self = cls()
+        m = m.eval()
+        stem: ConvBNReLU = m.features[0]
+        w, b = _fold(stem[0], stem[1])  # [32, 3, 3, 3]
+        self.register_buffer("stem_w", w.permute(2, 3, 1, 0).contiguous())  # [ky, kx, ci, co]
+        self.register_buffer("stem_b", b.contiguous())
+        self.blocks = nn.ModuleList([Block(ir) for ir in m.features[1:-1]])
+        head: ConvBNReLU = m.features[-1]
+        self.head = PW(*_fold(head[0], head[1]), act=1)
+        fc: nn.Linear = m.classifier[1]
+        self.fc = PW(fc.weight.detach().float()[:, :, None, None], fc.bias.detach().float(), act=0, out_f32=True)
+        return self
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        h = torch.ops.nnsx.stem_conv(x.contiguous(), self.stem_w, self.stem_b, 1)
+        for blk in self.blocks:
+            h = blk(h)
+        h = self.head(h)
+        h = torch.ops.nnsx.avgpool(h)
+        return self.fc(h)
+
+
+def fused_mobilenet_v2(seed: int = 0) -> FusedMobileNetV2:
+    from .mobilenet_v2 import mobilenet_v2
+
+    return FusedMobileNetV2.from_reference(mobilenet_v2(seed=seed)).eval()
