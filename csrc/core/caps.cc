@@ -658,6 +658,10 @@ struct CapsParser {
       if (!eat('=')) fail("expected '=' after " + field);
       Value v = value("");
       if (field == "framerate" && v.kind == Value::Kind::INT) v = Value::Fraction(v.i, 1);
+      // tensor dimension / type strings that happen to look numeric ("dimensions=10")
+      if ((field == "dimension" || field == "dimensions" || field == "type" || field == "types") &&
+          (v.kind == Value::Kind::INT || v.kind == Value::Kind::DOUBLE))
+        v = Value::String(v.kind == Value::Kind::INT ? std::to_string(v.i) : strip(v.to_string(false)));
       st.set(field, v);
     }
     return st;
@@ -754,8 +758,14 @@ MediaType structure_media_type(const Structure& s) {
   return MediaType::ANY;
 }
 
-bool config_from_structure(const Structure& st, TensorsConfig* config) {
+bool config_from_structure(const Structure& st_in, TensorsConfig* config) {
   *config = TensorsConfig();
+  // `dimensions=10` parses as an int in untyped caps strings: read it as text
+  Structure st = st_in;
+  for (const char* f : {"dimension", "dimensions", "types", "type"}) {
+    const Value* v = st.get(f);
+    if (v && v->kind == Value::Kind::INT) st.set(f, Value::String(std::to_string(v->i)));
+  }
   const std::string& name = st.name();
   if (name == kMimeTensor) {
     config->info.resize(1);

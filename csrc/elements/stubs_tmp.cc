@@ -3,7 +3,6 @@
 #include "elements/elements.h"
 
 namespace nnsx {
-void register_tensor_stream_elements() {}
 void register_extra_elements() {}
 void register_comm_elements() {}
 void register_bbox_decoder() {}

@@ -250,7 +250,8 @@ Pad* Element::get_compatible_pad(PadDirection dir, const std::string& hint) {
   if (!hint.empty()) {
     if (Pad* p = get_pad(hint)) return (p->direction() == dir && !p->is_linked()) ? p : nullptr;
     if (const PadTemplate* t = find_template(hint, dir)) {
-      if (t->presence == PadPresence::REQUEST) return request_pad(*t, hint.find('%') == std::string::npos ? hint : "");
+      // request pads, and sometimes-pads named explicitly in a link (delayed linking)
+      if (t->presence != PadPresence::ALWAYS) return request_pad(*t, hint.find('%') == std::string::npos ? hint : "");
     }
     return nullptr;
   }
