@@ -24,6 +24,16 @@ int frac_cmp(int64_t an, int64_t ad, int64_t bn, int64_t bd) {
 }
 
 bool is_tensor_dim_field(const std::string& f) { return f == "dimension" || f == "dimensions"; }
+bool is_tensor_type_field(const std::string& f) { return f == "type" || f == "types"; }
+
+// "float32.int32" and "float32,int32" name the same type list
+bool type_string_equal(const std::string& a, const std::string& b) {
+  auto pa = split_any(a, ",."), pb = split_any(b, ",.");
+  if (pa.size() != pb.size()) return false;
+  for (size_t i = 0; i < pa.size(); ++i)
+    if (lower(strip(pa[i])) != lower(strip(pb[i]))) return false;
+  return true;
+}
 
 bool needs_quotes(const std::string& s) {
   if (s.empty()) return true;
@@ -192,6 +202,8 @@ bool Value::intersect(const Value& a, const Value& b, Value* out, const std::str
       if (b.kind != Kind::STRING) return false;
       if (is_tensor_dim_field(field)) {
         if (!dimension_string_equal(a.s, b.s)) return false;
+      } else if (is_tensor_type_field(field)) {
+        if (!type_string_equal(a.s, b.s)) return false;
       } else if (a.s != b.s) {
         return false;
       }

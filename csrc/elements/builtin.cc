@@ -33,6 +33,7 @@ void ensure_builtin_elements() {
     register_comm_elements();
     register_host_frameworks();
     register_torch_frameworks();
+    register_torch_trainer();
     register_simple_decoders();
     register_bbox_decoder();
     register_segment_decoder();

@@ -3,7 +3,6 @@
 #include "elements/elements.h"
 
 namespace nnsx {
-void register_extra_elements() {}
 void register_comm_elements() {}
 void register_bbox_decoder() {}
 void register_segment_decoder() {}

@@ -27,5 +27,6 @@ bool unregister_cpp_filter(const std::string& name);
 
 void register_host_frameworks();   // custom, custom-easy, cpp
 void register_torch_frameworks();  // pytorch (libtorch, ROCm) -- torch TU
+void register_torch_trainer();     // tensor_trainer framework=pytorch -- torch TU
 
 }  // namespace nnsx

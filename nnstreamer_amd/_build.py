@@ -24,7 +24,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("NNSX_CXX", "/opt/rocm/lib/llvm/bin/clang++")
 
 # sources that include libtorch headers (slow to compile)
-TORCH_SOURCES = {"filter/pytorch.cc", "ops/torch_ops.cc"}
+TORCH_SOURCES = {"filter/pytorch.cc", "filter/torch_trainer.cc", "ops/torch_ops.cc"}
 # pybind11 sources
 PY_SOURCES = {"bindings/module.cc", "bindings/python_bridge.cc"}
 
