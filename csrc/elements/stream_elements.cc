@@ -30,6 +30,10 @@ struct PadState {
   BufferPtr last;  // GstTensorCollectPadData::buffer
 };
 
+// GstClockTime semantics: an unset timestamp (GST_CLOCK_TIME_NONE) compares as
+// the largest time, so untimestamped streams (multifilesrc) still pair up.
+inline int64_t sync_ts(const BufferPtr& b) { return b->pts < 0 ? INT64_MAX : b->pts; }
+
 class TimeSync {
  public:
   int mode = SYNC_SLOWEST;
@@ -63,14 +67,14 @@ class TimeSync {
           case SYNC_NOSYNC:
           case SYNC_SLOWEST:
           case SYNC_REFRESH:
-            if (*current < b->pts) upd = true;
+            if (*current < sync_ts(b)) upd = true;
             break;
           case SYNC_BASEPAD:
             if (count == basepad_id) upd = true;
             break;
         }
         if (upd) {
-          *current = b->pts;
+          *current = sync_ts(b);
           meta_out->copy_metadata_from(*b);
         }
       } else {
@@ -85,13 +89,13 @@ class TimeSync {
   bool buffer_update(CollectPads& cp, CollectPads::PadData* d, int64_t current, int64_t base) {
     BufferPtr b = cp.peek(d);
     if (!b) return true;
-    if (b->pts < current) {
+    if (sync_ts(b) < current) {
       d->last = cp.pop(d);
       return false;
     }
     auto absdiff = [](int64_t a, int64_t c) { return a > c ? a - c : c - a; };
-    bool keep = (mode == SYNC_SLOWEST && d->last && absdiff(current, d->last->pts) < absdiff(current, b->pts)) ||
-                (mode == SYNC_BASEPAD && d->last && absdiff(current, b->pts) > base);
+    bool keep = (mode == SYNC_SLOWEST && d->last && absdiff(current, sync_ts(d->last)) < absdiff(current, sync_ts(b))) ||
+                (mode == SYNC_BASEPAD && d->last && absdiff(current, sync_ts(b)) > base);
     if (!keep) d->last = cp.pop(d);
     return true;
   }

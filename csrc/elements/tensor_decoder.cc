@@ -160,6 +160,25 @@ class TensorDecoder : public BaseTransform {
     }
     if (ctx.device >= 0)
       for (auto& m : mems) m->record_use(ctx.stream, ctx.device);
+    if (ctx.out_frames > 1 && out->n_memory() == ctx.out_frames) {
+      // batched input: one output buffer per frame, timestamps spread over the batch duration
+      const unsigned n = ctx.out_frames;
+      const int64_t step = in->duration > 0 ? in->duration / n : 0;
+      for (unsigned f = 0; f < n; ++f) {
+        auto fb = make_buffer();
+        fb->copy_metadata_from(*out);
+        fb->mems.push_back(out->mems[f]);
+        if (in->pts >= 0) fb->pts = in->pts + step * f;
+        if (step > 0) fb->duration = step;
+        if (f + 1 == n) {
+          *outbuf = fb;
+          break;
+        }
+        FlowReturn r = src_pad()->push(fb);
+        if (!flow_ok(r)) return r;
+      }
+      return FlowReturn::OK;
+    }
     *outbuf = out;
     return FlowReturn::OK;
   }

@@ -52,6 +52,9 @@ struct InvokeContext {
   hipStream_t stream = nullptr;
   // set by the framework when outputs' shapes change (flexible / invoke-dynamic)
   TensorsInfo* out_info = nullptr;
+  // decoders: >1 when out->mems holds one memory per frame of a batched input;
+  // tensor_decoder then pushes them as consecutive buffers
+  unsigned out_frames = 1;
 };
 
 class FilterInstance {

@@ -1,0 +1,153 @@
+"""Decoder sub-plugins against the reference's own golden fixtures
+(tests/nnstreamer_decoder_boundingbox, _image_segment, _pose).  Fixture files
+are read in place from /root/reference (raw float tensors / text); tests skip
+when the reference tree is not mounted.  The muxes run sync-mode=nosync: the
+reference pairs the file frames through GStreamer preroll timestamps (pts 0
+before PLAYING), which a running-time stamped stream does not reproduce.  Labels are rendered with nnsx's own
+glyphs, so comparisons mask the label cells (computed by rendering the same
+frame with option9=solid) and compare every other pixel exactly."""
+import os
+
+import numpy as np
+import pytest
+
+REF = "/root/reference/tests"
+BB = f"{REF}/nnstreamer_decoder_boundingbox"
+
+needs_ref = pytest.mark.skipif(not os.path.isdir(BB), reason="reference fixtures not mounted")
+
+
+def _run_frames(nns, desc, n):
+    p = nns.parse_launch(desc)
+    out = []
+    p.get_by_name("sink").connect("new-data", lambda b: out.append(b.memory(0).bytes()))
+    msg = p.run(timeout=60)
+    p.stop()
+    assert len(out) == n, (msg, p.messages())
+    return out
+
+
+def _rgba_to_red_mask(buf, w, h):
+    a = np.frombuffer(buf, np.uint8).reshape(h, w, 4)
+    return (a[..., 0] == 255) & (a[..., 1] == 0) & (a[..., 2] == 0)
+
+
+def _bgrx_red_mask(path, w, h):
+    a = np.fromfile(path, np.uint8).reshape(h, w, 4)
+    return (a[..., 2] == 255) & (a[..., 1] == 0) & (a[..., 0] == 0)
+
+
+def _compare_with_golden(mine, solid, golden_paths, w, h):
+    for m, s, g in zip(mine, solid, golden_paths):
+        mm = _rgba_to_red_mask(m, w, h)
+        gm = _bgrx_red_mask(g, w, h)
+        cells = _label_cells(s, m, w, h)
+        assert np.array_equal(mm & ~cells, gm & ~cells), f"{g}: {np.argwhere((mm ^ gm) & ~cells)[:10]}"
+        assert mm.any() and gm.any()
+
+
+def _label_cells(solid, mine, w, h):
+    """Pixels that belong to label cells: red in the solid rendering but whose value
+    comes from a label sprite (differs between font and solid rendering, or is red
+    in solid and black in font)."""
+    s = np.frombuffer(solid, np.uint8).reshape(h, w, 4)
+    m = np.frombuffer(mine, np.uint8).reshape(h, w, 4)
+    differ = np.any(s != m, axis=-1)
+    # grow each differing pixel to its full 8x13 cell neighbourhood (cells are axis-aligned blocks)
+    cells = np.zeros((h, w), bool)
+    ys, xs = np.nonzero(differ)
+    for y, x in zip(ys, xs):
+        cells[max(0, y - 13):y + 14, max(0, x - 8):x + 9] = True
+    return cells
+
+
+def _ssd_desc(mode, style):
+    return (f"tensor_mux name=mux sync-mode=nosync ! tensor_decoder mode=bounding_boxes option1={mode} "
+            f"option2={BB}/coco_labels_list.txt option3={BB}/box_priors.txt option4=160:120 option5=300:300 "
+            f"option9={style} ! tensor_sink name=sink "
+            f"multifilesrc location={BB}/mobilenetssd_tensors.0.%d start-index=0 stop-index=1 "
+            "caps=application/octet-stream ! tensor_converter input-dim=4:1:1917:1 input-type=float32 ! mux.sink_0 "
+            f"multifilesrc location={BB}/mobilenetssd_tensors.1.%d start-index=0 stop-index=1 "
+            "caps=application/octet-stream ! tensor_converter input-dim=91:1917:1 input-type=float32 ! mux.sink_1")
+
+
+@needs_ref
+@pytest.mark.parametrize("mode", ["mobilenet-ssd", "tflite-ssd"])
+def test_bbox_mobilenet_ssd_golden(nns, mode):
+    mine = _run_frames(nns, _ssd_desc(mode, "font"), 2)
+    solid = _run_frames(nns, _ssd_desc(mode, "solid"), 2)
+    _compare_with_golden(mine, solid, [f"{BB}/mobilenetssd_golden.{i}" for i in range(2)], 160, 120)
+
+
+def _pp_desc(mode, style):
+    src = ""
+    dims = ["1", "100:1", "100:1", "4:100:1"]
+    for i, d in enumerate(dims):
+        src += (f" multifilesrc location={BB}/mobilenetssd_postprocess_tensors.{i}.%d start-index=0 stop-index=1 "
+                f"caps=application/octet-stream ! tensor_converter input-dim={d} input-type=float32 ! mux.sink_{i}")
+    return (f"tensor_mux name=mux sync-mode=nosync ! tensor_decoder mode=bounding_boxes option1={mode} "
+            f"option2={BB}/coco_labels_list.txt option4=160:120 option5=640:480 option9={style} "
+            "! tensor_sink name=sink" + src)
+
+
+@needs_ref
+@pytest.mark.parametrize("mode", ["mobilenet-ssd-postprocess", "tf-ssd"])
+def test_bbox_ssd_postprocess_golden(nns, mode):
+    mine = _run_frames(nns, _pp_desc(mode, "font"), 2)
+    solid = _run_frames(nns, _pp_desc(mode, "solid"), 2)
+    _compare_with_golden(mine, solid, [f"{BB}/mobilenetssd_postprocess_golden.{i}" for i in range(2)], 160, 120)
+
+
+@needs_ref
+def test_bbox_palm_detection_golden(nns):
+    desc = ("tensor_mux name=mux sync-mode=nosync ! tensor_decoder mode=bounding_boxes option1=mp-palm-detection "
+            "option3=0.5:4:1.0:1.0:0.5:0.5:8:16:16:16 option4=160:120 option5=300:300 ! tensor_sink name=sink "
+            f"multifilesrc location={BB}/palm_detection_input_0.%d start-index=0 stop-index=1 "
+            "caps=application/octet-stream ! tensor_converter input-dim=18:2016:1:1 input-type=float32 ! mux.sink_0 "
+            f"multifilesrc location={BB}/palm_detection_input_1.%d start-index=0 stop-index=1 "
+            "caps=application/octet-stream ! tensor_converter input-dim=1:2016:1:1 input-type=float32 ! mux.sink_1")
+    mine = _run_frames(nns, desc, 2)
+    for i, m in enumerate(mine):
+        g = np.fromfile(f"{BB}/palm_detection_result_golden.{i}", np.uint8)
+        # golden is RGBA after videoconvert: identical bytes expected (no labels in palm mode)
+        assert np.array_equal(np.frombuffer(m, np.uint8), g)
+
+
+def test_bbox_yolov5_synthetic(nns, workdir):
+    labels = f"{workdir}/yolo_labels.txt"
+    with open(labels, "w") as f:
+        f.write("\n".join(f"c{i}" for i in range(3)) + "\n")
+    iw = ih = 64
+    n = ((iw // 32) * (ih // 32) + (iw // 16) * (ih // 16) + (iw // 8) * (ih // 8)) * 3
+    x = np.zeros((n, 8), np.float32)
+    # two overlapping boxes (one suppressed) and one separate box
+    x[0] = [0.5, 0.5, 0.25, 0.25, 0.9, 0.1, 0.9, 0.1]
+    x[1] = [0.52, 0.5, 0.25, 0.25, 0.8, 0.1, 0.9, 0.1]
+    x[2] = [0.2, 0.2, 0.1, 0.1, 0.9, 0.9, 0.1, 0.1]
+    caps = f"other/tensors,format=static,num_tensors=1,dimensions=8:{n}:1,types=float32,framerate=0/1"
+    p = nns.parse_launch(f"appsrc name=src caps={caps} ! tensor_decoder mode=bounding_boxes option1=yolov5 "
+                         f"option2={labels} option4=64:64 option5=64:64 option9=none ! tensor_sink name=sink")
+    out = []
+    p.get_by_name("sink").connect("new-data", lambda b: out.append(b.memory(0).bytes()))
+    p.set_state("playing")
+    p.get_by_name("src").push_buffer(x.ravel(), pts=0)
+    p.get_by_name("src").end_of_stream()
+    p.wait(20)
+    p.stop()
+    mask = _rgba_to_red_mask(out[0], 64, 64)
+    # box 0: x = 32 - 8 = 24, w = 16 -> columns 24..40 on rows 24 and 40
+    assert mask[24, 24:41].all() and mask[40, 24:41].all()
+    # box 1 (shifted by ~1 px) is suppressed: its right edge column 41 has no vertical line
+    assert not mask[30, 41]
+    # box 2: x = 12.8 - 3.2 = 9 -> (9, 9) .. (15, 15)
+    assert mask[9, 9:16].all()
+
+
+def test_bbox_batched_equals_per_frame(nns, workdir):
+    from test_gpu_elements import _bbox_run, _ssd_fixture
+    pri, lab, boxes, logits = _ssd_fixture(workdir, batch=3, seed=3)
+    batched = _bbox_run(nns, pri, lab, boxes, logits, -1, 3)
+    assert len(batched) == 3
+    for i in range(3):
+        single = _bbox_run(nns, pri, lab, boxes[i:i + 1], logits[i:i + 1], -1, 1)
+        assert single[0][1] == batched[i][1]

@@ -1,0 +1,131 @@
+"""Device-resident paths of the stream / extra elements on the MI355X:
+each compares the HBM path against the host path of the same pipeline."""
+import numpy as np
+import pytest
+
+from conftest import run_pipeline
+from test_extra_elements import _trainer_setup
+
+pytestmark = pytest.mark.gpu
+
+RGB = "video/x-raw,format=RGB,width=40,height=30,framerate=30/1"
+
+
+def _both(nns, desc, collect):
+    cpu = run_pipeline(nns, desc.format(dev=-1), collect=collect)
+    gpu = run_pipeline(nns, desc.format(dev=0), collect=collect)
+    return cpu, gpu
+
+
+def test_merge_and_aggregator_device(nns):
+    desc = (f"videotestsrc num-buffers=4 pattern=snow ! {RGB} ! tensor_converter device={{dev}} ! m.sink_0 "
+            f"videotestsrc num-buffers=4 pattern=gradient ! {RGB} ! tensor_converter device={{dev}} ! m.sink_1 "
+            "tensor_merge name=m mode=linear option=1 ! tensor_aggregator frames-out=2 frames-dim=3 "
+            "! tensor_sink name=sink")
+    collect = lambda b: (b.memory(0).on_device, b.memory(0).numpy().copy())
+    cpu, gpu = _both(nns, desc, collect)
+    assert len(cpu) == len(gpu) == 2
+    assert all(d for d, _ in gpu)
+    for (_, a), (_, b) in zip(cpu, gpu):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_crop_device(nns):
+    raw = np.random.default_rng(1).integers(0, 255, 3 * 40 * 30, dtype=np.uint8)
+    regions = np.array([2, 3, 10, 7, 30, 20, 20, 20], np.uint32)
+    info = np.frombuffer(nns.meta_header(1, [4, 2], format=1) + regions.tobytes(), np.uint8)
+    res = {}
+    for dev in (-1, 0):
+        p = nns.parse_launch(
+            "appsrc name=r caps=other/tensors,format=static,num_tensors=1,dimensions=3:40:30:1,types=uint8,"
+            f"framerate=0/1 ! tensor_transform mode=typecast option=uint8 device={dev} ! c.raw "
+            "appsrc name=i caps=other/tensors,format=flexible,framerate=0/1 ! c.info "
+            "tensor_crop name=c ! tensor_sink name=sink")
+        out = []
+        p.get_by_name("sink").connect("new-data", lambda b: out.append(
+            [(b.memory(k).on_device, b.memory(k).bytes()) for k in range(b.n_memory)]))
+        p.set_state("playing")
+        p.get_by_name("r").push_buffer(raw, pts=0)
+        p.get_by_name("i").push_buffer(info, pts=0)
+        p.get_by_name("r").end_of_stream()
+        p.get_by_name("i").end_of_stream()
+        p.wait(30)
+        p.stop()
+        res[dev] = out[0]
+    assert all(d for d, _ in res[0])
+    img = raw.reshape(30, 40, 3)
+    for (_, c), (_, g), (x, y, w, h) in zip(res[-1], res[0], [(2, 3, 10, 7), (30, 20, 10, 10)]):
+        assert c[-w * h * 3:] == img[y:y + h, x:x + w].tobytes()
+        assert g[-w * h * 3:] == c[-w * h * 3:]
+
+
+def test_trainer_on_gpu(nns, workdir):
+    classes, feat, ntrain, nval, epochs = 4, 16, 128, 32, 3
+    cfg, centers, rng = _trainer_setup(workdir, classes, feat)
+    caps = f"other/tensors,format=static,num_tensors=2,dimensions={feat}:1.1:1,types=float32.int32,framerate=0/1"
+    p = nns.parse_launch(
+        f"appsrc name=src caps={caps} ! tensor_trainer name=tr model-config={cfg} num-inputs=1 num-labels=1 "
+        f"num-training-samples={ntrain} num-validation-samples={nval} epochs={epochs} device=0 "
+        "! tensor_sink name=sink")
+    stats = []
+    p.get_by_name("sink").connect("new-data", lambda b: stats.append(b.memory(0).numpy("float64").copy()))
+    p.set_state("playing")
+    for _ in range(epochs * (ntrain + nval)):
+        c = int(rng.integers(classes))
+        x = centers[c] + rng.normal(size=feat).astype(np.float32)
+        p.get_by_name("src").push_buffer([x.astype(np.float32), np.array([c], np.int32)], pts=0)
+    p.get_by_name("src").end_of_stream()
+    msg = p.wait(120)
+    p.stop()
+    assert msg and msg[0] == "eos", p.messages()
+    assert len(stats) == 1 + epochs
+    assert stats[-1][3] >= 0.9
+
+
+def _ssd_fixture(workdir, n=1917, c=91, batch=1, seed=0):
+    rng = np.random.default_rng(seed)
+    pri = f"{workdir}/priors_{n}.txt"
+    yc, xc = rng.uniform(0, 1, n), rng.uniform(0, 1, n)
+    h, w = rng.uniform(0.05, 0.4, n), rng.uniform(0.05, 0.4, n)
+    with open(pri, "w") as f:
+        for row in (yc, xc, h, w):
+            f.write(" ".join(f"{v:.6f}" for v in row) + "\n")
+    lab = f"{workdir}/ssd_labels.txt"
+    with open(lab, "w") as f:
+        f.write("\n".join(f"label{i}" for i in range(c)) + "\n")
+    boxes = rng.normal(0, 1, (batch, n, 4)).astype(np.float32)
+    logits = rng.normal(-4, 2, (batch, n, c)).astype(np.float32)
+    return pri, lab, boxes, logits
+
+
+def _bbox_run(nns, pri, lab, boxes, logits, dev, batch):
+    n, c = boxes.shape[1], logits.shape[2]
+    caps = (f"other/tensors,format=static,num_tensors=2,dimensions=4:1:{n}:{batch}.{c}:{n}:{batch},"
+            "types=float32.float32,framerate=0/1")
+    p = nns.parse_launch(
+        f"appsrc name=src caps={caps} ! tensor_transform mode=typecast option=float32 device={dev} "
+        f"! tensor_decoder mode=bounding_boxes option1=mobilenet-ssd option2={lab} option3={pri} "
+        "option4=320:240 option5=300:300 ! tensor_sink name=sink")
+    out = []
+    p.get_by_name("sink").connect("new-data", lambda b: out.append((b.memory(0).on_device, b.memory(0).bytes())))
+    p.set_state("playing")
+    p.get_by_name("src").push_buffer([boxes.ravel(), logits.ravel()], pts=0, duration=4 * 33000000)
+    p.get_by_name("src").end_of_stream()
+    msg = p.wait(60)
+    p.stop()
+    assert msg and msg[0] == "eos", p.messages()
+    return out
+
+
+def test_bbox_ssd_device_matches_host(nns, workdir):
+    pri, lab, boxes, logits = _ssd_fixture(workdir, batch=4)
+    host = _bbox_run(nns, pri, lab, boxes, logits, -1, 4)
+    dev = _bbox_run(nns, pri, lab, boxes, logits, 0, 4)
+    assert len(host) == len(dev) == 4
+    assert all(d for d, _ in dev)
+    for (_, h), (_, d) in zip(host, dev):
+        a = np.frombuffer(h, np.uint32)
+        b = np.frombuffer(d, np.uint32)
+        assert (a != 0).sum() > 100
+        # float rounding (expf / contraction) may move an edge by one pixel on rare anchors
+        assert (a == b).mean() > 0.995, (a != b).sum()
