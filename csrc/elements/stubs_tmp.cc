@@ -4,7 +4,5 @@
 
 namespace nnsx {
 void register_comm_elements() {}
-void register_segment_decoder() {}
-void register_pose_decoder() {}
 void register_serial_decoders() {}
 }  // namespace nnsx

@@ -1,0 +1,27 @@
+// Segmentation / pose post-processing kernels (kernels/vision.hip), used by
+// the image_segment and pose_estimation decoders.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+
+namespace nnsx {
+namespace kernels {
+
+// tflite-deeplab: prob [pixels][labels] -> RGBA; label = argmax (first max),
+// background when max <= threshold; colour = rgb_modifier * label | alpha.
+void segment_argmax_color(const float* prob, int labels, uint64_t pixels, uint32_t rgb_modifier, float threshold,
+                          uint32_t* out, hipStream_t s);
+// snpe-deeplab: label index map (float) -> RGBA
+void segment_index_color(const float* index_map, uint64_t pixels, int max_labels, uint32_t rgb_modifier,
+                         uint32_t* out, hipStream_t s);
+// snpe-depth: grayscale normalised by the per-frame maximum; ws holds `batch` uint32
+void segment_depth_gray(const float* in, uint64_t pixels_per_frame, int batch, uint32_t* ws, uint32_t* out,
+                        hipStream_t s);
+// pose: heat [B][gh][gw][K] -> out [B][K][3] = (grid x, grid y, score)
+void pose_heatmap_argmax(const float* heat, int keypoints, int grid_w, int grid_h, int batch, bool sigmoid,
+                         float* out, hipStream_t s);
+
+}  // namespace kernels
+}  // namespace nnsx

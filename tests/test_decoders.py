@@ -151,3 +151,104 @@ def test_bbox_batched_equals_per_frame(nns, workdir):
     for i in range(3):
         single = _bbox_run(nns, pri, lab, boxes[i:i + 1], logits[i:i + 1], -1, 1)
         assert single[0][1] == batched[i][1]
+
+
+# ------------------------------------------------------------ image_segment ----
+
+def _seg_run(nns, mode, arr, dims, dev=-1, extra=""):
+    caps = f"other/tensors,format=static,num_tensors=1,dimensions={dims},types=float32,framerate=0/1"
+    p = nns.parse_launch(f"appsrc name=src caps={caps} ! tensor_transform mode=typecast option=float32 device={dev} "
+                         f"! tensor_decoder mode=image_segment option1={mode} {extra} ! tensor_sink name=sink")
+    out = []
+    p.get_by_name("sink").connect("new-data", lambda b: out.append(np.frombuffer(b.memory(0).bytes(), np.uint32).copy()))
+    p.set_state("playing")
+    p.get_by_name("src").push_buffer(arr.ravel(), pts=0, duration=100)
+    p.get_by_name("src").end_of_stream()
+    msg = p.wait(30)
+    caps_out = p.get_by_name("sink").pad_caps("sink")
+    p.stop()
+    assert msg and msg[0] == "eos", p.messages()
+    return out, caps_out
+
+
+def _seg_color(label, max_labels=20):
+    mod = 0xFFFFFF // (max_labels + 1)
+    return 0 if label == 0 else ((mod * label) & 0xFFFFFF) | 0xFF000000
+
+
+def test_image_segment_tflite_deeplab(nns):
+    rng = np.random.default_rng(0)
+    h, w, L = 7, 9, 21
+    prob = rng.uniform(0, 0.4, (h, w, L)).astype(np.float32)
+    lab = rng.integers(0, L, (h, w))
+    for y in range(h):
+        for x in range(w):
+            if (x + y) % 3:
+                prob[y, x, lab[y, x]] = 0.9   # confident pixel
+    out, caps = _seg_run(nns, "tflite-deeplab", prob, f"{L}:{w}:{h}:1")
+    assert caps.get("width") == w and caps.get("height") == h
+    exp = np.array([_seg_color(int(lab[y, x])) if (x + y) % 3 else 0 for y in range(h) for x in range(w)], np.uint32)
+    np.testing.assert_array_equal(out[0], exp)
+
+
+def test_image_segment_snpe_modes(nns):
+    idx = np.array([[0, 1, 2], [20, 21, -1]], np.float32)
+    out, caps = _seg_run(nns, "snpe-deeplab", idx, "3:2:1")
+    np.testing.assert_array_equal(out[0], [0, _seg_color(1), _seg_color(2), _seg_color(20), 0, 0])
+    depth = np.array([0, 1, 2, 4], np.float32)
+    out, _ = _seg_run(nns, "snpe-depth", depth, "1:2:2")
+    g = [0, 63, 127, 255]
+    np.testing.assert_array_equal(out[0], [v | v << 8 | v << 16 | 0xFF000000 for v in g])
+
+
+def test_image_segment_batched(nns):
+    rng = np.random.default_rng(1)
+    prob = rng.uniform(0, 1, (3, 4, 5, 21)).astype(np.float32)
+    out, _ = _seg_run(nns, "tflite-deeplab", prob, "21:5:4:3")
+    assert len(out) == 3
+    for b in range(3):
+        single, _ = _seg_run(nns, "tflite-deeplab", prob[b], "21:5:4:1")
+        np.testing.assert_array_equal(out[b], single[0])
+
+
+# ---------------------------------------------------------- pose_estimation ----
+
+def test_pose_heatmap_only(nns):
+    K, gw, gh = 14, 8, 6
+    heat = np.zeros((gh, gw, K), np.float32)
+    peaks = {0: (1, 1), 1: (3, 2), 2: (5, 2)}
+    for k, (x, y) in peaks.items():
+        heat[y, x, k] = 0.9
+    caps = f"other/tensors,format=static,num_tensors=1,dimensions={K}:{gw}:{gh}:1,types=float32,framerate=0/1"
+    p = nns.parse_launch(f"appsrc name=src caps={caps} ! tensor_decoder mode=pose_estimation option1=160:120 "
+                         f"option2={gw}:{gh} ! tensor_sink name=sink")
+    out = []
+    p.get_by_name("sink").connect("new-data", lambda b: out.append(np.frombuffer(b.memory(0).bytes(), np.uint32).copy()))
+    p.set_state("playing")
+    p.get_by_name("src").push_buffer(heat.ravel(), pts=0)
+    p.get_by_name("src").end_of_stream()
+    p.wait(20)
+    p.stop()
+    img = out[0].reshape(120, 160)
+    # keypoint 1 (neck) at grid (3, 2) -> pixel (60, 40); connection 0-1 drawn with an end dot
+    assert img[40, 60] == 0xFFFFFFFF
+    assert img[40 + 3, 60] == 0xFFFFFFFF   # end dot radius
+    # midpoint of top(20,20)->neck(60,40) lies on the Bresenham line
+    assert (img[29:32, 39:42] == 0xFFFFFFFF).any()
+    # keypoints without a peak (score FLT_MIN < 0.5) are not drawn: bottom-right is empty
+    assert (img[90:, 120:] == 0).all()
+
+
+def test_pose_reference_pipelines_run(nns):
+    # tests/nnstreamer_decoder_pose/runTest.sh: RGB frames split + transposed as a fake heatmap
+    desc = ("videotestsrc num-buffers=4 ! video/x-raw,width=14,height=14,format=RGB ! tensor_converter "
+            "! tensor_transform mode=arithmetic option=typecast:float32,add:128,div:255 "
+            "! tensor_split name=a tensorseg=1:14:14:1,2:14:14:1 a.src_0 ! tensor_transform mode=transpose "
+            "option=1:2:0:3 ! tensor_decoder mode=pose_estimation option1=320:240 option2=14:14 ! tensor_sink name=sink "
+            "a.src_1 ! queue ! fakesink")
+    p = nns.parse_launch(desc)
+    n = []
+    p.get_by_name("sink").connect("new-data", lambda b: n.append(b.memory(0).size))
+    p.run(timeout=30)
+    p.stop()
+    assert n == [320 * 240 * 4] * 4

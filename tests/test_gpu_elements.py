@@ -129,3 +129,39 @@ def test_bbox_ssd_device_matches_host(nns, workdir):
         assert (a != 0).sum() > 100
         # float rounding (expf / contraction) may move an edge by one pixel on rare anchors
         assert (a == b).mean() > 0.995, (a != b).sum()
+
+
+def test_segment_device_matches_host(nns):
+    from test_decoders import _seg_run
+    rng = np.random.default_rng(5)
+    prob = rng.uniform(0, 1, (2, 65, 67, 21)).astype(np.float32)  # odd sizes: partial LDS tiles
+    host, _ = _seg_run(nns, "tflite-deeplab", prob, "21:67:65:2", dev=-1)
+    dev, _ = _seg_run(nns, "tflite-deeplab", prob, "21:67:65:2", dev=0)
+    for a, b in zip(host, dev):
+        np.testing.assert_array_equal(a, b)
+    depth = rng.uniform(0, 5, (3, 16, 16)).astype(np.float32)
+    host, _ = _seg_run(nns, "snpe-depth", depth, "1:16:16:3", dev=-1)
+    dev, _ = _seg_run(nns, "snpe-depth", depth, "1:16:16:3", dev=0)
+    for a, b in zip(host, dev):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_pose_device_matches_host(nns):
+    rng = np.random.default_rng(7)
+    K, gw, gh, B = 14, 33, 33, 2
+    heat = rng.uniform(-1, 1, (B, gh, gw, K)).astype(np.float32)
+    res = {}
+    for dev in (-1, 0):
+        caps = f"other/tensors,format=static,num_tensors=1,dimensions={K}:{gw}:{gh}:{B},types=float32,framerate=0/1"
+        p = nns.parse_launch(f"appsrc name=src caps={caps} ! tensor_transform mode=typecast option=float32 "
+                             f"device={dev} ! tensor_decoder mode=pose_estimation option1=320:240 option2=257:257 "
+                             "! tensor_sink name=sink")
+        out = []
+        p.get_by_name("sink").connect("new-data", lambda b: out.append(b.memory(0).bytes()))
+        p.set_state("playing")
+        p.get_by_name("src").push_buffer(heat.ravel(), pts=0, duration=66)
+        p.get_by_name("src").end_of_stream()
+        p.wait(30)
+        p.stop()
+        res[dev] = out
+    assert len(res[0]) == B and res[0] == res[-1]
