@@ -47,7 +47,33 @@ def parse_args():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="CPU reference path (device=-1, torch CPU)")
     ap.add_argument("--queue", type=int, default=4, help="queue depth between filter and decoder")
+    ap.add_argument("--config", default=os.environ.get("NNSX_BENCH_CONFIG", "mbv2"),
+                    choices=sorted(CONFIGS), help="BASELINE.json config (default: the headline MobileNetV2 pipeline)")
     return ap.parse_args()
+
+
+# BASELINE.json configs that run on one GPU per rank.  Each: input size, model,
+# normalisation, decoder string and whether the decoder emits one buffer per frame.
+CONFIGS = {
+    "mbv2": dict(size=224, model="mobilenet_v2_fused", norm="typecast:float32,add:-127.5,div:127.5",
+                 decoder="tensor_decoder mode=image_labeling option1={labels}", per_frame=False,
+                 metric="end-to-end frames/sec + p50 per-frame latency, MobileNetV2 224x224 pipeline",
+                 desc="MobileNetV2 224x224 (tensor_filter + image_labeling decoder)"),
+    "ssd": dict(size=300, model="ssd_fused", norm="typecast:float32,add:-127.5,div:127.5",
+                decoder="tensor_decoder mode=bounding_boxes option1=mobilenet-ssd option2={coco} option3={priors} "
+                        "option4=300:300 option5=300:300", per_frame=True,
+                metric="end-to-end frames/sec + p50 per-frame latency, SSD-MobileNet 300x300 + bounding_boxes + HIP NMS",
+                desc="SSDLite-MobileNetV2 300x300 (tensor_filter + bounding_boxes decoder, HIP NMS)"),
+    "deeplab": dict(size=513, model="deeplab_fused", norm="typecast:float32,div:255.0",
+                    decoder="tensor_decoder mode=image_segment option1=tflite-deeplab", per_frame=True,
+                    metric="end-to-end frames/sec + p50 per-frame latency, DeepLabV3 513x513 segmentation pipeline",
+                    desc="DeepLabV3-MobileNetV2 513x513 (tensor_filter + image_segment decoder)"),
+    "posenet": dict(size=257, model="posenet_fused", norm="typecast:float32,add:-127.5,div:127.5",
+                    decoder="tensor_decoder mode=pose_estimation option1=640:480 option2=257:257 option3={pose} "
+                            "option4=heatmap-offset", per_frame=True,
+                    metric="end-to-end frames/sec + p50 per-frame latency, PoseNet 257x257 pipeline",
+                    desc="PoseNet-MobileNetV1 257x257 (tensor_filter + pose_estimation decoder)"),
+}
 
 
 def main():
@@ -73,10 +99,19 @@ def main():
     dev = local_rank if use_gpu else -1
     workdir = os.path.join(tempfile.gettempdir(), f"nnsx_bench_{os.getuid()}_{rank}")
     os.makedirs(workdir, exist_ok=True)
-    model_path = os.path.join(workdir, f"{a.model}.pt")
+    cfg = CONFIGS[a.config]
+    model_name = a.model if a.config == "mbv2" else cfg["model"]
+    model_path = os.path.join(workdir, f"{model_name}.pt")
     layout = "nhwc"
-    export(a.model, model_path, layout=layout)
-    labels = write_labels(os.path.join(workdir, "labels.txt"))
+    export(model_name, model_path, layout=layout)
+    from nnstreamer_amd.models.posenet import write_pose_labels
+    from nnstreamer_amd.models.ssd import write_box_priors, write_coco_labels
+
+    files = dict(labels=write_labels(os.path.join(workdir, "labels.txt")),
+                 coco=write_coco_labels(os.path.join(workdir, "coco.txt")),
+                 priors=write_box_priors(os.path.join(workdir, "priors.txt")),
+                 pose=write_pose_labels(os.path.join(workdir, "pose17.txt")))
+    S = cfg["size"]
 
     B = a.batch
     total = a.warmup + a.steps
@@ -85,21 +120,27 @@ def main():
     accel = "true:gpu" if use_gpu else "false"
     desc = (
         f"videotestsrc num-buffers={frames} pattern=snow pool-size=16 "
-        f"! video/x-raw,format=RGB,width=224,height=224,framerate=0/1 "
+        f"! video/x-raw,format=RGB,width={S},height={S},framerate=0/1 "
         f"! tensor_converter frames-per-tensor={B} device={dev} "
-        f"! tensor_transform mode=arithmetic option=typecast:float32,add:-127.5,div:127.5 "
-        f"! tensor_filter framework=pytorch model={model_path} input=3:224:224:{B} inputtype=float32 "
+        f"! tensor_transform mode=arithmetic option={cfg['norm']} "
+        f"! tensor_filter framework=pytorch model={model_path} input=3:{S}:{S}:{B} inputtype=float32 "
         f"accelerator={accel} device={dev} custom=hipgraph:{graph} "
         f"! queue max-size-buffers={a.queue} "
-        f"! tensor_decoder mode=image_labeling option1={labels} "
+        f"! {cfg['decoder'].format(**files)} "
         f"! tensor_sink name=sink"
     )
+    per_step = B if cfg["per_frame"] else 1  # sink buffers per batch
     pipe = nns.parse_launch(desc)
     sink = pipe.get_by_name("sink")
     arrivals = []
     latencies = []
 
+    seen = [0]
+
     def on_data(buf):
+        seen[0] += 1
+        if seen[0] % per_step:
+            return  # a step ends with the last frame of the batch
         now = pipe.running_time()
         arrivals.append(time.perf_counter())
         if buf.pts >= 0:
@@ -139,7 +180,7 @@ def main():
     fps_total = world * a.steps * B / elapsed
     if rank == 0:
         out = {
-            "metric": "end-to-end frames/sec + p50 per-frame latency, MobileNetV2 224x224 pipeline",
+            "metric": cfg["metric"],
             "value": round(fps_total, 2),
             "unit": "frames/s",
             "n_gpus": world if use_gpu else 0,
@@ -156,7 +197,7 @@ def main():
             "frames_per_step_per_gpu": B,
             "wall_s": round(t_end - t_start, 3),
             "config": {
-                "model": "MobileNetV2 224x224 (tensor_filter + image_labeling decoder)",
+                "model": cfg["desc"],
                 "global_batch": B * world,
                 "seq_len": 1,
                 "parallelism": f"branch-dp{world}",

@@ -10,9 +10,9 @@ namespace kernels {
 // wt is zero-padded to [ceil16(N)][Kpad], Kpad = ceil32(K).  act: 0 none, 1 relu6, 2 relu
 void pw_gemm(const void* x, const void* wt, const float* bias, const void* res, void* y, int M, int N, int K, int Kpad,
              int act, bool out_f32, hipStream_t s);
-// depthwise 3x3, pad 1, stride 1|2; x [B][H][W][C], w [9][C], C % 8 == 0
-void dw3x3(const void* x, const void* w, const float* bias, void* y, int B, int H, int W, int C, int stride, int act,
-           hipStream_t s);
+// depthwise 3x3, stride 1|2, dilation d (padding d); x [B][H][W][C], w [9][C], C % 8 == 0
+void dw3x3(const void* x, const void* w, const float* bias, void* y, int B, int H, int W, int C, int stride, int dil,
+           int act, hipStream_t s);
 // 3x3/2 stem conv 3 -> 32 from an f32 NHWC frame; w f32 [3][3][3][32]
 void stem3x3(const float* x, const float* w, const float* bias, void* y, int B, int H, int W, int act, hipStream_t s);
 // mean over HW: x [B][HW][C] -> y [B][C] (bf16)

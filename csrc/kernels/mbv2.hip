@@ -141,7 +141,7 @@ __global__ void __launch_bounds__(256) dw3x3_kernel(const uint16_t* __restrict__
                                                     const float* __restrict__ bias,  // [C]
                                                     uint16_t* __restrict__ y,        // [B][Ho][Wo][C]
                                                     int B, int H, int W, int C, int Ho, int Wo, int stride,
-                                                    int act) {
+                                                    int dil, int act) {
   const int cg = C >> 3;
   const int64_t total = static_cast<int64_t>(B) * Ho * Wo * cg;
   for (int64_t t = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; t < total;
@@ -158,11 +158,11 @@ __global__ void __launch_bounds__(256) dw3x3_kernel(const uint16_t* __restrict__
     for (int q = 0; q < 8; ++q) acc[q] = bias[c + q];
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
-      const int iy = oy * stride - 1 + ky;
+      const int iy = oy * stride - dil + ky * dil;
       if (iy < 0 || iy >= H) continue;
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
-        const int ix = ox * stride - 1 + kx;
+        const int ix = ox * stride - dil + kx * dil;
         if (ix < 0 || ix >= W) continue;
         const uint4 xv = *reinterpret_cast<const uint4*>(x + ((static_cast<int64_t>(b) * H + iy) * W + ix) * C + c);
         const uint4 wv = *reinterpret_cast<const uint4*>(w + (ky * 3 + kx) * C + c);
@@ -278,12 +278,13 @@ void pw_gemm(const void* x, const void* wt, const float* bias, const void* res, 
                        static_cast<const uint16_t*>(wt), bias, static_cast<const uint16_t*>(res), y, M, N, K, Kpad, act);
 }
 
-void dw3x3(const void* x, const void* w, const float* bias, void* y, int B, int H, int W, int C, int stride, int act,
-           hipStream_t s) {
-  int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
+void dw3x3(const void* x, const void* w, const float* bias, void* y, int B, int H, int W, int C, int stride, int dil,
+           int act, hipStream_t s) {
+  // padding == dilation keeps "same" geometry: Ho = (H - 1) / stride + 1
+  int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
   int64_t work = static_cast<int64_t>(B) * Ho * Wo * (C / 8);
   hipLaunchKernelGGL(dw3x3_kernel, dim3(grid_cap(work)), dim3(256), 0, s, static_cast<const uint16_t*>(x),
-                     static_cast<const uint16_t*>(w), bias, static_cast<uint16_t*>(y), B, H, W, C, Ho, Wo, stride, act);
+                     static_cast<const uint16_t*>(w), bias, static_cast<uint16_t*>(y), B, H, W, C, Ho, Wo, stride, dil, act);
 }
 
 void stem3x3(const float* x, const float* w, const float* bias, void* y, int B, int H, int W, int act, hipStream_t s) {

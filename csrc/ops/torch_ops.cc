@@ -55,7 +55,8 @@ at::Tensor pw_conv_cpu(const at::Tensor& x, const at::Tensor& wt, const at::Tens
 }
 
 // ------------------------------------------------------------ dw_conv ----
-at::Tensor dw_conv_cuda(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int64_t stride, int64_t act) {
+at::Tensor dw_conv_cuda(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int64_t stride, int64_t act,
+                        int64_t dilation) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() == 4, "dw_conv: x [B,H,W,C] bf16");
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   TORCH_CHECK(C % 8 == 0 && w.numel() == 9 * C && w.scalar_type() == at::kBFloat16, "dw_conv: w [9,C] bf16, C%8==0");
@@ -63,15 +64,16 @@ at::Tensor dw_conv_cuda(const at::Tensor& x, const at::Tensor& w, const at::Tens
   at::Tensor y = at::empty({B, Ho, Wo, C}, x.options());
   nnsx::kernels::dw3x3(x.data_ptr(), w.data_ptr(), bias.data_ptr<float>(), y.data_ptr(), static_cast<int>(B),
                        static_cast<int>(H), static_cast<int>(W), static_cast<int>(C), static_cast<int>(stride),
-                       static_cast<int>(act), cur_stream());
+                       static_cast<int>(dilation), static_cast<int>(act), cur_stream());
   return y;
 }
 
-at::Tensor dw_conv_cpu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int64_t stride, int64_t act) {
+at::Tensor dw_conv_cpu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int64_t stride, int64_t act,
+                       int64_t dilation) {
   const int64_t C = x.size(3);
   at::Tensor xf = x.to(at::kFloat).permute({0, 3, 1, 2});
   at::Tensor wf = w.to(at::kFloat).view({3, 3, C}).permute({2, 0, 1}).unsqueeze(1).contiguous();
-  at::Tensor v = at::conv2d(xf, wf, bias, {stride, stride}, {1, 1}, {1, 1}, C);
+  at::Tensor v = at::conv2d(xf, wf, bias, {stride, stride}, {dilation, dilation}, {dilation, dilation}, C);
   return act_ref(v, act).permute({0, 2, 3, 1}).contiguous().to(at::kBFloat16);
 }
 
@@ -112,7 +114,7 @@ at::Tensor avgpool_cpu(const at::Tensor& x) { return x.to(at::kFloat).mean({1, 2
 
 TORCH_LIBRARY(nnsx, m) {
   m.def("pw_conv(Tensor x, Tensor wt, Tensor bias, Tensor? res, int N, int act, bool out_f32) -> Tensor");
-  m.def("dw_conv(Tensor x, Tensor w, Tensor bias, int stride, int act) -> Tensor");
+  m.def("dw_conv(Tensor x, Tensor w, Tensor bias, int stride, int act, int dilation=1) -> Tensor");
   m.def("stem_conv(Tensor x, Tensor w, Tensor bias, int act) -> Tensor");
   m.def("avgpool(Tensor x) -> Tensor");
 }

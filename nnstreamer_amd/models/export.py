@@ -49,14 +49,26 @@ def build_model(name: str, seed: int = 0, layout: str = "nchw", num_classes: int
         from .ssd import ssd_mobilenet
 
         return ssd_mobilenet(seed=seed).eval()
+    elif name in ("ssd_mobilenet_fused", "ssd_fused"):
+        from .ssd import fused_ssd_mobilenet
+
+        return fused_ssd_mobilenet(seed=seed)
     elif name in ("deeplabv3", "deeplab"):
         from .deeplab import deeplabv3
 
         return deeplabv3(seed=seed).eval()
+    elif name in ("deeplabv3_fused", "deeplab_fused"):
+        from .deeplab import fused_deeplabv3
+
+        return fused_deeplabv3(seed=seed)
     elif name in ("posenet", "pose"):
         from .posenet import posenet
 
         return posenet(seed=seed).eval()
+    elif name in ("posenet_fused", "pose_fused"):
+        from .posenet import fused_posenet
+
+        return fused_posenet(seed=seed)
     else:
         raise ValueError(f"unknown model {name}")
     return (NHWCWrapper(m) if layout == "nhwc" else NCHWWrapper(m)).eval()

@@ -56,15 +56,17 @@ class PW(nn.Module):
 
 
 class DW(nn.Module):
-    def __init__(self, w: torch.Tensor, b: torch.Tensor, stride: int):
+    def __init__(self, w: torch.Tensor, b: torch.Tensor, stride: int, dilation: int = 1, act: int = 1):
         super().__init__()
         c = w.shape[0]
         self.register_buffer("w", w.reshape(c, 9).t().contiguous().to(torch.bfloat16))  # [9, C]
         self.register_buffer("bias", b.contiguous())
         self.stride = int(stride)
+        self.dilation = int(dilation)
+        self.act = int(act)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return torch.ops.nnsx.dw_conv(x, self.w, self.bias, self.stride, 1)
+        return torch.ops.nnsx.dw_conv(x, self.w, self.bias, self.stride, self.act, self.dilation)
 
 
 class Block(nn.Module):

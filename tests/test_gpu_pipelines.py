@@ -62,3 +62,64 @@ def test_hipgraph_filter_matches_eager(nns, mbv2_model, labels):
     assert len(res["true"]) == 3
     for a, b in zip(res["true"], res["false"]):
         np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-4)
+
+
+# ------------------------------------------- BASELINE configs 3-5 on one GPU ----
+
+def _export(workdir, name):
+    import os
+    from nnstreamer_amd.models.export import export
+    path = os.path.join(workdir, f"{name}.pt")
+    if not os.path.exists(path):
+        export(name, path)
+    return path
+
+
+def test_ssd_pipeline_device_decoder_matches_host(nns, workdir):
+    from nnstreamer_amd.models.ssd import write_box_priors, write_coco_labels
+    model = _export(workdir, "ssd_fused")
+    pri = write_box_priors(f"{workdir}/ssd_priors.txt")
+    lab = write_coco_labels(f"{workdir}/coco.txt")
+    res = {}
+    for ddev in (0, -1):
+        desc = ("videotestsrc num-buffers=8 pattern=snow ! video/x-raw,format=RGB,width=300,height=300,framerate=30/1 "
+                "! tensor_converter frames-per-tensor=4 device=0 "
+                "! tensor_transform mode=arithmetic option=typecast:float32,add:-127.5,div:127.5 "
+                f"! tensor_filter framework=pytorch model={model} input=3:300:300:4 inputtype=float32 "
+                "accelerator=true:gpu custom=hipgraph:true "
+                f"! tensor_decoder mode=bounding_boxes device={ddev} option1=mobilenet-ssd option2={lab} "
+                f"option3={pri} option4=320:240 option5=300:300 ! tensor_sink name=sink")
+        res[ddev] = run_pipeline(nns, desc, collect=lambda b: (b.memory(0).on_device, b.memory(0).bytes()), timeout=180)
+    assert len(res[0]) == len(res[-1]) == 8
+    assert all(d for d, _ in res[0]) and not any(d for d, _ in res[-1])
+    for (_, a), (_, b) in zip(res[0], res[-1]):
+        a = np.frombuffer(a, np.uint32)
+        b = np.frombuffer(b, np.uint32)
+        assert (a == b).mean() > 0.995
+
+
+def test_deeplab_pipeline(nns, workdir):
+    model = _export(workdir, "deeplab_fused")
+    desc = ("videotestsrc num-buffers=4 pattern=snow ! video/x-raw,format=RGB,width=513,height=513,framerate=30/1 "
+            "! tensor_converter frames-per-tensor=2 device=0 "
+            "! tensor_transform mode=arithmetic option=typecast:float32,div:255.0 "
+            f"! tensor_filter framework=pytorch model={model} input=3:513:513:2 inputtype=float32 "
+            "accelerator=true:gpu custom=hipgraph:true "
+            "! tensor_decoder mode=image_segment option1=tflite-deeplab ! tensor_sink name=sink")
+    out = run_pipeline(nns, desc, collect=lambda b: (b.memory(0).on_device, b.memory(0).size), timeout=180)
+    assert len(out) == 4 and all(d and s == 513 * 513 * 4 for d, s in out)
+
+
+def test_posenet_pipeline(nns, workdir):
+    from nnstreamer_amd.models.posenet import write_pose_labels
+    model = _export(workdir, "posenet_fused")
+    lab = write_pose_labels(f"{workdir}/pose17.txt")
+    desc = ("videotestsrc num-buffers=4 pattern=snow ! video/x-raw,format=RGB,width=257,height=257,framerate=30/1 "
+            "! tensor_converter frames-per-tensor=2 device=0 "
+            "! tensor_transform mode=arithmetic option=typecast:float32,add:-127.5,div:127.5 "
+            f"! tensor_filter framework=pytorch model={model} input=3:257:257:2 inputtype=float32 "
+            "accelerator=true:gpu custom=hipgraph:true "
+            f"! tensor_decoder mode=pose_estimation option1=640:480 option2=257:257 option3={lab} "
+            "option4=heatmap-offset ! tensor_sink name=sink")
+    out = run_pipeline(nns, desc, collect=lambda b: b.memory(0).size, timeout=180)
+    assert out == [640 * 480 * 4] * 4
