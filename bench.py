@@ -52,6 +52,10 @@ def parse_args():
     return ap.parse_args()
 
 
+# best CPU reference path for the MobileNetV2 pipeline
+# (identical pipeline, host elements + fp32 PyTorch CPU, 8 vCPU).
+CPU_BASELINE_FPS = 254.1
+
 # BASELINE.json configs that run on one GPU per rank.  Each: input size, model,
 # normalisation, decoder string and whether the decoder emits one buffer per frame.
 CONFIGS = {
@@ -189,7 +193,7 @@ def main():
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": None,
+            "vs_baseline": (round(fps_total / CPU_BASELINE_FPS, 2) if a.config == "mbv2" else None),
             "dtype": "bf16" if "fused" in a.model else "fp32",
             "data": "synthetic video frames (videotestsrc pattern=snow), random-init weights",
             "p50_latency_ms": round(p50, 3),
