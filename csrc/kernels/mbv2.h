@@ -3,6 +3,9 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <cstddef>
+#include <cstdint>
+
 namespace nnsx {
 namespace kernels {
 
@@ -17,6 +20,29 @@ void dw3x3(const void* x, const void* w, const float* bias, void* y, int B, int 
 void stem3x3(const float* x, const float* w, const float* bias, void* y, int B, int H, int W, int act, hipStream_t s);
 // mean over HW: x [B][HW][C] -> y [B][C] (bf16)
 void avgpool(const void* x, void* y, int B, int HW, int C, hipStream_t s);
+
+// Fused inverted-residual block (ir_fused.hip): expand 1x1 + ReLU6 -> dw 3x3 +
+// ReLU6 -> project 1x1 (+ residual), hidden activation kept in LDS.
+//   we [hid][cin32] (K zero-padded), wd [9][hid], wp [ceil16(cout)][hid]
+//   (rows zero-padded); biases fp32.  has_expand = 0: hidden == input (t=1).
+struct IrBlockArgs {
+  const uint16_t* x = nullptr;
+  uint16_t* y = nullptr;
+  const uint16_t* we = nullptr;
+  const float* be = nullptr;
+  const uint16_t* wd = nullptr;
+  const float* bd = nullptr;
+  const uint16_t* wp = nullptr;
+  const float* bp = nullptr;
+  int B = 0, H = 0, W = 0, cin = 0, hid = 0, cout = 0, stride = 1;
+  int has_expand = 1, residual = 0;
+  // derived by ir_block()
+  int cin32 = 0, Ho = 0, Wo = 0, tiles_x = 0, tiles_y = 0;
+};
+bool ir_block_supported(int stride, int cin, int hid, int cout);
+size_t ir_block_lds_bytes(int stride, int cin32);
+// returns false (nothing launched) for unsupported shapes
+bool ir_block(const IrBlockArgs& a, hipStream_t s);
 
 }  // namespace kernels
 }  // namespace nnsx

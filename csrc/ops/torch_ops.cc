@@ -110,6 +110,60 @@ at::Tensor avgpool_cuda(const at::Tensor& x) {
 
 at::Tensor avgpool_cpu(const at::Tensor& x) { return x.to(at::kFloat).mean({1, 2}).to(at::kBFloat16); }
 
+// ----------------------------------------------------------- ir_block ----
+// Fused inverted residual.  we [hid, cin32], wd [9, hid], wp [ceil16(cout), hid] bf16; biases f32.
+at::Tensor ir_block_cuda(const at::Tensor& x, const at::Tensor& we, const at::Tensor& be, const at::Tensor& wd,
+                         const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, int64_t stride,
+                         int64_t cout, bool has_expand, bool residual) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() == 4,
+              "ir_block: x [B,H,W,C] bf16");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int64_t hid = wd.size(1);
+  TORCH_CHECK(wd.numel() == 9 * hid && wp.size(1) == hid && wp.size(0) >= (cout + 15) / 16 * 16, "ir_block: weights");
+  TORCH_CHECK(!has_expand || (we.size(0) == hid && we.size(1) >= C), "ir_block: expand weights");
+  TORCH_CHECK(!residual || (stride == 1 && C == cout), "ir_block: residual needs stride 1 and cin == cout");
+  const int64_t Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  at::Tensor y = at::empty({B, Ho, Wo, cout}, x.options());
+  nnsx::kernels::IrBlockArgs a;
+  a.x = static_cast<const uint16_t*>(x.data_ptr());
+  a.y = static_cast<uint16_t*>(y.data_ptr());
+  a.we = has_expand ? static_cast<const uint16_t*>(we.data_ptr()) : nullptr;
+  a.be = has_expand ? be.data_ptr<float>() : nullptr;
+  a.wd = static_cast<const uint16_t*>(wd.data_ptr());
+  a.bd = bd.data_ptr<float>();
+  a.wp = static_cast<const uint16_t*>(wp.data_ptr());
+  a.bp = bp.data_ptr<float>();
+  a.B = static_cast<int>(B);
+  a.H = static_cast<int>(H);
+  a.W = static_cast<int>(W);
+  a.cin = static_cast<int>(C);
+  a.hid = static_cast<int>(hid);
+  a.cout = static_cast<int>(cout);
+  a.stride = static_cast<int>(stride);
+  a.has_expand = has_expand ? 1 : 0;
+  a.residual = residual ? 1 : 0;
+  TORCH_CHECK(nnsx::kernels::ir_block(a, cur_stream()), "ir_block: unsupported shape (stride ", stride, ", cin ", C,
+              ", hid ", hid, ", cout ", cout, ")");
+  return y;
+}
+
+at::Tensor ir_block_cpu(const at::Tensor& x, const at::Tensor& we, const at::Tensor& be, const at::Tensor& wd,
+                        const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, int64_t stride,
+                        int64_t cout, bool has_expand, bool residual) {
+  at::Tensor h = x;
+  const int64_t hid = wd.size(1);
+  if (has_expand) h = pw_conv_cpu(x, we, be, c10::nullopt, hid, 1, false);
+  h = dw_conv_cpu(h, wd, bd, stride, 1, 1);
+  c10::optional<at::Tensor> res;
+  if (residual) res = x;
+  return pw_conv_cpu(h, wp, bp, res, cout, 0, false);
+}
+
+bool ir_supported(int64_t stride, int64_t cin, int64_t hid, int64_t cout) {
+  return nnsx::kernels::ir_block_supported(static_cast<int>(stride), static_cast<int>(cin), static_cast<int>(hid),
+                                           static_cast<int>(cout));
+}
+
 }  // namespace
 
 TORCH_LIBRARY(nnsx, m) {
@@ -117,6 +171,9 @@ TORCH_LIBRARY(nnsx, m) {
   m.def("dw_conv(Tensor x, Tensor w, Tensor bias, int stride, int act, int dilation=1) -> Tensor");
   m.def("stem_conv(Tensor x, Tensor w, Tensor bias, int act) -> Tensor");
   m.def("avgpool(Tensor x) -> Tensor");
+  m.def("ir_block(Tensor x, Tensor we, Tensor be, Tensor wd, Tensor bd, Tensor wp, Tensor bp, int stride, int cout, "
+        "bool has_expand, bool residual) -> Tensor");
+  m.def("ir_supported(int stride, int cin, int hid, int cout) -> bool", ir_supported);
 }
 
 TORCH_LIBRARY_IMPL(nnsx, CUDA, m) {
@@ -124,6 +181,7 @@ TORCH_LIBRARY_IMPL(nnsx, CUDA, m) {
   m.impl("dw_conv", dw_conv_cuda);
   m.impl("stem_conv", stem_conv_cuda);
   m.impl("avgpool", avgpool_cuda);
+  m.impl("ir_block", ir_block_cuda);
 }
 
 TORCH_LIBRARY_IMPL(nnsx, CPU, m) {
@@ -131,4 +189,5 @@ TORCH_LIBRARY_IMPL(nnsx, CPU, m) {
   m.impl("dw_conv", dw_conv_cpu);
   m.impl("stem_conv", stem_conv_cpu);
   m.impl("avgpool", avgpool_cpu);
+  m.impl("ir_block", ir_block_cpu);
 }

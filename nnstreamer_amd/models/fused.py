@@ -21,6 +21,11 @@ import torch.nn as nn
 
 from .mobilenet_v2 import ConvBNReLU, InvertedResidual, MobileNetV2
 
+import os
+
+# NNSX_FUSE_IR=0 keeps every inverted residual on the three-kernel path (A/B testing)
+FUSE_IR = os.environ.get("NNSX_FUSE_IR", "1") != "0"
+
 
 def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d):
     w = conv.weight.detach().double()
@@ -86,8 +91,20 @@ class Block(nn.Module):
         p: ConvBNReLU = layers[idx + 1]
         self.project = PW(*_fold(p[0], p[1]), act=0)
         self.use_res = bool(ir.use_res)
+        # fused single-kernel path (csrc/kernels/ir_fused.hip): hidden activation stays in LDS
+        hid = int(d[0].out_channels)
+        cin = int(ir.conv[0][0].in_channels)
+        self.hid = hid
+        self.cout = int(p[0].out_channels)
+        self.register_buffer("ir_we", self.expand.wt[:hid].contiguous() if self.has_expand else torch.zeros(1, dtype=torch.bfloat16))
+        self.register_buffer("ir_be", self.expand.bias[:hid].contiguous() if self.has_expand else torch.zeros(1))
+        self.use_ir = bool(torch.ops.nnsx.ir_supported(int(ir.stride), cin, hid, self.cout)) and FUSE_IR
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.use_ir and self.dw.dilation == 1:
+            return torch.ops.nnsx.ir_block(x, self.ir_we, self.ir_be, self.dw.w, self.dw.bias, self.project.wt,
+                                           self.project.bias, self.dw.stride, self.cout, self.has_expand,
+                                           self.use_res)
         h = self.expand(x) if self.has_expand else x
         h = self.dw(h)
         if self.use_res:

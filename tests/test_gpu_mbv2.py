@@ -83,3 +83,60 @@ def test_fused_mobilenet_matches_fp32_model(nns):
     agree = (out.argmax(1) == ref.argmax(1)).float().mean().item()
     assert agree >= 0.75
     torch.testing.assert_close(out, out_script)
+
+
+# ---------------------------------------------------- fused inverted residual ----
+# every MobileNetV2 block shape (H, cin, hid, cout, stride) + odd sizes for partial tiles
+IR_SHAPES = [(112, 32, 32, 16, 1), (112, 16, 96, 24, 2), (56, 24, 144, 24, 1), (56, 24, 144, 32, 2),
+             (28, 32, 192, 32, 1), (28, 32, 192, 64, 2), (14, 64, 384, 64, 1), (14, 64, 384, 96, 1),
+             (14, 96, 576, 96, 1), (7, 160, 960, 160, 1), (7, 160, 960, 320, 1), (19, 24, 96, 24, 1),
+             (13, 32, 64, 32, 2), (38, 32, 192, 64, 2)]
+
+
+@pytest.mark.parametrize("H,cin,hid,cout,stride", IR_SHAPES)
+def test_ir_block_matches_unfused(nns, H, cin, hid, cout, stride):
+    torch.manual_seed(H + cin + hid)
+    B = 3
+    has_expand = hid != cin or cin == 16
+    if cin == 32 and hid == 32:
+        has_expand = False
+    residual = stride == 1 and cin == cout
+    x = (torch.randn(B, H, H, cin, device="cuda") * 0.5).to(torch.bfloat16)
+    cin32 = (cin + 31) // 32 * 32
+    we = torch.zeros(hid, cin32, device="cuda")
+    we[:, :cin] = torch.randn(hid, cin, device="cuda") / cin ** 0.5
+    we = we.to(torch.bfloat16)
+    be = torch.randn(hid, device="cuda") * 0.1
+    wd = (torch.randn(9, hid, device="cuda") / 3).to(torch.bfloat16)
+    bd = torch.randn(hid, device="cuda") * 0.1
+    n64 = (cout + 63) // 64 * 64
+    wp = torch.zeros(n64, hid, device="cuda")
+    wp[:cout] = torch.randn(cout, hid, device="cuda") / hid ** 0.5
+    wp = wp.to(torch.bfloat16)
+    bp = torch.randn(n64, device="cuda") * 0.1
+    assert torch.ops.nnsx.ir_supported(stride, cin, hid, cout)
+    y = torch.ops.nnsx.ir_block(x, we, be, wd, bd, wp, bp, stride, cout, has_expand, residual)
+    # unfused chain of the same kernels (identical bf16 rounding points)
+    h = torch.ops.nnsx.pw_conv(x, we, be, None, hid, 1, False) if has_expand else x
+    h = torch.ops.nnsx.dw_conv(h, wd, bd, stride, 1)
+    ref = torch.ops.nnsx.pw_conv(h, wp, bp, x if residual else None, cout, 0, False)
+    assert y.shape == ref.shape
+    torch.testing.assert_close(y.float(), ref.float(), rtol=2e-2, atol=3e-2)
+
+
+def test_fused_model_ir_vs_unfused(nns):
+    import importlib
+    import os
+    from nnstreamer_amd.models import fused as fused_mod
+    from nnstreamer_amd.models.mobilenet_v2 import mobilenet_v2
+    ref = mobilenet_v2(seed=4)
+    m = fused_mod.FusedMobileNetV2.from_reference(ref).cuda().eval()
+    assert sum(int(b.use_ir) for b in m.blocks) >= 15
+    x = torch.rand(4, 224, 224, 3, device="cuda") * 2 - 1
+    with torch.no_grad():
+        y = m(x)
+        for b in m.blocks:
+            b.use_ir = False
+        y0 = m(x)
+    cos = F.cosine_similarity(y.flatten(), y0.flatten(), 0).item()
+    assert cos > 0.999, cos
