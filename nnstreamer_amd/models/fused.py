@@ -96,13 +96,31 @@ class Block(nn.Module):
         cin = int(ir.conv[0][0].in_channels)
         self.hid = hid
         self.cout = int(p[0].out_channels)
-        self.register_buffer("ir_we", self.expand.wt[:hid].contiguous() if self.has_expand else torch.zeros(1, dtype=torch.bfloat16))
-        self.register_buffer("ir_be", self.expand.bias[:hid].contiguous() if self.has_expand else torch.zeros(1))
-        self.use_ir = bool(torch.ops.nnsx.ir_supported(int(ir.stride), cin, hid, self.cout)) and FUSE_IR
+        # hidden width padded to the kernel's 32-channel chunk with zero weights/biases
+        # (padded channels stay exactly 0 through ReLU6 and contribute nothing)
+        hp = (hid + 31) // 32 * 32
+        we = torch.zeros(hp, self.expand.wt.shape[1], dtype=torch.bfloat16)
+        be = torch.zeros(hp)
+        if self.has_expand:
+            we[:hid] = self.expand.wt[:hid]
+            be[:hid] = self.expand.bias[:hid]
+        wd = torch.zeros(9, hp, dtype=torch.bfloat16)
+        wd[:, :hid] = self.dw.w
+        bd = torch.zeros(hp)
+        bd[:hid] = self.dw.bias
+        wp = torch.zeros(self.project.wt.shape[0], hp, dtype=torch.bfloat16)
+        wp[:, :hid] = self.project.wt[:, :hid]
+        self.register_buffer("ir_we", we)
+        self.register_buffer("ir_be", be)
+        self.register_buffer("ir_wd", wd)
+        self.register_buffer("ir_bd", bd)
+        self.register_buffer("ir_wp", wp)
+        self.use_ir = (bool(torch.ops.nnsx.ir_supported(int(ir.stride), cin, hp, self.cout)) and FUSE_IR
+                       and (self.has_expand or hid == hp))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.use_ir and self.dw.dilation == 1:
-            return torch.ops.nnsx.ir_block(x, self.ir_we, self.ir_be, self.dw.w, self.dw.bias, self.project.wt,
+            return torch.ops.nnsx.ir_block(x, self.ir_we, self.ir_be, self.ir_wd, self.ir_bd, self.ir_wp,
                                            self.project.bias, self.dw.stride, self.cout, self.has_expand,
                                            self.use_res)
         h = self.expand(x) if self.has_expand else x

@@ -110,14 +110,28 @@ def test_ir_block_matches_unfused(nns, H, cin, hid, cout, stride):
     wd = (torch.randn(9, hid, device="cuda") / 3).to(torch.bfloat16)
     bd = torch.randn(hid, device="cuda") * 0.1
     n64 = (cout + 63) // 64 * 64
-    wp = torch.zeros(n64, hid, device="cuda")
-    wp[:cout] = torch.randn(cout, hid, device="cuda") / hid ** 0.5
+    wp = torch.zeros(n64, (hid + 31) // 32 * 32, device="cuda")
+    wp[:cout, :hid] = torch.randn(cout, hid, device="cuda") / hid ** 0.5
     wp = wp.to(torch.bfloat16)
     bp = torch.randn(n64, device="cuda") * 0.1
-    assert torch.ops.nnsx.ir_supported(stride, cin, hid, cout)
-    y = torch.ops.nnsx.ir_block(x, we, be, wd, bd, wp, bp, stride, cout, has_expand, residual)
+    hp = (hid + 31) // 32 * 32  # the op takes the hidden width padded to 32 (zero weights)
+    assert torch.ops.nnsx.ir_supported(stride, cin, hp, cout)
+    wep = torch.zeros(hp, cin32, device="cuda", dtype=torch.bfloat16)
+    wep[:hid] = we
+    bep = torch.zeros(hp, device="cuda")
+    bep[:hid] = be
+    wdp = torch.zeros(9, hp, device="cuda", dtype=torch.bfloat16)
+    wdp[:, :hid] = wd
+    bdp = torch.zeros(hp, device="cuda")
+    bdp[:hid] = bd
+    wpp = wp
+    y = torch.ops.nnsx.ir_block(x, wep, bep, wdp, bdp, wpp, bp, stride, cout, has_expand, residual)
     # unfused chain of the same kernels (identical bf16 rounding points)
-    h = torch.ops.nnsx.pw_conv(x, we, be, None, hid, 1, False) if has_expand else x
+    we64 = torch.zeros((hid + 63) // 64 * 64, cin32, device="cuda", dtype=torch.bfloat16)
+    we64[:hid] = we
+    be64 = torch.zeros(we64.shape[0], device="cuda")
+    be64[:hid] = be
+    h = torch.ops.nnsx.pw_conv(x, we64, be64, None, hid, 1, False) if has_expand else x
     h = torch.ops.nnsx.dw_conv(h, wd, bd, stride, 1)
     ref = torch.ops.nnsx.pw_conv(h, wp, bp, x if residual else None, cout, 0, False)
     assert y.shape == ref.shape
