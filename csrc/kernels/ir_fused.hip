@@ -23,6 +23,7 @@
 // HBM traffic per block drops to input + output (+ weights through L2).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "kernels/mbv2.h"
@@ -35,6 +36,7 @@ namespace {
 typedef short bf16x8_t __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x8_mfma __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float bf2f(uint16_t b) { return __uint_as_float(static_cast<uint32_t>(b) << 16); }
 __device__ __forceinline__ uint16_t f2bf(float f) {
@@ -44,6 +46,7 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
 }
 __device__ __forceinline__ float relu6(float v) { return fminf(fmaxf(v, 0.f), 6.f); }
 
+constexpr size_t kLdsLimit = 160 * 1024;  // gfx950 LDS per CU (one workgroup may own it all)
 constexpr int TO = 8;       // output tile edge
 constexpr int HC = 32;      // hidden channels per chunk (= one MFMA K step)
 constexpr int HROW = HC + 8;  // LDS row pitch (elements) of the hidden / dw tiles
@@ -51,187 +54,289 @@ constexpr int HROW = HC + 8;  // LDS row pitch (elements) of the hidden / dw til
 __host__ __device__ constexpr int tile_in(int s) { return (TO - 1) * s + 3; }
 __host__ __device__ constexpr int tile_in_px16(int s) { return (tile_in(s) * tile_in(s) + 15) / 16 * 16; }
 
-template <int S, int NOT>
+template <int S, int NOT, int KS_MAX>
 __global__ void __launch_bounds__(256) ir_block_kernel(IrBlockArgs a) {
   constexpr int TI = tile_in(S);
   constexpr int PIN = TI * TI;
   constexpr int PIN16 = tile_in_px16(S);
+  constexpr int NB = PIN16 / 16;                       // 16-pixel B tiles of the halo tile
+  constexpr int NV = (PIN16 * 4 * KS_MAX + 255) / 256;  // 16-B input vectors per thread per tile
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int xrow = a.cin32 + 8;  // LDS pitch of the input tile
-  uint16_t* xs = smem;                        // [PIN16][xrow]
-  uint16_t* hid = xs + PIN16 * xrow;          // [PIN16][HROW]
-  uint16_t* dwo = hid + PIN16 * HROW;         // [64][HROW]
+  uint16_t* xs = smem;                          // [PIN16][xrow]
+  uint16_t* hidbuf = xs + PIN16 * xrow;         // 2 x [PIN16][HROW] (double buffered)
+  uint16_t* dwo = hidbuf + 2 * PIN16 * HROW;    // [64][HROW]
+  float* wds = reinterpret_cast<float*>(dwo + 64 * HROW);  // [9][hid] depthwise weights, fp32 (staged once)
+  float* bds = wds + 9 * a.hid;                             // [hid]    depthwise bias
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int li = lane & 15;
   const int kq = (lane >> 4) * 8;
-
-  // block -> (image, tile)
-  const int tiles = a.tiles_x * a.tiles_y;
-  const int b = blockIdx.x / tiles;
-  const int t = blockIdx.x % tiles;
-  const int ty = t / a.tiles_x, tx = t % a.tiles_x;
-  const int oy0 = ty * TO, ox0 = tx * TO;
-  const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
-
-  // ---- 1. stage the input halo tile (16-byte vectors; zero outside the image / K pad)
-  const uint16_t* xb = a.x + static_cast<int64_t>(b) * a.H * a.W * a.cin;
-  const int vec_per_px = a.cin32 / 8;
-  for (int v = tid; v < PIN16 * vec_per_px; v += 256) {
-    const int p = v / vec_per_px;
-    const int k = (v % vec_per_px) * 8;
-    bf16x8_t val = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-    if (p < PIN && k < a.cin) {
-      const int iy = iy0 + p / TI, ix = ix0 + p % TI;
-      if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
-        val = *reinterpret_cast<const bf16x8_t*>(xb + (static_cast<int64_t>(iy) * a.W + ix) * a.cin + k);
-    }
-    *reinterpret_cast<bf16x8_t*>(xs + p * xrow + k) = val;
-  }
-  __syncthreads();
-
-  f32x4_t acc[NOT];
-#pragma unroll
-  for (int i = 0; i < NOT; ++i) acc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
   const int ksteps = a.cin32 / 32;
-  for (int c0 = 0; c0 < a.hid; c0 += HC) {
-    // ---- 2a. expand (or copy, for t=1 blocks) into hid[px][0..32)
-    if (a.has_expand) {
-      constexpr int NB = PIN16 / 16;
-      for (int pair = wave; pair < 2 * NB; pair += 4) {
-        const int at = pair & 1, bt = pair >> 1;
-        f32x4_t e = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        const uint16_t* wrow = a.we + static_cast<int64_t>(c0 + at * 16 + li) * a.cin32 + kq;
-        const uint16_t* xrowp = xs + (bt * 16 + li) * xrow + kq;
-        for (int ks = 0; ks < ksteps; ++ks) {
-          const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(wrow + ks * 32);
-          const bf16x8_t bf = *reinterpret_cast<const bf16x8_t*>(xrowp + ks * 32);
-          e = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_mfma, af),
-                                                      __builtin_bit_cast(bf16x8_mfma, bf), e, 0, 0, 0);
-        }
-        // lane: hidden rows (lane>>4)*4+r of tile `at`, pixel bt*16+li
-        const int p = bt * 16 + li;
+  const int vec_per_px = a.cin32 / 8;
+  const int tiles_img = a.tiles_x * a.tiles_y;
+  const int total_tiles = tiles_img * a.B;
+  // persistent walk: this workgroup owns tiles [t_begin, t_end) (consecutive along x)
+  const int t_begin = blockIdx.x * a.tiles_per_wg;
+  const int t_end = min(total_tiles, t_begin + a.tiles_per_wg);
+
+  // expand operands of one chunk (registers): A fragments of both 16-row tiles + biases
+  bf16x8_t ea[2][KS_MAX];
+  float eb[2][4];
+  auto load_expand = [&](int c0) {
+#pragma unroll
+    for (int at = 0; at < 2; ++at) {
+      const uint16_t* wrow = a.we + static_cast<int64_t>(c0 + at * 16 + li) * a.cin32 + kq;
+#pragma unroll
+      for (int ks = 0; ks < KS_MAX; ++ks) ea[at][ks] = *reinterpret_cast<const bf16x8_t*>(wrow + ks * 32);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) eb[at][r] = a.be[c0 + at * 16 + (lane >> 4) * 4 + r];
+    }
+  };
+
+  // next tile's input vectors are fetched into registers while the current tile computes
+  bf16x8_t pf[NV];
+  auto fetch_tile = [&](int t) {
+    const int b = t / tiles_img, r = t % tiles_img;
+    const int iy0 = (r / a.tiles_x) * TO * S - 1, ix0 = (r % a.tiles_x) * TO * S - 1;
+    const uint16_t* xb = a.x + static_cast<int64_t>(b) * a.H * a.W * a.cin;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = tid + i * 256;
+      const int p = v / vec_per_px;
+      const int k = (v % vec_per_px) * 8;
+      bf16x8_t val = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      if (p < PIN && k < a.cin) {
         const int iy = iy0 + p / TI, ix = ix0 + p % TI;
-        const bool inside = p < PIN && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-        const int hc = at * 16 + (lane >> 4) * 4;
-        uint16_t o[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = inside ? f2bf(relu6(e[r] + a.be[c0 + hc + r])) : 0;
-        uint2 packed;
-        packed.x = static_cast<uint32_t>(o[0]) | (static_cast<uint32_t>(o[1]) << 16);
-        packed.y = static_cast<uint32_t>(o[2]) | (static_cast<uint32_t>(o[3]) << 16);
-        *reinterpret_cast<uint2*>(hid + p * HROW + hc) = packed;
+        if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
+          val = *reinterpret_cast<const bf16x8_t*>(xb + (static_cast<int64_t>(iy) * a.W + ix) * a.cin + k);
       }
-    } else {
-      for (int v = tid; v < PIN16 * (HC / 8); v += 256) {
-        const int p = v / (HC / 8), k = (v % (HC / 8)) * 8;
-        *reinterpret_cast<bf16x8_t*>(hid + p * HROW + k) = *reinterpret_cast<const bf16x8_t*>(xs + p * xrow + c0 + k);
-      }
+      pf[i] = val;
     }
-    __syncthreads();
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = tid + i * 256;
+      const int p = v / vec_per_px;
+      if (p < PIN16) *reinterpret_cast<bf16x8_t*>(xs + p * xrow + (v % vec_per_px) * 8) = pf[i];
+    }
+  };
 
-    // ---- 2b. depthwise 3x3 + bias + ReLU6: lane = 1 output pixel x 8 channels
-    {
-      const int q = tid >> 2;
-      const int g = (tid & 3) * 8;
-      const int oy = q / TO, ox = q % TO;
-      float d[8];
+  if (t_begin >= t_end) return;
+  if (a.has_expand) load_expand(0);
+  fetch_tile(t_begin);
+  for (int v = tid; v < 9 * a.hid / 8; v += 256)
+  {
+    const bf16x8_t w8 = *reinterpret_cast<const bf16x8_t*>(a.wd + v * 8);
 #pragma unroll
-      for (int r = 0; r < 8; ++r) d[r] = a.bd[c0 + g + r];
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          const int p = (oy * S + ky) * TI + (ox * S + kx);
-          const bf16x8_t hv = *reinterpret_cast<const bf16x8_t*>(hid + p * HROW + g);
-          const bf16x8_t wv = *reinterpret_cast<const bf16x8_t*>(a.wd + (ky * 3 + kx) * a.hid + c0 + g);
-#pragma unroll
-          for (int r = 0; r < 8; ++r)
-            d[r] += bf2f(static_cast<uint16_t>(hv[r])) * bf2f(static_cast<uint16_t>(wv[r]));
-        }
-      bf16x8_t o;
-#pragma unroll
-      for (int r = 0; r < 8; ++r) o[r] = static_cast<short>(f2bf(relu6(d[r])));
-      *reinterpret_cast<bf16x8_t*>(dwo + q * HROW + g) = o;
-    }
-    __syncthreads();
-
-    // ---- 2c. project: wave owns output pixels 16*wave .. +15
-    {
-      const bf16x8_t bf = *reinterpret_cast<const bf16x8_t*>(dwo + (wave * 16 + li) * HROW + kq);
-#pragma unroll
-      for (int ot = 0; ot < NOT; ++ot) {
-        const bf16x8_t af =
-            *reinterpret_cast<const bf16x8_t*>(a.wp + static_cast<int64_t>(ot * 16 + li) * a.hid + c0 + kq);
-        acc[ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_mfma, af),
-                                                          __builtin_bit_cast(bf16x8_mfma, bf), acc[ot], 0, 0, 0);
-      }
-    }
+    for (int r = 0; r < 8; ++r) wds[v * 8 + r] = bf2f(static_cast<uint16_t>(w8[r]));
   }
+  for (int v = tid; v < a.hid; v += 256) bds[v] = a.bd[v];
 
-  // ---- 3. epilogue: bias (+ residual from the LDS input tile) -> bf16
-  const int q = wave * 16 + li;
-  const int oy = q / TO, ox = q % TO;
-  const int gy = oy0 + oy, gx = ox0 + ox;
-  if (gy >= a.Ho || gx >= a.Wo) return;
-  uint16_t* yb = a.y + ((static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx) * a.cout;
+  // dw lane mapping == project mapping: wave w owns output pixels 16w..16w+15
+  const int q = tid >> 2;
+  const int g = (tid & 3) * 8;
+  const int qy = q / TO, qx = q % TO;
+
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    store_tile();
+    __syncthreads();
+    if (tile + 1 < t_end) fetch_tile(tile + 1);  // in flight during this tile's compute
+
+    const int b = tile / tiles_img, r = tile % tiles_img;
+    const int oy0 = (r / a.tiles_x) * TO, ox0 = (r % a.tiles_x) * TO;
+    const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
+
+    f32x4_t acc[NOT];
 #pragma unroll
-  for (int ot = 0; ot < NOT; ++ot) {
-    const int co = ot * 16 + (lane >> 4) * 4;
-    if (co >= a.cout) continue;
-    float v[4];
+    for (int i = 0; i < NOT; ++i) acc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    int buf = 0;
+    for (int c0 = 0; c0 < a.hid; c0 += HC, buf ^= 1) {
+      uint16_t* hid = hidbuf + buf * PIN16 * HROW;
+      // issue this chunk's project weight loads early (consumed after the barrier)
+      bf16x8_t pa[NOT];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = acc[ot][r] + a.bp[co + r];
-    if (a.residual) {  // stride 1, cin == cout: centre pixel of the halo tile
-      const uint16_t* rp = xs + ((oy + 1) * TI + (ox + 1)) * xrow + co;
+      for (int ot = 0; ot < NOT; ++ot)
+        pa[ot] = *reinterpret_cast<const bf16x8_t*>(a.wp + static_cast<int64_t>(ot * 16 + li) * a.hid + c0 + kq);
+
+      // ---- expand: wave w computes B tiles w, w+4, ... for both 16-channel A tiles
+      if (a.has_expand) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] += bf2f(rp[r]);
+        for (int it = 0; it < (NB + 3) / 4; ++it) {
+          const int bt = wave + 4 * it;
+          if (bt >= NB) break;
+          f32x4_t e0 = f32x4_t{0.f, 0.f, 0.f, 0.f}, e1 = e0;
+          const uint16_t* xrowp = xs + (bt * 16 + li) * xrow + kq;
+#pragma unroll
+          for (int ks = 0; ks < KS_MAX; ++ks) {
+            const bf16x8_mfma bfr =
+                __builtin_bit_cast(bf16x8_mfma, *reinterpret_cast<const bf16x8_t*>(xrowp + ks * 32));
+            e0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_mfma, ea[0][ks]), bfr, e0, 0, 0, 0);
+            e1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_mfma, ea[1][ks]), bfr, e1, 0, 0, 0);
+          }
+          const int p = bt * 16 + li;
+          const int iy = iy0 + p / TI, ix = ix0 + p % TI;
+          const bool inside = p < PIN && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+          const int hc = (lane >> 4) * 4;
+          uint2 p0 = make_uint2(0u, 0u), p1 = make_uint2(0u, 0u);
+          if (inside) {
+            p0.x = static_cast<uint32_t>(f2bf(relu6(e0[0] + eb[0][0]))) |
+                   (static_cast<uint32_t>(f2bf(relu6(e0[1] + eb[0][1]))) << 16);
+            p0.y = static_cast<uint32_t>(f2bf(relu6(e0[2] + eb[0][2]))) |
+                   (static_cast<uint32_t>(f2bf(relu6(e0[3] + eb[0][3]))) << 16);
+            p1.x = static_cast<uint32_t>(f2bf(relu6(e1[0] + eb[1][0]))) |
+                   (static_cast<uint32_t>(f2bf(relu6(e1[1] + eb[1][1]))) << 16);
+            p1.y = static_cast<uint32_t>(f2bf(relu6(e1[2] + eb[1][2]))) |
+                   (static_cast<uint32_t>(f2bf(relu6(e1[3] + eb[1][3]))) << 16);
+          }
+          *reinterpret_cast<uint2*>(hid + p * HROW + hc) = p0;
+          *reinterpret_cast<uint2*>(hid + p * HROW + 16 + hc) = p1;
+        }
+        // prefetch the next chunk's (or the next tile's first chunk's) expand operands
+        load_expand(c0 + HC < a.hid ? c0 + HC : 0);
+      } else {
+        for (int v = tid; v < PIN16 * (HC / 8); v += 256) {
+          const int p = v / (HC / 8), k = (v % (HC / 8)) * 8;
+          *reinterpret_cast<bf16x8_t*>(hid + p * HROW + k) =
+              *reinterpret_cast<const bf16x8_t*>(xs + p * xrow + c0 + k);
+        }
+      }
+      // one block barrier per chunk: hid is double buffered, dw/project are wave-local
+      __syncthreads();
+
+      // ---- depthwise 3x3 + bias + ReLU6 (lane = 1 output pixel x 8 channels)
+      {
+        // packed fp32 math: 2 channels per v_pk_fma_f32; bf16 -> f32 is a shift (low) / mask (high)
+        f32x2_t d[4];
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) d[rr] = *reinterpret_cast<const f32x2_t*>(bds + c0 + g + 2 * rr);
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) {
+            const int p = (qy * S + ky) * TI + (qx * S + kx);
+            const uint4 hv = *reinterpret_cast<const uint4*>(hid + p * HROW + g);
+            const float* wrow = wds + (ky * 3 + kx) * a.hid + c0 + g;
+            const f32x4_t w0 = *reinterpret_cast<const f32x4_t*>(wrow);
+            const f32x4_t w1 = *reinterpret_cast<const f32x4_t*>(wrow + 4);
+            const uint32_t hw[4] = {hv.x, hv.y, hv.z, hv.w};
+            const f32x2_t wp2[4] = {f32x2_t{w0[0], w0[1]}, f32x2_t{w0[2], w0[3]}, f32x2_t{w1[0], w1[1]},
+                                    f32x2_t{w1[2], w1[3]}};
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+              const f32x2_t h2 = f32x2_t{__uint_as_float(hw[rr] << 16), __uint_as_float(hw[rr] & 0xffff0000u)};
+              d[rr] = __builtin_elementwise_fma(h2, wp2[rr], d[rr]);
+            }
+          }
+        bf16x8_t o;
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr) o[rr] = static_cast<short>(f2bf(relu6(d[rr >> 1][rr & 1])));
+        *reinterpret_cast<bf16x8_t*>(dwo + q * HROW + g) = o;
+      }
+      // dwo rows of this wave were written by this wave only: a wave-level fence suffices
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+      // ---- project: D[out][px] += Wp[out][hid] . dw[px][hid]^T
+      {
+        const bf16x8_mfma bfr =
+            __builtin_bit_cast(bf16x8_mfma, *reinterpret_cast<const bf16x8_t*>(dwo + (wave * 16 + li) * HROW + kq));
+#pragma unroll
+        for (int ot = 0; ot < NOT; ++ot)
+          acc[ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_mfma, pa[ot]), bfr, acc[ot], 0,
+                                                            0, 0);
+      }
     }
-    uint2 o;
-    o.x = static_cast<uint32_t>(f2bf(v[0])) | (static_cast<uint32_t>(f2bf(v[1])) << 16);
-    o.y = static_cast<uint32_t>(f2bf(v[2])) | (static_cast<uint32_t>(f2bf(v[3])) << 16);
-    *reinterpret_cast<uint2*>(yb + co) = o;
+
+    // ---- epilogue: bias (+ residual from the LDS input tile) -> bf16
+    {
+      const int qo = wave * 16 + li;
+      const int oy = qo / TO, ox = qo % TO;
+      const int gy = oy0 + oy, gx = ox0 + ox;
+      if (gy < a.Ho && gx < a.Wo) {
+        uint16_t* yb = a.y + ((static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx) * a.cout;
+#pragma unroll
+        for (int ot = 0; ot < NOT; ++ot) {
+          const int co = ot * 16 + (lane >> 4) * 4;
+          if (co >= a.cout) continue;
+          float v[4];
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) v[rr] = acc[ot][rr] + a.bp[co + rr];
+          if (a.residual) {  // stride 1, cin == cout: centre pixel of the halo tile
+            const uint16_t* rp = xs + ((oy + 1) * TI + (ox + 1)) * xrow + co;
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) v[rr] += bf2f(rp[rr]);
+          }
+          uint2 o;
+          o.x = static_cast<uint32_t>(f2bf(v[0])) | (static_cast<uint32_t>(f2bf(v[1])) << 16);
+          o.y = static_cast<uint32_t>(f2bf(v[2])) | (static_cast<uint32_t>(f2bf(v[3])) << 16);
+          *reinterpret_cast<uint2*>(yb + co) = o;
+        }
+      }
+    }
+    __syncthreads();  // xs / hid are rewritten by the next tile
+  }
+}
+
+template <int S, int NOT, int KS>
+bool launch_one(const IrBlockArgs& a, size_t lds, dim3 grid, hipStream_t s) {
+  // dynamic LDS above 64 KiB must be opted into once per instantiation (a workgroup may use all 160 KiB)
+  static const bool attr_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&ir_block_kernel<S, NOT, KS>),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                  static_cast<int>(kLdsLimit)) == hipSuccess;
+  if (!attr_ok && lds > 64 * 1024) return false;
+  hipLaunchKernelGGL((ir_block_kernel<S, NOT, KS>), grid, dim3(256), lds, s, a);
+  return true;
+}
+
+template <int S, int NOT>
+bool launch_ks(const IrBlockArgs& a, size_t lds, dim3 grid, hipStream_t s) {
+  switch (a.cin32 / 32) {
+    case 1: return launch_one<S, NOT, 1>(a, lds, grid, s);
+    case 2: return launch_one<S, NOT, 2>(a, lds, grid, s);
+    case 3: return launch_one<S, NOT, 3>(a, lds, grid, s);
+    case 5: return launch_one<S, NOT, 5>(a, lds, grid, s);
+    default: return false;
   }
 }
 
 template <int S>
 bool launch_s(const IrBlockArgs& a, int n_ot, size_t lds, dim3 grid, hipStream_t s) {
-#define NNSX_IR_CASE(N)                                                                         \
-  case N:                                                                                       \
-    hipLaunchKernelGGL((ir_block_kernel<S, N>), grid, dim3(256), lds, s, a);                    \
-    return true;
   switch (n_ot) {
-    NNSX_IR_CASE(1)
-    NNSX_IR_CASE(2)
-    NNSX_IR_CASE(4)
-    NNSX_IR_CASE(6)
-    NNSX_IR_CASE(8)
-    NNSX_IR_CASE(10)
-    NNSX_IR_CASE(12)
-    NNSX_IR_CASE(16)
-    NNSX_IR_CASE(20)
-    default:
-      return false;
+    case 1: return launch_ks<S, 1>(a, lds, grid, s);
+    case 2: return launch_ks<S, 2>(a, lds, grid, s);
+    case 4: return launch_ks<S, 4>(a, lds, grid, s);
+    case 6: return launch_ks<S, 6>(a, lds, grid, s);
+    case 10: return launch_ks<S, 10>(a, lds, grid, s);
+    case 20: return launch_ks<S, 20>(a, lds, grid, s);
+    default: return false;
   }
-#undef NNSX_IR_CASE
 }
 
 }  // namespace
 
 size_t ir_block_lds_bytes(int stride, int cin32) {
   const int pin16 = tile_in_px16(stride);
-  return sizeof(uint16_t) * (static_cast<size_t>(pin16) * (cin32 + 8) + static_cast<size_t>(pin16) * HROW + 64 * HROW);
+  return sizeof(uint16_t) * (static_cast<size_t>(pin16) * (cin32 + 8) + 2 * static_cast<size_t>(pin16) * HROW + 64 * HROW);
+}
+
+size_t ir_block_lds_total(int stride, int cin32, int hid) {
+  return ir_block_lds_bytes(stride, cin32) + sizeof(float) * 10 * static_cast<size_t>(hid);
 }
 
 bool ir_block_supported(int stride, int cin, int hid, int cout) {
   if (stride != 1 && stride != 2) return false;
-  if (cin % 8 || cout % 8 || hid % HC) return false;
+  if (cin % 8 || cout % 8 || hid % HC || cin > 160) return false;
   const int n_ot = (cout + 15) / 16;
-  if (n_ot > 20 || (n_ot != 1 && n_ot != 2 && n_ot % 2)) return false;
-  return ir_block_lds_bytes(stride, (cin + 31) / 32 * 32) <= 64 * 1024;
+  if (n_ot != 1 && n_ot != 2 && n_ot != 4 && n_ot != 6 && n_ot != 10 && n_ot != 20) return false;
+  const int ks = (cin + 31) / 32;
+  if (ks != 1 && ks != 2 && ks != 3 && ks != 5) return false;
+  return ir_block_lds_total(stride, (cin + 31) / 32 * 32, hid) <= kLdsLimit;
 }
 
 bool ir_block(const IrBlockArgs& args, hipStream_t s) {
@@ -243,8 +348,14 @@ bool ir_block(const IrBlockArgs& args, hipStream_t s) {
   a.tiles_x = (a.Wo + TO - 1) / TO;
   if (!ir_block_supported(a.stride, a.cin, a.hid, a.cout)) return false;
   const int n_ot = (a.cout + 15) / 16;
-  const size_t lds = ir_block_lds_bytes(a.stride, a.cin32);
-  dim3 grid(static_cast<unsigned>(a.tiles_x * a.tiles_y * a.B));
+  const size_t lds = ir_block_lds_total(a.stride, a.cin32, a.hid);
+  // persistent grid: enough workgroups for every CU to hold several (LDS-limited), each
+  // walking a run of consecutive tiles so the next tile's input loads overlap compute
+  const int total_tiles = a.tiles_x * a.tiles_y * a.B;
+  const int per_cu = std::max<int>(1, std::min<int>(8, static_cast<int>(kLdsLimit / lds)));
+  const int max_wgs = 256 * per_cu * 2;
+  a.tiles_per_wg = std::max(1, (total_tiles + max_wgs - 1) / max_wgs);
+  dim3 grid(static_cast<unsigned>((total_tiles + a.tiles_per_wg - 1) / a.tiles_per_wg));
   return a.stride == 1 ? launch_s<1>(a, n_ot, lds, grid, s) : launch_s<2>(a, n_ot, lds, grid, s);
 }
 

@@ -37,7 +37,7 @@ struct IrBlockArgs {
   int B = 0, H = 0, W = 0, cin = 0, hid = 0, cout = 0, stride = 1;
   int has_expand = 1, residual = 0;
   // derived by ir_block()
-  int cin32 = 0, Ho = 0, Wo = 0, tiles_x = 0, tiles_y = 0;
+  int cin32 = 0, Ho = 0, Wo = 0, tiles_x = 0, tiles_y = 0, tiles_per_wg = 1;
 };
 bool ir_block_supported(int stride, int cin, int hid, int cout);
 size_t ir_block_lds_bytes(int stride, int cin32);

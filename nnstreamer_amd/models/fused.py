@@ -115,8 +115,10 @@ class Block(nn.Module):
         self.register_buffer("ir_wd", wd)
         self.register_buffer("ir_bd", bd)
         self.register_buffer("ir_wp", wp)
+        # measured on MI355X (scripts/bench_ir.py, batch 256): the fused kernel wins on every
+        # MobileNetV2 block except the 7x7 160->960->320 one (too few tiles, 20 output tiles/lane)
         self.use_ir = (bool(torch.ops.nnsx.ir_supported(int(ir.stride), cin, hp, self.cout)) and FUSE_IR
-                       and (self.has_expand or hid == hp))
+                       and (self.has_expand or hid == hp) and self.cout < 320)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.use_ir and self.dw.dilation == 1:
