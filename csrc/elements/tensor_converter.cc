@@ -14,6 +14,7 @@
 #include "core/log.h"
 #include "elements/elements.h"
 #include "elements/tensor_common.h"
+#include "kernels/kernels.h"
 #include "runtime/pipeline.h"
 #include "runtime/plugin_api.h"
 #include "runtime/video.h"
@@ -363,6 +364,26 @@ class TensorConverter : public Element {
     }
     out = dev >= 0 ? Memory::alloc_device(size, dev, s) : Memory::alloc_host(size);
     size_t done = 0;
+    if (dev >= 0 && gather_eligible(size)) {
+      // one gather launch per <=128 pieces instead of one hipMemcpyAsync per frame
+      kernels::GatherArgs g;
+      auto flush = [&]() {
+        kernels::gather_copy(g, out->data(), s);
+        g.n = 0;
+      };
+      while (done < size) {
+        Piece& p = adapter_.front();
+        size_t n = std::min(size - done, p.mem->size() - p.off);
+        if (p.mem->on_device()) p.mem->wait_ready(s);
+        g.seg[g.n++] = kernels::GatherSeg{static_cast<const char*>(p.mem->data()) + p.off, done, n};
+        p.mem->record_use(s, dev);
+        if (g.n == kernels::kGatherMax) flush();
+        done += n;
+        p.off += n;
+        if (p.off == p.mem->size()) adapter_.pop_front();
+      }
+      flush();
+    }
     while (done < size) {
       Piece& p = adapter_.front();
       size_t n = std::min(size - done, p.mem->size() - p.off);
@@ -383,6 +404,17 @@ class TensorConverter : public Element {
     if (dev >= 0) out->mark_ready(s);
     avail_ -= size;
     return out;
+  }
+
+  // every piece that feeds the next `size` bytes is device-readable in place (pinned host or HBM)
+  bool gather_eligible(size_t size) const {
+    size_t seen = 0;
+    for (const Piece& p : adapter_) {
+      if (p.mem->place() == MemPlace::HOST) return false;
+      seen += p.mem->size() - p.off;
+      if (seen >= size) return true;
+    }
+    return false;
   }
 
   FlowReturn push_out(BufferPtr b) {

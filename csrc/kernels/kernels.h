@@ -50,6 +50,22 @@ size_t stand_workspace_bytes(uint32_t channels);
 void stand(const void* in, DType in_t, void* out, DType out_t, uint64_t n, uint32_t channels, int mode,
            bool per_channel, void* ws, hipStream_t s);
 
+// -------------------------------------------------------------------- copy ----
+// One-launch gather of many host-pinned / device segments into one device block
+// (tensor_converter frames-per-tensor batching): replaces a hipMemcpyAsync per
+// frame.  Pinned host memory is read in place over the bus (zero copy).
+struct GatherSeg {
+  const void* src;
+  uint64_t dst_off;
+  uint64_t bytes;
+};
+constexpr int kGatherMax = 128;  // segments per launch (kernel-argument budget)
+struct GatherArgs {
+  int n = 0;
+  GatherSeg seg[kGatherMax];
+};
+void gather_copy(const GatherArgs& g, void* dst, hipStream_t s);
+
 // ------------------------------------------------------------------ decode ----
 // Global argmax over n elements (first max wins).  out_index: int32 on device.
 void argmax(const void* in, DType t, uint64_t n, int32_t* out_index, hipStream_t s);

@@ -378,5 +378,44 @@ void stand(const void* in, DType in_t, void* out, DType out_t, uint64_t n, uint3
 #undef NNSX_IN
 }
 
+// ----------------------------------------------------------------- gather ----
+namespace {
+
+__global__ void __launch_bounds__(256) gather_kernel(GatherArgs g, char* __restrict__ dst) {
+  const GatherSeg sg = g.seg[blockIdx.y];
+  char* d = dst + sg.dst_off;
+  const char* src = static_cast<const char*>(sg.src);
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(d) | sg.bytes) & 15) == 0) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    uint4* d4 = reinterpret_cast<uint4*>(d);
+    const uint64_t n = sg.bytes / 16;
+    // 4 independent 16-B loads in flight per lane (host reads cross the bus)
+    for (uint64_t i = t0; i < n; i += 4 * stride) {
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (i + u * stride < n) v[u] = s4[i + u * stride];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (i + u * stride < n) d4[i + u * stride] = v[u];
+    }
+  } else {
+    for (uint64_t i = t0; i < sg.bytes; i += stride) d[i] = src[i];
+  }
+}
+
+}  // namespace
+
+void gather_copy(const GatherArgs& g, void* dst, hipStream_t s) {
+  if (g.n <= 0) return;
+  uint64_t maxb = 0;
+  for (int i = 0; i < g.n; ++i) maxb = std::max<uint64_t>(maxb, g.seg[i].bytes);
+  // ~4 16-B vectors per lane per segment block
+  unsigned bx = static_cast<unsigned>(std::min<uint64_t>(64, std::max<uint64_t>(1, (maxb / 16 + 1023) / 1024)));
+  hipLaunchKernelGGL(gather_kernel, dim3(bx, static_cast<unsigned>(g.n)), dim3(256), 0, s, g, static_cast<char*>(dst));
+}
+
 }  // namespace kernels
 }  // namespace nnsx

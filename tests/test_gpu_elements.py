@@ -165,3 +165,15 @@ def test_pose_device_matches_host(nns):
         p.stop()
         res[dev] = out
     assert len(res[0]) == B and res[0] == res[-1]
+
+
+@pytest.mark.parametrize("w,h,n", [(224, 224, 6), (5, 3, 7), (64, 48, 130)])
+def test_converter_batched_gather_matches_host(nns, w, h, n):
+    desc = (f"videotestsrc num-buffers={2 * n} pattern=snow pool-size=5 ! video/x-raw,format=RGB,width={w},height={h},"
+            f"framerate=30/1 ! tensor_converter frames-per-tensor={n} device={{dev}} ! tensor_sink name=sink")
+    collect = lambda b: (b.memory(0).on_device, b.memory(0).bytes())
+    cpu, gpu = _both(nns, desc, collect)
+    assert len(cpu) == len(gpu) == 2
+    assert all(d for d, _ in gpu)
+    for (_, a), (_, b) in zip(cpu, gpu):
+        assert a == b
