@@ -122,8 +122,13 @@ def main():
     frames = total * B
     graph = "true" if (use_gpu and not a.no_graph) else "false"
     accel = "true:gpu" if use_gpu else "false"
+    # The source cycles through a ring of distinct pre-rendered frames (a camera ring
+    # buffer).  The ring is sized to 512 MiB, twice the MI355X's 256 MiB last-level
+    # cache, so every batch's H2D upload really crosses the host link.
+    frame_bytes = S * S * 3
+    pool = max(64, -(-512 * 2**20 // frame_bytes)) if use_gpu else 16
     desc = (
-        f"videotestsrc num-buffers={frames} pattern=snow pool-size=16 "
+        f"videotestsrc num-buffers={frames} pattern=snow pool-size={pool} "
         f"! video/x-raw,format=RGB,width={S},height={S},framerate=0/1 "
         f"! tensor_converter frames-per-tensor={B} device={dev} "
         f"! tensor_transform mode=arithmetic option={cfg['norm']} "

@@ -654,6 +654,13 @@ class VideoTestSrc : public BaseSrc {
     uint8_t* p = static_cast<uint8_t*>(m->data());
     std::memset(p, 0, info_.size);
     const std::string& f = info_.format;
+    if (f == "RGB" && info_.packed()) {  // fast path (benchmarks render large frame rings)
+      for (int y = 0; y < info_.height; ++y) {
+        uint8_t* row = p + y * info_.stride[0];
+        for (int x = 0; x < info_.width; ++x) color_of(x, y, frame, row + 3 * x);
+      }
+      return m;
+    }
     for (int y = 0; y < info_.height; ++y) {
       for (int x = 0; x < info_.width; ++x) {
         uint8_t c[3];
