@@ -18,6 +18,9 @@ void dw3x3(const void* x, const void* w, const float* bias, void* y, int B, int 
            int act, hipStream_t s);
 // 3x3/2 stem conv 3 -> 32 from an f32 NHWC frame; w f32 [3][3][3][32]
 void stem3x3(const float* x, const float* w, const float* bias, void* y, int B, int H, int W, int act, hipStream_t s);
+// same from the raw uint8 RGB frame, normalised in-kernel as (x + add) / div
+void stem3x3_u8(const uint8_t* x, const float* w, const float* bias, void* y, int B, int H, int W, int act, float add,
+                float div, hipStream_t s);
 // mean over HW: x [B][HW][C] -> y [B][C] (bf16)
 void avgpool(const void* x, void* y, int B, int HW, int C, hipStream_t s);
 

@@ -186,13 +186,19 @@ __global__ void __launch_bounds__(256) dw3x3_kernel(const uint16_t* __restrict__
 
 // --------------------------------------------------------------------- stem ----
 // x: f32 [B][H][W][3]; w: f32 [3][3][3][32] (ky,kx,ci,co); y: bf16 [B][Ho][Wo][32]
-__global__ void __launch_bounds__(256) stem_kernel(const float* __restrict__ x, const float* __restrict__ w,
+// T = float: the normalised frame; T = uint8_t: the raw RGB frame, normalised on
+// the fly through a 256-entry LUT lut[u] = (u + add) / div (bit-identical to the
+// tensor_transform arithmetic it replaces, padding stays 0 in the normalised domain)
+template <typename T>
+__global__ void __launch_bounds__(256) stem_kernel(const T* __restrict__ x, const float* __restrict__ w,
                                                    const float* __restrict__ bias, uint16_t* __restrict__ y, int B,
-                                                   int H, int W, int Ho, int Wo, int act) {
+                                                   int H, int W, int Ho, int Wo, int act, float add, float div) {
   __shared__ float sw[27 * 32];
   __shared__ float sb[32];
+  __shared__ float lut[256];
   for (int i = threadIdx.x; i < 27 * 32; i += blockDim.x) sw[i] = w[i];
   if (threadIdx.x < 32) sb[threadIdx.x] = bias[threadIdx.x];
+  if (sizeof(T) == 1) lut[threadIdx.x] = (static_cast<float>(threadIdx.x) + add) / div;
   __syncthreads();
   const int64_t total = static_cast<int64_t>(B) * Ho * Wo * 4;
   for (int64_t t = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; t < total;
@@ -214,8 +220,17 @@ __global__ void __launch_bounds__(256) stem_kernel(const float* __restrict__ x, 
       for (int kx = 0; kx < 3; ++kx) {
         const int ix = ox * 2 - 1 + kx;
         if (ix < 0 || ix >= W) continue;
-        const float* px = x + ((static_cast<int64_t>(b) * H + iy) * W + ix) * 3;
-        const float in0 = px[0], in1 = px[1], in2 = px[2];
+        const T* px = x + ((static_cast<int64_t>(b) * H + iy) * W + ix) * 3;
+        float in0, in1, in2;
+        if (sizeof(T) == 1) {
+          in0 = lut[static_cast<int>(px[0])];
+          in1 = lut[static_cast<int>(px[1])];
+          in2 = lut[static_cast<int>(px[2])];
+        } else {
+          in0 = static_cast<float>(px[0]);
+          in1 = static_cast<float>(px[1]);
+          in2 = static_cast<float>(px[2]);
+        }
         const float* wk = sw + ((ky * 3 + kx) * 3) * 32 + og * 8;
 #pragma unroll
         for (int q = 0; q < 8; ++q) acc[q] += in0 * wk[q] + in1 * wk[32 + q] + in2 * wk[64 + q];
@@ -290,8 +305,16 @@ void dw3x3(const void* x, const void* w, const float* bias, void* y, int B, int 
 void stem3x3(const float* x, const float* w, const float* bias, void* y, int B, int H, int W, int act, hipStream_t s) {
   int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
   int64_t work = static_cast<int64_t>(B) * Ho * Wo * 4;
-  hipLaunchKernelGGL(stem_kernel, dim3(grid_cap(work)), dim3(256), 0, s, x, w, bias, static_cast<uint16_t*>(y), B, H,
-                     W, Ho, Wo, act);
+  hipLaunchKernelGGL(stem_kernel<float>, dim3(grid_cap(work)), dim3(256), 0, s, x, w, bias, static_cast<uint16_t*>(y),
+                     B, H, W, Ho, Wo, act, 0.f, 1.f);
+}
+
+void stem3x3_u8(const uint8_t* x, const float* w, const float* bias, void* y, int B, int H, int W, int act, float add,
+                float div, hipStream_t s) {
+  int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  int64_t work = static_cast<int64_t>(B) * Ho * Wo * 4;
+  hipLaunchKernelGGL(stem_kernel<uint8_t>, dim3(grid_cap(work)), dim3(256), 0, s, x, w, bias,
+                     static_cast<uint16_t*>(y), B, H, W, Ho, Wo, act, add, div);
 }
 
 void avgpool(const void* x, void* y, int B, int HW, int C, hipStream_t s) {

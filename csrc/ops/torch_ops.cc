@@ -97,6 +97,26 @@ at::Tensor stem_conv_cpu(const at::Tensor& x, const at::Tensor& w, const at::Ten
   return act_ref(v, act).permute({0, 2, 3, 1}).contiguous().to(at::kBFloat16);
 }
 
+at::Tensor stem_conv_u8_cuda(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int64_t act, double add,
+                             double div) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kByte && x.is_contiguous() && x.dim() == 4 && x.size(3) == 3,
+              "stem_conv_u8: x [B,H,W,3] uint8");
+  TORCH_CHECK(w.numel() == 27 * 32 && w.scalar_type() == at::kFloat, "stem_conv_u8: w [3,3,3,32] f32");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2);
+  const int64_t Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  at::Tensor y = at::empty({B, Ho, Wo, 32}, x.options().dtype(at::kBFloat16));
+  nnsx::kernels::stem3x3_u8(x.data_ptr<uint8_t>(), w.data_ptr<float>(), bias.data_ptr<float>(), y.data_ptr(),
+                            static_cast<int>(B), static_cast<int>(H), static_cast<int>(W), static_cast<int>(act),
+                            static_cast<float>(add), static_cast<float>(div), cur_stream());
+  return y;
+}
+
+at::Tensor stem_conv_u8_cpu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int64_t act, double add,
+                            double div) {
+  at::Tensor xf = (x.to(at::kFloat) + static_cast<float>(add)) / static_cast<float>(div);
+  return stem_conv_cpu(xf, w, bias, act);
+}
+
 // ------------------------------------------------------------ avgpool ----
 at::Tensor avgpool_cuda(const at::Tensor& x) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() == 4, "avgpool: x [B,H,W,C] bf16");
@@ -170,6 +190,7 @@ TORCH_LIBRARY(nnsx, m) {
   m.def("pw_conv(Tensor x, Tensor wt, Tensor bias, Tensor? res, int N, int act, bool out_f32) -> Tensor");
   m.def("dw_conv(Tensor x, Tensor w, Tensor bias, int stride, int act, int dilation=1) -> Tensor");
   m.def("stem_conv(Tensor x, Tensor w, Tensor bias, int act) -> Tensor");
+  m.def("stem_conv_u8(Tensor x, Tensor w, Tensor bias, int act, float add, float div) -> Tensor");
   m.def("avgpool(Tensor x) -> Tensor");
   m.def("ir_block(Tensor x, Tensor we, Tensor be, Tensor wd, Tensor bd, Tensor wp, Tensor bp, int stride, int cout, "
         "bool has_expand, bool residual) -> Tensor");
@@ -180,6 +201,7 @@ TORCH_LIBRARY_IMPL(nnsx, CUDA, m) {
   m.impl("pw_conv", pw_conv_cuda);
   m.impl("dw_conv", dw_conv_cuda);
   m.impl("stem_conv", stem_conv_cuda);
+  m.impl("stem_conv_u8", stem_conv_u8_cuda);
   m.impl("avgpool", avgpool_cuda);
   m.impl("ir_block", ir_block_cuda);
 }
@@ -188,6 +210,7 @@ TORCH_LIBRARY_IMPL(nnsx, CPU, m) {
   m.impl("pw_conv", pw_conv_cpu);
   m.impl("dw_conv", dw_conv_cpu);
   m.impl("stem_conv", stem_conv_cpu);
+  m.impl("stem_conv_u8", stem_conv_u8_cpu);
   m.impl("avgpool", avgpool_cpu);
   m.impl("ir_block", ir_block_cpu);
 }

@@ -45,6 +45,15 @@ def _pw_weight(w: torch.Tensor):
     return out.to(torch.bfloat16)
 
 
+def stem(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, in_add: float, in_div: float) -> torch.Tensor:
+    """3x3/2 stem from either the raw uint8 frame (normalised in-kernel as
+    (x + in_add) / in_div, i.e. the pipeline's tensor_transform arithmetic fused
+    into the first conv) or an already-normalised float32 frame."""
+    if x.dtype == torch.uint8:
+        return torch.ops.nnsx.stem_conv_u8(x.contiguous(), w, b, 1, in_add, in_div)
+    return torch.ops.nnsx.stem_conv(x.contiguous().float(), w, b, 1)
+
+
 class PW(nn.Module):
     def __init__(self, w: torch.Tensor, b: torch.Tensor, act: int, out_f32: bool = False):
         super().__init__()
@@ -146,6 +155,7 @@ class FusedMobileNetV2(nn.Module):
         w, b = _fold(stem[0], stem[1])  # [32, 3, 3, 3]
         self.register_buffer("stem_w", w.permute(2, 3, 1, 0).contiguous())  # [ky, kx, ci, co]
         self.register_buffer("stem_b", b.contiguous())
+        self.in_add, self.in_div = -127.5, 127.5
         self.blocks = nn.ModuleList([Block(ir) for ir in m.features[1:-1]])
         head: ConvBNReLU = m.features[-1]
         self.head = PW(*_fold(head[0], head[1]), act=1)
@@ -154,7 +164,7 @@ class FusedMobileNetV2(nn.Module):
         return self
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        h = torch.ops.nnsx.stem_conv(x.contiguous(), self.stem_w, self.stem_b, 1)
+        h = stem(x, self.stem_w, self.stem_b, self.in_add, self.in_div)
         for blk in self.blocks:
             h = blk(h)
         h = self.head(h)

@@ -20,7 +20,7 @@ from typing import List, Tuple
 import torch
 import torch.nn as nn
 
-from .fused import DW, PW, Block, _fold
+from .fused import DW, PW, Block, _fold, stem
 from .mobilenet_v2 import ConvBNReLU, MobileNetV2
 
 ANCHORS = (3, 6, 6, 6, 6, 6)
@@ -165,6 +165,7 @@ class FusedSSDLite(nn.Module):
         w, b = _fold(stem[0], stem[1])
         self.register_buffer("stem_w", w.permute(2, 3, 1, 0).contiguous())
         self.register_buffer("stem_b", b.contiguous())
+        self.in_add, self.in_div = -127.5, 127.5  # uint8 input: the pipeline normalisation, fused
         self.blocks = nn.ModuleList([Block(ir) for ir in m.features[1:-1]])  # features[1..17]
         head: ConvBNReLU = m.features[-1]
         self.head = PW(*_fold(head[0], head[1]), act=1)
@@ -175,7 +176,7 @@ class FusedSSDLite(nn.Module):
         return self
 
     def forward(self, x: torch.Tensor):
-        h = torch.ops.nnsx.stem_conv(x.contiguous(), self.stem_w, self.stem_b, 1)
+        h = stem(x, self.stem_w, self.stem_b, self.in_add, self.in_div)
         feats: List[torch.Tensor] = []
         for i, blk in enumerate(self.blocks):
             if i == self.feat_block:

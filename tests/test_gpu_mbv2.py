@@ -154,3 +154,14 @@ def test_fused_model_ir_vs_unfused(nns):
         y0 = m(x)
     cos = F.cosine_similarity(y.flatten(), y0.flatten(), 0).item()
     assert cos > 0.999, cos
+
+
+def test_stem_u8_matches_float_path(nns):
+    torch.manual_seed(1)
+    x = torch.randint(0, 256, (3, 224, 224, 3), device="cuda", dtype=torch.uint8)
+    w = torch.randn(3, 3, 3, 32, device="cuda") * 0.2
+    b = torch.randn(32, device="cuda") * 0.1
+    y8 = torch.ops.nnsx.stem_conv_u8(x, w, b, 1, -127.5, 127.5)
+    xf = (x.float() + -127.5) / 127.5
+    yf = torch.ops.nnsx.stem_conv(xf.contiguous(), w, b, 1)
+    assert torch.equal(y8, yf)
