@@ -3,6 +3,5 @@
 #include "elements/elements.h"
 
 namespace nnsx {
-void register_comm_elements() {}
 void register_serial_decoders() {}
 }  // namespace nnsx
