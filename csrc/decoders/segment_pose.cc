@@ -14,8 +14,9 @@
 // input W:H, option3 keypoint/connection file, option4 heatmap-only |
 // heatmap-offset; per-keypoint heatmap argmax (first maximum, floor
 // FLT_MIN, :780-800), offset refinement, Bresenham skeleton with end dots
-// and labels.  The heatmap scan runs on the GPU for device input; drawing
-// (a few dozen line segments) runs on the host.
+// and labels.  For HBM-resident float input the whole decode runs on the GPU
+// (argmax kernel, then one raster kernel per batch of frames); otherwise on
+// the host.
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
@@ -260,20 +261,43 @@ class PoseEstimation : public DecoderInstance {
     }
     // per keypoint: (grid x, grid y, score)
     std::vector<float> kp(static_cast<size_t>(batch) * K * 3);
-    if (ctx.device >= 0 && hi.type == DType::FLOAT32) {
-      const float* x = static_cast<const float*>(in[0]->map_device(ctx.device, ctx.stream));
-      if (!dev_kp_ || dev_kp_->size() < kp.size() * sizeof(float) || dev_kp_->device() != ctx.device) {
-        dev_kp_ = Memory::alloc_device(kp.size() * sizeof(float), ctx.device, ctx.stream);
-        host_kp_ = Memory::alloc_pinned(kp.size() * sizeof(float));
-      }
+    const bool offsets_ok = mode_ == 0 || (config.info.num_tensors > 1 && config.info.at(1).type == DType::FLOAT32);
+    if (ctx.device >= 0 && hi.type == DType::FLOAT32 && offsets_ok && K <= 64) {
+      // all on the GPU: heatmap argmax, offset refinement and skeleton raster (no host sync)
+      const int dev = ctx.device;
+      hipStream_t s = ctx.stream;
+      const float* x = static_cast<const float*>(in[0]->map_device(dev, s));
+      if (!dev_kp_ || dev_kp_->size() < kp.size() * sizeof(float) || dev_kp_->device() != dev)
+        dev_kp_ = Memory::alloc_device(kp.size() * sizeof(float), dev, s);
+      ensure_device_meta(dev, s);
       kernels::pose_heatmap_argmax(x, K, gw, gh, static_cast<int>(batch), mode_ == 1,
-                                   static_cast<float*>(dev_kp_->data()), ctx.stream);
-      hip::check(hipMemcpyAsync(host_kp_->data(), dev_kp_->data(), kp.size() * sizeof(float), hipMemcpyDeviceToHost,
-                                ctx.stream),
-                 "pose D2H");
-      hip::check(hipStreamSynchronize(ctx.stream), "pose sync");
-      std::memcpy(kp.data(), host_kp_->data(), kp.size() * sizeof(float));
-    } else {
+                                   static_cast<float*>(dev_kp_->data()), s);
+      const size_t fsize = static_cast<size_t>(width_) * height_ * 4;
+      MemoryPtr frames = Memory::alloc_device(fsize * batch, dev, s);
+      hip::check(hipMemsetAsync(frames->data(), 0, fsize * batch, s), "pose clear");
+      kernels::PoseDrawArgs da;
+      da.kp = static_cast<const float*>(dev_kp_->data());
+      da.offsets = mode_ == 1 ? static_cast<const float*>(in[1]->map_device(dev, s)) : nullptr;
+      da.keypoints = K;
+      da.gw = gw;
+      da.gh = gh;
+      da.i_w = static_cast<int>(i_width_);
+      da.i_h = static_cast<int>(i_height_);
+      da.W = static_cast<int>(width_);
+      da.H = static_cast<int>(height_);
+      da.edges = static_cast<const int*>(dev_edges_->data());
+      da.n_edges = n_edges_;
+      da.labels = static_cast<const char*>(dev_labels_->data());
+      da.label_offs = static_cast<const int*>(dev_label_offs_->data());
+      da.frames = static_cast<uint32_t*>(frames->data());
+      kernels::pose_draw(da, static_cast<int>(batch), s);
+      frames->mark_ready(s);
+      dev_kp_->record_use(s, dev);
+      ctx.out_frames = batch;
+      for (unsigned b = 0; b < batch; ++b) out->mems.push_back(Memory::view(frames, b * fsize, fsize));
+      return FlowReturn::OK;
+    }
+    {
       const void* x = in[0]->map_host();
       for (unsigned b = 0; b < batch; ++b)
         for (int k = 0; k < K; ++k) {
@@ -361,7 +385,37 @@ class PoseEstimation : public DecoderInstance {
     }
     if (m.empty()) return false;
     meta_ = m;
+    dev_edges_.reset();
     return true;
+  }
+
+  void ensure_device_meta(int dev, hipStream_t s) {
+    if (dev_edges_ && dev_edges_->device() == dev) return;
+    std::vector<int> edges;
+    const int K = static_cast<int>(meta_.size());
+    for (int i = 0; i < K; ++i)
+      for (int k : meta_[static_cast<size_t>(i)].connections)
+        if (k >= 0 && k < K && k >= i) {
+          edges.push_back(i);
+          edges.push_back(k);
+        }
+    n_edges_ = static_cast<int>(edges.size() / 2);
+    std::string blob;
+    std::vector<int> offs;
+    for (auto& m : meta_) {
+      offs.push_back(static_cast<int>(blob.size()));
+      blob += m.label;
+      blob.push_back('\0');
+    }
+    if (edges.empty()) edges.push_back(0);
+    dev_edges_ = Memory::alloc_device(edges.size() * sizeof(int), dev, s);
+    dev_labels_ = Memory::alloc_device(blob.size(), dev, s);
+    dev_label_offs_ = Memory::alloc_device(offs.size() * sizeof(int), dev, s);
+    hip::check(hipMemcpyAsync(dev_edges_->data(), edges.data(), edges.size() * sizeof(int), hipMemcpyHostToDevice, s), "pose edges");
+    hip::check(hipMemcpyAsync(dev_labels_->data(), blob.data(), blob.size(), hipMemcpyHostToDevice, s), "pose labels");
+    hip::check(hipMemcpyAsync(dev_label_offs_->data(), offs.data(), offs.size() * sizeof(int), hipMemcpyHostToDevice, s),
+               "pose label offsets");
+    hip::check(hipStreamSynchronize(s), "pose meta");
   }
 
   void set_pixel(uint32_t* f, int x, int y) const {
@@ -442,7 +496,8 @@ class PoseEstimation : public DecoderInstance {
   unsigned width_ = 0, height_ = 0, i_width_ = 0, i_height_ = 0;
   int mode_ = 0;
   std::vector<PoseMeta> meta_;
-  MemoryPtr dev_kp_, host_kp_;
+  MemoryPtr dev_kp_, host_kp_, dev_edges_, dev_labels_, dev_label_offs_;
+  int n_edges_ = 0;
 };
 
 class PosePlugin : public DecoderSubplugin {

@@ -23,5 +23,19 @@ void segment_depth_gray(const float* in, uint64_t pixels_per_frame, int batch, u
 void pose_heatmap_argmax(const float* heat, int keypoints, int grid_w, int grid_h, int batch, bool sigmoid,
                          float* out, hipStream_t s);
 
+// pose: keypoint positions (+ offsets) and skeleton / dot / label raster into
+// zeroed RGBA frames [B][H][W]; edges = (i, k) pairs with k > i; <= 64 keypoints
+struct PoseDrawArgs {
+  const float* kp = nullptr;       // [B][K][3] from pose_heatmap_argmax
+  const float* offsets = nullptr;  // heatmap-offset mode: [B][gh][gw][2K], else null
+  int keypoints = 0, gw = 0, gh = 0, i_w = 0, i_h = 0, W = 0, H = 0;
+  const int* edges = nullptr;
+  int n_edges = 0;
+  const char* labels = nullptr;
+  const int* label_offs = nullptr;
+  uint32_t* frames = nullptr;
+};
+void pose_draw(const PoseDrawArgs& a, int batch, hipStream_t s);
+
 }  // namespace kernels
 }  // namespace nnsx

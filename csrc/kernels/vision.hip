@@ -12,6 +12,7 @@
 
 #include <cfloat>
 
+#include "decoders/font.h"
 #include "kernels/vision.h"
 
 namespace nnsx {
@@ -156,6 +157,107 @@ __global__ void __launch_bounds__(256) pose_argmax_kernel(const float* __restric
   }
 }
 
+
+// Pose skeleton rasteriser: one workgroup per frame.  Keypoint positions are
+// refined from the argmax (heatmap-offset mode adds the offset tensor) exactly
+// like the host path; connections are drawn one per lane (Bresenham, same pixel
+// value -> order free); labels are drawn keypoint by keypoint behind barriers
+// because their cells (which also write background zeros) may overlap.
+__device__ inline void pose_setpixel(uint32_t* f, int W, int H, int x, int y) {
+  if (x < 0 || x >= W || y < 0 || y >= H) return;
+  f[y * W + x] = 0xFFFFFFFFu;
+  if (x + 1 < W) f[y * W + x + 1] = 0xFFFFFFFFu;
+  if (y + 1 < H) f[(y + 1) * W + x] = 0xFFFFFFFFu;
+}
+
+__constant__ int kDotX[40] = {-4, 0, 4, 0,  -3, -3, -3, -2, -2, -2, -2, -2, -1, -1, -1, -1, -1, -1, -1, 0,
+                              0,  0, 0, 0,  0,  1,  1,  1,  1,  1,  1,  1,  2,  2,  2,  2,  2,  3,  3,  3};
+__constant__ int kDotY[40] = {0,  -4, 0,  4,  -1, 0,  1,  -2, -1, 0,  1,  2,  -3, -2, -1, 0,  1,  2,  3,  -3,
+                              -2, -1, 1,  2,  3,  -3, -2, -1, 0,  1,  2,  3,  -2, -1, 0,  1,  2,  -1, 0,  1};
+__constant__ uint8_t kFontPose[95][7] = NNSX_FONT5X7_DATA;
+
+__global__ void __launch_bounds__(256) pose_draw_kernel(PoseDrawArgs a) {
+  __shared__ int px[64], py[64];
+  __shared__ int valid[64];
+  const int b = blockIdx.x;
+  const int K = a.keypoints;
+  uint32_t* f = a.frames + static_cast<uint64_t>(b) * a.W * a.H;
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    const float* o = a.kp + (static_cast<uint64_t>(b) * K + k) * 3;
+    const int mx = static_cast<int>(o[0]), my = static_cast<int>(o[1]);
+    int x, y;
+    if (a.offsets) {
+      const uint64_t oi = static_cast<uint64_t>(b) * a.gw * a.gh * 2 * K + (static_cast<uint64_t>(my) * a.gw + mx) * K * 2 + k;
+      const float offy = a.offsets[oi], offx = a.offsets[oi + K];
+      const float fx = (static_cast<float>(mx) / (a.gw - 1)) * a.i_w + offx;
+      const float fy = (static_cast<float>(my) / (a.gh - 1)) * a.i_h + offy;
+      x = static_cast<int>(fx * a.W / a.i_w);
+      y = static_cast<int>(fy * a.H / a.i_h);
+    } else {
+      x = static_cast<int>((static_cast<unsigned>(mx) * a.W) / a.i_w);
+      y = static_cast<int>((static_cast<unsigned>(my) * a.H) / a.i_h);
+    }
+    x = static_cast<int>(min(static_cast<unsigned>(a.W), static_cast<unsigned>(max(0, x))));
+    y = static_cast<int>(min(static_cast<unsigned>(a.H), static_cast<unsigned>(max(0, y))));
+    px[k] = x;
+    py[k] = y;
+    valid[k] = o[2] >= 0.5f;
+  }
+  __syncthreads();
+  // connections (i -> k, k > i): one per lane
+  for (int e = threadIdx.x; e < a.n_edges; e += blockDim.x) {
+    const int i = a.edges[2 * e], k = a.edges[2 * e + 1];
+    if (!valid[i] || !valid[k]) continue;
+    int xs = px[i], ys = py[i], xe = px[k], ye = py[k];
+    if (xs > xe) {
+      int t = xs; xs = xe; xe = t;
+      t = ys; ys = ye; ye = t;
+    }
+    for (int d = 0; d < 40; ++d) {
+      int yy = ys + kDotY[d], xx = xs + kDotX[d];
+      if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) f[yy * a.W + xx] = 0xFFFFFFFFu;
+      yy = ye + kDotY[d];
+      xx = xe + kDotX[d];
+      if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) f[yy * a.W + xx] = 0xFFFFFFFFu;
+    }
+    const int dx = abs(xe - xs), sx = xs < xe ? 1 : -1;
+    const int dy = abs(ye - ys), sy = ys < ye ? 1 : -1;
+    int err = (dx > dy ? dx : -dy) / 2;
+    while (true) {
+      pose_setpixel(f, a.W, a.H, xs, ys);
+      if (xs == xe && ys == ye) break;
+      const int e2 = err;
+      if (e2 > -dx) {
+        err -= dy;
+        xs += sx;
+      }
+      if (e2 < dy) {
+        err += dx;
+        ys += sy;
+      }
+    }
+  }
+  __syncthreads();
+  // labels, keypoint order
+  for (int k = 0; k < K; ++k) {
+    if (valid[k]) {
+      const char* lab = a.labels + a.label_offs[k];
+      int len = 0;
+      while (lab[len]) ++len;
+      int fit = 0;
+      while (fit < len && px[k] + 9 * fit + 8 <= a.W) ++fit;
+      const int ly = max(0, py[k] - 14);
+      for (int p = threadIdx.x; p < fit * 13 * 8; p += blockDim.x) {
+        const int ch = p / 104, rem = p % 104, row = rem / 8, col = rem % 8;
+        const int yy = ly + row, xx = px[k] + 9 * ch + col;
+        if (yy < a.H && xx < a.W)
+          f[yy * a.W + xx] = font::cell_on(kFontPose, static_cast<unsigned char>(lab[ch]), row, col) ? 0xFFFFFFFFu : 0u;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 void segment_argmax_color(const float* prob, int labels, uint64_t pixels, uint32_t rgb_modifier, float threshold,
@@ -191,6 +293,11 @@ void pose_heatmap_argmax(const float* heat, int keypoints, int grid_w, int grid_
   if (keypoints == 0 || batch == 0) return;
   hipLaunchKernelGGL(pose_argmax_kernel, dim3(keypoints, batch), dim3(256), 0, s, heat, keypoints, grid_w, grid_h,
                      sigmoid ? 1 : 0, out);
+}
+
+void pose_draw(const PoseDrawArgs& a, int batch, hipStream_t s) {
+  if (batch == 0) return;
+  hipLaunchKernelGGL(pose_draw_kernel, dim3(batch), dim3(256), 0, s, a);
 }
 
 }  // namespace kernels
