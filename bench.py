@@ -136,6 +136,9 @@ def main():
         f"videotestsrc num-buffers={frames} pattern=snow pool-size={pool} "
         f"! video/x-raw,format=RGB,width={S},height={S},framerate=0/1 "
         f"! tensor_converter frames-per-tensor={B} device={dev} "
+        # thread boundary: the next batch's upload is issued while the filter thread
+        # is still submitting this batch's kernels
+        f"! queue max-size-buffers=2 "
         + (f"! tensor_transform mode=arithmetic option={cfg['norm']} " if not fuse_norm else "")
         + f"! tensor_filter framework=pytorch model={model_path} input=3:{S}:{S}:{B} "
         f"inputtype={'uint8' if fuse_norm else 'float32'} "
@@ -147,21 +150,11 @@ def main():
     per_step = B if cfg["per_frame"] else 1  # sink buffers per batch
     pipe = nns.parse_launch(desc)
     sink = pipe.get_by_name("sink")
-    arrivals = []
-    latencies = []
-
-    seen = [0]
-
-    def on_data(buf):
-        seen[0] += 1
-        if seen[0] % per_step:
-            return  # a step ends with the last frame of the batch
-        now = pipe.running_time()
-        arrivals.append(time.perf_counter())
-        if buf.pts >= 0:
-            latencies.append((now - buf.pts) / 1e6)
-
-    sink.connect("new-data", on_data)
+    # native per-buffer arrival stats (no Python callback per frame); sync-device
+    # makes an arrival mean "the GPU has produced this frame", not "it was queued"
+    sink.set_property("emit-signal", "false")
+    sink.set_property("sync-device", "true")
+    sink.set_property("stats-every", "1")
 
     if dist is not None:
         dist.barrier()
@@ -176,6 +169,10 @@ def main():
         dist.barrier()
     pipe.stop()
 
+    recs = [tuple(int(v) for v in e.split(":")) for e in sink.get_property("stats").split(",") if e]
+    arrivals = [t / 1e9 for i, (t, _) in enumerate(recs) if (i + 1) % per_step == 0]  # last frame of each batch
+    step_lat = [[lat / 1e6 for _, lat in recs[k * per_step:(k + 1) * per_step] if lat >= 0]
+                for k in range(len(arrivals))]
     n = len(arrivals)
     if n < total:
         raise SystemExit(f"rank {rank}: only {n}/{total} batches reached the sink")
@@ -183,7 +180,8 @@ def main():
     t0 = arrivals[a.warmup - 1] if a.warmup > 0 else t_start
     t1 = arrivals[a.warmup + a.steps - 1]
     elapsed = t1 - t0
-    lat = np.array(latencies[a.warmup:a.warmup + a.steps]) if latencies else np.array([0.0])
+    timed = [x for k in range(a.warmup, a.warmup + a.steps) for x in step_lat[k]]
+    lat = np.array(timed) if timed else np.array([0.0])
     stats = torch.tensor([elapsed, float(np.percentile(lat, 50)), float(np.percentile(lat, 99))], dtype=torch.float64)
     if dist is not None:
         if dist.get_backend() == "nccl":

@@ -580,8 +580,8 @@ class VideoTestSrc : public BaseSrc {
     // pre-render the whole frame ring up front (in parallel) so producing a frame
     // is O(1) and no rendering lands inside a measured run
     const bool animated = pattern_ == 1 || pattern_ == 12 || pattern_ == 18 || pattern_ == 25;
-    const int64_t n = animated ? std::max<int64_t>(1, pool_size_) : 1;
-    if (num_buffers_ >= 0 && num_buffers_ < n) return true;  // short runs render lazily
+    int64_t n = animated ? std::max<int64_t>(1, pool_size_) : 1;
+    if (num_buffers_ >= 0) n = std::min<int64_t>(n, std::max<int64_t>(1, num_buffers_));  // frames ever shown
     frames_.resize(static_cast<size_t>(n));
     const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<std::thread> th;

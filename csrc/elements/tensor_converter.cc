@@ -326,6 +326,13 @@ class TensorConverter : public Element {
       return m->size() == frame_size_ ? m : Memory::view(m, 0, frame_size_);
     }
     size_t stride = vinfo_.stride[0];
+    if (dev >= 0 && frames_per_tensor_ > 1 && m->place() != MemPlace::HOST && stride <= kernels::kGatherMaxStride &&
+        stride % 4 == 0 && m->size() >= stride * (vinfo_.height - 1) + row) {
+      // batched upload: the gather kernel strips the padding while reading the
+      // frame over the bus (the adapter piece is flagged padded)
+      padded_frame_ = true;
+      return m;
+    }
     if (dev >= 0 && frames_per_tensor_ == 1 && !m->on_device()) {
       auto out = Memory::alloc_device(frame_size_, dev, s);
       hip::check(hipMemcpy2DAsync(out->data(), row, m->data(), stride, row, vinfo_.height, hipMemcpyHostToDevice, s),
@@ -345,7 +352,21 @@ class TensorConverter : public Element {
     MemoryPtr mem;
     size_t off;
     int64_t pts, dts;
+    size_t row = 0, stride = 0, rows = 0;  // padded video frame (packed size row * rows)
+    bool padded() const { return row != 0; }
+    size_t size() const { return padded() ? row * rows : mem->size(); }
   };
+
+  // a padded piece that cannot go through the gather kernel whole: pack it on the host
+  void unpad(Piece& p) {
+    if (!p.padded()) return;
+    const uint8_t* src = static_cast<const uint8_t*>(p.mem->map_host());
+    auto out = Memory::alloc_host(p.row * p.rows);
+    for (size_t y = 0; y < p.rows; ++y)
+      std::memcpy(static_cast<uint8_t*>(out->data()) + y * p.row, src + y * p.stride, p.row);
+    p.mem = out;
+    p.row = p.stride = p.rows = 0;
+  }
 
   // take `size` bytes from the adapter: zero-copy view when inside one piece,
   // otherwise gathered into one block (on the device when uploading)
@@ -355,10 +376,10 @@ class TensorConverter : public Element {
     *dts = f.dts;
     *pts_dist = f.off;
     MemoryPtr out;
-    if (f.mem->size() - f.off >= size && dev < 0) {
+    if (!f.padded() && f.size() - f.off >= size && dev < 0) {
       out = Memory::view(f.mem, f.off, size);
       f.off += size;
-      if (f.off == f.mem->size()) adapter_.pop_front();
+      if (f.off == f.size()) adapter_.pop_front();
       avail_ -= size;
       return out;
     }
@@ -373,19 +394,26 @@ class TensorConverter : public Element {
       };
       while (done < size) {
         Piece& p = adapter_.front();
-        size_t n = std::min(size - done, p.mem->size() - p.off);
+        size_t n = std::min(size - done, p.size() - p.off);
         if (p.mem->on_device()) p.mem->wait_ready(s);
-        g.seg[g.n++] = kernels::GatherSeg{static_cast<const char*>(p.mem->data()) + p.off, done, n};
+        if (p.padded()) {  // whole frame (gather_eligible checked)
+          g.row = static_cast<uint32_t>(p.row);
+          g.stride = static_cast<uint32_t>(p.stride);
+          g.seg[g.n++] = kernels::GatherSeg{p.mem->data(), done, n | kernels::kGatherPadded};
+        } else {
+          g.seg[g.n++] = kernels::GatherSeg{static_cast<const char*>(p.mem->data()) + p.off, done, n};
+        }
         p.mem->record_use(s, dev);
         if (g.n == kernels::kGatherMax) flush();
         done += n;
         p.off += n;
-        if (p.off == p.mem->size()) adapter_.pop_front();
+        if (p.off == p.size()) adapter_.pop_front();
       }
       flush();
     }
     while (done < size) {
       Piece& p = adapter_.front();
+      unpad(p);
       size_t n = std::min(size - done, p.mem->size() - p.off);
       char* dst = static_cast<char*>(out->data()) + done;
       const char* srcp = static_cast<const char*>(p.mem->data()) + p.off;
@@ -411,7 +439,9 @@ class TensorConverter : public Element {
     size_t seen = 0;
     for (const Piece& p : adapter_) {
       if (p.mem->place() == MemPlace::HOST) return false;
-      seen += p.mem->size() - p.off;
+      // a padded frame goes through the kernel whole
+      if (p.padded() && (p.off != 0 || seen + p.size() > size)) return false;
+      seen += p.size() - p.off;
       if (seen >= size) return true;
     }
     return false;
@@ -629,8 +659,15 @@ class TensorConverter : public Element {
     int64_t duration = in->duration;
     if (duration >= 0) duration = duration * frames_out / std::max(1u, frames_in);
     for (auto& m : in->mems) {
-      adapter_.push_back(Piece{m, 0, in->pts, in->dts});
-      avail_ += m->size();
+      Piece pc{m, 0, in->pts, in->dts};
+      if (padded_frame_) {
+        pc.row = static_cast<size_t>(vinfo_.width) * vinfo_.channels;
+        pc.stride = vinfo_.stride[0];
+        pc.rows = static_cast<size_t>(vinfo_.height);
+        padded_frame_ = false;
+      }
+      avail_ += pc.size();
+      adapter_.push_back(pc);
       // only the first memory carries the timestamp
       in->pts = -1;
       in->dts = -1;
@@ -666,6 +703,7 @@ class TensorConverter : public Element {
   MediaType media_ = MediaType::INVALID;
   VideoInfo vinfo_;
   bool remove_padding_ = false;
+  bool padded_frame_ = false;  // video_frame() handed back a padded frame for the gather kernel
   size_t frame_size_ = 0, in_frame_size_ = 0;
   bool out_flexible_ = false, skip_header_ = false;
   int64_t old_pts_ = -1;

@@ -1,9 +1,13 @@
 // tensor_sink: application sink with `new-data`, `stream-start` and `eos`
 // signals (gst/nnstreamer/elements/gsttensor_sink.c:207-229, render :479-533).
 // nnsx adds per-buffer latency statistics (source PTS -> render wall clock)
-// read by the benchmark harness, and `sync-device` to wait for the device
+// (`stats-every=N`: every N-th buffer's arrival on the monotonic clock and its
+// source-PTS -> render latency, read back through the `stats` property without
+// a Python callback per frame), and `sync-device` to wait for the device
 // payloads before signalling (end-to-end timing).
 #include <algorithm>
+#include <mutex>
+#include <vector>
 
 #include "elements/elements.h"
 #include "elements/tensor_common.h"
@@ -24,6 +28,16 @@ class TensorSink : public BaseSink {
     prop_bool("emit-signal", &emit_signal_, "Emit signal for new data, stream start, eos");
     prop_bool("sync-device", &sync_device_, "nnsx: wait until device-resident payloads are produced before signalling");
     prop_readonly("frames", [this] { return std::to_string(frames_.load()); }, "nnsx: number of rendered frames");
+    prop_uint("stats-every", &stats_every_, "nnsx: record every N-th buffer's arrival time and latency (0 = off)");
+    prop_readonly(
+        "stats",
+        [this] {
+          std::lock_guard<std::mutex> lk(stats_mu_);
+          std::string r;
+          for (auto& e : stats_) r += std::to_string(e.first) + ":" + std::to_string(e.second) + ",";
+          return r;
+        },
+        "nnsx: 'monotonic_ns:latency_ns,' per recorded buffer (latency -1 without a PTS)");
     sync_ = false;
     qos_ = true;
   }
@@ -33,6 +47,8 @@ class TensorSink : public BaseSink {
     BaseSink::start();
     last_emit_ = -1;
     frames_ = 0;
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    stats_.clear();
     return true;
   }
 
@@ -46,7 +62,12 @@ class TensorSink : public BaseSink {
   FlowReturn render(const BufferPtr& buf) override {
     if (sync_device_)
       for (auto& m : buf->mems) m->sync_ready();
-    ++frames_;
+    const int64_t n = ++frames_;
+    if (stats_every_ > 0 && n % stats_every_ == 0) {
+      const int64_t lat = buf->pts >= 0 ? running_time() - buf->pts : -1;
+      std::lock_guard<std::mutex> lk(stats_mu_);
+      stats_.emplace_back(now_ns(), lat);
+    }
     if (!emit_signal_) return FlowReturn::OK;
     if (signal_rate_ > 0) {
       int64_t now = now_ns();
@@ -67,6 +88,9 @@ class TensorSink : public BaseSink {
   bool sync_device_ = false;
   int64_t last_emit_ = -1;
   std::atomic<int64_t> frames_{0};
+  unsigned stats_every_ = 0;
+  std::mutex stats_mu_;
+  std::vector<std::pair<int64_t, int64_t>> stats_;
   Caps caps_;
 };
 

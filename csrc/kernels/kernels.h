@@ -54,14 +54,20 @@ void stand(const void* in, DType in_t, void* out, DType out_t, uint64_t n, uint3
 // One-launch gather of many host-pinned / device segments into one device block
 // (tensor_converter frames-per-tensor batching): replaces a hipMemcpyAsync per
 // frame.  Pinned host memory is read in place over the bus (zero copy).
+// A segment flagged kGatherPadded is a video frame whose rows sit `stride`
+// bytes apart in the source (GStreamer 4-byte row alignment); `row` bytes of
+// each are copied, so the destination is packed ([H][W*C], K7 remove-padding).
+constexpr uint64_t kGatherPadded = 1ull << 63;
+constexpr uint32_t kGatherMaxStride = 8192;  // 4 padded rows fit the 32 KB LDS stage
 struct GatherSeg {
   const void* src;
   uint64_t dst_off;
-  uint64_t bytes;
+  uint64_t bytes;  // destination bytes | kGatherPadded
 };
 constexpr int kGatherMax = 128;  // segments per launch (kernel-argument budget)
 struct GatherArgs {
   int n = 0;
+  uint32_t row = 0, stride = 0;  // geometry of the padded segments
   GatherSeg seg[kGatherMax];
 };
 void gather_copy(const GatherArgs& g, void* dst, hipStream_t s);

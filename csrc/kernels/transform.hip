@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <stdexcept>
 #include <type_traits>
 
 #include "kernels/dtype.cuh"
@@ -381,16 +382,58 @@ void stand(const void* in, DType in_t, void* out, DType out_t, uint64_t n, uint3
 // ----------------------------------------------------------------- gather ----
 namespace {
 
+constexpr uint32_t kGatherLds = 32768;
+
+// padded frame: stage whole source rows (16-B loads, padding included) through
+// LDS, then write the packed rows out with consecutive lanes on consecutive bytes
+__device__ void gather_padded(const char* __restrict__ src, char* __restrict__ d, uint64_t bytes, uint32_t row,
+                              uint32_t stride, int part, int parts, uint4* lds4) {
+  char* lds = reinterpret_cast<char*>(lds4);
+  const uint32_t rows = static_cast<uint32_t>(bytes / row);
+  const uint32_t R = (kGatherLds / stride) & ~3u;  // rows per stage; R * stride % 16 == 0
+  const bool vec = (reinterpret_cast<uintptr_t>(src) & 15) == 0;
+  for (uint32_t r0 = static_cast<uint32_t>(part) * R; r0 < rows; r0 += static_cast<uint32_t>(parts) * R) {
+    const uint32_t nr = min(R, rows - r0);
+    const char* s = src + static_cast<uint64_t>(r0) * stride;
+    const uint32_t span = (nr - 1) * stride + row;  // the last row's padding may not exist
+    if (vec) {
+      const uint32_t nv = span / 16;
+      const uint4* s4 = reinterpret_cast<const uint4*>(s);
+      for (uint32_t i = threadIdx.x; i < nv; i += blockDim.x) lds4[i] = s4[i];
+      for (uint32_t i = nv * 16 + threadIdx.x; i < span; i += blockDim.x) lds[i] = s[i];
+    } else {
+      for (uint32_t i = threadIdx.x; i < span; i += blockDim.x) lds[i] = s[i];
+    }
+    __syncthreads();
+    char* o = d + static_cast<uint64_t>(r0) * row;
+    const uint32_t n = nr * row;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+      const uint32_t y = i / row, x = i - y * row;
+      o[i] = lds[y * stride + x];
+    }
+    __syncthreads();
+  }
+}
+
+template <bool kPad>
 __global__ void __launch_bounds__(256) gather_kernel(GatherArgs g, char* __restrict__ dst) {
   const GatherSeg sg = g.seg[blockIdx.y];
   char* d = dst + sg.dst_off;
   const char* src = static_cast<const char*>(sg.src);
+  const uint64_t bytes = sg.bytes & ~kGatherPadded;
+  if constexpr (kPad) {
+    __shared__ uint4 lds[kGatherLds / 16];
+    if (sg.bytes & kGatherPadded) {
+      gather_padded(src, d, bytes, g.row, g.stride, static_cast<int>(blockIdx.x), static_cast<int>(gridDim.x), lds);
+      return;
+    }
+  }
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(d) | sg.bytes) & 15) == 0) {
+  if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(d) | bytes) & 15) == 0) {
     const uint4* s4 = reinterpret_cast<const uint4*>(src);
     uint4* d4 = reinterpret_cast<uint4*>(d);
-    const uint64_t n = sg.bytes / 16;
+    const uint64_t n = bytes / 16;
     // 4 independent 16-B loads in flight per lane (host reads cross the bus)
     for (uint64_t i = t0; i < n; i += 4 * stride) {
       uint4 v[4];
@@ -402,7 +445,7 @@ __global__ void __launch_bounds__(256) gather_kernel(GatherArgs g, char* __restr
         if (i + u * stride < n) d4[i + u * stride] = v[u];
     }
   } else {
-    for (uint64_t i = t0; i < sg.bytes; i += stride) d[i] = src[i];
+    for (uint64_t i = t0; i < bytes; i += stride) d[i] = src[i];
   }
 }
 
@@ -410,11 +453,21 @@ __global__ void __launch_bounds__(256) gather_kernel(GatherArgs g, char* __restr
 
 void gather_copy(const GatherArgs& g, void* dst, hipStream_t s) {
   if (g.n <= 0) return;
-  uint64_t maxb = 0;
-  for (int i = 0; i < g.n; ++i) maxb = std::max<uint64_t>(maxb, g.seg[i].bytes);
-  // ~4 16-B vectors per lane per segment block
-  unsigned bx = static_cast<unsigned>(std::min<uint64_t>(64, std::max<uint64_t>(1, (maxb / 16 + 1023) / 1024)));
-  hipLaunchKernelGGL(gather_kernel, dim3(bx, static_cast<unsigned>(g.n)), dim3(256), 0, s, g, static_cast<char*>(dst));
+  // Host-link bound: 1-2 workgroups per frame already saturate the bus
+  // (~57 GB/s for 128 x 270 KB frames, scripts/micro/h2d_gather.hip), and a
+  // small grid leaves the CUs to the model kernels this copy overlaps with.
+  const unsigned bx = static_cast<unsigned>(std::max(1, std::min(4, 256 / g.n)));
+  bool pad = false;
+  for (int i = 0; i < g.n; ++i) pad |= (g.seg[i].bytes & kGatherPadded) != 0;
+  if (pad) {
+    if (g.row == 0 || g.row > g.stride || g.stride > kGatherMaxStride || (g.stride & 3))
+      throw std::invalid_argument("gather_copy: padded rows need 0 < row <= stride <= 8192, stride % 4 == 0");
+    hipLaunchKernelGGL(gather_kernel<true>, dim3(bx, static_cast<unsigned>(g.n)), dim3(256), 0, s, g,
+                       static_cast<char*>(dst));
+  } else {
+    hipLaunchKernelGGL(gather_kernel<false>, dim3(bx, static_cast<unsigned>(g.n)), dim3(256), 0, s, g,
+                       static_cast<char*>(dst));
+  }
 }
 
 }  // namespace kernels

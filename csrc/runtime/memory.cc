@@ -13,7 +13,7 @@ Memory::Memory(void* data, size_t size, MemPlace place, int device, Release rele
 Memory::~Memory() {
   if (release_) release_(this);
   if (ready_) hip::event_put(ready_dev_, ready_);
-  for (auto& u : uses_) hip::event_put(u.first, u.second);
+  for (auto& u : uses_) hip::event_put(u.dev, u.event);
 }
 
 MemoryPtr Memory::alloc_host(size_t size) {
@@ -71,6 +71,7 @@ void Memory::mark_ready(hipStream_t stream) {
     r->ready_dev_ = dev;
   }
   hip::check(hipEventRecord(r->ready_, stream), "hipEventRecord(ready)");
+  ++r->ready_gen_;
 }
 
 void Memory::wait_ready(hipStream_t stream) const {
@@ -82,36 +83,45 @@ void Memory::wait_ready(hipStream_t stream) const {
 void Memory::sync_ready() const {
   const Memory* r = root();
   hipEvent_t e;
+  uint64_t gen;
   {
     std::lock_guard<std::mutex> lk(r->ev_mu_);
+    if (r->ready_gen_ == r->synced_gen_) return;  // already waited for this recording
     e = r->ready_;
+    gen = r->ready_gen_;
   }
   if (e) hip::check(hipEventSynchronize(e), "hipEventSynchronize(ready)");
+  // views of one batch share the root: the first frame waits, the rest return here
+  std::lock_guard<std::mutex> lk(r->ev_mu_);
+  if (r->synced_gen_ < gen) r->synced_gen_ = gen;
 }
 
 void Memory::record_use(hipStream_t stream, int dev) {
   Memory* r = root();
+  std::lock_guard<std::mutex> lk(r->ev_mu_);
+  // one event per reading stream: work on a stream completes in order, so the
+  // latest record there covers every earlier read (a ring frame read by every
+  // pass keeps one event instead of one per frame)
+  for (auto& u : r->uses_)
+    if (u.stream == stream && u.dev == dev) {
+      hip::check(hipEventRecord(u.event, stream), "hipEventRecord(use)");
+      return;
+    }
   hipEvent_t e = hip::event_get(dev);
   hip::check(hipEventRecord(e, stream), "hipEventRecord(use)");
-  std::lock_guard<std::mutex> lk(r->ev_mu_);
-  r->uses_.emplace_back(dev, e);
-  // bound the list: a long-lived memory read by many frames keeps the tail only
-  if (r->uses_.size() > 64) {
-    hip::event_put(r->uses_.front().first, r->uses_.front().second);
-    r->uses_.erase(r->uses_.begin());
-  }
+  r->uses_.push_back({dev, stream, e});
 }
 
 void Memory::wait_uses(hipStream_t stream) const {
   const Memory* r = root();
   std::lock_guard<std::mutex> lk(r->ev_mu_);
-  for (auto& u : r->uses_) (void)hipStreamWaitEvent(stream, u.second, 0);
+  for (auto& u : r->uses_) (void)hipStreamWaitEvent(stream, u.event, 0);
 }
 
 void Memory::sync_uses() const {
   const Memory* r = root();
   std::lock_guard<std::mutex> lk(r->ev_mu_);
-  for (auto& u : r->uses_) (void)hipEventSynchronize(u.second);
+  for (auto& u : r->uses_) (void)hipEventSynchronize(u.event);
 }
 
 const void* Memory::map_host() {

@@ -101,9 +101,16 @@ class Memory : public std::enable_shared_from_this<Memory> {
   MemoryPtr parent_;  // for views
   hipEvent_t ready_ = nullptr;
   int ready_dev_ = 0;
+  uint64_t ready_gen_ = 0;           // mark_ready() count
+  mutable uint64_t synced_gen_ = 0;  // last ready_gen_ known complete on the host
   mutable std::mutex ev_mu_;  // ready_ / uses_ (only the root's is used)
   mutable std::mutex mu_;     // mirrors
-  std::vector<std::pair<int, hipEvent_t>> uses_;
+  struct Use {
+    int dev;
+    hipStream_t stream;
+    hipEvent_t event;  // re-recorded per use: the stream's latest read covers earlier ones
+  };
+  std::vector<Use> uses_;
   MemoryPtr host_mirror_;
   std::map<int, MemoryPtr> dev_mirror_;
   std::map<std::string, int64_t> tags_;

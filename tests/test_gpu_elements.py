@@ -167,7 +167,7 @@ def test_pose_device_matches_host(nns):
     assert len(res[0]) == B and res[0] == res[-1]
 
 
-@pytest.mark.parametrize("w,h,n", [(224, 224, 6), (5, 3, 7), (64, 48, 130)])
+@pytest.mark.parametrize("w,h,n", [(224, 224, 6), (5, 3, 7), (64, 48, 130), (257, 257, 9), (513, 11, 3), (2731, 5, 2)])
 def test_converter_batched_gather_matches_host(nns, w, h, n):
     desc = (f"videotestsrc num-buffers={2 * n} pattern=snow pool-size=5 ! video/x-raw,format=RGB,width={w},height={h},"
             f"framerate=30/1 ! tensor_converter frames-per-tensor={n} device={{dev}} ! tensor_sink name=sink")
