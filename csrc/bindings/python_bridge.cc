@@ -18,6 +18,7 @@
 #include "decoders/decoders.h"
 #include "runtime/hip_util.h"
 #include "runtime/plugin_api.h"
+#include "single/single.h"
 
 namespace py = pybind11;
 
@@ -398,6 +399,51 @@ py::list numpy_views(const std::vector<MemoryPtr>& in, const TensorsInfo* info) 
 TensorInfo tensor_info_from_py(py::handle o) { return info_from_shape(o); }
 
 void register_python_bridge(py::module_& m) {
+  py::register_exception<TimeoutError>(m, "NnsxTimeout", PyExc_TimeoutError);
+  // single-shot (ml_single_*): Python wrapper in nnstreamer_amd/single.py
+  py::class_<SingleShot>(m, "SingleShot")
+      .def(py::init([](const std::string& fw, std::vector<std::string> models, py::object in, py::object out,
+                       const std::string& accl, const std::string& custom, int device) {
+             SingleOptions o;
+             o.framework = fw;
+             o.models = std::move(models);
+             if (!in.is_none()) o.input_info = infos_from_list(in);
+             if (!out.is_none()) o.output_info = infos_from_list(out);
+             o.accelerator = accl;
+             o.custom = custom;
+             o.device = device;
+             py::gil_scoped_release nogil;  // opening may run Python frameworks on other threads
+             return std::make_unique<SingleShot>(o);
+           }),
+           py::arg("framework"), py::arg("models"), py::arg("input") = py::none(), py::arg("output") = py::none(),
+           py::arg("accelerator") = "", py::arg("custom") = "", py::arg("device") = -1)
+      .def("input_info", [](SingleShot& s) { return list_from_infos(s.input_info()); })
+      .def("output_info", [](SingleShot& s) { return list_from_infos(s.output_info()); })
+      .def("set_input_info", [](SingleShot& s, py::list in) {
+        TensorsInfo i = infos_from_list(in);
+        py::gil_scoped_release nogil;
+        s.set_input_info(i);
+      })
+      .def("invoke", [](SingleShot& s, py::list inputs) {
+        std::vector<MemoryPtr> in;
+        for (auto o : inputs) in.push_back(memory_from_python(o));
+        std::vector<MemoryPtr> out;
+        TensorsInfo oi;
+        {
+          py::gil_scoped_release nogil;
+          out = s.invoke(in, &oi);
+        }
+        return py::make_tuple(out, list_from_infos(oi));
+      })
+      .def("set_timeout", &SingleShot::set_timeout)
+      .def("timeout", &SingleShot::timeout)
+      .def("framework", &SingleShot::framework)
+      .def("device", &SingleShot::device)
+      .def("close", [](SingleShot& s) {
+        py::gil_scoped_release nogil;
+        s.close();
+      });
+
   register_filter_framework(std::make_shared<PyFilterFw>());
   register_decoder(std::make_shared<PyDecoderPlugin>());
   set_script_converter_factory([](const std::string& path) -> std::shared_ptr<ConverterSubplugin> {

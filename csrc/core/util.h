@@ -36,6 +36,11 @@ class Error : public std::runtime_error {
  public:
   using std::runtime_error::runtime_error;
 };
+// an operation gave up waiting (single-shot invoke timeout; Python: TimeoutError)
+class TimeoutError : public Error {
+ public:
+  using Error::Error;
+};
 
 // Monotonic clock in nanoseconds.
 int64_t now_ns();

@@ -168,38 +168,13 @@ class TensorFilter : public BaseTransform {
     if (inst_) return true;
     std::lock_guard<std::mutex> lk(open_mu_);
     if (inst_) return true;
-    std::string fwn = fw_name_;
-    if (fwn.empty() || fwn == "auto") {
-      fwn = detect_framework(props_.model_files);
-      if (fwn.empty()) {
-        NNSX_LOGE(name(), "tensor_filter: cannot detect the framework for model '", model_str_, "'");
-        return false;
-      }
-    }
-    fw_ = find_filter_framework(fwn);
+    std::string err;
+    fw_ = resolve_filter_framework(fw_name_, &props_, device_prop_, &err);
     if (!fw_) {
-      NNSX_LOGE(name(), "tensor_filter: framework '", fwn, "' is not available");
+      NNSX_LOGE(name(), "tensor_filter: ", err, " (model '", model_str_, "')");
       return false;
     }
-    props_.fwname = fw_->name();
-    if (props_.model_files.empty() && !fw_->run_without_model()) {
-      NNSX_LOGE(name(), "tensor_filter: model property is not set");
-      return false;
-    }
-    bool use_accl = false;
-    props_.accl = parse_accelerator(props_.accl_str, fw_->accelerators(), &use_accl);
-    props_.device = -1;
-    if ((props_.accl == Accelerator::GPU || props_.accl == Accelerator::AUTO ||
-         (props_.accl == Accelerator::DEFAULT && fw_->accelerators().find("gpu") != std::string::npos &&
-          Config::get().custom_bool("pytorch", "enable_use_gpu", true))) &&
-        hip::available() && fw_->check_availability(Accelerator::GPU)) {
-      int dev = device_prop_;
-      if (dev < 0) {
-        const char* lr = getenv("LOCAL_RANK");
-        dev = lr ? static_cast<int>(to_int(lr)) % hip::device_count() : 0;
-      }
-      props_.device = dev;
-    }
+    const std::string fwn = props_.fwname;
     if (!props_.shared_key.empty()) {
       std::lock_guard<std::mutex> lk2(g_shared_mu);
       auto it = g_shared.find(props_.shared_key);

@@ -172,6 +172,7 @@ class CustomEasy : public FilterInstance {
 class CustomEasyFw : public FilterFramework {
  public:
   std::string name() const override { return "custom-easy"; }
+  bool verify_model_path() const override { return false; }  // the model is a registered name
   std::unique_ptr<FilterInstance> open(FilterProperties& p) override { return std::make_unique<CustomEasy>(p); }
 };
 
@@ -210,6 +211,7 @@ class CppInstance : public FilterInstance {
 class CppFw : public FilterFramework {
  public:
   std::string name() const override { return "cpp"; }
+  bool verify_model_path() const override { return false; }  // the model is a registered name
   std::unique_ptr<FilterInstance> open(FilterProperties& p) override { return std::make_unique<CppInstance>(p); }
 };
 

@@ -109,6 +109,10 @@ class TorchInstance : public FilterInstance {
       for (size_t k = 0; k < outs.size(); ++k) r.at(static_cast<unsigned>(k)) = info_from_tensor(outs[k]);
       *out = r;
       if (device_ >= 0) hip::check(hipDeviceSynchronize(), "sync dry run");
+      // the caller now feeds this input (SET_INPUT_INFO): invoke wraps buffers with it
+      std::lock_guard<std::mutex> lk(mu_);
+      props_.input_info = in;
+      props_.output_info = r;
       return true;
     } catch (const std::exception& e) {
       NNSX_LOGE("pytorch", "set_input_info failed: ", e.what());

@@ -1,9 +1,11 @@
 #include "runtime/plugin_api.h"
 
+#include <cstdlib>
 #include <regex>
 
 #include "core/log.h"
 #include "core/util.h"
+#include "runtime/hip_util.h"
 
 namespace nnsx {
 
@@ -62,6 +64,43 @@ Accelerator parse_accelerator(const std::string& s, const std::string& supported
     if (x == "default") return Accelerator::DEFAULT;
   }
   return Accelerator::AUTO;
+}
+
+std::shared_ptr<FilterFramework> resolve_filter_framework(const std::string& fw_name, FilterProperties* props,
+                                                          int device_prop, std::string* err) {
+  std::string fwn = fw_name;
+  if (fwn.empty() || fwn == "auto") {
+    fwn = detect_framework(props->model_files);
+    if (fwn.empty()) {
+      *err = "cannot detect the framework for the model";
+      return nullptr;
+    }
+  }
+  auto fw = find_filter_framework(fwn);
+  if (!fw) {
+    *err = "framework '" + fwn + "' is not available";
+    return nullptr;
+  }
+  props->fwname = fw->name();
+  if (props->model_files.empty() && !fw->run_without_model()) {
+    *err = "model property is not set";
+    return nullptr;
+  }
+  bool use_accl = false;
+  props->accl = parse_accelerator(props->accl_str, fw->accelerators(), &use_accl);
+  props->device = -1;
+  if ((props->accl == Accelerator::GPU || props->accl == Accelerator::AUTO ||
+       (props->accl == Accelerator::DEFAULT && fw->accelerators().find("gpu") != std::string::npos &&
+        Config::get().custom_bool("pytorch", "enable_use_gpu", true))) &&
+      hip::available() && fw->check_availability(Accelerator::GPU)) {
+    int dev = device_prop;
+    if (dev < 0) {
+      const char* lr = getenv("LOCAL_RANK");
+      dev = lr ? static_cast<int>(to_int(lr)) % hip::device_count() : 0;
+    }
+    props->device = dev;
+  }
+  return fw;
 }
 
 // ------------------------------------------------------------ custom-easy ----

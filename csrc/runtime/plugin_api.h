@@ -105,6 +105,11 @@ std::shared_ptr<FilterFramework> find_filter_framework(const std::string& name);
 std::string detect_framework(const std::vector<std::string>& models);
 // accelerator string grammar "true:gpu,cpu" / "false" / "true:!npu" (tensor_filter_common.c:2495-2800)
 Accelerator parse_accelerator(const std::string& s, const std::string& supported, bool* use_accel);
+// Shared by tensor_filter and the single-shot API: framework=auto detection,
+// accelerator parsing and GPU selection (`device` >= 0, else LOCAL_RANK % #GPUs,
+// else 0) into props->fwname / accl / device.  nullptr + *err on failure.
+std::shared_ptr<FilterFramework> resolve_filter_framework(const std::string& fw_name, FilterProperties* props,
+                                                          int device_prop, std::string* err);
 
 // custom-easy (NNS_custom_easy_register)
 using CustomEasyFn = std::function<int(const std::vector<MemoryPtr>& in, std::vector<MemoryPtr>* out,

@@ -83,6 +83,7 @@ from ._C import (  # noqa: E402,F401
     version,
 )
 from .utils.tensors import TensorShape, to_numpy, to_torch  # noqa: E402,F401
+from .single import Single  # noqa: E402,F401
 
 __all__ = [
     "Buffer",
@@ -91,6 +92,7 @@ __all__ = [
     "Memory",
     "Pipeline",
     "TensorShape",
+    "Single",
     "parse_launch",
     "make_element",
     "to_numpy",
