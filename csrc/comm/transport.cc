@@ -9,12 +9,17 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <hip/hip_runtime_api.h>
+
 #include <chrono>
 #include <cstring>
+#include <fstream>
+#include <map>
 #include <thread>
 
 #include "core/log.h"
 #include "core/util.h"
+#include "runtime/hip_util.h"
 
 namespace nnsx {
 namespace comm {
@@ -56,7 +61,155 @@ bool resolve(const std::string& host, int port, sockaddr_in* out) {
   return true;
 }
 
+constexpr uint32_t kFlagIpc = 1u << 31;       // DATA: a u64 ring offset per blob follows the sizes
+constexpr uint64_t kInline = ~0ull;           // offset of a blob that travels as bytes
+constexpr uint64_t kMinIpcBytes = 4096;       // smaller device blobs are cheaper inline
+constexpr size_t kDefaultRing = 256ull << 20;  // per sending end; HBM is 288 GB
+constexpr int kRingWaitMs = 200;              // then the blob goes inline
+
+const std::string& boot_id() {
+  static const std::string id = [] {
+    std::ifstream f("/proc/sys/kernel/random/boot_id");
+    std::string v;
+    std::getline(f, v);
+    return strip(v);
+  }();
+  return id;
+}
+
+std::map<std::string, std::string> parse_kv(const std::string& s) {
+  std::map<std::string, std::string> kv;
+  for (auto& t : split(s, ';')) {
+    auto eq = t.find('=');
+    if (eq != std::string::npos) kv[t.substr(0, eq)] = t.substr(eq + 1);
+  }
+  return kv;
+}
+
+std::string to_hex(const void* p, size_t n) {
+  static const char* d = "0123456789abcdef";
+  std::string r;
+  for (size_t i = 0; i < n; ++i) {
+    const uint8_t b = static_cast<const uint8_t*>(p)[i];
+    r.push_back(d[b >> 4]);
+    r.push_back(d[b & 15]);
+  }
+  return r;
+}
+
+bool from_hex(const std::string& h, void* out, size_t n) {
+  if (h.size() != 2 * n) return false;
+  auto v = [](char c) { return c <= '9' ? c - '0' : c - 'a' + 10; };
+  for (size_t i = 0; i < n; ++i) static_cast<uint8_t*>(out)[i] = static_cast<uint8_t>(v(h[2 * i]) << 4 | v(h[2 * i + 1]));
+  return true;
+}
+
+uint64_t align_up(uint64_t n) { return (n + 255) & ~255ull; }
+
 }  // namespace
+
+// Sending end's HBM staging ring with an out-of-order slot allocator.
+struct IpcRing {
+  int dev = 0;
+  char* base = nullptr;
+  size_t size = 0;
+  hipStream_t stream = nullptr;
+  std::string desc;  // IPC_RING payload
+  std::mutex mu;
+  std::condition_variable cv;
+  std::map<uint64_t, uint64_t> used;  // offset -> bytes
+  uint64_t head = 0;
+
+  static std::shared_ptr<IpcRing> create(int dev, size_t bytes);
+  ~IpcRing() {
+    hip::DeviceGuard g(dev);
+    if (stream) {
+      (void)hipStreamSynchronize(stream);
+      (void)hipStreamDestroy(stream);
+    }
+    if (base) (void)hipFree(base);
+  }
+  // first fit at/after `head`, then from 0; waits for releases up to wait_ms
+  bool alloc(uint64_t n, int wait_ms, uint64_t* off) {
+    std::unique_lock<std::mutex> lk(mu);
+    auto fit = [&](uint64_t from, uint64_t limit, uint64_t* o) {
+      uint64_t cand = from;
+      for (auto it = used.upper_bound(from); ; ++it) {
+        if (it != used.begin()) {
+          auto p = std::prev(it);
+          cand = std::max(cand, p->first + p->second);
+        }
+        const uint64_t next = it == used.end() ? limit : std::min<uint64_t>(it->first, limit);
+        if (cand + n <= next) {
+          *o = cand;
+          return true;
+        }
+        if (it == used.end() || it->first >= limit) return false;
+      }
+    };
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(wait_ms);
+    while (true) {
+      if (n <= size && (fit(head, size, off) || fit(0, head, off))) {
+        used[*off] = n;
+        head = *off + n;
+        return true;
+      }
+      if (n > size || cv.wait_until(lk, deadline) == std::cv_status::timeout) return false;
+    }
+  }
+  void release(uint64_t off) {
+    std::lock_guard<std::mutex> lk(mu);
+    used.erase(off);
+    cv.notify_all();
+  }
+};
+
+namespace {
+// same-process peers reach a ring by its pointer: keep it alive while mapped
+std::mutex g_rings_mu;
+std::map<uintptr_t, std::weak_ptr<IpcRing>> g_rings;
+}  // namespace
+
+std::shared_ptr<IpcRing> IpcRing::create(int dev, size_t bytes) {
+  hip::DeviceGuard g(dev);
+  auto r = std::make_shared<IpcRing>();
+  r->dev = dev;
+  r->size = bytes;
+  void* p = nullptr;
+  hip::check(hipMalloc(&p, bytes), "IPC ring hipMalloc");  // IPC needs hipMalloc, not the async pool
+  r->base = static_cast<char*>(p);
+  hipIpcMemHandle_t h;
+  hip::check(hipIpcGetMemHandle(&h, p), "hipIpcGetMemHandle");
+  char pci[64] = {0};
+  hip::check(hipDeviceGetPCIBusId(pci, sizeof(pci), dev), "hipDeviceGetPCIBusId");
+  r->stream = hip::stream_create(dev);
+  r->desc = strfmt("boot=", boot_id(), ";pid=", static_cast<long>(getpid()), ";pci=", pci, ";size=", bytes,
+                   ";ptr=", reinterpret_cast<uintptr_t>(p), ";handle=", to_hex(&h, sizeof(h)));
+  std::lock_guard<std::mutex> lk(g_rings_mu);
+  g_rings[reinterpret_cast<uintptr_t>(p)] = r;
+  return r;
+}
+
+// Receiving end's mapping of the peer's ring.
+struct PeerRing {
+  char* base = nullptr;
+  size_t size = 0;
+  int dev = 0;
+  bool opened = false;           // hipIpcOpenMemHandle (other process)
+  std::shared_ptr<IpcRing> own;  // same process: the ring itself
+  ~PeerRing() {
+    if (opened) {
+      hip::DeviceGuard g(dev);
+      (void)hipIpcCloseMemHandle(base);
+    }
+  }
+};
+
+std::shared_ptr<Connection> make_connection(int fd, std::string peer) {
+  auto c = std::make_shared<Connection>(fd, std::move(peer));
+  c->self_ = c;
+  return c;
+}
 
 Connection::Connection(int fd, std::string peer) : fd_(fd), peer_(std::move(peer)) { tune(fd_); }
 
@@ -76,7 +229,7 @@ std::shared_ptr<Connection> Connection::connect(const std::string& host, int por
       return nullptr;
     }
     if (::connect(fd, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) == 0)
-      return std::make_shared<Connection>(fd, strfmt(host, ":", port));
+      return make_connection(fd, strfmt(host, ":", port));
     const int e = errno;
     ::close(fd);
     if (now_ns() >= deadline) {
@@ -132,54 +285,203 @@ bool Connection::read_all(void* p, size_t n, int timeout_ms, bool* timed_out) {
   return true;
 }
 
+bool Connection::send_ipc_hello(size_t ring_bytes) {
+  if (!hip::available() || boot_id().empty()) return false;
+  ring_bytes_ = ring_bytes ? ring_bytes : kDefaultRing;
+  hello_sent_ = true;
+  Message m;
+  m.type = MsgType::IPC_HELLO;
+  m.caps = strfmt("boot=", boot_id(), ";pid=", static_cast<long>(getpid()));
+  return send(m);
+}
+
+void Connection::send_ack(uint64_t off, uint64_t bytes) {
+  Message m;
+  m.type = MsgType::IPC_ACK;
+  m.seq = off;
+  m.duration = static_cast<int64_t>(bytes);
+  (void)send(m);
+}
+
+bool Connection::handle_control(const Message& m) {
+  switch (m.type) {
+    case MsgType::IPC_HELLO: {
+      auto kv = parse_kv(m.caps);
+      if (kv["boot"] == boot_id() && hip::available()) {
+        peer_ipc_ = true;
+        if (!hello_sent_) send_ipc_hello(ring_bytes_);  // answer: we take ring blobs too
+      }
+      return true;
+    }
+    case MsgType::IPC_RING: {
+      auto kv = parse_kv(m.caps);
+      auto pr = std::make_shared<PeerRing>();
+      pr->size = static_cast<size_t>(to_uint(kv["size"]));
+      if (hipDeviceGetByPCIBusId(&pr->dev, kv["pci"].c_str()) != hipSuccess) {
+        NNSX_LOGE("comm", "IPC ring on an unknown GPU (", kv["pci"], ") from ", peer_);
+        return false;
+      }
+      if (static_cast<long>(to_int(kv["pid"])) == static_cast<long>(getpid())) {
+        std::lock_guard<std::mutex> lk(g_rings_mu);
+        auto it = g_rings.find(static_cast<uintptr_t>(to_uint(kv["ptr"])));
+        pr->own = it == g_rings.end() ? nullptr : it->second.lock();
+        if (!pr->own) return false;
+        pr->base = pr->own->base;
+      } else {
+        hipIpcMemHandle_t h;
+        if (!from_hex(kv["handle"], &h, sizeof(h))) return false;
+        hip::DeviceGuard g(pr->dev);
+        void* p = nullptr;
+        if (hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+          NNSX_LOGE("comm", "hipIpcOpenMemHandle failed for the ring of ", peer_);
+          return false;
+        }
+        pr->base = static_cast<char*>(p);
+        pr->opened = true;
+      }
+      peer_ring_ = pr;
+      return true;
+    }
+    case MsgType::IPC_ACK:
+      if (ring_) ring_->release(m.seq);
+      return true;
+    default:
+      return true;
+  }
+}
+
 bool Connection::send(const Message& m) {
   if (!alive_) return false;
   if (m.blobs.size() > kMaxBlobs) return false;
-  WireHeader h{kMagic, kVersion, static_cast<uint32_t>(m.type), static_cast<uint32_t>(m.blobs.size()),
-               m.client_id, m.seq, m.pts, m.dts, m.duration, static_cast<uint32_t>(m.caps.size()), m.flags};
-  std::vector<uint64_t> sizes;
-  std::vector<const void*> ptrs;
-  for (const auto& b : m.blobs) {
-    sizes.push_back(b->size());
-    ptrs.push_back(b->map_host());  // HBM blobs: staged through a host mirror
+  std::vector<uint64_t> offs;
+  bool announce = false;
+  if (m.type == MsgType::DATA && peer_ipc_) {
+    std::lock_guard<std::mutex> lk(ipc_mu_);
+    for (size_t i = 0; i < m.blobs.size(); ++i) {
+      const MemoryPtr& b = m.blobs[i];
+      if (!b->on_device() || b->size() < kMinIpcBytes) continue;
+      if (offs.empty()) offs.assign(m.blobs.size(), kInline);
+      if (!ring_) {
+        try {
+          ring_ = IpcRing::create(b->device(), std::max<size_t>(ring_bytes_ ? ring_bytes_ : kDefaultRing, 2 * b->size()));
+          announce = true;
+        } catch (const std::exception& e) {
+          NNSX_LOGW("comm", "device-direct path unavailable (", e.what(), "); sending bytes");
+          peer_ipc_ = false;
+          offs.clear();
+          break;
+        }
+      }
+      uint64_t off;
+      if (!ring_->alloc(align_up(b->size()), kRingWaitMs, &off)) continue;  // full: inline
+      hip::DeviceGuard g(ring_->dev);
+      b->wait_ready(ring_->stream);
+      hip::check(hipMemcpyAsync(ring_->base + off, b->data(), b->size(), hipMemcpyDefault, ring_->stream),
+                 "IPC ring copy");
+      offs[i] = off;
+    }
+    if (!offs.empty()) {
+      // the receiver reads the slot as soon as the header lands: the copy must be done
+      hip::DeviceGuard g(ring_->dev);
+      hip::check(hipStreamSynchronize(ring_->stream), "IPC ring sync");
+      bool any = false;
+      for (auto o : offs) any |= o != kInline;
+      if (!any) offs.clear();
+    }
   }
   std::lock_guard<std::mutex> lk(send_mu_);
+  if (announce) {
+    Message r;
+    r.type = MsgType::IPC_RING;
+    r.caps = ring_->desc;
+    if (!send_locked(r, nullptr)) return false;
+  }
+  if (!send_locked(m, offs.empty() ? nullptr : &offs)) return false;
+  if (!offs.empty())
+    for (auto o : offs) ipc_sent_ += o != kInline;
+  return true;
+}
+
+bool Connection::send_locked(const Message& m, const std::vector<uint64_t>* offs) {
+  WireHeader h{kMagic, kVersion, static_cast<uint32_t>(m.type), static_cast<uint32_t>(m.blobs.size()),
+               m.client_id, m.seq, m.pts, m.dts, m.duration, static_cast<uint32_t>(m.caps.size()),
+               offs ? (m.flags | kFlagIpc) : (m.flags & ~kFlagIpc)};
+  std::vector<uint64_t> sizes;
+  std::vector<const void*> ptrs;
+  for (size_t i = 0; i < m.blobs.size(); ++i) {
+    const auto& b = m.blobs[i];
+    sizes.push_back(b->size());
+    const bool inline_bytes = !offs || (*offs)[i] == kInline;
+    ptrs.push_back(inline_bytes ? b->map_host() : nullptr);  // HBM blobs inline: staged through a host mirror
+  }
   if (!write_all(&h, sizeof(h))) return false;
   if (!sizes.empty() && !write_all(sizes.data(), sizes.size() * sizeof(uint64_t))) return false;
+  if (offs && !write_all(offs->data(), offs->size() * sizeof(uint64_t))) return false;
   if (!m.caps.empty() && !write_all(m.caps.data(), m.caps.size())) return false;
   for (size_t i = 0; i < ptrs.size(); ++i)
-    if (sizes[i] && !write_all(ptrs[i], sizes[i])) return false;
+    if (ptrs[i] && sizes[i] && !write_all(ptrs[i], sizes[i])) return false;
   return true;
 }
 
 bool Connection::recv(Message* m, int timeout_ms, bool* timed_out) {
   if (timed_out) *timed_out = false;
-  if (!alive_) return false;
-  WireHeader h;
-  if (!read_all(&h, sizeof(h), timeout_ms, timed_out)) return false;
-  if (h.magic != kMagic || h.version != kVersion || h.nblobs > kMaxBlobs) {
-    NNSX_LOGE("comm", "bad message header from ", peer_);
-    alive_ = false;
-    return false;
+  while (true) {
+    if (!alive_) return false;
+    WireHeader h;
+    if (!read_all(&h, sizeof(h), timeout_ms, timed_out)) return false;
+    if (h.magic != kMagic || h.version != kVersion || h.nblobs > kMaxBlobs) {
+      NNSX_LOGE("comm", "bad message header from ", peer_);
+      alive_ = false;
+      return false;
+    }
+    m->type = static_cast<MsgType>(h.type);
+    m->client_id = h.client_id;
+    m->seq = h.seq;
+    m->pts = h.pts;
+    m->dts = h.dts;
+    m->duration = h.duration;
+    m->flags = h.flags & ~kFlagIpc;
+    std::vector<uint64_t> sizes(h.nblobs), offs;
+    if (h.nblobs && !read_all(sizes.data(), sizes.size() * sizeof(uint64_t), -1, nullptr)) return false;
+    if (h.flags & kFlagIpc) {
+      offs.resize(h.nblobs);
+      if (h.nblobs && !read_all(offs.data(), offs.size() * sizeof(uint64_t), -1, nullptr)) return false;
+    }
+    m->caps.assign(h.caps_len, '\0');
+    if (h.caps_len && !read_all(&m->caps[0], h.caps_len, -1, nullptr)) return false;
+    m->blobs.clear();
+    for (size_t i = 0; i < sizes.size(); ++i) {
+      const uint64_t sz = sizes[i];
+      if (!offs.empty() && offs[i] != kInline) {
+        auto pr = peer_ring_;
+        if (!pr || offs[i] + sz > pr->size) {
+          NNSX_LOGE("comm", "ring blob without a mapped ring from ", peer_);
+          alive_ = false;
+          return false;
+        }
+        const uint64_t off = offs[i];
+        std::weak_ptr<Connection> w = self_;
+        // zero-copy: downstream reads the peer's slot; releasing it hands the slot back
+        m->blobs.push_back(Memory::wrap(pr->base + off, sz, MemPlace::DEVICE, pr->dev, [pr, w, off, sz](Memory* mm) {
+          mm->sync_uses();
+          if (auto c = w.lock()) c->send_ack(off, sz);
+        }));
+        ++ipc_recv_;
+        continue;
+      }
+      auto mem = Memory::alloc_pinned(sz);  // pinned: a later H2D is a DMA
+      if (sz && !read_all(mem->data(), sz, -1, nullptr)) return false;
+      m->blobs.push_back(mem);
+    }
+    if (m->type == MsgType::IPC_HELLO || m->type == MsgType::IPC_RING || m->type == MsgType::IPC_ACK) {
+      if (!handle_control(*m)) {
+        alive_ = false;
+        return false;
+      }
+      continue;  // control traffic is invisible to the elements
+    }
+    return true;
   }
-  m->type = static_cast<MsgType>(h.type);
-  m->client_id = h.client_id;
-  m->seq = h.seq;
-  m->pts = h.pts;
-  m->dts = h.dts;
-  m->duration = h.duration;
-  m->flags = h.flags;
-  std::vector<uint64_t> sizes(h.nblobs);
-  if (h.nblobs && !read_all(sizes.data(), sizes.size() * sizeof(uint64_t), -1, nullptr)) return false;
-  m->caps.assign(h.caps_len, '\0');
-  if (h.caps_len && !read_all(&m->caps[0], h.caps_len, -1, nullptr)) return false;
-  m->blobs.clear();
-  for (uint64_t sz : sizes) {
-    auto mem = Memory::alloc_pinned(sz);  // pinned: a later H2D is a DMA
-    if (sz && !read_all(mem->data(), sz, -1, nullptr)) return false;
-    m->blobs.push_back(mem);
-  }
-  return true;
 }
 
 void Connection::close() {
@@ -225,7 +527,7 @@ std::shared_ptr<Connection> Listener::accept(int timeout_ms) {
   if (fd < 0) return nullptr;
   char buf[64];
   inet_ntop(AF_INET, &peer.sin_addr, buf, sizeof(buf));
-  return std::make_shared<Connection>(fd, strfmt(buf, ":", ntohs(peer.sin_port)));
+  return make_connection(fd, strfmt(buf, ":", ntohs(peer.sin_port)));
 }
 
 void Listener::close() {

@@ -12,6 +12,16 @@
 //
 // HBM-resident blobs are staged through pinned memory on send; receivers
 // may upload into HBM (element `device` property).
+//
+// Device-direct path (connect-type=HIPIPC, same host): each sending end owns
+// a hipMalloc'd staging ring in HBM exported once with hipIpcGetMemHandle.
+// A device blob is copied D2D (or peer, over xGMI) into a ring slot and only
+// {offset, size} travels on the socket; the receiver maps the ring once
+// (hipIpcOpenMemHandle, lazily peer-enabled) and hands the slot downstream
+// zero-copy as a device Memory whose release sends IPC_ACK back, which frees
+// the slot.  Both ends announce the capability (IPC_HELLO with the kernel
+// boot id, so a cross-host peer never tries), and a full ring falls back to
+// the TCP byte path for that blob instead of blocking.
 #pragma once
 
 #include <atomic>
@@ -28,7 +38,15 @@
 namespace nnsx {
 namespace comm {
 
-enum class MsgType : uint32_t { HELLO = 1, CAPS = 2, DATA = 3, EOS = 4, ERROR = 5, BYE = 6 };
+enum class MsgType : uint32_t {
+  HELLO = 1, CAPS = 2, DATA = 3, EOS = 4, ERROR = 5, BYE = 6,
+  IPC_HELLO = 7,  // caps: "boot=<id>;pid=<n>" -- the sender can receive ring blobs
+  IPC_RING = 8,   // caps: ring description (handle, size, PCI bus id); precedes its first use
+  IPC_ACK = 9,    // seq = ring offset, duration = bytes: the receiver released a slot
+};
+
+struct IpcRing;      // transport.cc
+struct PeerRing;     // transport.cc
 
 struct Message {
   MsgType type = MsgType::DATA;
@@ -39,6 +57,9 @@ struct Message {
   std::string caps;
   std::vector<MemoryPtr> blobs;
 };
+
+class Connection;
+std::shared_ptr<Connection> make_connection(int fd, std::string peer);
 
 class Connection {
  public:
@@ -55,12 +76,32 @@ class Connection {
   const std::string& peer() const { return peer_; }
   uint64_t id = 0;  // server-assigned client id
 
+  // device-direct path: announce that this end takes ring blobs (and will
+  // export its own ring, sized `ring_bytes`, when it first sends a device blob)
+  bool send_ipc_hello(size_t ring_bytes = 0);
+  // the peer announced IPC and lives on this host: device blobs go through the ring
+  bool peer_ipc() const { return peer_ipc_.load(); }
+  // blobs sent through the ring / inline since the connection opened (tests, stats)
+  uint64_t ipc_blobs_sent() const { return ipc_sent_.load(); }
+  uint64_t ipc_blobs_received() const { return ipc_recv_.load(); }
+
  private:
+  bool send_locked(const Message& m, const std::vector<uint64_t>* offsets);
+  bool handle_control(const Message& m);  // IPC_* messages, consumed inside recv()
+  void send_ack(uint64_t off, uint64_t bytes);
+  std::weak_ptr<Connection> self_;  // for the ACK-on-release closures
+  friend std::shared_ptr<Connection> make_connection(int fd, std::string peer);
+  std::atomic<bool> peer_ipc_{false}, hello_sent_{false};
+  std::atomic<uint64_t> ipc_sent_{0}, ipc_recv_{0};
+  size_t ring_bytes_ = 0;
+  std::shared_ptr<IpcRing> ring_;      // ours (sending side)
+  std::shared_ptr<PeerRing> peer_ring_;  // theirs, mapped (receiving side)
+
   bool write_all(const void* p, size_t n);
   bool read_all(void* p, size_t n, int timeout_ms, bool* timed_out);
   int fd_;
   std::string peer_;
-  std::mutex send_mu_;
+  std::mutex send_mu_, ipc_mu_;
   std::atomic<bool> alive_{true};
 };
 

@@ -9,7 +9,10 @@
 // frames), tensor_query_server.c (id -> server registry, waits for the sink's
 // caps before answering clients), gst/edge/edge_sink.c / edge_src.c.  The
 // reference rides on the external nnstreamer-edge library (TCP / MQTT-hybrid
-// / AITT); nnsx implements the TCP connect-type natively.
+// / AITT); nnsx implements the TCP connect-type natively, plus HIPIPC: the
+// same framing with HBM-resident tensors handed over through an exported
+// device ring (zero-copy on the same GPU, one xGMI peer copy across GPUs;
+// see comm/transport.h).
 #include <algorithm>
 #include <atomic>
 #include <map>
@@ -27,21 +30,28 @@ namespace nnsx {
 
 namespace {
 
-const std::vector<std::string> kConnectTypes = {"TCP", "HYBRID", "MQTT", "AITT"};
+const std::vector<std::string> kConnectTypes = {"TCP", "HYBRID", "MQTT", "AITT", "HIPIPC"};
+constexpr int kHipIpc = 4;
 
 bool check_connect_type(Element* e, int type) {
-  if (type == 0) return true;
-  e->post_error("connect-type " + kConnectTypes[static_cast<size_t>(type)] + " is not supported (nnsx implements TCP)");
+  if (type == 0 || type == kHipIpc) return true;
+  e->post_error("connect-type " + kConnectTypes[static_cast<size_t>(type)] +
+                " is not supported (nnsx implements TCP and HIPIPC)");
   return false;
 }
 
-// received blobs -> memories on the requested device (-1: pinned host)
+// received host blobs -> memories on the requested device (-1: keep them in
+// pinned host memory); ring blobs already live in HBM and stay zero-copy
 std::vector<MemoryPtr> place_blobs(std::vector<MemoryPtr> blobs, int device, StreamSet& streams) {
   if (device < 0) return blobs;
   hip::DeviceGuard g(device);
   hipStream_t s = streams.get(device);
   std::vector<MemoryPtr> out;
   for (auto& b : blobs) {
+    if (b->on_device()) {
+      out.push_back(b);
+      continue;
+    }
     auto d = Memory::alloc_device(b->size(), device, s);
     if (b->size())
       hip::check(hipMemcpyAsync(d->data(), b->data(), b->size(), hipMemcpyHostToDevice, s), "comm H2D");
@@ -324,6 +334,10 @@ class QueryClient : public Element {
     prop_uint("max-request", &max_request_, "Requests kept in flight before waiting for a reply");
     prop_int("device", &device_, "nnsx: upload replies to this GPU (-1 = pinned host memory)");
     prop_readonly("client-id", [this] { return std::to_string(conn_ ? conn_->id : 0); }, "Client id assigned by the server");
+    prop_readonly(
+        "ipc-blobs",
+        [this] { return conn_ ? strfmt(conn_->ipc_blobs_sent(), ":", conn_->ipc_blobs_received()) : std::string("0:0"); },
+        "nnsx: tensors sent:received through the HIPIPC device ring");
   }
 
   bool start() override {
@@ -341,6 +355,8 @@ class QueryClient : public Element {
       return false;
     }
     conn_->id = hello.client_id;
+    if (connect_type_ == kHipIpc && !conn_->send_ipc_hello())
+      NNSX_LOGW(name(), "HIPIPC: no GPU here, requests travel as bytes");
     server_caps_ = hello.caps.empty() ? Caps::from_string(tensor_caps_template_all()) : Caps::from_string(hello.caps);
     pending_.clear();
     seq_ = 0;
@@ -479,7 +495,15 @@ class EdgeSink : public BaseSink {
         hello.type = comm::MsgType::HELLO;
         std::lock_guard<std::mutex> lk(mu_);
         hello.caps = caps_str_;
-        if (c->send(hello)) subs_.push_back(c);
+        if (c->send(hello)) {
+          subs_.push_back(c);
+          // subscribers only talk control traffic (IPC handshake, ring ACKs): drain it
+          readers_.emplace_back([this, c] {
+            comm::Message m;
+            bool to = false;
+            while (running_ && c->alive()) (void)c->recv(&m, 100, &to);
+          });
+        }
         cv_.notify_all();
       }
     });
@@ -489,9 +513,15 @@ class EdgeSink : public BaseSink {
     running_ = false;
     listener_.close();
     if (accept_thr_.joinable()) accept_thr_.join();
-    std::lock_guard<std::mutex> lk(mu_);
-    for (auto& c : subs_) c->close();
-    subs_.clear();
+    std::vector<std::thread> rs;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      for (auto& c : subs_) c->close();
+      subs_.clear();
+      rs.swap(readers_);
+    }
+    for (auto& t : rs)
+      if (t.joinable()) t.join();
     return true;
   }
   void unlock() override {
@@ -552,6 +582,7 @@ class EdgeSink : public BaseSink {
   std::atomic<bool> running_{false};
   bool waited_ = false;
   std::thread accept_thr_;
+  std::vector<std::thread> readers_;
   std::mutex mu_;
   std::condition_variable cv_;
   std::vector<std::shared_ptr<comm::Connection>> subs_;
@@ -569,6 +600,8 @@ class EdgeSrc : public BaseSrc {
     prop_enum("connect-type", &connect_type_, kConnectTypes, "The connections type between edgesink and edgesrc");
     prop_string("topic", &topic_, "The main topic of the host");
     prop_int("device", &device_, "nnsx: upload received tensors to this GPU (-1 = pinned host memory)");
+    prop_readonly("ipc-blobs", [this] { return std::to_string(conn_ ? conn_->ipc_blobs_received() : 0); },
+                  "nnsx: tensors received through the HIPIPC device ring");
     is_live_ = true;
   }
 
@@ -600,6 +633,7 @@ class EdgeSrc : public BaseSrc {
         if (timed_out && !flushing_.load()) continue;
         return false;
       }
+      if (m.type == comm::MsgType::HELLO && connect_type_ == kHipIpc) conn_->send_ipc_hello();
       if ((m.type == comm::MsgType::HELLO || m.type == comm::MsgType::CAPS) && !m.caps.empty()) caps_str_ = m.caps;
       if (m.type == comm::MsgType::EOS) return false;
     }
