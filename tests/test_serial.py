@@ -1,0 +1,122 @@
+"""protobuf / flatbuf / flexbuf decoders and converters (reference
+tests/nnstreamer_{protobuf,flatbuf,flexbuf}/runTest.sh: tensors -> wire format
+-> tensors must reproduce the raw frames).  Protobuf parity is pinned against
+the Python protobuf runtime with the reference schema (nnstreamer.proto)
+built at test time; flatbuf / flexbuf parity is round-trip only (no
+flatbuffers library in this image: parity unpinned)."""
+import numpy as np
+import pytest
+
+WIRES = [("protobuf", "other/protobuf-tensor"), ("flatbuf", "other/flatbuf-tensor"), ("flexbuf", "other/flexbuf")]
+
+
+def _collect(nns, desc, n=1):
+    p = nns.parse_launch(desc)
+    outs = []
+    p.get_by_name("sink").connect("new-data", lambda b: outs.append([b.memory(i).bytes() for i in range(b.n_memory)]))
+    p.run(timeout=30)
+    return outs
+
+
+@pytest.mark.parametrize("mode,caps", WIRES)
+@pytest.mark.parametrize("fmt,w,h", [("RGB", 320, 240), ("BGRx", 64, 48), ("GRAY8", 33, 17)])
+def test_roundtrip_video(nns, mode, caps, fmt, w, h):
+    src = f"videotestsrc num-buffers=3 pattern=13 ! video/x-raw,format={fmt},width={w},height={h},framerate=5/1 ! tensor_converter"
+    direct = _collect(nns, f"{src} ! tensor_sink name=sink")
+    via = _collect(nns, f"{src} ! tensor_decoder mode={mode} ! {caps} ! tensor_converter ! tensor_sink name=sink")
+    assert len(direct) == len(via) == 3
+    assert direct == via
+
+
+@pytest.mark.parametrize("mode,caps", WIRES)
+def test_roundtrip_multi_tensor_and_caps(nns, mode, caps):
+    desc = (f"tensor_mux name=mux ! tensor_decoder mode={mode} ! {caps} ! tensor_converter ! tensor_sink name=sink "
+            "videotestsrc num-buffers=2 pattern=snow ! video/x-raw,format=RGB,width=8,height=4,framerate=5/1 "
+            "! tensor_converter ! mux.sink_0 "
+            "audiotestsrc num-buffers=2 samplesperbuffer=100 ! audio/x-raw,format=S16LE,channels=1,rate=500 "
+            "! tensor_converter frames-per-tensor=100 ! mux.sink_1")
+    p = nns.parse_launch(desc)
+    got = []
+    p.get_by_name("sink").connect("new-data", lambda b: got.append(b))
+    p.run(timeout=30)
+    assert len(got) == 2
+    caps_str = str(p.get_by_name("sink").pad_caps("sink"))
+    assert "num_tensors=(int)2" in caps_str and "uint8,int16" in caps_str and "3:8:4:1" in caps_str, caps_str
+    assert got[0].memory(0).size == 96 and got[0].memory(1).size == 200
+
+
+def _pb_classes():
+    from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
+
+    fd = descriptor_pb2.FileDescriptorProto(name="nnstreamer_test.proto", package="nnstreamer.protobuf", syntax="proto3")
+    t = fd.message_type.add(name="Tensor")
+    t.field.add(name="name", number=1, type=9, label=1)
+    en = t.enum_type.add(name="Tensor_type")
+    for i, n in enumerate(["NNS_INT32", "NNS_UINT32", "NNS_INT16", "NNS_UINT16", "NNS_INT8", "NNS_UINT8",
+                           "NNS_FLOAT64", "NNS_FLOAT32", "NNS_INT64", "NNS_UINT64"]):
+        en.value.add(name=n, number=i)
+    t.field.add(name="type", number=2, type=14, label=1, type_name=".nnstreamer.protobuf.Tensor.Tensor_type")
+    t.field.add(name="dimension", number=3, type=13, label=3)
+    t.field.add(name="data", number=4, type=12, label=1)
+    ts = fd.message_type.add(name="Tensors")
+    ts.field.add(name="num_tensor", number=1, type=13, label=1)
+    fr = ts.nested_type.add(name="frame_rate")
+    fr.field.add(name="rate_n", number=1, type=5, label=1)
+    fr.field.add(name="rate_d", number=2, type=5, label=1)
+    ts.field.add(name="fr", number=2, type=11, label=1, type_name=".nnstreamer.protobuf.Tensors.frame_rate")
+    ts.field.add(name="tensor", number=3, type=11, label=3, type_name=".nnstreamer.protobuf.Tensor")
+    ef = ts.enum_type.add(name="Tensor_format")
+    for i, n in enumerate(["NNS_TENSOR_FORAMT_STATIC", "NNS_TENSOR_FORMAT_FLEXIBLE", "NNS_TENSOR_FORMAT_SPARSE"]):
+        ef.value.add(name=n, number=i)
+    ts.field.add(name="format", number=4, type=14, label=1, type_name=".nnstreamer.protobuf.Tensors.Tensor_format")
+    pool = descriptor_pool.DescriptorPool()
+    pool.Add(fd)
+    return message_factory.GetMessageClass(pool.FindMessageTypeByName("nnstreamer.protobuf.Tensors"))
+
+
+def test_protobuf_bytes_match_protobuf_runtime(nns):
+    Tensors = _pb_classes()
+    out = _collect(nns, "videotestsrc num-buffers=1 pattern=snow ! video/x-raw,format=RGB,width=6,height=5,framerate=5/1 "
+                        "! tensor_converter ! tensor_decoder mode=protobuf ! tensor_sink name=sink")
+    blob = out[0][0]
+    msg = Tensors()
+    msg.ParseFromString(blob)
+    assert msg.num_tensor == 1 and msg.fr.rate_n == 5 and msg.fr.rate_d == 1
+    t = msg.tensor[0]
+    assert t.type == 5 and list(t.dimension)[:4] == [3, 6, 5, 1] and len(t.data) == 90
+    # canonical serialization by the protobuf runtime is byte-identical
+    assert msg.SerializeToString() == blob
+
+
+def test_protobuf_runtime_message_converts(nns):
+    Tensors = _pb_classes()
+    msg = Tensors(num_tensor=2, format=0)
+    msg.fr.rate_n, msg.fr.rate_d = 30, 1
+    a = np.arange(12, dtype=np.float32)
+    b = np.arange(6, dtype=np.int64) - 3
+    msg.tensor.add(name="a", type=7, dimension=[4, 3, 1, 1, 0, 0, 0, 0], data=a.tobytes())
+    msg.tensor.add(name="b", type=8, dimension=[6], data=b.tobytes())
+    p = nns.parse_launch("appsrc name=src caps=other/protobuf-tensor,framerate=30/1 ! tensor_converter "
+                         "! tensor_sink name=sink")
+    got = []
+    p.get_by_name("sink").connect("new-data", lambda buf: got.append(buf))
+    p.set_state("playing")
+    p.get_by_name("src").push_buffer(msg.SerializeToString(), pts=0)
+    p.get_by_name("src").end_of_stream()
+    assert p.wait(20)[0] == "eos"
+    caps = str(p.get_by_name("sink").pad_caps("sink"))
+    p.stop()
+    np.testing.assert_array_equal(got[0].memory(0).numpy("float32"), a)
+    np.testing.assert_array_equal(got[0].memory(1).numpy("int64"), b)
+    assert "float32,int64" in caps and "4:3" in caps and "framerate=(fraction)30/1" in caps, caps
+
+
+@pytest.mark.parametrize("mode,caps", WIRES)
+def test_malformed_input_errors(nns, mode, caps):
+    p = nns.parse_launch(f"appsrc name=src caps={caps},framerate=0/1 ! tensor_converter ! tensor_sink name=sink")
+    p.set_state("playing")
+    p.get_by_name("src").push_buffer(b"\x07\x01garbage-not-a-valid-frame", pts=0)
+    p.get_by_name("src").end_of_stream()
+    msg = p.wait(20)
+    p.stop()
+    assert msg and msg[0] == "error"
