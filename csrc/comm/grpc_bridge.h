@@ -1,0 +1,45 @@
+// gRPC endpoint interface for tensor_src_grpc / tensor_sink_grpc.
+//
+// The reference links grpc++ (ext/nnstreamer/extra/nnstreamer_grpc_*.cc);
+// no C++ gRPC library exists in this image, so the HTTP/2 transport is the
+// grpcio runtime, driven through the Python bridge
+// (nnstreamer_amd/comm/grpc_transport.py).  Everything else stays native:
+// the elements, the Tensors (de)serialization (serial/serial.h: protobuf or
+// flatbuf IDL bytes) and the service names / method paths:
+//   /nnstreamer.<idl>.TensorService/SendTensors  (client -> server stream)
+//   /nnstreamer.<idl>.TensorService/RecvTensors  (server -> client stream)
+#pragma once
+
+#include <functional>
+#include <memory>
+#include <string>
+
+namespace nnsx {
+namespace comm {
+
+struct GrpcOptions {
+  bool server = false;   // run the service (else call it)
+  bool sending = false;  // sink side (else source side)
+  std::string idl = "protobuf";
+  std::string host = "localhost";
+  int port = 55115;  // 0: ephemeral (server), read back with port()
+  bool blocking = true;
+};
+
+class GrpcEndpoint {
+ public:
+  virtual ~GrpcEndpoint() = default;
+  virtual bool start(std::string* err) = 0;
+  virtual bool send(const std::string& msg) = 0;
+  // 1: got a message, 0: timeout, -1: stream finished / endpoint stopped
+  virtual int recv(std::string* msg, int timeout_ms) = 0;
+  virtual void stop() = 0;
+  virtual int port() = 0;
+};
+
+using GrpcFactory = std::function<std::shared_ptr<GrpcEndpoint>(const GrpcOptions&)>;
+void set_grpc_factory(GrpcFactory f);
+GrpcFactory grpc_factory();  // empty when the bridge is not loaded
+
+}  // namespace comm
+}  // namespace nnsx

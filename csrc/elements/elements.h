@@ -10,7 +10,8 @@ void register_basic_elements();
 void register_tensor_elements();   // converter/transform/sink/mux/demux/merge/split/...
 void register_filter_elements();   // tensor_filter
 void register_decoder_elements();  // tensor_decoder
-void register_comm_elements();     // tensor_query_* / edge / mqtt-like
+void register_comm_elements();
+void register_grpc_elements();     // tensor_src_grpc / tensor_sink_grpc     // tensor_query_* / edge / mqtt-like
 void register_extra_elements();    // crop/if/rate/repo/sparse/debug/trainer/iio/join/datarepo
 
 // appsrc / appsink application API (implemented by the element classes)
