@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 STEP=${1:-all}
 if [ "$STEP" = "all" ] || [ "$STEP" = "test" ]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -50 gpurun_out/pytest_gpu.log; exit 1; }
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -50 gpurun_out/pytest_gpu.log; exit 1; }
   tail -5 gpurun_out/pytest_gpu.log
 fi
 if [ "$STEP" = "all" ] || [ "$STEP" = "bench" ]; then
