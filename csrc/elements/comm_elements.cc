@@ -18,9 +18,11 @@
 #include <map>
 #include <thread>
 
+#include "comm/group.h"
 #include "comm/transport.h"
 #include "core/log.h"
 #include "elements/elements.h"
+#include "elements/rank_props.h"
 #include "elements/tensor_common.h"
 #include "runtime/base.h"
 #include "runtime/hip_util.h"
@@ -30,14 +32,42 @@ namespace nnsx {
 
 namespace {
 
-const std::vector<std::string> kConnectTypes = {"TCP", "HYBRID", "MQTT", "AITT", "HIPIPC"};
+const std::vector<std::string> kConnectTypes = {"TCP", "HYBRID", "MQTT", "AITT", "HIPIPC", "RCCL"};
 constexpr int kHipIpc = 4;
+constexpr int kRccl = 5;
+const std::vector<std::string> kRcclModes = {"broadcast", "scatter"};
+constexpr uint32_t kPktCaps = 1;  // packet carries only a caps string
 
 bool check_connect_type(Element* e, int type) {
-  if (type == 0 || type == kHipIpc) return true;
+  if (type == 0 || type == kHipIpc || type == kRccl) return true;
   e->post_error("connect-type " + kConnectTypes[static_cast<size_t>(type)] +
-                " is not supported (nnsx implements TCP and HIPIPC)");
+                " is not supported (nnsx implements TCP, HIPIPC and RCCL)");
   return false;
+}
+
+// channel name shared by the two ends of a connect-type=RCCL link
+std::string rccl_channel(const char* kind, const std::string& topic, unsigned port) {
+  return strfmt(kind, ":", topic.empty() ? std::to_string(port) : topic);
+}
+
+std::vector<MemoryPtr> place_blobs(std::vector<MemoryPtr> blobs, int device, StreamSet& streams);
+
+comm::Packet packet_of(const Buffer& b) {
+  comm::Packet p;
+  p.pts = b.pts;
+  p.dts = b.dts;
+  p.duration = b.duration;
+  p.blobs = b.mems;
+  return p;
+}
+
+BufferPtr buffer_of(comm::Packet& p, int device, StreamSet& streams) {
+  auto b = make_buffer();
+  b->mems = place_blobs(std::move(p.blobs), device, streams);
+  b->pts = p.pts;
+  b->dts = p.dts;
+  b->duration = p.duration;
+  return b;
 }
 
 // received host blobs -> memories on the requested device (-1: keep them in
@@ -127,6 +157,12 @@ class QueryServer {
 
   comm::MessageQueue incoming;
 
+  // connect-type=RCCL: the serversrc's rank settings + channel, read by the
+  // paired serversink (requests and replies ride one group per direction)
+  std::mutex rank_mu;
+  RankProps rank;
+  std::string channel;
+
  private:
   void accept_loop() {
     while (running_) {
@@ -212,6 +248,7 @@ class QueryServerSrc : public BaseSrc {
     prop_string("topic", &topic_, "The main topic of the host (HYBRID/MQTT)");
     prop_uint("id", &id_, "ID shared with the paired tensor_query_serversink");
     prop_int("device", &device_, "nnsx: upload received tensors to this GPU (-1 = keep in pinned host memory)");
+    rp_.install([this](PropSpec p) -> PropSpec& { return add_prop(p); }, false);
     is_live_ = true;
   }
 
@@ -219,6 +256,13 @@ class QueryServerSrc : public BaseSrc {
   bool on_start() override {
     if (!check_connect_type(this, connect_type_)) return false;
     server_ = query_server(static_cast<int>(id_));
+    if (connect_type_ == kRccl) {
+      rp_.device = device_;
+      std::lock_guard<std::mutex> lk(server_->rank_mu);
+      server_->rank = rp_;
+      server_->channel = rccl_channel("query", topic_, static_cast<unsigned>(port_));
+      return true;
+    }
     std::string err;
     if (!server_->start(host_, port_, &err)) {
       post_error("tensor_query_serversrc: " + err);
@@ -228,13 +272,36 @@ class QueryServerSrc : public BaseSrc {
     return true;
   }
   void on_stop() override {
-    if (server_) server_->stop();
+    if (server_ && connect_type_ != kRccl) server_->stop();
+    req_.reset();
   }
   void on_unlock() override {
     if (server_) server_->incoming.set_flushing(true);
+    if (auto g = req_) g->cancel();
   }
 
   FlowReturn create(BufferPtr* out) override {
+    if (connect_type_ == kRccl) {
+      if (!req_ && !(req_ = rp_.open(this, server_->channel + "/req"))) return FlowReturn::ERROR;
+      comm::Packet p;
+      std::string err;
+      const int64_t t0 = now_ns();
+      while (true) {
+        bool to = false;
+        if (req_->recv(&p, 100, &to, &err)) break;
+        if (flushing_.load()) return FlowReturn::FLUSHING;
+        if (!to) {
+          post_error("tensor_query_serversrc: " + err);
+          return FlowReturn::ERROR;
+        }
+        if (timeout_ms_ > 0 && now_ns() - t0 > static_cast<int64_t>(timeout_ms_) * 1000000) return FlowReturn::EOS;
+      }
+      if (p.eos) return create(out);  // a client left; keep serving the others
+      const uint64_t cid = static_cast<uint64_t>(p.src) + 1;
+      *out = buffer_of(p, device_, streams_);
+      (*out)->meta.client_id = cid;
+      return FlowReturn::OK;
+    }
     comm::Message m;
     const int64_t t0 = now_ns();
     while (true) {
@@ -259,6 +326,8 @@ class QueryServerSrc : public BaseSrc {
   int connect_type_ = 0, device_ = -1;
   std::shared_ptr<QueryServer> server_;
   StreamSet streams_;
+  RankProps rp_;
+  std::shared_ptr<comm::Group> req_;
 };
 
 // -------------------------------------------------------- serversink ----
@@ -287,11 +356,47 @@ class QueryServerSink : public BaseSink {
     return check_connect_type(this, connect_type_);
   }
   bool set_caps(const Caps& caps) override {
+    if (connect_type_ == kRccl) {
+      if (!open_rep()) return false;
+      // clients read the server's output caps from the group store
+      return rep_->put("caps", caps.to_string());
+    }
     server_->set_sink_caps(caps.to_string());
     return true;
   }
+  bool stop() override {
+    rep_.reset();
+    return true;
+  }
+  void unlock() override {
+    if (auto g = rep_) g->cancel();
+  }
+  bool open_rep() {
+    if (rep_) return true;
+    RankProps rp;
+    std::string ch;
+    {
+      std::lock_guard<std::mutex> lk(server_->rank_mu);
+      rp = server_->rank;
+      ch = server_->channel;
+    }
+    if (ch.empty()) {
+      post_error("tensor_query_serversink: no connect-type=RCCL tensor_query_serversrc with the same id");
+      return false;
+    }
+    return (rep_ = rp.open(this, ch + "/rep")) != nullptr;
+  }
   FlowReturn render(const BufferPtr& buf) override {
     const uint64_t cid = buf->meta.client_id;
+    if (connect_type_ == kRccl && cid != 0) {
+      metaless_ = 0;
+      std::string err;
+      if (!open_rep() || !rep_->send(static_cast<int>(cid - 1), packet_of(*buf), &err)) {
+        post_error("tensor_query_serversink: " + err);
+        return FlowReturn::ERROR;
+      }
+      return FlowReturn::OK;
+    }
     if (cid == 0) {
       if (++metaless_ > limit_) {
         post_error("tensor_query_serversink: too many frames without a query client id");
@@ -315,6 +420,7 @@ class QueryServerSink : public BaseSink {
   int connect_type_ = 0;
   unsigned timeout_ms_ = 0, id_ = 0, limit_ = 1, metaless_ = 0;
   std::shared_ptr<QueryServer> server_;
+  std::shared_ptr<comm::Group> rep_;
 };
 
 // ------------------------------------------------------------ client ----
@@ -338,10 +444,14 @@ class QueryClient : public Element {
         "ipc-blobs",
         [this] { return conn_ ? strfmt(conn_->ipc_blobs_sent(), ":", conn_->ipc_blobs_received()) : std::string("0:0"); },
         "nnsx: tensors sent:received through the HIPIPC device ring");
+    rp_.install([this](PropSpec p) -> PropSpec& { return add_prop(p); }, false);
   }
 
   bool start() override {
     if (!check_connect_type(this, connect_type_)) return false;
+    pending_.clear();
+    seq_ = 0;
+    if (connect_type_ == kRccl) return true;
     std::string err;
     conn_ = comm::Connection::connect(dest_host_, static_cast<int>(dest_port_),
                                       timeout_ms_ ? static_cast<int>(timeout_ms_) : 10000, &err);
@@ -370,13 +480,54 @@ class QueryClient : public Element {
       conn_->close();
       conn_.reset();
     }
+    req_.reset();
+    rep_.reset();
+    have_server_caps_ = false;
     return true;
   }
   void unlock() override {
     if (conn_) conn_->close();
+    if (auto g = req_) g->cancel();
+    if (auto g = rep_) g->cancel();
+  }
+
+  // connect-type=RCCL: join the request / reply groups and read the server's caps
+  bool open_rccl() {
+    if (req_) return true;
+    rp_.device = device_;
+    const std::string ch = rccl_channel("query", topic_, dest_port_);
+    // same order as the server: its serversink joins "rep" while the caps
+    // event travels (on the serversrc thread), before serversrc joins "req"
+    if (!(rep_ = rp_.open(this, ch + "/rep")) || !(req_ = rp_.open(this, ch + "/req"))) return false;
+    server_ = rp_.peer_in(*req_);
+    if (server_ < 0 || server_ == req_->rank()) {
+      post_error("tensor_query_client: peer-rank is not another member of the group");
+      return false;
+    }
+    std::string caps;
+    if (!rep_->get("caps", &caps, static_cast<int>(rp_.timeout_ms))) {
+      post_error("tensor_query_client: the server published no caps");
+      return false;
+    }
+    server_caps_ = Caps::from_string(caps);
+    have_server_caps_ = true;
+    return true;
   }
 
   bool sink_event(Pad*, Event& ev) override {
+    if (ev.type == EventType::CAPS && connect_type_ == kRccl) {
+      if (!open_rccl()) return false;
+      return src_pad()->push_event(Event::make_caps(server_caps_));
+    }
+    if (ev.type == EventType::EOS && connect_type_ == kRccl && req_) {
+      if (!flow_ok(drain(0))) return false;
+      // tell the server this client is done (it keeps serving the others)
+      comm::Packet bye;
+      bye.eos = true;
+      std::string err;
+      req_->send(server_, bye, &err);
+      return forward_event_downstream(ev);
+    }
     if (ev.type == EventType::CAPS) {
       comm::Message m;
       m.type = comm::MsgType::CAPS;
@@ -391,11 +542,21 @@ class QueryClient : public Element {
   }
 
   Caps query_caps(Pad* pad, const Caps* filter) override {
-    Caps c = pad->direction() == PadDirection::SRC && conn_ ? server_caps_ : pad->template_caps();
+    Caps c = pad->direction() == PadDirection::SRC && (conn_ || have_server_caps_) ? server_caps_ : pad->template_caps();
     return filter ? c.intersect(*filter) : c;
   }
 
   FlowReturn chain(Pad*, BufferPtr buf) override {
+    if (connect_type_ == kRccl) {
+      std::string err;
+      if (!open_rccl()) return FlowReturn::ERROR;
+      if (!req_->send(server_, packet_of(*buf), &err)) {
+        post_error("tensor_query_client: " + err);
+        return FlowReturn::ERROR;
+      }
+      pending_.push_back(buf);
+      return drain(std::max(1u, max_request_) - 1);
+    }
     if (!conn_) return FlowReturn::ERROR;
     comm::Message m;
     m.type = comm::MsgType::DATA;
@@ -416,6 +577,23 @@ class QueryClient : public Element {
  private:
   // receive replies until at most `keep` requests remain in flight
   FlowReturn drain(size_t keep) {
+    while (rep_ && pending_.size() > keep) {
+      comm::Packet r;
+      bool timed_out = false;
+      std::string err;
+      const int t = timeout_ms_ ? static_cast<int>(timeout_ms_) : -1;
+      if (!rep_->recv(&r, t, &timed_out, &err)) {
+        post_error(timed_out ? "tensor_query_client: timed out waiting for the server"
+                             : "tensor_query_client: " + err);
+        return FlowReturn::ERROR;
+      }
+      BufferPtr in = pending_.front();
+      pending_.pop_front();
+      auto out = buffer_of(r, device_, streams_);
+      out->copy_metadata_from(*in);
+      FlowReturn fr = src_pad()->push(out);
+      if (!flow_ok(fr)) return fr;
+    }
     while (pending_.size() > keep) {
       comm::Message r;
       bool timed_out = false;
@@ -446,6 +624,10 @@ class QueryClient : public Element {
   std::deque<BufferPtr> pending_;
   uint64_t seq_ = 0;
   StreamSet streams_;
+  RankProps rp_;
+  std::shared_ptr<comm::Group> req_, rep_;
+  int server_ = 0;  // server's rank inside the request / reply groups
+  bool have_server_caps_ = false;
 };
 
 // ============================================================== edgesink ====
@@ -475,12 +657,21 @@ class EdgeSink : public BaseSink {
     a.get = [] { return std::string("false"); };
     add_prop(a);
     prop_readonly("subscribers", [this] { return std::to_string(subscribers()); }, "Connected subscribers");
+    rp_.install([this](PropSpec p) -> PropSpec& { return add_prop(p); });
+    prop_enum("rccl-mode", &rccl_mode_, kRcclModes,
+              "nnsx (connect-type=RCCL): broadcast every frame to all subscribers, or scatter frames round-robin");
+    prop_readonly("comm-bytes", [this] { return std::to_string(g_ ? g_->bytes_sent() : 0); },
+                  "nnsx: payload bytes published on the rank group");
   }
 
  protected:
   bool start() override {
     BaseSink::start();
     if (!check_connect_type(this, connect_type_)) return false;
+    if (connect_type_ == kRccl) {
+      running_ = true;
+      return true;
+    }
     std::string err;
     if (!listener_.listen(host_, port_, &err)) {
       post_error("edgesink: " + err);
@@ -511,6 +702,7 @@ class EdgeSink : public BaseSink {
   }
   bool stop() override {
     running_ = false;
+    g_.reset();
     listener_.close();
     if (accept_thr_.joinable()) accept_thr_.join();
     std::vector<std::thread> rs;
@@ -527,8 +719,16 @@ class EdgeSink : public BaseSink {
   void unlock() override {
     running_ = false;
     cv_.notify_all();
+    if (auto g = g_) g->cancel();
   }
   bool set_caps(const Caps& caps) override {
+    if (connect_type_ == kRccl) {
+      if (!g_ && !(g_ = rp_.open(this, rccl_channel("edge", topic_, static_cast<unsigned>(port_))))) return false;
+      comm::Packet p;
+      p.caps = caps.to_string();
+      p.flags = kPktCaps;
+      return publish_rccl(p, true);
+    }
     comm::Message m;
     m.type = comm::MsgType::CAPS;
     std::lock_guard<std::mutex> lk(mu_);
@@ -538,6 +738,10 @@ class EdgeSink : public BaseSink {
     return true;
   }
   FlowReturn render(const BufferPtr& buf) override {
+    if (connect_type_ == kRccl) {
+      if (!g_) return FlowReturn::NOT_NEGOTIATED;
+      return publish_rccl(packet_of(*buf), false) ? FlowReturn::OK : FlowReturn::ERROR;
+    }
     if (wait_subscribers_ > 0 && !waited_) {
       std::unique_lock<std::mutex> lk(mu_);
       cv_.wait_for(lk, std::chrono::milliseconds(wait_timeout_ms_),
@@ -554,12 +758,38 @@ class EdgeSink : public BaseSink {
     return FlowReturn::OK;
   }
   void on_eos() override {
+    if (connect_type_ == kRccl) {
+      if (!g_) return;
+      comm::Packet p;
+      p.eos = true;
+      publish_rccl(p, true);
+      return;
+    }
     comm::Message m;
     m.type = comm::MsgType::EOS;
     publish(m);
   }
 
  private:
+  // broadcast: one collective per frame, root = this publisher; scatter:
+  // frames round-robin over the other members, control packets to all
+  bool publish_rccl(comm::Packet p, bool control) {
+    std::string err;
+    bool ok = true;
+    if (rccl_mode_ == 0) {
+      ok = g_->broadcast(g_->rank(), &p, &err);
+    } else if (control) {
+      for (int r = 0; r < g_->size() && ok; ++r)
+        if (r != g_->rank()) ok = g_->send(r, p, &err);
+    } else if (g_->size() > 1) {
+      int r = static_cast<int>(rr_++ % static_cast<unsigned>(g_->size() - 1));
+      if (r >= g_->rank()) ++r;
+      ok = g_->send(r, p, &err);
+    }
+    if (!ok && running_) post_error("edgesink: " + err);
+    return ok;
+  }
+
   void publish(const comm::Message& m) {
     std::vector<std::shared_ptr<comm::Connection>> subs;
     {
@@ -587,6 +817,10 @@ class EdgeSink : public BaseSink {
   std::condition_variable cv_;
   std::vector<std::shared_ptr<comm::Connection>> subs_;
   std::string caps_str_;
+  RankProps rp_;
+  int rccl_mode_ = 0;
+  unsigned rr_ = 0;
+  std::shared_ptr<comm::Group> g_;
 };
 
 // =============================================================== edgesrc ====
@@ -602,12 +836,18 @@ class EdgeSrc : public BaseSrc {
     prop_int("device", &device_, "nnsx: upload received tensors to this GPU (-1 = pinned host memory)");
     prop_readonly("ipc-blobs", [this] { return std::to_string(conn_ ? conn_->ipc_blobs_received() : 0); },
                   "nnsx: tensors received through the HIPIPC device ring");
+    rp_.install([this](PropSpec p) -> PropSpec& { return add_prop(p); }, false);
+    prop_enum("rccl-mode", &rccl_mode_, kRcclModes, "nnsx (connect-type=RCCL): must match the publishing edgesink");
+    prop_readonly("comm-bytes", [this] { return std::to_string(g_ ? g_->bytes_received() : 0); },
+                  "nnsx: payload bytes received on the rank group");
     is_live_ = true;
   }
 
  protected:
   bool on_start() override {
     if (!check_connect_type(this, connect_type_)) return false;
+    caps_str_.clear();
+    if (connect_type_ == kRccl) return true;
     std::string err;
     conn_ = comm::Connection::connect(dest_host_, static_cast<int>(dest_port_), 10000, &err);
     if (!conn_) {
@@ -619,13 +859,47 @@ class EdgeSrc : public BaseSrc {
   }
   void on_stop() override {
     if (conn_) conn_->close();
+    g_.reset();
   }
   void on_unlock() override {
     if (conn_) conn_->close();
+    if (auto g = g_) g->cancel();
+  }
+
+  // connect-type=RCCL: next packet from the publisher (false: cancelled / lost)
+  bool recv_rccl(comm::Packet* p) {
+    std::string err;
+    if (rccl_mode_ == 0) {
+      const int root = rp_.peer_in(*g_);
+      if (root < 0 || root == g_->rank()) {
+        post_error("edgesrc: peer-rank is not another member of the group");
+        return false;
+      }
+      *p = comm::Packet();
+      if (g_->broadcast(root, p, &err)) return true;
+    } else {
+      while (!flushing_.load()) {
+        bool to = false;
+        if (g_->recv(p, 100, &to, &err)) return true;
+        if (!to) break;
+      }
+    }
+    if (!flushing_.load() && !err.empty()) post_error("edgesrc: " + err);
+    return false;
   }
 
   // the publisher's caps arrive with HELLO (or a later CAPS message)
   bool negotiate() override {
+    if (connect_type_ == kRccl) {
+      rp_.device = device_;
+      if (!g_ && !(g_ = rp_.open(this, rccl_channel("edge", topic_, dest_port_)))) return false;
+      while (caps_str_.empty()) {
+        comm::Packet p;
+        if (!recv_rccl(&p) || p.eos) return false;
+        if (!p.caps.empty()) caps_str_ = p.caps;
+      }
+      return BaseSrc::negotiate();
+    }
     while (caps_str_.empty()) {
       comm::Message m;
       bool timed_out = false;
@@ -645,6 +919,20 @@ class EdgeSrc : public BaseSrc {
   }
 
   FlowReturn create(BufferPtr* out) override {
+    while (connect_type_ == kRccl) {
+      comm::Packet p;
+      if (!recv_rccl(&p)) return flushing_.load() ? FlowReturn::FLUSHING : FlowReturn::ERROR;
+      if (p.eos) return FlowReturn::EOS;
+      if (p.flags & kPktCaps) {
+        if (p.caps != caps_str_) {
+          caps_str_ = p.caps;
+          src_pad()->push_event(Event::make_caps(Caps::from_string(caps_str_)));
+        }
+        continue;
+      }
+      *out = buffer_of(p, device_, streams_);
+      return FlowReturn::OK;
+    }
     while (true) {
       comm::Message m;
       bool timed_out = false;
@@ -676,11 +964,183 @@ class EdgeSrc : public BaseSrc {
   std::shared_ptr<comm::Connection> conn_;
   std::string caps_str_;
   StreamSet streams_;
+  RankProps rp_;
+  int rccl_mode_ = 0;
+  std::shared_ptr<comm::Group> g_;
+};
+
+// ====================================================== tensor_allgather ====
+// N-rank fan-in with every rank receiving every stream (nnsx; the reference
+// has no cross-process mux -- tensor_mux over edge/query sockets is the
+// closest: nnstreamer_plugin_api_impl.c:266-441).  Each member contributes
+// its frame; the output carries all members' tensors in member order:
+//   mode=concat: num_tensors adds up (like tensor_mux),
+//   mode=stack:  one tensor per member, joined along `axis` (like
+//                tensor_merge); the joined tensor IS the ncclAllGather output.
+// Caps, frames and EOS are one collective each, so members stay in lock step;
+// the first EOS of any member ends the stream on every member.
+class TensorAllGather : public Element {
+ public:
+  explicit TensorAllGather(const std::string& name) : Element("tensor_allgather", name) {
+    add_template("sink", PadDirection::SINK, PadPresence::ALWAYS, Caps::from_string(tensor_caps_template_static()));
+    add_template("src", PadDirection::SRC, PadPresence::ALWAYS, Caps::from_string(tensor_caps_template_static()));
+    rp_.install([this](PropSpec p) -> PropSpec& { return add_prop(p); });
+    prop_string("channel", &channel_, "nnsx: group name shared by the members");
+    prop_enum("mode", &mode_, {"concat", "stack"}, "concat: append every member's tensors; stack: join along axis");
+    prop_int("axis", &axis_, "stack: axis to join along (every dim above it must be 1)");
+    prop_readonly("comm-bytes",
+                  [this] { return g_ ? strfmt(g_->bytes_sent(), ":", g_->bytes_received()) : std::string("0:0"); },
+                  "nnsx: payload bytes sent:received on the rank group");
+  }
+
+  bool stop() override {
+    g_.reset();
+    done_ = false;
+    return true;
+  }
+  void unlock() override {
+    if (auto g = g_) g->cancel();
+  }
+
+  Caps query_caps(Pad* pad, const Caps* filter) override {
+    Caps c = pad->direction() == PadDirection::SRC && have_out_ ? out_caps_ : pad->template_caps();
+    return filter ? c.intersect(*filter) : c;
+  }
+
+  bool sink_event(Pad*, Event& ev) override {
+    if (ev.type == EventType::CAPS) {
+      TensorsConfig in;
+      if (!tensor_config_from_caps(ev.caps, &in) || !in.is_static()) {
+        post_error("tensor_allgather: static tensor caps required");
+        return false;
+      }
+      if (!g_ && !(g_ = rp_.open(this, "allgather:" + channel_))) return false;
+      comm::Packet p;
+      p.caps = ev.caps.to_string();
+      p.flags = kPktCaps;
+      std::vector<comm::Packet> all;
+      std::string err;
+      if (!g_->allgather(p, &all, &err)) {
+        post_error("tensor_allgather: " + err);
+        return false;
+      }
+      TensorsConfig out;
+      if (!merge_configs(all, &out)) return false;
+      out_caps_ = tensor_src_caps(src_pad(), out);
+      have_out_ = true;
+      return src_pad()->push_event(Event::make_caps(out_caps_));
+    }
+    if (ev.type == EventType::EOS) {
+      if (g_ && !done_) {
+        comm::Packet p;
+        p.eos = true;
+        std::vector<comm::Packet> all;
+        std::string err;
+        g_->allgather(p, &all, &err);
+        done_ = true;
+      }
+      return forward_event_downstream(ev);
+    }
+    return forward_event_downstream(ev);
+  }
+
+  FlowReturn chain(Pad*, BufferPtr buf) override {
+    if (done_) return FlowReturn::EOS;
+    if (!g_) return FlowReturn::NOT_NEGOTIATED;
+    std::vector<comm::Packet> all;
+    std::string err;
+    MemoryPtr stacked;
+    if (!g_->allgather(packet_of(*buf), &all, &err, mode_ == 1 ? &stacked : nullptr)) {
+      post_error("tensor_allgather: " + err);
+      return FlowReturn::ERROR;
+    }
+    for (auto& p : all)
+      if (p.eos) {
+        // another member finished: end here too (its EOS round is this one)
+        done_ = true;
+        Event eos = Event::make_eos();
+        src_pad()->push_event(eos);
+        return FlowReturn::EOS;
+      }
+    auto out = make_buffer();
+    out->copy_metadata_from(*buf);
+    if (mode_ == 1) {
+      if (!stacked) {
+        post_error("tensor_allgather: mode=stack needs one equal-size tensor per member");
+        return FlowReturn::ERROR;
+      }
+      out->mems.push_back(stacked);
+    } else {
+      for (auto& p : all)
+        for (auto& m : p.blobs) out->mems.push_back(m);
+    }
+    return src_pad()->push(out);
+  }
+
+ private:
+  bool merge_configs(const std::vector<comm::Packet>& all, TensorsConfig* out) {
+    std::vector<TensorsConfig> cfgs;
+    for (auto& p : all) {
+      TensorsConfig c;
+      if (!tensor_config_from_caps(Caps::from_string(p.caps), &c) || !c.is_static()) {
+        post_error("tensor_allgather: member " + std::to_string(p.src) + " has no static tensor caps");
+        return false;
+      }
+      cfgs.push_back(c);
+    }
+    out->rate_n = cfgs[0].rate_n;
+    out->rate_d = cfgs[0].rate_d;
+    if (mode_ == 0) {
+      unsigned n = 0;
+      for (auto& c : cfgs) n += c.info.num_tensors;
+      if (n > static_cast<unsigned>(kSizeLimit)) {
+        post_error("tensor_allgather: more than 16 tensors in total; use mode=stack");
+        return false;
+      }
+      out->info.resize(n);
+      unsigned k = 0;
+      for (auto& c : cfgs)
+        for (unsigned i = 0; i < c.info.num_tensors; ++i) out->info.at(k++) = c.info.at(i);
+      return true;
+    }
+    if (axis_ < 0 || axis_ >= kRankLimit) {
+      post_error("tensor_allgather: axis out of range");
+      return false;
+    }
+    TensorInfo o = cfgs[0].info.at(0);
+    for (auto& c : cfgs) {
+      const TensorInfo& t = c.info.at(0);
+      bool ok = c.info.num_tensors == 1 && t.type == o.type;
+      for (int d = 0; d < kRankLimit && ok; ++d) {
+        if (d > axis_) ok = t.dim[d] == 1;
+        else if (d < axis_) ok = t.dim[d] == o.dim[d];
+      }
+      ok = ok && t.dim[axis_] == o.dim[axis_];
+      if (!ok) {
+        post_error("tensor_allgather: mode=stack needs one tensor per member, equal shape and type, "
+                   "and dims above `axis` equal to 1");
+        return false;
+      }
+    }
+    o.dim[axis_] *= static_cast<uint32_t>(cfgs.size());
+    out->info.resize(1);
+    out->info.at(0) = o;
+    return true;
+  }
+
+  RankProps rp_;
+  std::string channel_ = "default";
+  int mode_ = 0, axis_ = 3;
+  std::shared_ptr<comm::Group> g_;
+  bool done_ = false, have_out_ = false;
+  Caps out_caps_;
 };
 
 }  // namespace
 
 void register_comm_elements() {
+  register_element("tensor_allgather", "Muxer/Tensor/Rank", "Gathers every rank's tensors on every rank (RCCL all-gather)",
+                   [](const std::string& n) { return std::make_unique<TensorAllGather>(n); });
   register_element("tensor_query_serversrc", "Source/Tensor/Query", "Receives tensors from query clients",
                    [](const std::string& n) { return std::make_unique<QueryServerSrc>(n); });
   register_element("tensor_query_serversink", "Sink/Tensor/Query", "Sends results back to the query clients",

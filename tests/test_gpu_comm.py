@@ -119,3 +119,32 @@ def test_edge_hipipc_pubsub(nns):
     assert msg and msg[0] == "eos", sub.messages()
     assert got == [float(i) for i in range(8)]
     assert n_ipc == 8
+
+
+def test_allgather_rccl_single_member(nns):
+    """connect-type RCCL plumbing on one GPU: an RCCL communicator of one rank
+    (ncclCommInitRank + comm stream), tensors stay in HBM end to end."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    p = nns.parse_launch(
+        f"appsrc name=src caps={CAPS} ! tensor_transform mode=arithmetic option=mul:2 device=0 "
+        f"! tensor_allgather name=ag rank=0 world-size=1 device=0 comm-backend=rccl store=127.0.0.1:{port} mode=stack axis=1 "
+        "! tensor_sink name=sink")
+    out = []
+    p.get_by_name("sink").connect("new-data", lambda b: out.append(
+        (b.memory(0).on_device, b.memory(0).numpy("float32").copy())))
+    p.set_state("playing")
+    frames = [np.arange(N, dtype=np.float32) + i for i in range(3)]
+    for i, f in enumerate(frames):
+        p.get_by_name("src").push_buffer(f, pts=i)
+    p.get_by_name("src").end_of_stream()
+    msg = p.wait(60)
+    p.stop()
+    assert msg and msg[0] == "eos", p.messages()
+    assert len(out) == 3
+    for (on_dev, y), x in zip(out, frames):
+        assert on_dev
+        np.testing.assert_array_equal(y, 2 * x)

@@ -1,0 +1,177 @@
+"""Rank-group elements (connect-type=RCCL edge / query, tensor_allgather).
+
+On CPU the groups run with comm-backend=tcp (payload inline in the control
+store), so the same element logic -- collective ordering, caps exchange,
+client-id routing, EOS rounds -- is exercised without GPUs.  Ranks are
+simulated in one process with explicit rank= / world-size= properties, plus
+one multi-process case launched like torchrun (RANK / WORLD_SIZE /
+MASTER_ADDR / MASTER_PORT).  The RCCL data plane is covered by
+tests/test_gpu_comm.py (one GPU: single-member groups) and by the
+multi-GPU bench."""
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+
+import numpy as np
+import pytest
+
+F32 = "other/tensors,format=static,num_tensors=1,dimensions=4,types=float32,framerate=0/1"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank(k, n, store, extra=""):
+    return f"rank={k} world-size={n} store=127.0.0.1:{store} comm-backend=tcp comm-timeout=20000 {extra}"
+
+
+def _collect(p, name="sink"):
+    out = []
+    p.get_by_name(name).connect("new-data", lambda b: out.append(
+        (b.pts, [b.memory(i).numpy("float32").copy() for i in range(b.n_memory)])))
+    return out
+
+
+def _push(p, frames, src="src"):
+    for i, f in enumerate(frames):
+        p.get_by_name(src).push_buffer(f, pts=100 + i)
+    p.get_by_name(src).end_of_stream()
+
+
+def _wait_eos(p, t=30):
+    msg = p.wait(t)
+    assert msg and msg[0] == "eos", p.messages()
+
+
+@pytest.mark.parametrize("mode", ["broadcast", "scatter"])
+def test_edge_rank_group(nns, mode):
+    store = _free_port()
+    n = 3
+    pub = nns.parse_launch(f"appsrc name=src caps={F32} ! edgesink connect-type=RCCL topic=e-{mode} "
+                           f"rccl-mode={mode} {_rank(0, n, store)}")
+    subs, outs = [], []
+    for k in range(1, n):
+        s = nns.parse_launch(f"edgesrc connect-type=RCCL topic=e-{mode} rccl-mode={mode} {_rank(k, n, store)} "
+                             "! tensor_sink name=sink")
+        outs.append(_collect(s))
+        s.set_state("playing")
+        subs.append(s)
+    pub.set_state("playing")
+    frames = [np.full(4, i, np.float32) for i in range(6)]
+    _push(pub, frames)
+    _wait_eos(pub)
+    for s in subs:
+        _wait_eos(s)
+        s.stop()
+    pub.stop()
+    got = [[float(m[0][0]) for _, m in o] for o in outs]
+    if mode == "broadcast":
+        assert got == [[float(i) for i in range(6)]] * 2
+    else:  # round-robin over the two subscribers
+        assert got == [[0.0, 2.0, 4.0], [1.0, 3.0, 5.0]]
+        assert [t for t, _ in outs[0]] == [100, 102, 104]
+
+
+def test_query_rank_group_routes_replies(nns):
+    nns.register_custom_easy("rank_triple", lambda x: [x[0] * 3],
+                             [nns.TensorShape([4], np.float32)], [nns.TensorShape([4], np.float32)])
+    store = _free_port()
+    n = 3
+    server = nns.parse_launch(f"tensor_query_serversrc connect-type=RCCL id=31 topic=q1 {_rank(0, n, store)} ! {F32} "
+                              "! tensor_filter framework=custom-easy model=rank_triple "
+                              "! tensor_query_serversink connect-type=RCCL id=31")
+    server.set_state("playing")
+    clients, outs = [], []
+    for k in range(1, n):
+        c = nns.parse_launch(f"appsrc name=src caps={F32} ! tensor_query_client connect-type=RCCL topic=q1 "
+                             f"max-request=2 {_rank(k, n, store)} ! tensor_sink name=sink")
+        outs.append(_collect(c))
+        c.set_state("playing")
+        clients.append(c)
+    import threading
+    th = [threading.Thread(target=_push, args=(c, [np.full(4, 10 * k + i, np.float32) for i in range(8)]))
+          for k, c in enumerate(clients, 1)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    for c in clients:
+        _wait_eos(c)
+        c.stop()
+    server.stop()
+    for k, o in enumerate(outs, 1):
+        assert [t for t, _ in o] == [100 + i for i in range(8)]
+        assert [float(m[0][0]) for _, m in o] == [3.0 * (10 * k + i) for i in range(8)]
+
+
+@pytest.mark.parametrize("mode", ["concat", "stack"])
+def test_allgather_rank_group(nns, mode):
+    store = _free_port()
+    n = 3
+    caps = "other/tensors,format=static,num_tensors=1,dimensions=4:1:1:1,types=float32,framerate=0/1"
+    pipes, outs = [], []
+    for k in range(n):
+        p = nns.parse_launch(f"appsrc name=src caps={caps} ! tensor_allgather channel=ag-{mode} mode={mode} axis=1 "
+                             f"{_rank(k, n, store)} ! tensor_sink name=sink")
+        outs.append(_collect(p))
+        p.set_state("playing")
+        pipes.append(p)
+    import threading
+    th = [threading.Thread(target=_push, args=(p, [np.full(4, 10 * k + i, np.float32) for i in range(4)]))
+          for k, p in enumerate(pipes)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    for p in pipes:
+        _wait_eos(p)
+        p.stop()
+    for o in outs:
+        assert len(o) == 4
+        for i, (_, mems) in enumerate(o):
+            if mode == "concat":
+                assert [float(m[0]) for m in mems] == [float(10 * k + i) for k in range(n)]
+            else:
+                assert len(mems) == 1 and mems[0].shape == (12,)
+                np.testing.assert_array_equal(mems[0].reshape(n, 4)[:, 0], [10 * k + i for k in range(n)])
+
+
+def test_allgather_torchrun_style_processes(tmp_path):
+    """Two real processes, rank / world / store from the torchrun environment."""
+    script = tmp_path / "member.py"
+    script.write_text(textwrap.dedent(f"""
+        import os, sys
+        sys.path.insert(0, {ROOT!r})
+        import numpy as np
+        import nnstreamer_amd as nns
+        caps = "other/tensors,format=static,num_tensors=1,dimensions=2,types=float32,framerate=0/1"
+        p = nns.parse_launch(f"appsrc name=src caps={{caps}} ! tensor_allgather comm-backend=tcp ! tensor_sink name=sink")
+        out = []
+        p.get_by_name("sink").connect("new-data", lambda b: out.append(
+            [float(b.memory(i).numpy("float32")[0]) for i in range(b.n_memory)]))
+        p.set_state("playing")
+        r = int(os.environ["RANK"])
+        for i in range(3):
+            p.get_by_name("src").push_buffer(np.full(2, 100 * r + i, np.float32), pts=i)
+        p.get_by_name("src").end_of_stream()
+        msg = p.wait(60)
+        p.stop()
+        assert msg and msg[0] == "eos", p.messages()
+        print("OUT", out, flush=True)
+    """))
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = [p.communicate(timeout=120)[0] for p in procs]
+    for p, o in zip(procs, outs):
+        assert p.returncode == 0, o
+        line = [x for x in o.splitlines() if x.startswith("OUT")][0]
+        assert line == "OUT [[0.0, 100.0], [1.0, 101.0], [2.0, 102.0]]", o
