@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <type_traits>
 
 #include "kernels/mbv2.h"
 
@@ -44,30 +45,46 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   u += 0x7fffu + ((u >> 16) & 1u);
   return static_cast<uint16_t>(u >> 16);
 }
+// two floats -> packed bf16 pair (lo = a), round-to-nearest-even: one v_cvt_pk_bf16_f32 on gfx950
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2v __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2v){a, b}, b2v));
+}
 __device__ __forceinline__ float relu6(float v) { return fminf(fmaxf(v, 0.f), 6.f); }
 
 constexpr size_t kLdsLimit = 160 * 1024;  // gfx950 LDS per CU (one workgroup may own it all)
 constexpr int TO = 8;       // output tile edge
 constexpr int HC = 32;      // hidden channels per chunk (= one MFMA K step)
-constexpr int HROW = HC + 8;  // LDS row pitch (elements) of the hidden / dw tiles
+// LDS row pitches (elements).  Hidden tile: the depthwise lanes of one 32-lane
+// half read 8 pixels (stride S) x 4 channel quads with ds_read_b64, so a pixel's
+// pitch in dwords must tile the 64 banks: 24 dwords for S=1, 20 for S=2.
+// The hidden tile is fp32 (F = true: no bf16 pack/unpack on the VALU between
+// expand and dw; pitch 36 floats: expand stores conflict-free, dw reads 2-way)
+// when that costs no workgroup per CU, else bf16 (pitch: see above).
+__host__ __device__ constexpr int hrow(int s, bool f) { return f ? HC + 4 : (s == 1 ? HC + 16 : HC + 8); }
+__host__ __device__ constexpr int hbytes(bool f) { return f ? 4 : 2; }
+constexpr int DROW = HC + 8;  // dw output tile (project B operand)
 
 __host__ __device__ constexpr int tile_in(int s) { return (TO - 1) * s + 3; }
 __host__ __device__ constexpr int tile_in_px16(int s) { return (tile_in(s) * tile_in(s) + 15) / 16 * 16; }
 
-template <int S, int NOT, int KS_MAX>
+template <int S, bool F32H, int NOT, int KS_MAX>
 __global__ void __launch_bounds__(256) ir_block_kernel(IrBlockArgs a) {
   constexpr int TI = tile_in(S);
   constexpr int PIN = TI * TI;
   constexpr int PIN16 = tile_in_px16(S);
   constexpr int NB = PIN16 / 16;                       // 16-pixel B tiles of the halo tile
   constexpr int NV = (PIN16 * 4 * KS_MAX + 255) / 256;  // 16-B input vectors per thread per tile
+  constexpr int HROW = hrow(S, F32H);
+  using HT = typename std::conditional<F32H, float, uint16_t>::type;  // hidden tile element
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int xrow = a.cin32 + 8;  // LDS pitch of the input tile
-  uint16_t* xs = smem;                          // [PIN16][xrow]
-  uint16_t* hidbuf = xs + PIN16 * xrow;         // 2 x [PIN16][HROW] (double buffered)
-  uint16_t* dwo = hidbuf + 2 * PIN16 * HROW;    // [64][HROW]
-  float* wds = reinterpret_cast<float*>(dwo + 64 * HROW);  // [9][hid] depthwise weights, fp32 (staged once)
-  float* bds = wds + 9 * a.hid;                             // [hid]    depthwise bias
+  uint16_t* xs = smem;                                                // [PIN16][xrow]
+  HT* hidbuf = reinterpret_cast<HT*>(xs + PIN16 * xrow);             // 2 x [PIN16][HROW] (double buffered)
+  uint16_t* dwo = reinterpret_cast<uint16_t*>(hidbuf + 2 * PIN16 * HROW);  // [64][DROW]
+  HT* wds = reinterpret_cast<HT*>(dwo + 64 * DROW);                  // [9][hid] depthwise weights (staged once)
+  float* bds = reinterpret_cast<float*>(wds + 9 * a.hid);            // [hid] depthwise bias
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -128,18 +145,21 @@ __global__ void __launch_bounds__(256) ir_block_kernel(IrBlockArgs a) {
   if (t_begin >= t_end) return;
   if (a.has_expand) load_expand(0);
   fetch_tile(t_begin);
-  for (int v = tid; v < 9 * a.hid / 8; v += 256)
-  {
+  for (int v = tid; v < 9 * a.hid / 8; v += 256) {
     const bf16x8_t w8 = *reinterpret_cast<const bf16x8_t*>(a.wd + v * 8);
+    if constexpr (F32H) {
 #pragma unroll
-    for (int r = 0; r < 8; ++r) wds[v * 8 + r] = bf2f(static_cast<uint16_t>(w8[r]));
+      for (int r = 0; r < 8; ++r) wds[v * 8 + r] = bf2f(static_cast<uint16_t>(w8[r]));
+    } else {
+      *reinterpret_cast<bf16x8_t*>(wds + v * 8) = w8;
+    }
   }
   for (int v = tid; v < a.hid; v += 256) bds[v] = a.bd[v];
 
-  // dw lane mapping == project mapping: wave w owns output pixels 16w..16w+15
-  const int q = tid >> 2;
-  const int g = (tid & 3) * 8;
-  const int qy = q / TO, qx = q % TO;
+  // depthwise lane mapping: wave w owns output rows 2w, 2w+1 (= the project
+  // B-tile pixels 16w..16w+15); lane = column dx x channel quad dq, both rows
+  const int dx = lane & 7;
+  const int dq = (lane >> 3) * 4;
 
   for (int tile = t_begin; tile < t_end; ++tile) {
     store_tile();
@@ -156,7 +176,7 @@ __global__ void __launch_bounds__(256) ir_block_kernel(IrBlockArgs a) {
 
     int buf = 0;
     for (int c0 = 0; c0 < a.hid; c0 += HC, buf ^= 1) {
-      uint16_t* hid = hidbuf + buf * PIN16 * HROW;
+      HT* hid = hidbuf + buf * PIN16 * HROW;
       // issue this chunk's project weight loads early (consumed after the barrier)
       bf16x8_t pa[NOT];
 #pragma unroll
@@ -182,60 +202,98 @@ __global__ void __launch_bounds__(256) ir_block_kernel(IrBlockArgs a) {
           const int iy = iy0 + p / TI, ix = ix0 + p % TI;
           const bool inside = p < PIN && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
           const int hc = (lane >> 4) * 4;
-          uint2 p0 = make_uint2(0u, 0u), p1 = make_uint2(0u, 0u);
-          if (inside) {
-            p0.x = static_cast<uint32_t>(f2bf(relu6(e0[0] + eb[0][0]))) |
-                   (static_cast<uint32_t>(f2bf(relu6(e0[1] + eb[0][1]))) << 16);
-            p0.y = static_cast<uint32_t>(f2bf(relu6(e0[2] + eb[0][2]))) |
-                   (static_cast<uint32_t>(f2bf(relu6(e0[3] + eb[0][3]))) << 16);
-            p1.x = static_cast<uint32_t>(f2bf(relu6(e1[0] + eb[1][0]))) |
-                   (static_cast<uint32_t>(f2bf(relu6(e1[1] + eb[1][1]))) << 16);
-            p1.y = static_cast<uint32_t>(f2bf(relu6(e1[2] + eb[1][2]))) |
-                   (static_cast<uint32_t>(f2bf(relu6(e1[3] + eb[1][3]))) << 16);
+          if constexpr (F32H) {
+            f32x4_t v0 = f32x4_t{0.f, 0.f, 0.f, 0.f}, v1 = v0;
+            if (inside) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                v0[r] = relu6(e0[r] + eb[0][r]);
+                v1[r] = relu6(e1[r] + eb[1][r]);
+              }
+            }
+            *reinterpret_cast<f32x4_t*>(hid + p * HROW + hc) = v0;
+            *reinterpret_cast<f32x4_t*>(hid + p * HROW + 16 + hc) = v1;
+          } else {
+            uint2 p0 = make_uint2(0u, 0u), p1 = make_uint2(0u, 0u);
+            if (inside) {
+              p0.x = pk_bf16(relu6(e0[0] + eb[0][0]), relu6(e0[1] + eb[0][1]));
+              p0.y = pk_bf16(relu6(e0[2] + eb[0][2]), relu6(e0[3] + eb[0][3]));
+              p1.x = pk_bf16(relu6(e1[0] + eb[1][0]), relu6(e1[1] + eb[1][1]));
+              p1.y = pk_bf16(relu6(e1[2] + eb[1][2]), relu6(e1[3] + eb[1][3]));
+            }
+            *reinterpret_cast<uint2*>(hid + p * HROW + hc) = p0;
+            *reinterpret_cast<uint2*>(hid + p * HROW + 16 + hc) = p1;
           }
-          *reinterpret_cast<uint2*>(hid + p * HROW + hc) = p0;
-          *reinterpret_cast<uint2*>(hid + p * HROW + 16 + hc) = p1;
         }
         // prefetch the next chunk's (or the next tile's first chunk's) expand operands
         load_expand(c0 + HC < a.hid ? c0 + HC : 0);
       } else {
         for (int v = tid; v < PIN16 * (HC / 8); v += 256) {
           const int p = v / (HC / 8), k = (v % (HC / 8)) * 8;
-          *reinterpret_cast<bf16x8_t*>(hid + p * HROW + k) =
-              *reinterpret_cast<const bf16x8_t*>(xs + p * xrow + c0 + k);
+          const bf16x8_t x8 = *reinterpret_cast<const bf16x8_t*>(xs + p * xrow + c0 + k);
+          if constexpr (F32H) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) hid[p * HROW + k + r] = bf2f(static_cast<uint16_t>(x8[r]));
+          } else {
+            *reinterpret_cast<bf16x8_t*>(hid + p * HROW + k) = x8;
+          }
         }
       }
       // one block barrier per chunk: hid is double buffered, dw/project are wave-local
       __syncthreads();
 
-      // ---- depthwise 3x3 + bias + ReLU6 (lane = 1 output pixel x 8 channels)
+      // ---- depthwise 3x3 + bias + ReLU6: lane = 2 vertically adjacent output
+      // pixels x 4 channels.  The S+3 input rows are read once for both pixels
+      // (ds_read_b64) and the taps' bf16 weights once per chunk; packed fp32
+      // math, 2 channels per v_pk_fma_f32 (bf16 -> f32: shift low / mask high)
       {
-        // packed fp32 math: 2 channels per v_pk_fma_f32; bf16 -> f32 is a shift (low) / mask (high)
-        f32x2_t d[4];
+        const int ch = c0 + dq;
+        const f32x4_t bb = *reinterpret_cast<const f32x4_t*>(bds + ch);
+        f32x2_t d0[2] = {f32x2_t{bb[0], bb[1]}, f32x2_t{bb[2], bb[3]}};
+        f32x2_t d1[2] = {d0[0], d0[1]};
+        f32x2_t w[9][2];
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) d[rr] = *reinterpret_cast<const f32x2_t*>(bds + c0 + g + 2 * rr);
+        for (int t = 0; t < 9; ++t) {
+          if constexpr (F32H) {
+            const f32x4_t wv = *reinterpret_cast<const f32x4_t*>(wds + t * a.hid + ch);
+            w[t][0] = f32x2_t{wv[0], wv[1]};
+            w[t][1] = f32x2_t{wv[2], wv[3]};
+          } else {
+            const uint2 wv = *reinterpret_cast<const uint2*>(wds + t * a.hid + ch);
+            w[t][0] = f32x2_t{__uint_as_float(wv.x << 16), __uint_as_float(wv.x & 0xffff0000u)};
+            w[t][1] = f32x2_t{__uint_as_float(wv.y << 16), __uint_as_float(wv.y & 0xffff0000u)};
+          }
+        }
+        const int r0 = wave * 2 * S;
 #pragma unroll
-        for (int ky = 0; ky < 3; ++ky)
+        for (int rr = 0; rr < S + 3; ++rr)
 #pragma unroll
           for (int kx = 0; kx < 3; ++kx) {
-            const int p = (qy * S + ky) * TI + (qx * S + kx);
-            const uint4 hv = *reinterpret_cast<const uint4*>(hid + p * HROW + g);
-            const float* wrow = wds + (ky * 3 + kx) * a.hid + c0 + g;
-            const f32x4_t w0 = *reinterpret_cast<const f32x4_t*>(wrow);
-            const f32x4_t w1 = *reinterpret_cast<const f32x4_t*>(wrow + 4);
-            const uint32_t hw[4] = {hv.x, hv.y, hv.z, hv.w};
-            const f32x2_t wp2[4] = {f32x2_t{w0[0], w0[1]}, f32x2_t{w0[2], w0[3]}, f32x2_t{w1[0], w1[1]},
-                                    f32x2_t{w1[2], w1[3]}};
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-              const f32x2_t h2 = f32x2_t{__uint_as_float(hw[rr] << 16), __uint_as_float(hw[rr] & 0xffff0000u)};
-              d[rr] = __builtin_elementwise_fma(h2, wp2[rr], d[rr]);
+            const int p = (r0 + rr) * TI + dx * S + kx;
+            f32x2_t h0, h1;
+            if constexpr (F32H) {
+              const f32x4_t hv = *reinterpret_cast<const f32x4_t*>(hid + p * HROW + dq);
+              h0 = f32x2_t{hv[0], hv[1]};
+              h1 = f32x2_t{hv[2], hv[3]};
+            } else {
+              const uint2 hv = *reinterpret_cast<const uint2*>(hid + p * HROW + dq);
+              h0 = f32x2_t{__uint_as_float(hv.x << 16), __uint_as_float(hv.x & 0xffff0000u)};
+              h1 = f32x2_t{__uint_as_float(hv.y << 16), __uint_as_float(hv.y & 0xffff0000u)};
+            }
+            if (rr <= 2) {
+              d0[0] = __builtin_elementwise_fma(h0, w[rr * 3 + kx][0], d0[0]);
+              d0[1] = __builtin_elementwise_fma(h1, w[rr * 3 + kx][1], d0[1]);
+            }
+            if (rr >= S && rr - S <= 2) {
+              d1[0] = __builtin_elementwise_fma(h0, w[(rr - S) * 3 + kx][0], d1[0]);
+              d1[1] = __builtin_elementwise_fma(h1, w[(rr - S) * 3 + kx][1], d1[1]);
             }
           }
-        bf16x8_t o;
-#pragma unroll
-        for (int rr = 0; rr < 8; ++rr) o[rr] = static_cast<short>(f2bf(relu6(d[rr >> 1][rr & 1])));
-        *reinterpret_cast<bf16x8_t*>(dwo + q * HROW + g) = o;
+        auto pk = [](f32x2_t v) {
+          return pk_bf16(relu6(v[0]), relu6(v[1]));
+        };
+        *reinterpret_cast<uint2*>(dwo + (wave * 16 + dx) * DROW + dq) = make_uint2(pk(d0[0]), pk(d0[1]));
+        *reinterpret_cast<uint2*>(dwo + (wave * 16 + 8 + dx) * DROW + dq) = make_uint2(pk(d1[0]), pk(d1[1]));
       }
       // dwo rows of this wave were written by this wave only: a wave-level fence suffices
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -245,7 +303,7 @@ __global__ void __launch_bounds__(256) ir_block_kernel(IrBlockArgs a) {
       // ---- project: D[out][px] += Wp[out][hid] . dw[px][hid]^T
       {
         const bf16x8_mfma bfr =
-            __builtin_bit_cast(bf16x8_mfma, *reinterpret_cast<const bf16x8_t*>(dwo + (wave * 16 + li) * HROW + kq));
+            __builtin_bit_cast(bf16x8_mfma, *reinterpret_cast<const bf16x8_t*>(dwo + (wave * 16 + li) * DROW + kq));
 #pragma unroll
         for (int ot = 0; ot < NOT; ++ot)
           acc[ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_mfma, pa[ot]), bfr, acc[ot], 0,
@@ -273,8 +331,8 @@ __global__ void __launch_bounds__(256) ir_block_kernel(IrBlockArgs a) {
             for (int rr = 0; rr < 4; ++rr) v[rr] += bf2f(rp[rr]);
           }
           uint2 o;
-          o.x = static_cast<uint32_t>(f2bf(v[0])) | (static_cast<uint32_t>(f2bf(v[1])) << 16);
-          o.y = static_cast<uint32_t>(f2bf(v[2])) | (static_cast<uint32_t>(f2bf(v[3])) << 16);
+          o.x = pk_bf16(v[0], v[1]);
+          o.y = pk_bf16(v[2], v[3]);
           *reinterpret_cast<uint2*>(yb + co) = o;
         }
       }
@@ -283,50 +341,64 @@ __global__ void __launch_bounds__(256) ir_block_kernel(IrBlockArgs a) {
   }
 }
 
-template <int S, int NOT, int KS>
+template <int S, bool F, int NOT, int KS>
 bool launch_one(const IrBlockArgs& a, size_t lds, dim3 grid, hipStream_t s) {
   // dynamic LDS above 64 KiB must be opted into once per instantiation (a workgroup may use all 160 KiB)
-  static const bool attr_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&ir_block_kernel<S, NOT, KS>),
+  static const bool attr_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&ir_block_kernel<S, F, NOT, KS>),
                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
                                                   static_cast<int>(kLdsLimit)) == hipSuccess;
   if (!attr_ok && lds > 64 * 1024) return false;
-  hipLaunchKernelGGL((ir_block_kernel<S, NOT, KS>), grid, dim3(256), lds, s, a);
+  hipLaunchKernelGGL((ir_block_kernel<S, F, NOT, KS>), grid, dim3(256), lds, s, a);
   return true;
 }
 
-template <int S, int NOT>
+template <int S, bool F, int NOT>
 bool launch_ks(const IrBlockArgs& a, size_t lds, dim3 grid, hipStream_t s) {
   switch (a.cin32 / 32) {
-    case 1: return launch_one<S, NOT, 1>(a, lds, grid, s);
-    case 2: return launch_one<S, NOT, 2>(a, lds, grid, s);
-    case 3: return launch_one<S, NOT, 3>(a, lds, grid, s);
-    case 5: return launch_one<S, NOT, 5>(a, lds, grid, s);
+    case 1: return launch_one<S, F, NOT, 1>(a, lds, grid, s);
+    case 2: return launch_one<S, F, NOT, 2>(a, lds, grid, s);
+    case 3: return launch_one<S, F, NOT, 3>(a, lds, grid, s);
+    case 5: return launch_one<S, F, NOT, 5>(a, lds, grid, s);
     default: return false;
   }
 }
 
-template <int S>
+template <int S, bool F>
 bool launch_s(const IrBlockArgs& a, int n_ot, size_t lds, dim3 grid, hipStream_t s) {
   switch (n_ot) {
-    case 1: return launch_ks<S, 1>(a, lds, grid, s);
-    case 2: return launch_ks<S, 2>(a, lds, grid, s);
-    case 4: return launch_ks<S, 4>(a, lds, grid, s);
-    case 6: return launch_ks<S, 6>(a, lds, grid, s);
-    case 10: return launch_ks<S, 10>(a, lds, grid, s);
-    case 20: return launch_ks<S, 20>(a, lds, grid, s);
+    case 1: return launch_ks<S, F, 1>(a, lds, grid, s);
+    case 2: return launch_ks<S, F, 2>(a, lds, grid, s);
+    case 4: return launch_ks<S, F, 4>(a, lds, grid, s);
+    case 6: return launch_ks<S, F, 6>(a, lds, grid, s);
+    case 10: return launch_ks<S, F, 10>(a, lds, grid, s);
+    case 20: return launch_ks<S, F, 20>(a, lds, grid, s);
     default: return false;
   }
 }
 
 }  // namespace
 
-size_t ir_block_lds_bytes(int stride, int cin32) {
+namespace {
+size_t lds_total(int stride, bool f, int cin32, int hid) {
   const int pin16 = tile_in_px16(stride);
-  return sizeof(uint16_t) * (static_cast<size_t>(pin16) * (cin32 + 8) + 2 * static_cast<size_t>(pin16) * HROW + 64 * HROW);
+  return sizeof(uint16_t) * (static_cast<size_t>(pin16) * (cin32 + 8) + 64 * DROW) +
+         static_cast<size_t>(hbytes(f)) * 2 * static_cast<size_t>(pin16) * hrow(stride, f) +
+         (9 * static_cast<size_t>(hbytes(f)) + sizeof(float)) * static_cast<size_t>(hid);  // dw weights + bias
 }
+// fp32 hidden tile when it costs no workgroup per CU, or on the large early
+// feature maps (>= 56x56, many tiles per workgroup) as long as two workgroups
+// still fit.  Measured at batch 256 (scripts/bench_ir.py): fp32 wins at
+// 112/56 px even at 3-vs-4 workgroups per CU, loses at 28 px (3 vs 4) and
+// whenever it drops to 1 workgroup, ties at 14 px.
+bool use_f32_hidden(int stride, int cin32, int hid, int hw) {
+  const size_t f = lds_total(stride, true, cin32, hid), b = lds_total(stride, false, cin32, hid);
+  if (f > kLdsLimit) return false;
+  return kLdsLimit / f >= kLdsLimit / b || (hw >= 56 * 56 && kLdsLimit / f >= 2);
+}
+}  // namespace
 
 size_t ir_block_lds_total(int stride, int cin32, int hid) {
-  return ir_block_lds_bytes(stride, cin32) + sizeof(float) * 10 * static_cast<size_t>(hid);
+  return lds_total(stride, false, cin32, hid);  // the bf16 tile: what ir_block_supported() checks
 }
 
 bool ir_block_supported(int stride, int cin, int hid, int cout) {
@@ -348,15 +420,18 @@ bool ir_block(const IrBlockArgs& args, hipStream_t s) {
   a.tiles_x = (a.Wo + TO - 1) / TO;
   if (!ir_block_supported(a.stride, a.cin, a.hid, a.cout)) return false;
   const int n_ot = (a.cout + 15) / 16;
-  const size_t lds = ir_block_lds_total(a.stride, a.cin32, a.hid);
+  const bool f = use_f32_hidden(a.stride, a.cin32, a.hid, a.H * a.W);
+  const size_t lds = lds_total(a.stride, f, a.cin32, a.hid);
   // persistent grid: enough workgroups for every CU to hold several (LDS-limited), each
   // walking a run of consecutive tiles so the next tile's input loads overlap compute
+  // one resident round: every workgroup slot of the chip walks an equal run of tiles
   const int total_tiles = a.tiles_x * a.tiles_y * a.B;
   const int per_cu = std::max<int>(1, std::min<int>(8, static_cast<int>(kLdsLimit / lds)));
-  const int max_wgs = 256 * per_cu * 2;
+  const int max_wgs = 256 * per_cu;
   a.tiles_per_wg = std::max(1, (total_tiles + max_wgs - 1) / max_wgs);
   dim3 grid(static_cast<unsigned>((total_tiles + a.tiles_per_wg - 1) / a.tiles_per_wg));
-  return a.stride == 1 ? launch_s<1>(a, n_ot, lds, grid, s) : launch_s<2>(a, n_ot, lds, grid, s);
+  if (a.stride == 1) return f ? launch_s<1, true>(a, n_ot, lds, grid, s) : launch_s<1, false>(a, n_ot, lds, grid, s);
+  return f ? launch_s<2, true>(a, n_ot, lds, grid, s) : launch_s<2, false>(a, n_ot, lds, grid, s);
 }
 
 }  // namespace kernels

@@ -43,7 +43,6 @@ struct IrBlockArgs {
   int cin32 = 0, Ho = 0, Wo = 0, tiles_x = 0, tiles_y = 0, tiles_per_wg = 1;
 };
 bool ir_block_supported(int stride, int cin, int hid, int cout);
-size_t ir_block_lds_bytes(int stride, int cin32);
 // returns false (nothing launched) for unsupported shapes
 bool ir_block(const IrBlockArgs& a, hipStream_t s);
 

@@ -34,6 +34,12 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   u += 0x7fffu + ((u >> 16) & 1u);  // round-nearest-even (inputs are finite)
   return static_cast<uint16_t>(u >> 16);
 }
+// two floats -> packed bf16 pair (lo = a), round-to-nearest-even: one v_cvt_pk_bf16_f32 on gfx950
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2v __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2v){a, b}, b2v));
+}
 
 __device__ __forceinline__ float act_fn(float v, int act) {
   if (act == 1) return fminf(fmaxf(v, 0.f), 6.f);  // ReLU6
@@ -127,8 +133,8 @@ __global__ void __launch_bounds__(256) pw_gemm_kernel(const uint16_t* __restrict
         *reinterpret_cast<float4*>(static_cast<float*>(y) + static_cast<int64_t>(m) * N + n) = o;
       } else {
         uint2 o;
-        o.x = static_cast<uint32_t>(f2bf(v[0])) | (static_cast<uint32_t>(f2bf(v[1])) << 16);
-        o.y = static_cast<uint32_t>(f2bf(v[2])) | (static_cast<uint32_t>(f2bf(v[3])) << 16);
+        o.x = pk_bf16(v[0], v[1]);
+        o.y = pk_bf16(v[2], v[3]);
         *reinterpret_cast<uint2*>(static_cast<uint16_t*>(y) + static_cast<int64_t>(m) * N + n) = o;
       }
     }
@@ -178,8 +184,7 @@ __global__ void __launch_bounds__(256) dw3x3_kernel(const uint16_t* __restrict__
     uint32_t o[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      o[q] = static_cast<uint32_t>(f2bf(act_fn(acc[2 * q], act))) |
-             (static_cast<uint32_t>(f2bf(act_fn(acc[2 * q + 1], act))) << 16);
+      o[q] = pk_bf16(act_fn(acc[2 * q], act), act_fn(acc[2 * q + 1], act));
     *reinterpret_cast<uint4*>(y + ((static_cast<int64_t>(b) * Ho + oy) * Wo + ox) * C + c) = uint4{o[0], o[1], o[2], o[3]};
   }
 }
@@ -239,8 +244,7 @@ __global__ void __launch_bounds__(256) stem_kernel(const T* __restrict__ x, cons
     uint32_t o[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      o[q] = static_cast<uint32_t>(f2bf(act_fn(acc[2 * q], act))) |
-             (static_cast<uint32_t>(f2bf(act_fn(acc[2 * q + 1], act))) << 16);
+      o[q] = pk_bf16(act_fn(acc[2 * q], act), act_fn(acc[2 * q + 1], act));
     *reinterpret_cast<uint4*>(y + ((static_cast<int64_t>(b) * Ho + oy) * Wo + ox) * 32 + og * 8) = uint4{o[0], o[1], o[2], o[3]};
   }
 }
@@ -268,7 +272,7 @@ __global__ void __launch_bounds__(256) avgpool_kernel(const uint16_t* __restrict
     uint32_t o[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      o[q] = static_cast<uint32_t>(f2bf(acc[2 * q] * inv)) | (static_cast<uint32_t>(f2bf(acc[2 * q + 1] * inv)) << 16);
+      o[q] = pk_bf16(acc[2 * q] * inv, acc[2 * q + 1] * inv);
     *reinterpret_cast<uint4*>(y + static_cast<int64_t>(b) * C + c) = uint4{o[0], o[1], o[2], o[3]};
   }
 }

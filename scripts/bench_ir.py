@@ -26,6 +26,9 @@ def timeit(fn, n=20):
     return s.elapsed_time(e) / n * 1e3  # us
 
 
+ONLY = os.environ.get("NNSX_IR_ONLY")  # e.g. "56,24,144,24,1": one shape, fused only (for rocprof)
+if ONLY:
+    SHAPES = [tuple(int(v) for v in ONLY.split(","))]
 tot_f = tot_u = 0.0
 for H, cin, hid, cout, st in SHAPES:
     has_expand = not (cin == 32 and hid == 32)
@@ -46,7 +49,7 @@ for H, cin, hid, cout, st in SHAPES:
         h = torch.ops.nnsx.dw_conv(h, wd, bd, st, 1)
         return torch.ops.nnsx.pw_conv(h, wp, bp, x if res else None, cout, 0, False)
 
-    tu = timeit(unf)
+    tu = timeit(unf) if not ONLY else 0.0
     tf = timeit(lambda: torch.ops.nnsx.ir_block(x, we[:hp].contiguous(), be[:hp].contiguous(), wd, bd, wp, bp, st,
                                                 cout, has_expand, res)) if ok else float("nan")
     nbytes = (x.numel() + B * ((H - 1) // st + 1) ** 2 * cout) * 2
