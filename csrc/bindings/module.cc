@@ -8,6 +8,7 @@
 
 #include <cstring>
 
+#include "comm/mqtt.h"
 #include "core/caps.h"
 #include "core/log.h"
 #include "core/registry.h"
@@ -427,6 +428,23 @@ PYBIND11_MODULE(_C, m) {
       .def("stop", [](Pipeline& p) {
         py::gil_scoped_release r;
         p.set_state(State::NULL_);
+      });
+
+  // in-process MQTT broker (mqttsink / mqttsrc / connect-type=HYBRID without an external broker)
+  py::class_<comm::MqttBroker, std::shared_ptr<comm::MqttBroker>>(m, "MqttBroker")
+      .def(py::init([](int port, const std::string& host) {
+             std::string err;
+             auto b = comm::mqtt_broker_start(host, port, &err);
+             if (!b) throw Error(err);
+             return b;
+           }),
+           py::arg("port") = 0, py::arg("host") = "127.0.0.1")
+      .def_property_readonly("port", &comm::MqttBroker::port)
+      .def_property_readonly("clients", &comm::MqttBroker::clients)
+      .def_property_readonly("messages", &comm::MqttBroker::messages)
+      .def("stop", [](comm::MqttBroker& b) {
+        py::gil_scoped_release r;
+        b.stop();
       });
 
   m.def("parse_launch", [](const std::string& d) { return parse_launch(d); });

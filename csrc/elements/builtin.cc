@@ -31,6 +31,7 @@ void ensure_builtin_elements() {
     register_tensor_stream_elements();
     register_extra_elements();
     register_comm_elements();
+    register_mqtt_elements();
     register_grpc_elements();
     register_host_frameworks();
     register_torch_frameworks();

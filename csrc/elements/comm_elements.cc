@@ -9,16 +9,20 @@
 // frames), tensor_query_server.c (id -> server registry, waits for the sink's
 // caps before answering clients), gst/edge/edge_sink.c / edge_src.c.  The
 // reference rides on the external nnstreamer-edge library (TCP / MQTT-hybrid
-// / AITT); nnsx implements the TCP connect-type natively, plus HIPIPC: the
-// same framing with HBM-resident tensors handed over through an exported
-// device ring (zero-copy on the same GPU, one xGMI peer copy across GPUs;
-// see comm/transport.h).
+// / AITT); nnsx implements TCP and HYBRID (endpoint discovery through an MQTT
+// broker, comm/mqtt.h) natively, plus HIPIPC: the same framing with
+// HBM-resident tensors handed over through an exported device ring
+// (zero-copy on the same GPU, one xGMI peer copy across GPUs; see
+// comm/transport.h), and RCCL: rank groups over xGMI (comm/group.h).
 #include <algorithm>
 #include <atomic>
 #include <map>
 #include <thread>
 
+#include <unistd.h>
+
 #include "comm/group.h"
+#include "comm/mqtt.h"
 #include "comm/transport.h"
 #include "core/log.h"
 #include "elements/elements.h"
@@ -38,11 +42,89 @@ constexpr int kRccl = 5;
 const std::vector<std::string> kRcclModes = {"broadcast", "scatter"};
 constexpr uint32_t kPktCaps = 1;  // packet carries only a caps string
 
+constexpr int kHybrid = 1;
+
 bool check_connect_type(Element* e, int type) {
-  if (type == 0 || type == kHipIpc || type == kRccl) return true;
+  if (type == 0 || type == kHybrid || type == kHipIpc || type == kRccl) return true;
   e->post_error("connect-type " + kConnectTypes[static_cast<size_t>(type)] +
-                " is not supported (nnsx implements TCP, HIPIPC and RCCL)");
+                " is not supported (nnsx implements TCP, HYBRID, HIPIPC and RCCL)");
   return false;
+}
+
+// ---- connect-type=HYBRID: the MQTT broker at dest-host:dest-port only
+// carries each server's / publisher's TCP endpoint, retained on
+// nnsx/edge/<topic>/<id>; data flows over TCP (nnstreamer-edge HYBRID:
+// tensor_query_client.c:366-384 reconnects to another server on failure).
+std::string hybrid_topic(const std::string& topic) { return "nnsx/edge/" + (topic.empty() ? "default" : topic); }
+
+class HybridAnnouncer {
+ public:
+  ~HybridAnnouncer() { withdraw(); }
+  bool announce(const std::string& broker, int broker_port, const std::string& topic, const std::string& host,
+                int port, std::string* err) {
+    static std::atomic<unsigned> seq{0};
+    key_ = strfmt(hybrid_topic(topic), "/", getpid(), "-", seq++);
+    if (!cli_.connect(broker, broker_port, key_, 60, true, 5000, err)) return false;
+    const std::string ep = strfmt(host == "localhost" || host.empty() ? "127.0.0.1" : host, ":", port);
+    return cli_.publish(key_, ep.data(), ep.size(), 1, true);
+  }
+  void withdraw() {
+    if (!cli_.connected()) return;
+    cli_.publish(key_, "", 0, 1, true);  // empty retained payload clears the entry
+    cli_.close();
+  }
+
+ private:
+  comm::MqttClient cli_;
+  std::string key_;
+};
+
+// every endpoint announced on the topic (retained), in announcement-key order
+std::vector<std::pair<std::string, int>> hybrid_discover(const std::string& broker, int broker_port,
+                                                         const std::string& topic, int timeout_ms, std::string* err) {
+  comm::MqttClient cli;
+  std::vector<std::pair<std::string, int>> out;
+  if (!cli.connect(broker, broker_port, strfmt("nnsx-discover-", getpid(), "-", now_ns()), 0, true, 5000, err) ||
+      !cli.subscribe(hybrid_topic(topic) + "/+", 1)) {
+    if (err && err->empty()) *err = "HYBRID: broker subscription failed";
+    return out;
+  }
+  std::map<std::string, std::string> found;
+  const int64_t deadline = now_ns() + static_cast<int64_t>(timeout_ms) * 1000000;
+  while (now_ns() < deadline) {
+    comm::MqttMessage m;
+    // after the first answer only the rest of the retained burst is awaited
+    if (!cli.recv(&m, found.empty() ? 100 : 50)) {
+      if (!found.empty()) break;
+      continue;
+    }
+    if (m.payload.empty())
+      found.erase(m.topic);
+    else
+      found[m.topic] = m.payload;
+  }
+  cli.close();
+  for (auto& kv : found) {
+    const size_t c = kv.second.rfind(':');
+    if (c != std::string::npos) out.emplace_back(kv.second.substr(0, c), std::atoi(kv.second.c_str() + c + 1));
+  }
+  if (out.empty() && err) *err = "HYBRID: no server announced on " + hybrid_topic(topic);
+  return out;
+}
+
+// connect to the first reachable endpoint (TCP / HYBRID)
+std::shared_ptr<comm::Connection> connect_endpoint(int type, const std::string& host, unsigned port,
+                                                   const std::string& topic, int timeout_ms, std::string* err,
+                                                   const std::string& avoid = std::string()) {
+  if (type != kHybrid) return comm::Connection::connect(host, static_cast<int>(port), timeout_ms, err);
+  auto eps = hybrid_discover(host, static_cast<int>(port), topic, timeout_ms, err);
+  std::shared_ptr<comm::Connection> c;
+  for (int pass = 0; pass < 2 && !c; ++pass)
+    for (auto& ep : eps) {
+      if (pass == 0 && strfmt(ep.first, ":", ep.second) == avoid) continue;  // prefer another server
+      if ((c = comm::Connection::connect(ep.first, ep.second, timeout_ms, err))) break;
+    }
+  return c;
 }
 
 // channel name shared by the two ends of a connect-type=RCCL link
@@ -269,9 +351,17 @@ class QueryServerSrc : public BaseSrc {
       server_.reset();
       return false;
     }
+    if (connect_type_ == kHybrid) {
+      announcer_ = std::make_unique<HybridAnnouncer>();
+      if (!announcer_->announce(dest_host_, static_cast<int>(dest_port_), topic_, host_, server_->port(), &err)) {
+        post_error("tensor_query_serversrc: HYBRID announce: " + err);
+        return false;
+      }
+    }
     return true;
   }
   void on_stop() override {
+    announcer_.reset();
     if (server_ && connect_type_ != kRccl) server_->stop();
     req_.reset();
   }
@@ -328,6 +418,7 @@ class QueryServerSrc : public BaseSrc {
   StreamSet streams_;
   RankProps rp_;
   std::shared_ptr<comm::Group> req_;
+  std::unique_ptr<HybridAnnouncer> announcer_;
 };
 
 // -------------------------------------------------------- serversink ----
@@ -453,23 +544,57 @@ class QueryClient : public Element {
     seq_ = 0;
     if (connect_type_ == kRccl) return true;
     std::string err;
-    conn_ = comm::Connection::connect(dest_host_, static_cast<int>(dest_port_),
-                                      timeout_ms_ ? static_cast<int>(timeout_ms_) : 10000, &err);
-    if (!conn_) {
+    if (!connect_server(std::string(), &err)) {
       post_error("tensor_query_client: " + err);
       return false;
     }
+    return true;
+  }
+
+  // TCP / HYBRID / HIPIPC: connect + HELLO handshake (HYBRID: `avoid` = the
+  // server that just failed; another announced one is preferred)
+  bool connect_server(const std::string& avoid, std::string* err) {
+    conn_ = connect_endpoint(connect_type_, dest_host_, dest_port_, topic_,
+                             timeout_ms_ ? static_cast<int>(timeout_ms_) : 10000, err, avoid);
+    if (!conn_) return false;
     comm::Message hello;
     if (!conn_->recv(&hello, 30000) || hello.type != comm::MsgType::HELLO) {
-      post_error("tensor_query_client: no handshake from the server");
+      *err = "no handshake from the server";
       return false;
     }
     conn_->id = hello.client_id;
     if (connect_type_ == kHipIpc && !conn_->send_ipc_hello())
       NNSX_LOGW(name(), "HIPIPC: no GPU here, requests travel as bytes");
     server_caps_ = hello.caps.empty() ? Caps::from_string(tensor_caps_template_all()) : Caps::from_string(hello.caps);
-    pending_.clear();
-    seq_ = 0;
+    return true;
+  }
+
+  comm::Message request_of(const Buffer& b) {
+    comm::Message m;
+    m.type = comm::MsgType::DATA;
+    m.client_id = conn_->id;
+    m.seq = seq_++;
+    m.pts = b.pts;
+    m.dts = b.dts;
+    m.duration = b.duration;
+    m.blobs = b.mems;
+    return m;
+  }
+
+  // HYBRID failover (tensor_query_client.c:366-384): reconnect to another
+  // announced server and re-send every request still waiting for a reply
+  bool failover() {
+    if (connect_type_ != kHybrid) return false;
+    const std::string failed = conn_ ? conn_->peer() : std::string();
+    if (conn_) conn_->close();
+    std::string err;
+    if (!connect_server(failed, &err)) {
+      NNSX_LOGW(name(), "HYBRID failover: ", err);
+      return false;
+    }
+    NNSX_LOGI(name(), "HYBRID failover: ", failed, " -> ", conn_->peer());
+    for (auto& b : pending_)
+      if (!conn_->send(request_of(*b))) return false;
     return true;
   }
   bool stop() override {
@@ -558,17 +683,12 @@ class QueryClient : public Element {
       return drain(std::max(1u, max_request_) - 1);
     }
     if (!conn_) return FlowReturn::ERROR;
-    comm::Message m;
-    m.type = comm::MsgType::DATA;
-    m.client_id = conn_->id;
-    m.seq = seq_++;
-    m.pts = buf->pts;
-    m.dts = buf->dts;
-    m.duration = buf->duration;
-    m.blobs = buf->mems;
-    if (!conn_->send(m)) {
-      post_error("tensor_query_client: failed to send a request to " + conn_->peer());
-      return FlowReturn::ERROR;
+    if (!conn_->send(request_of(*buf))) {
+      const std::string peer = conn_->peer();
+      if (!failover() || !conn_->send(request_of(*buf))) {
+        post_error("tensor_query_client: failed to send a request to " + peer);
+        return FlowReturn::ERROR;
+      }
     }
     pending_.push_back(buf);
     return drain(std::max(1u, max_request_) - 1);
@@ -599,6 +719,7 @@ class QueryClient : public Element {
       bool timed_out = false;
       const int t = timeout_ms_ ? static_cast<int>(timeout_ms_) : -1;
       if (!conn_ || !conn_->recv(&r, t, &timed_out)) {
+        if (!timed_out && failover()) continue;
         post_error(timed_out ? "tensor_query_client: timed out waiting for the server"
                              : "tensor_query_client: connection to the server lost");
         return FlowReturn::ERROR;
@@ -677,6 +798,13 @@ class EdgeSink : public BaseSink {
       post_error("edgesink: " + err);
       return false;
     }
+    if (connect_type_ == kHybrid) {
+      announcer_ = std::make_unique<HybridAnnouncer>();
+      if (!announcer_->announce(dest_host_, static_cast<int>(dest_port_), topic_, host_, listener_.port(), &err)) {
+        post_error("edgesink: HYBRID announce: " + err);
+        return false;
+      }
+    }
     running_ = true;
     accept_thr_ = std::thread([this] {
       while (running_) {
@@ -703,6 +831,7 @@ class EdgeSink : public BaseSink {
   bool stop() override {
     running_ = false;
     g_.reset();
+    announcer_.reset();
     listener_.close();
     if (accept_thr_.joinable()) accept_thr_.join();
     std::vector<std::thread> rs;
@@ -821,6 +950,7 @@ class EdgeSink : public BaseSink {
   int rccl_mode_ = 0;
   unsigned rr_ = 0;
   std::shared_ptr<comm::Group> g_;
+  std::unique_ptr<HybridAnnouncer> announcer_;
 };
 
 // =============================================================== edgesrc ====
@@ -849,7 +979,7 @@ class EdgeSrc : public BaseSrc {
     caps_str_.clear();
     if (connect_type_ == kRccl) return true;
     std::string err;
-    conn_ = comm::Connection::connect(dest_host_, static_cast<int>(dest_port_), 10000, &err);
+    conn_ = connect_endpoint(connect_type_, dest_host_, dest_port_, topic_, 10000, &err);
     if (!conn_) {
       post_error("edgesrc: " + err);
       return false;

@@ -11,6 +11,7 @@ void register_tensor_elements();   // converter/transform/sink/mux/demux/merge/s
 void register_filter_elements();   // tensor_filter
 void register_decoder_elements();  // tensor_decoder
 void register_comm_elements();
+void register_mqtt_elements();     // mqttsink / mqttsrc
 void register_grpc_elements();     // tensor_src_grpc / tensor_sink_grpc     // tensor_query_* / edge / mqtt-like
 void register_extra_elements();    // crop/if/rate/repo/sparse/debug/trainer/iio/join/datarepo
 

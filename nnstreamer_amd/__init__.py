@@ -48,6 +48,7 @@ from ._C import (  # noqa: E402,F401
     Caps,
     Element,
     Memory,
+    MqttBroker,
     NnsxError,
     Pipeline,
     config_dump,
