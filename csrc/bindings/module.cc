@@ -16,6 +16,7 @@
 #include "filter/filter.h"
 #include "kernels/kernels.h"
 #include "runtime/hip_util.h"
+#include "runtime/pbtxt.h"
 #include "runtime/pipeline.h"
 #include "runtime/plugin_api.h"
 
@@ -448,6 +449,15 @@ PYBIND11_MODULE(_C, m) {
       });
 
   m.def("parse_launch", [](const std::string& d) { return parse_launch(d); });
+  m.def("to_pbtxt", [](const Pipeline& p, bool with_options) { return pipeline_to_pbtxt(p, with_options); },
+        py::arg("pipeline"), py::arg("with_options") = false,
+        "MediaPipe-style pbtxt of a pipeline (tools/development/parser/convert.c)");
+  m.def("pbtxt_to_launch", [](const std::string& t) {
+    std::string err;
+    std::string d = pbtxt_to_launch(t, &err);
+    if (d.empty()) throw Error(err);
+    return d;
+  }, py::arg("pbtxt"), "Launch description of a pbtxt graph (the reverse conversion)");
   m.def("make_element", [](const std::string& f, const std::string& n) { return make_element(f, n); },
         py::arg("factory"), py::arg("name") = "");
 

@@ -71,6 +71,8 @@ from ._C import (  # noqa: E402,F401
     parse_dimension,
     parse_launch,
     parse_meta_header,
+    pbtxt_to_launch,
+    to_pbtxt,
     register_converter_custom,
     register_custom_easy,
     register_decoder_custom,

@@ -34,3 +34,41 @@ def test_launch_errors():
     assert _run("nnstreamer_amd.tools.launch", "nosuchelement ! fakesink").returncode == 2
     r = _run("nnstreamer_amd.tools.launch", "-t", "1", "videotestsrc is-live=true ! fakesink")
     assert r.returncode == 3
+
+
+def test_pbtxt_matches_reference_converter_naming(nns):
+    """convert.c naming: sources/sinks are graph streams, internal streams
+    <factory>_<index>_<srcpad>, repeated factories <factory>_<n>."""
+    p = nns.parse_launch("videotestsrc num-buffers=1 ! video/x-raw,format=RGB,width=8,height=8 ! tensor_converter "
+                         "! tee name=t t. ! queue ! tensor_sink t. ! queue ! fakesink")
+    txt = nns.to_pbtxt(p)
+    assert txt.startswith('input_stream: "videotestsrc"\noutput_stream: "tensor_sink"\noutput_stream: "fakesink"\n')
+    assert 'calculator: "teeCalculator"\n\tinput_stream: "tensor_converter_0_0"\n\toutput_stream: "tee_0_0"\n' \
+           '\toutput_stream: "tee_0_1"' in txt
+    assert txt.count('calculator: "queueCalculator"') == 2
+    assert "capsfilter" not in txt  # caps are link attributes
+
+
+def test_pbtxt_roundtrip_runs(nns):
+    desc = ("videotestsrc num-buffers=3 ! video/x-raw,format=RGB,width=8,height=8 ! tensor_converter "
+            "! tensor_transform mode=typecast option=float32 ! tensor_sink name=out")
+    txt = nns.to_pbtxt(nns.parse_launch(desc), True)
+    back = nns.pbtxt_to_launch(txt)
+    p = nns.parse_launch(back)
+    got = []
+    p.get_by_name("tensor_sink").connect("new-data", lambda b: got.append(b.memory(0).size))
+    p.run(timeout=30)
+    p.stop()
+    assert got == [8 * 8 * 3 * 4] * 3
+
+
+def test_pbtxt_cli(tmp_path):
+    import subprocess
+    import sys
+    out = subprocess.run([sys.executable, "-m", "nnstreamer_amd.tools.pbtxt", "videotestsrc ! tensor_converter ! fakesink"],
+                         capture_output=True, text=True, cwd=ROOT, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert 'calculator: "tensor_converterCalculator"' in out.stdout
+    bad = subprocess.run([sys.executable, "-m", "nnstreamer_amd.tools.pbtxt", "-p"], input="node: { input_stream: \"x\" }",
+                         capture_output=True, text=True, cwd=ROOT, timeout=120)
+    assert bad.returncode == 1 and "calculator" in bad.stderr
