@@ -1,5 +1,8 @@
 """nnsx-check / nnsx-launch command-line tools (reference confchk and gst-launch)."""
 import json
+
+import numpy as np
+import pytest
 import os
 import subprocess
 import sys
@@ -72,3 +75,37 @@ def test_pbtxt_cli(tmp_path):
     bad = subprocess.run([sys.executable, "-m", "nnstreamer_amd.tools.pbtxt", "-p"], input="node: { input_stream: \"x\" }",
                          capture_output=True, text=True, cwd=ROOT, timeout=120)
     assert bad.returncode == 1 and "calculator" in bad.stderr
+
+
+@pytest.mark.parametrize("dynamic,allocate", [(False, False), (True, True)])
+def test_codegen_c_skeleton_builds_and_runs(nns, tmp_path, dynamic, allocate):
+    from nnstreamer_amd.tools.codegen import generate
+    files = generate("My Filter", dynamic, allocate, "c", str(tmp_path))
+    r = subprocess.run(["sh", files[1]], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    lib = tmp_path / "libnnsx_customfilter_my_filter.so"
+    caps = "other/tensors,format=static,num_tensors=1,dimensions=4,types=float32,framerate=0/1"
+    p = nns.parse_launch(f"appsrc name=src caps={caps} ! tensor_filter framework=custom model={lib} ! tensor_sink name=s")
+    got = []
+    p.get_by_name("s").connect("new-data", lambda b: got.append(b.memory(0).numpy("float32").copy()))
+    p.set_state("playing")
+    p.get_by_name("src").push_buffer(np.arange(4, dtype=np.float32), pts=0)
+    p.get_by_name("src").end_of_stream()
+    assert p.wait(30)[0] == "eos", p.messages()
+    p.stop()
+    np.testing.assert_array_equal(got[0], np.arange(4, dtype=np.float32))
+
+
+def test_codegen_python_skeleton_runs(nns, tmp_path):
+    from nnstreamer_amd.tools.codegen import generate
+    path = generate("py filter", False, False, "python", str(tmp_path))[0]
+    caps = "other/tensors,format=static,num_tensors=1,dimensions=4,types=float32,framerate=0/1"
+    p = nns.parse_launch(f"appsrc name=src caps={caps} ! tensor_filter framework=python3 model={path} ! tensor_sink name=s")
+    got = []
+    p.get_by_name("s").connect("new-data", lambda b: got.append(b.memory(0).numpy("float32").copy()))
+    p.set_state("playing")
+    p.get_by_name("src").push_buffer(np.ones(4, dtype=np.float32), pts=0)
+    p.get_by_name("src").end_of_stream()
+    assert p.wait(30)[0] == "eos", p.messages()
+    p.stop()
+    np.testing.assert_array_equal(got[0], np.ones(4, dtype=np.float32))
