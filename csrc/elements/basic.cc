@@ -583,11 +583,17 @@ class VideoTestSrc : public BaseSrc {
     int64_t n = animated ? std::max<int64_t>(1, pool_size_) : 1;
     if (num_buffers_ >= 0) n = std::min<int64_t>(n, std::max<int64_t>(1, num_buffers_));  // frames ever shown
     frames_.resize(static_cast<size_t>(n));
+    // one pinned block holds the whole ring (a camera's mmap'ed capture ring):
+    // consecutive frames are adjacent, so a batching consumer uploads a run of
+    // them with one DMA copy
+    ring_ = Memory::alloc_pinned(static_cast<size_t>(n) * info_.size);
+    for (int64_t i = 0; i < n; ++i)
+      frames_[static_cast<size_t>(i)] = Memory::view(ring_, static_cast<size_t>(i) * info_.size, info_.size);
     const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<std::thread> th;
     for (unsigned t = 0; t < nt; ++t)
       th.emplace_back([this, t, nt, n] {
-        for (int64_t i = t; i < n; i += nt) frames_[static_cast<size_t>(i)] = render(i);
+        for (int64_t i = t; i < n; i += nt) render(i, frames_[static_cast<size_t>(i)]);
       });
     for (auto& x : th) x.join();
     return true;
@@ -663,8 +669,8 @@ class VideoTestSrc : public BaseSrc {
     }
   }
 
-  MemoryPtr render(int64_t frame) {
-    auto m = Memory::alloc_pinned(info_.size);
+  MemoryPtr render(int64_t frame, MemoryPtr m = nullptr) {
+    if (!m) m = Memory::alloc_pinned(info_.size);
     uint8_t* p = static_cast<uint8_t*>(m->data());
     std::memset(p, 0, info_.size);
     const std::string& f = info_.format;
@@ -715,6 +721,7 @@ class VideoTestSrc : public BaseSrc {
   int64_t pool_size_ = 8;
   VideoInfo info_;
   std::vector<MemoryPtr> frames_;
+  MemoryPtr ring_;
 };
 
 // ----------------------------------------------------------- audiotestsrc ----

@@ -385,7 +385,24 @@ class TensorConverter : public Element {
     }
     out = dev >= 0 ? Memory::alloc_device(size, dev, s) : Memory::alloc_host(size);
     size_t done = 0;
-    if (dev >= 0 && gather_eligible(size)) {
+    std::vector<std::pair<const char*, size_t>> runs;
+    if (dev >= 0 && dma_runs(size, &runs)) {
+      // adjacent frames (a capture ring): a few DMA copies, no CU time spent on the upload
+      for (auto& r : runs) {
+        hip::check(hipMemcpyAsync(static_cast<char*>(out->data()) + done, r.first, r.second, hipMemcpyDefault, s),
+                   "ring upload");
+        done += r.second;
+      }
+      for (size_t left = size; left > 0;) {
+        Piece& p = adapter_.front();
+        const size_t n = std::min(left, p.size() - p.off);
+        p.mem->record_use(s, dev);
+        p.off += n;
+        left -= n;
+        if (p.off == p.size()) adapter_.pop_front();
+      }
+    }
+    if (dev >= 0 && done < size && gather_eligible(size)) {
       // one gather launch per <=128 pieces instead of one hipMemcpyAsync per frame
       kernels::GatherArgs g;
       auto flush = [&]() {
@@ -432,6 +449,29 @@ class TensorConverter : public Element {
     if (dev >= 0) out->mark_ready(s);
     avail_ -= size;
     return out;
+  }
+
+  // the next `size` bytes as at most kMaxRuns address-contiguous runs of unpadded
+  // pinned-host pieces
+  bool dma_runs(size_t size, std::vector<std::pair<const char*, size_t>>* runs) const {
+    constexpr size_t kMaxRuns = 4;
+    size_t seen = 0;
+    for (const Piece& p : adapter_) {
+      // pinned host pieces only (device pieces keep the kernel path, which waits on them)
+      if (p.padded() || p.mem->place() != MemPlace::PINNED) return runs->clear(), false;
+      const char* d = static_cast<const char*>(p.mem->data()) + p.off;
+      const size_t n = std::min(size - seen, p.size() - p.off);
+      if (!runs->empty() && runs->back().first + runs->back().second == d)
+        runs->back().second += n;
+      else if (runs->size() == kMaxRuns)
+        return runs->clear(), false;
+      else
+        runs->emplace_back(d, n);
+      seen += n;
+      if (seen >= size) break;
+    }
+    if (seen < size) return runs->clear(), false;
+    return true;
   }
 
   // every piece that feeds the next `size` bytes is device-readable in place (pinned host or HBM)

@@ -15,6 +15,7 @@
 //  * avgpool   global average pool [B,HW,C] -> [B,C].
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "kernels/mbv2.h"
@@ -60,7 +61,8 @@ __global__ void __launch_bounds__(256) pw_gemm_kernel(const uint16_t* __restrict
                                                       const float* __restrict__ bias,   // [N]
                                                       const uint16_t* __restrict__ res, // [M][N] or null
                                                       void* __restrict__ y,             // [M][N]
-                                                      int M, int N, int K, int Kpad, int act) {
+                                                      int M, int N, int K, int Kpad, int act,
+                                                      int kchunk) {  // k-steps of this grid.z slice
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int m_base = blockIdx.x * PW_BM + wave * (PW_RM * 16);
@@ -85,7 +87,9 @@ __global__ void __launch_bounds__(256) pw_gemm_kernel(const uint16_t* __restrict
 #pragma unroll
   for (int j = 0; j < PW_RN; ++j) wrow[j] = wt + static_cast<int64_t>(n_base + j * 16 + li) * Kpad;
 
-  for (int k0 = 0; k0 < Kpad; k0 += 32) {
+  const int kbeg = blockIdx.z * kchunk * 32;
+  const int kend = min(Kpad, kbeg + kchunk * 32);
+  for (int k0 = kbeg; k0 < kend; k0 += 32) {
     const int k = k0 + kq;
     bf16x8_t bfrag[PW_RM];
 #pragma unroll
@@ -117,6 +121,13 @@ __global__ void __launch_bounds__(256) pw_gemm_kernel(const uint16_t* __restrict
       const int n = n_base + j * 16 + (lane >> 4) * 4;
       if (n >= N) continue;
       float v[4];
+      if (OUT_F32 && gridDim.z > 1) {  // split-K partial sum (fp32, no residual / activation)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          atomicAdd(static_cast<float*>(y) + static_cast<int64_t>(m) * N + n + r,
+                    acc[i][j][r] + (blockIdx.z == 0 ? bias[n + r] : 0.f));
+        continue;
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bias[n + r];
       if (res) {
@@ -192,75 +203,111 @@ __global__ void __launch_bounds__(256) dw3x3_kernel(const uint16_t* __restrict__
 // --------------------------------------------------------------------- stem ----
 // x: f32 [B][H][W][3]; w: f32 [3][3][3][32] (ky,kx,ci,co); y: bf16 [B][Ho][Wo][32]
 // T = float: the normalised frame; T = uint8_t: the raw RGB frame, normalised on
-// the fly through a 256-entry LUT lut[u] = (u + add) / div (bit-identical to the
-// tensor_transform arithmetic it replaces, padding stays 0 in the normalised domain)
+// the fly through a 256-entry LUT lut[u] = (u + add) / div (the tensor_transform
+// arithmetic it replaces; padding stays 0 in the normalised domain)
+// MFMA stem: the 3x3/2 conv 3 -> 32 as D[co][px] = W[co][k] . P[px][k]^T with
+// k = (ky, kx, ci) = 27 padded to 32 -- two v_mfma_f32_16x16x32_bf16 per 16
+// output pixels.  A workgroup owns STEM_R output rows of one image: the
+// 2 * STEM_R + 1 input rows are normalised once into LDS (bf16, a zero column
+// on the left = the conv padding), each lane gathers its 8 patch values from
+// LDS (per-lane offsets fixed for the whole tile walk), and the epilogue writes
+// bias + act as bf16 NHWC.  The VALU direct-conv version did 27 byte loads and
+// 216 FMAs per 8 outputs and ran at ~1 TB/s of output; this one is bound by
+// the bf16 output stream.
+constexpr int STEM_R = 2;
+
 template <typename T>
-__global__ void __launch_bounds__(256) stem_kernel(const T* __restrict__ x, const float* __restrict__ w,
-                                                   const float* __restrict__ bias, uint16_t* __restrict__ y, int B,
-                                                   int H, int W, int Ho, int Wo, int act, float add, float div) {
-  __shared__ float sw[27 * 32];
-  __shared__ float sb[32];
+__global__ void __launch_bounds__(256) stem_mfma_kernel(const T* __restrict__ x, const float* __restrict__ w,
+                                                        const float* __restrict__ bias, uint16_t* __restrict__ y,
+                                                        int H, int W, int Ho, int Wo, int act, float add, float div) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t xin[];  // [2R+1][(W + 2) * 3] bf16
   __shared__ float lut[256];
-  for (int i = threadIdx.x; i < 27 * 32; i += blockDim.x) sw[i] = w[i];
-  if (threadIdx.x < 32) sb[threadIdx.x] = bias[threadIdx.x];
-  if (sizeof(T) == 1) lut[threadIdx.x] = (static_cast<float>(threadIdx.x) + add) / div;
-  __syncthreads();
-  const int64_t total = static_cast<int64_t>(B) * Ho * Wo * 4;
-  for (int64_t t = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; t < total;
-       t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const int og = static_cast<int>(t & 3);  // 8-channel output group
-    int64_t p = t >> 2;
-    const int ox = static_cast<int>(p % Wo);
-    p /= Wo;
-    const int oy = static_cast<int>(p % Ho);
-    const int b = static_cast<int>(p / Ho);
-    float acc[8];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, kq = (lane >> 4) * 8;
+  const int row_groups = (Ho + STEM_R - 1) / STEM_R;
+  const int b = blockIdx.x / row_groups;
+  const int oy0 = (blockIdx.x % row_groups) * STEM_R;
+  const int pitch = (W + 2) * 3;  // columns ix = -1 .. W (both pads)
+  if (sizeof(T) == 1) lut[tid] = (static_cast<float>(tid) + add) / div;
+  // A fragments (weights, rows = output channels) + this lane's bias values
+  bf16x8_t a[2];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) acc[q] = sb[og * 8 + q];
+  for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-      const int iy = oy * 2 - 1 + ky;
-      if (iy < 0 || iy >= H) continue;
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const int ix = ox * 2 - 1 + kx;
-        if (ix < 0 || ix >= W) continue;
-        const T* px = x + ((static_cast<int64_t>(b) * H + iy) * W + ix) * 3;
-        float in0, in1, in2;
-        if (sizeof(T) == 1) {
-          in0 = lut[static_cast<int>(px[0])];
-          in1 = lut[static_cast<int>(px[1])];
-          in2 = lut[static_cast<int>(px[2])];
-        } else {
-          in0 = static_cast<float>(px[0]);
-          in1 = static_cast<float>(px[1]);
-          in2 = static_cast<float>(px[2]);
-        }
-        const float* wk = sw + ((ky * 3 + kx) * 3) * 32 + og * 8;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) acc[q] += in0 * wk[q] + in1 * wk[32 + q] + in2 * wk[64 + q];
-      }
+    for (int j = 0; j < 8; ++j) {
+      const int k = kq + j;
+      a[t][j] = static_cast<short>(k < 27 ? f2bf(w[k * 32 + t * 16 + li]) : 0);
     }
-    uint32_t o[4];
+  float bv[2][4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      o[q] = pk_bf16(act_fn(acc[2 * q], act), act_fn(acc[2 * q + 1], act));
-    *reinterpret_cast<uint4*>(y + ((static_cast<int64_t>(b) * Ho + oy) * Wo + ox) * 32 + og * 8) = uint4{o[0], o[1], o[2], o[3]};
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[t][r] = bias[t * 16 + (lane >> 4) * 4 + r];
+  // this lane's 8 patch offsets relative to the pixel's top-left tap
+  int off[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = kq + j;
+    off[j] = k < 27 ? (k / 9) * pitch + ((k % 9) / 3) * 3 + (k % 3) : -1;
+  }
+  __syncthreads();  // lut
+  const int iy0 = oy0 * 2 - 1;
+  const int n_in = (2 * STEM_R + 1) * pitch;
+  const T* xb = x + static_cast<int64_t>(b) * H * W * 3;
+  for (int i = tid; i < n_in; i += 256) {
+    const int r = i / pitch, c = i % pitch;  // c = (ix + 1) * 3 + ci
+    const int iy = iy0 + r, ix = c / 3 - 1;
+    float v = 0.f;
+    if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+      const T raw = xb[(static_cast<int64_t>(iy) * W + ix) * 3 + c % 3];
+      v = sizeof(T) == 1 ? lut[static_cast<int>(raw)] : static_cast<float>(raw);
+    }
+    xin[i] = f2bf(v);
+  }
+  __syncthreads();
+  const int tiles_x = (Wo + 15) / 16;
+  for (int t = wave; t < STEM_R * tiles_x; t += 4) {
+    const int oyl = t / tiles_x, ox = (t % tiles_x) * 16 + li;
+    const int oy = oy0 + oyl;
+    // top-left tap of pixel ox: input row 2*oyl (local), column 2*ox - 1 (+1 pad) -> 2*ox
+    const int base = 2 * oyl * pitch + 2 * ox * 3;
+    const bool valid = ox < Wo && oy < Ho;
+    bf16x8_t bf;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bf[j] = static_cast<short>(valid && off[j] >= 0 ? xin[base + off[j]] : 0);
+    const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const f32x4_t d0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_mfma, a[0]),
+                                                               __builtin_bit_cast(bf16x8_mfma, bf), z, 0, 0, 0);
+    const f32x4_t d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_mfma, a[1]),
+                                                               __builtin_bit_cast(bf16x8_mfma, bf), z, 0, 0, 0);
+    if (!valid) continue;
+    uint16_t* yp = y + ((static_cast<int64_t>(b) * Ho + oy) * Wo + ox) * 32 + (lane >> 4) * 4;
+    uint2 o0, o1;
+    o0.x = pk_bf16(act_fn(d0[0] + bv[0][0], act), act_fn(d0[1] + bv[0][1], act));
+    o0.y = pk_bf16(act_fn(d0[2] + bv[0][2], act), act_fn(d0[3] + bv[0][3], act));
+    o1.x = pk_bf16(act_fn(d1[0] + bv[1][0], act), act_fn(d1[1] + bv[1][1], act));
+    o1.y = pk_bf16(act_fn(d1[2] + bv[1][2], act), act_fn(d1[3] + bv[1][3], act));
+    *reinterpret_cast<uint2*>(yp) = o0;
+    *reinterpret_cast<uint2*>(yp + 16) = o1;
   }
 }
 
 // ------------------------------------------------------------------ avgpool ----
+// One workgroup = one image x 64 channel groups (of 8); the 4 waves split the
+// pixels and meet in LDS.  (A thread per image x channel group gave only
+// B * C / 8 / 256 = 80 workgroups at batch 128: 18 us for 16 MB.)
 __global__ void __launch_bounds__(256) avgpool_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int B,
                                                       int HW, int C) {
+  __shared__ float part[4][64][9];  // +1: conflict-free column reads
   const int cg = C >> 3;
-  const int64_t total = static_cast<int64_t>(B) * cg;
-  for (int64_t t = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; t < total;
-       t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const int c = static_cast<int>(t % cg) * 8;
-    const int b = static_cast<int>(t / cg);
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int p = 0; p < HW; ++p) {
-      const uint4 v = *reinterpret_cast<const uint4*>(x + (static_cast<int64_t>(b) * HW + p) * C + c);
+  const int groups = (cg + 63) / 64;
+  const int b = blockIdx.x / groups;
+  const int g = (blockIdx.x % groups) * 64 + (threadIdx.x & 63);
+  const int wave = threadIdx.x >> 6;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (g < cg) {
+    for (int p = wave; p < HW; p += 4) {
+      const uint4 v = *reinterpret_cast<const uint4*>(x + (static_cast<int64_t>(b) * HW + p) * C + g * 8);
       const uint32_t vs[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -268,13 +315,20 @@ __global__ void __launch_bounds__(256) avgpool_kernel(const uint16_t* __restrict
         acc[2 * q + 1] += bf2f(vs[q] >> 16);
       }
     }
-    const float inv = 1.f / HW;
-    uint32_t o[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      o[q] = pk_bf16(acc[2 * q] * inv, acc[2 * q + 1] * inv);
-    *reinterpret_cast<uint4*>(y + static_cast<int64_t>(b) * C + c) = uint4{o[0], o[1], o[2], o[3]};
   }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) part[wave][threadIdx.x & 63][q] = acc[q];
+  __syncthreads();
+  if (wave != 0 || g >= cg) return;
+  const float inv = 1.f / HW;
+  float s[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) s[q] = (part[0][threadIdx.x][q] + part[1][threadIdx.x][q] + part[2][threadIdx.x][q] +
+                                      part[3][threadIdx.x][q]) * inv;
+  uint32_t o[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) o[q] = pk_bf16(s[2 * q], s[2 * q + 1]);
+  *reinterpret_cast<uint4*>(y + static_cast<int64_t>(b) * C + g * 8) = uint4{o[0], o[1], o[2], o[3]};
 }
 
 inline unsigned grid_cap(int64_t work) {
@@ -289,12 +343,26 @@ inline unsigned grid_cap(int64_t work) {
 void pw_gemm(const void* x, const void* wt, const float* bias, const void* res, void* y, int M, int N, int K, int Kpad,
              int act, bool out_f32, hipStream_t s) {
   dim3 grid((M + PW_BM - 1) / PW_BM, (N + PW_BN - 1) / PW_BN);
+  const int ksteps = Kpad / 32;
+  int chunk = ksteps;
+  // A small output grid (the classifier: M = batch, 16 workgroups) leaves most
+  // CUs idle while each workgroup walks all of K serially: split K over grid.z
+  // and reduce with fp32 atomics (fp32 output without residual / activation)
+  const int tiles = static_cast<int>(grid.x * grid.y);
+  if (out_f32 && !res && act == 0 && tiles < 256 && ksteps >= 8) {
+    const int splits = std::min(ksteps / 2, (1024 + tiles - 1) / tiles);
+    chunk = (ksteps + splits - 1) / splits;
+    grid.z = static_cast<unsigned>((ksteps + chunk - 1) / chunk);
+    (void)hipMemsetAsync(y, 0, static_cast<size_t>(M) * N * sizeof(float), s);
+  }
   if (out_f32)
     hipLaunchKernelGGL(pw_gemm_kernel<true>, grid, dim3(256), 0, s, static_cast<const uint16_t*>(x),
-                       static_cast<const uint16_t*>(wt), bias, static_cast<const uint16_t*>(res), y, M, N, K, Kpad, act);
+                       static_cast<const uint16_t*>(wt), bias, static_cast<const uint16_t*>(res), y, M, N, K, Kpad, act,
+                       chunk);
   else
     hipLaunchKernelGGL(pw_gemm_kernel<false>, grid, dim3(256), 0, s, static_cast<const uint16_t*>(x),
-                       static_cast<const uint16_t*>(wt), bias, static_cast<const uint16_t*>(res), y, M, N, K, Kpad, act);
+                       static_cast<const uint16_t*>(wt), bias, static_cast<const uint16_t*>(res), y, M, N, K, Kpad, act,
+                       chunk);
 }
 
 void dw3x3(const void* x, const void* w, const float* bias, void* y, int B, int H, int W, int C, int stride, int dil,
@@ -306,25 +374,34 @@ void dw3x3(const void* x, const void* w, const float* bias, void* y, int B, int 
                      static_cast<const uint16_t*>(w), bias, static_cast<uint16_t*>(y), B, H, W, C, Ho, Wo, stride, dil, act);
 }
 
+template <typename T>
+void stem_launch(const T* x, const float* w, const float* bias, void* y, int B, int H, int W, int act, float add,
+                 float div, hipStream_t s) {
+  const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  const size_t lds = sizeof(uint16_t) * (2 * STEM_R + 1) * (W + 2) * 3;
+  const unsigned grid = static_cast<unsigned>(B * ((Ho + STEM_R - 1) / STEM_R));
+  if (lds > 64 * 1024) {  // rows wider than ~3.6k pixels: opt into the full 160 KiB
+    static const bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_mfma_kernel<T>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+    if (!ok || lds > 160 * 1024) return;
+  }
+  hipLaunchKernelGGL(stem_mfma_kernel<T>, dim3(grid), dim3(256), lds, s, x, w, bias, static_cast<uint16_t*>(y), H, W,
+                     Ho, Wo, act, add, div);
+}
+
 void stem3x3(const float* x, const float* w, const float* bias, void* y, int B, int H, int W, int act, hipStream_t s) {
-  int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
-  int64_t work = static_cast<int64_t>(B) * Ho * Wo * 4;
-  hipLaunchKernelGGL(stem_kernel<float>, dim3(grid_cap(work)), dim3(256), 0, s, x, w, bias, static_cast<uint16_t*>(y),
-                     B, H, W, Ho, Wo, act, 0.f, 1.f);
+  stem_launch<float>(x, w, bias, y, B, H, W, act, 0.f, 1.f, s);
 }
 
 void stem3x3_u8(const uint8_t* x, const float* w, const float* bias, void* y, int B, int H, int W, int act, float add,
                 float div, hipStream_t s) {
-  int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
-  int64_t work = static_cast<int64_t>(B) * Ho * Wo * 4;
-  hipLaunchKernelGGL(stem_kernel<uint8_t>, dim3(grid_cap(work)), dim3(256), 0, s, x, w, bias,
-                     static_cast<uint16_t*>(y), B, H, W, Ho, Wo, act, add, div);
+  stem_launch<uint8_t>(x, w, bias, y, B, H, W, act, add, div, s);
 }
 
 void avgpool(const void* x, void* y, int B, int HW, int C, hipStream_t s) {
-  int64_t work = static_cast<int64_t>(B) * (C / 8);
-  hipLaunchKernelGGL(avgpool_kernel, dim3(grid_cap(work)), dim3(256), 0, s, static_cast<const uint16_t*>(x),
-                     static_cast<uint16_t*>(y), B, HW, C);
+  const int groups = (C / 8 + 63) / 64;
+  hipLaunchKernelGGL(avgpool_kernel, dim3(static_cast<unsigned>(B * groups)), dim3(256), 0, s,
+                     static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), B, HW, C);
 }
 
 }  // namespace kernels

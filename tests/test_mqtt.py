@@ -93,16 +93,25 @@ def test_mqtt_header_layout(nns):
     got = []
     ready = threading.Event()
 
+    def recv_exact(s, n):
+        buf = b""
+        while len(buf) < n:
+            chunk = s.recv(n - len(buf))
+            if not chunk:
+                break
+            buf += chunk
+        return buf
+
     def raw_sub():
         s = socket.create_connection(("127.0.0.1", b.port))
         s.sendall(b"\x10\x0f\x00\x04MQTT\x04\x02\x00\x3c\x00\x03raw")
-        s.recv(4)
+        assert recv_exact(s, 4) == b"\x20\x02\x00\x00"
         s.sendall(b"\x82\x08\x00\x01\x00\x03hdr\x00")
-        s.recv(5)
+        assert recv_exact(s, 5) == b"\x90\x03\x00\x01\x00"
         ready.set()
         data = b""
         t0 = time.time()
-        while len(data) < 1024 + 40 and time.time() - t0 < 10:
+        while len(data) < 1050 and time.time() - t0 < 10:
             data += s.recv(65536)
         got.append(data)
         s.close()
