@@ -254,15 +254,34 @@ __global__ void __launch_bounds__(256) stem_mfma_kernel(const T* __restrict__ x,
   const int iy0 = oy0 * 2 - 1;
   const int n_in = (2 * STEM_R + 1) * pitch;
   const T* xb = x + static_cast<int64_t>(b) * H * W * 3;
-  for (int i = tid; i < n_in; i += 256) {
-    const int r = i / pitch, c = i % pitch;  // c = (ix + 1) * 3 + ci
-    const int iy = iy0 + r, ix = c / 3 - 1;
-    float v = 0.f;
-    if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
-      const T raw = xb[(static_cast<int64_t>(iy) * W + ix) * 3 + c % 3];
-      v = sizeof(T) == 1 ? lut[static_cast<int>(raw)] : static_cast<float>(raw);
+  if (sizeof(T) == 1 && (W * 3) % 4 == 0) {
+    // raw uint8 rows: 4 bytes per load (a row starts 4-aligned), LUT-normalised into LDS
+    const int wpr = W * 3 / 4;  // words per row
+    for (int i = tid; i < (2 * STEM_R + 1) * wpr; i += 256) {
+      const int r = i / wpr, wd = i % wpr;
+      const int iy = iy0 + r;
+      uint32_t v4 = 0;
+      const bool in = iy >= 0 && iy < H;
+      if (in) v4 = reinterpret_cast<const uint32_t*>(xb + static_cast<int64_t>(iy) * W * 3)[wd];
+      uint16_t* dst = xin + r * pitch + 3 + wd * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dst[j] = in ? f2bf(lut[(v4 >> (8 * j)) & 255]) : 0;
     }
-    xin[i] = f2bf(v);
+    for (int i = tid; i < (2 * STEM_R + 1) * 6; i += 256) {  // left / right padding columns
+      const int r = i / 6, j = i % 6;
+      xin[r * pitch + (j < 3 ? j : pitch - 6 + j)] = 0;
+    }
+  } else {
+    for (int i = tid; i < n_in; i += 256) {
+      const int r = i / pitch, c = i % pitch;  // c = (ix + 1) * 3 + ci
+      const int iy = iy0 + r, ix = c / 3 - 1;
+      float v = 0.f;
+      if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+        const T raw = xb[(static_cast<int64_t>(iy) * W + ix) * 3 + c % 3];
+        v = sizeof(T) == 1 ? lut[static_cast<int>(raw)] : static_cast<float>(raw);
+      }
+      xin[i] = f2bf(v);
+    }
   }
   __syncthreads();
   const int tiles_x = (Wo + 15) / 16;
@@ -349,8 +368,10 @@ void pw_gemm(const void* x, const void* wt, const float* bias, const void* res, 
   // CUs idle while each workgroup walks all of K serially: split K over grid.z
   // and reduce with fp32 atomics (fp32 output without residual / activation)
   const int tiles = static_cast<int>(grid.x * grid.y);
-  if (out_f32 && !res && act == 0 && tiles < 256 && ksteps >= 8) {
-    const int splits = std::min(ksteps / 2, (1024 + tiles - 1) / tiles);
+  if (out_f32 && !res && act == 0 && tiles < 256 && ksteps >= 16) {
+    // >= 8 k-steps per slice: more slices only add fp32 atomics on the same outputs
+    // (20 slices x 2 k-steps ran 2x slower than no split for the 128 x 1000 x 1280 classifier)
+    const int splits = std::min(ksteps / 8, (256 + tiles - 1) / tiles);
     chunk = (ksteps + splits - 1) / splits;
     grid.z = static_cast<unsigned>((ksteps + chunk - 1) / chunk);
     (void)hipMemsetAsync(y, 0, static_cast<size_t>(M) * N * sizeof(float), s);
