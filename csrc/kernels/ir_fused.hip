@@ -79,7 +79,10 @@ __global__ void __launch_bounds__(256) ir_block_kernel(IrBlockArgs a) {
   constexpr int HROW = hrow(S, F32H);
   using HT = typename std::conditional<F32H, float, uint16_t>::type;  // hidden tile element
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  const int xrow = a.cin32 + 8;  // LDS pitch of the input tile
+  // a.cin32 == 32 * KS_MAX (the launcher picks the instantiation): every
+  // input-tile index below divides by compile-time constants
+  constexpr int CIN32 = 32 * KS_MAX;
+  constexpr int xrow = CIN32 + 8;  // LDS pitch of the input tile
   uint16_t* xs = smem;                                                // [PIN16][xrow]
   HT* hidbuf = reinterpret_cast<HT*>(xs + PIN16 * xrow);             // 2 x [PIN16][HROW] (double buffered)
   uint16_t* dwo = reinterpret_cast<uint16_t*>(hidbuf + 2 * PIN16 * HROW);  // [64][DROW]
@@ -91,8 +94,7 @@ __global__ void __launch_bounds__(256) ir_block_kernel(IrBlockArgs a) {
   const int wave = tid >> 6;
   const int li = lane & 15;
   const int kq = (lane >> 4) * 8;
-  const int ksteps = a.cin32 / 32;
-  const int vec_per_px = a.cin32 / 8;
+  constexpr int vec_per_px = CIN32 / 8;
   const int tiles_img = a.tiles_x * a.tiles_y;
   const int total_tiles = tiles_img * a.B;
   // persistent walk: this workgroup owns tiles [t_begin, t_end) (consecutive along x)
@@ -105,7 +107,7 @@ __global__ void __launch_bounds__(256) ir_block_kernel(IrBlockArgs a) {
   auto load_expand = [&](int c0) {
 #pragma unroll
     for (int at = 0; at < 2; ++at) {
-      const uint16_t* wrow = a.we + static_cast<int64_t>(c0 + at * 16 + li) * a.cin32 + kq;
+      const uint16_t* wrow = a.we + static_cast<int64_t>(c0 + at * 16 + li) * CIN32 + kq;
 #pragma unroll
       for (int ks = 0; ks < KS_MAX; ++ks) ea[at][ks] = *reinterpret_cast<const bf16x8_t*>(wrow + ks * 32);
 #pragma unroll
@@ -115,9 +117,24 @@ __global__ void __launch_bounds__(256) ir_block_kernel(IrBlockArgs a) {
 
   // next tile's input vectors are fetched into registers while the current tile computes
   bf16x8_t pf[NV];
-  auto fetch_tile = [&](int t) {
-    const int b = t / tiles_img, r = t % tiles_img;
-    const int iy0 = (r / a.tiles_x) * TO * S - 1, ix0 = (r % a.tiles_x) * TO * S - 1;
+  // tile coordinates advance incrementally (one SALU division per workgroup,
+  // not four per tile: at 112x112 a workgroup walks ~65 tiles)
+  struct TileXY {
+    int b, ty, tx;
+  };
+  auto next_xy = [&](TileXY c) {
+    if (++c.tx == a.tiles_x) {
+      c.tx = 0;
+      if (++c.ty == a.tiles_y) {
+        c.ty = 0;
+        ++c.b;
+      }
+    }
+    return c;
+  };
+  auto fetch_tile = [&](TileXY c) {
+    const int b = c.b;
+    const int iy0 = c.ty * TO * S - 1, ix0 = c.tx * TO * S - 1;
     const uint16_t* xb = a.x + static_cast<int64_t>(b) * a.H * a.W * a.cin;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
@@ -143,8 +160,12 @@ __global__ void __launch_bounds__(256) ir_block_kernel(IrBlockArgs a) {
   };
 
   if (t_begin >= t_end) return;
+  TileXY cur;
+  cur.b = t_begin / tiles_img;
+  cur.ty = (t_begin - cur.b * tiles_img) / a.tiles_x;
+  cur.tx = t_begin - cur.b * tiles_img - cur.ty * a.tiles_x;
   if (a.has_expand) load_expand(0);
-  fetch_tile(t_begin);
+  fetch_tile(cur);
   for (int v = tid; v < 9 * a.hid / 8; v += 256) {
     const bf16x8_t w8 = *reinterpret_cast<const bf16x8_t*>(a.wd + v * 8);
     if constexpr (F32H) {
@@ -161,13 +182,13 @@ __global__ void __launch_bounds__(256) ir_block_kernel(IrBlockArgs a) {
   const int dx = lane & 7;
   const int dq = (lane >> 3) * 4;
 
-  for (int tile = t_begin; tile < t_end; ++tile) {
+  for (int tile = t_begin; tile < t_end; ++tile, cur = next_xy(cur)) {
     store_tile();
     __syncthreads();
-    if (tile + 1 < t_end) fetch_tile(tile + 1);  // in flight during this tile's compute
+    if (tile + 1 < t_end) fetch_tile(next_xy(cur));  // in flight during this tile's compute
 
-    const int b = tile / tiles_img, r = tile % tiles_img;
-    const int oy0 = (r / a.tiles_x) * TO, ox0 = (r % a.tiles_x) * TO;
+    const int b = cur.b;
+    const int oy0 = cur.ty * TO, ox0 = cur.tx * TO;
     const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
 
     f32x4_t acc[NOT];

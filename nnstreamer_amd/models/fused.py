@@ -126,11 +126,17 @@ class Block(nn.Module):
         self.register_buffer("ir_wp", wp)
         # measured on MI355X (scripts/bench_ir.py, batch 256): the fused kernel wins on every
         # MobileNetV2 block except the 7x7 160->960->320 one (too few tiles, 20 output tiles/lane)
+        self.min_tiles = int(os.environ.get("NNSX_IR_MIN_TILES", "256"))
         self.use_ir = (bool(torch.ops.nnsx.ir_supported(int(ir.stride), cin, hp, self.cout)) and FUSE_IR
                        and (self.has_expand or hid == hp) and self.cout < 320)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if self.use_ir and self.dw.dilation == 1:
+        # the fused kernel walks one 8x8 output tile per workgroup slot: with fewer
+        # tiles than CUs (7x7 maps below batch 256) the unfused GEMM chain is faster
+        # (scripts/bench_ir.py: 56 vs 64 us at batch 128, 94 vs 67 us at batch 256)
+        ho = (x.shape[1] - 1) // self.dw.stride + 1
+        tiles = x.shape[0] * ((ho + 7) // 8) * ((ho + 7) // 8)
+        if self.use_ir and self.dw.dilation == 1 and tiles >= self.min_tiles:
             return torch.ops.nnsx.ir_block(x, self.ir_we, self.ir_be, self.ir_wd, self.ir_bd, self.ir_wp,
                                            self.project.bias, self.dw.stride, self.cout, self.has_expand,
                                            self.use_res)
