@@ -11,8 +11,9 @@ namespace kernels {
 
 // y[M][N] = act(x[M][K] . wt[N][K]^T + bias) (+ res), bf16 in, bf16/f32 out.
 // wt is zero-padded to [ceil16(N)][Kpad], Kpad = ceil32(K).  act: 0 none, 1 relu6, 2 relu
+// Npad: rows of wt (0 = ceil64(N)); large-M layers run the LDS-staged kernel
 void pw_gemm(const void* x, const void* wt, const float* bias, const void* res, void* y, int M, int N, int K, int Kpad,
-             int act, bool out_f32, hipStream_t s);
+             int act, bool out_f32, hipStream_t s, int Npad = 0);
 // depthwise 3x3, stride 1|2, dilation d (padding d); x [B][H][W][C], w [9][C], C % 8 == 0
 void dw3x3(const void* x, const void* w, const float* bias, void* y, int B, int H, int W, int C, int stride, int dil,
            int act, hipStream_t s);

@@ -89,6 +89,10 @@ __global__ void __launch_bounds__(256) pw_gemm_kernel(const uint16_t* __restrict
 
   const int kbeg = blockIdx.z * kchunk * 32;
   const int kend = min(Kpad, kbeg + kchunk * 32);
+  // unrolled so the loads of 4 k-steps are in flight together (the kernel has
+  // no LDS stage: with ~3 waves per SIMD a load -> MFMA chain per k-step left
+  // the small 7x7 / classifier GEMMs latency bound)
+#pragma unroll 4
   for (int k0 = kbeg; k0 < kend; k0 += 32) {
     const int k = k0 + kq;
     bf16x8_t bfrag[PW_RM];
@@ -142,6 +146,125 @@ __global__ void __launch_bounds__(256) pw_gemm_kernel(const uint16_t* __restrict
       if (OUT_F32) {
         float4 o{v[0], v[1], v[2], v[3]};
         *reinterpret_cast<float4*>(static_cast<float*>(y) + static_cast<int64_t>(m) * N + n) = o;
+      } else {
+        uint2 o;
+        o.x = pk_bf16(v[0], v[1]);
+        o.y = pk_bf16(v[2], v[3]);
+        *reinterpret_cast<uint2*>(static_cast<uint16_t*>(y) + static_cast<int64_t>(m) * N + n) = o;
+      }
+    }
+  }
+}
+
+// LDS-staged pointwise GEMM for the large-M layers (7x7 / 14x14 stages, the
+// head): the BM x 32 pixel tile and BN x 32 weight tile of each k-step are
+// loaded once per workgroup (coalesced 16-B vectors, prefetched into
+// registers one k-step ahead, double-buffered LDS, one barrier per k-step) and
+// shared by the 2 x 2 waves; each wave computes a (BM/2) x (BN/2) sub-tile.
+// The register-direct kernel above re-reads x once per 64-channel block and
+// the weights once per wave: ~120 MB of L2 traffic for the 6272 x 320 x 1280
+// head GEMM.  LDS rows are 48 bf16 (96 B): fragment reads conflict-free.
+constexpr int GP = 48;
+
+template <int BM, int BN, bool OUT_F32>
+__global__ void __launch_bounds__(256) pw_gemm_lds_kernel(const uint16_t* __restrict__ x,   // [M][K]
+                                                          const uint16_t* __restrict__ wt,  // [Npad][Kpad]
+                                                          const float* __restrict__ bias,   // [N]
+                                                          const uint16_t* __restrict__ res, // [M][N] or null
+                                                          void* __restrict__ y,             // [M][N]
+                                                          int M, int N, int K, int Kpad, int Npad, int act) {
+  constexpr int RM = BM / 32, RN = BN / 32;  // 16-row tiles per wave
+  constexpr int VX = BM / 64, VW = BN / 64;  // 16-B vectors per thread per tile
+  __shared__ __attribute__((aligned(16))) uint16_t xs[2][BM * GP];
+  __shared__ __attribute__((aligned(16))) uint16_t ws[2][BN * GP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int li = lane & 15, kq = (lane >> 4) * 8;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const bf16x8_t zero = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+
+  bf16x8_t px[VX], pw[VW];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      const int v = tid + i * 256, row = v >> 2, k = k0 + (v & 3) * 8;
+      const int m = m0 + row;
+      px[i] = (m < M && k < K) ? *reinterpret_cast<const bf16x8_t*>(x + static_cast<int64_t>(m) * K + k) : zero;
+    }
+#pragma unroll
+    for (int i = 0; i < VW; ++i) {
+      const int v = tid + i * 256, row = v >> 2, k = k0 + (v & 3) * 8;
+      const int n = n0 + row;
+      pw[i] = n < Npad ? *reinterpret_cast<const bf16x8_t*>(wt + static_cast<int64_t>(n) * Kpad + k) : zero;
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      const int v = tid + i * 256;
+      *reinterpret_cast<bf16x8_t*>(&xs[buf][(v >> 2) * GP + (v & 3) * 8]) = px[i];
+    }
+#pragma unroll
+    for (int i = 0; i < VW; ++i) {
+      const int v = tid + i * 256;
+      *reinterpret_cast<bf16x8_t*>(&ws[buf][(v >> 2) * GP + (v & 3) * 8]) = pw[i];
+    }
+  };
+
+  f32x4_t acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = Kpad / 32;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int ks = 0; ks < nk; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nk) gload((ks + 1) * 32);  // in flight during this k-step's MFMAs
+    bf16x8_t a[RN], b[RM];
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+      a[j] = *reinterpret_cast<const bf16x8_t*>(&ws[buf][(wn * (BN / 2) + j * 16 + li) * GP + kq]);
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+      b[i] = *reinterpret_cast<const bf16x8_t*>(&xs[buf][(wm * (BM / 2) + i * 16 + li) * GP + kq]);
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_mfma, a[j]),
+                                                            __builtin_bit_cast(bf16x8_mfma, b[i]), acc[i][j], 0, 0, 0);
+    if (ks + 1 < nk) lstore(buf ^ 1);  // buf ^ 1 was last read before the previous barrier
+    __syncthreads();
+  }
+
+  // epilogue: lane owns channels n..n+3 of pixel m (as pw_gemm_kernel)
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+    const int m = m0 + wm * (BM / 2) + i * 16 + li;
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const int n = n0 + wn * (BN / 2) + j * 16 + (lane >> 4) * 4;
+      if (n >= N) continue;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bias[n + r];
+      if (res) {
+        const uint2 rr = *reinterpret_cast<const uint2*>(res + static_cast<int64_t>(m) * N + n);
+        v[0] += bf2f(rr.x & 0xffff);
+        v[1] += bf2f(rr.x >> 16);
+        v[2] += bf2f(rr.y & 0xffff);
+        v[3] += bf2f(rr.y >> 16);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], act);
+      if (OUT_F32) {
+        *reinterpret_cast<float4*>(static_cast<float*>(y) + static_cast<int64_t>(m) * N + n) =
+            float4{v[0], v[1], v[2], v[3]};
       } else {
         uint2 o;
         o.x = pk_bf16(v[0], v[1]);
@@ -360,7 +483,34 @@ inline unsigned grid_cap(int64_t work) {
 }  // namespace
 
 void pw_gemm(const void* x, const void* wt, const float* bias, const void* res, void* y, int M, int N, int K, int Kpad,
-             int act, bool out_f32, hipStream_t s) {
+             int act, bool out_f32, hipStream_t s, int Npad) {
+  if (Npad <= 0) Npad = (N + 63) / 64 * 64;
+  // large M (the 7x7 / 14x14 stages and the head at batch >= 32): LDS-staged tiles,
+  // 128 x 128 when that still gives every CU a workgroup, else 64 x 64
+  if (M >= 2048 && K % 8 == 0 && N % 4 == 0) {
+    const auto* xp = static_cast<const uint16_t*>(x);
+    const auto* wp = static_cast<const uint16_t*>(wt);
+    const auto* rp = static_cast<const uint16_t*>(res);
+    const int big = ((M + 127) / 128) * ((N + 127) / 128);
+    if (big >= 256) {
+      const dim3 g((M + 127) / 128, (N + 127) / 128);
+      if (out_f32)
+        hipLaunchKernelGGL((pw_gemm_lds_kernel<128, 128, true>), g, dim3(256), 0, s, xp, wp, bias, rp, y, M, N, K, Kpad,
+                           Npad, act);
+      else
+        hipLaunchKernelGGL((pw_gemm_lds_kernel<128, 128, false>), g, dim3(256), 0, s, xp, wp, bias, rp, y, M, N, K,
+                           Kpad, Npad, act);
+    } else {
+      const dim3 g((M + 63) / 64, (N + 63) / 64);
+      if (out_f32)
+        hipLaunchKernelGGL((pw_gemm_lds_kernel<64, 64, true>), g, dim3(256), 0, s, xp, wp, bias, rp, y, M, N, K, Kpad,
+                           Npad, act);
+      else
+        hipLaunchKernelGGL((pw_gemm_lds_kernel<64, 64, false>), g, dim3(256), 0, s, xp, wp, bias, rp, y, M, N, K, Kpad,
+                           Npad, act);
+    }
+    return;
+  }
   dim3 grid((M + PW_BM - 1) / PW_BM, (N + PW_BN - 1) / PW_BN);
   const int ksteps = Kpad / 32;
   int chunk = ksteps;

@@ -40,7 +40,7 @@ at::Tensor pw_conv_cuda(const at::Tensor& x, const at::Tensor& wt, const at::Ten
   }
   nnsx::kernels::pw_gemm(x.data_ptr(), wt.data_ptr(), bias.data_ptr<float>(), r, y.data_ptr(), static_cast<int>(M),
                          static_cast<int>(N), static_cast<int>(K), static_cast<int>(Kpad), static_cast<int>(act), out_f32,
-                         cur_stream());
+                         cur_stream(), static_cast<int>(wt.size(0)));
   return y;
 }
 
