@@ -17,6 +17,7 @@
 #include "kernels/kernels.h"
 #include "runtime/hip_util.h"
 #include "runtime/pbtxt.h"
+#include "runtime/tracer.h"
 #include "runtime/pipeline.h"
 #include "runtime/plugin_api.h"
 
@@ -449,6 +450,10 @@ PYBIND11_MODULE(_C, m) {
       });
 
   m.def("parse_launch", [](const std::string& d) { return parse_launch(d); });
+  m.def("tracer_enable", [](const std::string& spec) { trace::enable(spec); }, py::arg("spec"),
+        "Enable built-in tracers: 'proctime;interlatency;framerate;roctx' ('' disables)");
+  m.def("tracer_reset", [] { trace::reset(); });
+  m.def("tracer_report", [] { return trace::report_json(); }, "Tracer statistics as a JSON string");
   m.def("to_pbtxt", [](const Pipeline& p, bool with_options) { return pipeline_to_pbtxt(p, with_options); },
         py::arg("pipeline"), py::arg("with_options") = false,
         "MediaPipe-style pbtxt of a pipeline (tools/development/parser/convert.c)");

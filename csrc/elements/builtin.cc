@@ -32,6 +32,7 @@ void ensure_builtin_elements() {
     register_extra_elements();
     register_comm_elements();
     register_mqtt_elements();
+    register_fault_inject();
     register_grpc_elements();
     register_host_frameworks();
     register_torch_frameworks();

@@ -12,6 +12,7 @@ void register_filter_elements();   // tensor_filter
 void register_decoder_elements();  // tensor_decoder
 void register_comm_elements();
 void register_mqtt_elements();     // mqttsink / mqttsrc
+void register_fault_inject();      // fault_inject (testing)
 void register_grpc_elements();     // tensor_src_grpc / tensor_sink_grpc     // tensor_query_* / edge / mqtt-like
 void register_extra_elements();    // crop/if/rate/repo/sparse/debug/trainer/iio/join/datarepo
 

@@ -1,4 +1,5 @@
 #include "runtime/element.h"
+#include "runtime/tracer.h"
 
 #include <algorithm>
 
@@ -78,7 +79,27 @@ FlowReturn Pad::push(BufferPtr buf) {
   }
   if (flushing_.load() || peer_->flushing_.load()) return FlowReturn::FLUSHING;
   if (peer_->eos_.load()) return FlowReturn::EOS;
-  FlowReturn r = peer_->parent()->chain(peer_, std::move(buf));
+  Element* sink = peer_->parent();
+  FlowReturn r;
+  const bool traced = trace::flags() != 0;
+  try {
+    if (traced) {  // built-in tracers (runtime/tracer.h)
+      if (buf->origin_ns < 0) buf->origin_ns = now_ns();
+      trace::src_push(parent());
+      trace::chain_enter(sink, buf->origin_ns);
+      r = sink->chain(peer_, std::move(buf));
+      trace::chain_exit(sink);
+    } else {
+      r = sink->chain(peer_, std::move(buf));
+    }
+  } catch (const std::exception& e) {
+    // failure detection: anything thrown downstream (a HIP error, a framework
+    // exception) becomes an error message of the element that threw, not a
+    // silently dead streaming thread
+    if (traced) trace::chain_exit(sink);
+    sink->post_error(e.what());
+    r = FlowReturn::ERROR;
+  }
   last_flow_.store(r);
   return r;
 }

@@ -36,7 +36,9 @@ std::string device_arch(int dev) {
 
 void check(hipError_t e, const char* what) {
   if (e != hipSuccess) {
-    throw Error(strfmt("HIP error ", hipGetErrorName(e), " (", hipGetErrorString(e), ") at ", what));
+    int dev = -1;
+    (void)hipGetDevice(&dev);
+    throw Error(strfmt("HIP error ", hipGetErrorName(e), " (", hipGetErrorString(e), ") at ", what, " on device ", dev));
   }
 }
 

@@ -140,6 +140,7 @@ struct Buffer {
   int64_t offset_end = -1;
   uint32_t flags = 0;
   BufferMeta meta;
+  int64_t origin_ns = -1;  // tracer: time of the first push at its source (interlatency)
 
   size_t n_memory() const { return mems.size(); }
   MemoryPtr& mem(size_t i) { return mems.at(i); }
@@ -156,6 +157,7 @@ struct Buffer {
     offset_end = o.offset_end;
     flags = o.flags;
     meta = o.meta;
+    origin_ns = o.origin_ns;
   }
 };
 using BufferPtr = std::shared_ptr<Buffer>;

@@ -184,6 +184,7 @@ bool Pipeline::set_state(State target) {
         }
       }
       state_ = next;
+      dump_dot();
     } else {
       State next = static_cast<State>(static_cast<int>(state_) - 1);
       if (next == State::READY) {
@@ -241,6 +242,18 @@ void Pipeline::send_eos() {
       Event ev = Event::make_eos();
       for (Pad* p : e->src_pads()) p->push_event(ev);
     }
+  }
+}
+
+// NNSX_DEBUG_DUMP_DOT_DIR=<dir>: <dir>/<pipeline>.<state>.dot after each upward state change
+void Pipeline::dump_dot() const {
+  const char* dir = std::getenv("NNSX_DEBUG_DUMP_DOT_DIR");
+  if (!dir || !*dir) return;
+  const std::string path = strfmt(dir, "/", name(), ".", state_name(state_), ".dot");
+  if (FILE* f = std::fopen(path.c_str(), "w")) {
+    const std::string d = dot();
+    std::fwrite(d.data(), 1, d.size(), f);
+    std::fclose(f);
   }
 }
 

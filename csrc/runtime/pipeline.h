@@ -68,6 +68,7 @@ class Pipeline : public Element {
   // called by sinks
   void sink_reached_eos(Element* sink);
   std::string dot() const;  // graph description (GST_DEBUG_DUMP_DOT_DIR analogue)
+  void dump_dot() const;    // to $NNSX_DEBUG_DUMP_DOT_DIR when set
 
  private:
   std::vector<std::unique_ptr<Element>> elems_;

@@ -73,6 +73,9 @@ from ._C import (  # noqa: E402,F401
     parse_meta_header,
     pbtxt_to_launch,
     to_pbtxt,
+    tracer_enable,
+    tracer_report,
+    tracer_reset,
     register_converter_custom,
     register_custom_easy,
     register_decoder_custom,

@@ -82,7 +82,7 @@ def write_ninja(debug: bool = False) -> str:
         "  deps = gcc",
         "  description = HIP $in",
         "rule link",
-        f"  command = $hipcc -shared -fPIC --offload-arch={ARCH} $in -o $out {lib_dirs} -ltorch -ltorch_cpu -ltorch_hip -lc10 -lc10_hip -lamdhip64 -L/opt/rocm/lib -lrccl -ldl -lpthread -Wl,--no-as-needed",
+        f"  command = $hipcc -shared -fPIC --offload-arch={ARCH} $in -o $out {lib_dirs} -ltorch -ltorch_cpu -ltorch_hip -lc10 -lc10_hip -lamdhip64 -L/opt/rocm/lib -lrccl -lrocprofiler-sdk-roctx -ldl -lpthread -Wl,--no-as-needed",
         "  description = LINK $out",
     ]
     objs = []

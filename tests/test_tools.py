@@ -109,3 +109,19 @@ def test_codegen_python_skeleton_runs(nns, tmp_path):
     assert p.wait(30)[0] == "eos", p.messages()
     p.stop()
     np.testing.assert_array_equal(got[0], np.ones(4, dtype=np.float32))
+
+
+def test_parallel_helpers(monkeypatch):
+    import nnstreamer_amd.parallel as P
+    monkeypatch.setenv("RANK", "2")
+    monkeypatch.setenv("WORLD_SIZE", "3")
+    monkeypatch.setenv("LOCAL_RANK", "2")
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", "30000")
+    monkeypatch.delenv("NNSX_STORE", raising=False)
+    info = P.rank_info(use_gpu=False)
+    assert (info.rank, info.world, info.device, info.store) == (2, 3, -1, "127.0.0.1:30017")
+    assert list(P.split_work(10, info)) == [7, 8, 9]
+    assert P.format_pipeline("tensor_allgather rank={rank} store={store}", info) == \
+        "tensor_allgather rank=2 store=127.0.0.1:30017"
+    assert P.gather_stats([1.5]) == [1.5]  # no process group: identity
