@@ -141,7 +141,7 @@ def test_transform_stand(nns):
     x = (np.random.rand(60) * 100).astype(np.float32)
     b = _transform(nns, "stand", "default", x, "float32", "3:20")
     ref = np.abs((x.astype(np.float64) - x.mean()) / x.std())
-    np.testing.assert_allclose(b.memory(0).numpy("float32"), ref, rtol=1e-5)
+    np.testing.assert_allclose(b.memory(0).numpy("float32"), ref, rtol=1e-5, atol=1e-6)
     b = _transform(nns, "stand", "dc-average:float64,per-channel:true", x, "float32", "3:20")
     x64 = x.reshape(20, 3).astype(np.float64)
     r2 = (x64 - x64.mean(0)).ravel()
