@@ -493,9 +493,18 @@ void Connection::close() {
   }
 }
 
-Listener::~Listener() { close(); }
+Listener::~Listener() {
+  close();
+  release();
+}
+
+void Listener::release() {
+  const int fd = fd_.exchange(-1);
+  if (fd >= 0) ::close(fd);
+}
 
 bool Listener::listen(const std::string& host, int port, std::string* err) {
+  release();  // a previous socket: its accept loop was joined after close()
   sockaddr_in addr;
   if (!resolve(host.empty() ? "0.0.0.0" : host, port, &addr)) {
     if (err) *err = "cannot resolve " + host;
@@ -518,25 +527,26 @@ bool Listener::listen(const std::string& host, int port, std::string* err) {
 }
 
 std::shared_ptr<Connection> Listener::accept(int timeout_ms) {
-  if (fd_ < 0 || closed_) return nullptr;
-  pollfd pfd{fd_, POLLIN, 0};
+  const int lfd = fd_.load();
+  if (lfd < 0 || closed_) return nullptr;
+  pollfd pfd{lfd, POLLIN, 0};
   if (::poll(&pfd, 1, timeout_ms) <= 0 || closed_) return nullptr;
   sockaddr_in peer;
   socklen_t len = sizeof(peer);
-  int fd = ::accept(fd_, reinterpret_cast<sockaddr*>(&peer), &len);
+  int fd = ::accept(lfd, reinterpret_cast<sockaddr*>(&peer), &len);
   if (fd < 0) return nullptr;
   char buf[64];
   inet_ntop(AF_INET, &peer.sin_addr, buf, sizeof(buf));
   return make_connection(fd, strfmt(buf, ":", ntohs(peer.sin_port)));
 }
 
+// wakes a blocked accept(); the descriptor itself stays open until release()
+// (destructor / next listen) so a concurrent accept() never polls a closed --
+// possibly already reused -- descriptor number (found by scripts/tsan_check.sh)
 void Listener::close() {
   closed_ = true;
-  if (fd_ >= 0) {
-    ::shutdown(fd_, SHUT_RDWR);
-    ::close(fd_);
-    fd_ = -1;
-  }
+  const int fd = fd_.load();
+  if (fd >= 0) ::shutdown(fd, SHUT_RDWR);
 }
 
 void MessageQueue::push(Message m) {

@@ -116,7 +116,8 @@ class Listener {
   int port() const { return port_; }
 
  private:
-  int fd_ = -1;
+  void release();     // ::close the socket (no accept() may still be running)
+  std::atomic<int> fd_{-1};
   int port_ = 0;
   std::atomic<bool> closed_{false};
 };

@@ -125,3 +125,13 @@ def test_parallel_helpers(monkeypatch):
     assert P.format_pipeline("tensor_allgather rank={rank} store={store}", info) == \
         "tensor_allgather rank=2 store=127.0.0.1:30017"
     assert P.gather_stats([1.5]) == [1.5]  # no process group: identity
+
+
+@pytest.mark.skipif(os.environ.get("NNSX_TSAN") != "1", reason="ThreadSanitizer build takes ~2 min: NNSX_TSAN=1")
+def test_tsan_host_runtime():
+    """scripts/tsan_check.sh: TSan build of the host runtime driving the threaded
+    elements (queue/tee/mux, query server+clients, MQTT, rank groups); exit 66 = race."""
+    r = subprocess.run(["bash", os.path.join(ROOT, "scripts", "tsan_check.sh")], capture_output=True, text=True,
+                       timeout=1500)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "WARNING: ThreadSanitizer" not in r.stderr
