@@ -129,11 +129,16 @@ class TorchInstance : public FilterInstance {
     }
   }
 
+  // hot reload (is-updatable, tensor_filter_common.c:1404-1462): the new
+  // module is loaded and placed on the device next to the running one, then
+  // swapped in under the invoke lock -- frames keep flowing during the load and
+  // no frame ever sees a half-loaded model
   bool reload_model(const FilterProperties& p) override {
     try {
+      torch::jit::Module fresh = load_module(p.model_files.at(0));
       std::lock_guard<std::mutex> lk(mu_);
-      load(p.model_files.at(0));
-      graphs_.clear();
+      module_ = std::move(fresh);
+      graphs_.clear();  // captured graphs point at the old weights
       return true;
     } catch (const std::exception& e) {
       NNSX_LOGE("pytorch", "reload failed: ", e.what());
@@ -155,16 +160,18 @@ class TorchInstance : public FilterInstance {
     }
   }
 
-  void load(const std::string& path) {
+  torch::jit::Module load_module(const std::string& path) {
     hip::DeviceGuard g(device_);
-    module_ = torch::jit::load(path, dev());
-    module_.eval();
+    torch::jit::Module m = torch::jit::load(path, dev());
+    m.eval();
     // inference-only: freeze when possible (constant-folds attributes)
     try {
-      module_ = torch::jit::freeze(module_);
+      m = torch::jit::freeze(m);
     } catch (...) {
     }
+    return m;
   }
+  void load(const std::string& path) { module_ = load_module(path); }
 
   at::Tensor prepare(at::Tensor t) {
     if (compute_dtype_ != DType::END && at::isFloatingType(t.scalar_type())) t = t.to(to_torch(compute_dtype_));

@@ -110,3 +110,40 @@ def test_pytorch_single_gpu_zero_copy(nns, tmp_path):
     (yn,) = s.invoke(x.cpu().numpy())
     np.testing.assert_allclose(yn.reshape(16, 6), m.cuda()(x).detach().cpu().numpy(), rtol=1e-4, atol=1e-4)
     s.close()
+
+
+class _Scale(torch.nn.Module):
+    def __init__(self, k: float):
+        super().__init__()
+        self.k = k
+
+    def forward(self, x):
+        return x * self.k
+
+
+def test_pytorch_hot_reload_mid_stream(nns, tmp_path):
+    """is-updatable + a new model= while PLAYING (tensor_filter_common.c:1404-1462):
+    frames before the swap see model A, frames after it model B, none is lost."""
+    a, b = tmp_path / "a.pt", tmp_path / "b.pt"
+    torch.jit.script(_Scale(2.0)).save(str(a))
+    torch.jit.script(_Scale(3.0)).save(str(b))
+    caps = "other/tensors,format=static,num_tensors=1,dimensions=4,types=float32,framerate=0/1"
+    p = nns.parse_launch(f"appsrc name=src caps={caps} ! tensor_filter name=f framework=pytorch model={a} "
+                         "is-updatable=true accelerator=false ! tensor_sink name=s")
+    got = []
+    p.get_by_name("s").connect("new-data", lambda buf: got.append(float(buf.memory(0).numpy("float32")[0])))
+    p.set_state("playing")
+    src = p.get_by_name("src")
+    for i in range(3):
+        src.push_buffer(np.ones(4, np.float32), pts=i)
+    import time
+    t0 = time.time()
+    while len(got) < 3 and time.time() - t0 < 10:
+        time.sleep(0.01)
+    p.get_by_name("f").set_property("model", str(b))
+    for i in range(3, 6):
+        src.push_buffer(np.ones(4, np.float32), pts=i)
+    src.end_of_stream()
+    assert p.wait(30)[0] == "eos", p.messages()
+    p.stop()
+    assert got == [2.0, 2.0, 2.0, 3.0, 3.0, 3.0]
