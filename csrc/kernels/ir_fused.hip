@@ -85,7 +85,8 @@ __global__ void __launch_bounds__(256) ir_block_kernel(IrBlockArgs a) {
   constexpr int xrow = CIN32 + 8;  // LDS pitch of the input tile
   uint16_t* xs = smem;                                                // [PIN16][xrow]
   HT* hidbuf = reinterpret_cast<HT*>(xs + PIN16 * xrow);             // 2 x [PIN16][HROW] (double buffered)
-  uint16_t* dwo = reinterpret_cast<uint16_t*>(hidbuf + 2 * PIN16 * HROW);  // [64][DROW]
+  // (bf16 without expand: no hidden tile at all, the depthwise stage reads xs)
+  uint16_t* dwo = reinterpret_cast<uint16_t*>(hidbuf + (a.has_expand || F32H ? 2 * PIN16 * HROW : 0));  // [64][DROW]
   HT* wds = reinterpret_cast<HT*>(dwo + 64 * DROW);                  // [9][hid] depthwise weights (staged once)
   float* bds = reinterpret_cast<float*>(wds + 9 * a.hid);            // [hid] depthwise bias
 
@@ -248,18 +249,21 @@ __global__ void __launch_bounds__(256) ir_block_kernel(IrBlockArgs a) {
         }
         // prefetch the next chunk's (or the next tile's first chunk's) expand operands
         load_expand(c0 + HC < a.hid ? c0 + HC : 0);
-      } else {
+      } else if constexpr (F32H) {
+        // no expand (t = 1): the hidden tile is the input tile, widened to fp32
         for (int v = tid; v < PIN16 * (HC / 8); v += 256) {
           const int p = v / (HC / 8), k = (v % (HC / 8)) * 8;
           const bf16x8_t x8 = *reinterpret_cast<const bf16x8_t*>(xs + p * xrow + c0 + k);
-          if constexpr (F32H) {
+          f32x4_t lo, hi;
 #pragma unroll
-            for (int r = 0; r < 8; ++r) hid[p * HROW + k + r] = bf2f(static_cast<uint16_t>(x8[r]));
-          } else {
-            *reinterpret_cast<bf16x8_t*>(hid + p * HROW + k) = x8;
+          for (int r = 0; r < 4; ++r) {
+            lo[r] = bf2f(static_cast<uint16_t>(x8[r]));
+            hi[r] = bf2f(static_cast<uint16_t>(x8[r + 4]));
           }
+          *reinterpret_cast<f32x4_t*>(hid + p * HROW + k) = lo;
+          *reinterpret_cast<f32x4_t*>(hid + p * HROW + k + 4) = hi;
         }
-      }
+      }  // bf16, no expand: the depthwise stage reads the input tile in place
       // one block barrier per chunk: hid is double buffered, dw/project are wave-local
       __syncthreads();
 
@@ -297,7 +301,8 @@ __global__ void __launch_bounds__(256) ir_block_kernel(IrBlockArgs a) {
               h0 = f32x2_t{hv[0], hv[1]};
               h1 = f32x2_t{hv[2], hv[3]};
             } else {
-              const uint2 hv = *reinterpret_cast<const uint2*>(hid + p * HROW + dq);
+              const uint2 hv = a.has_expand ? *reinterpret_cast<const uint2*>(hid + p * HROW + dq)
+                                            : *reinterpret_cast<const uint2*>(xs + p * xrow + c0 + dq);
               h0 = f32x2_t{__uint_as_float(hv.x << 16), __uint_as_float(hv.x & 0xffff0000u)};
               h1 = f32x2_t{__uint_as_float(hv.y << 16), __uint_as_float(hv.y & 0xffff0000u)};
             }
@@ -400,10 +405,10 @@ bool launch_s(const IrBlockArgs& a, int n_ot, size_t lds, dim3 grid, hipStream_t
 }  // namespace
 
 namespace {
-size_t lds_total(int stride, bool f, int cin32, int hid) {
+size_t lds_total(int stride, bool f, int cin32, int hid, bool has_expand = true) {
   const int pin16 = tile_in_px16(stride);
   return sizeof(uint16_t) * (static_cast<size_t>(pin16) * (cin32 + 8) + 64 * DROW) +
-         static_cast<size_t>(hbytes(f)) * 2 * static_cast<size_t>(pin16) * hrow(stride, f) +
+         (has_expand || f ? static_cast<size_t>(hbytes(f)) * 2 * static_cast<size_t>(pin16) * hrow(stride, f) : 0) +
          (9 * static_cast<size_t>(hbytes(f)) + sizeof(float)) * static_cast<size_t>(hid);  // dw weights + bias
 }
 // fp32 hidden tile when it costs no workgroup per CU, or on the large early
@@ -411,7 +416,8 @@ size_t lds_total(int stride, bool f, int cin32, int hid) {
 // still fit.  Measured at batch 256 (scripts/bench_ir.py): fp32 wins at
 // 112/56 px even at 3-vs-4 workgroups per CU, loses at 28 px (3 vs 4) and
 // whenever it drops to 1 workgroup, ties at 14 px.
-bool use_f32_hidden(int stride, int cin32, int hid, int hw) {
+bool use_f32_hidden(int stride, int cin32, int hid, int hw, bool has_expand) {
+  if (!has_expand) return false;  // bf16: the depthwise stage reads the input tile in place
   const size_t f = lds_total(stride, true, cin32, hid), b = lds_total(stride, false, cin32, hid);
   if (f > kLdsLimit) return false;
   return kLdsLimit / f >= kLdsLimit / b || (hw >= 56 * 56 && kLdsLimit / f >= 2);
@@ -441,8 +447,8 @@ bool ir_block(const IrBlockArgs& args, hipStream_t s) {
   a.tiles_x = (a.Wo + TO - 1) / TO;
   if (!ir_block_supported(a.stride, a.cin, a.hid, a.cout)) return false;
   const int n_ot = (a.cout + 15) / 16;
-  const bool f = use_f32_hidden(a.stride, a.cin32, a.hid, a.H * a.W);
-  const size_t lds = lds_total(a.stride, f, a.cin32, a.hid);
+  const bool f = use_f32_hidden(a.stride, a.cin32, a.hid, a.H * a.W, a.has_expand != 0);
+  const size_t lds = lds_total(a.stride, f, a.cin32, a.hid, a.has_expand != 0);
   // persistent grid: enough workgroups for every CU to hold several (LDS-limited), each
   // walking a run of consecutive tiles so the next tile's input loads overlap compute
   // one resident round: every workgroup slot of the chip walks an equal run of tiles
