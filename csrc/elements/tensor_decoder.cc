@@ -37,6 +37,7 @@ class TensorDecoder : public BaseTransform {
     for (int i = 0; i < 9; ++i) {
       prop_string("option" + std::to_string(i + 1), &options_[i], "Option " + std::to_string(i + 1) + " of the decoder mode",
                   [this, i] {
+                    if (i == 0 && mode_ == "custom-code") return load_mode();  // the callback's name
                     if (inst_ && !inst_->set_option(i, options_[i]))
                       throw Error("decoder " + mode_ + " rejected option" + std::to_string(i + 1) + "=" + options_[i]);
                   });
@@ -53,6 +54,10 @@ class TensorDecoder : public BaseTransform {
   void load_mode() {
     inst_.reset();
     auto parts = split(mode_, ':', 2);
+    // mode=custom-code option1=<name> (the reference's spelling, gsttensor_decoder.c:469,763)
+    // or mode=custom-code:<name>
+    if (mode_ == "custom-code" && options_[0].empty()) return;  // name follows in option1
+    if (mode_ == "custom-code") parts = {"custom-code", options_[0]};
     if (parts.size() == 2 && parts[0] == "custom-code") {
       auto fn = Registry::get().find_as<DecoderCustomFn>(SubpluginKind::CUSTOM_DECODER, parts[1], false);
       if (!fn) throw Error("custom-code decoder '" + parts[1] + "' is not registered");
