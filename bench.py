@@ -103,6 +103,12 @@ def main():
 
     use_gpu = (not a.cpu) and torch.cuda.is_available() and nns.gpu_count() > 0
     dev = local_rank if use_gpu else -1
+    numa = "off"
+    if use_gpu and os.environ.get("NNSX_BENCH_NUMA", "1") != "0":
+        # each rank's streaming threads and its pinned frame ring on the GPU's own
+        # NUMA node: with 8 ranks the host-to-device uploads never cross sockets
+        numa = nns.bind_numa(dev)
+        print(f"rank {rank}: GPU {dev} NUMA binding: {numa}", file=sys.stderr, flush=True)
     workdir = os.path.join(tempfile.gettempdir(), f"nnsx_bench_{os.getuid()}_{rank}")
     os.makedirs(workdir, exist_ok=True)
     cfg = CONFIGS[a.config]
@@ -211,6 +217,7 @@ def main():
             "preprocess": ("tensor_transform normalisation fused into the model's stem kernel (uint8 input)"
                            if fuse_norm else "tensor_transform element"),
             "wall_s": round(t_end - t_start, 3),
+            "numa_binding": numa,
             "config": {
                 "model": cfg["desc"],
                 "global_batch": B * world,

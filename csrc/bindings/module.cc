@@ -70,6 +70,9 @@ PYBIND11_MODULE(_C, m) {
     return py::make_tuple(a, b, c);
   });
   m.def("gpu_count", [] { return hip::device_count(); });
+  m.def("gpu_numa_node", [](int d) { return hip::numa_node(d); }, py::arg("device") = 0);
+  m.def("bind_numa", [](int d) { return hip::bind_numa(d); }, py::arg("device"),
+        "Pin the process to the GPU's NUMA node (CPUs + preferred memory); call before building pipelines");
   m.def("gpu_arch", [](int d) { return hip::device_arch(d); }, py::arg("device") = 0);
   m.def("set_debug", [](const std::string& s) { log::set_threshold(s); });
   m.def("last_error", [] { return log::last_error(); });

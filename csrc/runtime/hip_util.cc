@@ -1,8 +1,15 @@
 #include "runtime/hip_util.h"
 
+#include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <cctype>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
 #include <map>
+#include <sstream>
 #include <thread>
 
 #include "core/util.h"
@@ -26,6 +33,51 @@ int device_count() {
 }
 
 bool available() { return device_count() > 0; }
+
+int numa_node(int dev) {
+  if (!available()) return -1;
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) != hipSuccess) return -1;
+  std::string id(bus);
+  for (auto& c : id) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
+  std::ifstream f("/sys/bus/pci/devices/" + id + "/numa_node");
+  int node = -1;
+  if (!(f >> node)) return -1;
+  return node;
+}
+
+std::string bind_numa(int dev) {
+  const int node = numa_node(dev);
+  if (node < 0) return "no NUMA node for the device";
+  // CPUs of the node, intersected with what this process may use (cgroups)
+  std::ifstream f("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");
+  std::string list;
+  if (!std::getline(f, list)) return "no cpulist for node " + std::to_string(node);
+  cpu_set_t allowed, want;
+  CPU_ZERO(&want);
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return "sched_getaffinity failed";
+  int n = 0;
+  std::stringstream ss(list);
+  std::string range;
+  while (std::getline(ss, range, ',')) {
+    int a = -1, b = -1;
+    if (std::sscanf(range.c_str(), "%d-%d", &a, &b) == 1) b = a;
+    for (int c = a; c >= 0 && c <= b && c < CPU_SETSIZE; ++c)
+      if (CPU_ISSET(c, &allowed)) {
+        CPU_SET(c, &want);
+        ++n;
+      }
+  }
+  std::string what;
+  if (n > 0 && sched_setaffinity(0, sizeof(want), &want) == 0) what = strfmt(n, " CPUs");
+  // prefer the node for new pages (pinned staging rings, pools): MPOL_PREFERRED = 1
+  unsigned long mask[16] = {0};
+  if (node < 16 * 64) {
+    mask[node / 64] = 1ul << (node % 64);
+    if (syscall(SYS_set_mempolicy, 1, mask, 16 * 64 + 1) == 0) what += what.empty() ? "memory" : " + memory";
+  }
+  return what.empty() ? "binding refused" : strfmt("node ", node, ": ", what);
+}
 
 std::string device_arch(int dev) {
   if (!available()) return "";

@@ -21,6 +21,11 @@ namespace hip {
 
 int device_count();              // 0 when no GPU / no driver (never throws)
 bool available();                // device_count() > 0
+// NUMA node of the GPU's PCIe root (-1: unknown)
+int numa_node(int dev);
+// pin this process's future threads to the GPU's NUMA node CPUs and prefer
+// that node for new memory (pinned upload rings); returns what was done
+std::string bind_numa(int dev);
 std::string device_arch(int dev);  // e.g. "gfx950"
 void check(hipError_t e, const char* what);  // throws nnsx::Error
 #define NNSX_HIP_CHECK(x) ::nnsx::hip::check((x), #x)

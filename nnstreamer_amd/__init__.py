@@ -59,8 +59,10 @@ from ._C import (  # noqa: E402,F401
     dtype_name,
     dtype_size,
     element_exists,
+    bind_numa,
     gpu_arch,
     gpu_count,
+    gpu_numa_node,
     kernels,
     last_error,
     list_elements,
