@@ -37,8 +37,9 @@ void register_torch_trainer() {}
 STUB
 $CXX $FLAGS -fsanitize=thread -c "$OUT/stubs.cc" -o "$OUT/stubs.o"
 $CXX $FLAGS -fsanitize=thread -c "$ROOT/tests/native/tsan_main.cc" -o "$OUT/tsan_main.o"
-$HIPCC -fsanitize=thread --offload-arch=gfx950 "${objs[@]}" "$OUT/stubs.o" "$OUT/tsan_main.o" -o "$OUT/tsan_main" \
-  -L/opt/rocm/lib -lrccl -lrocprofiler-sdk-roctx -lamdhip64 -ldl -lpthread
+# host link (the fat objects register their device code through libamdhip64)
+$CXX -fsanitize=thread "${objs[@]}" "$OUT/stubs.o" "$OUT/tsan_main.o" -o "$OUT/tsan_main" \
+  -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lrccl -lrocprofiler-sdk-roctx -lamdhip64 -ldl -lpthread
 cd "$ROOT"
 NNSX_DISABLE_GPU=1 TSAN_OPTIONS="suppressions=$ROOT/scripts/tsan.supp second_deadlock_stack=1 exitcode=66" \
   timeout 600 "$OUT/tsan_main"
