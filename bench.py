@@ -74,6 +74,13 @@ CONFIGS = {
                     decoder="tensor_decoder mode=image_segment option1=tflite-deeplab", per_frame=True,
                     metric="end-to-end frames/sec + p50 per-frame latency, DeepLabV3 513x513 segmentation pipeline",
                     desc="DeepLabV3-MobileNetV2 513x513 (tensor_filter + image_segment decoder)"),
+    # BASELINE.json config 5: PoseNet multi-source, outputs all-gathered across ranks
+    "posenet_multi": dict(size=257, model="posenet_fused", norm="typecast:float32,add:-127.5,div:127.5",
+                          decoder="tensor_decoder mode=pose_estimation option1=640:480 option2=257:257 "
+                                  "option3={pose} option4=heatmap-offset", per_frame=True, gather=True,
+                          metric="end-to-end frames/sec + p50 per-frame latency, PoseNet multi-source "
+                                 "pipeline with RCCL all-gather",
+                          desc="PoseNet-MobileNetV1 257x257 per rank + tensor_allgather of the pose tensors"),
     "posenet": dict(size=257, model="posenet_fused", norm="typecast:float32,add:-127.5,div:127.5",
                     decoder="tensor_decoder mode=pose_estimation option1=640:480 option2=257:257 option3={pose} "
                             "option4=heatmap-offset", per_frame=True,
@@ -149,9 +156,15 @@ def main():
         + f"! tensor_filter framework=pytorch model={model_path} input=3:{S}:{S}:{B} "
         f"inputtype={'uint8' if fuse_norm else 'float32'} "
         f"accelerator={accel} device={dev} custom=hipgraph:{graph} "
-        f"! queue max-size-buffers={a.queue} "
-        f"! {cfg['decoder'].format(**files)} "
+        + (f"! tee name=t t. ! queue max-size-buffers={a.queue} " if cfg.get("gather") else
+           f"! queue max-size-buffers={a.queue} ")
+        + f"! {cfg['decoder'].format(**files)} "
         f"! tensor_sink name=sink"
+        # multi-source: every rank's PoseNet outputs are all-gathered (RCCL over xGMI
+        # between GPUs, the TCP store on CPU) so each rank holds the synchronised
+        # multi-camera set -- one collective per batch, beside the local decoder
+        + (f" t. ! queue max-size-buffers={a.queue} ! tensor_allgather name=ag channel=posenet mode=concat "
+           f"rank={rank} world-size={world} device={dev} ! fakesink" if cfg.get("gather") else "")
     )
     per_step = B if cfg["per_frame"] else 1  # sink buffers per batch
     pipe = nns.parse_launch(desc)
@@ -173,6 +186,7 @@ def main():
     t_end = time.perf_counter()
     if dist is not None:
         dist.barrier()
+    gathered = pipe.get_by_name("ag").get_property("comm-bytes") if cfg.get("gather") else None
     pipe.stop()
 
     recs = [tuple(int(v) for v in e.split(":")) for e in sink.get_property("stats").split(",") if e]
@@ -218,6 +232,7 @@ def main():
                            if fuse_norm else "tensor_transform element"),
             "wall_s": round(t_end - t_start, 3),
             "numa_binding": numa,
+            **({"allgather_bytes_sent_received_rank0": gathered} if gathered is not None else {}),
             "config": {
                 "model": cfg["desc"],
                 "global_batch": B * world,

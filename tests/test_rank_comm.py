@@ -175,3 +175,20 @@ def test_allgather_torchrun_style_processes(tmp_path):
         assert p.returncode == 0, o
         line = [x for x in o.splitlines() if x.startswith("OUT")][0]
         assert line == "OUT [[0.0, 100.0], [1.0, 101.0], [2.0, 102.0]]", o
+
+
+def test_bench_posenet_multi_two_ranks_cpu():
+    """BASELINE.json config 5 through bench.py: two torchrun ranks, every rank's
+    PoseNet outputs all-gathered (TCP data plane on CPU; RCCL on GPUs)."""
+    import json
+    port = _free_port()
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--cpu", "--config", "posenet_multi", "--batch", "2", "--steps", "2", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["config"]["parallelism"] == "branch-dp2" and d["value"] > 0
+    sent, recv = (int(v) for v in d["allgather_bytes_sent_received_rank0"].split(":"))
+    assert sent > 0 and recv == sent  # equal-size contributions from both ranks
