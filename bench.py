@@ -74,6 +74,13 @@ CONFIGS = {
                     decoder="tensor_decoder mode=image_segment option1=tflite-deeplab", per_frame=True,
                     metric="end-to-end frames/sec + p50 per-frame latency, DeepLabV3 513x513 segmentation pipeline",
                     desc="DeepLabV3-MobileNetV2 513x513 (tensor_filter + image_segment decoder)"),
+    # BASELINE.json config 4: one camera rank fans its batches out to the other ranks
+    # (edgesink connect-type=RCCL rccl-mode=scatter -> ncclSend/ncclRecv over xGMI);
+    # every other rank runs DeepLabV3 + image_segment on what it receives
+    "deeplab_fan": dict(size=513, model="deeplab_fused", norm="typecast:float32,div:255.0",
+                        decoder="tensor_decoder mode=image_segment option1=tflite-deeplab", per_frame=True, fan=True,
+                        metric="end-to-end frames/sec, DeepLabV3 513x513 segmentation, branches fanned over RCCL",
+                        desc="DeepLabV3-MobileNetV2 513x513 on N-1 ranks fed by a camera rank (RCCL scatter)"),
     # BASELINE.json config 5: PoseNet multi-source, outputs all-gathered across ranks
     "posenet_multi": dict(size=257, model="posenet_fused", norm="typecast:float32,add:-127.5,div:127.5",
                           decoder="tensor_decoder mode=pose_estimation option1=640:480 option2=257:257 "
@@ -166,14 +173,30 @@ def main():
         + (f" t. ! queue max-size-buffers={a.queue} ! tensor_allgather name=ag channel=posenet mode=concat "
            f"rank={rank} world-size={world} device={dev} ! fakesink" if cfg.get("gather") else "")
     )
+    fan = bool(cfg.get("fan")) and world > 1
+    workers = world - 1 if fan else world
+    if fan:
+        link = f"connect-type=RCCL rccl-mode=scatter topic=fan rank={rank} world-size={world} device={dev}"
+        if rank == 0:  # the camera rank: upload batches, scatter them round-robin to the workers
+            desc = (f"videotestsrc num-buffers={frames * workers} pattern=snow pool-size={pool} "
+                    f"! video/x-raw,format=RGB,width={S},height={S},framerate=0/1 "
+                    f"! tensor_converter frames-per-tensor={B} device={dev} ! queue max-size-buffers=4 "
+                    f"! edgesink {link}")
+        else:
+            desc = (f"edgesrc {link} peer-rank=0 ! queue max-size-buffers=2 "
+                    f"! tensor_filter framework=pytorch model={model_path} input=3:{S}:{S}:{B} "
+                    f"inputtype={'uint8' if fuse_norm else 'float32'} accelerator={accel} device={dev} "
+                    f"custom=hipgraph:{graph} ! queue max-size-buffers={a.queue} "
+                    f"! {cfg['decoder'].format(**files)} ! tensor_sink name=sink")
     per_step = B if cfg["per_frame"] else 1  # sink buffers per batch
     pipe = nns.parse_launch(desc)
     sink = pipe.get_by_name("sink")
     # native per-buffer arrival stats (no Python callback per frame); sync-device
     # makes an arrival mean "the GPU has produced this frame", not "it was queued"
-    sink.set_property("emit-signal", "false")
-    sink.set_property("sync-device", "true")
-    sink.set_property("stats-every", "1")
+    if sink is not None:  # (the fan-out camera rank has no sink: it only produces)
+        sink.set_property("emit-signal", "false")
+        sink.set_property("sync-device", "true")
+        sink.set_property("stats-every", "1")
 
     if dist is not None:
         dist.barrier()
@@ -189,20 +212,26 @@ def main():
     gathered = pipe.get_by_name("ag").get_property("comm-bytes") if cfg.get("gather") else None
     pipe.stop()
 
-    recs = [tuple(int(v) for v in e.split(":")) for e in sink.get_property("stats").split(",") if e]
+    recs = [tuple(int(v) for v in e.split(":")) for e in sink.get_property("stats").split(",") if e] if sink else []
     arrivals = [t / 1e9 for i, (t, _) in enumerate(recs) if (i + 1) % per_step == 0]  # last frame of each batch
     step_lat = [[lat / 1e6 for _, lat in recs[k * per_step:(k + 1) * per_step] if lat >= 0]
                 for k in range(len(arrivals))]
     n = len(arrivals)
-    if n < total:
-        raise SystemExit(f"rank {rank}: only {n}/{total} batches reached the sink")
-    # timed region: exactly K steps after W warmup steps
-    t0 = arrivals[a.warmup - 1] if a.warmup > 0 else t_start
-    t1 = arrivals[a.warmup + a.steps - 1]
-    elapsed = t1 - t0
-    timed = [x for k in range(a.warmup, a.warmup + a.steps) for x in step_lat[k]]
-    lat = np.array(timed) if timed else np.array([0.0])
-    stats = torch.tensor([elapsed, float(np.percentile(lat, 50)), float(np.percentile(lat, 99))], dtype=torch.float64)
+    if sink is None:
+        stats = torch.zeros(3, dtype=torch.float64)  # the workers' clocks decide
+    else:
+        if n < total:
+            raise SystemExit(f"rank {rank}: only {n}/{total} batches reached the sink")
+        # timed region: exactly K steps after W warmup steps
+        t0 = arrivals[a.warmup - 1] if a.warmup > 0 else t_start
+        t1 = arrivals[a.warmup + a.steps - 1]
+        elapsed = t1 - t0
+        timed = [x for k in range(a.warmup, a.warmup + a.steps) for x in step_lat[k]]
+        lat = np.array(timed) if timed else np.array([0.0])
+        if fan:  # PTS were stamped on the camera rank's clock: no per-frame latency here
+            lat = np.array([0.0])
+        stats = torch.tensor([elapsed, float(np.percentile(lat, 50)), float(np.percentile(lat, 99))],
+                             dtype=torch.float64)
     if dist is not None:
         if dist.get_backend() == "nccl":
             stats = stats.cuda()
@@ -210,7 +239,7 @@ def main():
         stats = stats.cpu()
     elapsed, p50, p99 = stats.tolist()
     ms_per_step = elapsed / a.steps * 1e3
-    fps_total = world * a.steps * B / elapsed
+    fps_total = workers * a.steps * B / elapsed
     if rank == 0:
         out = {
             "metric": cfg["metric"],
@@ -225,8 +254,8 @@ def main():
             "vs_baseline": (round(fps_total / CPU_BASELINE_FPS, 2) if a.config == "mbv2" else None),
             "dtype": "bf16" if "fused" in a.model else "fp32",
             "data": "synthetic video frames (videotestsrc pattern=snow), random-init weights",
-            "p50_latency_ms": round(p50, 3),
-            "p99_latency_ms": round(p99, 3),
+            "p50_latency_ms": None if fan else round(p50, 3),
+            "p99_latency_ms": None if fan else round(p99, 3),
             "frames_per_step_per_gpu": B,
             "preprocess": ("tensor_transform normalisation fused into the model's stem kernel (uint8 input)"
                            if fuse_norm else "tensor_transform element"),
@@ -237,7 +266,7 @@ def main():
                 "model": cfg["desc"],
                 "global_batch": B * world,
                 "seq_len": 1,
-                "parallelism": f"branch-dp{world}",
+                "parallelism": f"fan-out 1->{workers} (RCCL scatter)" if fan else f"branch-dp{world}",
                 "pipeline": desc,
             },
         }

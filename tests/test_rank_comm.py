@@ -192,3 +192,18 @@ def test_bench_posenet_multi_two_ranks_cpu():
     assert d["config"]["parallelism"] == "branch-dp2" and d["value"] > 0
     sent, recv = (int(v) for v in d["allgather_bytes_sent_received_rank0"].split(":"))
     assert sent > 0 and recv == sent  # equal-size contributions from both ranks
+
+
+def test_bench_deeplab_fan_three_ranks_cpu():
+    """BASELINE.json config 4 through bench.py: rank 0 uploads frames and scatters
+    the batches round-robin (edgesink connect-type=RCCL rccl-mode=scatter) to two
+    DeepLab worker ranks."""
+    import json
+    port = _free_port()
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--cpu", "--config", "deeplab_fan", "--batch", "1", "--steps", "2", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert d["config"]["parallelism"].startswith("fan-out 1->2") and d["value"] > 0
