@@ -49,6 +49,8 @@ def parse_args():
                     help="keep the normalisation as a separate tensor_transform element")
     ap.add_argument("--cpu", action="store_true", help="CPU reference path (device=-1, torch CPU)")
     ap.add_argument("--queue", type=int, default=4, help="queue depth between filter and decoder")
+    ap.add_argument("--comm-backend", default="auto", choices=["auto", "rccl", "tcp"],
+                    help="posenet_multi: tensor_allgather data plane")
     ap.add_argument("--config", default=os.environ.get("NNSX_BENCH_CONFIG", "mbv2"),
                     choices=sorted(CONFIGS), help="BASELINE.json config (default: the headline MobileNetV2 pipeline)")
     return ap.parse_args()
@@ -171,7 +173,7 @@ def main():
         # between GPUs, the TCP store on CPU) so each rank holds the synchronised
         # multi-camera set -- one collective per batch, beside the local decoder
         + (f" t. ! queue max-size-buffers={a.queue} ! tensor_allgather name=ag channel=posenet mode=concat "
-           f"rank={rank} world-size={world} device={dev} ! fakesink" if cfg.get("gather") else "")
+           f"rank={rank} world-size={world} device={dev} comm-backend={a.comm_backend} ! fakesink" if cfg.get("gather") else "")
     )
     fan = bool(cfg.get("fan")) and world > 1
     workers = world - 1 if fan else world

@@ -347,7 +347,9 @@ bool Group::init(const GroupSpec& in, std::string* err) {
       all_dev = all_dev && v == "1";
     }
   }
-  const bool want_rccl = spec_.backend == "rccl" || (spec_.backend == "auto" && all_dev);
+  // a group of one has no peers: "auto" skips the communicator (and RCCL's proxy
+  // thread) and the collectives stay local
+  const bool want_rccl = spec_.backend == "rccl" || (spec_.backend == "auto" && all_dev && n > 1);
   if (want_rccl) {
     if (!all_dev) {
       if (err) *err = "backend=rccl needs a GPU (device >= 0) on every member";
