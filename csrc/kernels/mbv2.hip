@@ -15,6 +15,8 @@
 //  * avgpool   global average pool [B,HW,C] -> [B,C].
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <cstdint>
 
@@ -276,18 +278,22 @@ __global__ void __launch_bounds__(256) pw_gemm_lds_kernel(const uint16_t* __rest
 }
 
 // -------------------------------------------------------------------- dw3x3 ----
+// I = int for every tensor below 2^31 lanes of work: 64-bit div/mod is a
+// ~40-instruction VALU sequence per op on CDNA (no integer divider), and the
+// index split below needs three of them per output.
+template <typename I>
 __global__ void __launch_bounds__(256) dw3x3_kernel(const uint16_t* __restrict__ x,  // [B][H][W][C]
                                                     const uint16_t* __restrict__ w,  // [9][C]
                                                     const float* __restrict__ bias,  // [C]
                                                     uint16_t* __restrict__ y,        // [B][Ho][Wo][C]
                                                     int B, int H, int W, int C, int Ho, int Wo, int stride,
                                                     int dil, int act) {
-  const int cg = C >> 3;
-  const int64_t total = static_cast<int64_t>(B) * Ho * Wo * cg;
-  for (int64_t t = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; t < total;
-       t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+  const I cg = C >> 3;
+  const I total = static_cast<I>(B) * Ho * Wo * cg;
+  for (I t = blockIdx.x * static_cast<I>(blockDim.x) + threadIdx.x; t < total;
+       t += static_cast<I>(gridDim.x) * blockDim.x) {
     const int c8 = static_cast<int>(t % cg);
-    int64_t p = t / cg;
+    I p = t / cg;
     const int ox = static_cast<int>(p % Wo);
     p /= Wo;
     const int oy = static_cast<int>(p % Ho);
@@ -492,7 +498,11 @@ void pw_gemm(const void* x, const void* wt, const float* bias, const void* res, 
     const auto* wp = static_cast<const uint16_t*>(wt);
     const auto* rp = static_cast<const uint16_t*>(res);
     const int big = ((M + 127) / 128) * ((N + 127) / 128);
-    if (big >= 256) {
+    static const int big_min = [] {
+      const char* e = std::getenv("NNSX_GEMM_BIG_MIN");
+      return e ? std::atoi(e) : 256;
+    }();
+    if (big >= big_min) {
       const dim3 g((M + 127) / 128, (N + 127) / 128);
       if (out_f32)
         hipLaunchKernelGGL((pw_gemm_lds_kernel<128, 128, true>), g, dim3(256), 0, s, xp, wp, bias, rp, y, M, N, K, Kpad,
@@ -541,7 +551,8 @@ void dw3x3(const void* x, const void* w, const float* bias, void* y, int B, int 
   // padding == dilation keeps "same" geometry: Ho = (H - 1) / stride + 1
   int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
   int64_t work = static_cast<int64_t>(B) * Ho * Wo * (C / 8);
-  hipLaunchKernelGGL(dw3x3_kernel, dim3(grid_cap(work)), dim3(256), 0, s, static_cast<const uint16_t*>(x),
+  auto k = work + static_cast<int64_t>(grid_cap(work)) * 256 < (int64_t(1) << 31) ? dw3x3_kernel<uint32_t> : dw3x3_kernel<int64_t>;
+  hipLaunchKernelGGL(k, dim3(grid_cap(work)), dim3(256), 0, s, static_cast<const uint16_t*>(x),
                      static_cast<const uint16_t*>(w), bias, static_cast<uint16_t*>(y), B, H, W, C, Ho, Wo, stride, dil, act);
 }
 

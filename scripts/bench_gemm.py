@@ -38,3 +38,13 @@ for M, K, N, act in SHAPES:
     flops = 2.0 * M * K * N
     print(f"M={M:6d} K={K:4d} N={N:4d}: nnsx {t_nnsx:7.1f}us ({flops / t_nnsx / 1e6:6.1f} TF/s)   "
           f"hipBLASLt matmul {t_blas:7.1f}us ({flops / t_blas / 1e6:6.1f} TF/s)", flush=True)
+
+
+DW = [(B, 112, 112, 96, 2), (B, 56, 56, 144, 1), (B, 14, 14, 576, 1), (B, 7, 7, 960, 1)]
+for b, h, w_, c, st in DW:
+    x = torch.randn(b, h, w_, c, device="cuda").to(torch.bfloat16)
+    wd = (torch.randn(9, c, device="cuda") * 0.1).to(torch.bfloat16)
+    bd = torch.zeros(c, device="cuda")
+    t = timeit(lambda: torch.ops.nnsx.dw_conv(x, wd, bd, st, 1))
+    nbytes = x.numel() * 2 * (1 + 1 / (st * st))
+    print(f"dw3x3 {b}x{h}x{w_}x{c} s{st}: {t:7.1f}us ({nbytes / t / 1e6:6.2f} TB/s)", flush=True)
