@@ -5,45 +5,63 @@ one pipeline per GPU (weak scaling: per-GPU work fixed as N grows).
 
     python bench.py --gpus N --steps K --warmup W
 
+`--gpus N` without a launcher: this process spawns N rank processes itself
+(RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set, one GPU each) BEFORE anything here
+touches the GPU, waits for them and exits with the first failure's code.
+Under torch.distributed.run the ranks come from the environment and
+WORLD_SIZE must equal N.
+
 Pipeline (one per rank, pinned to GPU LOCAL_RANK):
 
   videotestsrc pattern=snow ! video/x-raw,format=RGB,width=224,height=224
     ! tensor_converter frames-per-tensor=B device=<gpu>     # H2D into HBM, B frames per tensor
-    ! tensor_transform mode=arithmetic option=typecast:float32,add:-127.5,div:127.5   # HIP kernel
+    ! tensor_transform mode=arithmetic option=typecast:float32,add:-127.5,div:127.5   # fused into the stem
     ! tensor_filter framework=pytorch model=mbv2.pt accelerator=true:gpu custom=hipgraph:true
     ! tensor_decoder mode=image_labeling option1=labels.txt # HIP argmax, labels D2H
     ! tensor_sink
 
+Precision: the reference runs the model in float32 (tensor_filter_pytorch.cc
+:517-536), so the headline `value` is the fp32 engine (fp32 activations,
+weights and accumulation: v_mfma_f32_16x16x4_f32 GEMMs, fp32 depthwise).
+The bf16 engine is measured after it and reported as `value_bf16`.
+
 A "step" is one batch of B frames reaching the sink.  W batches warm up
 (graph capture, allocator), then the wall time of exactly K batches is
 measured at the sink; ranks are bracketed by barrier + device synchronize,
-the max over ranks is reported.  Latency = sink arrival - frame capture time
-(the PTS of the oldest frame in the batch).  Data: synthetic video frames,
-random-init weights.
+the max over ranks is reported.  Cross-check: the filter's HIP events give
+the device-clock time of the same K batches (`gpu_event_fps`).  Latency =
+sink arrival - frame capture time (the PTS of the oldest frame in the batch);
+`p50_latency_ms_b1` is a separate batch-1 run of the same pipeline.
+Data: synthetic video frames, random-init weights.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import tempfile
 import time
-
-import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 
-def parse_args():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=int(os.environ.get("NNSX_BENCH_BATCH", "128")))
-    ap.add_argument("--model", default=os.environ.get("NNSX_BENCH_MODEL", "mobilenet_v2_fused"),
-                    help="mobilenet_v2 (plain torch) | mobilenet_v2_fused (nnsx CDNA4 kernels)")
+    ap.add_argument("--precision", default=os.environ.get("NNSX_BENCH_PRECISION", "both"),
+                    choices=["fp32", "bf16", "both"],
+                    help="fp32 = reference precision (headline); bf16 = secondary; both = fp32 headline + bf16")
+    ap.add_argument("--engine", default=os.environ.get("NNSX_BENCH_ENGINE", "fused"), choices=["fused", "torch"],
+                    help="fused = nnsx CDNA4 kernels; torch = plain TorchScript/MIOpen model (fp32)")
+    ap.add_argument("--latency-frames", type=int, default=int(os.environ.get("NNSX_BENCH_LAT_FRAMES", "300")),
+                    help="frames of the batch-1 latency run (0 = skip)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-fuse-norm", action="store_true",
                     help="keep the normalisation as a separate tensor_transform element")
@@ -53,7 +71,7 @@ def parse_args():
                     help="posenet_multi: tensor_allgather data plane")
     ap.add_argument("--config", default=os.environ.get("NNSX_BENCH_CONFIG", "mbv2"),
                     choices=sorted(CONFIGS), help="BASELINE.json config (default: the headline MobileNetV2 pipeline)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 # best CPU reference path for the MobileNetV2 pipeline
@@ -98,51 +116,50 @@ CONFIGS = {
 }
 
 
-def main():
-    a = parse_args()
-    import torch
+# ----------------------------------------------------------------- launcher ----
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
 
-        backend = "nccl" if (torch.cuda.is_available() and not a.cpu) else "gloo"
-        if backend == "nccl":
-            torch.cuda.set_device(local_rank)
-        dist.init_process_group(backend=backend)
+def spawn_ranks(n: int, argv) -> int:
+    """Start n rank processes of this script (one per GPU) and wait for them.
 
-    import nnstreamer_amd as nns
-    from nnstreamer_amd.models.export import export, write_labels
+    Runs before anything in this process touches the GPU (no torch.cuda call,
+    no HIP runtime), and starts children instead of exec'ing.  Every rank
+    reads its GPU from LOCAL_RANK; rank 0 prints the JSON line."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), NNSX_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    alive = set(range(n))
+    while alive:
+        for r in sorted(alive):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            alive.discard(r)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print(f"bench: rank {r} exited with {code}; stopping the other ranks", file=sys.stderr, flush=True)
+                for q in alive:
+                    procs[q].terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
 
-    use_gpu = (not a.cpu) and torch.cuda.is_available() and nns.gpu_count() > 0
-    dev = local_rank if use_gpu else -1
-    numa = "off"
-    if use_gpu and os.environ.get("NNSX_BENCH_NUMA", "1") != "0":
-        # each rank's streaming threads and its pinned frame ring on the GPU's own
-        # NUMA node: with 8 ranks the host-to-device uploads never cross sockets
-        numa = nns.bind_numa(dev)
-        print(f"rank {rank}: GPU {dev} NUMA binding: {numa}", file=sys.stderr, flush=True)
-    workdir = os.path.join(tempfile.gettempdir(), f"nnsx_bench_{os.getuid()}_{rank}")
-    os.makedirs(workdir, exist_ok=True)
-    cfg = CONFIGS[a.config]
-    model_name = a.model if a.config == "mbv2" else cfg["model"]
-    model_path = os.path.join(workdir, f"{model_name}.pt")
-    layout = "nhwc"
-    export(model_name, model_path, layout=layout)
-    from nnstreamer_amd.models.posenet import write_pose_labels
-    from nnstreamer_amd.models.ssd import write_box_priors, write_coco_labels
 
-    files = dict(labels=write_labels(os.path.join(workdir, "labels.txt")),
-                 coco=write_coco_labels(os.path.join(workdir, "coco.txt")),
-                 priors=write_box_priors(os.path.join(workdir, "priors.txt")),
-                 pose=write_pose_labels(os.path.join(workdir, "pose17.txt")))
+# ---------------------------------------------------------------- one run ----
+def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, rank, world, dev, use_gpu, dist):
+    """Build and run one pipeline to EOS; return this rank's timing record."""
     S = cfg["size"]
-
-    B = a.batch
-    total = a.warmup + a.steps
+    total = warmup + steps
     frames = total * B
     graph = "true" if (use_gpu and not a.no_graph) else "false"
     # fused models take the raw uint8 frame and apply the tensor_transform normalisation
@@ -154,6 +171,10 @@ def main():
     # cache, so every batch's H2D upload really crosses the host link.
     frame_bytes = S * S * 3
     pool = max(64, -(-512 * 2**20 // frame_bytes)) if use_gpu else 16
+    pool = min(pool, max(frames, 16))
+    filt = (f"tensor_filter name=filt framework=pytorch model={model_path} input=3:{S}:{S}:{B} "
+            f"inputtype={'uint8' if fuse_norm else 'float32'} accelerator={accel} device={dev} "
+            f"custom=hipgraph:{graph} device-stats={'true' if use_gpu else 'false'} ")
     desc = (
         f"videotestsrc num-buffers={frames} pattern=snow pool-size={pool} "
         f"! video/x-raw,format=RGB,width={S},height={S},framerate=0/1 "
@@ -162,9 +183,7 @@ def main():
         # is still submitting this batch's kernels
         f"! queue max-size-buffers=2 "
         + (f"! tensor_transform mode=arithmetic option={cfg['norm']} " if not fuse_norm else "")
-        + f"! tensor_filter framework=pytorch model={model_path} input=3:{S}:{S}:{B} "
-        f"inputtype={'uint8' if fuse_norm else 'float32'} "
-        f"accelerator={accel} device={dev} custom=hipgraph:{graph} "
+        + f"! {filt}"
         + (f"! tee name=t t. ! queue max-size-buffers={a.queue} " if cfg.get("gather") else
            f"! queue max-size-buffers={a.queue} ")
         + f"! {cfg['decoder'].format(**files)} "
@@ -185,20 +204,20 @@ def main():
                     f"! tensor_converter frames-per-tensor={B} device={dev} ! queue max-size-buffers=4 "
                     f"! edgesink {link}")
         else:
-            desc = (f"edgesrc {link} peer-rank=0 ! queue max-size-buffers=2 "
-                    f"! tensor_filter framework=pytorch model={model_path} input=3:{S}:{S}:{B} "
-                    f"inputtype={'uint8' if fuse_norm else 'float32'} accelerator={accel} device={dev} "
-                    f"custom=hipgraph:{graph} ! queue max-size-buffers={a.queue} "
-                    f"! {cfg['decoder'].format(**files)} ! tensor_sink name=sink")
+            desc = (f"edgesrc {link} peer-rank=0 ! queue max-size-buffers=2 ! {filt}"
+                    f"! queue max-size-buffers={a.queue} ! {cfg['decoder'].format(**files)} ! tensor_sink name=sink")
     per_step = B if cfg["per_frame"] else 1  # sink buffers per batch
     pipe = nns.parse_launch(desc)
     sink = pipe.get_by_name("sink")
+    filt_el = pipe.get_by_name("filt")
     # native per-buffer arrival stats (no Python callback per frame); sync-device
     # makes an arrival mean "the GPU has produced this frame", not "it was queued"
     if sink is not None:  # (the fan-out camera rank has no sink: it only produces)
         sink.set_property("emit-signal", "false")
         sink.set_property("sync-device", "true")
         sink.set_property("stats-every", "1")
+
+    import torch
 
     if dist is not None:
         dist.barrier()
@@ -212,66 +231,202 @@ def main():
     if dist is not None:
         dist.barrier()
     gathered = pipe.get_by_name("ag").get_property("comm-bytes") if cfg.get("gather") else None
+    dev_stamps = filt_el.get_property("device-stamps") if (filt_el is not None and use_gpu) else ""
     pipe.stop()
 
-    recs = [tuple(int(v) for v in e.split(":")) for e in sink.get_property("stats").split(",") if e] if sink else []
+    import numpy as np
+
+    rec = dict(elapsed=0.0, p50=0.0, p99=0.0, gpu_elapsed=0.0, gpu_busy_ms=0.0, wall=t_end - t_start,
+               desc=desc, fan=fan, workers=workers, fuse_norm=fuse_norm, gathered=gathered)
+    if sink is None:
+        return rec  # the workers' clocks decide
+    recs = [tuple(int(v) for v in e.split(":")) for e in sink.get_property("stats").split(",") if e]
     arrivals = [t / 1e9 for i, (t, _) in enumerate(recs) if (i + 1) % per_step == 0]  # last frame of each batch
     step_lat = [[lat / 1e6 for _, lat in recs[k * per_step:(k + 1) * per_step] if lat >= 0]
                 for k in range(len(arrivals))]
-    n = len(arrivals)
-    if sink is None:
-        stats = torch.zeros(3, dtype=torch.float64)  # the workers' clocks decide
+    if len(arrivals) < total:
+        raise SystemExit(f"rank {rank}: only {len(arrivals)}/{total} batches reached the sink")
+    # timed region: exactly K steps after W warmup steps
+    t0 = arrivals[warmup - 1] if warmup > 0 else t_start
+    t1 = arrivals[warmup + steps - 1]
+    rec["elapsed"] = t1 - t0
+    timed = [x for k in range(warmup, warmup + steps) for x in step_lat[k]]
+    lat = np.array(timed) if (timed and not fan) else np.array([0.0])
+    rec["p50"] = float(np.percentile(lat, 50))
+    rec["p99"] = float(np.percentile(lat, 99))
+    # device-clock cross-check: the filter's end-of-invoke events of the same K batches
+    ds = [tuple(int(v) for v in e.split(":")) for e in dev_stamps.split(",") if e]
+    if len(ds) >= total and warmup > 0:
+        rec["gpu_elapsed"] = (ds[warmup + steps - 1][0] - ds[warmup - 1][0]) / 1e9
+        rec["gpu_busy_ms"] = float(np.median([d[1] for d in ds[warmup:warmup + steps]])) / 1e6
+    return rec
+
+
+def main():
+    a = parse_args()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        # launcher mode: N fresh rank processes, nothing here touches the GPU
+        sys.exit(spawn_ranks(a.gpus, sys.argv[1:]))
+
+    import numpy as np
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"bench: --gpus {a.gpus} but WORLD_SIZE={world}: refusing to report a mismatched run")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        backend = "nccl" if (torch.cuda.is_available() and not a.cpu) else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local_rank)
+        dist.init_process_group(backend=backend)
+        if dist.get_world_size() != a.gpus:
+            raise SystemExit(f"bench: process group has {dist.get_world_size()} ranks, expected {a.gpus}")
+
+    import nnstreamer_amd as nns
+    from nnstreamer_amd.models.export import export, write_labels
+
+    use_gpu = (not a.cpu) and torch.cuda.is_available() and nns.gpu_count() > 0
+    if use_gpu and world > nns.gpu_count():
+        raise SystemExit(f"bench: {world} ranks but only {nns.gpu_count()} GPUs visible")
+    dev = local_rank if use_gpu else -1
+    numa = "off"
+    if use_gpu and os.environ.get("NNSX_BENCH_NUMA", "1") != "0":
+        # each rank's streaming threads and its pinned frame ring on the GPU's own
+        # NUMA node: with 8 ranks the host-to-device uploads never cross sockets
+        numa = nns.bind_numa(dev)
+        print(f"rank {rank}: GPU {dev} NUMA binding: {numa}", file=sys.stderr, flush=True)
+    workdir = os.path.join(tempfile.gettempdir(), f"nnsx_bench_{os.getuid()}_{rank}")
+    os.makedirs(workdir, exist_ok=True)
+    cfg = CONFIGS[a.config]
+    from nnstreamer_amd.models.posenet import write_pose_labels
+    from nnstreamer_amd.models.ssd import write_box_priors, write_coco_labels
+
+    files = dict(labels=write_labels(os.path.join(workdir, "labels.txt")),
+                 coco=write_coco_labels(os.path.join(workdir, "coco.txt")),
+                 priors=write_box_priors(os.path.join(workdir, "priors.txt")),
+                 pose=write_pose_labels(os.path.join(workdir, "pose17.txt")))
+
+    # which engines to run: (label, model name, dtype)
+    base = cfg["model"]
+    if a.engine == "torch" or not use_gpu:
+        plain = base.replace("_fused", "")
+        runs = [("fp32", plain, "fp32")]
     else:
-        if n < total:
-            raise SystemExit(f"rank {rank}: only {n}/{total} batches reached the sink")
-        # timed region: exactly K steps after W warmup steps
-        t0 = arrivals[a.warmup - 1] if a.warmup > 0 else t_start
-        t1 = arrivals[a.warmup + a.steps - 1]
-        elapsed = t1 - t0
-        timed = [x for k in range(a.warmup, a.warmup + a.steps) for x in step_lat[k]]
-        lat = np.array(timed) if timed else np.array([0.0])
-        if fan:  # PTS were stamped on the camera rank's clock: no per-frame latency here
-            lat = np.array([0.0])
-        stats = torch.tensor([elapsed, float(np.percentile(lat, 50)), float(np.percentile(lat, 99))],
-                             dtype=torch.float64)
+        runs = []
+        if a.precision in ("fp32", "both"):
+            runs.append(("fp32", base + "_fp32", "fp32"))
+        if a.precision in ("bf16", "both"):
+            runs.append(("bf16", base, "bf16"))
+
+    results = {}
+    for label, model_name, dtype in runs:
+        model_path = os.path.join(workdir, f"{model_name}.pt")
+        export(model_name, model_path, layout="nhwc")
+        rec = run_pipeline(a, nns, cfg, model_name, model_path, files, a.batch, a.steps, a.warmup, rank, world, dev,
+                           use_gpu, dist)
+        rec["dtype"] = dtype
+        results[label] = rec
+
+    # batch-1 latency of the headline engine (the "p50 per-frame latency" half of the metric)
+    lat_b1 = None
+    if a.latency_frames > 0 and a.config == "mbv2" and not cfg.get("fan"):
+        label, model_name, _ = runs[0]
+        model_path = os.path.join(workdir, f"{model_name}.pt")
+        w1 = max(10, a.latency_frames // 5)
+        lat_b1 = run_pipeline(a, nns, cfg, model_name, model_path, files, 1, a.latency_frames, w1, rank, world, dev,
+                              use_gpu, dist)
+
+    # per-rank records, all-gathered over the job's process group (RCCL on GPUs):
+    # [elapsed, p50, p99, gpu_elapsed, gpu_busy] per engine + batch-1 p50/p99
+    vec = []
+    for label, _, _ in runs:
+        r = results[label]
+        vec += [r["elapsed"], r["p50"], r["p99"], r["gpu_elapsed"], r["gpu_busy_ms"]]
+    vec += [lat_b1["p50"], lat_b1["p99"]] if lat_b1 else [0.0, 0.0]
+    stats = torch.tensor(vec, dtype=torch.float64)
     if dist is not None:
         if dist.get_backend() == "nccl":
             stats = stats.cuda()
-        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
-        stats = stats.cpu()
-    elapsed, p50, p99 = stats.tolist()
-    ms_per_step = elapsed / a.steps * 1e3
-    fps_total = workers * a.steps * B / elapsed
+        gathered = [torch.zeros_like(stats) for _ in range(world)]
+        dist.all_gather(gathered, stats)
+        per_rank = torch.stack([g.cpu() for g in gathered])  # [world, len]
+        pg_world, pg_backend = len(gathered), ("rccl" if dist.get_backend() == "nccl" else dist.get_backend())
+    else:
+        per_rank = stats.view(1, -1)
+        pg_world, pg_backend = 1, None
     if rank == 0:
+        head_label = runs[0][0]
+        head = results[head_label]
+        workers = head["workers"]
+        fan = head["fan"]
+        B = a.batch
+
+        def agg(i):
+            cols = per_rank[:, i * 5:(i + 1) * 5]
+            active = cols[1:] if fan else cols  # the fan-out camera rank has no sink
+            elapsed = float(active[:, 0].max())
+            gpu_el = float(active[:, 3].max())
+            per = [round(a.steps * B / float(e), 2) if e > 0 else None for e in active[:, 0].tolist()]
+            return dict(
+                fps=workers * a.steps * B / elapsed if elapsed > 0 else 0.0,
+                ms=elapsed / a.steps * 1e3,
+                p50=float(active[:, 1].max()), p99=float(active[:, 2].max()),
+                gpu_fps=(workers * a.steps * B / gpu_el) if gpu_el > 0 else None,
+                gpu_busy=float(active[:, 4].max()), per_rank=per)
+
+        h = agg(0)
         out = {
             "metric": cfg["metric"],
-            "value": round(fps_total, 2),
+            "value": round(h["fps"], 2),
             "unit": "frames/s",
             "n_gpus": world if use_gpu else 0,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": round(ms_per_step, 4),
+            "ms_per_step": round(h["ms"], 4),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": (round(fps_total / CPU_BASELINE_FPS, 2) if a.config == "mbv2" else None),
-            "dtype": "bf16" if "fused" in a.model else "fp32",
+            "vs_baseline": (round(h["fps"] / CPU_BASELINE_FPS, 2) if a.config == "mbv2" else None),
+            "dtype": head["dtype"],
             "data": "synthetic video frames (videotestsrc pattern=snow), random-init weights",
-            "p50_latency_ms": None if fan else round(p50, 3),
-            "p99_latency_ms": None if fan else round(p99, 3),
+            "p50_latency_ms": None if fan else round(h["p50"], 3),
+            "p99_latency_ms": None if fan else round(h["p99"], 3),
+            "gpu_event_fps": round(h["gpu_fps"], 2) if h["gpu_fps"] else None,
+            "gpu_invoke_ms_median": round(h["gpu_busy"], 4),
+            "per_rank_fps": h["per_rank"],
+            # the per-rank records above travelled through one all_gather on this process group
+            "pg_world": pg_world,
+            "pg_backend": pg_backend,
             "frames_per_step_per_gpu": B,
+        }
+        if "bf16" in results and head_label != "bf16":
+            b = agg(1)
+            out.update(value_bf16=round(b["fps"], 2), ms_per_step_bf16=round(b["ms"], 4),
+                       p50_latency_ms_bf16=None if fan else round(b["p50"], 3),
+                       gpu_event_fps_bf16=round(b["gpu_fps"], 2) if b["gpu_fps"] else None,
+                       per_rank_fps_bf16=b["per_rank"])
+        if lat_b1:
+            n = len(runs)
+            out.update(p50_latency_ms_b1=round(float(per_rank[:, n * 5].max()), 3),
+                       p99_latency_ms_b1=round(float(per_rank[:, n * 5 + 1].max()), 3))
+        out.update({
             "preprocess": ("tensor_transform normalisation fused into the model's stem kernel (uint8 input)"
-                           if fuse_norm else "tensor_transform element"),
-            "wall_s": round(t_end - t_start, 3),
+                           if head["fuse_norm"] else "tensor_transform element"),
+            "wall_s": round(sum(r["wall"] for r in results.values()), 3),
             "numa_binding": numa,
-            **({"allgather_bytes_sent_received_rank0": gathered} if gathered is not None else {}),
+            **({"allgather_bytes_sent_received_rank0": head["gathered"]} if head["gathered"] is not None else {}),
             "config": {
                 "model": cfg["desc"],
                 "global_batch": B * world,
                 "seq_len": 1,
                 "parallelism": f"fan-out 1->{workers} (RCCL scatter)" if fan else f"branch-dp{world}",
-                "pipeline": desc,
+                "pipeline": head["desc"],
             },
-        }
+        })
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -115,10 +115,22 @@ class TensorFilter : public BaseTransform {
     prop_bool("latency-report", &latency_report_, "Report the latency of tensor filter to the pipeline bus (LATENCY message)");
     prop_int("invoke-dynamic", &props_.invoke_dynamic, "Flexible tensors whose shape can change per invoke (output caps become flexible)");
     prop_int("device", &device_prop_, "nnsx: GPU index for GPU frameworks (-2 = follow input placement, else LOCAL_RANK or 0)");
+    prop_bool("device-stats", &device_stamps_,
+              "nnsx: log every GPU invoke's device time (HIP events); read back with device-stamps");
+    prop_readonly("device-stamps", [this] {
+      poll_device_stats(true);
+      std::lock_guard<std::mutex> lk(stat_mu_);
+      std::string r;
+      for (auto& e : dev_log_) r += std::to_string(e.first) + ":" + std::to_string(e.second) + ",";
+      return r;
+    }, "nnsx: per-invoke 'end_ns:latency_ns' on the device clock (relative to the first invoke), comma separated");
     prop_string("config-file", &config_file_, "Path to a key=value file setting any of the properties", [this] { load_config_file(); });
   }
 
-  ~TensorFilter() override { close_fw(); }
+  ~TensorFilter() override {
+    release_timing_events();
+    close_fw();
+  }
 
  protected:
   // ------------------------------------------------------------ properties ----
@@ -378,7 +390,14 @@ class TensorFilter : public BaseTransform {
     return true;
   }
 
-  int64_t own_latency() const override { return latency_mode_ > 0 ? avg_latency_us() * 1000 : 0; }
+  int64_t own_latency() const override {
+    if (latency_mode_ <= 0) return 0;
+    std::lock_guard<std::mutex> lk(stat_mu_);
+    if (lat_.empty()) return 0;
+    int64_t s = 0;
+    for (auto v : lat_) s += v;
+    return s / static_cast<int64_t>(lat_.size());
+  }
 
   // ---------------------------------------------------------------- transform ----
   FlowReturn transform(const BufferPtr& inbuf, BufferPtr* outbuf) override {
@@ -428,17 +447,26 @@ class TensorFilter : public BaseTransform {
     std::vector<MemoryPtr> outs;
     int64_t t0 = now_ns();
     int ret;
+    // GPU invokes are asynchronous: statistics come from HIP events around
+    // the invoke on the element's stream (device time), not host enqueue time
+    const bool dev_timing = ctx.device >= 0 && ctx.stream && stats_enabled();
+    DevStamp ds;
     {
       hip::DeviceGuard g(ctx.device);
+      if (dev_timing) {
+        poll_device_stats(false);
+        ds = dev_stamp_begin(ctx.device, ctx.stream);
+      }
       if (shared_) {
         std::lock_guard<std::mutex> lk(shared_->invoke_mu);
         ret = inst_->invoke(model_in, &outs, ctx);
       } else {
         ret = inst_->invoke(model_in, &outs, ctx);
       }
+      if (dev_timing) dev_stamp_end(&ds, ctx.stream, ret);
     }
     int64_t t1 = now_ns();
-    record_stats(t1 - t0, t1);
+    if (!dev_timing) record_stats(t1 - t0, t1);
     if (ret > 0) return FlowReturn::CUSTOM_SUCCESS;  // drop this frame (tensor_filter.c:811-813)
     if (ret < 0) {
       post_error(strfmt("tensor_filter: invoke failed (", ret, ")"));
@@ -478,9 +506,93 @@ class TensorFilter : public BaseTransform {
   }
 
   // ---------------------------------------------------------------- stats ----
-  void record_stats(int64_t dur_ns, int64_t now) {
-    if (latency_mode_ <= 0 && throughput_mode_ <= 0 && !latency_report_) return;
+  // Reference: tensor_filter.c:354-495 (latency = invoke duration, throughput
+  // from the invoke timestamps).  On a GPU the invoke only enqueues work, so a
+  // pair of timing events brackets it on the element's stream: latency = the
+  // device time between them, the "timestamp" of an invoke = its end event on
+  // the device clock (relative to the first event this element recorded).
+  struct DevStamp {
+    hipEvent_t beg = nullptr, end = nullptr;
+    int dev = -1;
+  };
+  bool stats_enabled() const { return latency_mode_ > 0 || throughput_mode_ > 0 || latency_report_ || device_stamps_; }
+
+  hipEvent_t timing_event(int dev) {
     std::lock_guard<std::mutex> lk(stat_mu_);
+    if (!ev_free_.empty()) {
+      hipEvent_t e = ev_free_.back();
+      ev_free_.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    hip::check(hipEventCreate(&e), "hipEventCreate(timing)");
+    ev_all_.emplace_back(dev, e);
+    return e;
+  }
+
+  DevStamp dev_stamp_begin(int dev, hipStream_t s) {
+    DevStamp d;
+    d.dev = dev;
+    d.beg = timing_event(dev);
+    d.end = timing_event(dev);
+    hip::check(hipEventRecord(d.beg, s), "hipEventRecord(invoke begin)");
+    std::lock_guard<std::mutex> lk(stat_mu_);
+    if (!ev_base_) {
+      ev_base_ = d.beg;
+      ev_base_dev_ = dev;
+    }
+    return d;
+  }
+
+  void dev_stamp_end(DevStamp* d, hipStream_t s, int ret) {
+    if (ret != 0) {  // dropped / failed invoke: nothing to time
+      hip::check(hipEventSynchronize(d->beg), "sync timing event");
+      std::lock_guard<std::mutex> lk(stat_mu_);
+      if (d->beg != ev_base_) ev_free_.push_back(d->beg);
+      ev_free_.push_back(d->end);
+      return;
+    }
+    hip::check(hipEventRecord(d->end, s), "hipEventRecord(invoke end)");
+    std::lock_guard<std::mutex> lk(stat_mu_);
+    pending_.push_back(*d);
+    // bound the number of outstanding timing pairs (the stream is far ahead)
+    if (pending_.size() > 4096) drain_locked(true);
+  }
+
+  // fold completed timing pairs into the statistics; wait = block on all
+  void drain_locked(bool wait) {
+    while (!pending_.empty()) {
+      DevStamp d = pending_.front();
+      if (wait) {
+        hip::DeviceGuard g(d.dev);
+        if (hipEventSynchronize(d.end) != hipSuccess) break;
+      } else if (hipEventQuery(d.end) != hipSuccess) {
+        break;
+      }
+      pending_.pop_front();
+      float lat_ms = 0.f, at_ms = 0.f;
+      (void)hipEventElapsedTime(&lat_ms, d.beg, d.end);
+      if (ev_base_ && ev_base_dev_ == d.dev) (void)hipEventElapsedTime(&at_ms, ev_base_, d.end);
+      const int64_t dur = static_cast<int64_t>(static_cast<double>(lat_ms) * 1e6);
+      const int64_t at = static_cast<int64_t>(static_cast<double>(at_ms) * 1e6);
+      if (device_stamps_) dev_log_.emplace_back(at, dur);
+      add_sample_locked(dur, at);
+      if (d.beg != ev_base_) ev_free_.push_back(d.beg);
+      ev_free_.push_back(d.end);
+    }
+  }
+  void poll_device_stats(bool wait) {
+    std::lock_guard<std::mutex> lk(stat_mu_);
+    drain_locked(wait);
+  }
+
+  void record_stats(int64_t dur_ns, int64_t now) {
+    if (!stats_enabled()) return;
+    std::lock_guard<std::mutex> lk(stat_mu_);
+    add_sample_locked(dur_ns, now);
+  }
+
+  void add_sample_locked(int64_t dur_ns, int64_t now) {
     ++total_invoke_;
     if (total_invoke_ <= kWarmup) return;  // ignore warm-up samples
     lat_.push_back(dur_ns);
@@ -500,7 +612,8 @@ class TensorFilter : public BaseTransform {
     }
   }
 
-  int64_t avg_latency_us() const {
+  int64_t avg_latency_us() {
+    poll_device_stats(false);
     std::lock_guard<std::mutex> lk(stat_mu_);
     if (lat_.empty()) return 0;
     int64_t s = 0;
@@ -508,7 +621,8 @@ class TensorFilter : public BaseTransform {
     return s / static_cast<int64_t>(lat_.size()) / 1000;
   }
 
-  int64_t throughput_milli_fps() const {
+  int64_t throughput_milli_fps() {
+    poll_device_stats(false);
     std::lock_guard<std::mutex> lk(stat_mu_);
     if (stamps_.size() < 2) return 0;
     int64_t span = stamps_.back() - stamps_.front();
@@ -523,11 +637,26 @@ class TensorFilter : public BaseTransform {
       std::lock_guard<std::mutex> lk(stat_mu_);
       lat_.clear();
       stamps_.clear();
+      dev_log_.clear();
       total_invoke_ = 0;
     }
     return ensure_open();
   }
-  bool stop() override { return true; }
+  bool stop() override {
+    poll_device_stats(true);
+    return true;
+  }
+  void release_timing_events() {
+    std::lock_guard<std::mutex> lk(stat_mu_);
+    drain_locked(true);
+    for (auto& de : ev_all_) {
+      hip::DeviceGuard g(de.first);
+      (void)hipEventDestroy(de.second);
+    }
+    ev_all_.clear();
+    ev_free_.clear();
+    ev_base_ = nullptr;
+  }
   void close() override { close_fw(); }
 
  private:
@@ -552,6 +681,13 @@ class TensorFilter : public BaseTransform {
   mutable std::mutex stat_mu_;
   std::deque<int64_t> lat_, stamps_;
   int64_t total_invoke_ = 0, reported_ = 0;
+  bool device_stamps_ = false;
+  std::deque<DevStamp> pending_;
+  std::vector<hipEvent_t> ev_free_;
+  std::vector<std::pair<int, hipEvent_t>> ev_all_;
+  hipEvent_t ev_base_ = nullptr;
+  int ev_base_dev_ = -1;
+  std::vector<std::pair<int64_t, int64_t>> dev_log_;  // (end ns on the device clock, device latency ns)
   StreamSet streams_;
 };
 

@@ -47,5 +47,42 @@ bool ir_block_supported(int stride, int cin, int hid, int cout);
 // returns false (nothing launched) for unsupported shapes
 bool ir_block(const IrBlockArgs& a, hipStream_t s);
 
+// ---------------------------------------------------------------- fp32 ----
+// The reference-precision engine (mbv2_f32.hip): fp32 activations, weights
+// and accumulation, GEMMs on v_mfma_f32_16x16x4_f32.
+// y[M][N] = act(x[M][K] . wt[N][K]^T + bias) (+ res); wt zero-padded [Npad][Kpad]
+// (Kpad >= K, Kpad % 4 == 0), K % 4 == 0, N % 4 == 0.
+void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
+                 int Kpad, int Npad, int act, hipStream_t s);
+// depthwise 3x3, stride 1|2, dilation d (padding d); w [9][C], C % 4 == 0
+void dw3x3_f32(const float* x, const float* w, const float* bias, float* y, int B, int H, int W, int C, int stride,
+               int dil, int act, hipStream_t s);
+// 3x3/2 stem 3 -> 32, w [3][3][3][32]; fp32 output
+void stem3x3_f32(const float* x, const float* w, const float* bias, float* y, int B, int H, int W, int act,
+                 hipStream_t s);
+void stem3x3_u8_f32(const uint8_t* x, const float* w, const float* bias, float* y, int B, int H, int W, int act,
+                    float add, float div, hipStream_t s);
+void avgpool_f32(const float* x, float* y, int B, int HW, int C, hipStream_t s);
+
+// fused inverted residual, fp32.  we [hid][KIN] (KIN = ceil8(cin), zero
+// padded), wd [9][hid], wp [ceil16(cout)][hid] (rows zero padded); biases
+// [hid] / [hid] / [ceil16(cout)].
+struct IrBlockF32Args {
+  const float* x = nullptr;
+  float* y = nullptr;
+  const float* we = nullptr;
+  const float* be = nullptr;
+  const float* wd = nullptr;
+  const float* bd = nullptr;
+  const float* wp = nullptr;
+  const float* bp = nullptr;
+  int B = 0, H = 0, W = 0, cin = 0, hid = 0, cout = 0, stride = 1;
+  int has_expand = 1, residual = 0;
+  // derived by ir_block_f32()
+  int Ho = 0, Wo = 0, tiles_x = 0, tiles_y = 0;
+};
+bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout, bool has_expand);
+bool ir_block_f32(const IrBlockF32Args& a, hipStream_t s);
+
 }  // namespace kernels
 }  // namespace nnsx

@@ -1,0 +1,714 @@
+// fp32 MobileNet-family kernels for gfx950: the reference-precision engine.
+//
+// The reference runs MobileNetV2 through tensor_filter framework=pytorch on
+// float32 tensors (ext/nnstreamer/tensor_filter/tensor_filter_pytorch.cc
+// :517-536).  These kernels keep that precision end to end -- fp32
+// activations in HBM and LDS, fp32 weights, fp32 accumulation -- and put
+// every GEMM-shaped op on the matrix cores with v_mfma_f32_16x16x4_f32
+// (exact fp32 products, 64 FLOP/clk/SIMD on gfx950: the fp32 MFMA rate
+// equals the fp32 VALU rate, so the depthwise convs stay on the VALU).
+//
+// Operand convention (all MFMA kernels here): D[n][m] = A[n][k] . B[m][k]^T
+// with A = weights (rows = output channels), B = activations (rows =
+// pixels).  One lane (li = lane & 15, g = lane >> 4) loads a float4 of 4
+// consecutive k of each operand: MFMA j of the four consumes component j,
+// so lane-group g covers k = 16s + 4g + j -- a permutation of the 16 k of
+// step s applied to both operands, which a dot product does not see.
+// The 16x16 result puts 4 consecutive output channels (4g..4g+3) of one
+// pixel (li) in each lane: one float4 NHWC store.
+//
+// LDS images are "k4-major": [k/4][row][4] floats.  A fragment read (16
+// lanes of one g read 16 consecutive rows at one k-quad) is then 256
+// contiguous bytes: conflict-free ds_read_b128 for every lane group.
+//
+//  * pw_gemm_f32   1x1 conv / FC: LDS-staged 128x128 or 64x64 tiles,
+//                  32-k stages, double buffered; bias + act + residual
+//                  epilogue; split-K with fp32 atomics for small grids.
+//  * dw3x3_f32     depthwise 3x3 (stride 1/2, dilation d) + bias + act.
+//  * stem_f32      3x3/2 conv 3 -> 32 (uint8 frame normalised in-kernel, or
+//                  f32 frame) as 7 MFMA k-steps of 4 (27 taps + 1 zero).
+//  * avgpool_f32   global average pool.
+//  * ir_block_f32  the fused inverted residual (expand -> dw -> project),
+//                  hidden activation in LDS; see the comment at the kernel.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+
+#include "kernels/mbv2.h"
+
+namespace nnsx {
+namespace kernels {
+
+namespace {
+
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x4_t mfma4(float a, float b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+// one 16-k step: lane (li, g) holds k = 16s + 4g + j in component j of a and b
+__device__ __forceinline__ f32x4_t mfma_k16(f32x4_t a, f32x4_t b, f32x4_t c) {
+  c = mfma4(a[0], b[0], c);
+  c = mfma4(a[1], b[1], c);
+  c = mfma4(a[2], b[2], c);
+  return mfma4(a[3], b[3], c);
+}
+// an 8-k tail step: lane (li, g) holds k = 2g + j in component j
+__device__ __forceinline__ f32x4_t mfma_k8(f32x2_t a, f32x2_t b, f32x4_t c) {
+  c = mfma4(a[0], b[0], c);
+  return mfma4(a[1], b[1], c);
+}
+
+__device__ __forceinline__ float act_fn(float v, int act) {
+  if (act == 1) return fminf(fmaxf(v, 0.f), 6.f);  // ReLU6
+  if (act == 2) return fmaxf(v, 0.f);                // ReLU
+  return v;
+}
+__device__ __forceinline__ float relu6(float v) { return fminf(fmaxf(v, 0.f), 6.f); }
+__device__ __forceinline__ f32x4_t relu6x4(f32x4_t v) {
+  return f32x4_t{relu6(v[0]), relu6(v[1]), relu6(v[2]), relu6(v[3])};
+}
+
+// XCD-aware workgroup order: the dispatcher places consecutive workgroup ids
+// round-robin over the 8 XCDs (each with its own L2).  Renumber so that each
+// XCD walks a contiguous range of tiles: neighbouring tiles share halo rows
+// and the same image, and stay in one L2.
+__device__ __forceinline__ int xcd_remap(int bid, int n) {
+  if (n % 8) return bid;
+  return (bid % 8) * (n / 8) + bid / 8;
+}
+
+// ------------------------------------------------------------- pw_gemm_f32 ----
+constexpr int GKT = 32;       // k per LDS stage
+constexpr int GKQ = GKT / 4;  // k-quads per stage
+
+template <int BM, int BN>
+__global__ void __launch_bounds__(256) pw_gemm_f32_kernel(const float* __restrict__ x,    // [M][K]
+                                                          const float* __restrict__ wt,   // [Npad][Kpad]
+                                                          const float* __restrict__ bias, // [N]
+                                                          const float* __restrict__ res,  // [M][N] or null
+                                                          float* __restrict__ y,          // [M][N]
+                                                          int M, int N, int K, int Kpad, int Npad, int act,
+                                                          int kchunk) {  // k-stages of this grid.z slice
+  constexpr int RM = BM / 32, RN = BN / 32;  // 16-row fragments per wave (2 x 2 waves)
+  constexpr int VX = BM * GKQ / 256, VW = BN * GKQ / 256;
+  // k4-major images, row index XOR-swizzled with the k-quad (kq < 8): the
+  // staging writes (8 lanes = 8 k-quads of one row) then spread over the
+  // banks, and fragment reads stay conflict-free (16 rows of one 16-aligned
+  // block, permuted)
+  __shared__ __attribute__((aligned(16))) float xs[2][GKQ][BM][4];
+  __shared__ __attribute__((aligned(16))) float ws[2][GKQ][BN][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int li = lane & 15, g = lane >> 4;
+  const int nbx = gridDim.x, nby = gridDim.y;
+  const int flat = xcd_remap(blockIdx.y * nbx + blockIdx.x, nbx * nby);
+  const int m0 = (flat % nbx) * BM, n0 = (flat / nbx) * BN;
+  const f32x4_t zero = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int kbeg = blockIdx.z * kchunk * GKT;
+  const int kend = min(Kpad, kbeg + kchunk * GKT);
+  const int nk = (kend - kbeg + GKT - 1) / GKT;
+
+  f32x4_t px[VX], pw[VW];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      const int v = tid + i * 256, kq = v & 7, row = v >> 3;
+      const int m = m0 + row, k = k0 + kq * 4;
+      px[i] = (m < M && k < K) ? *reinterpret_cast<const f32x4_t*>(x + static_cast<int64_t>(m) * K + k) : zero;
+    }
+#pragma unroll
+    for (int i = 0; i < VW; ++i) {
+      const int v = tid + i * 256, kq = v & 7, row = v >> 3;
+      const int n = n0 + row, k = k0 + kq * 4;
+      pw[i] = (n < Npad && k < Kpad) ? *reinterpret_cast<const f32x4_t*>(wt + static_cast<int64_t>(n) * Kpad + k)
+                                     : zero;
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < VX; ++i) {
+      const int v = tid + i * 256, kq = v & 7, row = v >> 3;
+      *reinterpret_cast<f32x4_t*>(&xs[buf][kq][row ^ kq][0]) = px[i];
+    }
+#pragma unroll
+    for (int i = 0; i < VW; ++i) {
+      const int v = tid + i * 256, kq = v & 7, row = v >> 3;
+      *reinterpret_cast<f32x4_t*>(&ws[buf][kq][row ^ kq][0]) = pw[i];
+    }
+  };
+
+  f32x4_t acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = zero;
+
+  if (nk > 0) {
+    gload(kbeg);
+    lstore(0);
+    __syncthreads();
+  }
+  for (int ks = 0; ks < nk; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nk) gload(kbeg + (ks + 1) * GKT);  // in flight during this stage's MFMAs
+#pragma unroll
+    for (int s = 0; s < GKT / 16; ++s) {
+      const int kq = 4 * s + g;
+      f32x4_t a[RN], b[RM];
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+        a[j] = *reinterpret_cast<const f32x4_t*>(&ws[buf][kq][(wn * (BN / 2) + j * 16 + li) ^ kq][0]);
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+        b[i] = *reinterpret_cast<const f32x4_t*>(&xs[buf][kq][(wm * (BM / 2) + i * 16 + li) ^ kq][0]);
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) acc[i][j] = mfma_k16(a[j], b[i], acc[i][j]);
+    }
+    if (ks + 1 < nk) lstore(buf ^ 1);  // buf ^ 1 was last read before the previous barrier
+    __syncthreads();
+  }
+
+  // epilogue: lane owns channels n..n+3 of pixel m
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+    const int m = m0 + wm * (BM / 2) + i * 16 + li;
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const int n = n0 + wn * (BN / 2) + j * 16 + g * 4;
+      if (n >= N) continue;
+      float* yp = y + static_cast<int64_t>(m) * N + n;
+      if (gridDim.z > 1) {  // split-K partial sum (no residual / activation)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) atomicAdd(yp + r, acc[i][j][r] + (blockIdx.z == 0 ? bias[n + r] : 0.f));
+        continue;
+      }
+      f32x4_t v = acc[i][j] + *reinterpret_cast<const f32x4_t*>(bias + n);
+      if (res) v += *reinterpret_cast<const f32x4_t*>(res + static_cast<int64_t>(m) * N + n);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], act);
+      *reinterpret_cast<f32x4_t*>(yp) = v;
+    }
+  }
+}
+
+// --------------------------------------------------------------- dw3x3_f32 ----
+// one lane = one output pixel x 4 channels (float4 loads/stores)
+__global__ void __launch_bounds__(256) dw3x3_f32_kernel(const float* __restrict__ x,     // [B][H][W][C]
+                                                        const float* __restrict__ w,     // [9][C]
+                                                        const float* __restrict__ bias,  // [C]
+                                                        float* __restrict__ y,           // [B][Ho][Wo][C]
+                                                        int B, int H, int W, int C, int Ho, int Wo, int stride,
+                                                        int dil, int act) {
+  const uint32_t cg = static_cast<uint32_t>(C) >> 2;
+  const uint32_t total = static_cast<uint32_t>(B) * Ho * Wo * cg;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const int c = static_cast<int>(t % cg) * 4;
+    uint32_t p = t / cg;
+    const int ox = static_cast<int>(p % Wo);
+    p /= Wo;
+    const int oy = static_cast<int>(p % Ho);
+    const int b = static_cast<int>(p / Ho);
+    f32x4_t acc = *reinterpret_cast<const f32x4_t*>(bias + c);
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int iy = oy * stride - dil + ky * dil;
+      if (iy < 0 || iy >= H) continue;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int ix = ox * stride - dil + kx * dil;
+        if (ix < 0 || ix >= W) continue;
+        const f32x4_t xv = *reinterpret_cast<const f32x4_t*>(x + ((static_cast<int64_t>(b) * H + iy) * W + ix) * C + c);
+        const f32x4_t wv = *reinterpret_cast<const f32x4_t*>(w + (ky * 3 + kx) * C + c);
+        acc = __builtin_elementwise_fma(xv, wv, acc);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] = act_fn(acc[r], act);
+    *reinterpret_cast<f32x4_t*>(y + ((static_cast<int64_t>(b) * Ho + oy) * Wo + ox) * C + c) = acc;
+  }
+}
+
+// ---------------------------------------------------------------- stem_f32 ----
+// 3x3/2 conv 3 -> 32 as D[co][px] = W[co][k] . P[px][k]^T, k = (ky, kx, ci)
+// = 27 taps + 1 zero = 7 MFMA steps of 4 (step t: lane group g holds
+// k = 4t + g).  A workgroup owns STEM_R output rows of one image: the
+// 2 * STEM_R + 1 input rows are normalised once into LDS as fp32 (a zero
+// column each side = the conv padding); each lane gathers its 7 patch values
+// per 16-pixel tile from LDS.  T = uint8_t: raw RGB normalised as
+// (x + add) / div (the pipeline's tensor_transform arithmetic, exact fp32).
+constexpr int STEM_R = 2;
+
+template <typename T>
+__global__ void __launch_bounds__(256) stem_f32_kernel(const T* __restrict__ x, const float* __restrict__ w,
+                                                       const float* __restrict__ bias, float* __restrict__ y, int H,
+                                                       int W, int Ho, int Wo, int act, float add, float div) {
+  extern __shared__ __attribute__((aligned(16))) float xin[];  // [2R+1][(W + 2) * 3]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int row_groups = (Ho + STEM_R - 1) / STEM_R;
+  const int b = blockIdx.x / row_groups;
+  const int oy0 = (blockIdx.x % row_groups) * STEM_R;
+  const int pitch = (W + 2) * 3;
+  float a[2][7];
+  int off[7];
+#pragma unroll
+  for (int t = 0; t < 7; ++t) {
+    const int k = 4 * t + g;
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) a[ct][t] = k < 27 ? w[k * 32 + ct * 16 + li] : 0.f;
+    off[t] = k < 27 ? (k / 9) * pitch + ((k % 9) / 3) * 3 + (k % 3) : 0;
+  }
+  const f32x4_t bv0 = *reinterpret_cast<const f32x4_t*>(bias + g * 4);
+  const f32x4_t bv1 = *reinterpret_cast<const f32x4_t*>(bias + 16 + g * 4);
+  const int iy0 = oy0 * 2 - 1;
+  const T* xb = x + static_cast<int64_t>(b) * H * W * 3;
+  for (int i = tid; i < (2 * STEM_R + 1) * pitch; i += 256) {
+    const int r = i / pitch, c = i % pitch;  // c = (ix + 1) * 3 + ci
+    const int iy = iy0 + r, ix = c / 3 - 1;
+    float v = 0.f;
+    if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+      const T raw = xb[(static_cast<int64_t>(iy) * W + ix) * 3 + c % 3];
+      v = sizeof(T) == 1 ? (static_cast<float>(raw) + add) / div : static_cast<float>(raw);
+    }
+    xin[i] = v;
+  }
+  __syncthreads();
+  const int tiles_x = (Wo + 15) / 16;
+  for (int t = wave; t < STEM_R * tiles_x; t += 4) {
+    const int oyl = t / tiles_x, ox = (t % tiles_x) * 16 + li;
+    const int oy = oy0 + oyl;
+    const bool valid = ox < Wo && oy < Ho;
+    const int base = 2 * oyl * pitch + 2 * (valid ? ox : 0) * 3;
+    f32x4_t d0 = f32x4_t{0.f, 0.f, 0.f, 0.f}, d1 = d0;
+#pragma unroll
+    for (int s = 0; s < 7; ++s) {
+      const float bval = (4 * s + g < 27) ? xin[base + off[s]] : 0.f;
+      d0 = mfma4(a[0][s], bval, d0);
+      d1 = mfma4(a[1][s], bval, d1);
+    }
+    if (!valid) continue;
+    float* yp = y + ((static_cast<int64_t>(b) * Ho + oy) * Wo + ox) * 32 + g * 4;
+    f32x4_t o0 = d0 + bv0, o1 = d1 + bv1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      o0[r] = act_fn(o0[r], act);
+      o1[r] = act_fn(o1[r], act);
+    }
+    *reinterpret_cast<f32x4_t*>(yp) = o0;
+    *reinterpret_cast<f32x4_t*>(yp + 16) = o1;
+  }
+}
+
+// ------------------------------------------------------------- avgpool_f32 ----
+// one workgroup = one image x 64 channel quads; the 4 waves split the pixels
+__global__ void __launch_bounds__(256) avgpool_f32_kernel(const float* __restrict__ x, float* __restrict__ y, int HW,
+                                                          int C) {
+  __shared__ f32x4_t part[4][64];
+  const int cq = C >> 2;
+  const int groups = (cq + 63) / 64;
+  const int b = blockIdx.x / groups;
+  const int q = (blockIdx.x % groups) * 64 + (threadIdx.x & 63);
+  const int wave = threadIdx.x >> 6;
+  f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  if (q < cq)
+    for (int p = wave; p < HW; p += 4)
+      acc += *reinterpret_cast<const f32x4_t*>(x + (static_cast<int64_t>(b) * HW + p) * C + q * 4);
+  part[wave][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (wave != 0 || q >= cq) return;
+  const float inv = 1.f / HW;
+  const f32x4_t s = (part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] + part[3][threadIdx.x]) * inv;
+  *reinterpret_cast<f32x4_t*>(y + static_cast<int64_t>(b) * C + q * 4) = s;
+}
+
+// ------------------------------------------------------------ ir_block_f32 ----
+// Fused inverted residual, fp32:  y = project(dw3x3(expand(x))) (+ x).
+//
+// One workgroup = one TY x TX output tile of one image (4 waves).  Per tile:
+//   * the in-image part of the input halo tile ((TY-1)S+3 x (TX-1)S+3, clipped
+//     to the image) is staged in LDS, compactly (pixel c of the clipped
+//     rectangle), k4-major;
+//   * the hidden channels are walked in chunks of HC:
+//       expand  MFMA over the compact pixels only (no work for the conv's
+//               zero padding), bias + ReLU6, written into the chunk's hidden
+//               image laid out as the full halo grid (out-of-image cells are
+//               zeroed once per tile: they are the depthwise zero padding);
+//       dw 3x3  VALU, lane = one output pixel x 4 channels, bias + ReLU6,
+//               into a per-wave image of the wave's own output pixels;
+//       project MFMA accumulated in registers across chunks;
+//   * epilogue: bias (+ residual from the staged input tile) -> fp32 NHWC.
+// The hidden image is double-buffered, so one barrier per chunk orders
+// expand(c + 1) after every wave's dw(c).
+// has_expand = 0 (t = 1): the chunk's hidden image is a copy of the input.
+template <int S, int TY, int TX, int HC, int NOT, int KIN>
+struct IrF32Geom {
+  static constexpr int TIY = (TY - 1) * S + 3, TIX = (TX - 1) * S + 3;
+  static constexpr int PIN = TIY * TIX;           // halo grid cells
+  static constexpr int NC16 = (PIN + 15) / 16 * 16;  // compact pixels, padded
+  static constexpr int NPT = (TY * TX + 15) / 16;   // output pixel tiles
+  static constexpr int PTW = (NPT + 3) / 4;         // per wave
+  static constexpr int KQ = KIN / 4;
+  static constexpr int HQ = HC / 4;
+  static constexpr size_t xs_floats = static_cast<size_t>(KQ) * NC16 * 4;
+  static constexpr size_t hid_floats = static_cast<size_t>(2) * HQ * PIN * 4;
+  static constexpr size_t dwo_floats = static_cast<size_t>(HQ) * NPT * 16 * 4;
+  static size_t lds_bytes(int hid) { return 4 * (xs_floats + hid_floats + dwo_floats + static_cast<size_t>(10) * hid); }
+};
+
+template <int S, int TY, int TX, int HC, int NOT, int KIN>
+__global__ void __launch_bounds__(256) ir_block_f32_kernel(IrBlockF32Args a) {
+  using G = IrF32Geom<S, TY, TX, HC, NOT, KIN>;
+  constexpr int TIY = G::TIY, TIX = G::TIX, PIN = G::PIN, NC16 = G::NC16;
+  constexpr int NPT = G::NPT, PTW = G::PTW, KQ = G::KQ, HQ = G::HQ;
+  constexpr int NS16 = KIN / 16;         // full 16-k expand steps
+  constexpr bool KT8 = (KIN % 16) != 0;  // plus an 8-k tail
+  static_assert(KIN % 8 == 0 && HC % 16 == 0, "ir_block_f32: KIN % 8, HC % 16");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* xs = smem;                        // [KQ][NC16][4]   compact input tile
+  float* hidb = xs + G::xs_floats;         // [2][HQ][PIN][4] hidden chunk, halo grid
+  float* dwo = hidb + G::hid_floats;       // [HQ][NPT*16][4] dw output (project B operand)
+  float* wds = dwo + G::dwo_floats;        // [9][hid] depthwise weights
+  float* bds = wds + 9 * a.hid;            // [hid]    depthwise bias
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int tiles_img = a.tiles_x * a.tiles_y;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = tile / tiles_img;
+  const int tyx = tile - b * tiles_img;
+  const int oy0 = (tyx / a.tiles_x) * TY, ox0 = (tyx % a.tiles_x) * TX;
+  const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
+  const int ry0 = max(iy0, 0), ry1 = min(iy0 + TIY, a.H);
+  const int rx0 = max(ix0, 0), rx1 = min(ix0 + TIX, a.W);
+  const int RW = rx1 - rx0, NC = (ry1 - ry0) * RW;
+  const float* xb = a.x + static_cast<int64_t>(b) * a.H * a.W * a.cin;
+
+  // ---- stage the compact input tile (k4-major) + the depthwise weights
+  for (int v = tid; v < NC16 * KQ; v += 256) {
+    const int c = v / KQ, kq = v - c * KQ;
+    f32x4_t val = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    if (c < NC && kq * 4 < a.cin) {
+      const int yy = ry0 + c / RW, xx = rx0 + c % RW;
+      val = *reinterpret_cast<const f32x4_t*>(xb + (static_cast<int64_t>(yy) * a.W + xx) * a.cin + kq * 4);
+    }
+    *reinterpret_cast<f32x4_t*>(xs + (kq * NC16 + c) * 4) = val;
+  }
+  for (int v = tid; v < 9 * a.hid / 4; v += 256)
+    reinterpret_cast<f32x4_t*>(wds)[v] = reinterpret_cast<const f32x4_t*>(a.wd)[v];
+  for (int v = tid; v < a.hid; v += 256) bds[v] = a.bd[v];
+  // out-of-image halo cells are the depthwise zero padding: zero them in both
+  // hidden buffers (expand only ever writes in-image cells)
+  if (ry0 > iy0 || ry1 < iy0 + TIY || rx0 > ix0 || rx1 < ix0 + TIX) {
+    for (int v = tid; v < 2 * HQ * PIN; v += 256) {
+      const int p = v % PIN;
+      const int yy = iy0 + p / TIX, xx = ix0 + p % TIX;
+      if (yy < ry0 || yy >= ry1 || xx < rx0 || xx >= rx1)
+        reinterpret_cast<f32x4_t*>(hidb)[v] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+
+  // expand pixel tiles of this wave: halo-grid cell of each lane's compact pixel
+  constexpr int NBT_MAX = NC16 / 16;
+  constexpr int BTW = (NBT_MAX + 3) / 4;
+  const int nbt = (NC + 15) / 16;
+  int hcell[BTW];
+#pragma unroll
+  for (int j = 0; j < BTW; ++j) {
+    const int c = (wave + 4 * j) * 16 + li;
+    hcell[j] = c < NC ? (ry0 + c / RW - iy0) * TIX + (rx0 + c % RW - ix0) : -1;
+  }
+  // depthwise / project pixels of this wave: output pixel q -> its top-left halo cell
+  int dcell[PTW];
+#pragma unroll
+  for (int j = 0; j < PTW; ++j) {
+    const int q = (wave + 4 * j) * 16 + li;
+    const int qq = q < TY * TX ? q : 0;
+    dcell[j] = (qq / TX) * S * TIX + (qq % TX) * S;
+  }
+
+  f32x4_t acc[PTW][NOT];
+#pragma unroll
+  for (int j = 0; j < PTW; ++j)
+#pragma unroll
+    for (int o = 0; o < NOT; ++o) acc[j][o] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  __syncthreads();  // xs, wds, zeroed halo
+
+  int buf = 0;
+  for (int c0 = 0; c0 < a.hid; c0 += HC, buf ^= 1) {
+    float* hid = hidb + buf * (HQ * PIN * 4);
+    // project weights of this chunk (A operand), in flight during expand + dw
+    f32x4_t pa[NOT][HC / 16];
+#pragma unroll
+    for (int o = 0; o < NOT; ++o)
+#pragma unroll
+      for (int s = 0; s < HC / 16; ++s)
+        pa[o][s] = *reinterpret_cast<const f32x4_t*>(a.wp + static_cast<int64_t>(o * 16 + li) * a.hid + c0 + 16 * s +
+                                                     4 * g);
+
+    // ---- expand (MFMA over the compact in-image pixels) -> hidden halo grid
+    if (a.has_expand) {
+#pragma unroll
+      for (int t = 0; t < HC / 16; ++t) {
+        const float* wrow = a.we + static_cast<int64_t>(c0 + t * 16 + li) * KIN;
+        f32x4_t ea[NS16 > 0 ? NS16 : 1];
+        f32x2_t et = f32x2_t{0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < NS16; ++s) ea[s] = *reinterpret_cast<const f32x4_t*>(wrow + 16 * s + 4 * g);
+        if constexpr (KT8) et = *reinterpret_cast<const f32x2_t*>(wrow + 16 * NS16 + 2 * g);
+        const f32x4_t eb = *reinterpret_cast<const f32x4_t*>(a.be + c0 + t * 16 + 4 * g);
+#pragma unroll
+        for (int j = 0; j < BTW; ++j) {
+          const int bt = wave + 4 * j;
+          if (bt >= nbt) break;
+          const int c = bt * 16 + li;
+          f32x4_t e = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < NS16; ++s)
+            e = mfma_k16(ea[s], *reinterpret_cast<const f32x4_t*>(xs + ((4 * s + g) * NC16 + c) * 4), e);
+          if constexpr (KT8)
+            e = mfma_k8(et, *reinterpret_cast<const f32x2_t*>(xs + ((4 * NS16 + g / 2) * NC16 + c) * 4 + 2 * (g & 1)),
+                        e);
+          if (hcell[j] >= 0) *reinterpret_cast<f32x4_t*>(hid + ((t * 4 + g) * PIN + hcell[j]) * 4) = relu6x4(e + eb);
+        }
+      }
+    } else {
+      // t = 1: the hidden chunk is the input tile's channels c0 .. c0+HC
+      for (int v = tid; v < nbt * 16 * HQ; v += 256) {
+        const int c = v % (nbt * 16), hq = v / (nbt * 16);
+        if (c >= NC) continue;
+        const int cell = (ry0 + c / RW - iy0) * TIX + (rx0 + c % RW - ix0);
+        *reinterpret_cast<f32x4_t*>(hid + (hq * PIN + cell) * 4) =
+            *reinterpret_cast<const f32x4_t*>(xs + ((c0 / 4 + hq) * NC16 + c) * 4);
+      }
+    }
+    __syncthreads();  // hidden chunk complete (and, double buffered, dw(c-1) done everywhere)
+
+    // ---- depthwise 3x3 + bias + ReLU6: lane = output pixel (li) x channel quads g, g+4, ...
+#pragma unroll
+    for (int hq = g; hq < HQ; hq += 4) {
+      const int ch = c0 + hq * 4;
+      f32x4_t wv[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) wv[t] = *reinterpret_cast<const f32x4_t*>(wds + t * a.hid + ch);
+      const f32x4_t bb = *reinterpret_cast<const f32x4_t*>(bds + ch);
+      const float* hrow = hid + hq * PIN * 4;
+#pragma unroll
+      for (int j = 0; j < PTW; ++j) {
+        const int pt = wave + 4 * j;
+        if (pt >= NPT) break;
+        f32x4_t d = bb;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx)
+            d = __builtin_elementwise_fma(
+                *reinterpret_cast<const f32x4_t*>(hrow + (dcell[j] + ky * TIX + kx) * 4), wv[ky * 3 + kx], d);
+        *reinterpret_cast<f32x4_t*>(dwo + (hq * NPT * 16 + pt * 16 + li) * 4) = relu6x4(d);
+      }
+    }
+    // dwo pixel tiles of this wave are written and read by this wave only
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // ---- project: acc[pt][o] += Wp[o][chunk] . dw[pt][chunk]^T
+#pragma unroll
+    for (int j = 0; j < PTW; ++j) {
+      const int pt = wave + 4 * j;
+      if (pt >= NPT) break;
+#pragma unroll
+      for (int s = 0; s < HC / 16; ++s) {
+        const f32x4_t bf = *reinterpret_cast<const f32x4_t*>(dwo + ((4 * s + g) * NPT * 16 + pt * 16 + li) * 4);
+#pragma unroll
+        for (int o = 0; o < NOT; ++o) acc[j][o] = mfma_k16(pa[o][s], bf, acc[j][o]);
+      }
+    }
+  }
+
+  // ---- epilogue: bias (+ residual from the staged input tile) -> fp32 NHWC
+#pragma unroll
+  for (int j = 0; j < PTW; ++j) {
+    const int pt = wave + 4 * j;
+    if (pt >= NPT) break;
+    const int q = pt * 16 + li;
+    if (q >= TY * TX) continue;
+    const int gy = oy0 + q / TX, gx = ox0 + q % TX;
+    if (gy >= a.Ho || gx >= a.Wo) continue;
+    float* yp = a.y + ((static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx) * a.cout;
+    const int rc = (gy - ry0) * RW + (gx - rx0);  // compact index of the same pixel (stride 1)
+#pragma unroll
+    for (int o = 0; o < NOT; ++o) {
+      const int co = o * 16 + g * 4;
+      if (co >= a.cout) continue;
+      f32x4_t v = acc[j][o] + *reinterpret_cast<const f32x4_t*>(a.bp + co);
+      if (a.residual) v += *reinterpret_cast<const f32x4_t*>(xs + ((co / 4) * NC16 + rc) * 4);
+      *reinterpret_cast<f32x4_t*>(yp + co) = v;
+    }
+  }
+}
+
+// configurations (one instantiation each): MobileNetV2's fused blocks
+struct IrF32Cfg {
+  int S, TY, TX, HC, NOT, KIN;
+  void (*kernel)(IrBlockF32Args);
+  size_t (*lds)(int);
+};
+
+#define NNSX_IRF32(S, TY, TX, HC, NOT, KIN)                                                      \
+  IrF32Cfg {                                                                                     \
+    S, TY, TX, HC, NOT, KIN, &ir_block_f32_kernel<S, TY, TX, HC, NOT, KIN>,                      \
+        &IrF32Geom<S, TY, TX, HC, NOT, KIN>::lds_bytes                                           \
+  }
+
+const IrF32Cfg kIrF32Cfgs[] = {
+    // 112x112, t = 1 (32 -> 32 -> 16)
+    NNSX_IRF32(1, 14, 14, 16, 1, 32),
+    // 112 -> 56 (16 -> 96 -> 24)
+    NNSX_IRF32(2, 8, 8, 16, 2, 16),
+    // 56x56 (24 -> 144 -> 24)
+    NNSX_IRF32(1, 14, 14, 16, 2, 24),
+    // 56 -> 28 (24 -> 144 -> 32)
+    NNSX_IRF32(2, 7, 7, 16, 2, 24),
+    // 28x28 (32 -> 192 -> 32)
+    NNSX_IRF32(1, 14, 14, 16, 2, 32),
+    // 28 -> 14 (32 -> 192 -> 64)
+    NNSX_IRF32(2, 7, 7, 16, 4, 32),
+    // 14x14 (64 -> 384 -> 64 | 96, 96 -> 576 -> 96)
+    NNSX_IRF32(1, 7, 7, 16, 4, 64),
+    NNSX_IRF32(1, 7, 7, 16, 6, 64),
+    NNSX_IRF32(1, 7, 7, 16, 6, 96),
+};
+#undef NNSX_IRF32
+
+// tile shape per (stride, feature-map size): larger tiles cut the expand halo
+// recompute (14x14 tile: 1.31x the useful pixels, 8x8: 1.75x) within the LDS
+// budget of 2 workgroups per CU.  Any instantiated tile of the right stride
+// is correct for any map size (partial tiles are masked); the preference only
+// avoids partial tiles.
+int tile_pref(int S, int H, int W, int TY, int TX) {
+  const int Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
+  const bool fits = Ho % TY == 0 && Wo % TX == 0;
+  if (S == 1 && TY == 14 && TX == 14) return fits && Ho >= 28 ? 0 : 3;
+  if (S == 2 && TY == 8 && TX == 8) return fits && Ho >= 56 ? 0 : 3;
+  return fits ? 1 : 2;
+}
+
+const IrF32Cfg* find_cfg(int S, int H, int W, int cin, int hid, int cout, bool has_expand) {
+  const int kin = (cin + 7) / 8 * 8;
+  const int nout = (cout + 15) / 16;
+  if (!has_expand && hid != cin) return nullptr;
+  const IrF32Cfg* best = nullptr;
+  int best_pref = 1 << 30;
+  for (const auto& c : kIrF32Cfgs) {
+    if (c.S != S || c.KIN != kin || c.NOT != nout || hid % c.HC) continue;
+    if (c.lds(hid) > 160 * 1024) continue;
+    const int pref = tile_pref(S, H, W, c.TY, c.TX);
+    if (pref < best_pref) {
+      best = &c;
+      best_pref = pref;
+    }
+  }
+  return best;
+}
+
+}  // namespace
+
+void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
+                 int Kpad, int Npad, int act, hipStream_t s) {
+  const bool big = static_cast<int64_t>((M + 127) / 128) * ((N + 127) / 128) >= 256;
+  const int BM = big ? 128 : 64, BN = big ? 128 : 64;
+  dim3 grid((M + BM - 1) / BM, (N + BN - 1) / BN);
+  const int kstages = (Kpad + GKT - 1) / GKT;
+  int chunk = kstages;
+  // a small output grid (the classifier: M = batch) leaves most CUs idle while
+  // each workgroup walks all of K: split K over grid.z, reduce with fp32 atomics
+  const int tiles = static_cast<int>(grid.x * grid.y);
+  if (!res && act == 0 && tiles < 128 && kstages >= 8) {
+    const int splits = std::min(kstages / 4, (256 + tiles - 1) / tiles);
+    chunk = (kstages + splits - 1) / splits;
+    grid.z = static_cast<unsigned>((kstages + chunk - 1) / chunk);
+    (void)hipMemsetAsync(y, 0, static_cast<size_t>(M) * N * sizeof(float), s);
+  }
+  if (big)
+    hipLaunchKernelGGL((pw_gemm_f32_kernel<128, 128>), grid, dim3(256), 0, s, x, wt, bias, res, y, M, N, K, Kpad, Npad,
+                       act, chunk);
+  else
+    hipLaunchKernelGGL((pw_gemm_f32_kernel<64, 64>), grid, dim3(256), 0, s, x, wt, bias, res, y, M, N, K, Kpad, Npad,
+                       act, chunk);
+}
+
+void dw3x3_f32(const float* x, const float* w, const float* bias, float* y, int B, int H, int W, int C, int stride,
+               int dil, int act, hipStream_t s) {
+  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  const int64_t work = static_cast<int64_t>(B) * Ho * Wo * (C / 4);
+  const unsigned grid = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 16384)));
+  hipLaunchKernelGGL(dw3x3_f32_kernel, dim3(grid), dim3(256), 0, s, x, w, bias, y, B, H, W, C, Ho, Wo, stride, dil,
+                     act);
+}
+
+template <typename T>
+static void stem_f32_launch(const T* x, const float* w, const float* bias, float* y, int B, int H, int W, int act,
+                            float add, float div, hipStream_t s) {
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const size_t lds = sizeof(float) * (2 * STEM_R + 1) * (W + 2) * 3;
+  if (lds > 64 * 1024) {
+    static const bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_f32_kernel<T>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+    if (!ok || lds > 160 * 1024) return;
+  }
+  const unsigned grid = static_cast<unsigned>(B * ((Ho + STEM_R - 1) / STEM_R));
+  hipLaunchKernelGGL(stem_f32_kernel<T>, dim3(grid), dim3(256), lds, s, x, w, bias, y, H, W, Ho, Wo, act, add, div);
+}
+
+void stem3x3_f32(const float* x, const float* w, const float* bias, float* y, int B, int H, int W, int act,
+                 hipStream_t s) {
+  stem_f32_launch<float>(x, w, bias, y, B, H, W, act, 0.f, 1.f, s);
+}
+
+void stem3x3_u8_f32(const uint8_t* x, const float* w, const float* bias, float* y, int B, int H, int W, int act,
+                    float add, float div, hipStream_t s) {
+  stem_f32_launch<uint8_t>(x, w, bias, y, B, H, W, act, add, div, s);
+}
+
+void avgpool_f32(const float* x, float* y, int B, int HW, int C, hipStream_t s) {
+  const int groups = (C / 4 + 63) / 64;
+  hipLaunchKernelGGL(avgpool_f32_kernel, dim3(static_cast<unsigned>(B * groups)), dim3(256), 0, s, x, y, HW, C);
+}
+
+bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout, bool has_expand) {
+  if (stride != 1 && stride != 2) return false;
+  if (cin % 8 || cout % 4 || hid % 16) return false;
+  return find_cfg(stride, H, W, cin, hid, cout, has_expand) != nullptr;
+}
+
+bool ir_block_f32(const IrBlockF32Args& args, hipStream_t s) {
+  IrBlockF32Args a = args;
+  const IrF32Cfg* c = find_cfg(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0);
+  if (!c) return false;
+  a.Ho = (a.H - 1) / a.stride + 1;
+  a.Wo = (a.W - 1) / a.stride + 1;
+  a.tiles_y = (a.Ho + c->TY - 1) / c->TY;
+  a.tiles_x = (a.Wo + c->TX - 1) / c->TX;
+  const size_t lds = c->lds(a.hid);
+  if (lds > 64 * 1024) {
+    // opt in to the full 160 KiB once per instantiation
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(c->kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024) != hipSuccess)
+      return false;
+  }
+  const unsigned grid = static_cast<unsigned>(a.tiles_x * a.tiles_y * a.B);
+  hipLaunchKernelGGL(c->kernel, dim3(grid), dim3(256), lds, s, a);
+  return true;
+}
+
+}  // namespace kernels
+}  // namespace nnsx

@@ -20,8 +20,34 @@ at::Tensor act_ref(at::Tensor v, int64_t act) {
 }
 
 // ------------------------------------------------------------ pw_conv ----
+at::Tensor pw_conv_f32_cuda(const at::Tensor& x, const at::Tensor& wt, const at::Tensor& bias,
+                            const c10::optional<at::Tensor>& res, int64_t N, int64_t act) {
+  TORCH_CHECK(x.is_contiguous(), "pw_conv(f32): x must be contiguous");
+  TORCH_CHECK(wt.scalar_type() == at::kFloat && wt.is_contiguous() && wt.dim() == 2, "pw_conv(f32): wt [Npad,Kpad] f32");
+  TORCH_CHECK(bias.scalar_type() == at::kFloat && bias.numel() >= N, "pw_conv(f32): bias f32 [N]");
+  const int64_t K = x.size(-1);
+  const int64_t M = x.numel() / K;
+  const int64_t Kpad = wt.size(1), Npad = wt.size(0);
+  TORCH_CHECK(K % 4 == 0 && N % 4 == 0 && Kpad % 4 == 0 && Kpad >= K && Npad >= N,
+              "pw_conv(f32): shape constraints (K%4, N%4, Kpad%4, Kpad >= K, Npad >= N)");
+  auto sizes = x.sizes().vec();
+  sizes.back() = N;
+  at::Tensor y = at::empty(sizes, x.options());
+  const float* r = nullptr;
+  if (res.has_value() && res->defined()) {
+    TORCH_CHECK(res->scalar_type() == at::kFloat && res->is_contiguous() && res->numel() == M * N, "pw_conv(f32): residual");
+    r = res->data_ptr<float>();
+  }
+  nnsx::kernels::pw_gemm_f32(x.data_ptr<float>(), wt.data_ptr<float>(), bias.data_ptr<float>(), r, y.data_ptr<float>(),
+                             static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), static_cast<int>(Kpad),
+                             static_cast<int>(Npad), static_cast<int>(act), cur_stream());
+  return y;
+}
+
 at::Tensor pw_conv_cuda(const at::Tensor& x, const at::Tensor& wt, const at::Tensor& bias,
                         const c10::optional<at::Tensor>& res, int64_t N, int64_t act, bool out_f32) {
+  TORCH_CHECK(x.is_cuda(), "pw_conv: x must be a cuda tensor");
+  if (x.scalar_type() == at::kFloat) return pw_conv_f32_cuda(x, wt, bias, res, N, act);
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "pw_conv: x must be contiguous bf16 cuda");
   TORCH_CHECK(wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() && wt.dim() == 2, "pw_conv: wt [Npad,Kpad] bf16");
   TORCH_CHECK(bias.scalar_type() == at::kFloat && bias.numel() >= N, "pw_conv: bias f32 [N]");
@@ -51,12 +77,24 @@ at::Tensor pw_conv_cpu(const at::Tensor& x, const at::Tensor& wt, const at::Tens
   at::Tensor v = at::matmul(x.to(at::kFloat), w.t()) + bias.slice(0, 0, N);
   if (res.has_value() && res->defined()) v = v + res->to(at::kFloat);
   v = act_ref(v, act);
-  return v.to(out_f32 ? at::kFloat : at::kBFloat16);
+  return v.to(out_f32 || x.scalar_type() == at::kFloat ? at::kFloat : at::kBFloat16);
 }
 
 // ------------------------------------------------------------ dw_conv ----
 at::Tensor dw_conv_cuda(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int64_t stride, int64_t act,
                         int64_t dilation) {
+  if (x.scalar_type() == at::kFloat) {
+    TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() == 4, "dw_conv(f32): x [B,H,W,C] f32");
+    const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+    TORCH_CHECK(C % 4 == 0 && w.numel() == 9 * C && w.scalar_type() == at::kFloat && w.is_contiguous(),
+                "dw_conv(f32): w [9,C] f32, C%4==0");
+    const int64_t Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+    at::Tensor y = at::empty({B, Ho, Wo, C}, x.options());
+    nnsx::kernels::dw3x3_f32(x.data_ptr<float>(), w.data_ptr<float>(), bias.data_ptr<float>(), y.data_ptr<float>(),
+                             static_cast<int>(B), static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
+                             static_cast<int>(stride), static_cast<int>(dilation), static_cast<int>(act), cur_stream());
+    return y;
+  }
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() == 4, "dw_conv: x [B,H,W,C] bf16");
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   TORCH_CHECK(C % 8 == 0 && w.numel() == 9 * C && w.scalar_type() == at::kBFloat16, "dw_conv: w [9,C] bf16, C%8==0");
@@ -74,37 +112,49 @@ at::Tensor dw_conv_cpu(const at::Tensor& x, const at::Tensor& w, const at::Tenso
   at::Tensor xf = x.to(at::kFloat).permute({0, 3, 1, 2});
   at::Tensor wf = w.to(at::kFloat).view({3, 3, C}).permute({2, 0, 1}).unsqueeze(1).contiguous();
   at::Tensor v = at::conv2d(xf, wf, bias, {stride, stride}, {dilation, dilation}, {dilation, dilation}, C);
-  return act_ref(v, act).permute({0, 2, 3, 1}).contiguous().to(at::kBFloat16);
+  return act_ref(v, act).permute({0, 2, 3, 1}).contiguous().to(x.scalar_type() == at::kFloat ? at::kFloat : at::kBFloat16);
 }
 
 // --------------------------------------------------------------- stem ----
-at::Tensor stem_conv_cuda(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int64_t act) {
+at::Tensor stem_conv_cuda(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int64_t act, bool out_f32) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 4 && x.size(3) == 3,
               "stem_conv: x [B,H,W,3] f32");
   TORCH_CHECK(w.numel() == 27 * 32 && w.scalar_type() == at::kFloat, "stem_conv: w [3,3,3,32] f32");
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2);
   const int64_t Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
-  at::Tensor y = at::empty({B, Ho, Wo, 32}, x.options().dtype(at::kBFloat16));
+  at::Tensor y = at::empty({B, Ho, Wo, 32}, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  if (out_f32) {
+    nnsx::kernels::stem3x3_f32(x.data_ptr<float>(), w.data_ptr<float>(), bias.data_ptr<float>(), y.data_ptr<float>(),
+                               static_cast<int>(B), static_cast<int>(H), static_cast<int>(W), static_cast<int>(act),
+                               cur_stream());
+    return y;
+  }
   nnsx::kernels::stem3x3(x.data_ptr<float>(), w.data_ptr<float>(), bias.data_ptr<float>(), y.data_ptr(),
                          static_cast<int>(B), static_cast<int>(H), static_cast<int>(W), static_cast<int>(act), cur_stream());
   return y;
 }
 
-at::Tensor stem_conv_cpu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int64_t act) {
+at::Tensor stem_conv_cpu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int64_t act, bool out_f32) {
   at::Tensor xf = x.to(at::kFloat).permute({0, 3, 1, 2});
   at::Tensor wf = w.view({3, 3, 3, 32}).permute({3, 2, 0, 1}).contiguous();
   at::Tensor v = at::conv2d(xf, wf, bias, {2, 2}, {1, 1});
-  return act_ref(v, act).permute({0, 2, 3, 1}).contiguous().to(at::kBFloat16);
+  return act_ref(v, act).permute({0, 2, 3, 1}).contiguous().to(out_f32 ? at::kFloat : at::kBFloat16);
 }
 
 at::Tensor stem_conv_u8_cuda(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int64_t act, double add,
-                             double div) {
+                             double div, bool out_f32) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kByte && x.is_contiguous() && x.dim() == 4 && x.size(3) == 3,
               "stem_conv_u8: x [B,H,W,3] uint8");
   TORCH_CHECK(w.numel() == 27 * 32 && w.scalar_type() == at::kFloat, "stem_conv_u8: w [3,3,3,32] f32");
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2);
   const int64_t Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
-  at::Tensor y = at::empty({B, Ho, Wo, 32}, x.options().dtype(at::kBFloat16));
+  at::Tensor y = at::empty({B, Ho, Wo, 32}, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  if (out_f32) {
+    nnsx::kernels::stem3x3_u8_f32(x.data_ptr<uint8_t>(), w.data_ptr<float>(), bias.data_ptr<float>(),
+                                  y.data_ptr<float>(), static_cast<int>(B), static_cast<int>(H), static_cast<int>(W),
+                                  static_cast<int>(act), static_cast<float>(add), static_cast<float>(div), cur_stream());
+    return y;
+  }
   nnsx::kernels::stem3x3_u8(x.data_ptr<uint8_t>(), w.data_ptr<float>(), bias.data_ptr<float>(), y.data_ptr(),
                             static_cast<int>(B), static_cast<int>(H), static_cast<int>(W), static_cast<int>(act),
                             static_cast<float>(add), static_cast<float>(div), cur_stream());
@@ -112,13 +162,21 @@ at::Tensor stem_conv_u8_cuda(const at::Tensor& x, const at::Tensor& w, const at:
 }
 
 at::Tensor stem_conv_u8_cpu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int64_t act, double add,
-                            double div) {
+                            double div, bool out_f32) {
   at::Tensor xf = (x.to(at::kFloat) + static_cast<float>(add)) / static_cast<float>(div);
-  return stem_conv_cpu(xf, w, bias, act);
+  return stem_conv_cpu(xf, w, bias, act, out_f32);
 }
 
 // ------------------------------------------------------------ avgpool ----
 at::Tensor avgpool_cuda(const at::Tensor& x) {
+  if (x.scalar_type() == at::kFloat) {
+    TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() == 4 && x.size(3) % 4 == 0, "avgpool(f32): x [B,H,W,C%4]");
+    const int64_t B = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+    at::Tensor y = at::empty({B, C}, x.options());
+    nnsx::kernels::avgpool_f32(x.data_ptr<float>(), y.data_ptr<float>(), static_cast<int>(B), static_cast<int>(HW),
+                               static_cast<int>(C), cur_stream());
+    return y;
+  }
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() == 4, "avgpool: x [B,H,W,C] bf16");
   const int64_t B = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
   TORCH_CHECK(C % 8 == 0, "avgpool: C % 8");
@@ -128,13 +186,54 @@ at::Tensor avgpool_cuda(const at::Tensor& x) {
   return y;
 }
 
-at::Tensor avgpool_cpu(const at::Tensor& x) { return x.to(at::kFloat).mean({1, 2}).to(at::kBFloat16); }
+at::Tensor avgpool_cpu(const at::Tensor& x) { return x.to(at::kFloat).mean({1, 2}).to(x.scalar_type()); }
 
 // ----------------------------------------------------------- ir_block ----
 // Fused inverted residual.  we [hid, cin32], wd [9, hid], wp [ceil16(cout), hid] bf16; biases f32.
+at::Tensor ir_block_f32_cuda(const at::Tensor& x, const at::Tensor& we, const at::Tensor& be, const at::Tensor& wd,
+                             const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, int64_t stride,
+                             int64_t cout, bool has_expand, bool residual) {
+  TORCH_CHECK(x.is_contiguous() && x.dim() == 4, "ir_block(f32): x [B,H,W,C] f32");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int64_t hid = wd.size(1);
+  for (const auto* t : {&we, &be, &wd, &bd, &wp, &bp})
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "ir_block(f32): weights must be contiguous f32");
+  TORCH_CHECK(wd.numel() == 9 * hid && bd.numel() >= hid && wp.size(1) == hid && wp.size(0) >= (cout + 15) / 16 * 16 &&
+                  bp.numel() >= wp.size(0),
+              "ir_block(f32): dw / project weights");
+  TORCH_CHECK(!has_expand || (we.size(0) == hid && we.size(1) == (C + 7) / 8 * 8 && be.numel() >= hid),
+              "ir_block(f32): expand weights [hid, ceil8(cin)]");
+  TORCH_CHECK(!residual || (stride == 1 && C == cout), "ir_block(f32): residual needs stride 1 and cin == cout");
+  const int64_t Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  at::Tensor y = at::empty({B, Ho, Wo, cout}, x.options());
+  nnsx::kernels::IrBlockF32Args a;
+  a.x = x.data_ptr<float>();
+  a.y = y.data_ptr<float>();
+  a.we = has_expand ? we.data_ptr<float>() : nullptr;
+  a.be = has_expand ? be.data_ptr<float>() : nullptr;
+  a.wd = wd.data_ptr<float>();
+  a.bd = bd.data_ptr<float>();
+  a.wp = wp.data_ptr<float>();
+  a.bp = bp.data_ptr<float>();
+  a.B = static_cast<int>(B);
+  a.H = static_cast<int>(H);
+  a.W = static_cast<int>(W);
+  a.cin = static_cast<int>(C);
+  a.hid = static_cast<int>(hid);
+  a.cout = static_cast<int>(cout);
+  a.stride = static_cast<int>(stride);
+  a.has_expand = has_expand ? 1 : 0;
+  a.residual = residual ? 1 : 0;
+  TORCH_CHECK(nnsx::kernels::ir_block_f32(a, cur_stream()), "ir_block(f32): unsupported shape (stride ", stride, ", ",
+              H, "x", W, ", cin ", C, ", hid ", hid, ", cout ", cout, ")");
+  return y;
+}
+
 at::Tensor ir_block_cuda(const at::Tensor& x, const at::Tensor& we, const at::Tensor& be, const at::Tensor& wd,
                          const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, int64_t stride,
                          int64_t cout, bool has_expand, bool residual) {
+  TORCH_CHECK(x.is_cuda(), "ir_block: x must be a cuda tensor");
+  if (x.scalar_type() == at::kFloat) return ir_block_f32_cuda(x, we, be, wd, bd, wp, bp, stride, cout, has_expand, residual);
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() == 4,
               "ir_block: x [B,H,W,C] bf16");
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
@@ -176,7 +275,13 @@ at::Tensor ir_block_cpu(const at::Tensor& x, const at::Tensor& we, const at::Ten
   h = dw_conv_cpu(h, wd, bd, stride, 1, 1);
   c10::optional<at::Tensor> res;
   if (residual) res = x;
-  return pw_conv_cpu(h, wp, bp, res, cout, 0, false);
+  return pw_conv_cpu(h, wp, bp, res, cout, 0, false);  // (dtype follows x: f32 stays f32)
+}
+
+bool ir_supported_f32(int64_t stride, int64_t H, int64_t W, int64_t cin, int64_t hid, int64_t cout, bool has_expand) {
+  return nnsx::kernels::ir_block_f32_supported(static_cast<int>(stride), static_cast<int>(H), static_cast<int>(W),
+                                               static_cast<int>(cin), static_cast<int>(hid), static_cast<int>(cout),
+                                               has_expand);
 }
 
 bool ir_supported(int64_t stride, int64_t cin, int64_t hid, int64_t cout) {
@@ -189,12 +294,14 @@ bool ir_supported(int64_t stride, int64_t cin, int64_t hid, int64_t cout) {
 TORCH_LIBRARY(nnsx, m) {
   m.def("pw_conv(Tensor x, Tensor wt, Tensor bias, Tensor? res, int N, int act, bool out_f32) -> Tensor");
   m.def("dw_conv(Tensor x, Tensor w, Tensor bias, int stride, int act, int dilation=1) -> Tensor");
-  m.def("stem_conv(Tensor x, Tensor w, Tensor bias, int act) -> Tensor");
-  m.def("stem_conv_u8(Tensor x, Tensor w, Tensor bias, int act, float add, float div) -> Tensor");
+  m.def("stem_conv(Tensor x, Tensor w, Tensor bias, int act, bool out_f32=False) -> Tensor");
+  m.def("stem_conv_u8(Tensor x, Tensor w, Tensor bias, int act, float add, float div, bool out_f32=False) -> Tensor");
   m.def("avgpool(Tensor x) -> Tensor");
   m.def("ir_block(Tensor x, Tensor we, Tensor be, Tensor wd, Tensor bd, Tensor wp, Tensor bp, int stride, int cout, "
         "bool has_expand, bool residual) -> Tensor");
   m.def("ir_supported(int stride, int cin, int hid, int cout) -> bool", ir_supported);
+  m.def("ir_supported_f32(int stride, int H, int W, int cin, int hid, int cout, bool has_expand) -> bool",
+        ir_supported_f32);
 }
 
 TORCH_LIBRARY_IMPL(nnsx, CUDA, m) {

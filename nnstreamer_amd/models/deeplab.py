@@ -83,9 +83,10 @@ class FusedDeepLabV3(nn.Module):
         super().__init__()
 
     @classmethod
-    def from_reference(cls, m: DeepLabV3MobileNetV2) -> "FusedDeepLabV3":
+    def from_reference(cls, m: DeepLabV3MobileNetV2, precision: str = "bf16") -> "FusedDeepLabV3":
         self = cls()
         m = m.eval()
+        self.f32 = precision == "fp32"
         stem: ConvBNReLU = m.features[0]
         w, b = _fold(stem[0], stem[1])
         self.register_buffer("stem_w", w.permute(2, 3, 1, 0).contiguous())
@@ -93,14 +94,14 @@ class FusedDeepLabV3(nn.Module):
         self.in_add, self.in_div = 0.0, 255.0  # uint8 input: the pipeline normalisation, fused
         blocks = []
         for ir in m.features[1:]:
-            blk = Block(ir)
+            blk = Block(ir, precision)
             dwc = ir.conv[1 if ir.expand != 1 else 0][0]
             blk.dw.dilation = int(dwc.dilation[0])
             blocks.append(blk)
         self.blocks = nn.ModuleList(blocks)
-        self.aspp_conv = PW(*_fold(m.aspp_conv[0], m.aspp_conv[1]), act=1)
-        self.aspp_pool = PW(*_fold(m.aspp_pool[0], m.aspp_pool[1]), act=1)
-        self.project = PW(*_fold(m.project[0], m.project[1]), act=1)
+        self.aspp_conv = PW(*_fold(m.aspp_conv[0], m.aspp_conv[1]), act=1, precision=precision)
+        self.aspp_pool = PW(*_fold(m.aspp_pool[0], m.aspp_pool[1]), act=1, precision=precision)
+        self.project = PW(*_fold(m.project[0], m.project[1]), act=1, precision=precision)
         wc = m.classifier.weight.detach().float()
         bc = m.classifier.bias.detach().float()
         n = wc.shape[0]
@@ -109,13 +110,13 @@ class FusedDeepLabV3(nn.Module):
         wp[:n] = wc
         bp = torch.zeros(n8)
         bp[:n] = bc
-        self.classifier = PW(wp, bp, act=0, out_f32=True)
+        self.classifier = PW(wp, bp, act=0, out_f32=True, precision=precision)
         self.num_classes = int(n)
         self.out_size = int(m.out_size)
         return self
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        h = stem(x, self.stem_w, self.stem_b, self.in_add, self.in_div)
+        h = stem(x, self.stem_w, self.stem_b, self.in_add, self.in_div, self.f32)
         for blk in self.blocks:
             h = blk(h)
         a = self.aspp_conv(h)
@@ -130,5 +131,5 @@ class FusedDeepLabV3(nn.Module):
         return y.permute(0, 2, 3, 1).contiguous()
 
 
-def fused_deeplabv3(seed: int = 0) -> FusedDeepLabV3:
-    return FusedDeepLabV3.from_reference(deeplabv3(seed)).eval()
+def fused_deeplabv3(seed: int = 0, precision: str = "bf16") -> FusedDeepLabV3:
+    return FusedDeepLabV3.from_reference(deeplabv3(seed), precision).eval()

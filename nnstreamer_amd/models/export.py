@@ -41,34 +41,38 @@ def build_model(name: str, seed: int = 0, layout: str = "nchw", num_classes: int
     name = name.lower().replace("-", "_")
     if name in ("mobilenet_v2", "mbv2"):
         m = mobilenet_v2(num_classes=num_classes, seed=seed)
-    elif name in ("mobilenet_v2_fused", "mbv2_fused"):
+    elif name in ("mobilenet_v2_fused", "mbv2_fused", "mobilenet_v2_fused_bf16"):
         from .fused import FusedMobileNetV2
 
         return FusedMobileNetV2.from_reference(mobilenet_v2(num_classes=num_classes, seed=seed)).eval()
+    elif name in ("mobilenet_v2_fused_fp32", "mbv2_fused_fp32"):
+        from .fused import FusedMobileNetV2
+
+        return FusedMobileNetV2.from_reference(mobilenet_v2(num_classes=num_classes, seed=seed), "fp32").eval()
     elif name in ("ssd_mobilenet", "ssd"):
         from .ssd import ssd_mobilenet
 
         return ssd_mobilenet(seed=seed).eval()
-    elif name in ("ssd_mobilenet_fused", "ssd_fused"):
+    elif name in ("ssd_mobilenet_fused", "ssd_fused", "ssd_fused_fp32"):
         from .ssd import fused_ssd_mobilenet
 
-        return fused_ssd_mobilenet(seed=seed)
+        return fused_ssd_mobilenet(seed=seed, precision="fp32" if name.endswith("_fp32") else "bf16")
     elif name in ("deeplabv3", "deeplab"):
         from .deeplab import deeplabv3
 
         return deeplabv3(seed=seed).eval()
-    elif name in ("deeplabv3_fused", "deeplab_fused"):
+    elif name in ("deeplabv3_fused", "deeplab_fused", "deeplab_fused_fp32"):
         from .deeplab import fused_deeplabv3
 
-        return fused_deeplabv3(seed=seed)
+        return fused_deeplabv3(seed=seed, precision="fp32" if name.endswith("_fp32") else "bf16")
     elif name in ("posenet", "pose"):
         from .posenet import posenet
 
         return posenet(seed=seed).eval()
-    elif name in ("posenet_fused", "pose_fused"):
+    elif name in ("posenet_fused", "pose_fused", "posenet_fused_fp32"):
         from .posenet import fused_posenet
 
-        return fused_posenet(seed=seed)
+        return fused_posenet(seed=seed, precision="fp32" if name.endswith("_fp32") else "bf16")
     else:
         raise ValueError(f"unknown model {name}")
     return (NHWCWrapper(m) if layout == "nhwc" else NCHWWrapper(m)).eval()

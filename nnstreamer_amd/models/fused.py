@@ -1,9 +1,16 @@
 """FusedMobileNetV2: the inference form of MobileNetV2 that runs on the
-hand-written CDNA4 kernels (csrc/kernels/mbv2.hip) through torch.ops.nnsx.*.
+hand-written CDNA4 kernels through torch.ops.nnsx.*, in one of two precisions:
 
-* BatchNorm folded into conv weight + bias (fp32 fold, then bf16 weights).
-* NHWC bf16 activations end to end; the input is the NNStreamer video tensor
-  `3:224:224:B` (NHWC float32 after tensor_transform) -- no transpose needed.
+* ``precision="fp32"`` (reference precision, csrc/kernels/mbv2_f32.hip): fp32
+  weights, activations and accumulation; the GEMMs run on
+  v_mfma_f32_16x16x4_f32.  This is what the reference computes
+  (tensor_filter_pytorch.cc:517-536 runs the model on float32 tensors).
+* ``precision="bf16"`` (csrc/kernels/mbv2.hip, ir_fused.hip): bf16 weights and
+  activations, fp32 accumulation.
+
+* BatchNorm folded into conv weight + bias (fold in fp64, then fp32 / bf16).
+* NHWC activations end to end; the input is the NNStreamer video tensor
+  `3:224:224:B` (NHWC) -- no transpose needed.
 * 1x1 convs (expand / project / head / classifier) are MFMA GEMMs with
   bias + ReLU6 + residual fused in the epilogue; depthwise 3x3 and the stem are
   bandwidth kernels; global average pool is its own small kernel.
@@ -35,29 +42,37 @@ def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d):
     return w.float(), b.float()
 
 
-def _pw_weight(w: torch.Tensor):
-    """[N, K, 1, 1] fp32 -> zero-padded [ceil64(N), ceil32(K)] bf16 (K contiguous)."""
+PRECISIONS = ("bf16", "fp32")
+
+
+def _pw_weight(w: torch.Tensor, precision: str = "bf16"):
+    """[N, K, 1, 1] fp32 -> zero-padded weight matrix, K contiguous:
+    bf16 [ceil64(N), ceil32(K)] for the bf16 GEMMs, fp32 [ceil16(N), ceil8(K)]
+    for the fp32 ones."""
     n, k = w.shape[0], w.shape[1]
-    npad = (n + 63) // 64 * 64
-    kpad = (k + 31) // 32 * 32
+    if precision == "fp32":
+        npad, kpad = (n + 15) // 16 * 16, (k + 7) // 8 * 8
+    else:
+        npad, kpad = (n + 63) // 64 * 64, (k + 31) // 32 * 32
     out = torch.zeros(npad, kpad, dtype=torch.float32)
     out[:n, :k] = w.reshape(n, k)
-    return out.to(torch.bfloat16)
+    return out if precision == "fp32" else out.to(torch.bfloat16)
 
 
-def stem(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, in_add: float, in_div: float) -> torch.Tensor:
+def stem(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, in_add: float, in_div: float,
+         out_f32: bool = False) -> torch.Tensor:
     """3x3/2 stem from either the raw uint8 frame (normalised in-kernel as
     (x + in_add) / in_div, i.e. the pipeline's tensor_transform arithmetic fused
     into the first conv) or an already-normalised float32 frame."""
     if x.dtype == torch.uint8:
-        return torch.ops.nnsx.stem_conv_u8(x.contiguous(), w, b, 1, in_add, in_div)
-    return torch.ops.nnsx.stem_conv(x.contiguous().float(), w, b, 1)
+        return torch.ops.nnsx.stem_conv_u8(x.contiguous(), w, b, 1, in_add, in_div, out_f32)
+    return torch.ops.nnsx.stem_conv(x.contiguous().float(), w, b, 1, out_f32)
 
 
 class PW(nn.Module):
-    def __init__(self, w: torch.Tensor, b: torch.Tensor, act: int, out_f32: bool = False):
+    def __init__(self, w: torch.Tensor, b: torch.Tensor, act: int, out_f32: bool = False, precision: str = "bf16"):
         super().__init__()
-        self.register_buffer("wt", _pw_weight(w))
+        self.register_buffer("wt", _pw_weight(w, precision))
         bias = torch.zeros(self.wt.shape[0], dtype=torch.float32)
         bias[: b.numel()] = b
         self.register_buffer("bias", bias)
@@ -70,10 +85,12 @@ class PW(nn.Module):
 
 
 class DW(nn.Module):
-    def __init__(self, w: torch.Tensor, b: torch.Tensor, stride: int, dilation: int = 1, act: int = 1):
+    def __init__(self, w: torch.Tensor, b: torch.Tensor, stride: int, dilation: int = 1, act: int = 1,
+                 precision: str = "bf16"):
         super().__init__()
         c = w.shape[0]
-        self.register_buffer("w", w.reshape(c, 9).t().contiguous().to(torch.bfloat16))  # [9, C]
+        wdt = torch.float32 if precision == "fp32" else torch.bfloat16
+        self.register_buffer("w", w.reshape(c, 9).t().contiguous().to(wdt))  # [9, C]
         self.register_buffer("bias", b.contiguous())
         self.stride = int(stride)
         self.dilation = int(dilation)
@@ -84,27 +101,33 @@ class DW(nn.Module):
 
 
 class Block(nn.Module):
-    def __init__(self, ir: InvertedResidual):
+    def __init__(self, ir: InvertedResidual, precision: str = "bf16"):
         super().__init__()
+        assert precision in PRECISIONS, precision
         layers = list(ir.conv)
         self.has_expand = ir.expand != 1
+        self.f32 = precision == "fp32"
         idx = 0
         if self.has_expand:
             e: ConvBNReLU = layers[0]
-            self.expand = PW(*_fold(e[0], e[1]), act=1)
+            self.expand = PW(*_fold(e[0], e[1]), act=1, precision=precision)
             idx = 1
         else:
-            self.expand = PW(torch.zeros(8, 8, 1, 1), torch.zeros(8), act=0)  # unused placeholder
+            self.expand = PW(torch.zeros(8, 8, 1, 1), torch.zeros(8), act=0, precision=precision)  # unused placeholder
         d: ConvBNReLU = layers[idx]
-        self.dw = DW(*_fold(d[0], d[1]), stride=ir.stride)
+        self.dw = DW(*_fold(d[0], d[1]), stride=ir.stride, precision=precision)
         p: ConvBNReLU = layers[idx + 1]
-        self.project = PW(*_fold(p[0], p[1]), act=0)
+        self.project = PW(*_fold(p[0], p[1]), act=0, precision=precision)
         self.use_res = bool(ir.use_res)
-        # fused single-kernel path (csrc/kernels/ir_fused.hip): hidden activation stays in LDS
+        # fused single-kernel path (csrc/kernels/ir_fused.hip, mbv2_f32.hip): hidden activation stays in LDS
         hid = int(d[0].out_channels)
         cin = int(ir.conv[0][0].in_channels)
         self.hid = hid
+        self.cin = cin
         self.cout = int(p[0].out_channels)
+        if self.f32:
+            self._init_f32(cin, hid)
+            return
         # hidden width padded to the kernel's 32-channel chunk with zero weights/biases
         # (padded channels stay exactly 0 through ReLU6 and contribute nothing)
         hp = (hid + 31) // 32 * 32
@@ -130,7 +153,35 @@ class Block(nn.Module):
         self.use_ir = (bool(torch.ops.nnsx.ir_supported(int(ir.stride), cin, hp, self.cout)) and FUSE_IR
                        and (self.has_expand or hid == hp) and self.cout < 320)
 
+    def _init_f32(self, cin: int, hid: int):
+        """fp32 fused-block operands (mbv2_f32.hip): we [hid][ceil8(cin)],
+        wd [9][hid], wp [ceil16(cout)][hid]; no hidden padding (hid % 16 == 0)."""
+        kin = (cin + 7) // 8 * 8
+        we = torch.zeros(hid, kin)
+        be = torch.zeros(hid)
+        if self.has_expand:
+            we[:] = self.expand.wt[:hid, :kin]
+            be[:] = self.expand.bias[:hid]
+        self.register_buffer("ir_we", we)
+        self.register_buffer("ir_be", be)
+        self.register_buffer("ir_wd", self.dw.w.clone())
+        self.register_buffer("ir_bd", self.dw.bias.clone())
+        self.register_buffer("ir_wp", self.project.wt[:, :hid].contiguous().clone())
+        self.min_tiles = 0
+        self.use_ir = FUSE_IR and hid % 16 == 0 and (self.has_expand or hid == cin)
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.f32:
+            if self.use_ir and self.dw.dilation == 1 and bool(torch.ops.nnsx.ir_supported_f32(
+                    self.dw.stride, x.shape[1], x.shape[2], self.cin, self.hid, self.cout, self.has_expand)):
+                return torch.ops.nnsx.ir_block(x, self.ir_we, self.ir_be, self.ir_wd, self.ir_bd, self.ir_wp,
+                                               self.project.bias, self.dw.stride, self.cout, self.has_expand,
+                                               self.use_res)
+            h = self.expand(x) if self.has_expand else x
+            h = self.dw(h)
+            if self.use_res:
+                return self.project(h, x)
+            return self.project(h)
         # the fused kernel walks one 8x8 output tile per workgroup slot: with fewer
         # tiles than CUs (7x7 maps below batch 256) the unfused GEMM chain is faster
         # (scripts/bench_ir.py: 56 vs 64 us at batch 128, 94 vs 67 us at batch 256)
@@ -148,29 +199,33 @@ class Block(nn.Module):
 
 
 class FusedMobileNetV2(nn.Module):
-    """Input: [B, H, W, 3] float32 NHWC (NNStreamer `3:W:H:B`).  Output: [B, classes] fp32 logits."""
+    """Input: [B, H, W, 3] uint8 (raw frame, normalised in the stem) or float32
+    NHWC (NNStreamer `3:W:H:B`).  Output: [B, classes] fp32 logits."""
 
     def __init__(self):
         super().__init__()
 
     @classmethod
-    def from_reference(cls, m: MobileNetV2) -> "FusedMobileNetV2":
+    def from_reference(cls, m: MobileNetV2, precision: str = "bf16") -> "FusedMobileNetV2":
+        assert precision in PRECISIONS, precision
         self = cls()
         m = m.eval()
+        self.f32 = precision == "fp32"
         stem: ConvBNReLU = m.features[0]
         w, b = _fold(stem[0], stem[1])  # [32, 3, 3, 3]
         self.register_buffer("stem_w", w.permute(2, 3, 1, 0).contiguous())  # [ky, kx, ci, co]
         self.register_buffer("stem_b", b.contiguous())
         self.in_add, self.in_div = -127.5, 127.5
-        self.blocks = nn.ModuleList([Block(ir) for ir in m.features[1:-1]])
+        self.blocks = nn.ModuleList([Block(ir, precision) for ir in m.features[1:-1]])
         head: ConvBNReLU = m.features[-1]
-        self.head = PW(*_fold(head[0], head[1]), act=1)
+        self.head = PW(*_fold(head[0], head[1]), act=1, precision=precision)
         fc: nn.Linear = m.classifier[1]
-        self.fc = PW(fc.weight.detach().float()[:, :, None, None], fc.bias.detach().float(), act=0, out_f32=True)
+        self.fc = PW(fc.weight.detach().float()[:, :, None, None], fc.bias.detach().float(), act=0, out_f32=True,
+                     precision=precision)
         return self
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        h = stem(x, self.stem_w, self.stem_b, self.in_add, self.in_div)
+        h = stem(x, self.stem_w, self.stem_b, self.in_add, self.in_div, self.f32)
         for blk in self.blocks:
             h = blk(h)
         h = self.head(h)
@@ -178,7 +233,7 @@ class FusedMobileNetV2(nn.Module):
         return self.fc(h)
 
 
-def fused_mobilenet_v2(seed: int = 0) -> FusedMobileNetV2:
+def fused_mobilenet_v2(seed: int = 0, precision: str = "bf16") -> FusedMobileNetV2:
     from .mobilenet_v2 import mobilenet_v2
 
-    return FusedMobileNetV2.from_reference(mobilenet_v2(seed=seed)).eval()
+    return FusedMobileNetV2.from_reference(mobilenet_v2(seed=seed), precision).eval()

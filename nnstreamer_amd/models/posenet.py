@@ -70,7 +70,7 @@ def posenet(seed: int = 0) -> PoseNetMobileNetV1:
     return m.eval()
 
 
-def _padded_pw(conv: nn.Conv2d) -> PW:
+def _padded_pw(conv: nn.Conv2d, precision: str = "bf16") -> PW:
     w = conv.weight.detach().float()
     b = conv.bias.detach().float()
     n = w.shape[0]
@@ -79,7 +79,7 @@ def _padded_pw(conv: nn.Conv2d) -> PW:
     wp[:n] = w
     bp = torch.zeros(n8)
     bp[:n] = b
-    return PW(wp, bp, act=0, out_f32=True)
+    return PW(wp, bp, act=0, out_f32=True, precision=precision)
 
 
 class FusedPoseNet(nn.Module):
@@ -89,9 +89,10 @@ class FusedPoseNet(nn.Module):
         super().__init__()
 
     @classmethod
-    def from_reference(cls, m: PoseNetMobileNetV1) -> "FusedPoseNet":
+    def from_reference(cls, m: PoseNetMobileNetV1, precision: str = "bf16") -> "FusedPoseNet":
         self = cls()
         m = m.eval()
+        self.f32 = precision == "fp32"
         stem: ConvBNReLU = m.backbone[0]
         w, b = _fold(stem[0], stem[1])
         self.register_buffer("stem_w", w.permute(2, 3, 1, 0).contiguous())
@@ -102,17 +103,17 @@ class FusedPoseNet(nn.Module):
         for i in range(0, len(layers), 2):
             d: ConvBNReLU = layers[i]
             p: ConvBNReLU = layers[i + 1]
-            dws.append(DW(*_fold(d[0], d[1]), stride=int(d[0].stride[0])))
-            pws.append(PW(*_fold(p[0], p[1]), act=1))
+            dws.append(DW(*_fold(d[0], d[1]), stride=int(d[0].stride[0]), precision=precision))
+            pws.append(PW(*_fold(p[0], p[1]), act=1, precision=precision))
         self.dws = nn.ModuleList(dws)
         self.pws = nn.ModuleList(pws)
-        self.heat = _padded_pw(m.heatmap)
-        self.offs = _padded_pw(m.offsets)
+        self.heat = _padded_pw(m.heatmap, precision)
+        self.offs = _padded_pw(m.offsets, precision)
         self.k = int(m.heatmap.out_channels)
         return self
 
     def forward(self, x: torch.Tensor):
-        h = stem(x, self.stem_w, self.stem_b, self.in_add, self.in_div)
+        h = stem(x, self.stem_w, self.stem_b, self.in_add, self.in_div, self.f32)
         for d, p in zip(self.dws, self.pws):
             h = p(d(h))
         hm = self.heat(h)[..., : self.k].contiguous()
@@ -120,8 +121,8 @@ class FusedPoseNet(nn.Module):
         return hm, of
 
 
-def fused_posenet(seed: int = 0) -> FusedPoseNet:
-    return FusedPoseNet.from_reference(posenet(seed)).eval()
+def fused_posenet(seed: int = 0, precision: str = "bf16") -> FusedPoseNet:
+    return FusedPoseNet.from_reference(posenet(seed), precision).eval()
 
 
 def write_pose_labels(path: str) -> str:

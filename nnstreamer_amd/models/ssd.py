@@ -124,11 +124,11 @@ def _pad_rows(w: torch.Tensor, b: torch.Tensor, mult: int = 8):
 
 
 class FusedSepHead(nn.Module):
-    def __init__(self, h: SepHead, k: int):
+    def __init__(self, h: SepHead, k: int, precision: str = "bf16"):
         super().__init__()
-        self.dw = DW(*_fold(h.dw[0], h.dw[1]), stride=1)
+        self.dw = DW(*_fold(h.dw[0], h.dw[1]), stride=1, precision=precision)
         w, b = _pad_rows(h.pw.weight.detach().float(), h.pw.bias.detach().float())
-        self.pw = PW(w, b, act=0, out_f32=True)
+        self.pw = PW(w, b, act=0, out_f32=True, precision=precision)
         self.n = int(h.pw.out_channels)
         self.k = int(k)
 
@@ -141,11 +141,11 @@ class FusedSepHead(nn.Module):
 
 
 class FusedExtra(nn.Module):
-    def __init__(self, e: Extra):
+    def __init__(self, e: Extra, precision: str = "bf16"):
         super().__init__()
-        self.a = PW(*_fold(e[0][0], e[0][1]), act=1)
-        self.d = DW(*_fold(e[1][0], e[1][1]), stride=2)
-        self.c = PW(*_fold(e[2][0], e[2][1]), act=1)
+        self.a = PW(*_fold(e[0][0], e[0][1]), act=1, precision=precision)
+        self.d = DW(*_fold(e[1][0], e[1][1]), stride=2, precision=precision)
+        self.c = PW(*_fold(e[2][0], e[2][1]), act=1, precision=precision)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return self.c(self.d(self.a(x)))
@@ -158,25 +158,26 @@ class FusedSSDLite(nn.Module):
         super().__init__()
 
     @classmethod
-    def from_reference(cls, m: SSDLiteMobileNetV2) -> "FusedSSDLite":
+    def from_reference(cls, m: SSDLiteMobileNetV2, precision: str = "bf16") -> "FusedSSDLite":
         self = cls()
         m = m.eval()
+        self.f32 = precision == "fp32"
         stem: ConvBNReLU = m.features[0]
         w, b = _fold(stem[0], stem[1])
         self.register_buffer("stem_w", w.permute(2, 3, 1, 0).contiguous())
         self.register_buffer("stem_b", b.contiguous())
         self.in_add, self.in_div = -127.5, 127.5  # uint8 input: the pipeline normalisation, fused
-        self.blocks = nn.ModuleList([Block(ir) for ir in m.features[1:-1]])  # features[1..17]
+        self.blocks = nn.ModuleList([Block(ir, precision) for ir in m.features[1:-1]])  # features[1..17]
         head: ConvBNReLU = m.features[-1]
-        self.head = PW(*_fold(head[0], head[1]), act=1)
-        self.extras = nn.ModuleList([FusedExtra(e) for e in m.extras])
-        self.box_heads = nn.ModuleList([FusedSepHead(h, 4) for h in m.box_heads])
-        self.cls_heads = nn.ModuleList([FusedSepHead(h, m.num_classes) for h in m.cls_heads])
+        self.head = PW(*_fold(head[0], head[1]), act=1, precision=precision)
+        self.extras = nn.ModuleList([FusedExtra(e, precision) for e in m.extras])
+        self.box_heads = nn.ModuleList([FusedSepHead(h, 4, precision) for h in m.box_heads])
+        self.cls_heads = nn.ModuleList([FusedSepHead(h, m.num_classes, precision) for h in m.cls_heads])
         self.feat_block = 13  # blocks[13] == features[14]: its expansion output is SSD feature 1
         return self
 
     def forward(self, x: torch.Tensor):
-        h = stem(x, self.stem_w, self.stem_b, self.in_add, self.in_div)
+        h = stem(x, self.stem_w, self.stem_b, self.in_add, self.in_div, self.f32)
         feats: List[torch.Tensor] = []
         for i, blk in enumerate(self.blocks):
             if i == self.feat_block:
@@ -200,8 +201,8 @@ class FusedSSDLite(nn.Module):
         return bx.reshape(bx.shape[0], bx.shape[1], 1, 4), torch.cat(logits, 1)
 
 
-def fused_ssd_mobilenet(seed: int = 0) -> FusedSSDLite:
-    return FusedSSDLite.from_reference(ssd_mobilenet(seed)).eval()
+def fused_ssd_mobilenet(seed: int = 0, precision: str = "bf16") -> FusedSSDLite:
+    return FusedSSDLite.from_reference(ssd_mobilenet(seed), precision).eval()
 
 
 def box_priors(min_scale: float = 0.2, max_scale: float = 0.95):

@@ -1,0 +1,34 @@
+#!/bin/bash
+# One GPU-box session.  Each GPU step has its own time limit; the first failing
+# step ends the session (no retries).  STEPS: comma list of
+#   f32      new fp32 kernel tests            (tests/test_gpu_mbv2_f32.py)
+#   test     the whole GPU suite
+#   smoke    __graft_entry__.smoke()
+#   bench    bench.py (BENCH_ARGS)
+#   prof     rocprofv3 kernel stats of bench.py (PROF_ARGS)
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+STEPS=${STEPS:-f32,test,smoke,bench}
+R=$GRAFT_REPO_ROOT
+[ -z "$R" ] && R=$(pwd)
+for s in ${STEPS//,/ }; do
+  case $s in
+    f32)
+      timeout -k 10 600 python -u -m pytest tests/test_gpu_mbv2_f32.py -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_f32.log 2>&1 || { echo "f32 tests failed"; tail -60 gpurun_out/pytest_f32.log; exit 1; }
+      tail -3 gpurun_out/pytest_f32.log ;;
+    test)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo "gpu tests failed"; tail -60 gpurun_out/pytest_gpu.log; exit 1; }
+      tail -3 gpurun_out/pytest_gpu.log ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; tail -30 gpurun_out/smoke.log; exit 1; }
+      tail -2 gpurun_out/smoke.log ;;
+    bench)
+      timeout -k 10 600 python bench.py ${BENCH_ARGS} > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -40 gpurun_out/bench.log; exit 1; }
+      tail -1 gpurun_out/bench.log ;;
+    prof)
+      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run --output-format csv -- python3 $R/bench.py ${PROF_ARGS} > $R/gpurun_out/prof.log 2>&1) || { echo "prof failed"; tail -30 gpurun_out/prof.log; exit 1; }
+      find gpurun_out/prof -name "*kernel_stats.csv" ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done

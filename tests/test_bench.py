@@ -1,0 +1,36 @@
+"""bench.py launcher contract (CPU): `--gpus N` spawns N rank processes by
+itself, all-gathers the per-rank records and reports the whole-job value."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env=None, timeout=600):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                          env=e, timeout=timeout, cwd=ROOT)
+
+
+def test_bench_spawns_ranks_and_gathers():
+    r = _run(["--cpu", "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "1", "--latency-frames", "0"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["pg_world"] == 2 and out["pg_backend"] == "gloo"
+    assert len(out["per_rank_fps"]) == 2 and all(v > 0 for v in out["per_rank_fps"])
+    assert out["config"]["global_batch"] == 2 and out["config"]["parallelism"] == "branch-dp2"
+    assert out["steps"] == 2 and out["warmup"] == 1 and out["value"] > 0
+
+
+def test_bench_refuses_world_mismatch():
+    r = _run(["--cpu", "--gpus", "2", "--steps", "1", "--warmup", "1", "--batch", "1"],
+             env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0
+    assert "WORLD_SIZE=1" in (r.stderr + r.stdout)

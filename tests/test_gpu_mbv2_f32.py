@@ -1,0 +1,240 @@
+"""fp32 CDNA4 MobileNetV2 kernels (csrc/kernels/mbv2_f32.hip) vs float64
+references, plus model- and pipeline-level agreement gates for the benched
+engines (fp32 = reference precision, bf16 = secondary)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(y, ref, tol=2e-5):
+    """fp32 kernel vs fp64 oracle: relative to the output's scale."""
+    y = y.double().cpu()
+    ref = ref.double().cpu()
+    scale = max(1.0, ref.abs().max().item())
+    err = (y - ref).abs().max().item()
+    assert err <= tol * scale, f"max abs err {err} (scale {scale})"
+
+
+@pytest.mark.parametrize("M,K,N", [(1000, 16, 96), (777, 24, 144), (4096, 144, 24), (6272, 320, 1280),
+                                   (128, 1280, 1000), (130, 960, 160), (64, 32, 16), (6272, 160, 960),
+                                   (6272, 960, 320)])
+@pytest.mark.parametrize("act,use_res", [(1, False), (0, True), (0, False)])
+def test_pw_conv_f32(nns, M, K, N, act, use_res):
+    torch.manual_seed(M + K + N)
+    x = torch.randn(M, K, device="cuda")
+    npad, kpad = (N + 15) // 16 * 16, (K + 7) // 8 * 8
+    wt = torch.zeros(npad, kpad, device="cuda")
+    wt[:N, :K] = torch.randn(N, K, device="cuda") / K ** 0.5
+    bias = torch.randn(npad, device="cuda")
+    res = torch.randn(M, N, device="cuda") if use_res else None
+    y = torch.ops.nnsx.pw_conv(x, wt, bias, res, N, act, True)
+    assert y.dtype == torch.float32
+    ref = x.double().cpu() @ wt[:N, :K].double().cpu().t() + bias[:N].double().cpu()
+    if use_res:
+        ref = ref + res.double().cpu()
+    if act == 1:
+        ref = ref.clamp(0, 6)
+    _close(y, ref)
+
+
+def test_pw_conv_f32_identity_asymmetric(nns):
+    # A = I with an asymmetric B catches transposed fragment / k-permutation bugs exactly
+    M, K, N = 192, 64, 64
+    x = torch.arange(M * K, device="cuda", dtype=torch.float32).view(M, K).remainder(13) - 6
+    wt = torch.eye(64, device="cuda")
+    y = torch.ops.nnsx.pw_conv(x, wt, torch.zeros(64, device="cuda"), None, N, 0, True)
+    torch.testing.assert_close(y, x, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("B,H,W,C,stride,dil", [(2, 112, 112, 32, 1, 1), (3, 112, 112, 96, 2, 1), (1, 7, 7, 960, 1, 1),
+                                                (2, 15, 9, 144, 2, 1), (2, 33, 33, 320, 1, 2), (1, 65, 65, 64, 1, 4)])
+def test_dw_conv_f32(nns, B, H, W, C, stride, dil):
+    x = torch.randn(B, H, W, C, device="cuda")
+    w = torch.randn(9, C, device="cuda")
+    bias = torch.randn(C, device="cuda")
+    y = torch.ops.nnsx.dw_conv(x, w, bias, stride, 1, dil)
+    assert y.dtype == torch.float32
+    wf = w.double().cpu().view(3, 3, C).permute(2, 0, 1).unsqueeze(1)
+    ref = F.conv2d(x.double().cpu().permute(0, 3, 1, 2), wf, bias.double().cpu(), stride=stride, padding=dil,
+                   dilation=dil, groups=C).clamp(0, 6)
+    _close(y, ref.permute(0, 2, 3, 1))
+
+
+@pytest.mark.parametrize("H,W", [(224, 224), (300, 300), (57, 41)])
+def test_stem_f32_u8_and_pool(nns, H, W):
+    x = torch.randint(0, 256, (2, H, W, 3), device="cuda", dtype=torch.uint8)
+    w = torch.randn(3, 3, 3, 32, device="cuda") * 0.3
+    b = torch.randn(32, device="cuda")
+    y = torch.ops.nnsx.stem_conv_u8(x, w, b, 1, -127.5, 127.5, True)
+    assert y.dtype == torch.float32
+    xf = (x.double().cpu() - 127.5) / 127.5
+    ref = F.conv2d(xf.permute(0, 3, 1, 2), w.double().cpu().permute(3, 2, 0, 1), b.double().cpu(), stride=2,
+                   padding=1).clamp(0, 6)
+    _close(y, ref.permute(0, 2, 3, 1))
+    yf = torch.ops.nnsx.stem_conv(((x.float() - 127.5) / 127.5).contiguous(), w, b, 1, True)
+    _close(yf, ref.permute(0, 2, 3, 1))
+    p = torch.ops.nnsx.avgpool(y)
+    _close(p, y.double().cpu().mean((1, 2)))
+
+
+# every fused MobileNetV2 block (H, cin, hid, cout, stride, expand) + partial-tile shapes
+IR_F32_SHAPES = [(112, 32, 32, 16, 1, False), (112, 16, 96, 24, 2, True), (56, 24, 144, 24, 1, True),
+                 (56, 24, 144, 32, 2, True), (28, 32, 192, 32, 1, True), (28, 32, 192, 64, 2, True),
+                 (14, 64, 384, 64, 1, True), (14, 64, 384, 96, 1, True), (14, 96, 576, 96, 1, True),
+                 (21, 64, 384, 64, 1, True), (13, 96, 576, 96, 1, True), (15, 32, 192, 64, 2, True),
+                 (42, 32, 192, 32, 1, True), (40, 16, 96, 24, 2, True),
+                 (30, 24, 144, 24, 1, True), (17, 64, 384, 96, 1, True)]
+
+
+def _ir_ref64(x, we, be, wd, bd, wp, bp, stride, cout, has_expand, residual):
+    x64 = x.double().cpu()
+    cin = x.shape[-1]
+    hid = wd.shape[1]
+    h = x64
+    if has_expand:
+        h = (x64 @ we.double().cpu()[:, :cin].t() + be.double().cpu()).clamp(0, 6)
+    wdf = wd.double().cpu().view(3, 3, hid).permute(2, 0, 1).unsqueeze(1)
+    h = F.conv2d(h.permute(0, 3, 1, 2), wdf, bd.double().cpu(), stride=stride, padding=1, groups=hid).clamp(0, 6)
+    h = h.permute(0, 2, 3, 1)
+    y = h @ wp.double().cpu()[:cout].t() + bp.double().cpu()[:cout]
+    if residual:
+        y = y + x64
+    return y
+
+
+@pytest.mark.parametrize("H,cin,hid,cout,stride,has_expand", IR_F32_SHAPES)
+def test_ir_block_f32(nns, H, cin, hid, cout, stride, has_expand):
+    torch.manual_seed(H * 7 + cin + hid)
+    B = 3
+    assert torch.ops.nnsx.ir_supported_f32(stride, H, H, cin, hid, cout, has_expand)
+    x = torch.randn(B, H, H, cin, device="cuda")
+    kin = (cin + 7) // 8 * 8
+    we = torch.zeros(hid, kin, device="cuda")
+    we[:, :cin] = torch.randn(hid, cin, device="cuda") / cin ** 0.5
+    be = torch.randn(hid, device="cuda") * 0.1
+    wd = torch.randn(9, hid, device="cuda") / 3
+    bd = torch.randn(hid, device="cuda") * 0.1
+    npad = (cout + 15) // 16 * 16
+    wp = torch.zeros(npad, hid, device="cuda")
+    wp[:cout] = torch.randn(cout, hid, device="cuda") / hid ** 0.5
+    bp = torch.zeros(npad, device="cuda")
+    bp[:cout] = torch.randn(cout, device="cuda") * 0.1
+    residual = stride == 1 and cin == cout
+    y = torch.ops.nnsx.ir_block(x, we, be, wd, bd, wp, bp, stride, cout, has_expand, residual)
+    assert y.shape == (B, (H - 1) // stride + 1, (H - 1) // stride + 1, cout)
+    _close(y, _ir_ref64(x, we, be, wd, bd, wp, bp, stride, cout, has_expand, residual), tol=5e-5)
+
+
+def _agreement(f, m, n_images=256, batch=64, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    agree, worst = 0, 0.0
+    for _ in range(n_images // batch):
+        x = torch.randint(0, 256, (batch, 224, 224, 3), generator=g, dtype=torch.uint8).cuda()
+        with torch.no_grad():
+            ref = m(((x.float() - 127.5) / 127.5).permute(0, 3, 1, 2))
+            out = f(x)
+        agree += int((out.argmax(1) == ref.argmax(1)).sum())
+        worst = max(worst, ((out - ref).abs().max() / ref.abs().max()).item())
+    return agree / n_images, worst
+
+
+def test_fused_fp32_mobilenet_top1_matches_torch_fp32(nns):
+    """The benched headline engine: fp32 fused kernels vs the plain torch fp32
+    model on 256 images -- top-1 agreement >= 99.5 %."""
+    from nnstreamer_amd.models.fused import FusedMobileNetV2
+    from nnstreamer_amd.models.mobilenet_v2 import mobilenet_v2
+
+    torch.backends.cudnn.allow_tf32 = False
+    torch.backends.cuda.matmul.allow_tf32 = False
+    m = mobilenet_v2(seed=1).cuda().eval()
+    f = torch.jit.script(FusedMobileNetV2.from_reference(mobilenet_v2(seed=1), "fp32").cuda().eval())
+    agree, worst = _agreement(f, m)
+    assert agree >= 0.995, (agree, worst)
+    assert worst < 1e-3, worst
+
+
+def test_fused_bf16_mobilenet_top1_matches_torch_fp32(nns):
+    """The secondary bf16 engine: top-1 agreement with torch fp32 >= 98 %."""
+    from nnstreamer_amd.models.fused import FusedMobileNetV2
+    from nnstreamer_amd.models.mobilenet_v2 import mobilenet_v2
+
+    m = mobilenet_v2(seed=1).cuda().eval()
+    f = torch.jit.script(FusedMobileNetV2.from_reference(mobilenet_v2(seed=1), "bf16").cuda().eval())
+    agree, worst = _agreement(f, m)
+    assert agree >= 0.98, (agree, worst)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_benched_launch_string_labels_match_torch_fp32(nns, workdir, labels, precision):
+    """The exact bench.py pipeline shape (uint8 frames -> stem-normalised fused
+    model under hipGraph -> image_labeling) against torch.argmax of the plain
+    fp32 model on the same frames."""
+    import os
+
+    from nnstreamer_amd.models.export import export
+    from nnstreamer_amd.models.mobilenet_v2 import mobilenet_v2
+
+    name = "mobilenet_v2_fused_fp32" if precision == "fp32" else "mobilenet_v2_fused"
+    model = export(name, os.path.join(workdir, f"{name}.pt"), layout="nhwc")
+    B, nb = 16, 4
+    desc = (f"videotestsrc num-buffers={B * nb} pattern=snow pool-size=64 "
+            "! video/x-raw,format=RGB,width=224,height=224,framerate=0/1 "
+            f"! tee name=t t. ! queue ! tensor_converter frames-per-tensor={B} device=0 ! queue max-size-buffers=2 "
+            f"! tensor_filter framework=pytorch model={model} input=3:224:224:{B} inputtype=uint8 "
+            "accelerator=true:gpu device=0 custom=hipgraph:true ! queue max-size-buffers=4 "
+            f"! tensor_decoder mode=image_labeling option1={labels} ! tensor_sink name=sink "
+            f"t. ! queue ! tensor_converter frames-per-tensor={B} ! appsink name=raw")
+    p = nns.parse_launch(desc)
+    out = []
+    p.get_by_name("sink").connect("new-data", lambda b: out.append(b.memory(0).bytes().decode()))
+    raw = p.get_by_name("raw")
+    p.set_state("playing")
+    frames = []
+    while len(frames) < nb:
+        b = raw.pull(timeout=60)
+        assert b is not None
+        frames.append(b.memory(0).numpy("uint8").copy())
+    p.wait(timeout=120)
+    p.stop()
+    assert len(out) == nb
+    m = mobilenet_v2(seed=0).cuda().eval()  # export() uses seed 0
+    agree = total = 0
+    for labels_txt, fr in zip(out, frames):
+        x = torch.from_numpy(fr).cuda().view(B, 224, 224, 3).float()
+        with torch.no_grad():
+            ref = m(((x - 127.5) / 127.5).permute(0, 3, 1, 2)).argmax(1).tolist()
+        got = labels_txt.split("\n")
+        agree += sum(a == f"class_{i}" for a, i in zip(got, ref))
+        total += B
+    need = 1.0 if precision == "fp32" else 0.95
+    assert agree / total >= need, (agree, total)
+
+
+def test_filter_device_stats(nns, workdir, labels):
+    """tensor_filter latency / throughput / device-stamps come from HIP events
+    on the element's stream (device time), one record per invoke."""
+    import os
+
+    from nnstreamer_amd.models.export import export
+
+    model = export("mobilenet_v2_fused_fp32", os.path.join(workdir, "mbv2_f32_stats.pt"), layout="nhwc")
+    desc = ("videotestsrc num-buffers=40 pattern=snow ! video/x-raw,format=RGB,width=224,height=224,framerate=0/1 "
+            "! tensor_converter frames-per-tensor=4 device=0 "
+            f"! tensor_filter name=f framework=pytorch model={model} input=3:224:224:4 inputtype=uint8 "
+            "accelerator=true:gpu device=0 latency=1 throughput=1 device-stats=true "
+            f"! tensor_decoder mode=image_labeling option1={labels} ! tensor_sink name=sink")
+    p = nns.parse_launch(desc)
+    p.run(timeout=120)
+    f = p.get_by_name("f")
+    stamps = [tuple(int(v) for v in e.split(":")) for e in f.get_property("device-stamps").split(",") if e]
+    lat = int(f.get_property("latency"))
+    thr = int(f.get_property("throughput"))
+    p.stop()
+    assert len(stamps) == 10
+    ends = [s[0] for s in stamps]
+    assert all(b >= a for a, b in zip(ends, ends[1:])), ends
+    assert all(0 < s[1] < 1e9 for s in stamps), stamps
+    assert lat > 0 and thr > 0
