@@ -204,7 +204,9 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
                     f"! tensor_converter frames-per-tensor={B} device={dev} ! queue max-size-buffers=4 "
                     f"! edgesink {link}")
         else:
-            desc = (f"edgesrc {link} peer-rank=0 ! queue max-size-buffers=2 ! {filt}"
+            desc = (f"edgesrc {link} peer-rank=0 ! queue max-size-buffers=2 "
+                    + (f"! tensor_transform mode=arithmetic option={cfg['norm']} " if not fuse_norm else "")
+                    + f"! {filt}"
                     f"! queue max-size-buffers={a.queue} ! {cfg['decoder'].format(**files)} ! tensor_sink name=sink")
     per_step = B if cfg["per_frame"] else 1  # sink buffers per batch
     pipe = nns.parse_launch(desc)

@@ -184,7 +184,7 @@ def test_bench_posenet_multi_two_ranks_cpu():
     port = _free_port()
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-                        "--cpu", "--config", "posenet_multi", "--batch", "2", "--steps", "2", "--warmup", "1"],
+                        "--gpus", "2", "--cpu", "--config", "posenet_multi", "--batch", "2", "--steps", "2", "--warmup", "1"],
                        capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
@@ -202,7 +202,7 @@ def test_bench_deeplab_fan_three_ranks_cpu():
     port = _free_port()
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-                        "--cpu", "--config", "deeplab_fan", "--batch", "1", "--steps", "2", "--warmup", "1"],
+                        "--gpus", "3", "--cpu", "--config", "deeplab_fan", "--batch", "1", "--steps", "2", "--warmup", "1"],
                        capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
