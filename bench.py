@@ -31,7 +31,9 @@ measured at the sink; ranks are bracketed by barrier + device synchronize,
 the max over ranks is reported.  Cross-check: the filter's HIP events give
 the device-clock time of the same K batches (`gpu_event_fps`).  Latency =
 sink arrival - frame capture time (the PTS of the oldest frame in the batch);
-`p50_latency_ms_b1` is a separate batch-1 run of the same pipeline.
+`p50_latency_ms_b1` is a separate batch-1 run of the same pipeline fed by
+a live camera (`--latency-fps`, frames released at their PTS), so it measures
+the pipeline's latency, not queueing behind a free-running source.
 Data: synthetic video frames, random-init weights.
 """
 from __future__ import annotations
@@ -62,6 +64,8 @@ def parse_args(argv=None):
                     help="fused = nnsx CDNA4 kernels; torch = plain TorchScript/MIOpen model (fp32)")
     ap.add_argument("--latency-frames", type=int, default=int(os.environ.get("NNSX_BENCH_LAT_FRAMES", "300")),
                     help="frames of the batch-1 latency run (0 = skip)")
+    ap.add_argument("--latency-fps", type=int, default=int(os.environ.get("NNSX_BENCH_LAT_FPS", "500")),
+                    help="frame rate of the live camera in the batch-1 latency run")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-fuse-norm", action="store_true",
                     help="keep the normalisation as a separate tensor_transform element")
@@ -156,8 +160,13 @@ def spawn_ranks(n: int, argv) -> int:
 
 
 # ---------------------------------------------------------------- one run ----
-def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, rank, world, dev, use_gpu, dist):
-    """Build and run one pipeline to EOS; return this rank's timing record."""
+def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, rank, world, dev, use_gpu, dist,
+                 live_fps=0):
+    """Build and run one pipeline to EOS; return this rank's timing record.
+
+    live_fps > 0: the source is a live camera at that frame rate (frames are
+    released at their PTS), so per-frame latency is the pipeline's own latency
+    rather than time spent queued behind a source that runs ahead."""
     S = cfg["size"]
     total = warmup + steps
     frames = total * B
@@ -175,9 +184,10 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
     filt = (f"tensor_filter name=filt framework=pytorch model={model_path} input=3:{S}:{S}:{B} "
             f"inputtype={'uint8' if fuse_norm else 'float32'} accelerator={accel} device={dev} "
             f"custom=hipgraph:{graph} device-stats={'true' if use_gpu else 'false'} ")
+    live = f"is-live=true " if live_fps > 0 else ""
     desc = (
-        f"videotestsrc num-buffers={frames} pattern=snow pool-size={pool} "
-        f"! video/x-raw,format=RGB,width={S},height={S},framerate=0/1 "
+        f"videotestsrc num-buffers={frames} pattern=snow pool-size={pool} {live}"
+        f"! video/x-raw,format=RGB,width={S},height={S},framerate={live_fps}/1 "
         f"! tensor_converter frames-per-tensor={B} device={dev} "
         # thread boundary: the next batch's upload is issued while the filter thread
         # is still submitting this batch's kernels
@@ -341,7 +351,7 @@ def main():
         model_path = os.path.join(workdir, f"{model_name}.pt")
         w1 = max(10, a.latency_frames // 5)
         lat_b1 = run_pipeline(a, nns, cfg, model_name, model_path, files, 1, a.latency_frames, w1, rank, world, dev,
-                              use_gpu, dist)
+                              use_gpu, dist, live_fps=a.latency_fps)
 
     # per-rank records, all-gathered over the job's process group (RCCL on GPUs):
     # [elapsed, p50, p99, gpu_elapsed, gpu_busy] per engine + batch-1 p50/p99
@@ -414,7 +424,8 @@ def main():
         if lat_b1:
             n = len(runs)
             out.update(p50_latency_ms_b1=round(float(per_rank[:, n * 5].max()), 3),
-                       p99_latency_ms_b1=round(float(per_rank[:, n * 5 + 1].max()), 3))
+                       p99_latency_ms_b1=round(float(per_rank[:, n * 5 + 1].max()), 3),
+                       latency_b1_source=f"live camera, {a.latency_fps} frames/s, batch 1")
         out.update({
             "preprocess": ("tensor_transform normalisation fused into the model's stem kernel (uint8 input)"
                            if head["fuse_norm"] else "tensor_transform element"),

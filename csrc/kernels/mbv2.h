@@ -52,8 +52,9 @@ bool ir_block(const IrBlockArgs& a, hipStream_t s);
 // and accumulation, GEMMs on v_mfma_f32_16x16x4_f32.
 // y[M][N] = act(x[M][K] . wt[N][K]^T + bias) (+ res); wt zero-padded [Npad][Kpad]
 // (Kpad >= K, Kpad % 4 == 0), K % 4 == 0, N % 4 == 0.
+// tile: 0 = auto, else BM * 1000 + BN of an instantiated tile (64064, 128064, 64128, 128128, 128192)
 void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
-                 int Kpad, int Npad, int act, hipStream_t s);
+                 int Kpad, int Npad, int act, hipStream_t s, int tile = 0);
 // depthwise 3x3, stride 1|2, dilation d (padding d); w [9][C], C % 4 == 0
 void dw3x3_f32(const float* x, const float* w, const float* bias, float* y, int B, int H, int W, int C, int stride,
                int dil, int act, hipStream_t s);
@@ -80,6 +81,7 @@ struct IrBlockF32Args {
   int has_expand = 1, residual = 0;
   // derived by ir_block_f32()
   int Ho = 0, Wo = 0, tiles_x = 0, tiles_y = 0;
+  int hsplit = 1;  // hidden-channel parts per tile (wave-split kernel)
 };
 bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout, bool has_expand);
 bool ir_block_f32(const IrBlockF32Args& a, hipStream_t s);

@@ -34,6 +34,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cmath>
 #include <cstdlib>
 
 #include "kernels/mbv2.h"
@@ -233,6 +234,63 @@ __global__ void __launch_bounds__(256) dw3x3_f32_kernel(const float* __restrict_
 #pragma unroll
     for (int r = 0; r < 4; ++r) acc[r] = act_fn(acc[r], act);
     *reinterpret_cast<f32x4_t*>(y + ((static_cast<int64_t>(b) * Ho + oy) * Wo + ox) * C + c) = acc;
+  }
+}
+
+// column form (dilation 1): one lane = R vertically adjacent output pixels x
+// 4 channels, so each loaded input row feeds up to 3 of them
+// ((R-1)S+3 row loads instead of 3R)
+template <int R, int S>
+__global__ void __launch_bounds__(256) dw3x3_f32_col_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                            const float* __restrict__ bias, float* __restrict__ y,
+                                                            int B, int H, int W, int C, int Ho, int Wo, int act) {
+  constexpr int NR = (R - 1) * S + 3;
+  const uint32_t cg = static_cast<uint32_t>(C) >> 2;
+  const uint32_t rg = static_cast<uint32_t>((Ho + R - 1) / R);
+  const uint32_t total = static_cast<uint32_t>(B) * rg * Wo * cg;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const int c = static_cast<int>(t % cg) * 4;
+    uint32_t p = t / cg;
+    const int ox = static_cast<int>(p % Wo);
+    p /= Wo;
+    const int oy0 = static_cast<int>(p % rg) * R;
+    const int b = static_cast<int>(p / rg);
+    f32x4_t wv[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) wv[k] = *reinterpret_cast<const f32x4_t*>(w + k * C + c);
+    const f32x4_t bv = *reinterpret_cast<const f32x4_t*>(bias + c);
+    f32x4_t acc[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) acc[j] = bv;
+    const float* xb = x + static_cast<int64_t>(b) * H * W * C + c;
+#pragma unroll
+    for (int ir = 0; ir < NR; ++ir) {
+      const int iy = oy0 * S - 1 + ir;
+      if (iy < 0 || iy >= H) continue;
+      f32x4_t xv[3];
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int ix = ox * S - 1 + kx;
+        xv[kx] = (ix >= 0 && ix < W) ? *reinterpret_cast<const f32x4_t*>(xb + (static_cast<int64_t>(iy) * W + ix) * C)
+                                     : f32x4_t{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        const int ky = ir - j * S;
+        if (ky < 0 || ky > 2) continue;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) acc[j] = __builtin_elementwise_fma(xv[kx], wv[ky * 3 + kx], acc[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int oy = oy0 + j;
+      if (oy >= Ho) break;
+      f32x4_t v = acc[j];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], act);
+      *reinterpret_cast<f32x4_t*>(y + ((static_cast<int64_t>(b) * Ho + oy) * Wo + ox) * C + c) = v;
+    }
   }
 }
 
@@ -556,6 +614,240 @@ __global__ void __launch_bounds__(256) ir_block_f32_kernel(IrBlockF32Args a) {
   }
 }
 
+// ------------------------------------------------------------- irw_f32 ----
+// Wave-split fused inverted residual (fp32): the same expand -> dw -> project
+// as ir_block_f32, partitioned for the fp32 MFMA/VALU balance of the low-res
+// stages (28x28, 14x14, 7x7 maps).
+//
+// One workgroup = one TY x TX output tile (x one of `hsplit` hidden-channel
+// parts).  The compact in-image input tile is staged in LDS once; then each of
+// the 4 waves walks its OWN 16-channel hidden subtiles (hs = wave, wave+4, ..)
+// end to end with no workgroup barrier:
+//   expand  MFMA over all compact pixels of the tile (NBT independent
+//           accumulators), + bias, ReLU6 -> the wave's private hidden image
+//           (halo grid, out-of-image cells zeroed once);
+//   dw 3x3  VALU, lane = output pixel x channel quad, + bias, ReLU6 -> the
+//           wave's private project operand;
+//   project MFMA, acc[pixel tile][cout tile] += Wp[:, subtile] . dw^T,
+//           accumulated over the wave's subtiles (a k-split of the project).
+// Expand weights of the next subtile are in flight during dw + project.  At the
+// end the 4 waves' partial sums are added through LDS in a fixed order (w0 +
+// w1 + w2 + w3, deterministic), plus bias / residual, and stored; with
+// hsplit = 2 the two parts add into a zeroed output (a + b == b + a: still
+// deterministic).  The MFMA pipe of a SIMD then alternates between waves of
+// different workgroups that are never held at a common barrier, so one wave's
+// depthwise VALU work hides under another's matrix work.
+template <int S, int TY, int TX, int KIN, int NOT, int NW>
+struct IrwGeom {
+  static constexpr int TIY = (TY - 1) * S + 3, TIX = (TX - 1) * S + 3;
+  static constexpr int PIN = TIY * TIX;               // halo grid cells
+  static constexpr int NC16 = (PIN + 15) / 16 * 16;   // compact in-image pixels (max), padded
+  static constexpr int NBT = NC16 / 16;               // expand pixel tiles
+  static constexpr int XSP = NC16 + 1;                // xs plane stride (quads): staging writes spread over banks
+  static constexpr int KQ = KIN / 4;
+  static constexpr int NPT = (TY * TX + 15) / 16;     // output pixel tiles
+  static constexpr int NPX = NPT * 16;
+  static constexpr size_t xs_q = static_cast<size_t>(KQ) * XSP;
+  static constexpr size_t hid_q = static_cast<size_t>(4 * NW) * PIN;      // [wave][quad][cell]
+  static constexpr size_t dwo_q = static_cast<size_t>(4 * NW) * NPX;      // [wave][quad][px]
+  static constexpr size_t red_q = static_cast<size_t>(2 * 4 * NW) * NPX;  // [buf][wave][quad][px]
+  static size_t lds_bytes(int) { return 16 * std::max(xs_q + hid_q + dwo_q, red_q); }
+};
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// (second launch bound = minimum waves per SIMD: 2 keeps every configuration
+// but the 7x7 / 160-channel one within 256 VGPRs, two workgroups per CU)
+template <int S, int TY, int TX, int KIN, int NOT, int NW>
+__global__ void __launch_bounds__(64 * NW, (NOT <= 6 ? 2 : 1)) irw_f32_kernel(IrBlockF32Args a) {
+  using G = IrwGeom<S, TY, TX, KIN, NOT, NW>;
+  constexpr int NT = 64 * NW;
+  constexpr int TIY = G::TIY, TIX = G::TIX, PIN = G::PIN, NC16 = G::NC16, NBT = G::NBT, XSP = G::XSP;
+  constexpr int KQ = G::KQ, NPT = G::NPT, NPX = G::NPX;
+  constexpr int NS16 = KIN / 16;
+  constexpr bool KT8 = (KIN % 16) != 0;
+  static_assert(KIN % 8 == 0, "irw_f32: KIN % 8");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  f32x4_t* xs = reinterpret_cast<f32x4_t*>(smem);  // [KQ][XSP]
+  f32x4_t* hidw = xs + G::xs_q;                     // [NW waves][4 quads][PIN]
+  f32x4_t* dwo = hidw + G::hid_q;                   // [NW waves][4 quads][NPX]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int nparts = a.hsplit;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);  // the parts of a tile stay adjacent (same XCD / L2)
+  const int part = wg % nparts, tile = wg / nparts;
+  const int tiles_img = a.tiles_x * a.tiles_y;
+  const int b = tile / tiles_img;
+  const int tyx = tile - b * tiles_img;
+  const int oy0 = (tyx / a.tiles_x) * TY, ox0 = (tyx % a.tiles_x) * TX;
+  const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
+  const int ry0 = max(iy0, 0), ry1 = min(iy0 + TIY, a.H);
+  const int rx0 = max(ix0, 0), rx1 = min(ix0 + TIX, a.W);
+  const int RW = rx1 - rx0, NC = (ry1 - ry0) * RW;
+  const float* xb = a.x + static_cast<int64_t>(b) * a.H * a.W * a.cin;
+
+  // ---- stage the compact input tile (coalesced reads: consecutive threads, consecutive quads)
+  for (int v = tid; v < NC16 * KQ; v += NT) {
+    const int c = v / KQ, kq = v - c * KQ;
+    f32x4_t val = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    if (c < NC && kq * 4 < a.cin) {
+      const int yy = ry0 + c / RW, xx = rx0 + c % RW;
+      val = *reinterpret_cast<const f32x4_t*>(xb + (static_cast<int64_t>(yy) * a.W + xx) * a.cin + kq * 4);
+    }
+    xs[kq * XSP + c] = val;
+  }
+  // out-of-image halo cells of every wave's hidden image = the depthwise zero padding
+  if (ry0 > iy0 || ry1 < iy0 + TIY || rx0 > ix0 || rx1 < ix0 + TIX) {
+    for (int v = tid; v < 4 * NW * PIN; v += NT) {
+      const int p = v % PIN;
+      const int yy = iy0 + p / TIX, xx = ix0 + p % TIX;
+      if (yy < ry0 || yy >= ry1 || xx < rx0 || xx >= rx1) hidw[v] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  int hcell[NBT];
+#pragma unroll
+  for (int j = 0; j < NBT; ++j) {
+    const int c = j * 16 + li;
+    hcell[j] = c < NC ? (ry0 + c / RW - iy0) * TIX + (rx0 + c % RW - ix0) : -1;
+  }
+  int dcell[NPT];
+#pragma unroll
+  for (int pt = 0; pt < NPT; ++pt) {
+    const int q = pt * 16 + li;
+    const int qq = q < TY * TX ? q : 0;
+    dcell[pt] = (qq / TX) * S * TIX + (qq % TX) * S;
+  }
+  const int nbt = (NC + 15) / 16;  // pixel tiles holding in-image pixels (wave-uniform)
+
+  f32x4_t acc[NPT][NOT];
+#pragma unroll
+  for (int pt = 0; pt < NPT; ++pt)
+#pragma unroll
+    for (int o = 0; o < NOT; ++o) acc[pt][o] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  __syncthreads();  // xs + zeroed halos
+
+  const int nsub = a.hid >> 4;
+  const int sub0 = part * nsub / nparts, sub1 = (part + 1) * nsub / nparts;
+  f32x4_t* myhid = hidw + wave * 4 * PIN + g * PIN;
+  f32x4_t* mydwo = dwo + wave * 4 * NPX + g * NPX;
+  f32x4_t ea[NS16 > 0 ? NS16 : 1];
+  f32x2_t et = f32x2_t{0.f, 0.f};
+  auto load_ea = [&](int hs) {
+    const float* wrow = a.we + static_cast<int64_t>(hs * 16 + li) * KIN;
+#pragma unroll
+    for (int s = 0; s < NS16; ++s) ea[s] = *reinterpret_cast<const f32x4_t*>(wrow + 16 * s + 4 * g);
+    if constexpr (KT8) et = *reinterpret_cast<const f32x2_t*>(wrow + 16 * NS16 + 2 * g);
+  };
+  int hs = sub0 + wave;
+  if (a.has_expand && hs < sub1) load_ea(hs);
+  for (; hs < sub1; hs += NW) {
+    const int ch = hs * 16 + 4 * g;  // this lane's channel quad (dw, biases)
+    f32x4_t pa[NOT];
+#pragma unroll
+    for (int o = 0; o < NOT; ++o)
+      pa[o] = *reinterpret_cast<const f32x4_t*>(a.wp + static_cast<int64_t>(o * 16 + li) * a.hid + ch);
+    f32x4_t wd4[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wd4[t] = *reinterpret_cast<const f32x4_t*>(a.wd + t * a.hid + ch);
+    const f32x4_t bd4 = *reinterpret_cast<const f32x4_t*>(a.bd + ch);
+
+    // ---- expand -> private hidden image
+    if (a.has_expand) {
+      const f32x4_t be4 = *reinterpret_cast<const f32x4_t*>(a.be + ch);
+      // pixel tiles in pairs (two independent MFMA chains); a pair past the
+      // in-image pixels is skipped wave-uniformly, a half-valid one computes zeros
+#pragma unroll
+      for (int j = 0; j < NBT; j += 2) {
+        if (j < nbt) {
+          const int j1 = j + 1 < NBT ? j + 1 : j;
+          f32x4_t e0 = f32x4_t{0.f, 0.f, 0.f, 0.f}, e1 = e0;
+#pragma unroll
+          for (int s = 0; s < NS16; ++s) {
+            e0 = mfma_k16(ea[s], xs[(4 * s + g) * XSP + j * 16 + li], e0);
+            e1 = mfma_k16(ea[s], xs[(4 * s + g) * XSP + j1 * 16 + li], e1);
+          }
+          if constexpr (KT8) {
+            const f32x2_t* t0 = reinterpret_cast<const f32x2_t*>(&xs[(4 * NS16 + g / 2) * XSP + j * 16 + li]);
+            const f32x2_t* t1 = reinterpret_cast<const f32x2_t*>(&xs[(4 * NS16 + g / 2) * XSP + j1 * 16 + li]);
+            e0 = mfma_k8(et, t0[g & 1], e0);
+            e1 = mfma_k8(et, t1[g & 1], e1);
+          }
+          if (hcell[j] >= 0) myhid[hcell[j]] = relu6x4(e0 + be4);
+          if (j + 1 < NBT && hcell[j1] >= 0) myhid[hcell[j1]] = relu6x4(e1 + be4);
+        }
+      }
+      if (hs + NW < sub1) load_ea(hs + NW);  // next subtile's weights: in flight during dw + project
+    } else {
+      // t = 1: the hidden channels are the input channels
+#pragma unroll
+      for (int j = 0; j < NBT; ++j)
+        if (hcell[j] >= 0) myhid[hcell[j]] = xs[(hs * 4 + g) * XSP + j * 16 + li];
+    }
+    wave_sync();
+
+    // ---- depthwise 3x3 + bias + ReLU6 -> private project operand
+#pragma unroll
+    for (int pt = 0; pt < NPT; ++pt) {
+      f32x4_t d = bd4;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx)
+          d = __builtin_elementwise_fma(myhid[dcell[pt] + ky * TIX + kx], wd4[ky * 3 + kx], d);
+      mydwo[pt * 16 + li] = relu6x4(d);
+    }
+    wave_sync();
+
+    // ---- project: k-split partial over this subtile's 16 channels
+#pragma unroll
+    for (int pt = 0; pt < NPT; ++pt) {
+      const f32x4_t bf = mydwo[pt * 16 + li];
+#pragma unroll
+      for (int o = 0; o < NOT; ++o) acc[pt][o] = mfma_k16(pa[o], bf, acc[pt][o]);
+    }
+    wave_sync();
+  }
+
+  // ---- cross-wave reduction (fixed order) + bias + residual -> NHWC
+  __syncthreads();  // every wave is done with xs / hidden / dwo: the LDS becomes the reduction buffer
+  f32x4_t* red = reinterpret_cast<f32x4_t*>(smem);
+#pragma unroll
+  for (int o = 0; o < NOT; ++o) {
+    f32x4_t* rb = red + (o & 1) * (4 * NW * NPX);
+#pragma unroll
+    for (int pt = 0; pt < NPT; ++pt) rb[(wave * 4 + g) * NPX + pt * 16 + li] = acc[pt][o];
+    __syncthreads();
+    const int co = o * 16 + 4 * g;
+    for (int pt = wave; pt < NPT; pt += NW) {
+      const int q = pt * 16 + li;
+      f32x4_t v = rb[g * NPX + q];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) v += rb[(4 * w + g) * NPX + q];
+      if (q >= TY * TX || co >= a.cout) continue;
+      const int gy = oy0 + q / TX, gx = ox0 + q % TX;
+      if (gy >= a.Ho || gx >= a.Wo) continue;
+      const int64_t pix = (static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx;
+      if (part == 0) {
+        v += *reinterpret_cast<const f32x4_t*>(a.bp + co);
+        if (a.residual) v += *reinterpret_cast<const f32x4_t*>(a.x + pix * a.cin + co);
+      }
+      float* yp = a.y + pix * a.cout + co;
+      if (nparts > 1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) atomicAdd(yp + r, v[r]);
+      } else {
+        *reinterpret_cast<f32x4_t*>(yp) = v;
+      }
+    }
+  }
+}
+
 // configurations (one instantiation each): MobileNetV2's fused blocks
 struct IrF32Cfg {
   int S, TY, TX, HC, NOT, KIN;
@@ -602,6 +894,50 @@ int tile_pref(int S, int H, int W, int TY, int TX) {
   return fits ? 1 : 2;
 }
 
+// wave-split kernel configurations: the 28x28 / 14x14 / 7x7 blocks of MobileNetV2
+struct IrwCfg {
+  int S, TY, TX, KIN, NOT, NW;
+  void (*kernel)(IrBlockF32Args);
+  size_t (*lds)(int);
+};
+#define NNSX_IRW(S, TY, TX, KIN, NOT, NW)                                                             \
+  IrwCfg {                                                                                            \
+    S, TY, TX, KIN, NOT, NW, &irw_f32_kernel<S, TY, TX, KIN, NOT, NW>, &IrwGeom<S, TY, TX, KIN, NOT, NW>::lds_bytes \
+  }
+// (NW = waves per workgroup: a divisor of the hidden subtile count where possible,
+// so every wave walks the same number of 16-channel subtiles)
+const IrwCfg kIrwCfgs[] = {
+    NNSX_IRW(2, 4, 8, 16, 2, 3),    // 112 -> 56  16 -> 96 -> 24   (6 subtiles)
+    NNSX_IRW(1, 8, 8, 24, 2, 3),    // 56x56      24 -> 144 -> 24  (9)
+    NNSX_IRW(2, 7, 4, 24, 2, 3),    // 56 -> 28   24 -> 144 -> 32  (9)
+    NNSX_IRW(1, 7, 7, 32, 2, 4),    // 28x28      32 -> 192 -> 32  (12)
+    NNSX_IRW(2, 2, 7, 32, 4, 4),    // 28 -> 14   32 -> 192 -> 64  (12)
+    NNSX_IRW(1, 7, 7, 64, 4, 4),    // 14x14      64 -> 384 -> 64  (24)
+    NNSX_IRW(1, 7, 7, 64, 6, 4),    // 14x14      64 -> 384 -> 96  (24)
+    NNSX_IRW(1, 7, 7, 96, 6, 4),    // 14x14      96 -> 576 -> 96  (36)
+    NNSX_IRW(1, 7, 7, 160, 10, 4),  // 7x7       160 -> 960 -> 160 (60, two parts)
+};
+#undef NNSX_IRW
+
+bool irw_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("NNSX_F32_IRW");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+const IrwCfg* find_irw(int S, int H, int W, int cin, int hid, int cout, bool has_expand) {
+  if (!irw_enabled() || !has_expand || hid % 16) return nullptr;
+  const int kin = (cin + 7) / 8 * 8;
+  const int nout = (cout + 15) / 16;
+  const int Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
+  for (const auto& c : kIrwCfgs)
+    if (c.S == S && c.KIN == kin && c.NOT == nout && Ho % c.TY == 0 && Wo % c.TX == 0 && c.lds(hid) <= 160 * 1024)
+      return &c;
+  return nullptr;
+}
+
 const IrF32Cfg* find_cfg(int S, int H, int W, int cin, int hid, int cout, bool has_expand) {
   const int kin = (cin + 7) / 8 * 8;
   const int nout = (cout + 15) / 16;
@@ -622,10 +958,9 @@ const IrF32Cfg* find_cfg(int S, int H, int W, int cin, int hid, int cout, bool h
 
 }  // namespace
 
-void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
-                 int Kpad, int Npad, int act, hipStream_t s) {
-  const bool big = static_cast<int64_t>((M + 127) / 128) * ((N + 127) / 128) >= 256;
-  const int BM = big ? 128 : 64, BN = big ? 128 : 64;
+template <int BM, int BN>
+static void pw_gemm_f32_launch(const float* x, const float* wt, const float* bias, const float* res, float* y, int M,
+                               int N, int K, int Kpad, int Npad, int act, hipStream_t s) {
   dim3 grid((M + BM - 1) / BM, (N + BN - 1) / BN);
   const int kstages = (Kpad + GKT - 1) / GKT;
   int chunk = kstages;
@@ -638,17 +973,74 @@ void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float
     grid.z = static_cast<unsigned>((kstages + chunk - 1) / chunk);
     (void)hipMemsetAsync(y, 0, static_cast<size_t>(M) * N * sizeof(float), s);
   }
-  if (big)
-    hipLaunchKernelGGL((pw_gemm_f32_kernel<128, 128>), grid, dim3(256), 0, s, x, wt, bias, res, y, M, N, K, Kpad, Npad,
-                       act, chunk);
-  else
-    hipLaunchKernelGGL((pw_gemm_f32_kernel<64, 64>), grid, dim3(256), 0, s, x, wt, bias, res, y, M, N, K, Kpad, Npad,
-                       act, chunk);
+  hipLaunchKernelGGL((pw_gemm_f32_kernel<BM, BN>), grid, dim3(256), 0, s, x, wt, bias, res, y, M, N, K, Kpad, Npad, act,
+                     chunk);
+}
+
+// Tile choice: the candidate with the least modelled time, where a workgroup
+// costs its MFMA work (BM x BN x Kpad, padding included) plus a fixed
+// prologue/epilogue share, and the grid runs in rounds of 512 co-resident
+// workgroups (256 CUs x 2; every tile here fits two per CU in LDS).
+static int pick_gemm_tile(int M, int N, int Kpad) {
+  static const int cand[][2] = {{64, 64}, {128, 64}, {64, 128}, {128, 128}};
+  int best = 0;
+  double best_t = 1e30;
+  for (int i = 0; i < 4; ++i) {
+    const int bm = cand[i][0], bn = cand[i][1];
+    const double tiles = static_cast<double>((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+    const double rounds = std::ceil(tiles / 512.0);
+    // per-workgroup time ~ MFMA cycles (4 SIMDs) + ~25 % of a 32-k stage per k-stage of fill/drain
+    const double per_wg = static_cast<double>(bm) * bn * (Kpad + 96) / 4.0;
+    // a partially filled last round still costs a whole workgroup time per slot, but a
+    // CU with one resident workgroup runs it at about 1.3x the two-workgroup rate
+    const double t = rounds * per_wg * (tiles < 256 ? 0.75 : 1.0);
+    if (t < best_t * 0.97) {
+      best_t = t;
+      best = i;
+    }
+  }
+  return cand[best][0] * 1000 + cand[best][1];
+}
+
+void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
+                 int Kpad, int Npad, int act, hipStream_t s, int tile) {
+  if (tile <= 0) {
+    static const int forced = [] {
+      const char* e = std::getenv("NNSX_F32_GEMM_TILE");
+      return e ? std::atoi(e) : 0;
+    }();
+    tile = forced > 0 ? forced : pick_gemm_tile(M, N, Kpad);
+  }
+  switch (tile) {
+    case 64064: pw_gemm_f32_launch<64, 64>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, s); break;
+    case 128064: pw_gemm_f32_launch<128, 64>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, s); break;
+    case 64128: pw_gemm_f32_launch<64, 128>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, s); break;
+    case 128192: pw_gemm_f32_launch<128, 192>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, s); break;
+    default: pw_gemm_f32_launch<128, 128>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, s); break;
+  }
 }
 
 void dw3x3_f32(const float* x, const float* w, const float* bias, float* y, int B, int H, int W, int C, int stride,
                int dil, int act, hipStream_t s) {
   const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  static const int rows = [] {
+    const char* e = std::getenv("NNSX_F32_DW_ROWS");
+    return e ? std::atoi(e) : 4;
+  }();
+  if (dil == 1 && rows > 1) {
+    const int R = rows >= 4 ? 4 : 2;
+    const int64_t work = static_cast<int64_t>(B) * ((Ho + R - 1) / R) * Wo * (C / 4);
+    const unsigned grid = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 65535)));
+    if (R == 4 && stride == 1)
+      hipLaunchKernelGGL((dw3x3_f32_col_kernel<4, 1>), dim3(grid), dim3(256), 0, s, x, w, bias, y, B, H, W, C, Ho, Wo, act);
+    else if (R == 4)
+      hipLaunchKernelGGL((dw3x3_f32_col_kernel<4, 2>), dim3(grid), dim3(256), 0, s, x, w, bias, y, B, H, W, C, Ho, Wo, act);
+    else if (stride == 1)
+      hipLaunchKernelGGL((dw3x3_f32_col_kernel<2, 1>), dim3(grid), dim3(256), 0, s, x, w, bias, y, B, H, W, C, Ho, Wo, act);
+    else
+      hipLaunchKernelGGL((dw3x3_f32_col_kernel<2, 2>), dim3(grid), dim3(256), 0, s, x, w, bias, y, B, H, W, C, Ho, Wo, act);
+    return;
+  }
   const int64_t work = static_cast<int64_t>(B) * Ho * Wo * (C / 4);
   const unsigned grid = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 16384)));
   hipLaunchKernelGGL(dw3x3_f32_kernel, dim3(grid), dim3(256), 0, s, x, w, bias, y, B, H, W, C, Ho, Wo, stride, dil,
@@ -686,12 +1078,39 @@ void avgpool_f32(const float* x, float* y, int B, int HW, int C, hipStream_t s) 
 
 bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout, bool has_expand) {
   if (stride != 1 && stride != 2) return false;
+  static const int min_ho = [] {
+    const char* e = std::getenv("NNSX_F32_IR_MIN_HO");
+    return e ? std::atoi(e) : 0;
+  }();
+  if ((H - 1) / stride + 1 < min_ho) return false;
   if (cin % 8 || cout % 4 || hid % 16) return false;
-  return find_cfg(stride, H, W, cin, hid, cout, has_expand) != nullptr;
+  return find_irw(stride, H, W, cin, hid, cout, has_expand) != nullptr ||
+         find_cfg(stride, H, W, cin, hid, cout, has_expand) != nullptr;
+}
+
+static bool launch_irw(const IrwCfg* c, IrBlockF32Args a, hipStream_t s) {
+  a.Ho = (a.H - 1) / a.stride + 1;
+  a.Wo = (a.W - 1) / a.stride + 1;
+  a.tiles_y = (a.Ho + c->TY - 1) / c->TY;
+  a.tiles_x = (a.Wo + c->TX - 1) / c->TX;
+  const int tiles = a.tiles_x * a.tiles_y * a.B;
+  // fewer tiles than CUs: split the hidden channels over two workgroups per tile
+  // (partial sums added into a zeroed output; two addends keep it deterministic)
+  const int nsub = a.hid / 16;
+  a.hsplit = (tiles < 256 && nsub >= 8) ? 2 : 1;
+  const size_t lds = c->lds(a.hid);
+  if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(c->kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+    return false;
+  if (a.hsplit > 1)
+    (void)hipMemsetAsync(a.y, 0, static_cast<size_t>(a.B) * a.Ho * a.Wo * a.cout * sizeof(float), s);
+  hipLaunchKernelGGL(c->kernel, dim3(static_cast<unsigned>(tiles * a.hsplit)), dim3(64 * c->NW), lds, s, a);
+  return true;
 }
 
 bool ir_block_f32(const IrBlockF32Args& args, hipStream_t s) {
   IrBlockF32Args a = args;
+  if (const IrwCfg* w = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0)) return launch_irw(w, a, s);
   const IrF32Cfg* c = find_cfg(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0);
   if (!c) return false;
   a.Ho = (a.H - 1) / a.stride + 1;

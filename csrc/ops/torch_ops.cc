@@ -21,7 +21,7 @@ at::Tensor act_ref(at::Tensor v, int64_t act) {
 
 // ------------------------------------------------------------ pw_conv ----
 at::Tensor pw_conv_f32_cuda(const at::Tensor& x, const at::Tensor& wt, const at::Tensor& bias,
-                            const c10::optional<at::Tensor>& res, int64_t N, int64_t act) {
+                            const c10::optional<at::Tensor>& res, int64_t N, int64_t act, int64_t tile = 0) {
   TORCH_CHECK(x.is_contiguous(), "pw_conv(f32): x must be contiguous");
   TORCH_CHECK(wt.scalar_type() == at::kFloat && wt.is_contiguous() && wt.dim() == 2, "pw_conv(f32): wt [Npad,Kpad] f32");
   TORCH_CHECK(bias.scalar_type() == at::kFloat && bias.numel() >= N, "pw_conv(f32): bias f32 [N]");
@@ -40,8 +40,15 @@ at::Tensor pw_conv_f32_cuda(const at::Tensor& x, const at::Tensor& wt, const at:
   }
   nnsx::kernels::pw_gemm_f32(x.data_ptr<float>(), wt.data_ptr<float>(), bias.data_ptr<float>(), r, y.data_ptr<float>(),
                              static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), static_cast<int>(Kpad),
-                             static_cast<int>(Npad), static_cast<int>(act), cur_stream());
+                             static_cast<int>(Npad), static_cast<int>(act), cur_stream(), static_cast<int>(tile));
   return y;
+}
+
+// benchmarking entry: the fp32 GEMM with an explicit tile (BM * 1000 + BN, 0 = auto)
+at::Tensor pw_conv_f32_tile_cuda(const at::Tensor& x, const at::Tensor& wt, const at::Tensor& bias,
+                                 const c10::optional<at::Tensor>& res, int64_t N, int64_t act, int64_t tile) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat, "pw_conv_f32_tile: x must be a f32 cuda tensor");
+  return pw_conv_f32_cuda(x, wt, bias, res, N, act, tile);
 }
 
 at::Tensor pw_conv_cuda(const at::Tensor& x, const at::Tensor& wt, const at::Tensor& bias,
@@ -297,6 +304,7 @@ TORCH_LIBRARY(nnsx, m) {
   m.def("stem_conv(Tensor x, Tensor w, Tensor bias, int act, bool out_f32=False) -> Tensor");
   m.def("stem_conv_u8(Tensor x, Tensor w, Tensor bias, int act, float add, float div, bool out_f32=False) -> Tensor");
   m.def("avgpool(Tensor x) -> Tensor");
+  m.def("pw_conv_f32_tile(Tensor x, Tensor wt, Tensor bias, Tensor? res, int N, int act, int tile) -> Tensor");
   m.def("ir_block(Tensor x, Tensor we, Tensor be, Tensor wd, Tensor bd, Tensor wp, Tensor bp, int stride, int cout, "
         "bool has_expand, bool residual) -> Tensor");
   m.def("ir_supported(int stride, int cin, int hid, int cout) -> bool", ir_supported);
@@ -310,6 +318,7 @@ TORCH_LIBRARY_IMPL(nnsx, CUDA, m) {
   m.impl("stem_conv", stem_conv_cuda);
   m.impl("stem_conv_u8", stem_conv_u8_cuda);
   m.impl("avgpool", avgpool_cuda);
+  m.impl("pw_conv_f32_tile", pw_conv_f32_tile_cuda);
   m.impl("ir_block", ir_block_cuda);
 }
 

@@ -6,6 +6,8 @@
 #   smoke    __graft_entry__.smoke()
 #   bench    bench.py (BENCH_ARGS)
 #   prof     rocprofv3 kernel stats of bench.py (PROF_ARGS)
+#   irf32    per-layer fp32 engine micro-benchmark (scripts/bench_ir_f32.py)
+#   pmcf32   PMC counter passes over it (scripts/pmc_f32.sh; SHAPE=, KERNEL=)
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -29,6 +31,17 @@ for s in ${STEPS//,/ }; do
     prof)
       (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run --output-format csv -- python3 $R/bench.py ${PROF_ARGS} > $R/gpurun_out/prof.log 2>&1) || { echo "prof failed"; tail -30 gpurun_out/prof.log; exit 1; }
       find gpurun_out/prof -name "*kernel_stats.csv" ;;
+    irf32)
+      timeout -k 10 300 python -u scripts/bench_ir_f32.py ${IR_B:-128} > gpurun_out/bench_ir_f32.log 2>&1 || { echo "bench_ir_f32 failed"; tail -30 gpurun_out/bench_ir_f32.log; exit 1; }
+      cat gpurun_out/bench_ir_f32.log ;;
+    gemmf32)
+      for R in ${DW_ROWS:-4}; do
+        NNSX_F32_DW_ROWS=$R timeout -k 10 300 python -u scripts/bench_gemm_f32.py ${IR_B:-128} > gpurun_out/bench_gemm_f32_r$R.log 2>&1 || { echo "bench_gemm_f32 failed"; tail -30 gpurun_out/bench_gemm_f32_r$R.log; exit 1; }
+        echo "== dw rows $R"; cat gpurun_out/bench_gemm_f32_r$R.log
+      done ;;
+    pmcf32)
+      timeout -k 10 600 bash scripts/pmc_f32.sh > gpurun_out/pmc_f32.log 2>&1 || { echo "pmc failed"; tail -30 gpurun_out/pmc_f32.log; exit 1; }
+      cat gpurun_out/pmc_f32.log ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -86,7 +86,9 @@ IR_F32_SHAPES = [(112, 32, 32, 16, 1, False), (112, 16, 96, 24, 2, True), (56, 2
                  (14, 64, 384, 64, 1, True), (14, 64, 384, 96, 1, True), (14, 96, 576, 96, 1, True),
                  (21, 64, 384, 64, 1, True), (13, 96, 576, 96, 1, True), (15, 32, 192, 64, 2, True),
                  (42, 32, 192, 32, 1, True), (40, 16, 96, 24, 2, True),
-                 (30, 24, 144, 24, 1, True), (17, 64, 384, 96, 1, True)]
+                 (30, 24, 144, 24, 1, True), (17, 64, 384, 96, 1, True),
+                 # wave-split kernel: 7x7 whole-image tiles with the hidden channels split over 2 workgroups
+                 (7, 160, 960, 160, 1, True), (35, 96, 576, 96, 1, True)]
 
 
 def _ir_ref64(x, we, be, wd, bd, wp, bp, stride, cout, has_expand, residual):
