@@ -84,6 +84,26 @@ struct IrBlockF32Args {
   int hsplit = 1;  // hidden-channel parts per tile (wave-split kernel)
 };
 bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout, bool has_expand);
+
+// stem (3x3/2 conv 3 -> 32 on the uint8 frame, normalised as (x + add) / div,
+// + ReLU6) fused with an expand-free inverted residual 32 -> 32 -> 16
+// (dw 3x3 + ReLU6, project).  ws [3][3][3][32], bs [32], wd [9][32], bd [32],
+// wp [16][32], bp [16]; y [B][Ho][Wo][16], Ho = (H-1)/2+1.
+struct StemIr1F32Args {
+  const uint8_t* x = nullptr;
+  float* y = nullptr;
+  const float* ws = nullptr;
+  const float* bs = nullptr;
+  const float* wd = nullptr;
+  const float* bd = nullptr;
+  const float* wp = nullptr;
+  const float* bp = nullptr;
+  int B = 0, H = 0, W = 0;
+  float add = 0.f, div = 1.f;
+  // derived
+  int Ho = 0, Wo = 0, tiles_x = 0, tiles_y = 0;
+};
+bool stem_ir1_f32(const StemIr1F32Args& a, hipStream_t s);
 bool ir_block_f32(const IrBlockF32Args& a, hipStream_t s);
 
 }  // namespace kernels

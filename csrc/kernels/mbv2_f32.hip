@@ -44,6 +44,8 @@ namespace kernels {
 
 namespace {
 
+constexpr int kStemIr1TY = 8, kStemIr1TX = 16;
+
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
@@ -637,18 +639,24 @@ __global__ void __launch_bounds__(256) ir_block_f32_kernel(IrBlockF32Args a) {
 // deterministic).  The MFMA pipe of a SIMD then alternates between waves of
 // different workgroups that are never held at a common barrier, so one wave's
 // depthwise VALU work hides under another's matrix work.
-template <int S, int TY, int TX, int KIN, int NOT, int NW>
+template <int S, int TY, int TX, int KIN, int NOT, int NW, bool FULL>
 struct IrwGeom {
   static constexpr int TIY = (TY - 1) * S + 3, TIX = (TX - 1) * S + 3;
   static constexpr int PIN = TIY * TIX;               // halo grid cells
   static constexpr int NC16 = (PIN + 15) / 16 * 16;   // compact in-image pixels (max), padded
   static constexpr int NBT = NC16 / 16;               // expand pixel tiles
-  static constexpr int XSP = NC16 + 1;                // xs plane stride (quads): staging writes spread over banks
+  // LDS planes are multiples of 256 B (16 quads): a ds_read_b128 lane group
+  // ({0-3,12-15} of one 16-lane half + {4-11} of the next, etc.) then hits
+  // disjoint bank slots when each half reads 16 consecutive quads of its own
+  // plane.  xs positions are XOR-swizzled with (kq & 3) so the staging writes
+  // (8 consecutive lanes = 8 k-quads of one pixel) land in 4 slots, not 1.
+  static constexpr int XSP = NC16;                    // xs plane stride (quads)
+  static constexpr int PINP = (PIN + 15) / 16 * 16;   // hidden plane stride (quads)
   static constexpr int KQ = KIN / 4;
   static constexpr int NPT = (TY * TX + 15) / 16;     // output pixel tiles
   static constexpr int NPX = NPT * 16;
   static constexpr size_t xs_q = static_cast<size_t>(KQ) * XSP;
-  static constexpr size_t hid_q = static_cast<size_t>(4 * NW) * PIN;      // [wave][quad][cell]
+  static constexpr size_t hid_q = static_cast<size_t>(4 * NW) * PINP;     // [wave][quad][cell]
   static constexpr size_t dwo_q = static_cast<size_t>(4 * NW) * NPX;      // [wave][quad][px]
   static constexpr size_t red_q = static_cast<size_t>(2 * 4 * NW) * NPX;  // [buf][wave][quad][px]
   static size_t lds_bytes(int) { return 16 * std::max(xs_q + hid_q + dwo_q, red_q); }
@@ -662,18 +670,25 @@ __device__ __forceinline__ void wave_sync() {
 
 // (second launch bound = minimum waves per SIMD: 2 keeps every configuration
 // but the 7x7 / 160-channel one within 256 VGPRs, two workgroups per CU)
-template <int S, int TY, int TX, int KIN, int NOT, int NW>
+//
+// FULL = true (large maps, where most tiles are interior): the expand runs over
+// the whole halo grid (pixel index = halo cell, compile-time geometry, no
+// index tables) and writes zeros for out-of-image cells; FULL = false (small
+// maps, where every tile touches the border): only the in-image pixels are
+// expanded (compact index, halos zeroed once per tile).
+template <int S, int TY, int TX, int KIN, int NOT, int NW, bool FULL>
 __global__ void __launch_bounds__(64 * NW, (NOT <= 6 ? 2 : 1)) irw_f32_kernel(IrBlockF32Args a) {
-  using G = IrwGeom<S, TY, TX, KIN, NOT, NW>;
+  using G = IrwGeom<S, TY, TX, KIN, NOT, NW, FULL>;
   constexpr int NT = 64 * NW;
   constexpr int TIY = G::TIY, TIX = G::TIX, PIN = G::PIN, NC16 = G::NC16, NBT = G::NBT, XSP = G::XSP;
+  constexpr int PINP = G::PINP;
   constexpr int KQ = G::KQ, NPT = G::NPT, NPX = G::NPX;
   constexpr int NS16 = KIN / 16;
   constexpr bool KT8 = (KIN % 16) != 0;
   static_assert(KIN % 8 == 0, "irw_f32: KIN % 8");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   f32x4_t* xs = reinterpret_cast<f32x4_t*>(smem);  // [KQ][XSP]
-  f32x4_t* hidw = xs + G::xs_q;                     // [NW waves][4 quads][PIN]
+  f32x4_t* hidw = xs + G::xs_q;                     // [NW waves][4 quads][PINP]
   f32x4_t* dwo = hidw + G::hid_q;                   // [NW waves][4 quads][NPX]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -688,32 +703,55 @@ __global__ void __launch_bounds__(64 * NW, (NOT <= 6 ? 2 : 1)) irw_f32_kernel(Ir
   const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
   const int ry0 = max(iy0, 0), ry1 = min(iy0 + TIY, a.H);
   const int rx0 = max(ix0, 0), rx1 = min(ix0 + TIX, a.W);
-  const int RW = rx1 - rx0, NC = (ry1 - ry0) * RW;
+  const int RW = rx1 - rx0, NC = FULL ? PIN : (ry1 - ry0) * RW;
+  // c / RW for the small compact indices (c < 1024): (c + 0.5) * (1 / RW) in
+  // fp32 is at least 0.5 / RW away from an integer, so truncation is exact
+  const float rrw = 1.f / static_cast<float>(RW);
   const float* xb = a.x + static_cast<int64_t>(b) * a.H * a.W * a.cin;
 
-  // ---- stage the compact input tile (coalesced reads: consecutive threads, consecutive quads)
-  for (int v = tid; v < NC16 * KQ; v += NT) {
+  // ---- stage the input tile (coalesced reads: consecutive threads, consecutive
+  // quads; compile-time trip count, so every load is in flight before the stores)
+  constexpr int NSV = NC16 * KQ, NSIT = (NSV + NT - 1) / NT;
+#pragma unroll
+  for (int it = 0; it < NSIT; ++it) {
+    const int v = tid + it * NT;
+    if (NSV % NT != 0 && v >= NSV) break;
     const int c = v / KQ, kq = v - c * KQ;
     f32x4_t val = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    if (c < NC && kq * 4 < a.cin) {
-      const int yy = ry0 + c / RW, xx = rx0 + c % RW;
-      val = *reinterpret_cast<const f32x4_t*>(xb + (static_cast<int64_t>(yy) * a.W + xx) * a.cin + kq * 4);
+    int yy, xx;
+    if constexpr (FULL) {
+      yy = iy0 + c / TIX;
+      xx = ix0 + c % TIX;
+    } else {
+      const int cy = static_cast<int>((static_cast<float>(c) + 0.5f) * rrw);
+      yy = ry0 + cy;
+      xx = rx0 + c - cy * RW;
     }
-    xs[kq * XSP + c] = val;
+    if (c < NC && kq * 4 < a.cin && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W)
+      val = *reinterpret_cast<const f32x4_t*>(xb + (static_cast<int64_t>(yy) * a.W + xx) * a.cin + kq * 4);
+    xs[kq * XSP + (c ^ (kq & 3))] = val;
   }
   // out-of-image halo cells of every wave's hidden image = the depthwise zero padding
-  if (ry0 > iy0 || ry1 < iy0 + TIY || rx0 > ix0 || rx1 < ix0 + TIX) {
+  // (FULL: the expand itself writes them as zeros)
+  if (!FULL && (ry0 > iy0 || ry1 < iy0 + TIY || rx0 > ix0 || rx1 < ix0 + TIX)) {
     for (int v = tid; v < 4 * NW * PIN; v += NT) {
-      const int p = v % PIN;
+      const int pl = v / PIN, p = v - pl * PIN;
       const int yy = iy0 + p / TIX, xx = ix0 + p % TIX;
-      if (yy < ry0 || yy >= ry1 || xx < rx0 || xx >= rx1) hidw[v] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      if (yy < ry0 || yy >= ry1 || xx < rx0 || xx >= rx1) hidw[pl * PINP + p] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     }
   }
+  // expand pixel j*16+li -> its hidden cell (compact), or in-image flag (FULL)
   int hcell[NBT];
 #pragma unroll
   for (int j = 0; j < NBT; ++j) {
     const int c = j * 16 + li;
-    hcell[j] = c < NC ? (ry0 + c / RW - iy0) * TIX + (rx0 + c % RW - ix0) : -1;
+    if constexpr (FULL) {
+      const int yy = iy0 + c / TIX, xx = ix0 + c % TIX;
+      hcell[j] = (c < PIN && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) ? 1 : 0;
+    } else {
+      const int cy = static_cast<int>((static_cast<float>(c) + 0.5f) * rrw);
+      hcell[j] = c < NC ? (ry0 + cy - iy0) * TIX + (rx0 + c - cy * RW - ix0) : -1;
+    }
   }
   int dcell[NPT];
 #pragma unroll
@@ -734,7 +772,7 @@ __global__ void __launch_bounds__(64 * NW, (NOT <= 6 ? 2 : 1)) irw_f32_kernel(Ir
 
   const int nsub = a.hid >> 4;
   const int sub0 = part * nsub / nparts, sub1 = (part + 1) * nsub / nparts;
-  f32x4_t* myhid = hidw + wave * 4 * PIN + g * PIN;
+  f32x4_t* myhid = hidw + (wave * 4 + g) * PINP;
   f32x4_t* mydwo = dwo + wave * 4 * NPX + g * NPX;
   f32x4_t ea[NS16 > 0 ? NS16 : 1];
   f32x2_t et = f32x2_t{0.f, 0.f};
@@ -764,30 +802,43 @@ __global__ void __launch_bounds__(64 * NW, (NOT <= 6 ? 2 : 1)) irw_f32_kernel(Ir
       // in-image pixels is skipped wave-uniformly, a half-valid one computes zeros
 #pragma unroll
       for (int j = 0; j < NBT; j += 2) {
-        if (j < nbt) {
+        if (FULL || j < nbt) {
           const int j1 = j + 1 < NBT ? j + 1 : j;
           f32x4_t e0 = f32x4_t{0.f, 0.f, 0.f, 0.f}, e1 = e0;
 #pragma unroll
           for (int s = 0; s < NS16; ++s) {
-            e0 = mfma_k16(ea[s], xs[(4 * s + g) * XSP + j * 16 + li], e0);
-            e1 = mfma_k16(ea[s], xs[(4 * s + g) * XSP + j1 * 16 + li], e1);
+            e0 = mfma_k16(ea[s], xs[(4 * s + g) * XSP + j * 16 + (li ^ g)], e0);
+            e1 = mfma_k16(ea[s], xs[(4 * s + g) * XSP + j1 * 16 + (li ^ g)], e1);
           }
           if constexpr (KT8) {
-            const f32x2_t* t0 = reinterpret_cast<const f32x2_t*>(&xs[(4 * NS16 + g / 2) * XSP + j * 16 + li]);
-            const f32x2_t* t1 = reinterpret_cast<const f32x2_t*>(&xs[(4 * NS16 + g / 2) * XSP + j1 * 16 + li]);
+            // tail plane kq = 4 NS16 + g/2: swizzle (kq & 3) = g >> 1
+            const f32x2_t* t0 =
+                reinterpret_cast<const f32x2_t*>(&xs[(4 * NS16 + g / 2) * XSP + j * 16 + (li ^ (g >> 1))]);
+            const f32x2_t* t1 =
+                reinterpret_cast<const f32x2_t*>(&xs[(4 * NS16 + g / 2) * XSP + j1 * 16 + (li ^ (g >> 1))]);
             e0 = mfma_k8(et, t0[g & 1], e0);
             e1 = mfma_k8(et, t1[g & 1], e1);
           }
-          if (hcell[j] >= 0) myhid[hcell[j]] = relu6x4(e0 + be4);
-          if (j + 1 < NBT && hcell[j1] >= 0) myhid[hcell[j1]] = relu6x4(e1 + be4);
+          if constexpr (FULL) {
+            const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
+            myhid[j * 16 + li] = hcell[j] ? relu6x4(e0 + be4) : z;
+            if (j + 1 < NBT) myhid[j1 * 16 + li] = hcell[j1] ? relu6x4(e1 + be4) : z;
+          } else {
+            if (hcell[j] >= 0) myhid[hcell[j]] = relu6x4(e0 + be4);
+            if (j + 1 < NBT && hcell[j1] >= 0) myhid[hcell[j1]] = relu6x4(e1 + be4);
+          }
         }
       }
       if (hs + NW < sub1) load_ea(hs + NW);  // next subtile's weights: in flight during dw + project
     } else {
       // t = 1: the hidden channels are the input channels
 #pragma unroll
-      for (int j = 0; j < NBT; ++j)
-        if (hcell[j] >= 0) myhid[hcell[j]] = xs[(hs * 4 + g) * XSP + j * 16 + li];
+      for (int j = 0; j < NBT; ++j) {
+        if constexpr (FULL)
+          myhid[j * 16 + li] = xs[(hs * 4 + g) * XSP + j * 16 + (li ^ g)];  // (staged zeros outside the image)
+        else if (hcell[j] >= 0)
+          myhid[hcell[j]] = xs[(hs * 4 + g) * XSP + j * 16 + (li ^ g)];
+      }
     }
     wave_sync();
 
@@ -848,6 +899,160 @@ __global__ void __launch_bounds__(64 * NW, (NOT <= 6 ? 2 : 1)) irw_f32_kernel(Ir
   }
 }
 
+// --------------------------------------------------------- stem_ir1_f32 ----
+// The stem (3x3/2 conv 3 -> 32 on the raw uint8 frame, normalised in-kernel
+// as (x + add) / div, + bias, ReLU6) fused with MobileNetV2's first block
+// (t = 1: dw 3x3 on those 32 channels + ReLU6, project 32 -> 16).  The 32-
+// channel stem output -- the largest activation of the network, 205 MB per
+// 128 frames in fp32 -- never leaves LDS.
+//
+// One workgroup = one TY x TX tile of the 112x112 block output, 4 waves =
+// (16-channel half) x (pixel half): stem MFMA over the wave's half of the
+// (TY+2) x (TX+2) halo grid into its channel half's hidden image (out-of-map
+// cells = the dw zero padding); one barrier; dw + project partial (K = the
+// 16 channels) on the wave's half of the output pixels; the two channel
+// halves' partials are added in a fixed order through LDS.
+template <int TY, int TX>
+__global__ void __launch_bounds__(256, 2) stem_ir1_f32_kernel(StemIr1F32Args a) {
+  constexpr int HY = TY + 2, HX = TX + 2, PIN = HY * HX;
+  constexpr int NBT = (PIN + 15) / 16, PINP = NBT * 16;
+  constexpr int IY = 2 * HY + 1, IX = 2 * HX + 1, PITCH = IX * 3;
+  constexpr int NPT = (TY * TX + 15) / 16, NPX = NPT * 16;
+  constexpr int XIN = (IY * PITCH + 3) / 4 * 4;  // floats, 16-B aligned end
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* xin = smem;                                       // [IY][PITCH] normalised input
+  float* lut = smem + XIN;                                 // [256] (v + add) / div
+  f32x4_t* hidw = reinterpret_cast<f32x4_t*>(smem + XIN + 256);  // [2 channel halves][4 quads][PINP]
+  f32x4_t* dwo = hidw + 2 * 4 * PINP;                      // [2 channel halves][4 quads][NPX]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int chalf = wave & 1, phalf = wave >> 1;  // wave = (16-channel half, pixel half)
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int tiles_img = a.tiles_x * a.tiles_y;
+  const int b = tile / tiles_img;
+  const int tyx = tile - b * tiles_img;
+  const int oy0 = (tyx / a.tiles_x) * TY, ox0 = (tyx % a.tiles_x) * TX;
+  const int hy0 = oy0 - 1, hx0 = ox0 - 1;          // hidden halo origin (stem-output coords)
+  const int iy0 = 2 * hy0 - 1, ix0 = 2 * hx0 - 1;  // input patch origin
+  const uint8_t* xb = a.x + static_cast<int64_t>(b) * a.H * a.W * 3;
+
+  // ---- normalised input patch (zero outside the frame = the stem's padding);
+  // the normalisation (x + add) / div -- the pipeline's tensor_transform
+  // arithmetic, exact fp32 division -- is a 256-entry table.  Every byte load
+  // of the patch is issued before the first use (compile-time trip count).
+  constexpr int NIN = IY * PITCH, NIT = (NIN + 255) / 256;
+  int raw[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int i = tid + it * 256;
+    const int r = i / PITCH, c = i - r * PITCH;
+    const int iy = iy0 + r, ix = ix0 + c / 3;
+    raw[it] = (i < NIN && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
+                  ? static_cast<int>(xb[(static_cast<int64_t>(iy) * a.W + ix) * 3 + c % 3])
+                  : -1;
+  }
+  lut[tid] = (static_cast<float>(tid) + a.add) / a.div;
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int i = tid + it * 256;
+    if (i < NIN) xin[i] = raw[it] >= 0 ? lut[raw[it]] : 0.f;
+  }
+  // stem weights of this wave's 16 channels: k = 4t + g (27 taps + 1 zero)
+  float sa[7];
+  int off[7];
+#pragma unroll
+  for (int t = 0; t < 7; ++t) {
+    const int k = 4 * t + g;
+    sa[t] = k < 27 ? a.ws[k * 32 + chalf * 16 + li] : 0.f;
+    off[t] = k < 27 ? (k / 9) * PITCH + ((k % 9) / 3) * 3 + (k % 3) : 0;
+  }
+  const int ch = chalf * 16 + 4 * g;  // this lane's channel quad
+  const f32x4_t bs4 = *reinterpret_cast<const f32x4_t*>(a.bs + ch);
+  const f32x4_t bd4 = *reinterpret_cast<const f32x4_t*>(a.bd + ch);
+  f32x4_t wd4[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) wd4[t] = *reinterpret_cast<const f32x4_t*>(a.wd + t * 32 + ch);
+  const f32x4_t pa = *reinterpret_cast<const f32x4_t*>(a.wp + li * 32 + ch);
+  __syncthreads();
+
+  f32x4_t* myhid = hidw + (chalf * 4 + g) * PINP;
+  f32x4_t* mydwo = dwo + (chalf * 4 + g) * NPX;
+  const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // ---- stem MFMA over this pixel half of the halo grid, two pixel tiles at a time
+  constexpr int NBH = (NBT + 1) / 2;
+#pragma unroll
+  for (int jj = 0; jj < NBH; jj += 2) {
+    const int j = phalf * NBH + jj;
+    if (j >= NBT) break;
+    const int j1 = (jj + 1 < NBH && j + 1 < NBT) ? j + 1 : j;
+    const int c0 = j * 16 + li, c1 = j1 * 16 + li;
+    const int hy_0 = c0 / HX, hx_0 = c0 - hy_0 * HX, hy_1 = c1 / HX, hx_1 = c1 - hy_1 * HX;
+    const int base0 = c0 < PIN ? 2 * hy_0 * PITCH + 6 * hx_0 : 0;
+    const int base1 = c1 < PIN ? 2 * hy_1 * PITCH + 6 * hx_1 : 0;
+    f32x4_t e0 = z, e1 = z;
+#pragma unroll
+    for (int t = 0; t < 7; ++t) {
+      e0 = mfma4(sa[t], xin[base0 + off[t]], e0);
+      e1 = mfma4(sa[t], xin[base1 + off[t]], e1);
+    }
+    const bool in0 = c0 < PIN && hy0 + hy_0 >= 0 && hy0 + hy_0 < a.Ho && hx0 + hx_0 >= 0 && hx0 + hx_0 < a.Wo;
+    const bool in1 = c1 < PIN && hy0 + hy_1 >= 0 && hy0 + hy_1 < a.Ho && hx0 + hx_1 >= 0 && hx0 + hx_1 < a.Wo;
+    myhid[c0] = in0 ? relu6x4(e0 + bs4) : z;
+    if (j1 != j) myhid[c1] = in1 ? relu6x4(e1 + bs4) : z;
+  }
+  __syncthreads();  // both pixel halves of each channel half's hidden image
+  // ---- depthwise 3x3 + bias + ReLU6 on this wave's output pixel half
+  constexpr int NPH = (NPT + 1) / 2;
+#pragma unroll
+  for (int pp = 0; pp < NPH; ++pp) {
+    const int pt = phalf * NPH + pp;
+    if (pt >= NPT) break;
+    const int q = pt * 16 + li;
+    const int qq = q < TY * TX ? q : 0;
+    const int cell = (qq / TX) * HX + (qq % TX);
+    f32x4_t d = bd4;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) d = __builtin_elementwise_fma(myhid[cell + ky * HX + kx], wd4[ky * 3 + kx], d);
+    mydwo[pt * 16 + li] = relu6x4(d);
+  }
+  wave_sync();
+  // ---- project partial over this wave's 16 channels (K = 16 of 32)
+  f32x4_t acc[NPH];
+#pragma unroll
+  for (int pp = 0; pp < NPH; ++pp) {
+    const int pt = phalf * NPH + pp;
+    acc[pp] = pt < NPT ? mfma_k16(pa, mydwo[pt * 16 + li], z) : z;
+  }
+  // ---- channel half 0 + half 1 through LDS (the dwo planes of the other half
+  // are read only by their own wave, so the partials reuse this wave's own rows)
+  f32x4_t* red = dwo;  // [2 halves][4 quads][NPX]: overwrite own dw outputs with partials
+#pragma unroll
+  for (int pp = 0; pp < NPH; ++pp) {
+    const int pt = phalf * NPH + pp;
+    if (pt < NPT) red[(chalf * 4 + g) * NPX + pt * 16 + li] = acc[pp];
+  }
+  __syncthreads();
+  const f32x4_t bp4 = *reinterpret_cast<const f32x4_t*>(a.bp + 4 * g);
+  // waves of channel half 0 store (pixel half = phalf)
+  if (chalf == 0) {
+#pragma unroll
+    for (int pp = 0; pp < NPH; ++pp) {
+      const int pt = phalf * NPH + pp;
+      if (pt >= NPT) break;
+      const int q = pt * 16 + li;
+      if (q >= TY * TX) continue;
+      const int gy = oy0 + q / TX, gx = ox0 + q % TX;
+      if (gy >= a.Ho || gx >= a.Wo) continue;
+      const f32x4_t v = red[g * NPX + q] + red[(4 + g) * NPX + q] + bp4;
+      *reinterpret_cast<f32x4_t*>(a.y + ((static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx) * 16 + 4 * g) = v;
+    }
+  }
+}
+
 // configurations (one instantiation each): MobileNetV2's fused blocks
 struct IrF32Cfg {
   int S, TY, TX, HC, NOT, KIN;
@@ -897,25 +1102,27 @@ int tile_pref(int S, int H, int W, int TY, int TX) {
 // wave-split kernel configurations: the 28x28 / 14x14 / 7x7 blocks of MobileNetV2
 struct IrwCfg {
   int S, TY, TX, KIN, NOT, NW;
+  bool full;
   void (*kernel)(IrBlockF32Args);
   size_t (*lds)(int);
 };
-#define NNSX_IRW(S, TY, TX, KIN, NOT, NW)                                                             \
-  IrwCfg {                                                                                            \
-    S, TY, TX, KIN, NOT, NW, &irw_f32_kernel<S, TY, TX, KIN, NOT, NW>, &IrwGeom<S, TY, TX, KIN, NOT, NW>::lds_bytes \
+#define NNSX_IRW(S, TY, TX, KIN, NOT, NW, F)                                                    \
+  IrwCfg {                                                                                      \
+    S, TY, TX, KIN, NOT, NW, F, &irw_f32_kernel<S, TY, TX, KIN, NOT, NW, F>,                    \
+        &IrwGeom<S, TY, TX, KIN, NOT, NW, F>::lds_bytes                                         \
   }
 // (NW = waves per workgroup: a divisor of the hidden subtile count where possible,
 // so every wave walks the same number of 16-channel subtiles)
 const IrwCfg kIrwCfgs[] = {
-    NNSX_IRW(2, 4, 8, 16, 2, 3),    // 112 -> 56  16 -> 96 -> 24   (6 subtiles)
-    NNSX_IRW(1, 8, 8, 24, 2, 3),    // 56x56      24 -> 144 -> 24  (9)
-    NNSX_IRW(2, 7, 4, 24, 2, 3),    // 56 -> 28   24 -> 144 -> 32  (9)
-    NNSX_IRW(1, 7, 7, 32, 2, 4),    // 28x28      32 -> 192 -> 32  (12)
-    NNSX_IRW(2, 2, 7, 32, 4, 4),    // 28 -> 14   32 -> 192 -> 64  (12)
-    NNSX_IRW(1, 7, 7, 64, 4, 4),    // 14x14      64 -> 384 -> 64  (24)
-    NNSX_IRW(1, 7, 7, 64, 6, 4),    // 14x14      64 -> 384 -> 96  (24)
-    NNSX_IRW(1, 7, 7, 96, 6, 4),    // 14x14      96 -> 576 -> 96  (36)
-    NNSX_IRW(1, 7, 7, 160, 10, 4),  // 7x7       160 -> 960 -> 160 (60, two parts)
+    NNSX_IRW(2, 4, 8, 16, 2, 3, true),     // 112 -> 56  16 -> 96 -> 24   (6 subtiles)
+    NNSX_IRW(1, 8, 8, 24, 2, 3, true),     // 56x56      24 -> 144 -> 24  (9)
+    NNSX_IRW(2, 7, 4, 24, 2, 3, true),     // 56 -> 28   24 -> 144 -> 32  (9)
+    NNSX_IRW(1, 7, 7, 32, 2, 4, false),    // 28x28      32 -> 192 -> 32  (12)
+    NNSX_IRW(2, 2, 7, 32, 4, 4, false),    // 28 -> 14   32 -> 192 -> 64  (12)
+    NNSX_IRW(1, 7, 7, 64, 4, 4, false),    // 14x14      64 -> 384 -> 64  (24)
+    NNSX_IRW(1, 7, 7, 64, 6, 4, false),    // 14x14      64 -> 384 -> 96  (24)
+    NNSX_IRW(1, 7, 7, 96, 6, 4, false),    // 14x14      96 -> 576 -> 96  (36)
+    NNSX_IRW(1, 7, 7, 160, 10, 4, false),  // 7x7       160 -> 960 -> 160 (60, two parts)
 };
 #undef NNSX_IRW
 
@@ -1105,6 +1312,31 @@ static bool launch_irw(const IrwCfg* c, IrBlockF32Args a, hipStream_t s) {
   if (a.hsplit > 1)
     (void)hipMemsetAsync(a.y, 0, static_cast<size_t>(a.B) * a.Ho * a.Wo * a.cout * sizeof(float), s);
   hipLaunchKernelGGL(c->kernel, dim3(static_cast<unsigned>(tiles * a.hsplit)), dim3(64 * c->NW), lds, s, a);
+  return true;
+}
+
+size_t stem_ir1_lds_bytes() {
+  constexpr int TY = kStemIr1TY, TX = kStemIr1TX;
+  constexpr int HY = TY + 2, HX = TX + 2, PIN = HY * HX, PINP = (PIN + 15) / 16 * 16;
+  constexpr int IY = 2 * HY + 1, PITCH = (2 * HX + 1) * 3;
+  constexpr int NPX = (TY * TX + 15) / 16 * 16;
+  return static_cast<size_t>((IY * PITCH + 3) / 4 * 4 + 256) * 4 + 16 * (8 * PINP + 8 * NPX);
+}
+
+bool stem_ir1_f32(const StemIr1F32Args& args, hipStream_t s) {
+  StemIr1F32Args a = args;
+  a.Ho = (a.H - 1) / 2 + 1;
+  a.Wo = (a.W - 1) / 2 + 1;
+  a.tiles_y = (a.Ho + kStemIr1TY - 1) / kStemIr1TY;
+  a.tiles_x = (a.Wo + kStemIr1TX - 1) / kStemIr1TX;
+  const size_t lds = stem_ir1_lds_bytes();
+  if (lds > 160 * 1024) return false;
+  const void* fn = reinterpret_cast<const void*>(&stem_ir1_f32_kernel<kStemIr1TY, kStemIr1TX>);
+  if (lds > 64 * 1024 &&
+      hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+    return false;
+  hipLaunchKernelGGL((stem_ir1_f32_kernel<kStemIr1TY, kStemIr1TX>),
+                     dim3(static_cast<unsigned>(a.tiles_x * a.tiles_y * a.B)), dim3(256), lds, s, a);
   return true;
 }
 

@@ -285,6 +285,43 @@ at::Tensor ir_block_cpu(const at::Tensor& x, const at::Tensor& we, const at::Ten
   return pw_conv_cpu(h, wp, bp, res, cout, 0, false);  // (dtype follows x: f32 stays f32)
 }
 
+// stem + first (t = 1) block, fused (fp32): uint8 frame -> [B, Ho, Wo, 16]
+at::Tensor stem_ir1_cuda(const at::Tensor& x, const at::Tensor& ws, const at::Tensor& bs, const at::Tensor& wd,
+                         const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, double add, double div) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kByte && x.is_contiguous() && x.dim() == 4 && x.size(3) == 3,
+              "stem_ir1: x [B,H,W,3] uint8");
+  for (const auto* t : {&ws, &bs, &wd, &bd, &wp, &bp})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous(), "stem_ir1: f32 weights");
+  TORCH_CHECK(ws.numel() == 27 * 32 && bs.numel() >= 32 && wd.numel() == 9 * 32 && bd.numel() >= 32 &&
+                  wp.size(0) >= 16 && wp.size(1) == 32 && bp.numel() >= 16,
+              "stem_ir1: ws [3,3,3,32], wd [9,32], wp [16,32]");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2);
+  at::Tensor y = at::empty({B, (H - 1) / 2 + 1, (W - 1) / 2 + 1, 16}, x.options().dtype(at::kFloat));
+  nnsx::kernels::StemIr1F32Args a;
+  a.x = x.data_ptr<uint8_t>();
+  a.y = y.data_ptr<float>();
+  a.ws = ws.data_ptr<float>();
+  a.bs = bs.data_ptr<float>();
+  a.wd = wd.data_ptr<float>();
+  a.bd = bd.data_ptr<float>();
+  a.wp = wp.data_ptr<float>();
+  a.bp = bp.data_ptr<float>();
+  a.B = static_cast<int>(B);
+  a.H = static_cast<int>(H);
+  a.W = static_cast<int>(W);
+  a.add = static_cast<float>(add);
+  a.div = static_cast<float>(div);
+  TORCH_CHECK(nnsx::kernels::stem_ir1_f32(a, cur_stream()), "stem_ir1: launch failed");
+  return y;
+}
+
+at::Tensor stem_ir1_cpu(const at::Tensor& x, const at::Tensor& ws, const at::Tensor& bs, const at::Tensor& wd,
+                        const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, double add, double div) {
+  at::Tensor h = stem_conv_u8_cpu(x, ws, bs, 1, add, div, true);
+  h = dw_conv_cpu(h, wd, bd, 1, 1, 1);
+  return pw_conv_cpu(h, wp, bp, c10::nullopt, 16, 0, true);
+}
+
 bool ir_supported_f32(int64_t stride, int64_t H, int64_t W, int64_t cin, int64_t hid, int64_t cout, bool has_expand) {
   return nnsx::kernels::ir_block_f32_supported(static_cast<int>(stride), static_cast<int>(H), static_cast<int>(W),
                                                static_cast<int>(cin), static_cast<int>(hid), static_cast<int>(cout),
@@ -304,6 +341,7 @@ TORCH_LIBRARY(nnsx, m) {
   m.def("stem_conv(Tensor x, Tensor w, Tensor bias, int act, bool out_f32=False) -> Tensor");
   m.def("stem_conv_u8(Tensor x, Tensor w, Tensor bias, int act, float add, float div, bool out_f32=False) -> Tensor");
   m.def("avgpool(Tensor x) -> Tensor");
+  m.def("stem_ir1(Tensor x, Tensor ws, Tensor bs, Tensor wd, Tensor bd, Tensor wp, Tensor bp, float add, float div) -> Tensor");
   m.def("pw_conv_f32_tile(Tensor x, Tensor wt, Tensor bias, Tensor? res, int N, int act, int tile) -> Tensor");
   m.def("ir_block(Tensor x, Tensor we, Tensor be, Tensor wd, Tensor bd, Tensor wp, Tensor bp, int stride, int cout, "
         "bool has_expand, bool residual) -> Tensor");
@@ -318,6 +356,7 @@ TORCH_LIBRARY_IMPL(nnsx, CUDA, m) {
   m.impl("stem_conv", stem_conv_cuda);
   m.impl("stem_conv_u8", stem_conv_u8_cuda);
   m.impl("avgpool", avgpool_cuda);
+  m.impl("stem_ir1", stem_ir1_cuda);
   m.impl("pw_conv_f32_tile", pw_conv_f32_tile_cuda);
   m.impl("ir_block", ir_block_cuda);
 }
@@ -328,5 +367,6 @@ TORCH_LIBRARY_IMPL(nnsx, CPU, m) {
   m.impl("stem_conv", stem_conv_cpu);
   m.impl("stem_conv_u8", stem_conv_u8_cpu);
   m.impl("avgpool", avgpool_cpu);
+  m.impl("stem_ir1", stem_ir1_cpu);
   m.impl("ir_block", ir_block_cpu);
 }

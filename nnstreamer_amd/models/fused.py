@@ -32,6 +32,8 @@ import os
 
 # NNSX_FUSE_IR=0 keeps every inverted residual on the three-kernel path (A/B testing)
 FUSE_IR = os.environ.get("NNSX_FUSE_IR", "1") != "0"
+# NNSX_FUSE_STEM=0 keeps the fp32 stem and first block as separate kernels (A/B testing)
+FUSE_STEM = os.environ.get("NNSX_FUSE_STEM", "1") != "0"
 
 
 def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d):
@@ -217,6 +219,15 @@ class FusedMobileNetV2(nn.Module):
         self.register_buffer("stem_b", b.contiguous())
         self.in_add, self.in_div = -127.5, 127.5
         self.blocks = nn.ModuleList([Block(ir, precision) for ir in m.features[1:-1]])
+        # fp32 + uint8 frames: the stem and the first (t = 1, 32 -> 16) block run as
+        # one kernel (stem_ir1), the 32-channel stem output never leaves LDS
+        b0 = self.blocks[0]
+        self.stem_ir1 = bool(self.f32 and not b0.has_expand and b0.cin == 32 and b0.cout == 16
+                             and b0.dw.stride == 1 and not b0.use_res and FUSE_STEM)
+        self.register_buffer("s1_wd", b0.dw.w.clone() if self.stem_ir1 else torch.zeros(1))
+        self.register_buffer("s1_bd", b0.dw.bias.clone() if self.stem_ir1 else torch.zeros(1))
+        self.register_buffer("s1_wp", b0.project.wt.clone() if self.stem_ir1 else torch.zeros(1))
+        self.register_buffer("s1_bp", b0.project.bias.clone() if self.stem_ir1 else torch.zeros(1))
         head: ConvBNReLU = m.features[-1]
         self.head = PW(*_fold(head[0], head[1]), act=1, precision=precision)
         fc: nn.Linear = m.classifier[1]
@@ -225,9 +236,18 @@ class FusedMobileNetV2(nn.Module):
         return self
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        h = stem(x, self.stem_w, self.stem_b, self.in_add, self.in_div, self.f32)
+        start = 0
+        if self.stem_ir1 and x.dtype == torch.uint8 and x.is_cuda:
+            h = torch.ops.nnsx.stem_ir1(x.contiguous(), self.stem_w, self.stem_b, self.s1_wd, self.s1_bd, self.s1_wp,
+                                        self.s1_bp, self.in_add, self.in_div)
+            start = 1
+        else:
+            h = stem(x, self.stem_w, self.stem_b, self.in_add, self.in_div, self.f32)
+        i = 0
         for blk in self.blocks:
-            h = blk(h)
+            if i >= start:
+                h = blk(h)
+            i += 1
         h = self.head(h)
         h = torch.ops.nnsx.avgpool(h)
         return self.fc(h)

@@ -87,6 +87,14 @@ if not ONLY:
     us = timeit(lambda: torch.ops.nnsx.stem_conv_u8(xu, ws, bs, 1, -127.5, 127.5, True))
     total += us
     row("stem 224 u8 -> 32", us, 2 * B * 112 * 112 * 32 * 27)
+    wd1 = torch.randn(9, 32, device="cuda")
+    bd1 = torch.zeros(32, device="cuda")
+    wp1 = torch.randn(16, 32, device="cuda") * 0.1
+    bp1 = torch.zeros(16, device="cuda")
+    us1 = timeit(lambda: torch.ops.nnsx.stem_ir1(xu, ws, bs, wd1, bd1, wp1, bp1, -127.5, 127.5))
+    row("stem+block1 fused (replaces both)", us1,
+        2 * B * 112 * 112 * (32 * 27 + 32 * 9 + 32 * 16))
+    print(f"  fused saves {us + seen[(112, 32, 32, 16, 1)] - us1:.1f} us")
     xh = torch.randn(B * 49, 320, device="cuda")
     wh = torch.randn(1280, 320, device="cuda") * 0.05
     bh = torch.zeros(1280, device="cuda")

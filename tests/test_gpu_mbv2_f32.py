@@ -80,6 +80,28 @@ def test_stem_f32_u8_and_pool(nns, H, W):
     _close(p, y.double().cpu().mean((1, 2)))
 
 
+@pytest.mark.parametrize("H,W,B", [(224, 224, 3), (300, 300, 2), (57, 41, 2), (17, 35, 1)])
+def test_stem_ir1_f32(nns, H, W, B):
+    """stem + first block fused (uint8 frame -> 16 channels) vs the fp64 chain."""
+    torch.manual_seed(H + W)
+    x = torch.randint(0, 256, (B, H, W, 3), device="cuda", dtype=torch.uint8)
+    ws = torch.randn(3, 3, 3, 32, device="cuda") * 0.3
+    bs = torch.randn(32, device="cuda") * 0.1
+    wd = torch.randn(9, 32, device="cuda") / 3
+    bd = torch.randn(32, device="cuda") * 0.1
+    wp = torch.randn(16, 32, device="cuda") / 32 ** 0.5
+    bp = torch.randn(16, device="cuda") * 0.1
+    y = torch.ops.nnsx.stem_ir1(x, ws, bs, wd, bd, wp, bp, -127.5, 127.5)
+    assert y.shape == (B, (H - 1) // 2 + 1, (W - 1) // 2 + 1, 16) and y.dtype == torch.float32
+    xf = (x.double().cpu() - 127.5) / 127.5
+    h = F.conv2d(xf.permute(0, 3, 1, 2), ws.double().cpu().permute(3, 2, 0, 1), bs.double().cpu(), stride=2,
+                 padding=1).clamp(0, 6)
+    h = F.conv2d(h, wd.double().cpu().view(3, 3, 32).permute(2, 0, 1).unsqueeze(1), bd.double().cpu(), padding=1,
+                 groups=32).clamp(0, 6)
+    ref = h.permute(0, 2, 3, 1) @ wp.double().cpu().t() + bp.double().cpu()
+    _close(y, ref, tol=5e-5)
+
+
 # every fused MobileNetV2 block (H, cin, hid, cout, stride, expand) + partial-tile shapes
 IR_F32_SHAPES = [(112, 32, 32, 16, 1, False), (112, 16, 96, 24, 2, True), (56, 24, 144, 24, 1, True),
                  (56, 24, 144, 32, 2, True), (28, 32, 192, 32, 1, True), (28, 32, 192, 64, 2, True),
