@@ -205,7 +205,12 @@ std::shared_ptr<StoreClient> StoreClient::connect(const std::string& host, int p
 }
 
 bool StoreClient::call(const std::string& op, const std::string& key, const std::string* val, int64_t arg, int wait_ms,
-                       std::string* out, int64_t* iout) {
+                       std::string* out, int64_t* iout, int* status) {
+  // status: 0 ok, 1 the server's own wait expired (a timeout: retryable),
+  // 2 anything else (lost or failed connection, server error: not retryable)
+  int st_local = 2;
+  int& st = status ? *status : st_local;
+  st = 2;
   std::lock_guard<std::mutex> lk(mu_);
   if (!conn_ || !conn_->alive()) return false;
   Message m;
@@ -219,7 +224,11 @@ bool StoreClient::call(const std::string& op, const std::string& key, const std:
   // the server answers a timed get itself; allow slack for the round trip
   const int t = wait_ms < 0 ? -1 : wait_ms + 30000;
   if (!conn_->recv(&r, t)) return false;
-  if (r.flags != 0) return false;
+  if (r.flags != 0) {
+    st = r.flags == 1 ? 1 : 2;
+    return false;
+  }
+  st = 0;
   if (out) {
     out->clear();
     if (!r.blobs.empty() && r.blobs[0]->size())
@@ -232,8 +241,11 @@ bool StoreClient::call(const std::string& op, const std::string& key, const std:
 bool StoreClient::set(const std::string& key, const std::string& val, int readers) {
   return call("set", key, &val, readers, 0, nullptr, nullptr);
 }
-bool StoreClient::get(const std::string& key, std::string* val, int timeout_ms) {
-  return call("get", key, nullptr, 0, timeout_ms, val, nullptr);
+bool StoreClient::get(const std::string& key, std::string* val, int timeout_ms, bool* timed_out) {
+  int st = 2;
+  const bool ok = call("get", key, nullptr, 0, timeout_ms, val, nullptr, &st);
+  if (timed_out) *timed_out = st == 1;
+  return ok;
 }
 int64_t StoreClient::add(const std::string& key, int64_t delta) {
   int64_t v = INT64_MIN;
@@ -745,8 +757,12 @@ bool Group::recv(Packet* p, int timeout_ms, bool* timed_out, std::string* err) {
   if (timed_out) *timed_out = false;
   const std::string k = key(strfmt("p2p/", grank_, "/", recv_seq_));
   std::string v;
-  if (!store_->get(k, &v, timeout_ms)) {
-    if (timed_out) *timed_out = true;
+  bool to = false;
+  if (!store_->get(k, &v, timeout_ms, &to)) {
+    // only the store's own wait running out is a timeout; a lost store (its
+    // hosting rank died) is an error, so callers stop instead of retrying
+    if (timed_out) *timed_out = to;
+    if (err && !to) *err = "recv: lost the rendezvous store connection";
     return false;
   }
   ++recv_seq_;

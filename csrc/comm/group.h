@@ -51,7 +51,8 @@ class StoreClient {
   // readers > 0: the key is erased after that many successful get()s
   bool set(const std::string& key, const std::string& val, int readers = 0);
   // false on timeout / lost connection
-  bool get(const std::string& key, std::string* val, int timeout_ms);
+  // timed_out: set when the server's wait expired (false on a lost connection)
+  bool get(const std::string& key, std::string* val, int timeout_ms, bool* timed_out = nullptr);
   // atomic add on a decimal counter (missing = 0); returns the new value, INT64_MIN on error
   int64_t add(const std::string& key, int64_t delta);
   bool del(const std::string& key);
@@ -59,7 +60,7 @@ class StoreClient {
 
  private:
   bool call(const std::string& op, const std::string& key, const std::string* val, int64_t arg, int wait_ms,
-            std::string* out, int64_t* iout);
+            std::string* out, int64_t* iout, int* status = nullptr);
   std::shared_ptr<Connection> conn_;
   std::mutex mu_;
 };

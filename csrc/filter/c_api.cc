@@ -39,8 +39,12 @@ void info_to_c(const TensorsInfo& a, NNSX_TensorsInfo* b) {
   }
 }
 
+// counts come from user code: never index past info[NNSX_SIZE_LIMIT]
+bool info_ok(const NNSX_TensorsInfo& b) { return b.num_tensors <= NNSX_SIZE_LIMIT; }
+
 void info_from_c(const NNSX_TensorsInfo& b, TensorsInfo* a) {
   *a = TensorsInfo();
+  if (!info_ok(b)) return;
   a->resize(b.num_tensors);
   a->format = static_cast<Format>(b.format);
   for (unsigned i = 0; i < b.num_tensors; ++i) {
@@ -81,6 +85,7 @@ extern "C" {
 int NNS_custom_easy_register(const char* modelname, NNS_custom_easy_invoke func, void* data,
                              const NNSX_TensorsInfo* in_info, const NNSX_TensorsInfo* out_info) {
   if (!modelname || !func || !in_info || !out_info) return -22;  // -EINVAL
+  if (!info_ok(*in_info) || !info_ok(*out_info)) return -22;
   {
     CustomEasyFn f;
     TensorsInfo a, b;
@@ -130,6 +135,10 @@ int nnstreamer_converter_custom_register(const char* name, tensor_converter_cust
     NNSX_TensorMemory out[NNSX_SIZE_LIMIT];
     std::memset(out, 0, sizeof(out));
     if (func(bytes.data(), bytes.size(), data, &c, out) != 0) return nullptr;
+    if (!info_ok(c.info)) {
+      NNSX_LOGE("c_api", "custom converter returned num_tensors=%u (limit %d)", c.info.num_tensors, NNSX_SIZE_LIMIT);
+      return nullptr;
+    }
     info_from_c(c.info, &config->info);
     config->rate_n = c.rate_n;
     config->rate_d = c.rate_d;

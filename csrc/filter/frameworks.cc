@@ -30,6 +30,10 @@ void to_c(const TensorsInfo& a, NNSX_TensorsInfo* b) {
 }
 
 void from_c(const NNSX_TensorsInfo& b, TensorsInfo* a) {
+  // the count comes from a user plugin: never index past info[NNSX_SIZE_LIMIT]
+  if (b.num_tensors > NNSX_SIZE_LIMIT)
+    throw Error("plugin returned num_tensors=" + std::to_string(b.num_tensors) + " (limit " +
+                std::to_string(NNSX_SIZE_LIMIT) + ")");
   *a = TensorsInfo();
   a->resize(b.num_tensors);
   a->format = static_cast<Format>(b.format);
@@ -91,6 +95,7 @@ class CustomSo : public FilterInstance {
   }
   int invoke(const std::vector<MemoryPtr>& in, std::vector<MemoryPtr>* out, InvokeContext&) override {
     NNSX_TensorMemory ci[NNSX_SIZE_LIMIT], co[NNSX_SIZE_LIMIT];
+    std::memset(ci, 0, sizeof(ci));
     std::memset(co, 0, sizeof(co));
     for (size_t i = 0; i < in.size() && i < NNSX_SIZE_LIMIT; ++i) {
       ci[i].data = const_cast<void*>(in[i]->map_host());

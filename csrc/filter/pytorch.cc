@@ -74,6 +74,14 @@ class TorchInstance : public FilterInstance {
     device_ = p.device;
     load(p.model_files.at(0));
   }
+  ~TorchInstance() override {
+    graphs_.clear();
+    if (cap_stream_) {
+      hip::DeviceGuard g(device_);
+      (void)hipStreamSynchronize(cap_stream_);
+      (void)hipStreamDestroy(cap_stream_);
+    }
+  }
 
   bool wants_host_input() const override { return device_ < 0; }
 
@@ -231,7 +239,7 @@ class TorchInstance : public FilterInstance {
 
     std::vector<at::Tensor> outs;
     if (use_graph_ && dev_idx >= 0) {
-      GraphState& gs = graph_for(inputs, s);
+      GraphState& gs = graph_for(inputs, s, dev_idx);
       for (size_t i = 0; i < inputs.size(); ++i) gs.static_in[i].copy_(inputs[i], /*non_blocking=*/true);
       gs.graph->replay();
       // replay reuses the static outputs: hand downstream a private copy
@@ -254,7 +262,13 @@ class TorchInstance : public FilterInstance {
     return 0;
   }
 
-  GraphState& graph_for(const std::vector<at::Tensor>& inputs, hipStream_t s) {
+  // Capture runs on a private stream of this filter, ordered after the element
+  // stream `s` by events.  `s` itself is never in capture mode, so other threads
+  // may keep enqueueing on it meanwhile -- e.g. the release of an earlier output
+  // still queued downstream makes `s` wait for that output's readers
+  // (wrap_output) -- which would otherwise invalidate a capture that starts
+  // after a hot reload or a new input shape.
+  GraphState& graph_for(const std::vector<at::Tensor>& inputs, hipStream_t s, int dev_idx) {
     std::string key;
     for (auto& t : inputs) {
       for (auto d : t.sizes()) key += std::to_string(d) + "x";
@@ -262,23 +276,34 @@ class TorchInstance : public FilterInstance {
     }
     auto it = graphs_.find(key);
     if (it != graphs_.end()) return *it->second;
+    hip::DeviceGuard dg(dev_idx);
+    if (!cap_stream_) hip::check(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "capture stream");
+    hipEvent_t ev;
+    hip::check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "capture event");
+    hip::check(hipEventRecord(ev, s), "capture event record");  // inputs were produced on s
+    hip::check(hipStreamWaitEvent(cap_stream_, ev, 0), "capture stream wait");
     auto gs = std::make_unique<GraphState>();
-    for (auto& t : inputs) gs->static_in.push_back(torch::empty_like(t, t.options()).copy_(t));
-    std::vector<c10::IValue> iv;
-    // warm up on the capture stream (lazy init, autotuning) before capturing
-    for (int w = 0; w < 3; ++w) {
+    {
+      c10::hip::HIPStreamGuardMasqueradingAsCUDA cg(
+          c10::hip::getStreamFromExternalMasqueradingAsCUDA(cap_stream_, static_cast<c10::DeviceIndex>(dev_idx)));
+      for (auto& t : inputs) gs->static_in.push_back(torch::empty_like(t, t.options()).copy_(t));
+      std::vector<c10::IValue> iv;
+      // warm up on the capture stream (lazy init, autotuning) before capturing
+      for (int w = 0; w < 3; ++w) {
+        iv.clear();
+        for (auto& t : gs->static_in) iv.push_back(prepare(t));
+        std::vector<at::Tensor> tmp;
+        flatten(module_.forward(iv), &tmp);
+      }
+      hip::check(hipStreamSynchronize(cap_stream_), "graph warmup sync");
+      gs->graph = std::make_unique<at::cuda::CUDAGraph>();
+      gs->graph->capture_begin({0, 0}, hipStreamCaptureModeThreadLocal);
       iv.clear();
       for (auto& t : gs->static_in) iv.push_back(prepare(t));
-      std::vector<at::Tensor> tmp;
-      flatten(module_.forward(iv), &tmp);
+      flatten(module_.forward(iv), &gs->static_out);
+      gs->graph->capture_end();
     }
-    hip::check(hipStreamSynchronize(s), "graph warmup sync");
-    gs->graph = std::make_unique<at::cuda::CUDAGraph>();
-    gs->graph->capture_begin({0, 0}, hipStreamCaptureModeThreadLocal);
-    iv.clear();
-    for (auto& t : gs->static_in) iv.push_back(prepare(t));
-    flatten(module_.forward(iv), &gs->static_out);
-    gs->graph->capture_end();
+    hip::check(hipEventDestroy(ev), "capture event destroy");
     NNSX_LOGI("pytorch", "captured hipGraph for input shape ", key);
     auto& ref = *gs;
     graphs_[key] = std::move(gs);
@@ -293,6 +318,7 @@ class TorchInstance : public FilterInstance {
   DType compute_dtype_ = DType::END;
   std::mutex mu_;
   std::map<std::string, std::unique_ptr<GraphState>> graphs_;
+  hipStream_t cap_stream_ = nullptr;  // private capture stream (graph_for)
 };
 
 class TorchFw : public FilterFramework {
