@@ -63,8 +63,11 @@ bool Registry::load_library(const std::string& path, std::string* err) {
     if (err) *err = dlerror();
     return false;
   }
-  std::lock_guard<std::mutex> lk(mu_);
-  handles_.push_back(h);
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    handles_.push_back(h);
+  }
+  if (hook_) hook_(h, path);
   return true;
 }
 

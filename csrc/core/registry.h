@@ -31,6 +31,10 @@ class Registry {
   std::vector<std::string> names(SubpluginKind kind, bool scan_paths = false);
   // dlopen a shared object explicitly
   bool load_library(const std::string& path, std::string* err = nullptr);
+  // called after every successful load_library() (outside the registry lock):
+  // the C sub-plugin ABI uses it to run the library's nnsx_subplugin_init()
+  using LibraryHook = void (*)(void* handle, const std::string& path);
+  void set_library_hook(LibraryHook h) { hook_ = h; }
 
   template <typename T>
   std::shared_ptr<T> find_as(SubpluginKind kind, const std::string& name, bool try_load = true) {
@@ -42,6 +46,7 @@ class Registry {
   std::mutex mu_;
   std::map<int, std::map<std::string, std::shared_ptr<void>>> tables_;
   std::vector<void*> handles_;
+  LibraryHook hook_ = nullptr;
 };
 
 // -------------------------------------------------------------- config ----
