@@ -255,10 +255,30 @@ class TensorIf : public Element {
       unsigned nth = static_cast<unsigned>(to_uint(cv_opt_));
       if (nth >= in.n_memory()) return false;
       const TensorInfo& ti = config_.info.at(nth);
-      const void* p = in.mems[nth]->map_host();
+      const MemoryPtr& m = in.mems[nth];
       uint64_t n = element_count(ti.dim);
       double avg = 0;
-      for (uint64_t i = 0; i < n; ++i) avg = (cpu::read_as_double(p, ti.type, i) - avg) / (i + 1) + avg;
+      if (m->on_device()) {
+        // K22: reduce on the GPU, only the 8-byte mean crosses to the host
+        const int dev = m->device();
+        hip::DeviceGuard g(dev);
+        hipStream_t s = streams_.get(dev);
+        if (!mean_ws_) {
+          mean_ws_ = Memory::alloc_device(kernels::mean_workspace_bytes(), dev, s);
+          mean_host_ = Memory::alloc_pinned(8);
+        }
+        double* ws = static_cast<double*>(mean_ws_->data());
+        if (!kernels::tensor_mean(m->map_device(dev, s), ti.type, n, ws, s)) return false;
+        hip::check(hipMemcpyAsync(mean_host_->data(), ws + kernels::mean_workspace_bytes() / 8 - 1, 8,
+                                  hipMemcpyDeviceToHost, s),
+                   "tensor_if mean D2H");
+        hip::check(hipStreamSynchronize(s), "tensor_if mean sync");
+        m->record_use(s, dev);
+        std::memcpy(&avg, mean_host_->data(), 8);
+      } else {
+        const void* p = m->map_host();
+        for (uint64_t i = 0; i < n; ++i) avg = (cpu::read_as_double(p, ti.type, i) - avg) / (i + 1) + avg;
+      }
       // the reference casts the average to the tensor type before comparing
       uint8_t tmp[8];
       cpu::write_from_double(tmp, ti.type, 0, avg);
@@ -286,6 +306,8 @@ class TensorIf : public Element {
   std::string cv_opt_, sv_str_, then_opt_, else_opt_;
   std::vector<double> sv_;
   TensorsConfig config_;
+  StreamSet streams_;             // device average (K22)
+  MemoryPtr mean_ws_, mean_host_;
 };
 
 
@@ -754,6 +776,82 @@ bool sparse_decode(const MemoryPtr& m, MemoryPtr* out, TensorInfo* ti) {
   return true;
 }
 
+
+// Device-resident tensors stay on the GPU (kernels/sparse.hip, K21): encode =
+// count + scan, one 4-byte read-back of nnz to size the output, then the
+// order-preserving compaction; decode = read back the 128-B header, zero-fill,
+// scatter.  Small pinned read-back slots per element.
+struct SparseDeviceCtx {
+  StreamSet streams;
+  MemoryPtr pinned;  // [0..3] nnz / bad flag, [128..255] header
+  uint8_t* host(int dev, hipStream_t) {
+    (void)dev;
+    if (!pinned) pinned = Memory::alloc_pinned(256);
+    return static_cast<uint8_t*>(pinned->data());
+  }
+};
+
+MemoryPtr sparse_encode_device(const MemoryPtr& m, const TensorInfo& ti, int dev, SparseDeviceCtx& c) {
+  hip::DeviceGuard g(dev);
+  hipStream_t s = c.streams.get(dev);
+  const void* x = m->map_device(dev, s);
+  const int es = static_cast<int>(dtype_size(ti.type));
+  const uint64_t n = element_count(ti.dim);
+  const uint32_t nt = kernels::sparse_tiles(n);
+  auto counts = Memory::alloc_device(std::max<size_t>(1, nt) * 4 + 4, dev, s);
+  uint32_t* d_counts = static_cast<uint32_t*>(counts->data());
+  uint32_t* d_nnz = d_counts + std::max<uint32_t>(1, nt);
+  if (!kernels::sparse_count(x, es, n, d_counts, d_nnz, s)) return nullptr;
+  uint8_t* h = c.host(dev, s);
+  hip::check(hipMemcpyAsync(h, d_nnz, 4, hipMemcpyDeviceToHost, s), "sparse nnz D2H");
+  hip::check(hipStreamSynchronize(s), "sparse nnz sync");
+  uint32_t nnz;
+  std::memcpy(&nnz, h, 4);
+  MetaInfo meta = MetaInfo::from_info(ti, Format::SPARSE);
+  meta.nnz = nnz;
+  uint8_t hdr[kMetaHeaderSize];
+  meta.write(hdr);
+  auto out = Memory::alloc_device(kMetaHeaderSize + static_cast<size_t>(nnz) * (es + 4), dev, s);
+  if (!kernels::sparse_compact(x, es, n, d_counts, out->data(), nnz, hdr, s)) return nullptr;
+  m->record_use(s, dev);
+  counts->record_use(s, dev);
+  out->mark_ready(s);
+  return out;
+}
+
+bool sparse_decode_device(const MemoryPtr& m, MemoryPtr* out, TensorInfo* ti, int dev, SparseDeviceCtx& c) {
+  hip::DeviceGuard g(dev);
+  hipStream_t s = c.streams.get(dev);
+  if (m->size() < kMetaHeaderSize) return false;
+  const uint8_t* src = static_cast<const uint8_t*>(m->map_device(dev, s));
+  uint8_t* h = c.host(dev, s);
+  hip::check(hipMemcpyAsync(h + 128, src, kMetaHeaderSize, hipMemcpyDeviceToHost, s), "sparse header D2H");
+  hip::check(hipStreamSynchronize(s), "sparse header sync");
+  MetaInfo meta;
+  if (!MetaInfo::parse(h + 128, kMetaHeaderSize, &meta) || meta.format != static_cast<uint32_t>(Format::SPARSE))
+    return false;
+  if (!meta.to_info(ti)) return false;
+  const size_t es = dtype_size(ti->type);
+  if (kMetaHeaderSize + static_cast<size_t>(meta.nnz) * (es + 4) > m->size()) return false;
+  auto o = Memory::alloc_device(ti->size(), dev, s);
+  auto flag = Memory::alloc_device(4, dev, s);
+  int* d_bad = static_cast<int*>(flag->data());
+  hip::check(hipMemsetAsync(o->data(), 0, o->size(), s), "sparse zero fill");
+  hip::check(hipMemsetAsync(d_bad, 0, 4, s), "sparse flag clear");
+  if (!kernels::sparse_scatter(src + kMetaHeaderSize, static_cast<int>(es), meta.nnz, o->data(),
+                               element_count(ti->dim), d_bad, s))
+    return false;
+  hip::check(hipMemcpyAsync(h, d_bad, 4, hipMemcpyDeviceToHost, s), "sparse flag D2H");
+  hip::check(hipStreamSynchronize(s), "sparse decode sync");
+  int bad;
+  std::memcpy(&bad, h, 4);
+  if (bad) return false;
+  m->record_use(s, dev);
+  o->mark_ready(s);
+  *out = o;
+  return true;
+}
+
 class TensorSparseEnc : public BaseTransform {
  public:
   explicit TensorSparseEnc(const std::string& name)
@@ -779,14 +877,20 @@ class TensorSparseEnc : public BaseTransform {
     if (!buffer_from_config(inbuf, config_, &in)) return FlowReturn::ERROR;
     auto out = make_buffer();
     out->copy_metadata_from(*in);
-    for (size_t i = 0; i < in->n_memory(); ++i)
-      out->mems.push_back(sparse_encode(in->mems[i], config_.info.at(static_cast<unsigned>(i))));
+    for (size_t i = 0; i < in->n_memory(); ++i) {
+      const MemoryPtr& m = in->mems[i];
+      const TensorInfo& ti = config_.info.at(static_cast<unsigned>(i));
+      MemoryPtr o = m->on_device() ? sparse_encode_device(m, ti, m->device(), dev_) : sparse_encode(m, ti);
+      if (!o) return FlowReturn::ERROR;
+      out->mems.push_back(o);
+    }
     *outbuf = out;
     return FlowReturn::OK;
   }
 
  private:
   TensorsConfig config_;
+  SparseDeviceCtx dev_;
 };
 
 class TensorSparseDec : public BaseTransform {
@@ -826,7 +930,8 @@ class TensorSparseDec : public BaseTransform {
     for (auto& m : split_in->mems) {
       MemoryPtr o;
       TensorInfo ti;
-      if (!sparse_decode(m, &o, &ti)) {
+      const bool ok = m->on_device() ? sparse_decode_device(m, &o, &ti, m->device(), dev_) : sparse_decode(m, &o, &ti);
+      if (!ok) {
         post_error("tensor_sparse_dec: invalid sparse tensor");
         return FlowReturn::ERROR;
       }
@@ -852,6 +957,7 @@ class TensorSparseDec : public BaseTransform {
 
  private:
   TensorsConfig last_;
+  SparseDeviceCtx dev_;
 };
 
 // ============================================================= tensor_debug ====

@@ -78,5 +78,24 @@ void argmax(const void* in, DType t, uint64_t n, int32_t* out_index, hipStream_t
 // Batched argmax: rows of `n` elements, `batch` rows -> out_index[batch]
 void argmax_rows(const void* in, DType t, uint64_t n, uint32_t batch, int32_t* out_index, hipStream_t s);
 
+// sparse tensor codec (sparse.hip; gsttensor_sparseutil.c): elem_size 1/2/4/8.
+// Encode = sparse_count (tile counts -> exclusive offsets in d_counts, total
+// -> *d_nnz; d_counts holds sparse_tiles(n) entries) then, once the host knows
+// nnz, sparse_compact (header + nnz values + nnz uint32 indices into out).
+uint32_t sparse_tiles(uint64_t n);
+bool sparse_count(const void* x, int elem_size, uint64_t n, uint32_t* d_counts, uint32_t* d_nnz, hipStream_t s);
+bool sparse_compact(const void* x, int elem_size, uint64_t n, const uint32_t* d_offsets, void* out, uint32_t nnz,
+                    const void* header128, hipStream_t s);
+// decode: out (n elements, zero-filled by the caller) <- payload (values then
+// indices); *d_bad = 1 on an index >= n
+bool sparse_scatter(const void* payload, int elem_size, uint32_t nnz, void* out, uint64_t n, int* d_bad,
+                    hipStream_t s);
+
+// tensor_if TENSOR_AVERAGE on a device tensor (sparse.hip, K22): the fp64
+// mean lands at d_ws[mean_workspace_bytes() / 8 - 1]; d_ws holds
+// mean_workspace_bytes()
+size_t mean_workspace_bytes();
+bool tensor_mean(const void* x, DType t, uint64_t n, double* d_ws, hipStream_t s);
+
 }  // namespace kernels
 }  // namespace nnsx
