@@ -42,7 +42,7 @@ constexpr float kYoloConf = 0.25f, kYoloIou = 0.45f;
 constexpr unsigned kPalmMax = 2016;
 constexpr int kNmsCap = 4096;  // device NMS capacity per frame (top-scoring candidates)
 
-const uint8_t kFont[95][7] = NNSX_FONT5X7_DATA;
+const uint8_t kFont[95][13] = NNSX_FONT8X13_DATA;
 
 struct Det {
   bool valid = false;
@@ -143,8 +143,9 @@ class BoundingBoxes : public DecoderInstance {
       return FlowReturn::ERROR;
     }
     use_labels_ = !labels_.empty();
-    const bool gpu_mode = (mode_ == SSD || mode_ == OLD_SSD || mode_ == YOLOV5) &&
-                          config.info.at(0).type == DType::FLOAT32 && ctx.device >= 0;
+    // every mode has a device path for float32 tensors (K9-K12 + ov-*); other
+    // element types decode on the host
+    const bool gpu_mode = config.info.at(0).type == DType::FLOAT32 && ctx.device >= 0;
     ctx.out_frames = batch;
     if (gpu_mode) return decode_device(config, in, out, ctx, batch);
     const size_t fsize = static_cast<size_t>(width_) * height_ * 4;
@@ -595,7 +596,9 @@ class BoundingBoxes : public DecoderInstance {
                            InvokeContext& ctx, unsigned batch) {
     const int dev = ctx.device;
     hipStream_t s = ctx.stream;
-    const int n = static_cast<int>(is_ssd() ? std::min(max_detection_, kSsdMax) : max_detection_);
+    const int n = static_cast<int>(is_ssd()                                ? std::min(max_detection_, kSsdMax)
+                                   : (mode_ == OV_PERSON || mode_ == OV_FACE) ? kOvMax
+                                                                               : max_detection_);
     const int k = std::min(kNmsCap, (n + 63) / 64 * 64);
     const size_t need = kernels::det_scratch_bytes(n, k, static_cast<int>(batch));
     if (!scratch_ || scratch_->size() < need || scratch_->device() != dev) {
@@ -621,6 +624,33 @@ class BoundingBoxes : public DecoderInstance {
       kernels::ssd_candidates(boxes, scores, static_cast<const float*>(dev_priors_->data()),
                               static_cast<int>(config.info.at(1).dim[0]), static_cast<int>(batch), p, ds, s);
       kernels::sort_nms(ds, static_cast<int>(batch), ssd_params_[5], s);
+    } else if (is_ssd_pp()) {
+      auto ptr = [&](int i) { return static_cast<const float*>(in[static_cast<size_t>(pp_map_[i])]->map_device(dev, s)); };
+      kernels::pp_candidates(ptr(0), ptr(1), ptr(2), ptr(3),
+                             static_cast<int>(config.info.at(static_cast<unsigned>(pp_map_[0])).dim[0]), pp_thr_,
+                             static_cast<int>(i_width_), static_cast<int>(i_height_), ds, s);
+      kernels::sort_keep_all(ds, 1, s);
+    } else if (mode_ == OV_PERSON || mode_ == OV_FACE) {
+      kernels::ov_candidates(static_cast<const float*>(in[0]->map_device(dev, s)), kOvConf, static_cast<int>(i_width_),
+                             static_cast<int>(i_height_), ds, s);
+      kernels::sort_keep_all(ds, 1, s);
+    } else if (mode_ == MP_PALM) {
+      if (!dev_anchors_ || dev_anchors_->device() != dev || dev_anchor_count_ != anchors_.size()) {
+        std::vector<float> flat;
+        for (const Anchor& a : anchors_) flat.insert(flat.end(), {a.xc, a.yc, a.w, a.h});
+        dev_anchors_ = Memory::alloc_device(flat.size() * sizeof(float), dev, s);
+        hip::check(hipMemcpyAsync(dev_anchors_->data(), flat.data(), flat.size() * sizeof(float),
+                                  hipMemcpyHostToDevice, s),
+                   "anchors H2D");
+        hip::check(hipStreamSynchronize(s), "anchors sync");
+        dev_anchor_count_ = anchors_.size();
+      }
+      kernels::palm_candidates(static_cast<const float*>(in[0]->map_device(dev, s)),
+                               static_cast<const float*>(in[1]->map_device(dev, s)),
+                               static_cast<const float*>(dev_anchors_->data()),
+                               static_cast<int>(config.info.at(0).dim[0]), palm_thr_, static_cast<int>(i_width_),
+                               static_cast<int>(i_height_), ds, s);
+      kernels::sort_nms(ds, 1, 0.05f, s);
     } else {
       const float* x = static_cast<const float*>(in[0]->map_device(dev, s));
       kernels::yolov5_candidates(x, static_cast<int>(labels_.size()), static_cast<int>(batch), kYoloConf,
@@ -678,7 +708,8 @@ class BoundingBoxes : public DecoderInstance {
   std::vector<int> palm_strides_ = {8, 16, 16, 16};
   std::vector<Anchor> anchors_;
   // device state
-  MemoryPtr scratch_, dev_priors_, dev_labels_, dev_label_offs_;
+  MemoryPtr scratch_, dev_priors_, dev_labels_, dev_label_offs_, dev_anchors_;
+  size_t dev_anchor_count_ = 0;
   std::vector<Det> last_;
 };
 

@@ -34,7 +34,7 @@ namespace nnsx {
 
 namespace {
 
-const uint8_t kFontTable[95][7] = NNSX_FONT5X7_DATA;
+const uint8_t kFontTable[95][13] = NNSX_FONT8X13_DATA;
 
 bool rest_ones(const Dims& d, int from) {
   for (int i = from; i < kRankLimit; ++i)

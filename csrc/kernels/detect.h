@@ -52,6 +52,18 @@ void ssd_candidates(const float* boxes, const float* scores, const float* priors
 void yolov5_candidates(const float* in, int classes, int batch, float conf_threshold, int scaled_output,
                        int i_width, int i_height, const DetScratch& s, hipStream_t stream);
 
+// mobilenet-ssd-postprocess / tf-ssd (one frame): loc [n][bpi] (ymin, xmin,
+// ymax, xmax), cls [n], score [n], num [1]; drawn in input order, no NMS
+void pp_candidates(const float* loc, const float* cls, const float* score, const float* num, int bpi, float thr,
+                   int i_width, int i_height, const DetScratch& s, hipStream_t stream);
+// ov-person / ov-face (one frame): in [n <= 256][7]; drawn in input order, no NMS
+void ov_candidates(const float* in, float conf, int i_width, int i_height, const DetScratch& s, hipStream_t stream);
+// mp-palm-detection (one frame): boxes [n][bpi], scores [n] (logits), anchors [n][4] (xc, yc, w, h)
+void palm_candidates(const float* boxes, const float* scores, const float* anchors, int bpi, float thr, int i_width,
+                     int i_height, const DetScratch& s, hipStream_t stream);
+// order-preserving modes: sort by the candidates' order keys, keep all
+void sort_keep_all(const DetScratch& s, int batch, hipStream_t stream);
+
 // sort + NMS (suppress when IoU > iou_threshold, reference integer-box IoU)
 void sort_nms(const DetScratch& s, int batch, float iou_threshold, hipStream_t stream);
 

@@ -10,6 +10,8 @@
 // reference (tensordec-boundingbox.c:1215-1262) in O(n) wave steps.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "decoders/font.h"
 #include "kernels/detect.h"
 
@@ -18,7 +20,7 @@ namespace kernels {
 
 namespace {
 
-__constant__ uint8_t kFontDev[95][7] = NNSX_FONT5X7_DATA;
+__constant__ uint8_t kFontDev[95][13] = NNSX_FONT8X13_DATA;
 
 constexpr int kLdsKeys = 8192;  // 64 KiB of keys per workgroup
 
@@ -29,6 +31,14 @@ inline int next_pow2(int x) {
   while (p < x) p <<= 1;
   return p;
 }
+
+// exp as the host decoder computes it (glibc expf, correctly rounded in
+// practice): the fp64 exp rounded once to fp32, so device and host boxes
+// truncate to the same integers
+__device__ inline float exp_ref(float x) { return static_cast<float>(exp(static_cast<double>(x))); }
+
+// sort keys that keep the input order (modes drawn without NMS)
+__device__ inline uint64_t order_key(int anchor) { return static_cast<uint32_t>(anchor); }
 
 __device__ inline uint64_t make_key(float score, int anchor) {
   // ascending key order == score descending, anchor ascending (stable sort order)
@@ -58,12 +68,12 @@ __global__ void __launch_bounds__(256) ssd_cand_kernel(const float* __restrict__
   }
   if (found < 0 || lane != 0) return;
   const float* bx = boxes + (static_cast<size_t>(b) * n + a) * 4;
-  const float score = 1.f / (1.f + expf(-det[found]));
+  const float score = 1.f / (1.f + exp_ref(-det[found]));
   const float py = priors[a], px = priors[n + a], ph = priors[2 * n + a], pw = priors[3 * n + a];
   const float ycenter = bx[0] / p.y_scale * ph + py;
   const float xcenter = bx[1] / p.x_scale * pw + px;
-  const float h = expf(bx[2] / p.h_scale) * ph;
-  const float w = expf(bx[3] / p.w_scale) * pw;
+  const float h = exp_ref(bx[2] / p.h_scale) * ph;
+  const float w = exp_ref(bx[3] / p.w_scale) * pw;
   const float ymin = ycenter - h / 2.f;
   const float xmin = xcenter - w / 2.f;
   const int x = static_cast<int>(xmin * p.i_width);
@@ -123,6 +133,90 @@ __global__ void __launch_bounds__(256) yolo_cand_kernel(const float* __restrict_
   s.prob[o] = score;
   const int slot = atomicAdd(&s.count[b], 1);
   s.keys[static_cast<size_t>(b) * s.key_cap + slot] = make_key(score, a);
+}
+
+// mobilenet-ssd-postprocess / tf-ssd (K10, tensordec-boundingbox.c:1309-1341):
+// the model already ran NMS; every detection d < num with score >= threshold
+// is drawn, in input order.  Float32 arithmetic as the host path.
+__global__ void __launch_bounds__(256) pp_cand_kernel(const float* __restrict__ loc, const float* __restrict__ cls,
+                                                      const float* __restrict__ score, const float* __restrict__ num,
+                                                      int bpi, float thr, int iw, int ih, DetScratch s) {
+#pragma clang fp contract(off)
+  const int d = blockIdx.x * 256 + threadIdx.x;
+  const int n = min(static_cast<int>(num[0]), s.n);
+  if (d >= n) return;
+  const float sc = score[d];
+  if (sc < thr) return;
+  auto c01 = [](float v) { return fminf(fmaxf(v, 0.f), 1.f); };
+  const float* b = loc + static_cast<size_t>(d) * bpi;
+  const float y1 = c01(b[0]), x1 = c01(b[1]), y2 = c01(b[2]), x2 = c01(b[3]);
+  s.box[d] = make_int4(static_cast<int>(x1 * static_cast<float>(iw)), static_cast<int>(y1 * static_cast<float>(ih)),
+                       static_cast<int>((x2 - x1) * static_cast<float>(iw)),
+                       static_cast<int>((y2 - y1) * static_cast<float>(ih)));
+  s.cls[d] = static_cast<int>(cls[d]);
+  s.prob[d] = sc;
+  const int slot = atomicAdd(&s.count[0], 1);
+  s.keys[slot] = order_key(d);
+}
+
+// ov-person-detection / ov-face-detection: [200][7] rows (image_id, label,
+// conf, x_min, y_min, x_max, y_max); the list ends at the first negative
+// image_id; rows with conf >= 0.8 are drawn in order (fp64 box math as the
+// host path).  One workgroup: the end marker is a workgroup min-reduction.
+__global__ void __launch_bounds__(256) ov_cand_kernel(const float* __restrict__ in, int rows, float conf, int iw,
+                                                      int ih, DetScratch s) {
+  __shared__ int first_end;
+  const int d = threadIdx.x;
+  if (d == 0) first_end = rows;
+  __syncthreads();
+  const float* r = in + static_cast<size_t>(d) * 7;
+  if (d < rows && static_cast<int>(static_cast<double>(r[0])) < 0) atomicMin(&first_end, d);
+  __syncthreads();
+  if (d >= first_end || d >= rows) return;
+  if (static_cast<double>(r[2]) < static_cast<double>(conf)) return;
+  const double x0 = r[3], y0 = r[4], x1 = r[5], y1 = r[6];
+  s.box[d] = make_int4(static_cast<int>(x0 * iw), static_cast<int>(y0 * ih), static_cast<int>((x1 - x0) * iw),
+                       static_cast<int>((y1 - y0) * ih));
+  s.cls[d] = -1;
+  s.prob[d] = 1.f;
+  const int slot = atomicAdd(&s.count[0], 1);
+  s.keys[slot] = order_key(d);
+}
+
+// mp-palm-detection (K12, tensordec-boundingbox.c:1407-1451): sigmoid of the
+// clamped logit, anchor-relative box; NMS at IoU 0.05 follows.
+__global__ void __launch_bounds__(256) palm_cand_kernel(const float* __restrict__ boxes,
+                                                        const float* __restrict__ scores,
+                                                        const float* __restrict__ anchors, int bpi, float thr, int iw,
+                                                        int ih, DetScratch s) {
+#pragma clang fp contract(off)
+  const int d = blockIdx.x * 256 + threadIdx.x;
+  if (d >= s.n) return;
+  float sc = fminf(fmaxf(scores[d], -100.f), 100.f);
+  sc = 1.0f / (1.0f + exp_ref(-sc));
+  if (sc < thr) return;
+  const float* a = anchors + static_cast<size_t>(d) * 4;  // xc, yc, w, h
+  const float* b = boxes + static_cast<size_t>(d) * bpi;
+  const float fw = static_cast<float>(iw), fh = static_cast<float>(ih);
+  const float yc = b[0] / fh * a[3] + a[1];
+  const float xc = b[1] / fw * a[2] + a[0];
+  const float h = b[2] / fh * a[3];
+  const float w = b[3] / fw * a[2];
+  const float ymin = yc - h / 2.f, xmin = xc - w / 2.f;
+  s.box[d] = make_int4(max(0, static_cast<int>(xmin * fw)), max(0, static_cast<int>(ymin * fh)),
+                       static_cast<int>(w * fw), static_cast<int>(h * fh));
+  s.cls[d] = 0;
+  s.prob[d] = sc;
+  const int slot = atomicAdd(&s.count[0], 1);
+  s.keys[slot] = make_key(sc, d);
+}
+
+// modes without NMS: keep every sorted candidate
+__global__ void keep_all_kernel(DetScratch s) {
+  const int b = blockIdx.x;
+  const int n = s.count[b];
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s.kept[static_cast<size_t>(b) * s.k + i] = i;
+  if (threadIdx.x == 0) s.nkept[b] = n;
 }
 
 __device__ void bitonic_sort(uint64_t* a, int m) {
@@ -342,6 +436,32 @@ void yolov5_candidates(const float* in, int classes, int batch, float conf_thres
   dim3 grid((s.n + 3) / 4, batch);
   hipLaunchKernelGGL(yolo_cand_kernel, grid, dim3(256), 0, stream, in, classes, conf_threshold, scaled_output,
                      i_width, i_height, s);
+}
+
+void pp_candidates(const float* loc, const float* cls, const float* score, const float* num, int bpi, float thr,
+                   int i_width, int i_height, const DetScratch& s, hipStream_t stream) {
+  hipMemsetAsync(s.count, 0, sizeof(int), stream);
+  hipLaunchKernelGGL(pp_cand_kernel, dim3((s.n + 255) / 256), dim3(256), 0, stream, loc, cls, score, num, bpi, thr,
+                     i_width, i_height, s);
+}
+
+void ov_candidates(const float* in, float conf, int i_width, int i_height, const DetScratch& s, hipStream_t stream) {
+  hipMemsetAsync(s.count, 0, sizeof(int), stream);
+  hipLaunchKernelGGL(ov_cand_kernel, dim3(1), dim3(256), 0, stream, in, std::min(s.n, 256), conf, i_width, i_height,
+                     s);
+}
+
+void palm_candidates(const float* boxes, const float* scores, const float* anchors, int bpi, float thr, int i_width,
+                     int i_height, const DetScratch& s, hipStream_t stream) {
+  hipMemsetAsync(s.count, 0, sizeof(int), stream);
+  hipLaunchKernelGGL(palm_cand_kernel, dim3((s.n + 255) / 256), dim3(256), 0, stream, boxes, scores, anchors, bpi,
+                     thr, i_width, i_height, s);
+}
+
+void sort_keep_all(const DetScratch& s, int batch, hipStream_t stream) {
+  const int lds_keys = std::min(s.key_cap, kLdsKeys);
+  hipLaunchKernelGGL(sort_kernel, dim3(batch), dim3(1024), sizeof(uint64_t) * lds_keys, stream, s);
+  hipLaunchKernelGGL(keep_all_kernel, dim3(batch), dim3(256), 0, stream, s);
 }
 
 void sort_nms(const DetScratch& s, int batch, float iou_threshold, hipStream_t stream) {

@@ -174,7 +174,7 @@ __constant__ int kDotX[40] = {-4, 0, 4, 0,  -3, -3, -3, -2, -2, -2, -2, -2, -1, 
                               0,  0, 0, 0,  0,  1,  1,  1,  1,  1,  1,  1,  2,  2,  2,  2,  2,  3,  3,  3};
 __constant__ int kDotY[40] = {0,  -4, 0,  4,  -1, 0,  1,  -2, -1, 0,  1,  2,  -3, -2, -1, 0,  1,  2,  3,  -3,
                               -2, -1, 1,  2,  3,  -3, -2, -1, 0,  1,  2,  3,  -2, -1, 0,  1,  2,  -1, 0,  1};
-__constant__ uint8_t kFontPose[95][7] = NNSX_FONT5X7_DATA;
+__constant__ uint8_t kFontPose[95][13] = NNSX_FONT8X13_DATA;
 
 __global__ void __launch_bounds__(256) pose_draw_kernel(PoseDrawArgs a) {
   __shared__ int px[64], py[64];

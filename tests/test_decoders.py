@@ -3,16 +3,20 @@
 are read in place from /root/reference (raw float tensors / text); tests skip
 when the reference tree is not mounted.  The muxes run sync-mode=nosync: the
 reference pairs the file frames through GStreamer preroll timestamps (pts 0
-before PLAYING), which a running-time stamped stream does not reproduce.  Labels are rendered with nnsx's own
-glyphs, so comparisons mask the label cells (computed by rendering the same
-frame with option9=solid) and compare every other pixel exactly."""
+before PLAYING), which a running-time stamped stream does not reproduce.  Labels
+are drawn with the reference's own 8x13 raster font (csrc/decoders/font.h), so the
+RGBA output, swapped to the golden's BGRx byte order, must equal the golden file
+byte for byte -- boxes and label glyphs alike."""
 import os
 
 import numpy as np
 import pytest
 
 REF = "/root/reference/tests"
-BB = f"{REF}/nnstreamer_decoder_boundingbox"
+# the bounding-box fixtures travel in-tree (tests/fixtures, copied from the reference's
+# tests/nnstreamer_decoder_boundingbox) so GPU boxes without the reference run them too
+_LOCAL_BB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fixtures", "nnstreamer_decoder_boundingbox")
+BB = _LOCAL_BB if os.path.isdir(_LOCAL_BB) else f"{REF}/nnstreamer_decoder_boundingbox"
 
 needs_ref = pytest.mark.skipif(not os.path.isdir(BB), reason="reference fixtures not mounted")
 
@@ -37,32 +41,18 @@ def _bgrx_red_mask(path, w, h):
     return (a[..., 2] == 255) & (a[..., 1] == 0) & (a[..., 0] == 0)
 
 
-def _compare_with_golden(mine, solid, golden_paths, w, h):
-    for m, s, g in zip(mine, solid, golden_paths):
-        mm = _rgba_to_red_mask(m, w, h)
-        gm = _bgrx_red_mask(g, w, h)
-        cells = _label_cells(s, m, w, h)
-        assert np.array_equal(mm & ~cells, gm & ~cells), f"{g}: {np.argwhere((mm ^ gm) & ~cells)[:10]}"
-        assert mm.any() and gm.any()
+def _compare_with_golden(mine, golden_paths, w, h):
+    """Byte-exact: the decoder's RGBA frame in the golden's BGRx byte order."""
+    for m, g in zip(mine, golden_paths):
+        bgrx = np.frombuffer(m, np.uint8).reshape(h, w, 4)[..., [2, 1, 0, 3]]
+        gold = np.fromfile(g, np.uint8).reshape(h, w, 4)
+        diff = np.argwhere(np.any(bgrx != gold, axis=-1))
+        assert diff.size == 0, f"{g}: {len(diff)} pixels differ, first {diff[:10].tolist()}"
+        assert _bgrx_red_mask(g, w, h).any()
 
 
-def _label_cells(solid, mine, w, h):
-    """Pixels that belong to label cells: red in the solid rendering but whose value
-    comes from a label sprite (differs between font and solid rendering, or is red
-    in solid and black in font)."""
-    s = np.frombuffer(solid, np.uint8).reshape(h, w, 4)
-    m = np.frombuffer(mine, np.uint8).reshape(h, w, 4)
-    differ = np.any(s != m, axis=-1)
-    # grow each differing pixel to its full 8x13 cell neighbourhood (cells are axis-aligned blocks)
-    cells = np.zeros((h, w), bool)
-    ys, xs = np.nonzero(differ)
-    for y, x in zip(ys, xs):
-        cells[max(0, y - 13):y + 14, max(0, x - 8):x + 9] = True
-    return cells
-
-
-def _ssd_desc(mode, style):
-    return (f"tensor_mux name=mux sync-mode=nosync ! tensor_decoder mode=bounding_boxes option1={mode} "
+def _ssd_desc(mode, style, dev=-1):
+    return (f"tensor_mux name=mux sync-mode=nosync ! tensor_decoder mode=bounding_boxes option1={mode} device={dev} "
             f"option2={BB}/coco_labels_list.txt option3={BB}/box_priors.txt option4=160:120 option5=300:300 "
             f"option9={style} ! tensor_sink name=sink "
             f"multifilesrc location={BB}/mobilenetssd_tensors.0.%d start-index=0 stop-index=1 "
@@ -75,17 +65,16 @@ def _ssd_desc(mode, style):
 @pytest.mark.parametrize("mode", ["mobilenet-ssd", "tflite-ssd"])
 def test_bbox_mobilenet_ssd_golden(nns, mode):
     mine = _run_frames(nns, _ssd_desc(mode, "font"), 2)
-    solid = _run_frames(nns, _ssd_desc(mode, "solid"), 2)
-    _compare_with_golden(mine, solid, [f"{BB}/mobilenetssd_golden.{i}" for i in range(2)], 160, 120)
+    _compare_with_golden(mine, [f"{BB}/mobilenetssd_golden.{i}" for i in range(2)], 160, 120)
 
 
-def _pp_desc(mode, style):
+def _pp_desc(mode, style, dev=-1):
     src = ""
     dims = ["1", "100:1", "100:1", "4:100:1"]
     for i, d in enumerate(dims):
         src += (f" multifilesrc location={BB}/mobilenetssd_postprocess_tensors.{i}.%d start-index=0 stop-index=1 "
                 f"caps=application/octet-stream ! tensor_converter input-dim={d} input-type=float32 ! mux.sink_{i}")
-    return (f"tensor_mux name=mux sync-mode=nosync ! tensor_decoder mode=bounding_boxes option1={mode} "
+    return (f"tensor_mux name=mux sync-mode=nosync ! tensor_decoder mode=bounding_boxes option1={mode} device={dev} "
             f"option2={BB}/coco_labels_list.txt option4=160:120 option5=640:480 option9={style} "
             "! tensor_sink name=sink" + src)
 
@@ -94,19 +83,22 @@ def _pp_desc(mode, style):
 @pytest.mark.parametrize("mode", ["mobilenet-ssd-postprocess", "tf-ssd"])
 def test_bbox_ssd_postprocess_golden(nns, mode):
     mine = _run_frames(nns, _pp_desc(mode, "font"), 2)
-    solid = _run_frames(nns, _pp_desc(mode, "solid"), 2)
-    _compare_with_golden(mine, solid, [f"{BB}/mobilenetssd_postprocess_golden.{i}" for i in range(2)], 160, 120)
+    _compare_with_golden(mine, [f"{BB}/mobilenetssd_postprocess_golden.{i}" for i in range(2)], 160, 120)
 
 
-@needs_ref
-def test_bbox_palm_detection_golden(nns):
-    desc = ("tensor_mux name=mux sync-mode=nosync ! tensor_decoder mode=bounding_boxes option1=mp-palm-detection "
+def _palm_desc(dev=-1):
+    return (f"tensor_mux name=mux sync-mode=nosync ! tensor_decoder mode=bounding_boxes option1=mp-palm-detection "
+            f"device={dev} "
             "option3=0.5:4:1.0:1.0:0.5:0.5:8:16:16:16 option4=160:120 option5=300:300 ! tensor_sink name=sink "
             f"multifilesrc location={BB}/palm_detection_input_0.%d start-index=0 stop-index=1 "
             "caps=application/octet-stream ! tensor_converter input-dim=18:2016:1:1 input-type=float32 ! mux.sink_0 "
             f"multifilesrc location={BB}/palm_detection_input_1.%d start-index=0 stop-index=1 "
             "caps=application/octet-stream ! tensor_converter input-dim=1:2016:1:1 input-type=float32 ! mux.sink_1")
-    mine = _run_frames(nns, desc, 2)
+
+
+@needs_ref
+def test_bbox_palm_detection_golden(nns):
+    mine = _run_frames(nns, _palm_desc(), 2)
     for i, m in enumerate(mine):
         g = np.fromfile(f"{BB}/palm_detection_result_golden.{i}", np.uint8)
         # golden is RGBA after videoconvert: identical bytes expected (no labels in palm mode)

@@ -95,7 +95,7 @@ def test_ssd_pipeline_device_decoder_matches_host(nns, workdir):
     for (_, a), (_, b) in zip(res[0], res[-1]):
         a = np.frombuffer(a, np.uint32)
         b = np.frombuffer(b, np.uint32)
-        assert (a == b).mean() > 0.995
+        assert np.array_equal(a, b), (a != b).sum()
 
 
 def test_deeplab_pipeline(nns, workdir):
