@@ -71,6 +71,9 @@ def parse_args(argv=None):
                     help="keep the normalisation as a separate tensor_transform element")
     ap.add_argument("--cpu", action="store_true", help="CPU reference path (device=-1, torch CPU)")
     ap.add_argument("--queue", type=int, default=4, help="queue depth between filter and decoder")
+    ap.add_argument("--model-broadcast", default=os.environ.get("NNSX_BENCH_BCAST", "tcp"),
+                    choices=["off", "tcp", "rccl", "auto"],
+                    help="N > 1: rank 0 broadcasts the model bytes to every rank at load over this data plane")
     ap.add_argument("--comm-backend", default="auto", choices=["auto", "rccl", "tcp"],
                     help="posenet_multi: tensor_allgather data plane")
     ap.add_argument("--config", default=os.environ.get("NNSX_BENCH_CONFIG", "mbv2"),
@@ -181,9 +184,15 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
     frame_bytes = S * S * 3
     pool = max(64, -(-512 * 2**20 // frame_bytes)) if use_gpu else 16
     pool = min(pool, max(frames, 16))
+    # with several ranks the model is loaded once: rank 0 reads the file and
+    # broadcasts its bytes to every rank at filter start (custom=broadcast:0;
+    # --model-broadcast selects the data plane, TCP store by default)
+    bcast = ""
+    if world > 1 and a.model_broadcast != "off" and not cfg.get("fan"):  # (fan-out: rank 0 runs no filter)
+        bcast = f",broadcast:0,broadcast-backend:{a.model_broadcast},broadcast-name:{model_name}-b{B}"
     filt = (f"tensor_filter name=filt framework=pytorch model={model_path} input=3:{S}:{S}:{B} "
             f"inputtype={'uint8' if fuse_norm else 'float32'} accelerator={accel} device={dev} "
-            f"custom=hipgraph:{graph} device-stats={'true' if use_gpu else 'false'} ")
+            f"custom=hipgraph:{graph}{bcast} device-stats={'true' if use_gpu else 'false'} ")
     live = f"is-live=true " if live_fps > 0 else ""
     desc = (
         f"videotestsrc num-buffers={frames} pattern=snow pool-size={pool} {live}"

@@ -13,11 +13,18 @@
 //   hipgraph:true|false   capture/replay the forward (static shapes)
 //   dtype:bfloat16|float16|float32   cast floating inputs before forward
 //   channels_last:true    pass 4-D inputs in channels-last memory format
+//   broadcast:<rank>      load the model once: <rank> broadcasts the file's bytes
+//                         to every rank of the job (RCCL / TCP), see load_broadcast
+//   broadcast-backend:auto|rccl|tcp, broadcast-store:host:port, broadcast-name:<channel>
 #include <ATen/hip/HIPGraph.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/script.h>
 
+#include <fstream>
+#include <sstream>
+
+#include "comm/group.h"
 #include "core/log.h"
 #include "filter/filter.h"
 #include "filter/torch_util.h"
@@ -165,6 +172,10 @@ class TorchInstance : public FilterInstance {
       if (k == "hipgraph" || k == "graph") use_graph_ = to_bool(v, false);
       else if (k == "dtype") compute_dtype_ = dtype_from_string(v);
       else if (k == "channels_last") channels_last_ = to_bool(v, false);
+      else if (k == "broadcast") bcast_root_ = static_cast<int>(to_int(v));
+      else if (k == "broadcast-backend") bcast_backend_ = v;
+      else if (k == "broadcast-store") bcast_store_ = v;
+      else if (k == "broadcast-name") bcast_name_ = v;
     }
   }
 
@@ -179,7 +190,53 @@ class TorchInstance : public FilterInstance {
     }
     return m;
   }
-  void load(const std::string& path) { module_ = load_module(path); }
+  void load(const std::string& path) { module_ = bcast_root_ >= 0 ? load_broadcast(path) : load_module(path); }
+
+  // custom=broadcast:<root rank>: one-process-per-GPU deployments load the
+  // model once -- rank <root> reads the TorchScript file and broadcasts its
+  // bytes to every rank of the job (comm::Group: RCCL over xGMI between GPUs,
+  // the TCP store on hosts), and every rank deserialises the same bytes onto
+  // its own device.  Other ranks' model= paths are not read.  Multi-rank
+  // counterpart of the reference's in-process shared model table
+  // (tensor_filter_common.c:2911-3076).  Group membership comes from the job
+  // environment (RANK / WORLD_SIZE / MASTER_ADDR:MASTER_PORT, or
+  // broadcast-store:host:port).
+  torch::jit::Module load_broadcast(const std::string& path) {
+    comm::GroupSpec spec;
+    spec.name = "model-broadcast/" + (bcast_name_.empty() ? std::string("default") : bcast_name_);
+    spec.device = device_;
+    spec.backend = bcast_backend_;
+    spec.store = bcast_store_;
+    std::string err;
+    auto g = comm::Group::open(spec, &err);
+    if (!g) throw Error("model broadcast: cannot join the rank group: " + err);
+    int root = -1;
+    for (int i = 0; i < g->size(); ++i)
+      if (g->global_rank(i) == bcast_root_) root = i;
+    if (root < 0) throw Error("model broadcast: root rank " + std::to_string(bcast_root_) + " is not in the job");
+    comm::Packet pkt;
+    if (g->rank() == root) {
+      std::ifstream f(path, std::ios::binary);
+      if (!f) throw Error("model broadcast: cannot read " + path);
+      std::string bytes((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+      pkt.blobs.push_back(Memory::from_bytes(bytes.data(), bytes.size()));
+    }
+    if (!g->broadcast(root, &pkt, &err) || pkt.blobs.empty()) throw Error("model broadcast failed: " + err);
+    const MemoryPtr& blob = pkt.blobs[0];
+    std::string bytes(static_cast<const char*>(blob->map_host()), blob->size());
+    bcast_bytes_ = bytes.size();
+    NNSX_LOGI("pytorch", "model of rank ", bcast_root_, " received over ", g->backend_name(), " (", bytes.size(),
+              " bytes, group rank ", g->rank(), "/", g->size(), ")");
+    hip::DeviceGuard dg(device_);
+    std::istringstream is(bytes);
+    torch::jit::Module m = torch::jit::load(is, dev());
+    m.eval();
+    try {
+      m = torch::jit::freeze(m);
+    } catch (...) {
+    }
+    return m;
+  }
 
   at::Tensor prepare(at::Tensor t) {
     if (compute_dtype_ != DType::END && at::isFloatingType(t.scalar_type())) t = t.to(to_torch(compute_dtype_));
@@ -314,6 +371,9 @@ class TorchInstance : public FilterInstance {
   int device_ = -1;
   torch::jit::script::Module module_;
   bool use_graph_ = false;
+  int bcast_root_ = -1;  // custom=broadcast:<rank>
+  std::string bcast_backend_ = "auto", bcast_store_, bcast_name_;
+  size_t bcast_bytes_ = 0;
   bool channels_last_ = false;
   DType compute_dtype_ = DType::END;
   std::mutex mu_;
