@@ -37,12 +37,28 @@ def output_path() -> str:
     return os.path.join(ROOT, "nnstreamer_amd", "_C" + ext_suffix())
 
 
+def runtime_lib_path() -> str:
+    return os.path.join(ROOT, "nnstreamer_amd", "libnnsx.so")
+
+
+# native command-line tools: csrc/tools/<name>.cc is part of libnnsx (entry
+# point <name>_main); bin/<name with - for _> is csrc/tools/tool_main.cc built
+# for that entry (it loads torch's HIP runtime, then libnnsx)
+TOOLS = ("nnsx_launch", "nnsx_check")
+
+
+def tool_path(name: str) -> str:
+    return os.path.join(ROOT, "bin", name.replace("_", "-"))
+
+
 def _sources():
     out = []
     for dp, _, files in os.walk(CSRC):
         for f in sorted(files):
             if f.endswith((".cc", ".hip")):
                 rel = os.path.relpath(os.path.join(dp, f), CSRC)
+                if rel == os.path.join("tools", "tool_main.cc"):
+                    continue  # the executables' shim, linked separately
                 out.append(rel)
     return sorted(out)
 
@@ -81,11 +97,19 @@ def write_ninja(debug: bool = False) -> str:
         "  depfile = $out.d",
         "  deps = gcc",
         "  description = HIP $in",
-        "rule link",
-        f"  command = $hipcc -shared -fPIC --offload-arch={ARCH} $in -o $out {lib_dirs} -ltorch -ltorch_cpu -ltorch_hip -lc10 -lc10_hip -lamdhip64 -L/opt/rocm/lib -lrccl -lrocprofiler-sdk-roctx -ldl -lpthread -Wl,--no-as-needed",
+        # the runtime (core, elements, kernels, filters, comm) as one shared library
+        # the Python extension and the native tools link against
+        "rule linklib",
+        f"  command = $hipcc -shared -fPIC --offload-arch={ARCH} $in -o $out -Wl,-soname,libnnsx.so {lib_dirs} -ltorch -ltorch_cpu -ltorch_hip -lc10 -lc10_hip -lamdhip64 -L/opt/rocm/lib -lrccl -lrocprofiler-sdk-roctx -ldl -lpthread -Wl,--no-as-needed",
         "  description = LINK $out",
+        "rule linkext",
+        f"  command = $hipcc -shared -fPIC $in -o $out -L{ROOT}/nnstreamer_amd -lnnsx -Wl,-rpath,'$$ORIGIN' {lib_dirs} -ltorch -ltorch_cpu -lc10 -lamdhip64 -L/opt/rocm/lib -ldl -lpthread",
+        "  description = LINK $out",
+        "rule tool",
+        f"  command = $cxx -O2 -std=c++17 -DNNSX_TOOL_ENTRY=$entry -DNNSX_TORCH_LIB='\"{tlib[0]}\"' $in -o $out -ldl",
+        "  description = TOOL $out",
     ]
-    objs = []
+    lib_objs, py_objs = [], []
     for rel in _sources():
         obj = os.path.join(BUILD, rel.replace("/", "_") + ".o")
         extra = ""
@@ -97,9 +121,16 @@ def write_ninja(debug: bool = False) -> str:
         lines.append(f"build {obj}: {rule} {os.path.join(CSRC, rel)}")
         if extra:
             lines.append(f"  extra = {extra}")
-        objs.append(obj)
-    lines.append(f"build {output_path()}: link {' '.join(objs)}")
-    lines.append(f"default {output_path()}")
+        (py_objs if rel in PY_SOURCES else lib_objs).append(obj)
+    lib = runtime_lib_path()
+    lines.append(f"build {lib}: linklib {' '.join(lib_objs)}")
+    lines.append(f"build {output_path()}: linkext {' '.join(py_objs)} | {lib}")
+    outs = [lib, output_path()]
+    for t in TOOLS:
+        lines.append(f"build {tool_path(t)}: tool {os.path.join(CSRC, 'tools', 'tool_main.cc')}")
+        lines.append(f"  entry = {t}_main")
+        outs.append(tool_path(t))
+    lines.append(f"default {' '.join(outs)}")
     path = os.path.join(BUILD, "build.ninja")
     content = "\n".join(lines) + "\n"
     old = open(path).read() if os.path.exists(path) else None

@@ -1,4 +1,6 @@
-"""nnsx-check / nnsx-launch command-line tools (reference confchk and gst-launch)."""
+"""nnsx-check / nnsx-launch command-line tools (reference confchk and gst-launch):
+the native executables bin/nnsx-check and bin/nnsx-launch (csrc/tools), plus
+the Python modules of the same names."""
 import json
 
 import numpy as np
@@ -14,6 +16,32 @@ ENV = dict(os.environ, PYTHONPATH=ROOT, NNSX_DISABLE_GPU="1")
 def _run(*args, timeout=120):
     return subprocess.run([sys.executable, "-m", *args], cwd=ROOT, env=ENV, capture_output=True, text=True,
                           timeout=timeout)
+
+
+def _native(tool, *args, timeout=120):
+    return subprocess.run([os.path.join(ROOT, "bin", tool), *args], cwd=ROOT, env=ENV, capture_output=True, text=True,
+                          timeout=timeout)
+
+
+def test_native_check_json():
+    r = _native("nnsx-check", "--json")
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout)
+    assert "tensor_filter" in d["elements"] and "pytorch" in d["subplugins"]["filter"]
+    assert "bounding_boxes" in d["subplugins"]["decoder"] and d["version"].startswith("nnsx")
+
+
+def test_native_launch_eos_caps_and_errors(tmp_path):
+    dot = tmp_path / "g.dot"
+    r = _native("nnsx-launch", "-v", "--dot", str(dot), "videotestsrc", "num-buffers=3", "!",
+                "video/x-raw,format=RGB,width=8,height=4", "!", "tensor_converter", "!", "tensor_sink")
+    assert r.returncode == 0, r.stderr
+    assert "dimensions=(string)3:8:4:1" in r.stdout and "Got EOS" in r.stdout
+    assert "digraph" in dot.read_text()
+    assert _native("nnsx-launch", "nosuchelement ! fakesink").returncode == 2
+    assert _native("nnsx-launch", "-t", "1", "videotestsrc is-live=true ! fakesink").returncode == 3
+    r = _native("nnsx-launch", "-m", "videotestsrc num-buffers=2 ! tensor_converter ! tensor_sink")
+    assert r.returncode == 0 and "Got message from" in r.stdout
 
 
 def test_check_json():
