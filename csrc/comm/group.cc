@@ -11,6 +11,7 @@
 #include <thread>
 
 #include "core/log.h"
+#include "core/registry.h"
 #include "core/util.h"
 #include "runtime/hip_util.h"
 
@@ -300,8 +301,17 @@ bool Group::init(const GroupSpec& in, std::string* err) {
     return false;
   }
   device_ = spec_.device;
+  // [rccl] section (ini / NNSTREAMER_rccl_<key>): job-wide defaults for what
+  // an element or spec leaves unset -- backend (auto|rccl|tcp), store
+  // (host:port of the control-plane store), timeout_ms (rendezvous and
+  // control-plane waits)
+  const Config& cfg = Config::get();
+  if (spec_.backend.empty() || spec_.backend == "auto") spec_.backend = cfg.custom_value("rccl", "backend", "auto");
+  if (spec_.timeout_ms <= 0)
+    spec_.timeout_ms = static_cast<int>(to_int(cfg.custom_value("rccl", "timeout_ms", "60000"), 60000));
   // ---- control plane ----
   std::string addr = spec_.store;
+  if (addr.empty()) addr = cfg.custom_value("rccl", "store", "");
   if (addr.empty()) {
     if (const char* e = std::getenv("NNSX_STORE")) addr = e;
   }

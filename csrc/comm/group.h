@@ -76,10 +76,10 @@ struct GroupSpec {
   int rank = -1;               // global rank (-1: $RANK or 0)
   int world = -1;              // global world size (-1: $WORLD_SIZE or 1)
   std::vector<int> members;    // global ranks in the group (empty: all)
-  std::string store;           // "host:port" ("": $NNSX_STORE, else $MASTER_ADDR:$MASTER_PORT+17)
+  std::string store;           // "host:port" ("": ini [rccl] store, $NNSX_STORE, else $MASTER_ADDR:$MASTER_PORT+17)
   int device = -1;             // GPU of this member (-1: host only)
-  std::string backend = "auto";  // auto | rccl | tcp
-  int timeout_ms = 60000;      // rendezvous timeout
+  std::string backend = "auto";  // auto | rccl | tcp ("auto": ini [rccl] backend, default auto)
+  int timeout_ms = 0;          // rendezvous timeout (0: ini [rccl] timeout_ms, default 60000)
 };
 
 // One message: what an element hands to / gets from the group.

@@ -20,7 +20,7 @@ struct RankProps {
   std::string ranks;       // "0,1,3": member global ranks ("" = all)
   std::string store;       // control-plane store host:port
   int backend = 0;         // auto | rccl | tcp
-  unsigned timeout_ms = 60000;
+  unsigned timeout_ms = 0;  // 0: ini [rccl] timeout_ms (default 60000)
   int peer = -1;           // publisher / query server global rank (-1: first member)
   int device = -1;         // GPU of this member (-1: $LOCAL_RANK's GPU when any is visible)
 

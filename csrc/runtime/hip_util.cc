@@ -12,6 +12,7 @@
 #include <sstream>
 #include <thread>
 
+#include "core/registry.h"
 #include "core/util.h"
 
 namespace nnsx {
@@ -142,8 +143,20 @@ void event_put(int dev, hipEvent_t ev) {
   pool.free[dev].push_back(ev);
 }
 
+// [hip] stream_priority (ini / NNSTREAMER_hip_stream_priority): priority of the
+// element streams (0 = normal; lower = more urgent, clamped to the device range)
+int configured_stream_priority(int dev) {
+  static const int prio = static_cast<int>(to_int(Config::get().custom_value("hip", "stream_priority", "0"), 0));
+  if (prio == 0) return 0;
+  int lo = 0, hi = 0;  // hi = greatest priority (numerically lowest)
+  if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return 0;
+  (void)dev;
+  return std::min(std::max(prio, hi), lo);
+}
+
 hipStream_t stream_create(int dev, int priority) {
   DeviceGuard g(dev);
+  if (priority == kConfiguredPriority) priority = configured_stream_priority(dev);
   hipStream_t s;
   check(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority), "hipStreamCreateWithPriority");
   return s;
@@ -183,7 +196,12 @@ void configure_pool(int dev) {
     DeviceGuard g(dev);
     hipMemPool_t pool;
     if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-      uint64_t thr = UINT64_MAX;  // keep everything cached: 288 GB of HBM per GPU
+      // [hip] pool_release_threshold: bytes the stream-ordered pool keeps cached
+      // after a sync ("max" = everything: 288 GB of HBM per GPU leaves no reason
+      // to give memory back; lower it when several processes share a GPU)
+      const std::string v = lower(Config::get().custom_value("hip", "pool_release_threshold", "max"));
+      uint64_t thr = UINT64_MAX;
+      if (v != "max" && !v.empty()) thr = static_cast<uint64_t>(std::strtoull(v.c_str(), nullptr, 10));
       (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
     }
     (void)hipGetLastError();

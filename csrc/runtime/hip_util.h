@@ -46,7 +46,9 @@ hipEvent_t event_get(int dev);
 void event_put(int dev, hipEvent_t ev);
 
 // A non-blocking stream owned by the caller (released with stream_destroy).
-hipStream_t stream_create(int dev, int priority = 0);
+// priority kConfiguredPriority: the ini's [hip] stream_priority (default 0)
+constexpr int kConfiguredPriority = -1000000;
+hipStream_t stream_create(int dev, int priority = kConfiguredPriority);
 void stream_destroy(int dev, hipStream_t s);
 // Process-lifetime stream on which pooled device blocks are returned.
 hipStream_t release_stream(int dev);

@@ -207,3 +207,38 @@ def test_bench_deeplab_fan_three_ranks_cpu():
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     assert d["config"]["parallelism"].startswith("fan-out 1->2") and d["value"] > 0
+
+
+def test_ini_rccl_and_hip_sections(tmp_path):
+    """[rccl] timeout_ms / backend / store and [hip] keys from the ini: a rank
+    group whose second member never comes fails after the ini's 400 ms
+    rendezvous timeout instead of the 60 s default; nnsx-check shows the keys."""
+    ini = tmp_path / "nnstreamer.ini"
+    port = _free_port()
+    ini.write_text(f"[rccl]\ntimeout_ms=400\nbackend=tcp\nstore=127.0.0.1:{port}\n"
+                   "[hip]\npool_release_threshold=1073741824\nstream_priority=-1\n")
+    script = tmp_path / "lonely.py"
+    script.write_text(textwrap.dedent(f"""
+        import sys, time
+        sys.path.insert(0, {ROOT!r})
+        import nnstreamer_amd as nns
+        caps = "other/tensors,format=static,num_tensors=1,dimensions=2,types=float32,framerate=0/1"
+        p = nns.parse_launch(f"appsrc name=src caps={{caps}} ! tensor_allgather rank=0 world-size=2 ! tensor_sink")
+        t0 = time.time()
+        try:
+            ok = p.set_state("playing")
+            msg = p.wait(20)
+        except Exception as e:
+            ok, msg = False, ("error", "", str(e))
+        print("ELAPSED", time.time() - t0, ok, msg, flush=True)
+        p.stop()
+    """))
+    env = dict(os.environ, NNSTREAMER_CONF=str(ini), RANK="0", WORLD_SIZE="2")
+    r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=120)
+    line = [x for x in r.stdout.splitlines() if x.startswith("ELAPSED")][-1]
+    elapsed = float(line.split()[1])
+    assert elapsed < 10, line  # not the 60 s default
+    assert "False" in line or "error" in line, line
+    chk = subprocess.run([os.path.join(ROOT, "bin", "nnsx-check")], env=env, capture_output=True, text=True,
+                         timeout=120)
+    assert "[rccl]" in chk.stdout and "timeout_ms = 400" in chk.stdout and "stream_priority = -1" in chk.stdout
