@@ -911,7 +911,10 @@ __global__ void __launch_bounds__(64 * NW, (NOT <= 6 ? 2 : 1)) irw_f32_kernel(Ir
 // (TY+2) x (TX+2) halo grid into its channel half's hidden image (out-of-map
 // cells = the dw zero padding); one barrier; dw + project partial (K = the
 // 16 channels) on the wave's half of the output pixels; the two channel
-// halves' partials are added in a fixed order through LDS.
+// halves' partials are added in a fixed order through LDS.  Persistent: a
+// resident set of workgroups walks all tiles, the weights / normalisation
+// table are set up once per workgroup and the next tile's input bytes are in
+// flight while the current tile computes.
 template <int TY, int TX>
 __global__ void __launch_bounds__(256, 2) stem_ir1_f32_kernel(StemIr1F32Args a) {
   constexpr int HY = TY + 2, HX = TX + 2, PIN = HY * HX;
@@ -919,6 +922,7 @@ __global__ void __launch_bounds__(256, 2) stem_ir1_f32_kernel(StemIr1F32Args a) 
   constexpr int IY = 2 * HY + 1, IX = 2 * HX + 1, PITCH = IX * 3;
   constexpr int NPT = (TY * TX + 15) / 16, NPX = NPT * 16;
   constexpr int XIN = (IY * PITCH + 3) / 4 * 4;  // floats, 16-B aligned end
+  constexpr int NIN = IY * PITCH, NIT = (NIN + 255) / 256;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* xin = smem;                                       // [IY][PITCH] normalised input
   float* lut = smem + XIN;                                 // [256] (v + add) / div
@@ -928,39 +932,14 @@ __global__ void __launch_bounds__(256, 2) stem_ir1_f32_kernel(StemIr1F32Args a) 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, g = lane >> 4;
   const int chalf = wave & 1, phalf = wave >> 1;  // wave = (16-channel half, pixel half)
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int tiles_img = a.tiles_x * a.tiles_y;
-  const int b = tile / tiles_img;
-  const int tyx = tile - b * tiles_img;
-  const int oy0 = (tyx / a.tiles_x) * TY, ox0 = (tyx % a.tiles_x) * TX;
-  const int hy0 = oy0 - 1, hx0 = ox0 - 1;          // hidden halo origin (stem-output coords)
-  const int iy0 = 2 * hy0 - 1, ix0 = 2 * hx0 - 1;  // input patch origin
-  const uint8_t* xb = a.x + static_cast<int64_t>(b) * a.H * a.W * 3;
+  const int ntiles = tiles_img * a.B;
 
-  // ---- normalised input patch (zero outside the frame = the stem's padding);
-  // the normalisation (x + add) / div -- the pipeline's tensor_transform
-  // arithmetic, exact fp32 division -- is a 256-entry table.  Every byte load
-  // of the patch is issued before the first use (compile-time trip count).
-  constexpr int NIN = IY * PITCH, NIT = (NIN + 255) / 256;
-  int raw[NIT];
-#pragma unroll
-  for (int it = 0; it < NIT; ++it) {
-    const int i = tid + it * 256;
-    const int r = i / PITCH, c = i - r * PITCH;
-    const int iy = iy0 + r, ix = ix0 + c / 3;
-    raw[it] = (i < NIN && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
-                  ? static_cast<int>(xb[(static_cast<int64_t>(iy) * a.W + ix) * 3 + c % 3])
-                  : -1;
-  }
+  // ---- once per workgroup: normalisation table, weights in registers.  The
+  // normalisation (x + add) / div -- the pipeline's tensor_transform arithmetic,
+  // exact fp32 division -- is a 256-entry table.
   lut[tid] = (static_cast<float>(tid) + a.add) / a.div;
-  __syncthreads();
-#pragma unroll
-  for (int it = 0; it < NIT; ++it) {
-    const int i = tid + it * 256;
-    if (i < NIN) xin[i] = raw[it] >= 0 ? lut[raw[it]] : 0.f;
-  }
-  // stem weights of this wave's 16 channels: k = 4t + g (27 taps + 1 zero)
-  float sa[7];
+  float sa[7];  // stem weights of this wave's 16 channels: k = 4t + g (27 taps + 1 zero)
   int off[7];
 #pragma unroll
   for (int t = 0; t < 7; ++t) {
@@ -975,80 +954,111 @@ __global__ void __launch_bounds__(256, 2) stem_ir1_f32_kernel(StemIr1F32Args a) 
 #pragma unroll
   for (int t = 0; t < 9; ++t) wd4[t] = *reinterpret_cast<const f32x4_t*>(a.wd + t * 32 + ch);
   const f32x4_t pa = *reinterpret_cast<const f32x4_t*>(a.wp + li * 32 + ch);
-  __syncthreads();
-
+  const f32x4_t bp4 = *reinterpret_cast<const f32x4_t*>(a.bp + 4 * g);
   f32x4_t* myhid = hidw + (chalf * 4 + g) * PINP;
   f32x4_t* mydwo = dwo + (chalf * 4 + g) * NPX;
   const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  // ---- stem MFMA over this pixel half of the halo grid, two pixel tiles at a time
-  constexpr int NBH = (NBT + 1) / 2;
+
+  // the raw bytes of a tile's input patch, -1 outside the frame (the stem's
+  // zero padding); every load of the patch is in flight at once
+  int raw[NIT];
+  auto fetch = [&](int tile) {
+    const int b = tile / tiles_img;
+    const int tyx = tile - b * tiles_img;
+    const int iy0 = 2 * ((tyx / a.tiles_x) * TY - 1) - 1, ix0 = 2 * ((tyx % a.tiles_x) * TX - 1) - 1;
+    const uint8_t* xb = a.x + static_cast<int64_t>(b) * a.H * a.W * 3;
 #pragma unroll
-  for (int jj = 0; jj < NBH; jj += 2) {
-    const int j = phalf * NBH + jj;
-    if (j >= NBT) break;
-    const int j1 = (jj + 1 < NBH && j + 1 < NBT) ? j + 1 : j;
-    const int c0 = j * 16 + li, c1 = j1 * 16 + li;
-    const int hy_0 = c0 / HX, hx_0 = c0 - hy_0 * HX, hy_1 = c1 / HX, hx_1 = c1 - hy_1 * HX;
-    const int base0 = c0 < PIN ? 2 * hy_0 * PITCH + 6 * hx_0 : 0;
-    const int base1 = c1 < PIN ? 2 * hy_1 * PITCH + 6 * hx_1 : 0;
-    f32x4_t e0 = z, e1 = z;
-#pragma unroll
-    for (int t = 0; t < 7; ++t) {
-      e0 = mfma4(sa[t], xin[base0 + off[t]], e0);
-      e1 = mfma4(sa[t], xin[base1 + off[t]], e1);
+    for (int it = 0; it < NIT; ++it) {
+      const int i = tid + it * 256;
+      const int r = i / PITCH, c = i - r * PITCH;
+      const int iy = iy0 + r, ix = ix0 + c / 3;
+      raw[it] = (i < NIN && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
+                    ? static_cast<int>(xb[(static_cast<int64_t>(iy) * a.W + ix) * 3 + c % 3])
+                    : -1;
     }
-    const bool in0 = c0 < PIN && hy0 + hy_0 >= 0 && hy0 + hy_0 < a.Ho && hx0 + hx_0 >= 0 && hx0 + hx_0 < a.Wo;
-    const bool in1 = c1 < PIN && hy0 + hy_1 >= 0 && hy0 + hy_1 < a.Ho && hx0 + hx_1 >= 0 && hx0 + hx_1 < a.Wo;
-    myhid[c0] = in0 ? relu6x4(e0 + bs4) : z;
-    if (j1 != j) myhid[c1] = in1 ? relu6x4(e1 + bs4) : z;
-  }
-  __syncthreads();  // both pixel halves of each channel half's hidden image
-  // ---- depthwise 3x3 + bias + ReLU6 on this wave's output pixel half
-  constexpr int NPH = (NPT + 1) / 2;
+  };
+
+  // persistent: the workgroup walks tiles blockIdx.x, + gridDim.x, ...; the
+  // next tile's patch loads overlap this tile's MFMA / depthwise work
+  int tile = blockIdx.x;
+  if (tile < ntiles) fetch(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    const int b = tile / tiles_img;
+    const int tyx = tile - b * tiles_img;
+    const int oy0 = (tyx / a.tiles_x) * TY, ox0 = (tyx % a.tiles_x) * TX;
+    const int hy0 = oy0 - 1, hx0 = ox0 - 1;  // hidden halo origin (stem-output coords)
+    __syncthreads();  // previous tile done with xin / hidden / dwo (and lut written)
 #pragma unroll
-  for (int pp = 0; pp < NPH; ++pp) {
-    const int pt = phalf * NPH + pp;
-    if (pt >= NPT) break;
-    const int q = pt * 16 + li;
-    const int qq = q < TY * TX ? q : 0;
-    const int cell = (qq / TX) * HX + (qq % TX);
-    f32x4_t d = bd4;
+    for (int it = 0; it < NIT; ++it) {
+      const int i = tid + it * 256;
+      if (i < NIN) xin[i] = raw[it] >= 0 ? lut[raw[it]] : 0.f;
+    }
+    if (tile + static_cast<int>(gridDim.x) < ntiles) fetch(tile + gridDim.x);
+    __syncthreads();
+
+    // ---- stem MFMA over this pixel half of the halo grid, two pixel tiles at a time
+    constexpr int NBH = (NBT + 1) / 2;
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
+    for (int jj = 0; jj < NBH; jj += 2) {
+      const int j = phalf * NBH + jj;
+      if (j >= NBT) break;
+      const int j1 = (jj + 1 < NBH && j + 1 < NBT) ? j + 1 : j;
+      const int c0 = j * 16 + li, c1 = j1 * 16 + li;
+      const int hy_0 = c0 / HX, hx_0 = c0 - hy_0 * HX, hy_1 = c1 / HX, hx_1 = c1 - hy_1 * HX;
+      const int base0 = c0 < PIN ? 2 * hy_0 * PITCH + 6 * hx_0 : 0;
+      const int base1 = c1 < PIN ? 2 * hy_1 * PITCH + 6 * hx_1 : 0;
+      f32x4_t e0 = z, e1 = z;
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) d = __builtin_elementwise_fma(myhid[cell + ky * HX + kx], wd4[ky * 3 + kx], d);
-    mydwo[pt * 16 + li] = relu6x4(d);
-  }
-  wave_sync();
-  // ---- project partial over this wave's 16 channels (K = 16 of 32)
-  f32x4_t acc[NPH];
-#pragma unroll
-  for (int pp = 0; pp < NPH; ++pp) {
-    const int pt = phalf * NPH + pp;
-    acc[pp] = pt < NPT ? mfma_k16(pa, mydwo[pt * 16 + li], z) : z;
-  }
-  // ---- channel half 0 + half 1 through LDS (the dwo planes of the other half
-  // are read only by their own wave, so the partials reuse this wave's own rows)
-  f32x4_t* red = dwo;  // [2 halves][4 quads][NPX]: overwrite own dw outputs with partials
-#pragma unroll
-  for (int pp = 0; pp < NPH; ++pp) {
-    const int pt = phalf * NPH + pp;
-    if (pt < NPT) red[(chalf * 4 + g) * NPX + pt * 16 + li] = acc[pp];
-  }
-  __syncthreads();
-  const f32x4_t bp4 = *reinterpret_cast<const f32x4_t*>(a.bp + 4 * g);
-  // waves of channel half 0 store (pixel half = phalf)
-  if (chalf == 0) {
+      for (int t = 0; t < 7; ++t) {
+        e0 = mfma4(sa[t], xin[base0 + off[t]], e0);
+        e1 = mfma4(sa[t], xin[base1 + off[t]], e1);
+      }
+      const bool in0 = c0 < PIN && hy0 + hy_0 >= 0 && hy0 + hy_0 < a.Ho && hx0 + hx_0 >= 0 && hx0 + hx_0 < a.Wo;
+      const bool in1 = c1 < PIN && hy0 + hy_1 >= 0 && hy0 + hy_1 < a.Ho && hx0 + hx_1 >= 0 && hx0 + hx_1 < a.Wo;
+      myhid[c0] = in0 ? relu6x4(e0 + bs4) : z;
+      if (j1 != j) myhid[c1] = in1 ? relu6x4(e1 + bs4) : z;
+    }
+    __syncthreads();  // both pixel halves of each channel half's hidden image
+    // ---- depthwise 3x3 + bias + ReLU6 on this wave's output pixel half
+    constexpr int NPH = (NPT + 1) / 2;
 #pragma unroll
     for (int pp = 0; pp < NPH; ++pp) {
       const int pt = phalf * NPH + pp;
       if (pt >= NPT) break;
       const int q = pt * 16 + li;
-      if (q >= TY * TX) continue;
-      const int gy = oy0 + q / TX, gx = ox0 + q % TX;
-      if (gy >= a.Ho || gx >= a.Wo) continue;
-      const f32x4_t v = red[g * NPX + q] + red[(4 + g) * NPX + q] + bp4;
-      *reinterpret_cast<f32x4_t*>(a.y + ((static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx) * 16 + 4 * g) = v;
+      const int qq = q < TY * TX ? q : 0;
+      const int cell = (qq / TX) * HX + (qq % TX);
+      f32x4_t d = bd4;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx)
+          d = __builtin_elementwise_fma(myhid[cell + ky * HX + kx], wd4[ky * 3 + kx], d);
+      mydwo[pt * 16 + li] = relu6x4(d);
+    }
+    wave_sync();
+    // ---- project partial over this wave's 16 channels (K = 16 of 32), written over
+    // the wave's own dw outputs (the other channel half reads only its own rows)
+#pragma unroll
+    for (int pp = 0; pp < NPH; ++pp) {
+      const int pt = phalf * NPH + pp;
+      if (pt < NPT) mydwo[pt * 16 + li] = mfma_k16(pa, mydwo[pt * 16 + li], z);
+    }
+    __syncthreads();
+    // ---- channel half 0 + half 1 (fixed order), + bias -> [B][Ho][Wo][16]; the
+    // waves of channel half 0 store their pixel half
+    if (chalf == 0) {
+#pragma unroll
+      for (int pp = 0; pp < NPH; ++pp) {
+        const int pt = phalf * NPH + pp;
+        if (pt >= NPT) break;
+        const int q = pt * 16 + li;
+        if (q >= TY * TX) continue;
+        const int gy = oy0 + q / TX, gx = ox0 + q % TX;
+        if (gy >= a.Ho || gx >= a.Wo) continue;
+        const f32x4_t v = dwo[g * NPX + q] + dwo[(4 + g) * NPX + q] + bp4;
+        *reinterpret_cast<f32x4_t*>(a.y + ((static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx) * 16 + 4 * g) = v;
+      }
     }
   }
 }
@@ -1335,8 +1345,18 @@ bool stem_ir1_f32(const StemIr1F32Args& args, hipStream_t s) {
   if (lds > 64 * 1024 &&
       hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
     return false;
-  hipLaunchKernelGGL((stem_ir1_f32_kernel<kStemIr1TY, kStemIr1TX>),
-                     dim3(static_cast<unsigned>(a.tiles_x * a.tiles_y * a.B)), dim3(256), lds, s, a);
+  // persistent grid: exactly the workgroups that fit resident at once (LDS and
+  // registers decide; a workgroup that has to wait for a slot would serialise
+  // its whole tile loop behind the others)
+  static const int resident = [fn, lds] {
+    int dev = 0, ncu = 256, per_cu = 1;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+    return ncu * per_cu;
+  }();
+  const int tiles = a.tiles_x * a.tiles_y * a.B;
+  const unsigned grid = static_cast<unsigned>(std::min(tiles, resident));
+  hipLaunchKernelGGL((stem_ir1_f32_kernel<kStemIr1TY, kStemIr1TX>), dim3(grid), dim3(256), lds, s, a);
   return true;
 }
 
