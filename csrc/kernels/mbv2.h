@@ -82,8 +82,11 @@ struct IrBlockF32Args {
   // derived by ir_block_f32()
   int Ho = 0, Wo = 0, tiles_x = 0, tiles_y = 0;
   int hsplit = 1;  // hidden-channel parts per tile (wave-split kernel)
+  float* ws = nullptr;  // partial-sum workspace (ir_block_f32_workspace_bytes; small batches)
 };
 bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout, bool has_expand);
+// device workspace ir_block_f32 needs for these args (0 = none)
+size_t ir_block_f32_workspace_bytes(const IrBlockF32Args& a);
 
 // stem (3x3/2 conv 3 -> 32 on the uint8 frame, normalised as (x + add) / div,
 // + ReLU6) fused with an expand-free inverted residual 32 -> 32 -> 16

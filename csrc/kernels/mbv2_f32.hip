@@ -884,6 +884,11 @@ __global__ void __launch_bounds__(64 * NW, (NOT <= 6 ? 2 : 1)) irw_f32_kernel(Ir
       const int gy = oy0 + q / TX, gx = ox0 + q % TX;
       if (gy >= a.Ho || gx >= a.Wo) continue;
       const int64_t pix = (static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx;
+      if (a.ws) {  // > 2 parts: this part's slab of the workspace (irw_reduce adds them in order)
+        const int64_t plane = static_cast<int64_t>(a.B) * a.Ho * a.Wo * a.cout;
+        *reinterpret_cast<f32x4_t*>(a.ws + part * plane + pix * a.cout + co) = v;
+        continue;
+      }
       if (part == 0) {
         v += *reinterpret_cast<const f32x4_t*>(a.bp + co);
         if (a.residual) v += *reinterpret_cast<const f32x4_t*>(a.x + pix * a.cin + co);
@@ -1060,6 +1065,24 @@ __global__ void __launch_bounds__(256, 2) stem_ir1_f32_kernel(StemIr1F32Args a) 
         *reinterpret_cast<f32x4_t*>(a.y + ((static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx) * 16 + 4 * g) = v;
       }
     }
+  }
+}
+
+// the hidden-split partials of irw_f32 (> 2 parts), added in part order
+// (deterministic), + bias (+ residual)
+__global__ void __launch_bounds__(256) irw_reduce_kernel(const float* __restrict__ ws, int parts, int64_t plane,
+                                                         const float* __restrict__ bias, const float* __restrict__ x,
+                                                         int cin, int cout, int residual, float* __restrict__ y) {
+  const int64_t nq = plane / 4;
+  for (int64_t q = blockIdx.x * 256ll + threadIdx.x; q < nq; q += static_cast<int64_t>(gridDim.x) * 256) {
+    const int64_t e = q * 4;
+    f32x4_t v = *reinterpret_cast<const f32x4_t*>(ws + e);
+    for (int p = 1; p < parts; ++p) v += *reinterpret_cast<const f32x4_t*>(ws + p * plane + e);
+    const int64_t pix = e / cout;
+    const int co = static_cast<int>(e - pix * cout);
+    v += *reinterpret_cast<const f32x4_t*>(bias + co);
+    if (residual) v += *reinterpret_cast<const f32x4_t*>(x + pix * cin + co);
+    *reinterpret_cast<f32x4_t*>(y + e) = v;
   }
 }
 
@@ -1305,24 +1328,54 @@ bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout
          find_cfg(stride, H, W, cin, hid, cout, has_expand) != nullptr;
 }
 
+// Hidden-channel parts per tile.  Fewer tiles than CUs: split the hidden
+// channels over workgroups (every wave keeps >= 1 subtile).  Two parts add
+// into a zeroed output (a + b == b + a: deterministic); more parts (small
+// batches: one 14x14 / 7x7 image is 1-4 tiles) write workspace slabs that
+// irw_reduce adds in part order.
+static int irw_parts(const IrwCfg* c, int tiles, int hid) {
+  const int nsub = hid / 16;
+  if (tiles >= 256 || nsub < 8) return 1;
+  if (tiles >= 128) return 2;
+  const int want = (512 + tiles - 1) / tiles;
+  return std::max(2, std::min(want, nsub / c->NW));
+}
+
+static void irw_geometry(const IrwCfg* c, IrBlockF32Args* a) {
+  a->Ho = (a->H - 1) / a->stride + 1;
+  a->Wo = (a->W - 1) / a->stride + 1;
+  a->tiles_y = (a->Ho + c->TY - 1) / c->TY;
+  a->tiles_x = (a->Wo + c->TX - 1) / c->TX;
+  a->hsplit = irw_parts(c, a->tiles_x * a->tiles_y * a->B, a->hid);
+}
+
 static bool launch_irw(const IrwCfg* c, IrBlockF32Args a, hipStream_t s) {
-  a.Ho = (a.H - 1) / a.stride + 1;
-  a.Wo = (a.W - 1) / a.stride + 1;
-  a.tiles_y = (a.Ho + c->TY - 1) / c->TY;
-  a.tiles_x = (a.Wo + c->TX - 1) / c->TX;
+  irw_geometry(c, &a);
   const int tiles = a.tiles_x * a.tiles_y * a.B;
-  // fewer tiles than CUs: split the hidden channels over two workgroups per tile
-  // (partial sums added into a zeroed output; two addends keep it deterministic)
-  const int nsub = a.hid / 16;
-  a.hsplit = (tiles < 256 && nsub >= 8) ? 2 : 1;
+  const int64_t plane = static_cast<int64_t>(a.B) * a.Ho * a.Wo * a.cout;
+  if (a.hsplit > 2 && !a.ws) return false;  // the caller sizes the workspace (ir_block_f32_workspace_bytes)
+  if (a.hsplit <= 2) a.ws = nullptr;
   const size_t lds = c->lds(a.hid);
   if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(c->kernel),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
     return false;
-  if (a.hsplit > 1)
-    (void)hipMemsetAsync(a.y, 0, static_cast<size_t>(a.B) * a.Ho * a.Wo * a.cout * sizeof(float), s);
+  if (a.hsplit == 2) (void)hipMemsetAsync(a.y, 0, static_cast<size_t>(plane) * sizeof(float), s);
   hipLaunchKernelGGL(c->kernel, dim3(static_cast<unsigned>(tiles * a.hsplit)), dim3(64 * c->NW), lds, s, a);
+  if (a.ws) {
+    const unsigned grid = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((plane / 4 + 255) / 256, 4096)));
+    hipLaunchKernelGGL(irw_reduce_kernel, dim3(grid), dim3(256), 0, s, a.ws, a.hsplit, plane, a.bp, a.x, a.cin,
+                       a.cout, a.residual, a.y);
+  }
   return true;
+}
+
+size_t ir_block_f32_workspace_bytes(const IrBlockF32Args& args) {
+  IrBlockF32Args a = args;
+  const IrwCfg* c = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0);
+  if (!c) return 0;
+  irw_geometry(c, &a);
+  if (a.hsplit <= 2) return 0;
+  return static_cast<size_t>(a.hsplit) * a.B * a.Ho * a.Wo * a.cout * sizeof(float);
 }
 
 size_t stem_ir1_lds_bytes() {

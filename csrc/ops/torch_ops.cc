@@ -231,6 +231,11 @@ at::Tensor ir_block_f32_cuda(const at::Tensor& x, const at::Tensor& we, const at
   a.stride = static_cast<int>(stride);
   a.has_expand = has_expand ? 1 : 0;
   a.residual = residual ? 1 : 0;
+  at::Tensor ws;
+  if (const size_t wsb = nnsx::kernels::ir_block_f32_workspace_bytes(a)) {
+    ws = at::empty({static_cast<int64_t>(wsb / sizeof(float))}, x.options());  // caching allocator: graph-capture safe
+    a.ws = ws.data_ptr<float>();
+  }
   TORCH_CHECK(nnsx::kernels::ir_block_f32(a, cur_stream()), "ir_block(f32): unsupported shape (stride ", stride, ", ",
               H, "x", W, ", cin ", C, ", hid ", hid, ", cout ", cout, ")");
   return y;

@@ -130,9 +130,9 @@ def _ir_ref64(x, we, be, wd, bd, wp, bp, stride, cout, has_expand, residual):
 
 
 @pytest.mark.parametrize("H,cin,hid,cout,stride,has_expand", IR_F32_SHAPES)
-def test_ir_block_f32(nns, H, cin, hid, cout, stride, has_expand):
+@pytest.mark.parametrize("B", [3, 1])
+def test_ir_block_f32(nns, H, cin, hid, cout, stride, has_expand, B):
     torch.manual_seed(H * 7 + cin + hid)
-    B = 3
     assert torch.ops.nnsx.ir_supported_f32(stride, H, H, cin, hid, cout, has_expand)
     x = torch.randn(B, H, H, cin, device="cuda")
     kin = (cin + 7) // 8 * 8
