@@ -195,17 +195,21 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
             f"inputtype={'uint8' if fuse_norm else 'float32'} accelerator={accel} device={dev} "
             f"custom=hipgraph:{graph}{bcast} device-stats={'true' if use_gpu else 'false'} ")
     live = f"is-live=true " if live_fps > 0 else ""
+    # throughput runs: queues are thread boundaries, so the next batch's upload
+    # is issued while the filter thread still submits this batch's kernels, and
+    # the decoder's read-back overlaps the next forward.  The live batch-1
+    # latency run keeps the whole chain in the source's streaming thread: no
+    # queue hand-off on the path of a frame.
+    q1 = "! queue max-size-buffers=2 " if live_fps <= 0 else ""
+    q2 = f"! queue max-size-buffers={a.queue} " if live_fps <= 0 else ""
     desc = (
         f"videotestsrc num-buffers={frames} pattern=snow pool-size={pool} {live}"
         f"! video/x-raw,format=RGB,width={S},height={S},framerate={live_fps}/1 "
         f"! tensor_converter frames-per-tensor={B} device={dev} "
-        # thread boundary: the next batch's upload is issued while the filter thread
-        # is still submitting this batch's kernels
-        f"! queue max-size-buffers=2 "
+        + q1
         + (f"! tensor_transform mode=arithmetic option={cfg['norm']} " if not fuse_norm else "")
         + f"! {filt}"
-        + (f"! tee name=t t. ! queue max-size-buffers={a.queue} " if cfg.get("gather") else
-           f"! queue max-size-buffers={a.queue} ")
+        + (f"! tee name=t t. ! queue max-size-buffers={a.queue} " if cfg.get("gather") else q2)
         + f"! {cfg['decoder'].format(**files)} "
         f"! tensor_sink name=sink"
         # multi-source: every rank's PoseNet outputs are all-gathered (RCCL over xGMI
