@@ -15,4 +15,4 @@ for P in "$P1" "$P2" "$P3" "$P4"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $P -d $OUT/p$i -o p$i --output-format csv -- python3 scripts/bench_ir_f32.py ${B:-128} > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
 done
-python3 scripts/pmc_summary.py $OUT "${KERNEL:-}"
+python3 scripts/pmc_report.py $OUT "${KERNEL:-}"
