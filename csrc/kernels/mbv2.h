@@ -54,7 +54,10 @@ bool ir_block(const IrBlockArgs& a, hipStream_t s);
 // (Kpad >= K, Kpad % 4 == 0), K % 4 == 0, N % 4 == 0.
 // tile: 0 = auto, else BM * 1000 + BN of an instantiated tile (64064, 128064, 64128, 128128, 128192)
 void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
-                 int Kpad, int Npad, int act, hipStream_t s, int tile = 0);
+                 int Kpad, int Npad, int act, hipStream_t s, int tile = 0, float* ws = nullptr);
+// split-K workspace the GEMM wants for this shape (0: no split; without it the
+// GEMM runs unsplit)
+size_t pw_gemm_f32_workspace_bytes(int M, int N, int Kpad, bool has_res, int tile = 0);
 // depthwise 3x3, stride 1|2, dilation d (padding d); w [9][C], C % 4 == 0
 void dw3x3_f32(const float* x, const float* w, const float* bias, float* y, int B, int H, int W, int C, int stride,
                int dil, int act, hipStream_t s);

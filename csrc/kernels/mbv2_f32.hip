@@ -188,9 +188,9 @@ __global__ void __launch_bounds__(256) pw_gemm_f32_kernel(const float* __restric
       const int n = n0 + wn * (BN / 2) + j * 16 + g * 4;
       if (n >= N) continue;
       float* yp = y + static_cast<int64_t>(m) * N + n;
-      if (gridDim.z > 1) {  // split-K partial sum (no residual / activation)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) atomicAdd(yp + r, acc[i][j][r] + (blockIdx.z == 0 ? bias[n + r] : 0.f));
+      if (gridDim.z > 1) {  // split-K: this slice's slab of the workspace (gemm_splitk_reduce adds them)
+        *reinterpret_cast<f32x4_t*>(y + static_cast<int64_t>(blockIdx.z) * M * N + static_cast<int64_t>(m) * N + n) =
+            acc[i][j];
         continue;
       }
       f32x4_t v = acc[i][j] + *reinterpret_cast<const f32x4_t*>(bias + n);
@@ -199,6 +199,22 @@ __global__ void __launch_bounds__(256) pw_gemm_f32_kernel(const float* __restric
       for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], act);
       *reinterpret_cast<f32x4_t*>(yp) = v;
     }
+  }
+}
+
+// split-K epilogue: y = act(sum_z ws[z] + bias), slabs added in z order
+// (deterministic, unlike fp32 atomics whose arrival order varies)
+__global__ void __launch_bounds__(256) gemm_splitk_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N,
+                                                                 const float* __restrict__ bias, int act,
+                                                                 float* __restrict__ y) {
+  const int64_t plane = static_cast<int64_t>(M) * N, nq = plane / 4;
+  for (int64_t q = blockIdx.x * 256 + threadIdx.x; q < nq; q += static_cast<int64_t>(gridDim.x) * 256) {
+    f32x4_t v = reinterpret_cast<const f32x4_t*>(ws)[q];
+    for (int z = 1; z < splits; ++z) v += reinterpret_cast<const f32x4_t*>(ws + z * plane)[q];
+    v += *reinterpret_cast<const f32x4_t*>(bias + (q * 4) % N);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], act);
+    reinterpret_cast<f32x4_t*>(y)[q] = v;
   }
 }
 
@@ -635,8 +651,8 @@ __global__ void __launch_bounds__(256) ir_block_f32_kernel(IrBlockF32Args a) {
 // Expand weights of the next subtile are in flight during dw + project.  At the
 // end the 4 waves' partial sums are added through LDS in a fixed order (w0 +
 // w1 + w2 + w3, deterministic), plus bias / residual, and stored; with
-// hsplit = 2 the two parts add into a zeroed output (a + b == b + a: still
-// deterministic).  The MFMA pipe of a SIMD then alternates between waves of
+// hsplit > 1 each part stores its slab of a workspace and irw_reduce adds the
+// slabs in part order (deterministic).  The MFMA pipe of a SIMD then alternates between waves of
 // different workgroups that are never held at a common barrier, so one wave's
 // depthwise VALU work hides under another's matrix work.
 template <int S, int TY, int TX, int KIN, int NOT, int NW, bool FULL>
@@ -884,7 +900,7 @@ __global__ void __launch_bounds__(64 * NW, (NOT <= 6 ? 2 : 1)) irw_f32_kernel(Ir
       const int gy = oy0 + q / TX, gx = ox0 + q % TX;
       if (gy >= a.Ho || gx >= a.Wo) continue;
       const int64_t pix = (static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx;
-      if (a.ws) {  // > 2 parts: this part's slab of the workspace (irw_reduce adds them in order)
+      if (a.ws) {  // hidden parts: this part's slab of the workspace (irw_reduce adds them in order)
         const int64_t plane = static_cast<int64_t>(a.B) * a.Ho * a.Wo * a.cout;
         *reinterpret_cast<f32x4_t*>(a.ws + part * plane + pix * a.cout + co) = v;
         continue;
@@ -1156,6 +1172,7 @@ const IrwCfg kIrwCfgs[] = {
     NNSX_IRW(1, 7, 7, 64, 6, 4, false),    // 14x14      64 -> 384 -> 96  (24)
     NNSX_IRW(1, 7, 7, 96, 6, 4, false),    // 14x14      96 -> 576 -> 96  (36)
     NNSX_IRW(1, 7, 7, 160, 10, 4, false),  // 7x7       160 -> 960 -> 160 (60, two parts)
+    NNSX_IRW(2, 7, 7, 96, 10, 3, false),   // 14 -> 7    96 -> 576 -> 160 (36, two parts; 3 waves: LDS)
 };
 #undef NNSX_IRW
 
@@ -1198,23 +1215,45 @@ const IrF32Cfg* find_cfg(int S, int H, int W, int cin, int hid, int cout, bool h
 
 }  // namespace
 
+// K-split slices for a small output grid (the classifier: M = batch, 32
+// tiles of 64 x 64) -- otherwise most CUs idle while each workgroup walks all
+// of K.  Returns the k-stages per slice (kstages: no split).
+static int gemm_kchunk(int tiles, int kstages, int N, bool plain) {
+  static const bool splitk = [] {
+    const char* e = std::getenv("NNSX_F32_SPLITK");
+    return !(e && e[0] == '0');
+  }();
+  if (!splitk || !plain || tiles >= 128 || kstages < 8 || N % 4) return kstages;
+  const int splits = std::min(kstages / 4, (512 + tiles - 1) / tiles);
+  return (kstages + splits - 1) / splits;
+}
+
+template <int BM, int BN>
+static int gemm_splits(int M, int N, int Kpad, bool plain) {
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  const int kstages = (Kpad + GKT - 1) / GKT;
+  const int chunk = gemm_kchunk(tiles, kstages, N, plain);
+  return (kstages + chunk - 1) / chunk;
+}
+
 template <int BM, int BN>
 static void pw_gemm_f32_launch(const float* x, const float* wt, const float* bias, const float* res, float* y, int M,
-                               int N, int K, int Kpad, int Npad, int act, hipStream_t s) {
+                               int N, int K, int Kpad, int Npad, int act, float* ws, hipStream_t s) {
   dim3 grid((M + BM - 1) / BM, (N + BN - 1) / BN);
   const int kstages = (Kpad + GKT - 1) / GKT;
-  int chunk = kstages;
-  // a small output grid (the classifier: M = batch) leaves most CUs idle while
-  // each workgroup walks all of K: split K over grid.z, reduce with fp32 atomics
-  const int tiles = static_cast<int>(grid.x * grid.y);
-  if (!res && act == 0 && tiles < 128 && kstages >= 8) {
-    const int splits = std::min(kstages / 4, (256 + tiles - 1) / tiles);
-    chunk = (kstages + splits - 1) / splits;
-    grid.z = static_cast<unsigned>((kstages + chunk - 1) / chunk);
-    (void)hipMemsetAsync(y, 0, static_cast<size_t>(M) * N * sizeof(float), s);
+  int chunk = ws ? gemm_kchunk(static_cast<int>(grid.x * grid.y), kstages, N, !res) : kstages;
+  grid.z = static_cast<unsigned>((kstages + chunk - 1) / chunk);
+  if (grid.z == 1) {
+    hipLaunchKernelGGL((pw_gemm_f32_kernel<BM, BN>), grid, dim3(256), 0, s, x, wt, bias, res, y, M, N, K, Kpad, Npad,
+                       act, kstages);
+    return;
   }
-  hipLaunchKernelGGL((pw_gemm_f32_kernel<BM, BN>), grid, dim3(256), 0, s, x, wt, bias, res, y, M, N, K, Kpad, Npad, act,
-                     chunk);
+  hipLaunchKernelGGL((pw_gemm_f32_kernel<BM, BN>), grid, dim3(256), 0, s, x, wt, bias, res, ws, M, N, K, Kpad, Npad,
+                     act, chunk);
+  const int64_t nq = static_cast<int64_t>(M) * N / 4;
+  const unsigned rg = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((nq + 255) / 256, 2048)));
+  hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(rg), dim3(256), 0, s, ws, static_cast<int>(grid.z), M, N, bias,
+                     act, y);
 }
 
 // Tile choice: the candidate with the least modelled time, where a workgroup
@@ -1242,21 +1281,35 @@ static int pick_gemm_tile(int M, int N, int Kpad) {
   return cand[best][0] * 1000 + cand[best][1];
 }
 
-void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
-                 int Kpad, int Npad, int act, hipStream_t s, int tile) {
-  if (tile <= 0) {
-    static const int forced = [] {
-      const char* e = std::getenv("NNSX_F32_GEMM_TILE");
-      return e ? std::atoi(e) : 0;
-    }();
-    tile = forced > 0 ? forced : pick_gemm_tile(M, N, Kpad);
+static int resolve_tile(int M, int N, int Kpad, int tile) {
+  if (tile > 0) return tile;
+  static const int forced = [] {
+    const char* e = std::getenv("NNSX_F32_GEMM_TILE");
+    return e ? std::atoi(e) : 0;
+  }();
+  return forced > 0 ? forced : pick_gemm_tile(M, N, Kpad);
+}
+
+size_t pw_gemm_f32_workspace_bytes(int M, int N, int Kpad, bool has_res, int tile) {
+  int splits = 1;
+  switch (resolve_tile(M, N, Kpad, tile)) {
+    case 64064: splits = gemm_splits<64, 64>(M, N, Kpad, !has_res); break;
+    case 128064: splits = gemm_splits<128, 64>(M, N, Kpad, !has_res); break;
+    case 64128: splits = gemm_splits<64, 128>(M, N, Kpad, !has_res); break;
+    case 128192: splits = gemm_splits<128, 192>(M, N, Kpad, !has_res); break;
+    default: splits = gemm_splits<128, 128>(M, N, Kpad, !has_res); break;
   }
-  switch (tile) {
-    case 64064: pw_gemm_f32_launch<64, 64>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, s); break;
-    case 128064: pw_gemm_f32_launch<128, 64>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, s); break;
-    case 64128: pw_gemm_f32_launch<64, 128>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, s); break;
-    case 128192: pw_gemm_f32_launch<128, 192>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, s); break;
-    default: pw_gemm_f32_launch<128, 128>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, s); break;
+  return splits > 1 ? static_cast<size_t>(splits) * M * N * sizeof(float) : 0;
+}
+
+void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
+                 int Kpad, int Npad, int act, hipStream_t s, int tile, float* ws) {
+  switch (resolve_tile(M, N, Kpad, tile)) {
+    case 64064: pw_gemm_f32_launch<64, 64>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s); break;
+    case 128064: pw_gemm_f32_launch<128, 64>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s); break;
+    case 64128: pw_gemm_f32_launch<64, 128>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s); break;
+    case 128192: pw_gemm_f32_launch<128, 192>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s); break;
+    default: pw_gemm_f32_launch<128, 128>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s); break;
   }
 }
 
@@ -1329,12 +1382,27 @@ bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout
 }
 
 // Hidden-channel parts per tile.  Fewer tiles than CUs: split the hidden
-// channels over workgroups (every wave keeps >= 1 subtile).  Two parts add
-// into a zeroed output (a + b == b + a: deterministic); more parts (small
-// batches: one 14x14 / 7x7 image is 1-4 tiles) write workspace slabs that
-// irw_reduce adds in part order.
+// channels over workgroups (every wave keeps >= 1 subtile).  The parts write
+// workspace slabs that irw_reduce adds in part order.  (Adding two parts into a
+// zeroed output with fp32 atomics, NNSX_F32_IRW_ATOMIC2=1, is also
+// deterministic but measured 86 vs 71 us on the 7x7 960-hidden block at batch
+// 128: the L2 atomic unit, 4 B per request, is the bottleneck.)
+static int irw_env(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+
+// two hidden parts: add into a zeroed output with fp32 atomics (1) or write
+// workspace slabs + irw_reduce like more parts (0)
+static bool irw_atomic2() {
+  static const bool on = irw_env("NNSX_F32_IRW_ATOMIC2", 0) != 0;
+  return on;
+}
+
 static int irw_parts(const IrwCfg* c, int tiles, int hid) {
   const int nsub = hid / 16;
+  static const int forced = irw_env("NNSX_F32_IRW_PARTS", 0);
+  if (forced > 0) return std::min(forced, std::max(1, nsub / c->NW));
   if (tiles >= 256 || nsub < 8) return 1;
   if (tiles >= 128) return 2;
   const int want = (512 + tiles - 1) / tiles;
@@ -1353,13 +1421,14 @@ static bool launch_irw(const IrwCfg* c, IrBlockF32Args a, hipStream_t s) {
   irw_geometry(c, &a);
   const int tiles = a.tiles_x * a.tiles_y * a.B;
   const int64_t plane = static_cast<int64_t>(a.B) * a.Ho * a.Wo * a.cout;
-  if (a.hsplit > 2 && !a.ws) return false;  // the caller sizes the workspace (ir_block_f32_workspace_bytes)
-  if (a.hsplit <= 2) a.ws = nullptr;
+  const bool slabs = a.hsplit > 2 || (a.hsplit == 2 && !irw_atomic2());
+  if (slabs && !a.ws) return false;  // the caller sizes the workspace (ir_block_f32_workspace_bytes)
+  if (!slabs) a.ws = nullptr;
   const size_t lds = c->lds(a.hid);
   if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(c->kernel),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
     return false;
-  if (a.hsplit == 2) (void)hipMemsetAsync(a.y, 0, static_cast<size_t>(plane) * sizeof(float), s);
+  if (a.hsplit == 2 && !slabs) (void)hipMemsetAsync(a.y, 0, static_cast<size_t>(plane) * sizeof(float), s);
   hipLaunchKernelGGL(c->kernel, dim3(static_cast<unsigned>(tiles * a.hsplit)), dim3(64 * c->NW), lds, s, a);
   if (a.ws) {
     const unsigned grid = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((plane / 4 + 255) / 256, 4096)));
@@ -1374,7 +1443,7 @@ size_t ir_block_f32_workspace_bytes(const IrBlockF32Args& args) {
   const IrwCfg* c = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0);
   if (!c) return 0;
   irw_geometry(c, &a);
-  if (a.hsplit <= 2) return 0;
+  if (a.hsplit < 2 || (a.hsplit == 2 && irw_atomic2())) return 0;
   return static_cast<size_t>(a.hsplit) * a.B * a.Ho * a.Wo * a.cout * sizeof(float);
 }
 

@@ -38,9 +38,14 @@ at::Tensor pw_conv_f32_cuda(const at::Tensor& x, const at::Tensor& wt, const at:
     TORCH_CHECK(res->scalar_type() == at::kFloat && res->is_contiguous() && res->numel() == M * N, "pw_conv(f32): residual");
     r = res->data_ptr<float>();
   }
+  const size_t wsb = nnsx::kernels::pw_gemm_f32_workspace_bytes(static_cast<int>(M), static_cast<int>(N),
+                                                                 static_cast<int>(Kpad), r != nullptr, static_cast<int>(tile));
+  at::Tensor ws;
+  if (wsb) ws = at::empty({static_cast<int64_t>(wsb / sizeof(float))}, x.options());
   nnsx::kernels::pw_gemm_f32(x.data_ptr<float>(), wt.data_ptr<float>(), bias.data_ptr<float>(), r, y.data_ptr<float>(),
                              static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), static_cast<int>(Kpad),
-                             static_cast<int>(Npad), static_cast<int>(act), cur_stream(), static_cast<int>(tile));
+                             static_cast<int>(Npad), static_cast<int>(act), cur_stream(), static_cast<int>(tile),
+                             wsb ? ws.data_ptr<float>() : nullptr);
   return y;
 }
 

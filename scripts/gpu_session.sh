@@ -7,6 +7,7 @@
 #   bench    bench.py (BENCH_ARGS)
 #   prof     rocprofv3 kernel stats of bench.py (PROF_ARGS)
 #   irf32    per-layer fp32 engine micro-benchmark (scripts/bench_ir_f32.py)
+#   irvar    bench_ir_f32 once per IR_VARIANTS env set
 #   pmcf32   PMC counter passes over it (scripts/pmc_f32.sh; SHAPE=, KERNEL=)
 set -o pipefail
 mkdir -p gpurun_out
@@ -34,6 +35,13 @@ for s in ${STEPS//,/ }; do
     irf32)
       timeout -k 10 300 python -u scripts/bench_ir_f32.py ${IR_B:-128} > gpurun_out/bench_ir_f32.log 2>&1 || { echo "bench_ir_f32 failed"; tail -30 gpurun_out/bench_ir_f32.log; exit 1; }
       cat gpurun_out/bench_ir_f32.log ;;
+    irvar)
+      # IR_VARIANTS: ';'-separated env assignments, one bench_ir_f32 run each
+      IFS=';' read -ra VARS <<< "${IR_VARIANTS:-NNSX_F32_IRW=1}"
+      for V in "${VARS[@]}"; do
+        env $V timeout -k 10 300 python -u scripts/bench_ir_f32.py ${IR_B:-128} > gpurun_out/irvar.log 2>&1 || { echo "irvar $V failed"; tail -30 gpurun_out/irvar.log; exit 1; }
+        echo "== $V"; grep -v amdgpu.ids gpurun_out/irvar.log
+      done ;;
     gemmf32)
       for R in ${DW_ROWS:-4}; do
         NNSX_F32_DW_ROWS=$R timeout -k 10 300 python -u scripts/bench_gemm_f32.py ${IR_B:-128} > gpurun_out/bench_gemm_f32_r$R.log 2>&1 || { echo "bench_gemm_f32 failed"; tail -30 gpurun_out/bench_gemm_f32_r$R.log; exit 1; }

@@ -110,7 +110,9 @@ IR_F32_SHAPES = [(112, 32, 32, 16, 1, False), (112, 16, 96, 24, 2, True), (56, 2
                  (42, 32, 192, 32, 1, True), (40, 16, 96, 24, 2, True),
                  (30, 24, 144, 24, 1, True), (17, 64, 384, 96, 1, True),
                  # wave-split kernel: 7x7 whole-image tiles with the hidden channels split over 2 workgroups
-                 (7, 160, 960, 160, 1, True), (35, 96, 576, 96, 1, True)]
+                 (7, 160, 960, 160, 1, True), (35, 96, 576, 96, 1, True),
+                 # 14 -> 7 stride-2 block (B14): one 7x7 image per tile, 3 waves
+                 (14, 96, 576, 160, 2, True)]
 
 
 def _ir_ref64(x, we, be, wd, bd, wp, bp, stride, cout, has_expand, residual):
@@ -150,6 +152,37 @@ def test_ir_block_f32(nns, H, cin, hid, cout, stride, has_expand, B):
     y = torch.ops.nnsx.ir_block(x, we, be, wd, bd, wp, bp, stride, cout, has_expand, residual)
     assert y.shape == (B, (H - 1) // stride + 1, (H - 1) // stride + 1, cout)
     _close(y, _ir_ref64(x, we, be, wd, bd, wp, bp, stride, cout, has_expand, residual), tol=5e-5)
+
+
+@pytest.mark.parametrize("H,cin,hid,cout,stride", [(7, 160, 960, 160, 1), (14, 96, 576, 160, 2)])
+def test_ir_block_f32_two_parts_deterministic(nns, H, cin, hid, cout, stride):
+    """batch 128 on the 7x7 blocks: 128 tiles -> two hidden parts per tile
+    (workspace slabs + ordered reduce); bitwise repeatable."""
+    torch.manual_seed(cin + hid)
+    B = 128
+    x = torch.randn(B, H, H, cin, device="cuda")
+    we = torch.randn(hid, cin, device="cuda") / cin ** 0.5
+    be = torch.randn(hid, device="cuda") * 0.1
+    wd = torch.randn(9, hid, device="cuda") / 3
+    bd = torch.randn(hid, device="cuda") * 0.1
+    wp = torch.randn(cout, hid, device="cuda") / hid ** 0.5
+    bp = torch.randn(cout, device="cuda") * 0.1
+    res = stride == 1 and cin == cout
+    y = torch.ops.nnsx.ir_block(x, we, be, wd, bd, wp, bp, stride, cout, True, res)
+    y2 = torch.ops.nnsx.ir_block(x, we, be, wd, bd, wp, bp, stride, cout, True, res)
+    assert torch.equal(y, y2)
+    _close(y, _ir_ref64(x, we, be, wd, bd, wp, bp, stride, cout, True, res), tol=5e-5)
+
+
+def test_classifier_split_k_deterministic(nns):
+    """M = batch GEMM (split over K, slabs added in order): bitwise repeatable."""
+    torch.manual_seed(5)
+    x = torch.randn(128, 1280, device="cuda")
+    wt = torch.randn(1008, 1280, device="cuda") / 1280 ** 0.5
+    bias = torch.randn(1008, device="cuda")
+    ys = [torch.ops.nnsx.pw_conv(x, wt, bias, None, 1000, 0, True) for _ in range(3)]
+    assert all(torch.equal(ys[0], y) for y in ys[1:])
+    _close(ys[0], x.double().cpu() @ wt[:1000].double().cpu().t() + bias[:1000].double().cpu())
 
 
 def _agreement(f, m, n_images=256, batch=64, seed=0):
