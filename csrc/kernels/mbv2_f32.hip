@@ -673,9 +673,13 @@ struct IrwGeom {
   static constexpr int NPX = NPT * 16;
   static constexpr size_t xs_q = static_cast<size_t>(KQ) * XSP;
   static constexpr size_t hid_q = static_cast<size_t>(4 * NW) * PINP;     // [wave][quad][cell]
-  static constexpr size_t dwo_q = static_cast<size_t>(4 * NW) * NPX;      // [wave][quad][px]
   static constexpr size_t red_q = static_cast<size_t>(2 * 4 * NW) * NPX;  // [buf][wave][quad][px]
-  static size_t lds_bytes(int) { return 16 * std::max(xs_q + hid_q + dwo_q, red_q); }
+  static size_t lds_bytes(int) { return 16 * std::max(xs_q + hid_q, red_q); }
+  // minimum resident workgroups per CU the register budget is sized for.  28x28
+  // (KIN 32, stride 1): 4 (128 VGPRs, LDS allows 4) measured 57 -> 53.5 us at
+  // batch 128 despite 6 spilled VGPRs; the same on the 14x14 64-channel block
+  // (3, 21 spills) lost 40 -> 45 us.
+  static constexpr int MINB = (KIN == 32 && S == 1) ? 4 : NOT <= 6 ? 2 : 1;
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -693,7 +697,7 @@ __device__ __forceinline__ void wave_sync() {
 // maps, where every tile touches the border): only the in-image pixels are
 // expanded (compact index, halos zeroed once per tile).
 template <int S, int TY, int TX, int KIN, int NOT, int NW, bool FULL>
-__global__ void __launch_bounds__(64 * NW, (NOT <= 6 ? 2 : 1)) irw_f32_kernel(IrBlockF32Args a) {
+__global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FULL>::MINB)) irw_f32_kernel(IrBlockF32Args a) {
   using G = IrwGeom<S, TY, TX, KIN, NOT, NW, FULL>;
   constexpr int NT = 64 * NW;
   constexpr int TIY = G::TIY, TIX = G::TIX, PIN = G::PIN, NC16 = G::NC16, NBT = G::NBT, XSP = G::XSP;
@@ -705,7 +709,6 @@ __global__ void __launch_bounds__(64 * NW, (NOT <= 6 ? 2 : 1)) irw_f32_kernel(Ir
   extern __shared__ __attribute__((aligned(16))) float smem[];
   f32x4_t* xs = reinterpret_cast<f32x4_t*>(smem);  // [KQ][XSP]
   f32x4_t* hidw = xs + G::xs_q;                     // [NW waves][4 quads][PINP]
-  f32x4_t* dwo = hidw + G::hid_q;                   // [NW waves][4 quads][NPX]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, g = lane >> 4;
@@ -789,7 +792,6 @@ __global__ void __launch_bounds__(64 * NW, (NOT <= 6 ? 2 : 1)) irw_f32_kernel(Ir
   const int nsub = a.hid >> 4;
   const int sub0 = part * nsub / nparts, sub1 = (part + 1) * nsub / nparts;
   f32x4_t* myhid = hidw + (wave * 4 + g) * PINP;
-  f32x4_t* mydwo = dwo + wave * 4 * NPX + g * NPX;
   f32x4_t ea[NS16 > 0 ? NS16 : 1];
   f32x2_t et = f32x2_t{0.f, 0.f};
   auto load_ea = [&](int hs) {
@@ -858,7 +860,9 @@ __global__ void __launch_bounds__(64 * NW, (NOT <= 6 ? 2 : 1)) irw_f32_kernel(Ir
     }
     wave_sync();
 
-    // ---- depthwise 3x3 + bias + ReLU6 -> private project operand
+    // ---- depthwise 3x3 + bias + ReLU6, straight into the project MFMA: the
+    // lane computing output pixel pt*16+li, channel quad g is exactly the lane
+    // that holds that k-quad of column li in the B operand (mfma_k16 layout)
 #pragma unroll
     for (int pt = 0; pt < NPT; ++pt) {
       f32x4_t d = bd4;
@@ -867,18 +871,12 @@ __global__ void __launch_bounds__(64 * NW, (NOT <= 6 ? 2 : 1)) irw_f32_kernel(Ir
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx)
           d = __builtin_elementwise_fma(myhid[dcell[pt] + ky * TIX + kx], wd4[ky * 3 + kx], d);
-      mydwo[pt * 16 + li] = relu6x4(d);
-    }
-    wave_sync();
-
-    // ---- project: k-split partial over this subtile's 16 channels
-#pragma unroll
-    for (int pt = 0; pt < NPT; ++pt) {
-      const f32x4_t bf = mydwo[pt * 16 + li];
+      const f32x4_t bf = relu6x4(d);
+      // ---- project: k-split partial over this subtile's 16 channels
 #pragma unroll
       for (int o = 0; o < NOT; ++o) acc[pt][o] = mfma_k16(pa[o], bf, acc[pt][o]);
     }
-    wave_sync();
+    wave_sync();  // this wave's hidden image is read out before the next subtile's expand
   }
 
   // ---- cross-wave reduction (fixed order) + bias + residual -> NHWC
@@ -1055,15 +1053,10 @@ __global__ void __launch_bounds__(256, 2) stem_ir1_f32_kernel(StemIr1F32Args a) 
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx)
           d = __builtin_elementwise_fma(myhid[cell + ky * HX + kx], wd4[ky * 3 + kx], d);
-      mydwo[pt * 16 + li] = relu6x4(d);
-    }
-    wave_sync();
-    // ---- project partial over this wave's 16 channels (K = 16 of 32), written over
-    // the wave's own dw outputs (the other channel half reads only its own rows)
-#pragma unroll
-    for (int pp = 0; pp < NPH; ++pp) {
-      const int pt = phalf * NPH + pp;
-      if (pt < NPT) mydwo[pt * 16 + li] = mfma_k16(pa, mydwo[pt * 16 + li], z);
+      // ---- project partial over this wave's 16 channels (K = 16 of 32): the lane
+      // holding pixel q, channel quad g is the one that feeds that k-quad of
+      // column li to the MFMA, so the dw output goes straight in
+      mydwo[pt * 16 + li] = mfma_k16(pa, relu6x4(d), z);
     }
     __syncthreads();
     // ---- channel half 0 + half 1 (fixed order), + bias -> [B][Ho][Wo][16]; the
@@ -1165,6 +1158,7 @@ struct IrwCfg {
 const IrwCfg kIrwCfgs[] = {
     NNSX_IRW(2, 4, 8, 16, 2, 3, true),     // 112 -> 56  16 -> 96 -> 24   (6 subtiles)
     NNSX_IRW(1, 8, 8, 24, 2, 3, true),     // 56x56      24 -> 144 -> 24  (9)
+    NNSX_IRW(2, 4, 4, 24, 2, 3, true),     // 56 -> 28   24 -> 144 -> 32  (9)
     NNSX_IRW(2, 7, 4, 24, 2, 3, true),     // 56 -> 28   24 -> 144 -> 32  (9)
     NNSX_IRW(1, 7, 7, 32, 2, 4, false),    // 28x28      32 -> 192 -> 32  (12)
     NNSX_IRW(2, 2, 7, 32, 4, 4, false),    // 28 -> 14   32 -> 192 -> 64  (12)
