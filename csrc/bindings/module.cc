@@ -8,6 +8,7 @@
 
 #include <cstring>
 
+#include "comm/hpack.h"
 #include "comm/mqtt.h"
 #include "core/caps.h"
 #include "core/log.h"
@@ -466,6 +467,27 @@ PYBIND11_MODULE(_C, m) {
     if (d.empty()) throw Error(err);
     return d;
   }, py::arg("pbtxt"), "Launch description of a pbtxt graph (the reverse conversion)");
+  // HPACK codec of the native gRPC transport (comm/hpack.h), for its tests
+  m.def("hpack_huffman_encode", [](const std::string& s) { return py::bytes(hpack::huffman_encode(s)); });
+  m.def("hpack_huffman_decode", [](const py::bytes& b) {
+    const std::string in = b;
+    std::string out;
+    if (!hpack::huffman_decode(reinterpret_cast<const uint8_t*>(in.data()), in.size(), &out))
+      throw std::invalid_argument("invalid HPACK Huffman string");
+    return out;
+  });
+  m.def("hpack_decode_blocks", [](const std::vector<py::bytes>& blocks) {
+    hpack::Decoder d;  // one connection's decoder: the dynamic table carries over between blocks
+    std::vector<hpack::Headers> out;
+    for (const auto& b : blocks) {
+      const std::string in = b;
+      hpack::Headers h;
+      std::string err;
+      if (!d.decode(reinterpret_cast<const uint8_t*>(in.data()), in.size(), &h, &err)) throw std::invalid_argument(err);
+      out.push_back(std::move(h));
+    }
+    return out;
+  });
   m.def("make_element", [](const std::string& f, const std::string& n) { return make_element(f, n); },
         py::arg("factory"), py::arg("name") = "");
 

@@ -19,7 +19,6 @@
 #include "runtime/hip_util.h"
 #include "runtime/plugin_api.h"
 #include "single/single.h"
-#include "comm/grpc_bridge.h"
 
 namespace py = pybind11;
 
@@ -397,52 +396,6 @@ py::list numpy_views(const std::vector<MemoryPtr>& in, const TensorsInfo* info) 
 
 }  // namespace
 
-// grpcio-backed endpoint of tensor_src_grpc / tensor_sink_grpc (comm/grpc_bridge.h)
-class PyGrpcEndpoint : public comm::GrpcEndpoint {
- public:
-  explicit PyGrpcEndpoint(const comm::GrpcOptions& o) {
-    py::gil_scoped_acquire g;
-    obj_ = py::module_::import("nnstreamer_amd.comm.grpc_transport")
-               .attr("Endpoint")(o.server, o.sending, o.idl, o.host, o.port, o.blocking);
-  }
-  ~PyGrpcEndpoint() override {
-    if (!Py_IsInitialized()) return;
-    py::gil_scoped_acquire g;
-    try {
-      obj_.attr("stop")();
-    } catch (...) {
-    }
-    obj_ = py::object();
-  }
-  bool start(std::string* err) override {
-    py::gil_scoped_acquire g;
-    *err = obj_.attr("start")().cast<std::string>();
-    return err->empty();
-  }
-  bool send(const std::string& m) override {
-    py::gil_scoped_acquire g;
-    return obj_.attr("send")(py::bytes(m)).cast<bool>();
-  }
-  int recv(std::string* m, int timeout_ms) override {
-    py::gil_scoped_acquire g;
-    py::tuple r = obj_.attr("recv")(timeout_ms);
-    const int code = r[0].cast<int>();
-    if (code > 0) *m = r[1].cast<std::string>();
-    return code;
-  }
-  void stop() override {
-    py::gil_scoped_acquire g;
-    obj_.attr("stop")();
-  }
-  int port() override {
-    py::gil_scoped_acquire g;
-    return obj_.attr("port")().cast<int>();
-  }
-
- private:
-  py::object obj_;
-};
-
 TensorInfo tensor_info_from_py(py::handle o) { return info_from_shape(o); }
 
 void register_python_bridge(py::module_& m) {
@@ -491,9 +444,6 @@ void register_python_bridge(py::module_& m) {
         s.close();
       });
 
-  comm::set_grpc_factory([](const comm::GrpcOptions& o) -> std::shared_ptr<comm::GrpcEndpoint> {
-    return std::make_shared<PyGrpcEndpoint>(o);
-  });
   register_filter_framework(std::make_shared<PyFilterFw>());
   register_decoder(std::make_shared<PyDecoderPlugin>());
   set_script_converter_factory([](const std::string& path) -> std::shared_ptr<ConverterSubplugin> {

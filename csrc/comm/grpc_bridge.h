@@ -1,11 +1,10 @@
 // gRPC endpoint interface for tensor_src_grpc / tensor_sink_grpc.
 //
 // The reference links grpc++ (ext/nnstreamer/extra/nnstreamer_grpc_*.cc);
-// no C++ gRPC library exists in this image, so the HTTP/2 transport is the
-// grpcio runtime, driven through the Python bridge
-// (nnstreamer_amd/comm/grpc_transport.py).  Everything else stays native:
-// the elements, the Tensors (de)serialization (serial/serial.h: protobuf or
-// flatbuf IDL bytes) and the service names / method paths:
+// no C++ gRPC library exists in this image, so the transport is our own
+// HTTP/2 (h2c) + HPACK + gRPC-framing implementation (comm/grpc_native.cc),
+// wire-compatible with grpc++ / grpcio peers.  The Tensors payloads are the
+// protobuf or flatbuf IDL bytes of serial/serial.h; service names / paths:
 //   /nnstreamer.<idl>.TensorService/SendTensors  (client -> server stream)
 //   /nnstreamer.<idl>.TensorService/RecvTensors  (server -> client stream)
 #pragma once
@@ -37,9 +36,12 @@ class GrpcEndpoint {
   virtual int port() = 0;
 };
 
+// the native HTTP/2 endpoint (comm/grpc_native.cc)
+std::shared_ptr<GrpcEndpoint> make_native_grpc_endpoint(const GrpcOptions& o);
+
 using GrpcFactory = std::function<std::shared_ptr<GrpcEndpoint>(const GrpcOptions&)>;
-void set_grpc_factory(GrpcFactory f);
-GrpcFactory grpc_factory();  // empty when the bridge is not loaded
+void set_grpc_factory(GrpcFactory f);  // replaces the native endpoint (tests, other transports)
+GrpcFactory grpc_factory();            // the replacement, else make_native_grpc_endpoint
 
 }  // namespace comm
 }  // namespace nnsx

@@ -4,7 +4,8 @@
 // idl (protobuf | flatbuf), host, port, out.  Defaults as the reference: the
 // sink is a client, the source a server, port 55115.  Each buffer is one
 // `Tensors` message (serial/serial.h); the source's output caps come from
-// downstream (a capsfilter), like the reference push-src.
+// downstream (a capsfilter), like the reference push-src.  Transport: the
+// native HTTP/2 gRPC endpoint (comm/grpc_native.cc).
 #include <atomic>
 #include <mutex>
 
@@ -29,7 +30,8 @@ void set_grpc_factory(GrpcFactory f) {
 }
 GrpcFactory grpc_factory() {
   std::lock_guard<std::mutex> lk(g_grpc_mu);
-  return g_grpc;
+  if (g_grpc) return g_grpc;
+  return make_native_grpc_endpoint;
 }
 }  // namespace comm
 
@@ -71,10 +73,6 @@ class GrpcElement : public Base {
 
 std::shared_ptr<comm::GrpcEndpoint> open_endpoint(Element* e, const comm::GrpcOptions& o) {
   auto f = comm::grpc_factory();
-  if (!f) {
-    e->post_error("gRPC transport unavailable (the nnstreamer_amd Python bridge provides grpcio)");
-    return nullptr;
-  }
   const std::string idl = lower(o.idl);
   if (idl != "protobuf" && idl != "flatbuf") {
     e->post_error("unknown idl " + o.idl + " (protobuf or flatbuf)");
