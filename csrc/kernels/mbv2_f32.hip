@@ -44,7 +44,15 @@ namespace kernels {
 
 namespace {
 
-constexpr int kStemIr1TY = 8, kStemIr1TX = 16;
+// stem_ir1 tile (TY, TX) and waves: 16 x 16 with 8 waves measured 136 us at
+// batch 128 vs 145 (8 x 16, 4 waves) and 147 (8 x 32, 8 waves) -- the per-tile
+// fixed cost (4 barriers, patch staging; ~55 us of the kernel when every
+// compute phase is ablated) is amortised over twice the pixels
+#ifndef NNSX_STEM_TILE
+#define NNSX_STEM_TILE 16, 16, 8
+#endif
+constexpr int kStemIr1Cfg[3] = {NNSX_STEM_TILE};
+constexpr int kStemIr1TY = kStemIr1Cfg[0], kStemIr1TX = kStemIr1Cfg[1], kStemIr1NW = kStemIr1Cfg[2];
 
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
@@ -934,14 +942,16 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
 // resident set of workgroups walks all tiles, the weights / normalisation
 // table are set up once per workgroup and the next tile's input bytes are in
 // flight while the current tile computes.
-template <int TY, int TX>
-__global__ void __launch_bounds__(256, 2) stem_ir1_f32_kernel(StemIr1F32Args a) {
+template <int TY, int TX, int NW>
+__global__ void __launch_bounds__(64 * NW, 8 / NW) stem_ir1_f32_kernel(StemIr1F32Args a) {
+  constexpr int NT = 64 * NW, NPP = NW / 2;  // waves = 2 channel halves x NPP pixel parts
+  static_assert(NW % 2 == 0 && NT >= 256, "stem_ir1: waves");
   constexpr int HY = TY + 2, HX = TX + 2, PIN = HY * HX;
   constexpr int NBT = (PIN + 15) / 16, PINP = NBT * 16;
   constexpr int IY = 2 * HY + 1, IX = 2 * HX + 1, PITCH = IX * 3;
   constexpr int NPT = (TY * TX + 15) / 16, NPX = NPT * 16;
   constexpr int XIN = (IY * PITCH + 3) / 4 * 4;  // floats, 16-B aligned end
-  constexpr int NIN = IY * PITCH, NIT = (NIN + 255) / 256;
+  constexpr int NIN = IY * PITCH, NIT = (NIN + NT - 1) / NT;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* xin = smem;                                       // [IY][PITCH] normalised input
   float* lut = smem + XIN;                                 // [256] (v + add) / div
@@ -950,14 +960,14 @@ __global__ void __launch_bounds__(256, 2) stem_ir1_f32_kernel(StemIr1F32Args a) 
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, g = lane >> 4;
-  const int chalf = wave & 1, phalf = wave >> 1;  // wave = (16-channel half, pixel half)
+  const int chalf = wave & 1, phalf = wave >> 1;  // wave = (16-channel half, pixel part)
   const int tiles_img = a.tiles_x * a.tiles_y;
   const int ntiles = tiles_img * a.B;
 
   // ---- once per workgroup: normalisation table, weights in registers.  The
   // normalisation (x + add) / div -- the pipeline's tensor_transform arithmetic,
   // exact fp32 division -- is a 256-entry table.
-  lut[tid] = (static_cast<float>(tid) + a.add) / a.div;
+  if (tid < 256) lut[tid] = (static_cast<float>(tid) + a.add) / a.div;
   float sa[7];  // stem weights of this wave's 16 channels: k = 4t + g (27 taps + 1 zero)
   int off[7];
 #pragma unroll
@@ -988,7 +998,7 @@ __global__ void __launch_bounds__(256, 2) stem_ir1_f32_kernel(StemIr1F32Args a) 
     const uint8_t* xb = a.x + static_cast<int64_t>(b) * a.H * a.W * 3;
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
-      const int i = tid + it * 256;
+      const int i = tid + it * NT;
       const int r = i / PITCH, c = i - r * PITCH;
       const int iy = iy0 + r, ix = ix0 + c / 3;
       raw[it] = (i < NIN && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
@@ -1009,14 +1019,14 @@ __global__ void __launch_bounds__(256, 2) stem_ir1_f32_kernel(StemIr1F32Args a) 
     __syncthreads();  // previous tile done with xin / hidden / dwo (and lut written)
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
-      const int i = tid + it * 256;
+      const int i = tid + it * NT;
       if (i < NIN) xin[i] = raw[it] >= 0 ? lut[raw[it]] : 0.f;
     }
     if (tile + static_cast<int>(gridDim.x) < ntiles) fetch(tile + gridDim.x);
     __syncthreads();
 
-    // ---- stem MFMA over this pixel half of the halo grid, two pixel tiles at a time
-    constexpr int NBH = (NBT + 1) / 2;
+    // ---- stem MFMA over this pixel part of the halo grid, two pixel tiles at a time
+    constexpr int NBH = (NBT + NPP - 1) / NPP;
 #pragma unroll
     for (int jj = 0; jj < NBH; jj += 2) {
       const int j = phalf * NBH + jj;
@@ -1037,9 +1047,9 @@ __global__ void __launch_bounds__(256, 2) stem_ir1_f32_kernel(StemIr1F32Args a) 
       myhid[c0] = in0 ? relu6x4(e0 + bs4) : z;
       if (j1 != j) myhid[c1] = in1 ? relu6x4(e1 + bs4) : z;
     }
-    __syncthreads();  // both pixel halves of each channel half's hidden image
-    // ---- depthwise 3x3 + bias + ReLU6 on this wave's output pixel half
-    constexpr int NPH = (NPT + 1) / 2;
+    __syncthreads();  // all pixel parts of each channel half's hidden image
+    // ---- depthwise 3x3 + bias + ReLU6 on this wave's output pixel part
+    constexpr int NPH = (NPT + NPP - 1) / NPP;
 #pragma unroll
     for (int pp = 0; pp < NPH; ++pp) {
       const int pt = phalf * NPH + pp;
@@ -1457,7 +1467,7 @@ bool stem_ir1_f32(const StemIr1F32Args& args, hipStream_t s) {
   a.tiles_x = (a.Wo + kStemIr1TX - 1) / kStemIr1TX;
   const size_t lds = stem_ir1_lds_bytes();
   if (lds > 160 * 1024) return false;
-  const void* fn = reinterpret_cast<const void*>(&stem_ir1_f32_kernel<kStemIr1TY, kStemIr1TX>);
+  const void* fn = reinterpret_cast<const void*>(&stem_ir1_f32_kernel<kStemIr1TY, kStemIr1TX, kStemIr1NW>);
   if (lds > 64 * 1024 &&
       hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
     return false;
@@ -1467,12 +1477,14 @@ bool stem_ir1_f32(const StemIr1F32Args& args, hipStream_t s) {
   static const int resident = [fn, lds] {
     int dev = 0, ncu = 256, per_cu = 1;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * kStemIr1NW, lds) != hipSuccess || per_cu < 1)
+      per_cu = 1;
     return ncu * per_cu;
   }();
   const int tiles = a.tiles_x * a.tiles_y * a.B;
   const unsigned grid = static_cast<unsigned>(std::min(tiles, resident));
-  hipLaunchKernelGGL((stem_ir1_f32_kernel<kStemIr1TY, kStemIr1TX>), dim3(grid), dim3(256), lds, s, a);
+  hipLaunchKernelGGL((stem_ir1_f32_kernel<kStemIr1TY, kStemIr1TX, kStemIr1NW>), dim3(grid), dim3(64 * kStemIr1NW), lds,
+                     s, a);
   return true;
 }
 
