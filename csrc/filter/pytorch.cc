@@ -21,6 +21,8 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/script.h>
 
+#include <atomic>
+#include <cstdlib>
 #include <fstream>
 #include <sstream>
 
@@ -69,9 +71,10 @@ void flatten(const c10::IValue& v, std::vector<at::Tensor>* out) {
 
 struct GraphState {
   std::unique_ptr<at::cuda::CUDAGraph> graph;
-  std::vector<at::Tensor> static_in;
+  std::vector<at::Tensor> static_in;  // the stable input slot the frame is copied into
   std::vector<at::Tensor> static_out;
-  std::vector<std::vector<int64_t>> shapes;
+  // downstream holders of static_out handed out without a copy (0 = free)
+  std::shared_ptr<std::atomic<int>> out_held = std::make_shared<std::atomic<int>>(0);
 };
 
 class TorchInstance : public FilterInstance {
@@ -244,17 +247,19 @@ class TorchInstance : public FilterInstance {
     return t;
   }
 
-  MemoryPtr wrap_output(at::Tensor t, int dev_idx, hipStream_t s) {
+  MemoryPtr wrap_output(at::Tensor t, int dev_idx, hipStream_t s, std::shared_ptr<std::atomic<int>> held = nullptr) {
     t = t.contiguous();
     auto holder = std::make_shared<at::Tensor>(t);
     size_t bytes = t.numel() * t.element_size();
     if (dev_idx >= 0) {
-      auto m = Memory::wrap(t.data_ptr(), bytes, MemPlace::DEVICE, dev_idx, [holder, s, dev_idx](Memory* mm) {
-        // the caching allocator reuses the block in the order of its stream: make
-        // that stream wait for every downstream reader before dropping the tensor
+      auto m = Memory::wrap(t.data_ptr(), bytes, MemPlace::DEVICE, dev_idx, [holder, s, dev_idx, held](Memory* mm) {
+        // the caching allocator (or the next graph replay, for a static output)
+        // reuses the block in the order of its stream: make that stream wait for
+        // every downstream reader before dropping the tensor
         hip::DeviceGuard g(dev_idx);
         mm->wait_uses(s);
         holder->reset();
+        if (held) held->fetch_sub(1);
       });
       m->mark_ready(s);
       return m;
@@ -295,12 +300,21 @@ class TorchInstance : public FilterInstance {
     }
 
     std::vector<at::Tensor> outs;
-    if (use_graph_ && dev_idx >= 0) {
-      GraphState& gs = graph_for(inputs, s, dev_idx);
-      for (size_t i = 0; i < inputs.size(); ++i) gs.static_in[i].copy_(inputs[i], /*non_blocking=*/true);
-      gs.graph->replay();
-      // replay reuses the static outputs: hand downstream a private copy
-      for (auto& t : gs.static_out) outs.push_back(t.clone());
+    std::shared_ptr<std::atomic<int>> held;  // static outputs handed out as they are
+    GraphState* gs = use_graph_ && dev_idx >= 0 ? graph_for(inputs, s, dev_idx) : nullptr;
+    if (gs) {
+      // an instance whose static outputs no downstream element holds: the replay
+      // rewrites them and hands them out as they are (no copy); they return to
+      // the instance when their last reader is done
+      for (size_t i = 0; i < gs->static_in.size(); ++i) gs->static_in[i].copy_(inputs[i], /*non_blocking=*/true);
+      gs->graph->replay();
+      if (copy_out_) {  // NNSX_GRAPH_COPY_OUT=1: one instance, private copies of its outputs
+        for (auto& t : gs->static_out) outs.push_back(t.clone());
+      } else {
+        held = gs->out_held;
+        held->store(1);
+        outs = gs->static_out;
+      }
     } else {
       std::vector<c10::IValue> iv;
       for (auto& t : inputs) iv.push_back(prepare(t));
@@ -312,9 +326,10 @@ class TorchInstance : public FilterInstance {
       ctx.out_info->resize(static_cast<unsigned>(outs.size()));
       for (size_t k = 0; k < outs.size(); ++k) ctx.out_info->at(static_cast<unsigned>(k)) = info_from_tensor(outs[k]);
     }
+    if (held) held->store(static_cast<int>(outs.size()));  // one count per handed-out tensor
     for (auto& t : outs) {
       if (dev_idx < 0 && t.is_cuda()) t = t.cpu();
-      out->push_back(wrap_output(t, dev_idx, s));
+      out->push_back(wrap_output(t, dev_idx, s, held));
     }
     return 0;
   }
@@ -325,14 +340,23 @@ class TorchInstance : public FilterInstance {
   // still queued downstream makes `s` wait for that output's readers
   // (wrap_output) -- which would otherwise invalidate a capture that starts
   // after a hot reload or a new input shape.
-  GraphState& graph_for(const std::vector<at::Tensor>& inputs, hipStream_t s, int dev_idx) {
+  //
+  // A replay rewrites its instance's static outputs, so an instance is only
+  // replayed when downstream holds none of them (double/triple buffering of the
+  // outputs); each input shape keeps up to kInstances instances -- created in
+  // the first frames, while the downstream queues fill -- and when all are
+  // held the frame runs eagerly (nullptr).
+  static constexpr size_t kInstances = 6;
+  GraphState* graph_for(const std::vector<at::Tensor>& inputs, hipStream_t s, int dev_idx) {
     std::string key;
     for (auto& t : inputs) {
       for (auto d : t.sizes()) key += std::to_string(d) + "x";
       key += std::string(c10::toString(t.scalar_type())) + ";";
     }
-    auto it = graphs_.find(key);
-    if (it != graphs_.end()) return *it->second;
+    auto& set = graphs_[key];
+    for (auto& g : set)
+      if (g->out_held->load() == 0) return g.get();  // (never held with copy_out_)
+    if (set.size() >= kInstances) return nullptr;
     hip::DeviceGuard dg(dev_idx);
     if (!cap_stream_) hip::check(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "capture stream");
     hipEvent_t ev;
@@ -344,11 +368,13 @@ class TorchInstance : public FilterInstance {
       c10::hip::HIPStreamGuardMasqueradingAsCUDA cg(
           c10::hip::getStreamFromExternalMasqueradingAsCUDA(cap_stream_, static_cast<c10::DeviceIndex>(dev_idx)));
       for (auto& t : inputs) gs->static_in.push_back(torch::empty_like(t, t.options()).copy_(t));
+      const std::vector<at::Tensor>& src = gs->static_in;
       std::vector<c10::IValue> iv;
-      // warm up on the capture stream (lazy init, autotuning) before capturing
-      for (int w = 0; w < 3; ++w) {
+      // warm up on the capture stream (lazy init, autotuning) before capturing;
+      // later instances of a shape need only one pass
+      for (int w = 0; w < (set.empty() ? 3 : 1); ++w) {
         iv.clear();
-        for (auto& t : gs->static_in) iv.push_back(prepare(t));
+        for (auto& t : src) iv.push_back(prepare(t));
         std::vector<at::Tensor> tmp;
         flatten(module_.forward(iv), &tmp);
       }
@@ -356,15 +382,21 @@ class TorchInstance : public FilterInstance {
       gs->graph = std::make_unique<at::cuda::CUDAGraph>();
       gs->graph->capture_begin({0, 0}, hipStreamCaptureModeThreadLocal);
       iv.clear();
-      for (auto& t : gs->static_in) iv.push_back(prepare(t));
+      for (auto& t : src) iv.push_back(prepare(t));
       flatten(module_.forward(iv), &gs->static_out);
       gs->graph->capture_end();
     }
     hip::check(hipEventDestroy(ev), "capture event destroy");
-    NNSX_LOGI("pytorch", "captured hipGraph for input shape ", key);
-    auto& ref = *gs;
-    graphs_[key] = std::move(gs);
-    return ref;
+    // the replay runs on s, after the capture stream's work (the static outputs'
+    // first contents are not handed out, but keep the streams ordered)
+    hipEvent_t done;
+    hip::check(hipEventCreateWithFlags(&done, hipEventDisableTiming), "capture done event");
+    hip::check(hipEventRecord(done, cap_stream_), "capture done record");
+    hip::check(hipStreamWaitEvent(s, done, 0), "capture done wait");
+    hip::check(hipEventDestroy(done), "capture done destroy");
+    NNSX_LOGI("pytorch", "captured hipGraph for input shape ", key, ", instance ", set.size());
+    set.push_back(std::move(gs));
+    return set.back().get();
   }
 
   FilterProperties props_;
@@ -374,10 +406,14 @@ class TorchInstance : public FilterInstance {
   int bcast_root_ = -1;  // custom=broadcast:<rank>
   std::string bcast_backend_ = "auto", bcast_store_, bcast_name_;
   size_t bcast_bytes_ = 0;
+  const bool copy_out_ = [] {
+    const char* e = std::getenv("NNSX_GRAPH_COPY_OUT");
+    return e && e[0] == '1';
+  }();
   bool channels_last_ = false;
   DType compute_dtype_ = DType::END;
   std::mutex mu_;
-  std::map<std::string, std::unique_ptr<GraphState>> graphs_;
+  std::map<std::string, std::vector<std::unique_ptr<GraphState>>> graphs_;
   hipStream_t cap_stream_ = nullptr;  // private capture stream (graph_for)
 };
 

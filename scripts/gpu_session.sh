@@ -7,6 +7,7 @@
 #   bench    bench.py (BENCH_ARGS)
 #   prof     rocprofv3 kernel stats of bench.py (PROF_ARGS)
 #   irf32    per-layer fp32 engine micro-benchmark (scripts/bench_ir_f32.py)
+#   latprof  rocprofv3 host+device trace of the batch-1 latency run
 #   irvar    bench_ir_f32 once per IR_VARIANTS env set
 #   pmcf32   PMC counter passes over it (scripts/pmc_f32.sh; SHAPE=, KERNEL=)
 set -o pipefail
@@ -32,6 +33,10 @@ for s in ${STEPS//,/ }; do
     prof)
       (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run --output-format csv -- python3 $R/bench.py ${PROF_ARGS} > $R/gpurun_out/prof.log 2>&1) || { echo "prof failed"; tail -30 gpurun_out/prof.log; exit 1; }
       find gpurun_out/prof -name "*kernel_stats.csv" ;;
+    latprof)
+      # host (HIP API) + device timeline of the batch-1 latency run
+      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --hip-trace --memory-copy-trace -d $R/gpurun_out/latprof -o run --output-format csv -- python3 $R/bench.py --precision fp32 --steps 3 --warmup 2 --latency-frames 200 > $R/gpurun_out/latprof.log 2>&1) || { echo "latprof failed"; tail -30 gpurun_out/latprof.log; exit 1; }
+      tail -1 gpurun_out/latprof.log | cut -c1-300 ;;
     irf32)
       timeout -k 10 300 python -u scripts/bench_ir_f32.py ${IR_B:-128} > gpurun_out/bench_ir_f32.log 2>&1 || { echo "bench_ir_f32 failed"; tail -30 gpurun_out/bench_ir_f32.log; exit 1; }
       cat gpurun_out/bench_ir_f32.log ;;
