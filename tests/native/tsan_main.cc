@@ -38,6 +38,24 @@ int main() {
   run(src + " ! tee name=t t. ! queue ! tensor_mux name=m sync-mode=nosync ! fakesink "
             "t. ! queue ! tensor_transform mode=typecast option=float32 ! m.");
   run(src + " ! tensor_aggregator frames-out=4 frames-dim=3 ! queue ! tensor_demux name=d d.src_0 ! queue ! fakesink");
+  // sparse codec round trip, protobuf serialisation round trip, tensor_if
+  run(src + " ! tensor_sparse_enc ! queue ! tensor_sparse_dec ! fakesink");
+  run(src + " ! tensor_decoder mode=protobuf ! queue ! tensor_converter ! fakesink");
+  run(src + " ! tensor_if name=tif compared-value=TENSOR_AVERAGE_VALUE supplied-value=100 operator=GT "
+            "then=PASSTHROUGH else=PASSTHROUGH tif.src_0 ! queue ! fakesink tif.src_1 ! queue ! fakesink");
+  // native gRPC (HTTP/2): source server thread + sink client pipeline
+  {
+    auto server = parse_launch("tensor_src_grpc name=gs server=true port=0 ! other/tensors,format=static,"
+                               "num_tensors=1,dimensions=3:32:32:1,types=uint8,framerate=30/1 ! queue ! fakesink");
+    server->set_state(State::PLAYING);
+    std::string port = "0";
+    for (int i = 0; i < 500 && port == "0"; ++i) {
+      port = server->get_by_name("gs")->get_property("port");
+      std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    }
+    run(src + " ! tensor_sink_grpc host=127.0.0.1 port=" + port);
+    server->set_state(State::NULL_);
+  }
   // tensor_query in-process over TCP: server thread + client pipeline
   {
     auto server = parse_launch(
