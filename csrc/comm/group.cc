@@ -191,8 +191,7 @@ std::map<std::string, std::weak_ptr<Group>> g_groups;
 // Process-local hand-off for point-to-point sends to oneself (a query client
 // and server in the same process): the header still goes through the store so
 // the FIFO order is shared with remote senders; the blobs stay zero-copy.
-std::mutex g_local_mu;
-std::map<std::string, std::vector<MemoryPtr>> g_local;
+constexpr uint64_t kTagP2P = 0;  // mesh tags: p2p messages; collectives use 1 + their sequence
 
 }  // namespace
 
@@ -258,6 +257,153 @@ bool StoreClient::del(const std::string& key) { return call("del", key, nullptr,
 void StoreClient::close() {
   if (conn_) conn_->close();
 }
+std::string StoreClient::local_ip() const { return conn_ ? conn_->local_ip() : std::string("127.0.0.1"); }
+
+// ================================================================== mesh ====
+Mesh::~Mesh() { close(); }
+
+bool Mesh::start(StoreClient* store, const std::string& prefix, int grank, int n, int timeout_ms, std::string* err) {
+  store_ = store;
+  prefix_ = prefix;
+  grank_ = grank;
+  n_ = n;
+  timeout_ms_ = timeout_ms;
+  out_.assign(static_cast<size_t>(n), nullptr);
+  out_mu_ = std::vector<std::mutex>(static_cast<size_t>(n));
+  lost_.assign(static_cast<size_t>(n), 0);
+  if (!lis_.listen("0.0.0.0", 0, err)) return false;
+  const std::string addr = strfmt(store->local_ip(), ":", lis_.port());
+  if (!store->set(strfmt(prefix_, "/mesh/", grank_), addr)) {
+    if (err) *err = "mesh: cannot publish the link address";
+    return false;
+  }
+  acceptor_ = std::thread([this] {
+    while (!closed_.load()) {
+      auto c = lis_.accept(100);
+      if (!c) continue;
+      std::lock_guard<std::mutex> lk(mu_);
+      if (closed_.load()) {
+        c->close();
+        break;
+      }
+      in_.push_back(c);
+      readers_.emplace_back([this, c] { reader(c); });
+    }
+  });
+  return true;
+}
+
+void Mesh::reader(std::shared_ptr<Connection> c) {
+  Message hello;
+  if (!c->recv(&hello, timeout_ms_, nullptr) || hello.type != MsgType::HELLO) return;
+  const int src = static_cast<int>(hello.client_id);
+  if (src < 0 || src >= n_) return;
+  while (true) {
+    Message m;
+    if (!c->recv(&m, -1, nullptr)) {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (!closed_.load()) lost_[static_cast<size_t>(src)] = 1;  // broke without a goodbye
+      cv_.notify_all();
+      return;
+    }
+    if (m.type == MsgType::BYE) return;
+    std::lock_guard<std::mutex> lk(mu_);
+    const uint64_t tag = m.seq;
+    inbox_.push_back(Item{src, tag, std::move(m)});
+    cv_.notify_all();
+  }
+}
+
+bool Mesh::send(int peer, uint64_t tag, Message m, std::string* err) {
+  std::lock_guard<std::mutex> lk(out_mu_[static_cast<size_t>(peer)]);
+  auto& c = out_[static_cast<size_t>(peer)];
+  if (!c) {
+    std::string addr, host;
+    int port = 0;
+    if (!store_->get(strfmt(prefix_, "/mesh/", peer), &addr, timeout_ms_) || !split_hostport(addr, &host, &port)) {
+      if (err) *err = strfmt("mesh: no link address of member ", peer);
+      return false;
+    }
+    c = Connection::connect(host, port, timeout_ms_, err);
+    if (!c) return false;
+    Message h;
+    h.type = MsgType::HELLO;
+    h.client_id = static_cast<uint64_t>(grank_);
+    if (!c->send(h)) {
+      c.reset();
+      if (err) *err = strfmt("mesh: cannot greet member ", peer);
+      return false;
+    }
+  }
+  m.type = MsgType::DATA;
+  m.seq = tag;
+  if (!c->send(m)) {
+    if (err) *err = strfmt("mesh: the link to member ", peer, " broke");
+    return false;
+  }
+  return true;
+}
+
+void Mesh::deliver_local(uint64_t tag, Message m) {
+  std::lock_guard<std::mutex> lk(mu_);
+  inbox_.push_back(Item{grank_, tag, std::move(m)});
+  cv_.notify_all();
+}
+
+bool Mesh::recv(uint64_t tag, int src, Message* m, int* from, int timeout_ms, bool* timed_out, std::string* err) {
+  if (timed_out) *timed_out = false;
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(std::max(0, timeout_ms));
+  std::unique_lock<std::mutex> lk(mu_);
+  while (true) {
+    for (auto it = inbox_.begin(); it != inbox_.end(); ++it)
+      if (it->tag == tag && (src < 0 || it->src == src)) {
+        *m = std::move(it->m);
+        if (from) *from = it->src;
+        inbox_.erase(it);
+        return true;
+      }
+    if (closed_.load()) {
+      if (err) *err = "mesh: closed";
+      return false;
+    }
+    for (int r = 0; r < n_; ++r)
+      if (lost_[static_cast<size_t>(r)] && (src < 0 || src == r)) {
+        if (err) *err = strfmt("lost the link to member ", r);
+        return false;
+      }
+    if (timeout_ms < 0) {
+      cv_.wait(lk);
+    } else if (cv_.wait_until(lk, deadline) == std::cv_status::timeout) {
+      if (timed_out) *timed_out = true;
+      return false;
+    }
+  }
+}
+
+void Mesh::close() {
+  if (closed_.exchange(true)) return;
+  lis_.close();
+  if (acceptor_.joinable()) acceptor_.join();
+  for (size_t r = 0; r < out_.size(); ++r) {
+    std::lock_guard<std::mutex> lk(out_mu_[r]);
+    if (!out_[r]) continue;
+    Message bye;
+    bye.type = MsgType::BYE;
+    (void)out_[r]->send(bye);  // orderly goodbye: the peer's reader ends without a "lost" mark
+    out_[r]->close();
+  }
+  std::vector<std::thread> readers;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (auto& c : in_) c->shutdown();  // the readers own their descriptors until joined
+    readers.swap(readers_);
+    cv_.notify_all();
+  }
+  for (auto& t : readers)
+    if (t.joinable()) t.join();
+  std::lock_guard<std::mutex> lk(mu_);
+  in_.clear();
+}
 
 std::shared_ptr<void> host_store(const std::string& host, int port, bool* in_use, std::string* err) {
   std::lock_guard<std::mutex> lk(g_store_mu);
@@ -271,6 +417,7 @@ std::shared_ptr<void> host_store(const std::string& host, int port, bool* in_use
 
 // ================================================================= group ====
 Group::~Group() {
+  mesh_.reset();  // goodbyes first: peers see an orderly end of our links
   if (comm_) {
     hip::DeviceGuard g(device_);
     if (stream_) (void)hipStreamSynchronize(stream_);
@@ -355,6 +502,11 @@ bool Group::init(const GroupSpec& in, std::string* err) {
       return false;
     }
   }
+  // ---- member-to-member links (headers; payloads too on the tcp backend) ----
+  if (n > 1) {
+    mesh_ = std::make_unique<Mesh>();
+    if (!mesh_->start(store_.get(), prefix_, grank_, n, spec_.timeout_ms, err)) return false;
+  }
   // ---- data plane: RCCL when every member holds a GPU ----
   bool all_dev = device_ >= 0 && hip::available();
   if (n > 1) {
@@ -403,6 +555,10 @@ bool Group::init(const GroupSpec& in, std::string* err) {
 
 void Group::cancel() {
   if (store_) store_->close();
+  if (mesh_) mesh_->close();
+  std::lock_guard<std::mutex> lk(local_mu_);
+  cancelled_.store(true);
+  local_cv_.notify_all();
 }
 
 bool Group::put(const std::string& k, const std::string& v, int readers) { return store_->set(key(k), v, readers); }
@@ -502,6 +658,47 @@ void Group::finish_inputs(const std::vector<MemoryPtr>& in) {
     if (m->size()) m->record_use(stream_, device_);
 }
 
+// ------------------------------------------------------------ messages ----
+// packet -> mesh message: the encoded header rides in `caps`; on the tcp
+// backend the payload blobs follow it on the same link
+Message Group::to_message(const Packet& p) {
+  Message m;
+  m.caps = encode(p, false);
+  if (!rccl()) {
+    m.blobs = p.blobs;
+    for (auto& b : p.blobs) bytes_sent_ += b->size();
+  }
+  return m;
+}
+
+// mesh message -> packet header (+ payload on the tcp backend)
+bool Group::from_message(Message&& m, Packet* p, std::vector<size_t>* sizes, std::vector<std::string>* metas) {
+  if (!decode(m.caps, p, false, sizes, metas)) return false;
+  if (rccl()) return true;
+  if (m.blobs.size() != sizes->size()) return false;
+  for (size_t i = 0; i < m.blobs.size(); ++i) {
+    if (!(*metas)[i].empty()) {
+      MetaInfo mi;
+      if (MetaInfo::parse((*metas)[i].data(), (*metas)[i].size(), &mi)) m.blobs[i]->set_meta(mi);
+    }
+    bytes_recv_ += m.blobs[i]->size();
+  }
+  p->blobs = std::move(m.blobs);
+  return true;
+}
+
+bool Group::recv_from(uint64_t tag, int src, Packet* p, std::vector<size_t>* sizes, std::vector<std::string>* metas,
+                      std::string* err, const char* what) {
+  Message m;
+  bool to = false;
+  std::string e;
+  if (!mesh_->recv(tag, src, &m, nullptr, spec_.timeout_ms, &to, &e) || !from_message(std::move(m), p, sizes, metas)) {
+    if (err) *err = strfmt(what, ": no message from member ", src, to ? " (timed out)" : (e.empty() ? "" : " (" + e + ")"));
+    return false;
+  }
+  return true;
+}
+
 // ----------------------------------------------------------- allgather ----
 bool Group::allgather(const Packet& mine, std::vector<Packet>* all, std::string* err, MemoryPtr* stacked) {
   const int n = size();
@@ -514,11 +711,9 @@ bool Group::allgather(const Packet& mine, std::vector<Packet>* all, std::string*
     if (stacked && mine.blobs.size() == 1) *stacked = mine.blobs[0];
     return true;
   }
-  const bool inl = !rccl();
-  if (!put(strfmt("ag/", seq, "/", grank_), encode(mine, inl), n - 1)) {
-    if (err) *err = "allgather: store write failed";
-    return false;
-  }
+  const uint64_t tag = 1 + seq;
+  for (int r = 0; r < n; ++r)
+    if (r != grank_ && !mesh_->send(r, tag, to_message(mine), err)) return false;
   std::vector<std::vector<size_t>> sizes(n);
   std::vector<std::vector<std::string>> metas(n);
   for (int r = 0; r < n; ++r) {
@@ -529,16 +724,12 @@ bool Group::allgather(const Packet& mine, std::vector<Packet>* all, std::string*
       }
       continue;
     }
-    std::string v;
-    if (!get(strfmt("ag/", seq, "/", r), &v, -1) || !decode(v, &(*all)[r], inl, &sizes[r], &metas[r])) {
-      if (err) *err = strfmt("allgather: no header from member ", r);
-      return false;
-    }
+    if (!recv_from(tag, r, &(*all)[r], &sizes[r], &metas[r], err, "allgather")) return false;
   }
   bool one_uniform = true;
   for (int r = 0; r < n; ++r)
     one_uniform = one_uniform && sizes[r].size() == 1 && sizes[r][0] == sizes[0][0] && sizes[0][0] > 0;
-  if (inl) {
+  if (!rccl()) {
     if (stacked && one_uniform) {
       const size_t s = sizes[0][0];
       auto out = Memory::alloc_pinned(s * n);
@@ -619,23 +810,17 @@ bool Group::broadcast(int root, Packet* pkt, std::string* err) {
   const int n = size();
   const uint64_t seq = seq_++;
   if (n == 1) return true;
-  const bool inl = !rccl();
+  const uint64_t tag = 1 + seq;
   std::vector<size_t> sizes;
   std::vector<std::string> metas;
   if (grank_ == root) {
-    if (!put(strfmt("bc/", seq), encode(*pkt, inl), n - 1)) {
-      if (err) *err = "broadcast: store write failed";
-      return false;
-    }
+    for (int r = 0; r < n; ++r)
+      if (r != root && !mesh_->send(r, tag, to_message(*pkt), err)) return false;
     for (auto& b : pkt->blobs) sizes.push_back(b->size());
-  } else {
-    std::string v;
-    if (!get(strfmt("bc/", seq), &v, -1) || !decode(v, pkt, inl, &sizes, &metas)) {
-      if (err) *err = "broadcast: no header from the root";
-      return false;
-    }
+  } else if (!recv_from(tag, root, pkt, &sizes, &metas, err, "broadcast")) {
+    return false;
   }
-  if (inl) return true;
+  if (!rccl()) return true;
   hip::DeviceGuard dg(device_);
   auto comm = static_cast<ncclComm_t>(comm_);
   std::vector<MemoryPtr> outs;
@@ -667,7 +852,7 @@ bool Group::broadcast(int root, Packet* pkt, std::string* err) {
 bool Group::scatter(int root, const std::vector<Packet>* parts, Packet* mine, std::string* err) {
   const int n = size();
   const uint64_t seq = seq_++;
-  const bool inl = !rccl();
+  const uint64_t tag = 1 + seq;
   if (grank_ == root) {
     if (!parts || static_cast<int>(parts->size()) != n) {
       if (err) *err = "scatter: the root needs one part per member";
@@ -676,11 +861,8 @@ bool Group::scatter(int root, const std::vector<Packet>* parts, Packet* mine, st
     *mine = (*parts)[root];
     mine->src = root;
     for (int r = 0; r < n; ++r)
-      if (r != root && !put(strfmt("sc/", seq, "/", r), encode((*parts)[r], inl), 1)) {
-        if (err) *err = "scatter: store write failed";
-        return false;
-      }
-    if (inl || n == 1) return true;
+      if (r != root && !mesh_->send(r, tag, to_message((*parts)[r]), err)) return false;
+    if (!rccl() || n == 1) return true;
     hip::DeviceGuard dg(device_);
     auto comm = static_cast<ncclComm_t>(comm_);
     if (!nccl_ok(ncclGroupStart(), "ncclGroupStart", err)) return false;
@@ -700,14 +882,10 @@ bool Group::scatter(int root, const std::vector<Packet>* parts, Packet* mine, st
       if (r != root) finish_inputs((*parts)[r].blobs);
     return true;
   }
-  std::string v;
   std::vector<size_t> sizes;
   std::vector<std::string> metas;
-  if (!get(strfmt("sc/", seq, "/", grank_), &v, -1) || !decode(v, mine, inl, &sizes, &metas)) {
-    if (err) *err = "scatter: no header from the root";
-    return false;
-  }
-  if (inl) return true;
+  if (!recv_from(tag, root, mine, &sizes, &metas, err, "scatter")) return false;
+  if (!rccl()) return true;
   hip::DeviceGuard dg(device_);
   mine->blobs = alloc_recv(sizes, metas);
   auto comm = static_cast<ncclComm_t>(comm_);
@@ -724,29 +902,29 @@ bool Group::scatter(int root, const std::vector<Packet>* parts, Packet* mine, st
 }
 
 // -------------------------------------------------------- point to point ----
+// header (and tcp payload) on the direct link to the peer; a member's message
+// to itself goes straight into its own inbox with the blobs as they are
 bool Group::send(int peer, const Packet& p, std::string* err) {
   if (peer < 0 || peer >= size()) {
     if (err) *err = strfmt("send: no member ", peer);
     return false;
   }
-  const int64_t t = store_->add(key(strfmt("p2p/", peer, "/tail")), 1);
-  if (t == INT64_MIN) {
-    if (err) *err = "send: store unreachable";
-    return false;
+  if (peer == grank_) {
+    Message m;
+    m.caps = encode(p, false);
+    m.blobs = p.blobs;
+    m.flags = 1;  // in-process: blobs handed over as they are
+    if (!mesh_) {
+      std::lock_guard<std::mutex> lk(local_mu_);
+      local_.push_back(std::move(m));
+      local_cv_.notify_all();
+    } else {
+      mesh_->deliver_local(kTagP2P, std::move(m));
+    }
+    return true;
   }
-  const std::string k = key(strfmt("p2p/", peer, "/", t - 1));
-  const bool local = peer == grank_;
-  Packet h = p;
-  if (local) {
-    h.flags |= 0x80000000u;  // blobs handed over in-process
-    std::lock_guard<std::mutex> lk(g_local_mu);
-    g_local[k] = p.blobs;
-  }
-  if (!store_->set(k, encode(h, !local && !rccl()), 1)) {
-    if (err) *err = "send: store write failed";
-    return false;
-  }
-  if (local || !rccl()) return true;
+  if (!mesh_->send(peer, kTagP2P, to_message(p), err)) return false;
+  if (!rccl()) return true;
   hip::DeviceGuard dg(device_);
   auto comm = static_cast<ncclComm_t>(comm_);
   if (!nccl_ok(ncclGroupStart(), "ncclGroupStart", err)) return false;
@@ -765,44 +943,51 @@ bool Group::send(int peer, const Packet& p, std::string* err) {
 
 bool Group::recv(Packet* p, int timeout_ms, bool* timed_out, std::string* err) {
   if (timed_out) *timed_out = false;
-  const std::string k = key(strfmt("p2p/", grank_, "/", recv_seq_));
-  std::string v;
-  bool to = false;
-  if (!store_->get(k, &v, timeout_ms, &to)) {
-    // only the store's own wait running out is a timeout; a lost store (its
-    // hosting rank died) is an error, so callers stop instead of retrying
-    if (timed_out) *timed_out = to;
-    if (err && !to) *err = "recv: lost the rendezvous store connection";
-    return false;
+  Message m;
+  if (!mesh_) {  // a group of one: only its own messages
+    std::unique_lock<std::mutex> lk(local_mu_);
+    auto ready = [&] { return !local_.empty() || cancelled_.load(); };
+    if (timeout_ms < 0) {
+      local_cv_.wait(lk, ready);
+    } else {
+      local_cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), ready);
+    }
+    if (local_.empty()) {
+      if (timed_out) *timed_out = !cancelled_.load();
+      if (err && cancelled_.load()) *err = "recv: cancelled";
+      return false;
+    }
+    m = std::move(local_.front());
+    local_.pop_front();
+  } else {
+    bool to = false;
+    std::string e;
+    if (!mesh_->recv(kTagP2P, -1, &m, nullptr, timeout_ms, &to, &e)) {
+      // only the wait running out is a timeout; a broken link (the member died)
+      // or a closed mesh is an error, so callers stop instead of retrying
+      if (timed_out) *timed_out = to;
+      if (err && !to) *err = "recv: " + e;
+      return false;
+    }
   }
-  ++recv_seq_;
   std::vector<size_t> sizes;
   std::vector<std::string> metas;
-  // peek the local flag before deciding whether the payload is inline
-  Packet hdr;
-  if (!decode(v, &hdr, false, &sizes, &metas)) {
+  if (m.flags & 1) {  // in-process
+    if (!decode(m.caps, p, false, &sizes, &metas)) return false;
+    p->blobs = std::move(m.blobs);
+    return true;
+  }
+  if (!from_message(std::move(m), p, &sizes, &metas)) {
     if (err) *err = "recv: bad header";
     return false;
   }
-  if (hdr.flags & 0x80000000u) {
-    *p = hdr;
-    p->flags &= ~0x80000000u;
-    std::lock_guard<std::mutex> lk(g_local_mu);
-    auto it = g_local.find(k);
-    if (it != g_local.end()) {
-      p->blobs = std::move(it->second);
-      g_local.erase(it);
-    }
-    return true;
-  }
-  if (!rccl()) return decode(v, p, true, &sizes, &metas);
-  *p = hdr;
+  if (!rccl()) return true;
   hip::DeviceGuard dg(device_);
   p->blobs = alloc_recv(sizes, metas);
   auto comm = static_cast<ncclComm_t>(comm_);
   if (!nccl_ok(ncclGroupStart(), "ncclGroupStart", err)) return false;
   for (auto& b : p->blobs)
-    if (b->size() && !nccl_ok(ncclRecv(b->data(), b->size(), ncclUint8, hdr.src, comm, stream_), "ncclRecv", err)) {
+    if (b->size() && !nccl_ok(ncclRecv(b->data(), b->size(), ncclUint8, p->src, comm, stream_), "ncclRecv", err)) {
       ncclGroupEnd();
       return false;
     }

@@ -14,16 +14,19 @@
 //                                              grouped ncclBroadcast per root
 //   request/reply (tensor_query_*)         -> ncclSend / ncclRecv pairs
 //
-// Control plane: headers (pts, caps, blob sizes, flexible meta, EOS) travel
-// through a small key/value store hosted by the group's first member
+// Rendezvous: a small key/value store hosted by the group's first member
 // (TCPStore analogue: set / blocking get / add; a key written with
-// `readers = n` is erased after n gets, so steady state keeps no garbage).
+// `readers = n` is erased after n gets) -- used to join, to exchange the RCCL
+// unique id and the members' link addresses, and for element handshakes.
+// Per-message headers (pts, caps, blob sizes, flexible meta, EOS) travel on
+// direct member-to-member TCP links (Mesh): one message, no store round trip.
 // Payloads travel on the group's RCCL communicator and its own high-priority
 // HIP stream, ordered against producers / consumers with the Memory ready /
 // use events -- never a host sync on the data path.
 //
-// Without GPUs (or backend=tcp) the payload rides inside the store value
-// (host bytes), so the same elements and tests run on CPU-only boxes.
+// Without GPUs (or backend=tcp) the payload rides on the same direct link
+// behind its header (host bytes), so the same elements and tests run on
+// CPU-only boxes.
 //
 // Threading rule: a Group is driven by one thread at a time (RCCL
 // communicators are not thread-safe); elements that talk in both
@@ -32,10 +35,14 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <atomic>
+#include <condition_variable>
 #include <cstdint>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "comm/transport.h"
@@ -57,6 +64,7 @@ class StoreClient {
   int64_t add(const std::string& key, int64_t delta);
   bool del(const std::string& key);
   void close();
+  std::string local_ip() const;  // this process's address on the store's network
 
  private:
   bool call(const std::string& op, const std::string& key, const std::string* val, int64_t arg, int wait_ms,
@@ -69,6 +77,48 @@ class StoreClient {
 // groups may share it).  Returns a handle that keeps it alive, or nullptr
 // with *in_use=true when another process already listens there.
 std::shared_ptr<void> host_store(const std::string& host, int port, bool* in_use, std::string* err);
+
+// ------------------------------------------------------------- mesh ----
+// Direct member-to-member links of a group: every member listens on an
+// ephemeral port (address published once in the store), a sender connects to
+// a receiver on first use and keeps the connection.  One message = one
+// transport Message (comm/transport.h) carrying a tag (p2p or the collective
+// sequence), the encoded packet header and -- on the tcp backend -- the payload
+// blobs.  An acceptor thread and one reader thread per inbound connection fill
+// a single inbox that receives match by (tag, source).
+class Mesh {
+ public:
+  ~Mesh();
+  bool start(StoreClient* store, const std::string& prefix, int grank, int n, int timeout_ms, std::string* err);
+  bool send(int peer, uint64_t tag, Message m, std::string* err);
+  void deliver_local(uint64_t tag, Message m);  // a member's message to itself
+  // next message with this tag from `src` (-1: any member), FIFO per source.
+  // false: *timed_out on timeout, else the mesh is closed or the awaited
+  // member's link broke without its goodbye (*err says which)
+  bool recv(uint64_t tag, int src, Message* m, int* from, int timeout_ms, bool* timed_out, std::string* err);
+  void close();
+
+ private:
+  struct Item {
+    int src;
+    uint64_t tag;
+    Message m;
+  };
+  void reader(std::shared_ptr<Connection> c);
+  StoreClient* store_ = nullptr;
+  std::string prefix_;
+  int grank_ = 0, n_ = 1, timeout_ms_ = 60000;
+  Listener lis_;
+  std::thread acceptor_;
+  std::vector<std::thread> readers_;
+  std::vector<std::shared_ptr<Connection>> in_, out_;
+  std::vector<std::mutex> out_mu_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<Item> inbox_;
+  std::vector<int> lost_;  // per member: 1 = its link broke without a goodbye
+  std::atomic<bool> closed_{false};
+};
 
 // ------------------------------------------------------------ group ----
 struct GroupSpec {
@@ -144,6 +194,10 @@ class Group {
   // device pointer of a blob for the data plane (uploads host blobs)
   void* dev_ptr(const MemoryPtr& m);
   std::vector<MemoryPtr> alloc_recv(const std::vector<size_t>& sizes, const std::vector<std::string>& metas);
+  Message to_message(const Packet& p);
+  bool from_message(Message&& m, Packet* p, std::vector<size_t>* sizes, std::vector<std::string>* metas);
+  bool recv_from(uint64_t tag, int src, Packet* p, std::vector<size_t>* sizes, std::vector<std::string>* metas,
+                 std::string* err, const char* what);
   void finish_inputs(const std::vector<MemoryPtr>& in);
 
   GroupSpec spec_;
@@ -153,10 +207,14 @@ class Group {
   std::string prefix_;
   std::shared_ptr<void> store_host_;
   std::shared_ptr<StoreClient> store_;
+  std::unique_ptr<Mesh> mesh_;  // member-to-member links (headers; tcp payloads)
   void* comm_ = nullptr;  // ncclComm_t
   hipStream_t stream_ = nullptr;
-  uint64_t seq_ = 0;       // collective sequence
-  uint64_t recv_seq_ = 0;  // p2p receive cursor
+  uint64_t seq_ = 0;            // collective sequence
+  std::deque<Message> local_;   // a group of one: its messages to itself
+  std::mutex local_mu_;
+  std::condition_variable local_cv_;
+  std::atomic<bool> cancelled_{false};
   uint64_t bytes_sent_ = 0, bytes_recv_ = 0;
 };
 

@@ -484,6 +484,10 @@ bool Connection::recv(Message* m, int timeout_ms, bool* timed_out) {
   }
 }
 
+void Connection::shutdown() {
+  if (alive_.exchange(false) && fd_ >= 0) ::shutdown(fd_, SHUT_RDWR);
+}
+
 void Connection::close() {
   bool was = alive_.exchange(false);
   if (fd_ >= 0) {
@@ -501,6 +505,15 @@ Listener::~Listener() {
 void Listener::release() {
   const int fd = fd_.exchange(-1);
   if (fd >= 0) ::close(fd);
+}
+
+std::string Connection::local_ip() const {
+  sockaddr_in addr{};
+  socklen_t len = sizeof(addr);
+  if (getsockname(fd_, reinterpret_cast<sockaddr*>(&addr), &len) != 0) return "127.0.0.1";
+  char buf[64];
+  inet_ntop(AF_INET, &addr.sin_addr, buf, sizeof(buf));
+  return buf;
 }
 
 bool Listener::listen(const std::string& host, int port, std::string* err) {

@@ -72,8 +72,12 @@ class Connection {
   // returns false on timeout (timed_out = true) or on a closed/broken stream
   bool recv(Message* m, int timeout_ms, bool* timed_out = nullptr);
   void close();
+  // wakes a recv() blocked in another thread (shutdown only: that thread still
+  // owns the descriptor, which the destructor closes)
+  void shutdown();
   bool alive() const { return alive_.load(); }
   const std::string& peer() const { return peer_; }
+  std::string local_ip() const;  // this end's IPv4 address (what peers can reach us at)
   uint64_t id = 0;  // server-assigned client id
 
   // device-direct path: announce that this end takes ring blobs (and will
