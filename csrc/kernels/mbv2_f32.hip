@@ -1405,9 +1405,9 @@ static bool irw_atomic2() {
 
 static int irw_parts(const IrwCfg* c, int tiles, int hid) {
   const int nsub = hid / 16;
-  static const int forced = irw_env("NNSX_F32_IRW_PARTS", 0);
-  if (forced > 0) return std::min(forced, std::max(1, nsub / c->NW));
+  static const int forced = irw_env("NNSX_F32_IRW_PARTS", 0);  // (tuning: blocks that split at all)
   if (tiles >= 256 || nsub < 8) return 1;
+  if (forced > 0) return std::min(forced, std::max(1, nsub / c->NW));
   if (tiles >= 128) return 2;
   const int want = (512 + tiles - 1) / tiles;
   return std::max(2, std::min(want, nsub / c->NW));
