@@ -467,6 +467,31 @@ PYBIND11_MODULE(_C, m) {
     if (d.empty()) throw Error(err);
     return d;
   }, py::arg("pbtxt"), "Launch description of a pbtxt graph (the reverse conversion)");
+  // the reference's >16-tensor buffer form (GstTensorExtraInfo in the 16th memory)
+  m.def("pack_extra", [](py::list arrays, std::vector<std::string> dims, std::vector<std::string> types) {
+    std::vector<MemoryPtr> mems;
+    for (auto a : arrays) mems.push_back(memory_from_python(a));
+    TensorsInfo info;
+    info.num_tensors = static_cast<unsigned>(mems.size());
+    for (size_t i = 0; i < mems.size() && i < dims.size() && i < types.size(); ++i) {
+      parse_dimension(dims[i], info.at(static_cast<unsigned>(i)).dim);
+      info.at(static_cast<unsigned>(i)).type = dtype_from_string(types[i]);
+    }
+    return pack_extra(mems, info);
+  }, "Pack >16 tensors into 16 memories (reference GstTensorExtraInfo layout)");
+  m.def("unpack_extra", [](std::vector<MemoryPtr> mems) {
+    TensorsInfo info;
+    info.num_tensors = static_cast<unsigned>(mems.size());
+    auto out = unpack_extra(mems, &info);
+    std::vector<std::pair<std::string, std::string>> ti;
+    for (size_t i = mems.size(); i < out.size(); ++i) {
+      const auto& t = info.at(static_cast<unsigned>(i));
+      std::string d;
+      for (int k = 0; k < kRankLimit; ++k) d += (k ? ":" : "") + std::to_string(t.dim[k]);
+      ti.emplace_back(d, dtype_name(t.type) ? dtype_name(t.type) : "");
+    }
+    return py::make_tuple(out, ti);
+  }, "Inverse of pack_extra: one memory per tensor, plus (dims, type) of the extra ones");
   // HPACK codec of the native gRPC transport (comm/hpack.h), for its tests
   m.def("hpack_huffman_encode", [](const std::string& s) { return py::bytes(hpack::huffman_encode(s)); });
   m.def("hpack_huffman_decode", [](const py::bytes& b) {

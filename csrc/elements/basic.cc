@@ -385,6 +385,9 @@ class AppSrc : public BaseSrc, public AppSrcIface {
   }
 
   FlowReturn push(BufferPtr buf) override {
+    // an application buffer in the reference's >16-tensor form (16 memories,
+    // the last one a GstTensorExtraInfo block): one memory per tensor downstream
+    if (buf && buf->mems.size() == static_cast<size_t>(kSizeLimit)) buf->mems = unpack_extra(buf->mems, nullptr);
     std::unique_lock<std::mutex> lk(mu_);
     if (eos_) return FlowReturn::EOS;
     if (flushing_.load() || unlocked_) return FlowReturn::FLUSHING;

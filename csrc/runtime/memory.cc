@@ -280,18 +280,28 @@ std::vector<uint8_t> serialize_with_header(const MemoryPtr& mem) {
 }
 
 namespace {
+// Byte layout of the reference's GstTensorExtraInfo on LP64
+// (nnstreamer_plugin_api_impl.c:1477-1490, tensor_typedef.h GstTensorInfo):
+// u32 magic, u32 version, u32 num_extra_tensors, (pad), u64 reserved (= size
+// of the 16th tensor), then 200 GstTensorInfo {char* name; tensor_type type;
+// uint32 dimension[8]} of 48 bytes each (name is a pointer in the writer's
+// process: written as 0, ignored on read).  The 16th tensor's bytes follow the
+// header, then each extra tensor's.
 struct ExtraHeader {
   uint32_t magic;
   uint32_t version;
   uint32_t num_extra;
   uint32_t pad;
-  uint64_t reserved;  // size of the 16th tensor
+  uint64_t reserved;
 };
 struct ExtraEntry {
+  uint64_t name;
   uint32_t type;
   uint32_t dim[kRankLimit];
+  uint32_t pad;
 };
-constexpr size_t kExtraInfoSize = sizeof(ExtraHeader) + sizeof(ExtraEntry) * kSizeExtraLimit;
+static_assert(sizeof(ExtraHeader) == 24 && sizeof(ExtraEntry) == 48, "GstTensorExtraInfo layout");
+constexpr size_t kExtraInfoSize = sizeof(ExtraHeader) + sizeof(ExtraEntry) * kSizeExtraLimit;  // 9624
 }  // namespace
 
 std::vector<MemoryPtr> pack_extra(const std::vector<MemoryPtr>& mems, const TensorsInfo& info) {
@@ -306,6 +316,7 @@ std::vector<MemoryPtr> pack_extra(const std::vector<MemoryPtr>& mems, const Tens
   h->num_extra = static_cast<uint32_t>(mems.size() - kSizeLimit);
   h->reserved = mems[kSizeLimit - 1]->size();
   auto* ent = reinterpret_cast<ExtraEntry*>(h + 1);
+  for (int i = 0; i < kSizeExtraLimit; ++i) ent[i].type = static_cast<uint32_t>(DType::END);  // gst_tensor_info_init
   for (size_t i = kSizeLimit; i < mems.size(); ++i) {
     const auto& ti = info.at(static_cast<unsigned>(i));
     ent[i - kSizeLimit].type = static_cast<uint32_t>(ti.type);
