@@ -683,10 +683,12 @@ struct IrwGeom {
   static constexpr size_t hid_q = static_cast<size_t>(4 * NW) * PINP;     // [wave][quad][cell]
   static constexpr size_t red_q = static_cast<size_t>(2 * 4 * NW) * NPX;  // [buf][wave][quad][px]
   static size_t lds_bytes(int) { return 16 * std::max(xs_q + hid_q, red_q); }
-  // minimum resident workgroups per CU the register budget is sized for.  28x28
-  // (KIN 32, stride 1): 4 (128 VGPRs, LDS allows 4) measured 57 -> 53.5 us at
+  // minimum waves per SIMD the register budget is sized for (hipcc reads the
+  // second launch bound that way).  4 (128 VGPRs) where the LDS allows more
+  // workgroups than the registers: 28x28 (KIN 32) measured 57 -> 53.5 us at
   // batch 128 despite 6 spilled VGPRs; the same on the 14x14 64-channel block
-  // (3, 21 spills) lost 40 -> 45 us.
+  // (3, 21 spills) lost 40 -> 45 us, and on the 56x56 block (1 spill, 5
+  // workgroups/CU instead of 4) 128 -> 144 us.
   static constexpr int MINB = (KIN == 32 && S == 1) ? 4 : NOT <= 6 ? 2 : 1;
 };
 
