@@ -1178,7 +1178,7 @@ const IrwCfg kIrwCfgs[] = {
     NNSX_IRW(1, 7, 7, 64, 6, 4, false),    // 14x14      64 -> 384 -> 96  (24)
     NNSX_IRW(1, 7, 7, 96, 6, 4, false),    // 14x14      96 -> 576 -> 96  (36)
     NNSX_IRW(1, 7, 7, 160, 10, 4, false),  // 7x7       160 -> 960 -> 160 (60, two parts)
-    NNSX_IRW(2, 7, 7, 96, 10, 3, false),   // 14 -> 7    96 -> 576 -> 160 (36, two parts; 3 waves: LDS)
+    NNSX_IRW(2, 7, 7, 96, 10, 4, false),   // 14 -> 7    96 -> 576 -> 160 (36, two parts; 154 KB LDS)
 };
 #undef NNSX_IRW
 
