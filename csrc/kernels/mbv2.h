@@ -90,6 +90,12 @@ struct IrBlockF32Args {
 bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout, bool has_expand);
 // device workspace ir_block_f32 needs for these args (0 = none)
 size_t ir_block_f32_workspace_bytes(const IrBlockF32Args& a);
+// expand 1x1 + ReLU6 + depthwise 3x3 + ReLU6 in one kernel, the depthwise
+// output to y [B][Ho][Wo][hid] (the hidden map never touches HBM; the caller
+// runs the project as a GEMM).  wp / bp / cout / residual are unused.
+// (B > 0: whether it is the faster path at this batch; B = 0: supported at all)
+bool ir_expand_dw_f32_supported(int stride, int H, int W, int cin, int hid, int B = 0);
+bool ir_expand_dw_f32(const IrBlockF32Args& a, hipStream_t s);
 
 // stem (3x3/2 conv 3 -> 32 on the uint8 frame, normalised as (x + add) / div,
 // + ReLU6) fused with an expand-free inverted residual 32 -> 32 -> 16

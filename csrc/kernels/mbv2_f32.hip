@@ -791,11 +791,14 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
   }
   const int nbt = (NC + 15) / 16;  // pixel tiles holding in-image pixels (wave-uniform)
 
-  f32x4_t acc[NPT][NOT];
+  // NOT = 0: no project -- the depthwise output itself is the result
+  // ([B][Ho][Wo][hid] in a.y; blocks whose project is a plain GEMM)
+  constexpr int NOA = NOT > 0 ? NOT : 1;
+  f32x4_t acc[NPT][NOA];
 #pragma unroll
   for (int pt = 0; pt < NPT; ++pt)
 #pragma unroll
-    for (int o = 0; o < NOT; ++o) acc[pt][o] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int o = 0; o < NOA; ++o) acc[pt][o] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   __syncthreads();  // xs + zeroed halos
 
@@ -814,7 +817,7 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
   if (a.has_expand && hs < sub1) load_ea(hs);
   for (; hs < sub1; hs += NW) {
     const int ch = hs * 16 + 4 * g;  // this lane's channel quad (dw, biases)
-    f32x4_t pa[NOT];
+    f32x4_t pa[NOA];
 #pragma unroll
     for (int o = 0; o < NOT; ++o)
       pa[o] = *reinterpret_cast<const f32x4_t*>(a.wp + static_cast<int64_t>(o * 16 + li) * a.hid + ch);
@@ -882,12 +885,20 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
         for (int kx = 0; kx < 3; ++kx)
           d = __builtin_elementwise_fma(myhid[dcell[pt] + ky * TIX + kx], wd4[ky * 3 + kx], d);
       const f32x4_t bf = relu6x4(d);
+      if constexpr (NOT == 0) {
+        const int q = pt * 16 + li;
+        const int gy = oy0 + q / TX, gx = ox0 + q % TX;
+        if (q < TY * TX && gy < a.Ho && gx < a.Wo)
+          *reinterpret_cast<f32x4_t*>(a.y + ((static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx) * a.hid + ch) = bf;
+        continue;
+      }
       // ---- project: k-split partial over this subtile's 16 channels
 #pragma unroll
       for (int o = 0; o < NOT; ++o) acc[pt][o] = mfma_k16(pa[o], bf, acc[pt][o]);
     }
     wave_sync();  // this wave's hidden image is read out before the next subtile's expand
   }
+  if constexpr (NOT == 0) return;
 
   // ---- cross-wave reduction (fixed order) + bias + residual -> NHWC
   __syncthreads();  // every wave is done with xs / hidden / dwo: the LDS becomes the reduction buffer
@@ -1179,6 +1190,10 @@ const IrwCfg kIrwCfgs[] = {
     NNSX_IRW(1, 7, 7, 96, 6, 4, false),    // 14x14      96 -> 576 -> 96  (36)
     NNSX_IRW(1, 7, 7, 160, 10, 4, false),  // 7x7       160 -> 960 -> 160 (60, two parts)
     NNSX_IRW(2, 7, 7, 96, 10, 4, false),   // 14 -> 7    96 -> 576 -> 160 (36, two parts; 154 KB LDS)
+    // expand + depthwise only (NOT = 0: the depthwise output goes to HBM and
+    // the project is a plain GEMM): 7x7 160 -> 960 whose project (-> 320)
+    // needs more accumulators than a wave holds
+    NNSX_IRW(1, 7, 7, 160, 0, 4, false),
 };
 #undef NNSX_IRW
 
@@ -1197,6 +1212,16 @@ const IrwCfg* find_irw(int S, int H, int W, int cin, int hid, int cout, bool has
   const int Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
   for (const auto& c : kIrwCfgs)
     if (c.S == S && c.KIN == kin && c.NOT == nout && Ho % c.TY == 0 && Wo % c.TX == 0 && c.lds(hid) <= 160 * 1024)
+      return &c;
+  return nullptr;
+}
+
+const IrwCfg* find_irw_dw(int S, int H, int W, int cin, int hid) {
+  if (!irw_enabled() || hid % 16) return nullptr;
+  const int kin = (cin + 7) / 8 * 8;
+  const int Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
+  for (const auto& c : kIrwCfgs)
+    if (c.NOT == 0 && c.S == S && c.KIN == kin && Ho % c.TY == 0 && Wo % c.TX == 0 && c.lds(hid) <= 160 * 1024)
       return &c;
   return nullptr;
 }
@@ -1407,6 +1432,8 @@ static bool irw_atomic2() {
 
 static int irw_parts(const IrwCfg* c, int tiles, int hid) {
   const int nsub = hid / 16;
+  if (c->NOT == 0)  // depthwise output: parts need no reduction, so fill the chip
+    return std::max(1, std::min((1024 + tiles - 1) / tiles, nsub / c->NW));
   static const int forced = irw_env("NNSX_F32_IRW_PARTS", 0);  // (tuning: blocks that split at all)
   if (tiles >= 256 || nsub < 8) return 1;
   if (forced > 0) return std::min(forced, std::max(1, nsub / c->NW));
@@ -1441,6 +1468,31 @@ static bool launch_irw(const IrwCfg* c, IrBlockF32Args a, hipStream_t s) {
     hipLaunchKernelGGL(irw_reduce_kernel, dim3(grid), dim3(256), 0, s, a.ws, a.hsplit, plane, a.bp, a.x, a.cin,
                        a.cout, a.residual, a.y);
   }
+  return true;
+}
+
+// used for small batches only: at batch 128 the 7x7 160 -> 960 expand GEMM +
+// depthwise kernel (46 us) beat this kernel (54 us); at batch 1 it saves a
+// launch and 4 us
+bool ir_expand_dw_f32_supported(int stride, int H, int W, int cin, int hid, int B) {
+  const IrwCfg* c = cin % 8 == 0 ? find_irw_dw(stride, H, W, cin, hid) : nullptr;
+  if (!c) return false;
+  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  return B <= 0 || B * (Ho / c->TY) * (Wo / c->TX) <= 32;
+}
+
+bool ir_expand_dw_f32(const IrBlockF32Args& args, hipStream_t s) {
+  IrBlockF32Args a = args;
+  const IrwCfg* c = find_irw_dw(a.stride, a.H, a.W, a.cin, a.hid);
+  if (!c || !a.has_expand) return false;
+  irw_geometry(c, &a);
+  a.ws = nullptr;
+  const size_t lds = c->lds(a.hid);
+  if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(c->kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+    return false;
+  const int tiles = a.tiles_x * a.tiles_y * a.B;
+  hipLaunchKernelGGL(c->kernel, dim3(static_cast<unsigned>(tiles * a.hsplit)), dim3(64 * c->NW), lds, s, a);
   return true;
 }
 

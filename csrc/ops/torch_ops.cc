@@ -246,6 +246,53 @@ at::Tensor ir_block_f32_cuda(const at::Tensor& x, const at::Tensor& we, const at
   return y;
 }
 
+// expand + depthwise (fp32), the depthwise output [B, Ho, Wo, hid]: blocks
+// whose project runs as a plain GEMM afterwards
+at::Tensor ir_expand_dw_cuda(const at::Tensor& x, const at::Tensor& we, const at::Tensor& be, const at::Tensor& wd,
+                             const at::Tensor& bd, int64_t stride) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 4,
+              "ir_expand_dw: x [B,H,W,C] f32");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int64_t hid = wd.size(1);
+  for (const auto* t : {&we, &be, &wd, &bd})
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "ir_expand_dw: weights must be contiguous f32");
+  TORCH_CHECK(wd.numel() == 9 * hid && bd.numel() >= hid && we.size(0) == hid && we.size(1) == (C + 7) / 8 * 8 &&
+                  be.numel() >= hid,
+              "ir_expand_dw: weights (we [hid, ceil8(cin)], wd [9, hid])");
+  const int64_t Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  at::Tensor y = at::empty({B, Ho, Wo, hid}, x.options());
+  nnsx::kernels::IrBlockF32Args a;
+  a.x = x.data_ptr<float>();
+  a.y = y.data_ptr<float>();
+  a.we = we.data_ptr<float>();
+  a.be = be.data_ptr<float>();
+  a.wd = wd.data_ptr<float>();
+  a.bd = bd.data_ptr<float>();
+  a.B = static_cast<int>(B);
+  a.H = static_cast<int>(H);
+  a.W = static_cast<int>(W);
+  a.cin = static_cast<int>(C);
+  a.hid = static_cast<int>(hid);
+  a.cout = 0;
+  a.stride = static_cast<int>(stride);
+  a.has_expand = 1;
+  TORCH_CHECK(nnsx::kernels::ir_expand_dw_f32(a, cur_stream()), "ir_expand_dw: unsupported shape (stride ", stride,
+              ", ", H, "x", W, ", cin ", C, ", hid ", hid, ")");
+  return y;
+}
+
+at::Tensor ir_expand_dw_cpu(const at::Tensor& x, const at::Tensor& we, const at::Tensor& be, const at::Tensor& wd,
+                            const at::Tensor& bd, int64_t stride) {
+  const int64_t hid = wd.size(1);
+  at::Tensor h = pw_conv_cpu(x, we, be, c10::nullopt, hid, 1, false);
+  return dw_conv_cpu(h, wd, bd, stride, 1, 1);
+}
+
+bool ir_expand_dw_supported_f32(int64_t stride, int64_t H, int64_t W, int64_t cin, int64_t hid, int64_t B) {
+  return nnsx::kernels::ir_expand_dw_f32_supported(static_cast<int>(stride), static_cast<int>(H), static_cast<int>(W),
+                                                   static_cast<int>(cin), static_cast<int>(hid), static_cast<int>(B));
+}
+
 at::Tensor ir_block_cuda(const at::Tensor& x, const at::Tensor& we, const at::Tensor& be, const at::Tensor& wd,
                          const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, int64_t stride,
                          int64_t cout, bool has_expand, bool residual) {
@@ -358,6 +405,9 @@ TORCH_LIBRARY(nnsx, m) {
   m.def("ir_supported(int stride, int cin, int hid, int cout) -> bool", ir_supported);
   m.def("ir_supported_f32(int stride, int H, int W, int cin, int hid, int cout, bool has_expand) -> bool",
         ir_supported_f32);
+  m.def("ir_expand_dw_supported_f32(int stride, int H, int W, int cin, int hid, int B=0) -> bool",
+        ir_expand_dw_supported_f32);
+  m.def("ir_expand_dw(Tensor x, Tensor we, Tensor be, Tensor wd, Tensor bd, int stride) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(nnsx, CUDA, m) {
@@ -369,6 +419,7 @@ TORCH_LIBRARY_IMPL(nnsx, CUDA, m) {
   m.impl("stem_ir1", stem_ir1_cuda);
   m.impl("pw_conv_f32_tile", pw_conv_f32_tile_cuda);
   m.impl("ir_block", ir_block_cuda);
+  m.impl("ir_expand_dw", ir_expand_dw_cuda);
 }
 
 TORCH_LIBRARY_IMPL(nnsx, CPU, m) {
@@ -379,4 +430,5 @@ TORCH_LIBRARY_IMPL(nnsx, CPU, m) {
   m.impl("avgpool", avgpool_cpu);
   m.impl("stem_ir1", stem_ir1_cpu);
   m.impl("ir_block", ir_block_cpu);
+  m.impl("ir_expand_dw", ir_expand_dw_cpu);
 }

@@ -179,8 +179,14 @@ class Block(nn.Module):
                 return torch.ops.nnsx.ir_block(x, self.ir_we, self.ir_be, self.ir_wd, self.ir_bd, self.ir_wp,
                                                self.project.bias, self.dw.stride, self.cout, self.has_expand,
                                                self.use_res)
-            h = self.expand(x) if self.has_expand else x
-            h = self.dw(h)
+            if self.use_ir and self.has_expand and self.dw.dilation == 1 and bool(
+                    torch.ops.nnsx.ir_expand_dw_supported_f32(self.dw.stride, x.shape[1], x.shape[2], self.cin,
+                                                              self.hid, x.shape[0])):
+                # expand + depthwise in one kernel (no hidden map in HBM), project as a GEMM
+                h = torch.ops.nnsx.ir_expand_dw(x, self.ir_we, self.ir_be, self.ir_wd, self.ir_bd, self.dw.stride)
+            else:
+                h = self.expand(x) if self.has_expand else x
+                h = self.dw(h)
             if self.use_res:
                 return self.project(h, x)
             return self.project(h)

@@ -67,9 +67,12 @@ for H, cin, hid, cout, st in SHAPES:
     if ok:
         fn = lambda: torch.ops.nnsx.ir_block(x, we, be, wd, bd, wp, bp, st, cout, has_expand, res)  # noqa: E731
         tag = "fused"
+    elif has_expand and bool(torch.ops.nnsx.ir_expand_dw_supported_f32(st, H, H, cin, hid, B)):
+        def fn():
+            h = torch.ops.nnsx.ir_expand_dw(x, we, be, wd, bd, st)
+            return torch.ops.nnsx.pw_conv(h, wp, bp, x if res else None, cout, 0, True)
+        tag = "exp+dw, GEMM"
     else:
-        hpad = (hid + 15) // 16 * 16
-
         def fn():
             h = torch.ops.nnsx.pw_conv(x, we, be, None, hid, 1, True) if has_expand else x
             h = torch.ops.nnsx.dw_conv(h, wd, bd, st, 1, 1)

@@ -174,6 +174,25 @@ def test_ir_block_f32_two_parts_deterministic(nns, H, cin, hid, cout, stride):
     _close(y, _ir_ref64(x, we, be, wd, bd, wp, bp, stride, cout, True, res), tol=5e-5)
 
 
+@pytest.mark.parametrize("B", [128, 3, 1])
+def test_ir_expand_dw_f32(nns, B):
+    """expand + depthwise in one kernel, depthwise output to HBM (the 7x7
+    160 -> 960 block whose project to 320 runs as a GEMM) vs fp64."""
+    torch.manual_seed(B)
+    cin, hid, H = 160, 960, 7
+    assert torch.ops.nnsx.ir_expand_dw_supported_f32(1, H, H, cin, hid)
+    x = torch.randn(B, H, H, cin, device="cuda")
+    we = torch.randn(hid, cin, device="cuda") / cin ** 0.5
+    be = torch.randn(hid, device="cuda") * 0.1
+    wd = torch.randn(9, hid, device="cuda") / 3
+    bd = torch.randn(hid, device="cuda") * 0.1
+    y = torch.ops.nnsx.ir_expand_dw(x, we, be, wd, bd, 1)
+    h = (x.double().cpu() @ we.double().cpu().t() + be.double().cpu()).clamp(0, 6)
+    ref = F.conv2d(h.permute(0, 3, 1, 2), wd.double().cpu().view(3, 3, hid).permute(2, 0, 1).unsqueeze(1),
+                   bd.double().cpu(), padding=1, groups=hid).clamp(0, 6).permute(0, 2, 3, 1)
+    _close(y, ref, tol=5e-5)
+
+
 def test_classifier_split_k_deterministic(nns):
     """M = batch GEMM (split over K, slabs added in order): bitwise repeatable."""
     torch.manual_seed(5)
