@@ -629,10 +629,18 @@ int64_t Element::running_time() const { return pipeline_ ? now_ns() - pipeline_-
 
 bool Element::wait_until_running_time(int64_t t) {
   if (t < 0) return true;
+  // sleep to within kSpinNs of the deadline, then yield-spin: a plain sleep
+  // overshoots by the timer slack (50 us by default on Linux) plus the
+  // wake-up latency, which a live source would add to every frame's latency
+  constexpr int64_t kSpinNs = 150000;
   while (!flushing_.load()) {
     int64_t now = running_time();
     if (now >= t) return true;
-    int64_t d = std::min<int64_t>(t - now, 5000000);  // re-check flushing every 5 ms
+    if (t - now <= kSpinNs) {
+      std::this_thread::yield();
+      continue;
+    }
+    int64_t d = std::min<int64_t>(t - now - kSpinNs, 5000000);  // re-check flushing every 5 ms
     std::this_thread::sleep_for(std::chrono::nanoseconds(d));
   }
   return false;
