@@ -57,7 +57,7 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("NNSX_BENCH_BATCH", "128")))
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("NNSX_BENCH_BATCH", "512")))
     ap.add_argument("--precision", default=os.environ.get("NNSX_BENCH_PRECISION", "both"),
                     choices=["fp32", "bf16", "both"],
                     help="fp32 = reference precision (headline); bf16 = secondary; both = fp32 headline + bf16")

@@ -232,6 +232,22 @@ def test_fused_fp32_mobilenet_top1_matches_torch_fp32(nns):
     assert worst < 1e-3, worst
 
 
+def test_fused_fp32_mobilenet_bench_batch_matches_torch_fp32(nns):
+    """The same gate at bench.py's batch (512 frames per invoke: every block
+    runs one hidden part per tile, the persistent stem walks 2 tiles per
+    workgroup more than at 128)."""
+    from nnstreamer_amd.models.fused import FusedMobileNetV2
+    from nnstreamer_amd.models.mobilenet_v2 import mobilenet_v2
+
+    torch.backends.cudnn.allow_tf32 = False
+    torch.backends.cuda.matmul.allow_tf32 = False
+    m = mobilenet_v2(seed=2).cuda().eval()
+    f = torch.jit.script(FusedMobileNetV2.from_reference(mobilenet_v2(seed=2), "fp32").cuda().eval())
+    agree, worst = _agreement(f, m, n_images=512, batch=512, seed=2)
+    assert agree >= 0.995, (agree, worst)
+    assert worst < 1e-3, worst
+
+
 def test_fused_bf16_mobilenet_top1_matches_torch_fp32(nns):
     """The secondary bf16 engine: top-1 agreement with torch fp32 >= 98 %."""
     from nnstreamer_amd.models.fused import FusedMobileNetV2
