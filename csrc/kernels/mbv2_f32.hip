@@ -1292,6 +1292,15 @@ static void pw_gemm_f32_launch(const float* x, const float* wt, const float* bia
 // prologue/epilogue share, and the grid runs in rounds of 512 co-resident
 // workgroups (256 CUs x 2; every tile here fits two per CU in LDS).
 static int pick_gemm_tile(int M, int N, int Kpad) {
+  // Large grids (>= 128 tiles of 64 x 64; M >= 8192, or M >= 512 with a deep
+  // K): 128 x 64 tiles, which re-read the weights half as often per output.
+  // The round model below ties them with 64 x 64 there; measured at batch 512
+  // (M = 25088 / 512): 7x7 expand + project chain 300 -> 289 us, head 210 ->
+  // 203 us, classifier 37 -> 24 us.  At batch 128 (M = 6272) the same switch
+  // was neutral to slightly slower (chain 89 -> 92 us), so it stays off there.
+  if (M >= 512 && (M >= 8192 || Kpad >= 1024) &&
+      static_cast<int64_t>((M + 63) / 64) * ((N + 63) / 64) >= 128)
+    return 128064;
   static const int cand[][2] = {{64, 64}, {128, 64}, {64, 128}, {128, 128}};
   int best = 0;
   double best_t = 1e30;
