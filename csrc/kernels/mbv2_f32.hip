@@ -1100,6 +1100,177 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) stem_ir1_f32_kernel(StemIr1F3
   }
 }
 
+// ------------------------------------------------------- stem_ir1w_f32 ----
+// The same stem + block-1 fusion as stem_ir1_f32, one WAVE per tile: a
+// workgroup is a single wave that owns a TY x TX output tile end to end --
+// both 16-channel halves of the stem over the (TY+2) x (TX+2) halo grid, the
+// depthwise 3x3 over all 32 channels and the whole K = 32 project -- so there
+// is no workgroup barrier and no cross-wave reduction anywhere.  8 x 8 tiles
+// keep a wave's LDS (input patch + 32-channel hidden image + normalisation
+// table) under 20 KB, so 8 waves are resident per CU and one wave's MFMA
+// work overlaps the others' staging / depthwise VALU work.  The price is the
+// halo: 100 stem cells per 64 outputs (1.56x) against 324 per 256 (1.27x).
+// (second launch bound: 2 waves per SIMD = 256 VGPRs; 8 such waves per CU.)
+// Persistent: a resident set of waves walks the tiles; the next tile's input
+// bytes are in flight while the current one computes.
+template <int TY, int TX, bool PAIR>
+__global__ void __launch_bounds__(64, 2) stem_ir1w_f32_kernel(StemIr1F32Args a) {
+  constexpr int HY = TY + 2, HX = TX + 2, PIN = HY * HX;
+  constexpr int NBT = (PIN + 15) / 16;
+  constexpr int IY = 2 * HY + 1, IX = 2 * HX + 1, PITCH = IX * 3;
+  constexpr int NIN = IY * PITCH;
+  constexpr int XIN = (NIN + 3) / 4 * 4;
+  constexpr int NPT = (TY * TX + 15) / 16;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* xin = smem;                                             // [IY][PITCH] normalised input
+  float* lut = smem + XIN;                                       // [256] (v + add) / div
+  f32x4_t* hid = reinterpret_cast<f32x4_t*>(smem + XIN + 256);  // [8 quads][PIN] (32 channels)
+
+  const int lane = threadIdx.x;
+  const int li = lane & 15, g = lane >> 4;
+  const int tiles_img = a.tiles_x * a.tiles_y;
+  const int ntiles = tiles_img * a.B;
+
+#pragma unroll
+  for (int i = 0; i < 4; ++i) lut[lane * 4 + i] = (static_cast<float>(lane * 4 + i) + a.add) / a.div;
+  float sa[2][7];  // stem weights: half h, k = 4t + g (27 taps + 1 zero); A row li = channel 16h + li
+  int off[7];
+#pragma unroll
+  for (int t = 0; t < 7; ++t) {
+    const int k = 4 * t + g;
+    sa[0][t] = k < 27 ? a.ws[k * 32 + li] : 0.f;
+    sa[1][t] = k < 27 ? a.ws[k * 32 + 16 + li] : 0.f;
+    off[t] = k < 27 ? (k / 9) * PITCH + ((k % 9) / 3) * 3 + (k % 3) : 0;
+  }
+  f32x4_t bs4[2], bd4[2], pa[2], wd4[2][9];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int ch = 16 * h + 4 * g;  // this lane's channel quad in half h
+    bs4[h] = *reinterpret_cast<const f32x4_t*>(a.bs + ch);
+    bd4[h] = *reinterpret_cast<const f32x4_t*>(a.bd + ch);
+    pa[h] = *reinterpret_cast<const f32x4_t*>(a.wp + li * 32 + ch);  // project A: row li, k = 16h + 4g + j
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wd4[h][t] = *reinterpret_cast<const f32x4_t*>(a.wd + t * 32 + ch);
+  }
+  const f32x4_t bp4 = *reinterpret_cast<const f32x4_t*>(a.bp + 4 * g);
+  const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // the patch is fetched row by row, lane = byte column (PITCH <= 64): the
+  // per-lane address terms are then the same for every row (few live registers)
+  static_assert(PITCH <= 64, "stem_ir1w: one patch row per wave load");
+  const int pcol = lane < PITCH ? lane : 0;
+  const int pdx = pcol / 3, pch = pcol - 3 * pdx;
+  int raw[IY];
+  auto fetch = [&](int tile) {
+    const int b = tile / tiles_img;
+    const int tyx = tile - b * tiles_img;
+    const int iy0 = 2 * ((tyx / a.tiles_x) * TY - 1) - 1, ix = 2 * ((tyx % a.tiles_x) * TX - 1) - 1 + pdx;
+    const bool colok = lane < PITCH && ix >= 0 && ix < a.W;
+    const uint8_t* xc = a.x + static_cast<int64_t>(b) * a.H * a.W * 3 + static_cast<int64_t>(ix) * 3 + pch;
+#pragma unroll
+    for (int r = 0; r < IY; ++r) {
+      const int iy = iy0 + r;
+      raw[r] = (colok && iy >= 0 && iy < a.H) ? static_cast<int>(xc[static_cast<int64_t>(iy) * a.W * 3]) : -1;
+    }
+  };
+
+  int tile = blockIdx.x;
+  if (tile < ntiles) fetch(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    const int b = tile / tiles_img;
+    const int tyx = tile - b * tiles_img;
+    const int oy0 = (tyx / a.tiles_x) * TY, ox0 = (tyx % a.tiles_x) * TX;
+    const int hy0 = oy0 - 1, hx0 = ox0 - 1;  // hidden halo origin (stem-output coords)
+    __syncthreads();  // (one wave: orders the previous tile's LDS reads before these writes; lut on entry)
+    if (lane < PITCH) {
+#pragma unroll
+      for (int r = 0; r < IY; ++r) xin[r * PITCH + lane] = raw[r] >= 0 ? lut[raw[r]] : 0.f;
+    }
+    if (tile + static_cast<int>(gridDim.x) < ntiles) fetch(tile + gridDim.x);
+    __syncthreads();
+
+    // ---- stem MFMA, both channel halves per pixel tile (two independent chains
+    // sharing each B operand read)
+#pragma unroll 1
+    for (int j = 0; j < NBT; ++j) {
+      const int c = j * 16 + li;
+      const int hy = c / HX, hx = c - hy * HX;
+      const int base = c < PIN ? 2 * hy * PITCH + 6 * hx : 0;
+      f32x4_t e0 = z, e1 = z;
+#pragma unroll
+      for (int t = 0; t < 7; ++t) {
+        const float xv = xin[base + off[t]];
+        e0 = mfma4(sa[0][t], xv, e0);
+        e1 = mfma4(sa[1][t], xv, e1);
+      }
+      if (c < PIN) {
+        const bool in = hy0 + hy >= 0 && hy0 + hy < a.Ho && hx0 + hx >= 0 && hx0 + hx < a.Wo;
+        hid[g * PIN + c] = in ? relu6x4(e0 + bs4[0]) : z;
+        hid[(4 + g) * PIN + c] = in ? relu6x4(e1 + bs4[1]) : z;
+      }
+    }
+    __syncthreads();
+
+    // ---- depthwise 3x3 + bias + ReLU6 (32 channels), straight into the K = 32
+    // project MFMA (lane (li, g) holds pixel li's channel quad g of each half:
+    // exactly its B-operand k-quad), + bias -> [B][Ho][Wo][16]
+    if constexpr (PAIR) {
+      // pixel tiles 2pp and 2pp + 1 hold vertically adjacent outputs in each
+      // lane (row 2pp + 4 (li / 8) and the row below, column li % 8), so the
+      // two 3x3 windows share 2 of their 4 input rows: 12 LDS reads, not 18
+      static_assert(TX == 8 && TY == 8, "stem_ir1w: pair mapping assumes 8 x 8 tiles");
+#pragma unroll 1
+      for (int pp = 0; pp < 2; ++pp) {
+        const int oy = 2 * pp + 4 * (li >> 3), ox = li & 7;
+        f32x4_t acc0 = z, acc1 = z;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x4_t* hp = hid + (4 * h + g) * PIN + oy * HX + ox;
+          f32x4_t d0 = bd4[h], d1 = bd4[h];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+              const f32x4_t v = hp[r * HX + kx];
+              if (r < 3) d0 = __builtin_elementwise_fma(v, wd4[h][r * 3 + kx], d0);
+              if (r > 0) d1 = __builtin_elementwise_fma(v, wd4[h][(r - 1) * 3 + kx], d1);
+            }
+          acc0 = mfma_k16(pa[h], relu6x4(d0), acc0);
+          acc1 = mfma_k16(pa[h], relu6x4(d1), acc1);
+        }
+        const int gy = oy0 + oy, gx = ox0 + ox;
+        float* yp = a.y + ((static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx) * 16 + 4 * g;
+        if (gx < a.Wo) {
+          if (gy < a.Ho) *reinterpret_cast<f32x4_t*>(yp) = acc0 + bp4;
+          if (gy + 1 < a.Ho) *reinterpret_cast<f32x4_t*>(yp + static_cast<int64_t>(a.Wo) * 16) = acc1 + bp4;
+        }
+      }
+    } else {
+#pragma unroll 1
+      for (int pt = 0; pt < NPT; ++pt) {
+        const int q = pt * 16 + li;
+        const int qq = q < TY * TX ? q : 0;
+        const int cell = (qq / TX) * HX + (qq % TX);
+        f32x4_t acc = z;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x4_t* hp = hid + (4 * h + g) * PIN + cell;
+          f32x4_t d = bd4[h];
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) d = __builtin_elementwise_fma(hp[ky * HX + kx], wd4[h][ky * 3 + kx], d);
+          acc = mfma_k16(pa[h], relu6x4(d), acc);
+        }
+        const int gy = oy0 + qq / TX, gx = ox0 + qq % TX;
+        if (q < TY * TX && gy < a.Ho && gx < a.Wo)
+          *reinterpret_cast<f32x4_t*>(a.y + ((static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx) * 16 + 4 * g) =
+              acc + bp4;
+      }
+    }
+  }
+}
+
 // the hidden-split partials of irw_f32 (> 2 parts), added in part order
 // (deterministic), + bias (+ residual)
 __global__ void __launch_bounds__(256) irw_reduce_kernel(const float* __restrict__ ws, int parts, int64_t plane,
@@ -1522,8 +1693,48 @@ size_t stem_ir1_lds_bytes() {
   return static_cast<size_t>((IY * PITCH + 3) / 4 * 4 + 256) * 4 + 16 * (8 * PINP + 8 * NPX);
 }
 
+// one-wave-per-tile variant (stem_ir1w_f32_kernel): 8 x 8 tiles
+constexpr int kStemW = 8;
+static size_t stem_ir1w_lds_bytes() {
+  constexpr int HY = kStemW + 2, HX = kStemW + 2, PIN = HY * HX;
+  constexpr int NIN = (2 * HY + 1) * (2 * HX + 1) * 3;
+  return static_cast<size_t>((NIN + 3) / 4 * 4 + 256) * 4 + 16 * 8 * PIN;
+}
+
+static bool stem_ir1w_f32(StemIr1F32Args a, hipStream_t s) {
+  a.tiles_y = (a.Ho + kStemW - 1) / kStemW;
+  a.tiles_x = (a.Wo + kStemW - 1) / kStemW;
+  const size_t lds = stem_ir1w_lds_bytes();
+  static const bool pair = irw_env("NNSX_STEM_WAVE", 2) == 2;
+  const void* fn = pair ? reinterpret_cast<const void*>(&stem_ir1w_f32_kernel<kStemW, kStemW, true>)
+                        : reinterpret_cast<const void*>(&stem_ir1w_f32_kernel<kStemW, kStemW, false>);
+  static const int resident = [fn, lds] {
+    int dev = 0, ncu = 256, per_cu = 1;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+    return ncu * per_cu;
+  }();
+  const int tiles = a.tiles_x * a.tiles_y * a.B;
+  const unsigned grid = static_cast<unsigned>(std::min(tiles, resident));
+  if (pair)
+    hipLaunchKernelGGL((stem_ir1w_f32_kernel<kStemW, kStemW, true>), dim3(grid), dim3(64), lds, s, a);
+  else
+    hipLaunchKernelGGL((stem_ir1w_f32_kernel<kStemW, kStemW, false>), dim3(grid), dim3(64), lds, s, a);
+  return true;
+}
+
 bool stem_ir1_f32(const StemIr1F32Args& args, hipStream_t s) {
   StemIr1F32Args a = args;
+  // one wave per 8 x 8 tile with paired-row depthwise (default, 2), the same
+  // without the row pairing (1), or the 8-wave 16 x 16 tile kernel (0).
+  // Batch 512 on one box: 525 / 514 / 510 us for 0 / 1 / 2 (another box: 520 vs
+  // 492 us for 0 vs 1); PMC (profiles/r2_pmc_stem_ir1.txt): wait cycles 39 -> 31 %
+  static const bool wave_tiles = irw_env("NNSX_STEM_WAVE", 2) != 0;
+  if (wave_tiles) {
+    a.Ho = (a.H - 1) / 2 + 1;
+    a.Wo = (a.W - 1) / 2 + 1;
+    return stem_ir1w_f32(a, s);
+  }
   a.Ho = (a.H - 1) / 2 + 1;
   a.Wo = (a.W - 1) / 2 + 1;
   a.tiles_y = (a.Ho + kStemIr1TY - 1) / kStemIr1TY;

@@ -4,6 +4,7 @@ pw -> dw -> pw chain), the stem, the head GEMM, pool and classifier.
 Prints GPU time (CUDA events) and the fraction of the fp32 MFMA peak.
 
     python scripts/bench_ir_f32.py [B]          # NNSX_IR_ONLY=H,cin,hid,cout,s: one block (for rocprof)
+                                                # NNSX_IR_ONLY=stem: the fused stem + block 1 only
 """
 import os
 import sys
@@ -40,6 +41,13 @@ def row(name, us, flop):
 
 
 ONLY = os.environ.get("NNSX_IR_ONLY")
+if ONLY == "stem":  # only the fused stem + block 1 (for rocprof)
+    xu = torch.randint(0, 256, (B, 224, 224, 3), device="cuda", dtype=torch.uint8)
+    w = [torch.randn(3, 3, 3, 32, device="cuda"), torch.zeros(32, device="cuda"), torch.randn(9, 32, device="cuda"),
+         torch.zeros(32, device="cuda"), torch.randn(16, 32, device="cuda") * 0.1, torch.zeros(16, device="cuda")]
+    us1 = timeit(lambda: torch.ops.nnsx.stem_ir1(xu, *w, -127.5, 127.5))
+    print(f"stem+block1 fused {us1:.1f} us at batch {B}")
+    sys.exit(0)
 if ONLY:
     SHAPES = [tuple(int(v) for v in ONLY.split(","))]
 total = 0.0
