@@ -807,11 +807,23 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
   f32x4_t* myhid = hidw + (wave * 4 + g) * PINP;
   f32x4_t ea[NS16 > 0 ? NS16 : 1];
   f32x2_t et = f32x2_t{0.f, 0.f};
+  f32x4_t be4 = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // PREB: the expand bias is fetched one subtile ahead with the expand
+  // weights.  vmcnt waits count in issue order, so a bias load issued after the
+  // subtile's depthwise / project weights makes the first expand epilogue wait
+  // for all of them (vmcnt(0)); fetched ahead, the expand waits only for loads
+  // issued a subtile earlier and the dw / project weights land during the
+  // expand.  Measured at batch 512: 112->56 594 -> 569 us, 56x56 465 -> 456; on
+  // the other blocks the 4-12 extra VGPRs cost more (56->28 and 28->14 lose a
+  // wave per SIMD; 14x14/96 278 -> 306 us, 7x7 223 -> 240), so only the two
+  // large-map 3-wave configurations use it.
+  constexpr bool PREB = FULL && NW == 3 && TY * TX >= 32;
   auto load_ea = [&](int hs) {
     const float* wrow = a.we + static_cast<int64_t>(hs * 16 + li) * KIN;
 #pragma unroll
     for (int s = 0; s < NS16; ++s) ea[s] = *reinterpret_cast<const f32x4_t*>(wrow + 16 * s + 4 * g);
     if constexpr (KT8) et = *reinterpret_cast<const f32x2_t*>(wrow + 16 * NS16 + 2 * g);
+    if constexpr (PREB) be4 = *reinterpret_cast<const f32x4_t*>(a.be + hs * 16 + 4 * g);
   };
   int hs = sub0 + wave;
   if (a.has_expand && hs < sub1) load_ea(hs);
@@ -828,7 +840,7 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
 
     // ---- expand -> private hidden image
     if (a.has_expand) {
-      const f32x4_t be4 = *reinterpret_cast<const f32x4_t*>(a.be + ch);
+      if constexpr (!PREB) be4 = *reinterpret_cast<const f32x4_t*>(a.be + ch);
       // pixel tiles in pairs (two independent MFMA chains); a pair past the
       // in-image pixels is skipped wave-uniformly, a half-valid one computes zeros
 #pragma unroll
