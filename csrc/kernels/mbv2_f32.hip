@@ -739,26 +739,40 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
   const float* xb = a.x + static_cast<int64_t>(b) * a.H * a.W * a.cin;
 
   // ---- stage the input tile (coalesced reads: consecutive threads, consecutive
-  // quads; compile-time trip count, so every load is in flight before the stores)
+  // quads).  Two phases with branch-free loads: every load of the tile is
+  // issued back to back (out-of-tile lanes read the image's first quad and
+  // select zero), then the LDS stores.  A load under a branch became
+  // load / s_waitcnt vmcnt(0) / store per iteration, one exposed memory
+  // latency per 256 quads of the tile.
   constexpr int NSV = NC16 * KQ, NSIT = (NSV + NT - 1) / NT;
+  {
+    f32x4_t sv[NSIT];
+    bool sok[NSIT];
 #pragma unroll
-  for (int it = 0; it < NSIT; ++it) {
-    const int v = tid + it * NT;
-    if (NSV % NT != 0 && v >= NSV) break;
-    const int c = v / KQ, kq = v - c * KQ;
-    f32x4_t val = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    int yy, xx;
-    if constexpr (FULL) {
-      yy = iy0 + c / TIX;
-      xx = ix0 + c % TIX;
-    } else {
-      const int cy = static_cast<int>((static_cast<float>(c) + 0.5f) * rrw);
-      yy = ry0 + cy;
-      xx = rx0 + c - cy * RW;
+    for (int it = 0; it < NSIT; ++it) {
+      const int v = tid + it * NT;
+      const int c = v / KQ, kq = v - c * KQ;
+      int yy, xx;
+      if constexpr (FULL) {
+        yy = iy0 + c / TIX;
+        xx = ix0 + c % TIX;
+      } else {
+        const int cy = static_cast<int>((static_cast<float>(c) + 0.5f) * rrw);
+        yy = ry0 + cy;
+        xx = rx0 + c - cy * RW;
+      }
+      sok[it] = (NSV % NT == 0 || v < NSV) && c < NC && kq * 4 < a.cin && yy >= 0 && yy < a.H && xx >= 0 &&
+                xx < a.W;
+      const int64_t off = sok[it] ? (static_cast<int64_t>(yy) * a.W + xx) * a.cin + kq * 4 : 0;
+      sv[it] = *reinterpret_cast<const f32x4_t*>(xb + off);
     }
-    if (c < NC && kq * 4 < a.cin && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W)
-      val = *reinterpret_cast<const f32x4_t*>(xb + (static_cast<int64_t>(yy) * a.W + xx) * a.cin + kq * 4);
-    xs[kq * XSP + (c ^ (kq & 3))] = val;
+#pragma unroll
+    for (int it = 0; it < NSIT; ++it) {
+      const int v = tid + it * NT;
+      if (NSV % NT != 0 && v >= NSV) break;
+      const int c = v / KQ, kq = v - c * KQ;
+      xs[kq * XSP + (c ^ (kq & 3))] = sok[it] ? sv[it] : f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
   }
   // out-of-image halo cells of every wave's hidden image = the depthwise zero padding
   // (FULL: the expand itself writes them as zeros)
