@@ -712,6 +712,7 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
   constexpr int NT = 64 * NW;
   constexpr int TIY = G::TIY, TIX = G::TIX, PIN = G::PIN, NC16 = G::NC16, NBT = G::NBT, XSP = G::XSP;
   constexpr int PINP = G::PINP;
+  static_assert(FULL || PINP > PIN, "irw_f32: the compact expand needs a scratch hidden cell");
   constexpr int KQ = G::KQ, NPT = G::NPT, NPX = G::NPX;
   constexpr int NS16 = KIN / 16;
   constexpr bool KT8 = (KIN % 16) != 0;
@@ -793,7 +794,7 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
       hcell[j] = (c < PIN && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) ? 1 : 0;
     } else {
       const int cy = static_cast<int>((static_cast<float>(c) + 0.5f) * rrw);
-      hcell[j] = c < NC ? (ry0 + cy - iy0) * TIX + (rx0 + c - cy * RW - ix0) : -1;
+      hcell[j] = c < NC ? (ry0 + cy - iy0) * TIX + (rx0 + c - cy * RW - ix0) : PIN;  // PIN: scratch cell
     }
   }
   int dcell[NPT];
@@ -881,8 +882,11 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
             myhid[j * 16 + li] = hcell[j] ? relu6x4(e0 + be4) : z;
             if (j + 1 < NBT) myhid[j1 * 16 + li] = hcell[j1] ? relu6x4(e1 + be4) : z;
           } else {
-            if (hcell[j] >= 0) myhid[hcell[j]] = relu6x4(e0 + be4);
-            if (j + 1 < NBT && hcell[j1] >= 0) myhid[hcell[j1]] = relu6x4(e1 + be4);
+            // branch-free: padding pixels store to the unused cell PIN (a per-lane
+            // `if` compiled to exec-mask branches that kept the next pair's LDS
+            // reads from overlapping this epilogue)
+            myhid[hcell[j]] = relu6x4(e0 + be4);
+            if (j + 1 < NBT) myhid[hcell[j1]] = relu6x4(e1 + be4);
           }
         }
       }
