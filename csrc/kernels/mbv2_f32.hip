@@ -1213,26 +1213,46 @@ __global__ void __launch_bounds__(64, 2) stem_ir1w_f32_kernel(StemIr1F32Args a) 
     const int hy0 = oy0 - 1, hx0 = ox0 - 1;  // hidden halo origin (stem-output coords)
     __syncthreads();  // (one wave: orders the previous tile's LDS reads before these writes; lut on entry)
     if (lane < PITCH) {
+      // all table reads first, then the stores: lut and xin share the LDS
+      // array, so read / store pairs in one loop were ordered one after the
+      // other (an LDS round trip per patch row)
+      float nv[IY];
 #pragma unroll
-      for (int r = 0; r < IY; ++r) xin[r * PITCH + lane] = raw[r] >= 0 ? lut[raw[r]] : 0.f;
+      for (int r = 0; r < IY; ++r) nv[r] = lut[raw[r] >= 0 ? raw[r] : 0];
+#pragma unroll
+      for (int r = 0; r < IY; ++r) xin[r * PITCH + lane] = raw[r] >= 0 ? nv[r] : 0.f;
     }
     if (tile + static_cast<int>(gridDim.x) < ntiles) fetch(tile + gridDim.x);
     __syncthreads();
 
     // ---- stem MFMA, both channel halves per pixel tile (two independent chains
     // sharing each B operand read)
+    // (the next pixel tile's 7 B operands are read before this tile's MFMAs and
+    // hidden stores: xin and hid share the LDS array, so reads placed after the
+    // stores could not be hoisted above them)
+    auto patch_base = [&](int c) { return c < PIN ? 2 * (c / HX) * PITCH + 6 * (c % HX) : 0; };
+    float xv[7];
+    {
+      const int base = patch_base(li);
+#pragma unroll
+      for (int t = 0; t < 7; ++t) xv[t] = xin[base + off[t]];
+    }
 #pragma unroll 1
     for (int j = 0; j < NBT; ++j) {
       const int c = j * 16 + li;
       const int hy = c / HX, hx = c - hy * HX;
-      const int base = c < PIN ? 2 * hy * PITCH + 6 * hx : 0;
+      float xn[7];
+      const int nbase = patch_base(c + 16);
+#pragma unroll
+      for (int t = 0; t < 7; ++t) xn[t] = j + 1 < NBT ? xin[nbase + off[t]] : 0.f;
       f32x4_t e0 = z, e1 = z;
 #pragma unroll
       for (int t = 0; t < 7; ++t) {
-        const float xv = xin[base + off[t]];
-        e0 = mfma4(sa[0][t], xv, e0);
-        e1 = mfma4(sa[1][t], xv, e1);
+        e0 = mfma4(sa[0][t], xv[t], e0);
+        e1 = mfma4(sa[1][t], xv[t], e1);
       }
+#pragma unroll
+      for (int t = 0; t < 7; ++t) xv[t] = xn[t];
       if (c < PIN) {
         const bool in = hy0 + hy >= 0 && hy0 + hy < a.Ho && hx0 + hx >= 0 && hx0 + hx < a.Wo;
         hid[g * PIN + c] = in ? relu6x4(e0 + bs4[0]) : z;
