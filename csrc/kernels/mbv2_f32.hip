@@ -858,15 +858,38 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
       if constexpr (!PREB) be4 = *reinterpret_cast<const f32x4_t*>(a.be + ch);
       // pixel tiles in pairs (two independent MFMA chains); a pair past the
       // in-image pixels is skipped wave-uniformly, a half-valid one computes zeros
+      // PREX (whole halo grid, one 16-k step): the next pair's B operands are
+      // read before this pair's MFMAs and hidden stores -- xs and the hidden
+      // images share the LDS array, so reads placed after the stores cannot be
+      // hoisted above them and each pair waited for its own LDS round trip
+      constexpr bool PREX = FULL && NS16 == 1;
+      f32x4_t bx0 = f32x4_t{0.f, 0.f, 0.f, 0.f}, bx1 = bx0;
+      if constexpr (PREX) {
+        bx0 = xs[g * XSP + (li ^ g)];
+        bx1 = xs[g * XSP + (NBT > 1 ? 16 : 0) + (li ^ g)];
+      }
 #pragma unroll
       for (int j = 0; j < NBT; j += 2) {
         if (FULL || j < nbt) {
           const int j1 = j + 1 < NBT ? j + 1 : j;
           f32x4_t e0 = f32x4_t{0.f, 0.f, 0.f, 0.f}, e1 = e0;
+          if constexpr (PREX) {
+            f32x4_t n0 = bx0, n1 = bx1;
+            if (j + 2 < NBT) {
+              const int k1 = j + 3 < NBT ? j + 3 : j + 2;
+              n0 = xs[g * XSP + (j + 2) * 16 + (li ^ g)];
+              n1 = xs[g * XSP + k1 * 16 + (li ^ g)];
+            }
+            e0 = mfma_k16(ea[0], bx0, e0);
+            e1 = mfma_k16(ea[0], bx1, e1);
+            bx0 = n0;
+            bx1 = n1;
+          } else {
 #pragma unroll
-          for (int s = 0; s < NS16; ++s) {
-            e0 = mfma_k16(ea[s], xs[(4 * s + g) * XSP + j * 16 + (li ^ g)], e0);
-            e1 = mfma_k16(ea[s], xs[(4 * s + g) * XSP + j1 * 16 + (li ^ g)], e1);
+            for (int s = 0; s < NS16; ++s) {
+              e0 = mfma_k16(ea[s], xs[(4 * s + g) * XSP + j * 16 + (li ^ g)], e0);
+              e1 = mfma_k16(ea[s], xs[(4 * s + g) * XSP + j1 * 16 + (li ^ g)], e1);
+            }
           }
           if constexpr (KT8) {
             // tail plane kq = 4 NS16 + g/2: swizzle (kq & 3) = g >> 1
