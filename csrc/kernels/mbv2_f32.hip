@@ -186,7 +186,28 @@ __global__ void __launch_bounds__(256) pw_gemm_f32_kernel(const float* __restric
     __syncthreads();
   }
 
-  // epilogue: lane owns channels n..n+3 of pixel m
+  // epilogue: lane owns channels n..n+3 of pixel m.  Bias (and residual)
+  // values are all loaded up front, branch-free: loaded at each store behind
+  // the bounds checks they were fetched and waited for one at a time.
+  const bool slab = gridDim.z > 1;
+  f32x4_t bv[RN], rv[RM][RN];
+#pragma unroll
+  for (int j = 0; j < RN; ++j) {
+    const int n = n0 + wn * (BN / 2) + j * 16 + g * 4;
+    bv[j] = slab ? zero : *reinterpret_cast<const f32x4_t*>(bias + (n < N ? n : 0));
+  }
+  if (res && !slab) {
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      const int m = m0 + wm * (BM / 2) + i * 16 + li;
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int n = n0 + wn * (BN / 2) + j * 16 + g * 4;
+        const int64_t off = (m < M && n < N) ? static_cast<int64_t>(m) * N + n : 0;
+        rv[i][j] = *reinterpret_cast<const f32x4_t*>(res + off);
+      }
+    }
+  }
 #pragma unroll
   for (int i = 0; i < RM; ++i) {
     const int m = m0 + wm * (BM / 2) + i * 16 + li;
@@ -196,13 +217,13 @@ __global__ void __launch_bounds__(256) pw_gemm_f32_kernel(const float* __restric
       const int n = n0 + wn * (BN / 2) + j * 16 + g * 4;
       if (n >= N) continue;
       float* yp = y + static_cast<int64_t>(m) * N + n;
-      if (gridDim.z > 1) {  // split-K: this slice's slab of the workspace (gemm_splitk_reduce adds them)
+      if (slab) {  // split-K: this slice's slab of the workspace (gemm_splitk_reduce adds them)
         *reinterpret_cast<f32x4_t*>(y + static_cast<int64_t>(blockIdx.z) * M * N + static_cast<int64_t>(m) * N + n) =
             acc[i][j];
         continue;
       }
-      f32x4_t v = acc[i][j] + *reinterpret_cast<const f32x4_t*>(bias + n);
-      if (res) v += *reinterpret_cast<const f32x4_t*>(res + static_cast<int64_t>(m) * N + n);
+      f32x4_t v = acc[i][j] + bv[j];
+      if (res) v += rv[i][j];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], act);
       *reinterpret_cast<f32x4_t*>(yp) = v;
