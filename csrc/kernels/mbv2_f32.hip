@@ -30,6 +30,10 @@
 //  * avgpool_f32   global average pool.
 //  * ir_block_f32  the fused inverted residual (expand -> dw -> project),
 //                  hidden activation in LDS; see the comment at the kernel.
+//  * irw_f32       the wave-split fused inverted residual (each wave walks its
+//                  own hidden subtiles; no barriers in the channel loop).
+//  * stem_ir1w_f32 stem + first block, one wave per 8x8 tile (the model's
+//                  default; stem_ir1_f32 is the 8-wave 16x16 variant).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
