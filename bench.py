@@ -15,15 +15,26 @@ Pipeline (one per rank, pinned to GPU LOCAL_RANK):
 
   videotestsrc pattern=snow ! video/x-raw,format=RGB,width=224,height=224
     ! tensor_converter frames-per-tensor=B device=<gpu>     # H2D into HBM, B frames per tensor
-    ! tensor_transform mode=arithmetic option=typecast:float32,add:-127.5,div:127.5   # fused into the stem
+    ! tensor_transform mode=arithmetic option=typecast:float32,add:-127.5,div:127.5   # the reference string
+    ! queue
     ! tensor_filter framework=pytorch model=mbv2.pt accelerator=true:gpu custom=hipgraph:true
     ! tensor_decoder mode=image_labeling option1=labels.txt # HIP argmax, labels D2H
     ! tensor_sink
 
+The tensor_transform is the reference's own normalisation element
+(gsttensor_transform.c:1241-1412).  At caps negotiation tensor_filter absorbs
+it (runtime/fusion.h): the model's uint8 input table takes the transform's exact
+fp32 arithmetic and the transform passes the uint8 frames through, so the
+first kernel reads 1 byte per channel instead of 4.  `--no-absorb` keeps the
+transform's own kernel (float32 frames into the model) for comparison.
+
 Precision: the reference runs the model in float32 (tensor_filter_pytorch.cc
 :517-536), so the headline `value` is the fp32 engine (fp32 activations,
 weights and accumulation: v_mfma_f32_16x16x4_f32 GEMMs, fp32 depthwise).
-The bf16 engine is measured after it (at `--batch-bf16`, 128) and reported as `value_bf16`.
+`--precision bf16|both` also measures the bf16 engine (`value_bf16`).
+After the headline run a short sweep over smaller batches (`--sweep`,
+default 8,32,128) reports throughput and p50 latency per batch size
+(`sweep`), and a live batch-1 run reports the pipeline's per-frame latency.
 
 A "step" is one batch of B frames reaching the sink.  W batches warm up
 (graph capture, allocator), then the wall time of exactly K batches is
@@ -61,7 +72,7 @@ def parse_args(argv=None):
     ap.add_argument("--batch-bf16", type=int, default=int(os.environ.get("NNSX_BENCH_BATCH_BF16", "128")),
                     help="batch of the secondary bf16 run (its kernels were tuned at 128; at 512 they "
                          "measured 71-125k frames/s from run to run, at 128 117-125k)")
-    ap.add_argument("--precision", default=os.environ.get("NNSX_BENCH_PRECISION", "both"),
+    ap.add_argument("--precision", default=os.environ.get("NNSX_BENCH_PRECISION", "fp32"),
                     choices=["fp32", "bf16", "both"],
                     help="fp32 = reference precision (headline); bf16 = secondary; both = fp32 headline + bf16")
     ap.add_argument("--engine", default=os.environ.get("NNSX_BENCH_ENGINE", "fused"), choices=["fused", "torch"],
@@ -71,11 +82,15 @@ def parse_args(argv=None):
     ap.add_argument("--latency-fps", type=int, default=int(os.environ.get("NNSX_BENCH_LAT_FPS", "500")),
                     help="frame rate of the live camera in the batch-1 latency run")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--no-fuse-norm", action="store_true",
-                    help="keep the normalisation as a separate tensor_transform element")
+    ap.add_argument("--no-absorb", "--no-fuse-norm", dest="no_absorb", action="store_true",
+                    help="tensor_filter absorb-transform=false: the tensor_transform runs its own kernel and the "
+                         "model reads float32 frames")
+    ap.add_argument("--sweep", default=os.environ.get("NNSX_BENCH_SWEEP", "8,32,128"),
+                    help="comma-separated batch sizes of the throughput / latency sweep ('' = skip)")
+    ap.add_argument("--sweep-steps", type=int, default=10, help="timed steps per sweep point")
     ap.add_argument("--cpu", action="store_true", help="CPU reference path (device=-1, torch CPU)")
     ap.add_argument("--queue", type=int, default=4, help="queue depth between filter and decoder")
-    ap.add_argument("--model-broadcast", default=os.environ.get("NNSX_BENCH_BCAST", "tcp"),
+    ap.add_argument("--model-broadcast", default=os.environ.get("NNSX_BENCH_BCAST", "auto"),
                     choices=["off", "tcp", "rccl", "auto"],
                     help="N > 1: rank 0 broadcasts the model bytes to every rank at load over this data plane")
     ap.add_argument("--comm-backend", default="auto", choices=["auto", "rccl", "tcp"],
@@ -178,9 +193,9 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
     total = warmup + steps
     frames = total * B
     graph = "true" if (use_gpu and not a.no_graph) else "false"
-    # fused models take the raw uint8 frame and apply the tensor_transform normalisation
-    # ((x + add) / div, bit-identical) inside their first kernel; plain models keep the element
-    fuse_norm = "fused" in model_name and not a.no_fuse_norm
+    # the reference string always carries the tensor_transform; tensor_filter absorbs it
+    # into fused models (uint8 input table) unless --no-absorb
+    absorb = "false" if a.no_absorb else "true"
     accel = "true:gpu" if use_gpu else "false"
     # The source cycles through a ring of distinct pre-rendered frames (a camera ring
     # buffer).  The ring is sized to 512 MiB, twice the MI355X's 256 MiB last-level
@@ -195,7 +210,7 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
     if world > 1 and a.model_broadcast != "off" and not cfg.get("fan"):  # (fan-out: rank 0 runs no filter)
         bcast = f",broadcast:0,broadcast-backend:{a.model_broadcast},broadcast-name:{model_name}-b{B}"
     filt = (f"tensor_filter name=filt framework=pytorch model={model_path} input=3:{S}:{S}:{B} "
-            f"inputtype={'uint8' if fuse_norm else 'float32'} accelerator={accel} device={dev} "
+            f"inputtype=float32 absorb-transform={absorb} accelerator={accel} device={dev} "
             f"custom=hipgraph:{graph}{bcast} device-stats={'true' if use_gpu else 'false'} ")
     live = f"is-live=true " if live_fps > 0 else ""
     # throughput runs: queues are thread boundaries, so the next batch's upload
@@ -209,8 +224,8 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
         f"videotestsrc num-buffers={frames} pattern=snow pool-size={pool} {live}"
         f"! video/x-raw,format=RGB,width={S},height={S},framerate={live_fps}/1 "
         f"! tensor_converter frames-per-tensor={B} device={dev} "
+        + f"! tensor_transform name=norm mode=arithmetic option={cfg['norm']} "
         + q1
-        + (f"! tensor_transform mode=arithmetic option={cfg['norm']} " if not fuse_norm else "")
         + f"! {filt}"
         + (f"! tee name=t t. ! queue max-size-buffers={a.queue} " if cfg.get("gather") else q2)
         + f"! {cfg['decoder'].format(**files)} "
@@ -232,7 +247,7 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
                     f"! edgesink {link}")
         else:
             desc = (f"edgesrc {link} peer-rank=0 ! queue max-size-buffers=2 "
-                    + (f"! tensor_transform mode=arithmetic option={cfg['norm']} " if not fuse_norm else "")
+                    + f"! tensor_transform name=norm mode=arithmetic option={cfg['norm']} "
                     + f"! {filt}"
                     f"! queue max-size-buffers={a.queue} ! {cfg['decoder'].format(**files)} ! tensor_sink name=sink")
     per_step = B if cfg["per_frame"] else 1  # sink buffers per batch
@@ -261,12 +276,13 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
         dist.barrier()
     gathered = pipe.get_by_name("ag").get_property("comm-bytes") if cfg.get("gather") else None
     dev_stamps = filt_el.get_property("device-stamps") if (filt_el is not None and use_gpu) else ""
+    absorbed = filt_el.get_property("absorbed") if filt_el is not None else ""
     pipe.stop()
 
     import numpy as np
 
     rec = dict(elapsed=0.0, p50=0.0, p99=0.0, gpu_elapsed=0.0, gpu_busy_ms=0.0, wall=t_end - t_start,
-               desc=desc, fan=fan, workers=workers, fuse_norm=fuse_norm, gathered=gathered)
+               desc=desc, fan=fan, workers=workers, absorbed=absorbed, gathered=gathered)
     if sink is None:
         return rec  # the workers' clocks decide
     recs = [tuple(int(v) for v in e.split(":")) for e in sink.get_property("stats").split(",") if e]
@@ -372,13 +388,28 @@ def main():
         lat_b1 = run_pipeline(a, nns, cfg, model_name, model_path, files, 1, a.latency_frames, w1, rank, world, dev,
                               use_gpu, dist, live_fps=a.latency_fps)
 
+    # throughput / latency trade-off at smaller batches (same engine, same pipeline)
+    sweep = []
+    if a.sweep and use_gpu and not cfg.get("fan"):
+        label, model_name, _ = runs[0]
+        model_path = os.path.join(workdir, f"{model_name}.pt")
+        for sb in [int(x) for x in a.sweep.split(",") if x.strip()]:
+            if sb == a.batch:
+                continue
+            r = run_pipeline(a, nns, cfg, model_name, model_path, files, sb, a.sweep_steps, 3, rank, world, dev,
+                             use_gpu, dist)
+            sweep.append((sb, r))
+
     # per-rank records, all-gathered over the job's process group (RCCL on GPUs):
     # [elapsed, p50, p99, gpu_elapsed, gpu_busy] per engine + batch-1 p50/p99
+    # + [max(sink, device) elapsed, p50] per sweep batch
     vec = []
     for label, _, _ in runs:
         r = results[label]
         vec += [r["elapsed"], r["p50"], r["p99"], r["gpu_elapsed"], r["gpu_busy_ms"]]
     vec += [lat_b1["p50"], lat_b1["p99"]] if lat_b1 else [0.0, 0.0]
+    for _, r in sweep:
+        vec += [max(r["elapsed"], r["gpu_elapsed"]), r["p50"]]
     stats = torch.tensor(vec, dtype=torch.float64)
     if dist is not None:
         if dist.get_backend() == "nccl":
@@ -454,9 +485,20 @@ def main():
             out.update(p50_latency_ms_b1=round(float(per_rank[:, n * 5].max()), 3),
                        p99_latency_ms_b1=round(float(per_rank[:, n * 5 + 1].max()), 3),
                        latency_b1_source=f"live camera, {a.latency_fps} frames/s, batch 1")
+        if sweep:
+            n = len(runs)
+            base_i = n * 5 + 2
+            pts = []
+            for j, (sb, _) in enumerate(sweep):
+                el = float(per_rank[:, base_i + 2 * j].max())
+                pts.append({"batch": sb, "frames_per_s": round(workers * a.sweep_steps * sb / el, 1) if el > 0 else None,
+                            "p50_latency_ms": round(float(per_rank[:, base_i + 2 * j + 1].max()), 3)})
+            pts.append({"batch": B, "frames_per_s": round(h["fps"], 1), "p50_latency_ms": round(h["p50"], 3)})
+            out["sweep"] = sorted(pts, key=lambda d: d["batch"])
         out.update({
-            "preprocess": ("tensor_transform normalisation fused into the model's stem kernel (uint8 input)"
-                           if head["fuse_norm"] else "tensor_transform element"),
+            "preprocess": (f"tensor_transform (reference string) absorbed by tensor_filter into the model's uint8 "
+                           f"input table ({head['absorbed']}: frames stay uint8)" if head["absorbed"]
+                           else "tensor_transform element (own kernel, float32 frames into the model)"),
             "wall_s": round(sum(r["wall"] for r in results.values()), 3),
             "numa_binding": numa,
             **({"allgather_bytes_sent_received_rank0": head["gathered"]} if head["gathered"] is not None else {}),

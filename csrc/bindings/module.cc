@@ -274,6 +274,20 @@ PYBIND11_MODULE(_C, m) {
           default: return py::str(v);
         }
       })
+      .def("query_latency", [](Element& e) -> py::object {
+        // latency query from this element's first sink pad upstream (GST_QUERY_LATENCY)
+        Pad* sp = e.sink_pad(0);
+        if (!sp) return py::none();
+        bool live = false;
+        int64_t mn = 0, mx = -1;
+        bool ok;
+        {
+          py::gil_scoped_release r;
+          ok = e.query_latency(sp, &live, &mn, &mx);
+        }
+        if (!ok) return py::none();
+        return py::make_tuple(live, mn, mx);
+      }, "Latency query from this element's sink pad: (live, min_ns, max_ns) or None")
       .def("properties", [](Element& e) {
         std::vector<std::tuple<std::string, std::string, std::string>> v;
         for (auto& p : e.properties()) v.emplace_back(p.name, p.blurb, p.default_value);

@@ -10,12 +10,14 @@
 // device; GPU frameworks consume device memories in place and return
 // device-resident, allocate-in-invoke outputs (no per-frame PCIe copies).
 #include <algorithm>
+#include <cmath>
 #include <deque>
 
 #include "core/log.h"
 #include "elements/elements.h"
 #include "elements/tensor_common.h"
 #include "runtime/base.h"
+#include "runtime/fusion.h"
 #include "runtime/pipeline.h"
 #include "runtime/plugin_api.h"
 
@@ -48,7 +50,7 @@ std::vector<int> parse_ranks(const std::string& s) {
   return v;
 }
 
-class TensorFilter : public BaseTransform {
+class TensorFilter : public BaseTransform, public TransformAbsorber {
  public:
   explicit TensorFilter(const std::string& name)
       : BaseTransform("tensor_filter", name, Caps::from_string(tensor_caps_template_all()),
@@ -92,7 +94,7 @@ class TensorFilter : public BaseTransform {
       s.type = PropType::INT;
       s.blurb = "The average latency over the recent 10 inferences in microseconds (write 1 to enable, 0 to disable; -1 when disabled)";
       s.set = [this](const std::string& v) { latency_mode_ = static_cast<int>(to_int(v)); };
-      s.get = [this] { return std::to_string(latency_mode_ > 0 ? avg_latency_us() : -1); };
+      s.get = [this] { return std::to_string(latency_mode_ == 1 ? avg_latency_us() : -1); };
       add_prop(s);
     }
     {
@@ -101,7 +103,7 @@ class TensorFilter : public BaseTransform {
       s.type = PropType::INT;
       s.blurb = "The average throughput in frames per second x 1000 (write 1 to enable, 0 to disable; -1 when disabled)";
       s.set = [this](const std::string& v) { throughput_mode_ = static_cast<int>(to_int(v)); };
-      s.get = [this] { return std::to_string(throughput_mode_ > 0 ? throughput_milli_fps() : -1); };
+      s.get = [this] { return std::to_string(throughput_mode_ == 1 ? throughput_milli_fps() : -1); };
       add_prop(s);
     }
     prop_string("input-combination", &input_comb_str_, "Select the input tensor(s) to invoke the models", [this] {
@@ -125,6 +127,46 @@ class TensorFilter : public BaseTransform {
       return r;
     }, "nnsx: per-invoke 'end_ns:latency_ns' on the device clock (relative to the first invoke), comma separated");
     prop_string("config-file", &config_file_, "Path to a key=value file setting any of the properties", [this] { load_config_file(); });
+    prop_bool("absorb-transform", &absorb_enabled_,
+              "nnsx: fold an adjacent upstream tensor_transform (uint8 -> float32 elementwise arithmetic) into the "
+              "model when the model maps uint8 frames through an input table");
+    prop_readonly("absorbed", [this] { return absorbed_from_; },
+                  "nnsx: name of the tensor_transform absorbed at caps negotiation (empty: none)");
+  }
+
+  // ---- TransformAbsorber (runtime/fusion.h) ----
+  bool absorb_arith(const ArithPrefix& p, const std::string& by) override {
+    if (!inst_ || !input_comb_.empty() || p.in_type != DType::UINT8 || p.out_type != DType::FLOAT32) return false;
+    if (!inst_->accepts_input_table(p.tensor)) return false;
+    std::vector<float> lut;
+    if (!arith_table_u8(p.params, p.out_type, &lut)) return false;
+    if (!inst_->set_input_table(p.tensor, lut)) return false;
+    // the model input is now the transform's input: uint8
+    if (props_.input_info.num_tensors > p.tensor) props_.input_info.at(p.tensor).type = DType::UINT8;
+    if (model_in_.num_tensors > p.tensor) model_in_.at(p.tensor).type = DType::UINT8;
+    absorbed_from_ = by;
+    NNSX_LOGI(name(), "absorbed ", by, " into the model's uint8 input table");
+    return true;
+  }
+
+  // walk upstream through queues to an absorbable element (tensor_transform)
+  void attach_absorbable() {
+    detach_absorbable();
+    if (!absorb_enabled_ || !inst_ || !inst_->accepts_input_table(0)) return;
+    Pad* sp = sink_pad(0);
+    Element* up = sp && sp->peer() ? sp->peer()->parent() : nullptr;
+    while (up && up->factory() == "queue") {
+      Pad* s = up->sink_pad(0);
+      up = s && s->peer() ? s->peer()->parent() : nullptr;
+    }
+    if (auto* ab = dynamic_cast<AbsorbableElement*>(up)) {
+      ab->set_absorber(this);
+      absorbable_up_ = ab;
+    }
+  }
+  void detach_absorbable() {
+    if (absorbable_up_) absorbable_up_->set_absorber(nullptr);
+    absorbable_up_ = nullptr;
   }
 
   ~TensorFilter() override {
@@ -390,14 +432,6 @@ class TensorFilter : public BaseTransform {
     return true;
   }
 
-  int64_t own_latency() const override {
-    if (latency_mode_ <= 0) return 0;
-    std::lock_guard<std::mutex> lk(stat_mu_);
-    if (lat_.empty()) return 0;
-    int64_t s = 0;
-    for (auto v : lat_) s += v;
-    return s / static_cast<int64_t>(lat_.size());
-  }
 
   // ---------------------------------------------------------------- transform ----
   FlowReturn transform(const BufferPtr& inbuf, BufferPtr* outbuf) override {
@@ -592,42 +626,102 @@ class TensorFilter : public BaseTransform {
     add_sample_locked(dur_ns, now);
   }
 
+  // tensor_filter.c:378-455 record_statistics: the first measurement is
+  // ignored (latency_ignore_count = 1, tensor_filter_common.c:579); latency =
+  // mean of the last 10 invokes (us); throughput = invokes x 1e6 x 1000 /
+  // total invoke latency (us), i.e. FPS x 1000; totals are rebased past 2000
+  // invokes (cache at 1000) so they never overflow.
   void add_sample_locked(int64_t dur_ns, int64_t now) {
+    (void)now;
     ++total_invoke_;
-    if (total_invoke_ <= kWarmup) return;  // ignore warm-up samples
+    if (ignore_count_ > 0) {
+      --ignore_count_;
+      return;
+    }
+    sum_lat_ns_ += dur_ns;
+    sum_num_ += 1;
     lat_.push_back(dur_ns);
-    if (lat_.size() > 10) lat_.pop_front();
-    stamps_.push_back(now);
-    if (stamps_.size() > 10) stamps_.pop_front();
-    if (latency_report_) {
+    if (lat_.size() > kMaxRecent) lat_.pop_front();
+    if (latency_mode_ > 0 || latency_report_) {
       int64_t avg = 0;
       for (auto v : lat_) avg += v;
-      avg /= static_cast<int64_t>(lat_.size());
-      if (reported_ <= 0 || avg > reported_ * 125 / 100 || avg < reported_ * 75 / 100) {
-        reported_ = avg;
-        Structure s("latency");
-        s.set("latency-ns", Value::Int(avg * 105 / 100));  // +5% headroom like the reference
-        post_latency();
-      }
+      avg = avg / static_cast<int64_t>(lat_.size()) / 1000;  // us, like g_get_real_time deltas
+      prop_latency_us_ = avg <= INT32_MAX ? avg : -1;
     }
+    if (throughput_mode_ > 0) {
+      int64_t thr = -1;
+      if (sum_lat_ns_ != 0) {
+        const double t = static_cast<double>(sum_num_) * 1e12 / static_cast<double>(sum_lat_ns_);
+        if (t <= INT32_MAX) thr = static_cast<int64_t>(t);
+      }
+      prop_throughput_ = thr;
+    }
+    if (sum_num_ > kDropOld) {
+      sum_lat_ns_ -= old_lat_ns_;
+      sum_num_ -= old_num_;
+      old_lat_ns_ = 0;
+      old_num_ = 0;
+    } else if (sum_num_ > kCacheOld && old_num_ == 0) {
+      old_lat_ns_ = sum_lat_ns_;
+      old_num_ = sum_num_;
+    }
+    if (latency_report_) track_latency_locked();
+  }
+
+  // tensor_filter.c:470-495 track_latency: post LATENCY when the estimate
+  // exceeds what the last latency query reported, or deviates from it by more
+  // than 25 %.  The latency query (query_latency below) stores the reported
+  // value with 5 % headroom (tensor_filter.c:1338-1349).
+  void track_latency_locked() {
+    const double estimated = static_cast<double>(prop_latency_us_) * 1000.0;
+    const double reported = static_cast<double>(latency_reported_ns_);
+    if (estimated <= 0) return;
+    const double deviation = reported > 0 ? std::abs(estimated - reported) / reported : 0.0;
+    if (estimated > reported || deviation > kLatencyReportThreshold) {
+      ++latency_posts_;
+      post_latency();
+    }
+  }
+
+  bool query_latency(Pad* pad, bool* live, int64_t* min_lat, int64_t* max_lat) override {
+    int64_t est;
+    {
+      std::lock_guard<std::mutex> lk(stat_mu_);
+      est = prop_latency_us_;
+    }
+    bool ok = Element::query_latency(pad, live, min_lat, max_lat);
+    if (latency_report_ && est > 0 && ok) {
+      const int64_t lat = static_cast<int64_t>(static_cast<double>(est) * 1000.0 * (1.0 + kLatencyReportHeadroom));
+      {
+        std::lock_guard<std::mutex> lk(stat_mu_);
+        latency_reported_ns_ = lat;
+      }
+      *min_lat += lat;
+      if (*max_lat >= 0) *max_lat += lat;
+    }
+    return ok;
   }
 
   int64_t avg_latency_us() {
     poll_device_stats(false);
     std::lock_guard<std::mutex> lk(stat_mu_);
-    if (lat_.empty()) return 0;
-    int64_t s = 0;
-    for (auto v : lat_) s += v;
-    return s / static_cast<int64_t>(lat_.size()) / 1000;
+    return prop_latency_us_;
   }
 
   int64_t throughput_milli_fps() {
     poll_device_stats(false);
     std::lock_guard<std::mutex> lk(stat_mu_);
-    if (stamps_.size() < 2) return 0;
-    int64_t span = stamps_.back() - stamps_.front();
-    if (span <= 0) return 0;
-    return static_cast<int64_t>((stamps_.size() - 1) * 1000.0 * 1e9 / static_cast<double>(span));
+    return prop_throughput_;
+  }
+
+  void reset_stats_locked() {
+    lat_.clear();
+    dev_log_.clear();
+    total_invoke_ = 0;
+    ignore_count_ = 1;
+    sum_lat_ns_ = sum_num_ = old_lat_ns_ = old_num_ = 0;
+    prop_latency_us_ = prop_throughput_ = 0;
+    latency_reported_ns_ = 0;
   }
 
   bool start() override {
@@ -635,15 +729,15 @@ class TensorFilter : public BaseTransform {
     throttle_delay_ = 0;
     {
       std::lock_guard<std::mutex> lk(stat_mu_);
-      lat_.clear();
-      stamps_.clear();
-      dev_log_.clear();
-      total_invoke_ = 0;
+      reset_stats_locked();
     }
-    return ensure_open();
+    if (!ensure_open()) return false;
+    attach_absorbable();
+    return true;
   }
   bool stop() override {
     poll_device_stats(true);
+    detach_absorbable();
     return true;
   }
   void release_timing_events() {
@@ -660,7 +754,9 @@ class TensorFilter : public BaseTransform {
   void close() override { close_fw(); }
 
  private:
-  static constexpr int64_t kWarmup = 0;
+  static constexpr size_t kMaxRecent = 10;             // GST_TF_STAT_MAX_RECENT
+  static constexpr int64_t kDropOld = 2000, kCacheOld = 1000;  // THRESHOLD_DROP_OLD / _CACHE_OLD
+  static constexpr double kLatencyReportThreshold = 0.25, kLatencyReportHeadroom = 0.05;
   std::string fw_name_, model_str_, input_str_, inputtype_str_, inputname_str_, inputranks_str_, output_str_,
       outputtype_str_, outputname_str_, outputranks_str_, input_comb_str_, output_comb_str_, config_file_;
   FilterProperties props_;
@@ -668,6 +764,9 @@ class TensorFilter : public BaseTransform {
   std::vector<std::pair<bool, int>> out_comb_;
   bool latency_report_ = false;
   int latency_mode_ = 0, throughput_mode_ = 0;
+  bool absorb_enabled_ = true;
+  AbsorbableElement* absorbable_up_ = nullptr;
+  std::string absorbed_from_;
   int device_prop_ = -1;
   std::shared_ptr<FilterFramework> fw_;
   std::shared_ptr<FilterInstance> inst_;
@@ -679,8 +778,11 @@ class TensorFilter : public BaseTransform {
   bool in_flexible_ = false, out_flexible_ = false, configured_ = false;
   int64_t throttle_delay_ = 0, prev_ts_ = -1;
   mutable std::mutex stat_mu_;
-  std::deque<int64_t> lat_, stamps_;
-  int64_t total_invoke_ = 0, reported_ = 0;
+  std::deque<int64_t> lat_;
+  int64_t total_invoke_ = 0;
+  int ignore_count_ = 1;
+  int64_t sum_lat_ns_ = 0, sum_num_ = 0, old_lat_ns_ = 0, old_num_ = 0;
+  int64_t prop_latency_us_ = 0, prop_throughput_ = 0, latency_reported_ns_ = 0, latency_posts_ = 0;
   bool device_stamps_ = false;
   std::deque<DevStamp> pending_;
   std::vector<hipEvent_t> ev_free_;

@@ -16,6 +16,7 @@
 #include "elements/tensor_common.h"
 #include "kernels/kernels.h"
 #include "runtime/base.h"
+#include "runtime/fusion.h"
 #include "runtime/pipeline.h"
 
 namespace nnsx {
@@ -171,7 +172,7 @@ void cpu_stand(const void* in, DType in_t, void* out, DType out_t, uint64_t n, u
   }
 }
 
-class TensorTransform : public BaseTransform {
+class TensorTransform : public BaseTransform, public AbsorbableElement {
  public:
   explicit TensorTransform(const std::string& name)
       : BaseTransform("tensor_transform", name,
@@ -189,8 +190,24 @@ class TensorTransform : public BaseTransform {
                 });
     prop_uint("transpose-rank-limit", &transpose_rank_limit_, "The rank limit of transpose, which varies per version of nnstreamer and may be lower than the global rank limit if it is over 4.");
     prop_int("device", &device_, "nnsx: -2 follow input placement, -1 CPU, N run on GPU N");
+    prop_bool("absorbable", &absorbable_,
+              "nnsx: let a downstream tensor_filter whose model takes uint8 frames fold this elementwise arithmetic "
+              "into the model (the transform then passes the frames through)");
+    prop_readonly("absorbed-by", [this] { return absorbed_ ? absorbed_by_ : std::string(); },
+                  "nnsx: the element that absorbed this transform at caps negotiation (empty: runs its own kernel)");
     mode_ = MODE_UNKNOWN;
   }
+
+  // ---- AbsorbableElement (runtime/fusion.h) ----
+  void set_absorber(TransformAbsorber* a) override {
+    std::lock_guard<std::mutex> lk(absorb_mu_);
+    absorber_ = a;
+    if (!a) {
+      absorbed_ = false;
+      absorbed_by_.clear();
+    }
+  }
+  bool absorbed() const override { return absorbed_; }
 
  protected:
   bool applies(unsigned i) const {
@@ -351,12 +368,42 @@ class TensorTransform : public BaseTransform {
     }
   }
 
+  // An elementwise uint8 -> float32 arithmetic / typecast on a single static
+  // tensor, offered to the downstream absorber once per negotiation.
+  bool try_absorb(const TensorsConfig& in) {
+    std::lock_guard<std::mutex> lk(absorb_mu_);
+    if (!absorber_ || !absorbable_ || !loaded_) return false;
+    if (mode_ != ARITHMETIC && mode_ != TYPECAST) return false;
+    if (!in.is_static() || in.info.num_tensors != 1 || !applies(0)) return false;
+    const TensorInfo& ti = in.info.at(0);
+    if (ti.type != DType::UINT8) return false;
+    if (mode_ == ARITHMETIC && per_channel_) return false;
+    const DType out = mode_ == TYPECAST ? cast_to_ : (arith_out_ == DType::END ? ti.type : arith_out_);
+    if (out != DType::FLOAT32) return false;
+    if (absorbed_) return true;
+    ArithPrefix p;
+    p.tensor = 0;
+    p.in_type = ti.type;
+    p.out_type = out;
+    p.params = effective_params(ti);
+    if (!absorber_->absorb_arith(p, name())) return false;
+    absorbed_ = true;
+    Element* e = dynamic_cast<Element*>(absorber_);
+    absorbed_by_ = e ? e->name() : std::string("?");
+    NNSX_LOGI(name(), "arithmetic absorbed by ", absorbed_by_, ": uint8 frames pass through");
+    return true;
+  }
+
   Caps transform_caps(PadDirection dir, const Caps& caps, const Caps* filter) override {
     Caps r;
     for (size_t i = 0; i < caps.size(); ++i) {
       const Structure& st = caps.at(i);
       TensorsConfig in;
       if (!config_from_structure(st, &in) || !loaded_) {
+        r.append(st);
+        continue;
+      }
+      if (dir == PadDirection::SINK && try_absorb(in)) {  // pass-through caps
         r.append(st);
         continue;
       }
@@ -401,6 +448,10 @@ class TensorTransform : public BaseTransform {
   Caps fixate_caps(PadDirection, const Caps& caps, Caps othercaps) override {
     TensorsConfig in;
     if (caps.size() && config_from_structure(caps.at(0), &in) && !in.is_flexible() && loaded_) {
+      if (absorbed_) {  // pass-through: the output is the input
+        Caps peer = src_pad()->peer_query_caps(nullptr);
+        return pad_caps_from_config(in, &peer);
+      }
       TensorsConfig out = in;
       for (unsigned t = 0; t < in.info.num_tensors; ++t)
         if (applies(t)) convert_info(in.info.at(t), &out.info.at(t));
@@ -418,6 +469,7 @@ class TensorTransform : public BaseTransform {
     if (!tensor_config_from_caps(incaps, &in_config_) || !tensor_config_from_caps(outcaps, &out_config_)) return false;
     in_flexible_ = in_config_.is_flexible();
     out_flexible_ = out_config_.is_flexible();
+    if (absorbed_) return true;  // pass-through
     if (!in_flexible_) {
       // validate the output config against the conversion
       for (unsigned t = 0; t < in_config_.info.num_tensors; ++t) {
@@ -431,6 +483,10 @@ class TensorTransform : public BaseTransform {
 
   FlowReturn transform(const BufferPtr& inbuf, BufferPtr* outbuf) override {
     if (!loaded_) return FlowReturn::ERROR;
+    if (absorbed_) {  // the downstream filter applies this arithmetic inside its model
+      *outbuf = inbuf;
+      return FlowReturn::OK;
+    }
     BufferPtr in;
     if (!buffer_from_config(inbuf, in_config_, &in)) {
       post_error("tensor_transform: input buffer does not match the negotiated caps");
@@ -582,9 +638,23 @@ class TensorTransform : public BaseTransform {
   TensorsConfig in_config_, out_config_;
   bool in_flexible_ = false, out_flexible_ = false;
   StreamSet streams_;
+  std::mutex absorb_mu_;
+  TransformAbsorber* absorber_ = nullptr;
+  bool absorbable_ = true;
+  std::atomic<bool> absorbed_{false};
+  std::string absorbed_by_;
 };
 
 }  // namespace
+
+bool arith_table_u8(const kernels::ArithParams& p, DType out, std::vector<float>* lut) {
+  if (out != DType::FLOAT32) return false;
+  uint8_t in[256];
+  for (int i = 0; i < 256; ++i) in[i] = static_cast<uint8_t>(i);
+  lut->assign(256, 0.f);
+  cpu_arith(in, DType::UINT8, lut->data(), DType::FLOAT32, 256, p);
+  return true;
+}
 
 void register_tensor_transform() {
   register_element("tensor_transform", "Filter/Tensor", "Transforms other/tensor dimensions for different models or frameworks",

@@ -95,6 +95,26 @@ class TorchInstance : public FilterInstance {
 
   bool wants_host_input() const override { return device_ < 0; }
 
+  // models exposing a float32 [256] attribute `in_lut` map a uint8 input 0
+  // through it (nnstreamer_amd.models.fused: the fused stems); an upstream
+  // tensor_transform's arithmetic is folded into that table (runtime/fusion.h)
+  bool accepts_input_table(unsigned index) const override { return index == 0 && has_lut_; }
+
+  bool set_input_table(unsigned index, const std::vector<float>& lut) override {
+    if (index != 0 || !has_lut_ || lut.size() != 256) return false;
+    std::lock_guard<std::mutex> lk(mu_);
+    try {
+      apply_lut(module_, lut);
+    } catch (const std::exception& e) {
+      NNSX_LOGE("pytorch", "set_input_table failed: ", e.what());
+      return false;
+    }
+    lut_ = lut;
+    if (props_.input_info.num_tensors > 0) props_.input_info.at(0).type = DType::UINT8;
+    graphs_.clear();
+    return true;
+  }
+
   bool get_model_info(TensorsInfo* in, TensorsInfo* out) override {
     if (props_.input_info.num_tensors > 0 && props_.input_info.valid() && props_.output_info.num_tensors > 0 &&
         props_.output_info.valid()) {
@@ -154,6 +174,7 @@ class TorchInstance : public FilterInstance {
   bool reload_model(const FilterProperties& p) override {
     try {
       torch::jit::Module fresh = load_module(p.model_files.at(0));
+      if (!lut_.empty()) apply_lut(fresh, lut_);  // keep an absorbed transform
       std::lock_guard<std::mutex> lk(mu_);
       module_ = std::move(fresh);
       graphs_.clear();  // captured graphs point at the old weights
@@ -185,13 +206,35 @@ class TorchInstance : public FilterInstance {
   torch::jit::Module load_module(const std::string& path) {
     hip::DeviceGuard g(device_);
     torch::jit::Module m = torch::jit::load(path, dev());
+    return finish_module(std::move(m));
+  }
+
+  // eval + freeze (constant-folds attributes); `in_lut` stays a mutable
+  // attribute so an absorbed transform can rewrite it in place
+  torch::jit::Module finish_module(torch::jit::Module m) {
     m.eval();
-    // inference-only: freeze when possible (constant-folds attributes)
+    has_lut_ = false;
+    if (m.hasattr("in_lut")) {
+      const c10::IValue v = m.attr("in_lut");
+      has_lut_ = v.isTensor() && v.toTensor().scalar_type() == torch::kFloat && v.toTensor().numel() == 256;
+    }
     try {
-      m = torch::jit::freeze(m);
+      if (has_lut_)
+        m = torch::jit::freeze(m, std::vector<std::string>{"in_lut"});
+      else
+        m = torch::jit::freeze(m);
     } catch (...) {
     }
     return m;
+  }
+
+  void apply_lut(torch::jit::Module& m, const std::vector<float>& lut) {
+    torch::NoGradGuard ng;
+    hip::DeviceGuard g(device_);
+    at::Tensor t = m.attr("in_lut").toTensor();
+    at::Tensor src = torch::from_blob(const_cast<float*>(lut.data()), {256}, torch::kFloat).clone();
+    t.copy_(src.to(t.device()));
+    if (device_ >= 0) hip::check(hipDeviceSynchronize(), "in_lut upload");
   }
   void load(const std::string& path) { module_ = bcast_root_ >= 0 ? load_broadcast(path) : load_module(path); }
 
@@ -232,13 +275,7 @@ class TorchInstance : public FilterInstance {
               " bytes, group rank ", g->rank(), "/", g->size(), ")");
     hip::DeviceGuard dg(device_);
     std::istringstream is(bytes);
-    torch::jit::Module m = torch::jit::load(is, dev());
-    m.eval();
-    try {
-      m = torch::jit::freeze(m);
-    } catch (...) {
-    }
-    return m;
+    return finish_module(torch::jit::load(is, dev()));
   }
 
   at::Tensor prepare(at::Tensor t) {
@@ -413,6 +450,8 @@ class TorchInstance : public FilterInstance {
   bool channels_last_ = false;
   DType compute_dtype_ = DType::END;
   std::mutex mu_;
+  bool has_lut_ = false;       // the model maps uint8 input 0 through attribute in_lut
+  std::vector<float> lut_;     // the absorbed table (re-applied on hot reload)
   std::map<std::string, std::vector<std::unique_ptr<GraphState>>> graphs_;
   hipStream_t cap_stream_ = nullptr;  // private capture stream (graph_for)
 };

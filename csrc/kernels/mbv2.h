@@ -19,9 +19,10 @@ void dw3x3(const void* x, const void* w, const float* bias, void* y, int B, int 
            int act, hipStream_t s);
 // 3x3/2 stem conv 3 -> 32 from an f32 NHWC frame; w f32 [3][3][3][32]
 void stem3x3(const float* x, const float* w, const float* bias, void* y, int B, int H, int W, int act, hipStream_t s);
-// same from the raw uint8 RGB frame, normalised in-kernel as (x + add) / div
-void stem3x3_u8(const uint8_t* x, const float* w, const float* bias, void* y, int B, int H, int W, int act, float add,
-                float div, hipStream_t s);
+// same from the raw uint8 RGB frame, mapped in-kernel through lut[256] (device,
+// f32: the upstream tensor_transform arithmetic folded into a table)
+void stem3x3_u8(const uint8_t* x, const float* w, const float* bias, void* y, int B, int H, int W, int act,
+                const float* lut, hipStream_t s);
 // mean over HW: x [B][HW][C] -> y [B][C] (bf16)
 void avgpool(const void* x, void* y, int B, int HW, int C, hipStream_t s);
 
@@ -65,7 +66,7 @@ void dw3x3_f32(const float* x, const float* w, const float* bias, float* y, int 
 void stem3x3_f32(const float* x, const float* w, const float* bias, float* y, int B, int H, int W, int act,
                  hipStream_t s);
 void stem3x3_u8_f32(const uint8_t* x, const float* w, const float* bias, float* y, int B, int H, int W, int act,
-                    float add, float div, hipStream_t s);
+                    const float* lut, hipStream_t s);
 void avgpool_f32(const float* x, float* y, int B, int HW, int C, hipStream_t s);
 
 // fused inverted residual, fp32.  we [hid][KIN] (KIN = ceil8(cin), zero
@@ -97,7 +98,7 @@ size_t ir_block_f32_workspace_bytes(const IrBlockF32Args& a);
 bool ir_expand_dw_f32_supported(int stride, int H, int W, int cin, int hid, int B = 0);
 bool ir_expand_dw_f32(const IrBlockF32Args& a, hipStream_t s);
 
-// stem (3x3/2 conv 3 -> 32 on the uint8 frame, normalised as (x + add) / div,
+// stem (3x3/2 conv 3 -> 32 on the uint8 frame, mapped through lut[256],
 // + ReLU6) fused with an expand-free inverted residual 32 -> 32 -> 16
 // (dw 3x3 + ReLU6, project).  ws [3][3][3][32], bs [32], wd [9][32], bd [32],
 // wp [16][32], bp [16]; y [B][Ho][Wo][16], Ho = (H-1)/2+1.
@@ -111,7 +112,7 @@ struct StemIr1F32Args {
   const float* wp = nullptr;
   const float* bp = nullptr;
   int B = 0, H = 0, W = 0;
-  float add = 0.f, div = 1.f;
+  const float* lut = nullptr;  // [256] f32, device
   // derived
   int Ho = 0, Wo = 0, tiles_x = 0, tiles_y = 0;
 };

@@ -332,8 +332,8 @@ __global__ void __launch_bounds__(256) dw3x3_kernel(const uint16_t* __restrict__
 // --------------------------------------------------------------------- stem ----
 // x: f32 [B][H][W][3]; w: f32 [3][3][3][32] (ky,kx,ci,co); y: bf16 [B][Ho][Wo][32]
 // T = float: the normalised frame; T = uint8_t: the raw RGB frame, normalised on
-// the fly through a 256-entry LUT lut[u] = (u + add) / div (the tensor_transform
-// arithmetic it replaces; padding stays 0 in the normalised domain)
+// the fly through a 256-entry LUT (the tensor_transform arithmetic folded into
+// a table by the filter; padding stays 0 in the normalised domain)
 // MFMA stem: the 3x3/2 conv 3 -> 32 as D[co][px] = W[co][k] . P[px][k]^T with
 // k = (ky, kx, ci) = 27 padded to 32 -- two v_mfma_f32_16x16x32_bf16 per 16
 // output pixels.  A workgroup owns STEM_R output rows of one image: the
@@ -348,7 +348,7 @@ constexpr int STEM_R = 2;
 template <typename T>
 __global__ void __launch_bounds__(256) stem_mfma_kernel(const T* __restrict__ x, const float* __restrict__ w,
                                                         const float* __restrict__ bias, uint16_t* __restrict__ y,
-                                                        int H, int W, int Ho, int Wo, int act, float add, float div) {
+                                                        int H, int W, int Ho, int Wo, int act, const float* __restrict__ lut_g) {
   extern __shared__ __attribute__((aligned(16))) uint16_t xin[];  // [2R+1][(W + 2) * 3] bf16
   __shared__ float lut[256];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -357,7 +357,7 @@ __global__ void __launch_bounds__(256) stem_mfma_kernel(const T* __restrict__ x,
   const int b = blockIdx.x / row_groups;
   const int oy0 = (blockIdx.x % row_groups) * STEM_R;
   const int pitch = (W + 2) * 3;  // columns ix = -1 .. W (both pads)
-  if (sizeof(T) == 1) lut[tid] = (static_cast<float>(tid) + add) / div;
+  if (sizeof(T) == 1) lut[tid] = lut_g[tid];
   // A fragments (weights, rows = output channels) + this lane's bias values
   bf16x8_t a[2];
 #pragma unroll
@@ -557,8 +557,8 @@ void dw3x3(const void* x, const void* w, const float* bias, void* y, int B, int 
 }
 
 template <typename T>
-void stem_launch(const T* x, const float* w, const float* bias, void* y, int B, int H, int W, int act, float add,
-                 float div, hipStream_t s) {
+void stem_launch(const T* x, const float* w, const float* bias, void* y, int B, int H, int W, int act,
+                 const float* lut, hipStream_t s) {
   const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
   const size_t lds = sizeof(uint16_t) * (2 * STEM_R + 1) * (W + 2) * 3;
   const unsigned grid = static_cast<unsigned>(B * ((Ho + STEM_R - 1) / STEM_R));
@@ -568,16 +568,16 @@ void stem_launch(const T* x, const float* w, const float* bias, void* y, int B, 
     if (!ok || lds > 160 * 1024) return;
   }
   hipLaunchKernelGGL(stem_mfma_kernel<T>, dim3(grid), dim3(256), lds, s, x, w, bias, static_cast<uint16_t*>(y), H, W,
-                     Ho, Wo, act, add, div);
+                     Ho, Wo, act, lut);
 }
 
 void stem3x3(const float* x, const float* w, const float* bias, void* y, int B, int H, int W, int act, hipStream_t s) {
-  stem_launch<float>(x, w, bias, y, B, H, W, act, 0.f, 1.f, s);
+  stem_launch<float>(x, w, bias, y, B, H, W, act, nullptr, s);
 }
 
-void stem3x3_u8(const uint8_t* x, const float* w, const float* bias, void* y, int B, int H, int W, int act, float add,
-                float div, hipStream_t s) {
-  stem_launch<uint8_t>(x, w, bias, y, B, H, W, act, add, div, s);
+void stem3x3_u8(const uint8_t* x, const float* w, const float* bias, void* y, int B, int H, int W, int act,
+                const float* lut, hipStream_t s) {
+  stem_launch<uint8_t>(x, w, bias, y, B, H, W, act, lut, s);
 }
 
 void avgpool(const void* x, void* y, int B, int HW, int C, hipStream_t s) {

@@ -351,14 +351,14 @@ __global__ void __launch_bounds__(256) dw3x3_f32_col_kernel(const float* __restr
 // k = 4t + g).  A workgroup owns STEM_R output rows of one image: the
 // 2 * STEM_R + 1 input rows are normalised once into LDS as fp32 (a zero
 // column each side = the conv padding); each lane gathers its 7 patch values
-// per 16-pixel tile from LDS.  T = uint8_t: raw RGB normalised as
-// (x + add) / div (the pipeline's tensor_transform arithmetic, exact fp32).
+// per 16-pixel tile from LDS.  T = uint8_t: raw RGB mapped through the
+// 256-entry input table (the pipeline's tensor_transform arithmetic).
 constexpr int STEM_R = 2;
 
 template <typename T>
 __global__ void __launch_bounds__(256) stem_f32_kernel(const T* __restrict__ x, const float* __restrict__ w,
                                                        const float* __restrict__ bias, float* __restrict__ y, int H,
-                                                       int W, int Ho, int Wo, int act, float add, float div) {
+                                                       int W, int Ho, int Wo, int act, const float* __restrict__ lut) {
   extern __shared__ __attribute__((aligned(16))) float xin[];  // [2R+1][(W + 2) * 3]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, g = lane >> 4;
@@ -385,7 +385,7 @@ __global__ void __launch_bounds__(256) stem_f32_kernel(const T* __restrict__ x, 
     float v = 0.f;
     if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
       const T raw = xb[(static_cast<int64_t>(iy) * W + ix) * 3 + c % 3];
-      v = sizeof(T) == 1 ? (static_cast<float>(raw) + add) / div : static_cast<float>(raw);
+      v = sizeof(T) == 1 ? lut[static_cast<int>(raw)] : static_cast<float>(raw);
     }
     xin[i] = v;
   }
@@ -1018,8 +1018,8 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
 }
 
 // --------------------------------------------------------- stem_ir1_f32 ----
-// The stem (3x3/2 conv 3 -> 32 on the raw uint8 frame, normalised in-kernel
-// as (x + add) / div, + bias, ReLU6) fused with MobileNetV2's first block
+// The stem (3x3/2 conv 3 -> 32 on the raw uint8 frame, mapped in-kernel
+// through the 256-entry input table, + bias, ReLU6) fused with MobileNetV2's first block
 // (t = 1: dw 3x3 on those 32 channels + ReLU6, project 32 -> 16).  The 32-
 // channel stem output -- the largest activation of the network, 205 MB per
 // 128 frames in fp32 -- never leaves LDS.
@@ -1045,7 +1045,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) stem_ir1_f32_kernel(StemIr1F3
   constexpr int NIN = IY * PITCH, NIT = (NIN + NT - 1) / NT;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* xin = smem;                                       // [IY][PITCH] normalised input
-  float* lut = smem + XIN;                                 // [256] (v + add) / div
+  float* lut = smem + XIN;                                 // [256] input table
   f32x4_t* hidw = reinterpret_cast<f32x4_t*>(smem + XIN + 256);  // [2 channel halves][4 quads][PINP]
   f32x4_t* dwo = hidw + 2 * 4 * PINP;                      // [2 channel halves][4 quads][NPX]
 
@@ -1055,10 +1055,10 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) stem_ir1_f32_kernel(StemIr1F3
   const int tiles_img = a.tiles_x * a.tiles_y;
   const int ntiles = tiles_img * a.B;
 
-  // ---- once per workgroup: normalisation table, weights in registers.  The
-  // normalisation (x + add) / div -- the pipeline's tensor_transform arithmetic,
-  // exact fp32 division -- is a 256-entry table.
-  if (tid < 256) lut[tid] = (static_cast<float>(tid) + a.add) / a.div;
+  // ---- once per workgroup: input table, weights in registers.  The table is
+  // the pipeline's tensor_transform arithmetic (computed by the filter in the
+  // transform's own fp32 arithmetic), 256 entries.
+  if (tid < 256) lut[tid] = a.lut[tid];
   float sa[7];  // stem weights of this wave's 16 channels: k = 4t + g (27 taps + 1 zero)
   int off[7];
 #pragma unroll
@@ -1201,7 +1201,7 @@ __global__ void __launch_bounds__(64, 2) stem_ir1w_f32_kernel(StemIr1F32Args a) 
   constexpr int NPT = (TY * TX + 15) / 16;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* xin = smem;                                             // [IY][PITCH] normalised input
-  float* lut = smem + XIN;                                       // [256] (v + add) / div
+  float* lut = smem + XIN;                                       // [256] input table
   f32x4_t* hid = reinterpret_cast<f32x4_t*>(smem + XIN + 256);  // [8 quads][PIN] (32 channels)
 
   const int lane = threadIdx.x;
@@ -1210,7 +1210,7 @@ __global__ void __launch_bounds__(64, 2) stem_ir1w_f32_kernel(StemIr1F32Args a) 
   const int ntiles = tiles_img * a.B;
 
 #pragma unroll
-  for (int i = 0; i < 4; ++i) lut[lane * 4 + i] = (static_cast<float>(lane * 4 + i) + a.add) / a.div;
+  for (int i = 0; i < 4; ++i) lut[lane * 4 + i] = a.lut[lane * 4 + i];
   float sa[2][7];  // stem weights: half h, k = 4t + g (27 taps + 1 zero); A row li = channel 16h + li
   int off[7];
 #pragma unroll
@@ -1651,7 +1651,7 @@ void dw3x3_f32(const float* x, const float* w, const float* bias, float* y, int 
 
 template <typename T>
 static void stem_f32_launch(const T* x, const float* w, const float* bias, float* y, int B, int H, int W, int act,
-                            float add, float div, hipStream_t s) {
+                            const float* lut, hipStream_t s) {
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   const size_t lds = sizeof(float) * (2 * STEM_R + 1) * (W + 2) * 3;
   if (lds > 64 * 1024) {
@@ -1660,17 +1660,17 @@ static void stem_f32_launch(const T* x, const float* w, const float* bias, float
     if (!ok || lds > 160 * 1024) return;
   }
   const unsigned grid = static_cast<unsigned>(B * ((Ho + STEM_R - 1) / STEM_R));
-  hipLaunchKernelGGL(stem_f32_kernel<T>, dim3(grid), dim3(256), lds, s, x, w, bias, y, H, W, Ho, Wo, act, add, div);
+  hipLaunchKernelGGL(stem_f32_kernel<T>, dim3(grid), dim3(256), lds, s, x, w, bias, y, H, W, Ho, Wo, act, lut);
 }
 
 void stem3x3_f32(const float* x, const float* w, const float* bias, float* y, int B, int H, int W, int act,
                  hipStream_t s) {
-  stem_f32_launch<float>(x, w, bias, y, B, H, W, act, 0.f, 1.f, s);
+  stem_f32_launch<float>(x, w, bias, y, B, H, W, act, nullptr, s);
 }
 
 void stem3x3_u8_f32(const uint8_t* x, const float* w, const float* bias, float* y, int B, int H, int W, int act,
-                    float add, float div, hipStream_t s) {
-  stem_f32_launch<uint8_t>(x, w, bias, y, B, H, W, act, add, div, s);
+                    const float* lut, hipStream_t s) {
+  stem_f32_launch<uint8_t>(x, w, bias, y, B, H, W, act, lut, s);
 }
 
 void avgpool_f32(const float* x, float* y, int B, int HW, int C, hipStream_t s) {

@@ -153,8 +153,10 @@ at::Tensor stem_conv_cpu(const at::Tensor& x, const at::Tensor& w, const at::Ten
   return act_ref(v, act).permute({0, 2, 3, 1}).contiguous().to(out_f32 ? at::kFloat : at::kBFloat16);
 }
 
-at::Tensor stem_conv_u8_cuda(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int64_t act, double add,
-                             double div, bool out_f32) {
+at::Tensor stem_conv_u8_cuda(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int64_t act,
+                             const at::Tensor& lut, bool out_f32) {
+  TORCH_CHECK(lut.is_cuda() && lut.scalar_type() == at::kFloat && lut.numel() == 256 && lut.is_contiguous(),
+              "stem_conv_u8: lut [256] f32 on the device");
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kByte && x.is_contiguous() && x.dim() == 4 && x.size(3) == 3,
               "stem_conv_u8: x [B,H,W,3] uint8");
   TORCH_CHECK(w.numel() == 27 * 32 && w.scalar_type() == at::kFloat, "stem_conv_u8: w [3,3,3,32] f32");
@@ -164,18 +166,18 @@ at::Tensor stem_conv_u8_cuda(const at::Tensor& x, const at::Tensor& w, const at:
   if (out_f32) {
     nnsx::kernels::stem3x3_u8_f32(x.data_ptr<uint8_t>(), w.data_ptr<float>(), bias.data_ptr<float>(),
                                   y.data_ptr<float>(), static_cast<int>(B), static_cast<int>(H), static_cast<int>(W),
-                                  static_cast<int>(act), static_cast<float>(add), static_cast<float>(div), cur_stream());
+                                  static_cast<int>(act), lut.data_ptr<float>(), cur_stream());
     return y;
   }
   nnsx::kernels::stem3x3_u8(x.data_ptr<uint8_t>(), w.data_ptr<float>(), bias.data_ptr<float>(), y.data_ptr(),
                             static_cast<int>(B), static_cast<int>(H), static_cast<int>(W), static_cast<int>(act),
-                            static_cast<float>(add), static_cast<float>(div), cur_stream());
+                            lut.data_ptr<float>(), cur_stream());
   return y;
 }
 
-at::Tensor stem_conv_u8_cpu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int64_t act, double add,
-                            double div, bool out_f32) {
-  at::Tensor xf = (x.to(at::kFloat) + static_cast<float>(add)) / static_cast<float>(div);
+at::Tensor stem_conv_u8_cpu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int64_t act,
+                            const at::Tensor& lut, bool out_f32) {
+  at::Tensor xf = lut.to(at::kFloat).index_select(0, x.to(at::kLong).flatten()).view(x.sizes());
   return stem_conv_cpu(xf, w, bias, act, out_f32);
 }
 
@@ -344,7 +346,9 @@ at::Tensor ir_block_cpu(const at::Tensor& x, const at::Tensor& we, const at::Ten
 
 // stem + first (t = 1) block, fused (fp32): uint8 frame -> [B, Ho, Wo, 16]
 at::Tensor stem_ir1_cuda(const at::Tensor& x, const at::Tensor& ws, const at::Tensor& bs, const at::Tensor& wd,
-                         const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, double add, double div) {
+                         const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, const at::Tensor& lut) {
+  TORCH_CHECK(lut.is_cuda() && lut.scalar_type() == at::kFloat && lut.numel() == 256 && lut.is_contiguous(),
+              "stem_ir1: lut [256] f32 on the device");
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kByte && x.is_contiguous() && x.dim() == 4 && x.size(3) == 3,
               "stem_ir1: x [B,H,W,3] uint8");
   for (const auto* t : {&ws, &bs, &wd, &bd, &wp, &bp})
@@ -366,15 +370,14 @@ at::Tensor stem_ir1_cuda(const at::Tensor& x, const at::Tensor& ws, const at::Te
   a.B = static_cast<int>(B);
   a.H = static_cast<int>(H);
   a.W = static_cast<int>(W);
-  a.add = static_cast<float>(add);
-  a.div = static_cast<float>(div);
+  a.lut = lut.data_ptr<float>();
   TORCH_CHECK(nnsx::kernels::stem_ir1_f32(a, cur_stream()), "stem_ir1: launch failed");
   return y;
 }
 
 at::Tensor stem_ir1_cpu(const at::Tensor& x, const at::Tensor& ws, const at::Tensor& bs, const at::Tensor& wd,
-                        const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, double add, double div) {
-  at::Tensor h = stem_conv_u8_cpu(x, ws, bs, 1, add, div, true);
+                        const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, const at::Tensor& lut) {
+  at::Tensor h = stem_conv_u8_cpu(x, ws, bs, 1, lut, true);
   h = dw_conv_cpu(h, wd, bd, 1, 1, 1);
   return pw_conv_cpu(h, wp, bp, c10::nullopt, 16, 0, true);
 }
@@ -396,9 +399,9 @@ TORCH_LIBRARY(nnsx, m) {
   m.def("pw_conv(Tensor x, Tensor wt, Tensor bias, Tensor? res, int N, int act, bool out_f32) -> Tensor");
   m.def("dw_conv(Tensor x, Tensor w, Tensor bias, int stride, int act, int dilation=1) -> Tensor");
   m.def("stem_conv(Tensor x, Tensor w, Tensor bias, int act, bool out_f32=False) -> Tensor");
-  m.def("stem_conv_u8(Tensor x, Tensor w, Tensor bias, int act, float add, float div, bool out_f32=False) -> Tensor");
+  m.def("stem_conv_u8(Tensor x, Tensor w, Tensor bias, int act, Tensor lut, bool out_f32=False) -> Tensor");
   m.def("avgpool(Tensor x) -> Tensor");
-  m.def("stem_ir1(Tensor x, Tensor ws, Tensor bs, Tensor wd, Tensor bd, Tensor wp, Tensor bp, float add, float div) -> Tensor");
+  m.def("stem_ir1(Tensor x, Tensor ws, Tensor bs, Tensor wd, Tensor bd, Tensor wp, Tensor bp, Tensor lut) -> Tensor");
   m.def("pw_conv_f32_tile(Tensor x, Tensor wt, Tensor bias, Tensor? res, int N, int act, int tile) -> Tensor");
   m.def("ir_block(Tensor x, Tensor we, Tensor be, Tensor wd, Tensor bd, Tensor wp, Tensor bp, int stride, int cout, "
         "bool has_expand, bool residual) -> Tensor");

@@ -1,0 +1,56 @@
+// Cross-element fusion at caps negotiation.
+//
+// The reference classification pipeline normalises frames in a separate
+// element: `tensor_converter ! tensor_transform mode=arithmetic
+// option=typecast:float32,add:-127.5,div:127.5 ! tensor_filter ...`
+// (gsttensor_transform.c:1241-1412).  Run as written, that is one more kernel
+// and a 4x larger tensor (uint8 -> float32) between the two elements.  nnsx
+// lets the consumer absorb the transform instead: when the filter's model maps
+// a uint8 input through a 256-entry table (the fused CDNA4 stems do), the
+// filter registers itself as the transform's absorber; at caps negotiation the
+// transform describes its per-element arithmetic, the filter folds it into the
+// model's table (computed in the transform's own fp32 arithmetic, so results
+// are bit-identical) and the transform passes the uint8 frames through.  Any
+// arithmetic the model cannot take (per-channel ops, stand, transpose, other
+// input types) keeps running in the transform's own kernel.
+#pragma once
+
+#include <string>
+#include <vector>
+
+#include "core/types.h"
+#include "kernels/kernels.h"
+
+namespace nnsx {
+
+// The per-element arithmetic an upstream tensor_transform applies to one tensor.
+struct ArithPrefix {
+  unsigned tensor = 0;           // tensor index in the stream
+  DType in_type = DType::END;    // element type entering the transform
+  DType out_type = DType::END;   // element type it produces
+  kernels::ArithParams params;   // add/mul/div chain in order (nops == 0: typecast only)
+};
+
+class TransformAbsorber {
+ public:
+  virtual ~TransformAbsorber() = default;
+  // Called by the transform while it negotiates.  true = the absorber now
+  // applies `p` itself and accepts `p.in_type` data; the transform passes
+  // buffers through unchanged.  `by` names the transform (logs, properties).
+  virtual bool absorb_arith(const ArithPrefix& p, const std::string& by) = 0;
+};
+
+// Implemented by elements whose work a downstream consumer may absorb.
+class AbsorbableElement {
+ public:
+  virtual ~AbsorbableElement() = default;
+  virtual void set_absorber(TransformAbsorber* a) = 0;
+  virtual bool absorbed() const = 0;
+};
+
+// The transform's output for every uint8 value 0..255 (out must be FLOAT32):
+// the table an absorbing model applies.  Computed with the transform's own
+// host arithmetic (tensor_transform.cc), which its device kernel matches.
+bool arith_table_u8(const kernels::ArithParams& p, DType out, std::vector<float>* lut);
+
+}  // namespace nnsx

@@ -82,6 +82,19 @@ class FilterInstance {
   }
   // true when input memories must be on the host (CPU frameworks)
   virtual bool wants_host_input() const { return true; }
+  // Upstream-arithmetic absorption (runtime/fusion.h): true when the model maps
+  // a uint8 input `index` through a 256-entry f32 table it can be given.
+  virtual bool accepts_input_table(unsigned index) const {
+    (void)index;
+    return false;
+  }
+  // Install that table; the input then arrives as uint8 (the caller updates
+  // the negotiated input type).  Must survive a hot reload.
+  virtual bool set_input_table(unsigned index, const std::vector<float>& lut) {
+    (void)index;
+    (void)lut;
+    return false;
+  }
 };
 
 class FilterFramework {

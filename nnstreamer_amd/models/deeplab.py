@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .fused import DW, PW, Block, _fold, stem
+from .fused import DW, PW, Block, _fold, input_lut, stem
 from .mobilenet_v2 import ConvBNReLU, InvertedResidual, MobileNetV2
 
 
@@ -91,7 +91,7 @@ class FusedDeepLabV3(nn.Module):
         w, b = _fold(stem[0], stem[1])
         self.register_buffer("stem_w", w.permute(2, 3, 1, 0).contiguous())
         self.register_buffer("stem_b", b.contiguous())
-        self.in_add, self.in_div = 0.0, 255.0  # uint8 input: the pipeline normalisation, fused
+        self.register_buffer("in_lut", input_lut(0.0, 255.0))  # uint8 input table (absorbable transform)
         blocks = []
         for ir in m.features[1:]:
             blk = Block(ir, precision)
@@ -116,7 +116,7 @@ class FusedDeepLabV3(nn.Module):
         return self
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        h = stem(x, self.stem_w, self.stem_b, self.in_add, self.in_div, self.f32)
+        h = stem(x, self.stem_w, self.stem_b, self.in_lut, self.f32)
         for blk in self.blocks:
             h = blk(h)
         a = self.aspp_conv(h)

@@ -61,13 +61,20 @@ def _pw_weight(w: torch.Tensor, precision: str = "bf16"):
     return out if precision == "fp32" else out.to(torch.bfloat16)
 
 
-def stem(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, in_add: float, in_div: float,
+def input_lut(add: float, div: float) -> torch.Tensor:
+    """256-entry table of a uint8 input: what `tensor_transform mode=arithmetic
+    option=typecast:float32,add:<add>,div:<div>` computes for every byte value,
+    in the transform's own fp32 arithmetic (bit-identical to its kernel)."""
+    v = torch.arange(256, dtype=torch.float32)
+    return (v + torch.tensor(add, dtype=torch.float32)) / torch.tensor(div, dtype=torch.float32)
+
+
+def stem(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, lut: torch.Tensor,
          out_f32: bool = False) -> torch.Tensor:
-    """3x3/2 stem from either the raw uint8 frame (normalised in-kernel as
-    (x + in_add) / in_div, i.e. the pipeline's tensor_transform arithmetic fused
-    into the first conv) or an already-normalised float32 frame."""
+    """3x3/2 stem from either the raw uint8 frame (mapped in-kernel through
+    the 256-entry input table `lut`) or an already-normalised float32 frame."""
     if x.dtype == torch.uint8:
-        return torch.ops.nnsx.stem_conv_u8(x.contiguous(), w, b, 1, in_add, in_div, out_f32)
+        return torch.ops.nnsx.stem_conv_u8(x.contiguous(), w, b, 1, lut, out_f32)
     return torch.ops.nnsx.stem_conv(x.contiguous().float(), w, b, 1, out_f32)
 
 
@@ -207,8 +214,16 @@ class Block(nn.Module):
 
 
 class FusedMobileNetV2(nn.Module):
-    """Input: [B, H, W, 3] uint8 (raw frame, normalised in the stem) or float32
-    NHWC (NNStreamer `3:W:H:B`).  Output: [B, classes] fp32 logits."""
+    """Input: [B, H, W, 3] uint8 (raw frame, mapped through `in_lut` in the
+    stem) or float32 NHWC (NNStreamer `3:W:H:B`).  Output: [B, classes] fp32
+    logits.
+
+    `in_lut` ([256] f32) is the model's uint8 input contract: by default the
+    MobileNetV2 normalisation (x - 127.5) / 127.5.  tensor_filter
+    framework=pytorch rewrites it at caps negotiation when it absorbs an
+    upstream `tensor_transform mode=arithmetic` (the transform then passes the
+    uint8 frames through), so the reference pipeline string runs the fused
+    uint8 stem with the transform's exact arithmetic."""
 
     def __init__(self):
         super().__init__()
@@ -223,7 +238,7 @@ class FusedMobileNetV2(nn.Module):
         w, b = _fold(stem[0], stem[1])  # [32, 3, 3, 3]
         self.register_buffer("stem_w", w.permute(2, 3, 1, 0).contiguous())  # [ky, kx, ci, co]
         self.register_buffer("stem_b", b.contiguous())
-        self.in_add, self.in_div = -127.5, 127.5
+        self.register_buffer("in_lut", input_lut(-127.5, 127.5))
         self.blocks = nn.ModuleList([Block(ir, precision) for ir in m.features[1:-1]])
         # fp32 + uint8 frames: the stem and the first (t = 1, 32 -> 16) block run as
         # one kernel (stem_ir1), the 32-channel stem output never leaves LDS
@@ -245,10 +260,10 @@ class FusedMobileNetV2(nn.Module):
         start = 0
         if self.stem_ir1 and x.dtype == torch.uint8 and x.is_cuda:
             h = torch.ops.nnsx.stem_ir1(x.contiguous(), self.stem_w, self.stem_b, self.s1_wd, self.s1_bd, self.s1_wp,
-                                        self.s1_bp, self.in_add, self.in_div)
+                                        self.s1_bp, self.in_lut)
             start = 1
         else:
-            h = stem(x, self.stem_w, self.stem_b, self.in_add, self.in_div, self.f32)
+            h = stem(x, self.stem_w, self.stem_b, self.in_lut, self.f32)
         i = 0
         for blk in self.blocks:
             if i >= start:

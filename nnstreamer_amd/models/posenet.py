@@ -14,7 +14,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from .fused import DW, PW, _fold, stem
+from .fused import DW, PW, _fold, input_lut, stem
 from .mobilenet_v2 import ConvBNReLU
 
 # (out channels, stride) of the 13 depthwise-separable blocks of MobileNetV1
@@ -97,7 +97,7 @@ class FusedPoseNet(nn.Module):
         w, b = _fold(stem[0], stem[1])
         self.register_buffer("stem_w", w.permute(2, 3, 1, 0).contiguous())
         self.register_buffer("stem_b", b.contiguous())
-        self.in_add, self.in_div = -127.5, 127.5  # uint8 input: the pipeline normalisation, fused
+        self.register_buffer("in_lut", input_lut(-127.5, 127.5))  # uint8 input table (absorbable transform)
         dws, pws = [], []
         layers = list(m.backbone)[1:]
         for i in range(0, len(layers), 2):
@@ -113,7 +113,7 @@ class FusedPoseNet(nn.Module):
         return self
 
     def forward(self, x: torch.Tensor):
-        h = stem(x, self.stem_w, self.stem_b, self.in_add, self.in_div, self.f32)
+        h = stem(x, self.stem_w, self.stem_b, self.in_lut, self.f32)
         for d, p in zip(self.dws, self.pws):
             h = p(d(h))
         hm = self.heat(h)[..., : self.k].contiguous()

@@ -20,7 +20,7 @@ from typing import List, Tuple
 import torch
 import torch.nn as nn
 
-from .fused import DW, PW, Block, _fold, stem
+from .fused import DW, PW, Block, _fold, input_lut, stem
 from .mobilenet_v2 import ConvBNReLU, MobileNetV2
 
 ANCHORS = (3, 6, 6, 6, 6, 6)
@@ -166,7 +166,7 @@ class FusedSSDLite(nn.Module):
         w, b = _fold(stem[0], stem[1])
         self.register_buffer("stem_w", w.permute(2, 3, 1, 0).contiguous())
         self.register_buffer("stem_b", b.contiguous())
-        self.in_add, self.in_div = -127.5, 127.5  # uint8 input: the pipeline normalisation, fused
+        self.register_buffer("in_lut", input_lut(-127.5, 127.5))  # uint8 input table (absorbable transform)
         self.blocks = nn.ModuleList([Block(ir, precision) for ir in m.features[1:-1]])  # features[1..17]
         head: ConvBNReLU = m.features[-1]
         self.head = PW(*_fold(head[0], head[1]), act=1, precision=precision)
@@ -177,7 +177,7 @@ class FusedSSDLite(nn.Module):
         return self
 
     def forward(self, x: torch.Tensor):
-        h = stem(x, self.stem_w, self.stem_b, self.in_add, self.in_div, self.f32)
+        h = stem(x, self.stem_w, self.stem_b, self.in_lut, self.f32)
         feats: List[torch.Tensor] = []
         for i, blk in enumerate(self.blocks):
             if i == self.feat_block:

@@ -13,8 +13,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 import nnstreamer_amd  # noqa: F401,E402
+from nnstreamer_amd.models.fused import input_lut  # noqa: E402
 
 PEAK = 157.3e12
+LUT = input_lut(-127.5, 127.5).cuda() if torch.cuda.is_available() else None
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 128
 SHAPES = [(112, 32, 32, 16, 1), (112, 16, 96, 24, 2), (56, 24, 144, 24, 1), (56, 24, 144, 32, 2),
           (28, 32, 192, 32, 1), (28, 32, 192, 32, 1), (28, 32, 192, 64, 2), (14, 64, 384, 64, 1),
@@ -45,7 +47,7 @@ if ONLY == "stem":  # only the fused stem + block 1 (for rocprof)
     xu = torch.randint(0, 256, (B, 224, 224, 3), device="cuda", dtype=torch.uint8)
     w = [torch.randn(3, 3, 3, 32, device="cuda"), torch.zeros(32, device="cuda"), torch.randn(9, 32, device="cuda"),
          torch.zeros(32, device="cuda"), torch.randn(16, 32, device="cuda") * 0.1, torch.zeros(16, device="cuda")]
-    us1 = timeit(lambda: torch.ops.nnsx.stem_ir1(xu, *w, -127.5, 127.5))
+    us1 = timeit(lambda: torch.ops.nnsx.stem_ir1(xu, *w, LUT))
     print(f"stem+block1 fused {us1:.1f} us at batch {B}")
     sys.exit(0)
 if ONLY:
@@ -95,14 +97,14 @@ if not ONLY:
     xu = torch.randint(0, 256, (B, 224, 224, 3), device="cuda", dtype=torch.uint8)
     ws = torch.randn(3, 3, 3, 32, device="cuda")
     bs = torch.zeros(32, device="cuda")
-    us = timeit(lambda: torch.ops.nnsx.stem_conv_u8(xu, ws, bs, 1, -127.5, 127.5, True))
+    us = timeit(lambda: torch.ops.nnsx.stem_conv_u8(xu, ws, bs, 1, LUT, True))
     total += us
     row("stem 224 u8 -> 32", us, 2 * B * 112 * 112 * 32 * 27)
     wd1 = torch.randn(9, 32, device="cuda")
     bd1 = torch.zeros(32, device="cuda")
     wp1 = torch.randn(16, 32, device="cuda") * 0.1
     bp1 = torch.zeros(16, device="cuda")
-    us1 = timeit(lambda: torch.ops.nnsx.stem_ir1(xu, ws, bs, wd1, bd1, wp1, bp1, -127.5, 127.5))
+    us1 = timeit(lambda: torch.ops.nnsx.stem_ir1(xu, ws, bs, wd1, bd1, wp1, bp1, LUT))
     row("stem+block1 fused (replaces both)", us1,
         2 * B * 112 * 112 * (32 * 27 + 32 * 9 + 32 * 16))
     print(f"  fused saves {us + seen[(112, 32, 32, 16, 1)] - us1:.1f} us")

@@ -3,6 +3,8 @@ import pytest
 import torch
 import torch.nn.functional as F
 
+from nnstreamer_amd.models.fused import input_lut
+
 pytestmark = pytest.mark.gpu
 
 
@@ -161,7 +163,7 @@ def test_stem_u8_matches_float_path(nns):
     x = torch.randint(0, 256, (3, 224, 224, 3), device="cuda", dtype=torch.uint8)
     w = torch.randn(3, 3, 3, 32, device="cuda") * 0.2
     b = torch.randn(32, device="cuda") * 0.1
-    y8 = torch.ops.nnsx.stem_conv_u8(x, w, b, 1, -127.5, 127.5)
+    y8 = torch.ops.nnsx.stem_conv_u8(x, w, b, 1, input_lut(-127.5, 127.5).cuda())
     xf = (x.float() + -127.5) / 127.5
     yf = torch.ops.nnsx.stem_conv(xf.contiguous(), w, b, 1)
     # torch's scalar division may round the normalised input 1 ulp differently from the

@@ -6,6 +6,8 @@ import pytest
 import torch
 import torch.nn.functional as F
 
+from nnstreamer_amd.models.fused import input_lut
+
 pytestmark = pytest.mark.gpu
 
 
@@ -68,7 +70,7 @@ def test_stem_f32_u8_and_pool(nns, H, W):
     x = torch.randint(0, 256, (2, H, W, 3), device="cuda", dtype=torch.uint8)
     w = torch.randn(3, 3, 3, 32, device="cuda") * 0.3
     b = torch.randn(32, device="cuda")
-    y = torch.ops.nnsx.stem_conv_u8(x, w, b, 1, -127.5, 127.5, True)
+    y = torch.ops.nnsx.stem_conv_u8(x, w, b, 1, input_lut(-127.5, 127.5).cuda(), True)
     assert y.dtype == torch.float32
     xf = (x.double().cpu() - 127.5) / 127.5
     ref = F.conv2d(xf.permute(0, 3, 1, 2), w.double().cpu().permute(3, 2, 0, 1), b.double().cpu(), stride=2,
@@ -91,7 +93,7 @@ def test_stem_ir1_f32(nns, H, W, B):
     bd = torch.randn(32, device="cuda") * 0.1
     wp = torch.randn(16, 32, device="cuda") / 32 ** 0.5
     bp = torch.randn(16, device="cuda") * 0.1
-    y = torch.ops.nnsx.stem_ir1(x, ws, bs, wd, bd, wp, bp, -127.5, 127.5)
+    y = torch.ops.nnsx.stem_ir1(x, ws, bs, wd, bd, wp, bp, input_lut(-127.5, 127.5).cuda())
     assert y.shape == (B, (H - 1) // 2 + 1, (W - 1) // 2 + 1, 16) and y.dtype == torch.float32
     xf = (x.double().cpu() - 127.5) / 127.5
     h = F.conv2d(xf.permute(0, 3, 1, 2), ws.double().cpu().permute(3, 2, 0, 1), bs.double().cpu(), stride=2,
@@ -330,3 +332,59 @@ def test_filter_device_stats(nns, workdir, labels):
     assert all(b >= a for a, b in zip(ends, ends[1:])), ends
     assert all(0 < s[1] < 1e9 for s in stamps), stamps
     assert lat > 0 and thr > 0
+
+
+def _ref_string_labels(nns, model, labels, B, absorb):
+    """bench.py's reference string at batch B: uint8 frames -> tensor_transform
+    (normalisation) -> tensor_filter (fused fp32, hipGraph) -> image_labeling.
+    Returns (labels per frame, frames, absorbed-by)."""
+    desc = (f"videotestsrc num-buffers={B} pattern=snow pool-size={B} "
+            "! video/x-raw,format=RGB,width=224,height=224,framerate=0/1 "
+            f"! tee name=t t. ! queue ! tensor_converter frames-per-tensor={B} device=0 "
+            "! tensor_transform name=norm mode=arithmetic option=typecast:float32,add:-127.5,div:127.5 "
+            f"! queue max-size-buffers=2 ! tensor_filter name=f framework=pytorch model={model} "
+            f"input=3:224:224:{B} inputtype=float32 absorb-transform={'true' if absorb else 'false'} "
+            "accelerator=true:gpu device=0 custom=hipgraph:true ! queue max-size-buffers=4 "
+            f"! tensor_decoder mode=image_labeling option1={labels} ! tensor_sink name=sink "
+            f"t. ! queue ! tensor_converter frames-per-tensor={B} ! appsink name=raw")
+    p = nns.parse_launch(desc)
+    out = []
+    p.get_by_name("sink").connect("new-data", lambda b: out.append(b.memory(0).bytes().decode()))
+    raw = p.get_by_name("raw")
+    p.set_state("playing")
+    b = raw.pull(timeout=120)
+    assert b is not None
+    frames = b.memory(0).numpy("uint8").copy()
+    p.wait(timeout=300)
+    absorbed = p.get_by_name("norm").get_property("absorbed-by")
+    p.stop()
+    assert len(out) == 1
+    return out[0].split("\n"), frames, absorbed
+
+
+def test_reference_string_absorbed_at_bench_batch(nns, workdir, labels):
+    """The reference pipeline string at the benched batch (512): the filter
+    absorbs the tensor_transform into the fused stem's input table; labels
+    equal the same string with the transform's own kernel (float32 frames into
+    the unfused stem path) and torch.argmax of the plain fp32 model."""
+    import os
+
+    from nnstreamer_amd.models.export import export
+    from nnstreamer_amd.models.mobilenet_v2 import mobilenet_v2
+
+    model = export("mobilenet_v2_fused_fp32", os.path.join(workdir, "mbv2_f32_refstr.pt"), layout="nhwc")
+    B = 512
+    got, frames, absorbed = _ref_string_labels(nns, model, labels, B, True)
+    assert absorbed == "f"
+    got_k, frames_k, absorbed_k = _ref_string_labels(nns, model, labels, B, False)
+    assert absorbed_k == ""
+    assert np.array_equal(frames, frames_k)  # snow is seeded: the same 512 frames
+    m = mobilenet_v2(seed=0).cuda().eval()
+    x = torch.from_numpy(frames).cuda().view(B, 224, 224, 3).float()
+    with torch.no_grad():
+        ref = m(((x - 127.5) / 127.5).permute(0, 3, 1, 2)).argmax(1).tolist()
+    ref = [f"class_{i}" for i in ref]
+    same = sum(a == b for a, b in zip(got, got_k))
+    agree = sum(a == b for a, b in zip(got, ref))
+    assert same >= B - 2, (same, B)       # two fp32 kernel paths: ties may flip at most a frame or two
+    assert agree >= 0.995 * B, (agree, B)
