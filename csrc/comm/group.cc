@@ -298,6 +298,10 @@ void Mesh::reader(std::shared_ptr<Connection> c) {
   if (!c->recv(&hello, timeout_ms_, nullptr) || hello.type != MsgType::HELLO) return;
   const int src = static_cast<int>(hello.client_id);
   if (src < 0 || src >= n_) return;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    lost_[static_cast<size_t>(src)] = 0;  // (re)connected
+  }
   while (true) {
     Message m;
     if (!c->recv(&m, -1, nullptr)) {
@@ -366,11 +370,31 @@ bool Mesh::recv(uint64_t tag, int src, Message* m, int* from, int timeout_ms, bo
       if (err) *err = "mesh: closed";
       return false;
     }
-    for (int r = 0; r < n_; ++r)
-      if (lost_[static_cast<size_t>(r)] && (src < 0 || src == r)) {
-        if (err) *err = strfmt("lost the link to member ", r);
+    if (src >= 0) {
+      if (lost_[static_cast<size_t>(src)]) {
+        if (err) *err = strfmt("lost the link to member ", src);
         return false;
       }
+    } else {
+      // any-source: one member's broken link must not stop the traffic of the
+      // live ones (a query server keeps serving its other clients).  The loss
+      // is reported once per member; the receive fails only when no other
+      // member is left that could still send.
+      int alive = 0;
+      for (int r = 0; r < n_; ++r) {
+        if (r == grank_) continue;
+        if (!lost_[static_cast<size_t>(r)]) {
+          ++alive;
+        } else if (lost_[static_cast<size_t>(r)] == 1) {
+          lost_[static_cast<size_t>(r)] = 2;  // reported
+          NNSX_LOGW("mesh", "lost the link to member ", r, " (any-source receives continue with the others)");
+        }
+      }
+      if (alive == 0 && n_ > 1) {
+        if (err) *err = "mesh: lost the links to every other member";
+        return false;
+      }
+    }
     if (timeout_ms < 0) {
       cv_.wait(lk);
     } else if (cv_.wait_until(lk, deadline) == std::cv_status::timeout) {

@@ -116,7 +116,7 @@ class Mesh {
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<Item> inbox_;
-  std::vector<int> lost_;  // per member: 1 = its link broke without a goodbye
+  std::vector<int> lost_;  // per member: 1 = its link broke without a goodbye, 2 = that was reported
   std::atomic<bool> closed_{false};
 };
 

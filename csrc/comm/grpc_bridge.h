@@ -23,6 +23,9 @@ struct GrpcOptions {
   std::string host = "localhost";
   int port = 55115;  // 0: ephemeral (server), read back with port()
   bool blocking = true;
+  // largest gRPC message accepted (gRPC's default receive limit is 4 MiB;
+  // < 0 = unlimited); a larger one ends its call with RESOURCE_EXHAUSTED
+  int64_t max_recv_bytes = 4 << 20;
 };
 
 class GrpcEndpoint {

@@ -45,6 +45,15 @@ constexpr uint8_t F_END_STREAM = 0x1, F_ACK = 0x1, F_END_HEADERS = 0x4, F_PADDED
 constexpr char kPreface[] = "PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n";
 constexpr size_t kPrefaceLen = 24;
 constexpr uint32_t kOurMaxFrame = 1 << 20;  // what we accept (SETTINGS_MAX_FRAME_SIZE)
+constexpr uint32_t kMaxHeaderList = 64 << 10;  // SETTINGS_MAX_HEADER_LIST_SIZE: a header block larger than this
+                                               // (HEADERS + CONTINUATION) ends the connection
+constexpr uint32_t kMaxStreams = 128;          // SETTINGS_MAX_CONCURRENT_STREAMS (peer-opened)
+// google.protobuf.Empty / nnstreamer.flatbuf.Empty as serialized messages: protobuf
+// encodes an empty message as 0 bytes; flatbuffers' builder emits a finished
+// buffer for the empty root table (root uoffset 8, vtable {4, 4}, soffset 4),
+// what CreateEmpty + Finish produce in the reference (nnstreamer_grpc_flatbuf.cc
+// :269-276, :397-402) and what its verifier expects
+const std::string kFlatbufEmpty("\x08\x00\x00\x00\x04\x00\x04\x00\x04\x00\x00\x00", 12);
 constexpr int64_t kOurWindow = (1u << 30);  // stream + connection receive windows we advertise
 
 bool write_all(int fd, const void* p, size_t n) {
@@ -102,9 +111,13 @@ class H2Conn {
     virtual void on_message(H2Conn* c, uint32_t sid, std::string&& msg) = 0;
     virtual void on_end(H2Conn* c, uint32_t sid) = 0;  // peer half-closed (END_STREAM) or reset
     virtual void on_closed(H2Conn* c) = 0;
+    // a message whose gRPC length prefix exceeds the receive limit: its stream
+    // no longer delivers data (the endpoint ends the call)
+    virtual void on_oversize(H2Conn* c, uint32_t sid, uint64_t bytes) = 0;
   };
 
-  H2Conn(int fd, bool server, Events* ev) : fd_(fd), server_(server), ev_(ev) {
+  H2Conn(int fd, bool server, Events* ev, int64_t max_msg)
+      : fd_(fd), server_(server), ev_(ev), max_msg_(max_msg) {
     int one = 1;
     (void)setsockopt(fd_, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
   }
@@ -128,6 +141,8 @@ class H2Conn {
     setting(0x2, 0);  // ENABLE_PUSH
     setting(0x4, static_cast<uint32_t>(kOurWindow));  // INITIAL_WINDOW_SIZE
     setting(0x5, kOurMaxFrame);  // MAX_FRAME_SIZE
+    setting(0x6, kMaxHeaderList);  // MAX_HEADER_LIST_SIZE
+    if (server_) setting(0x3, kMaxStreams);  // MAX_CONCURRENT_STREAMS
     append_frame(&out, SETTINGS, 0, 0, s);
     std::string wu;
     put32(&wu, static_cast<uint32_t>(kOurWindow - 65535));
@@ -232,10 +247,10 @@ class H2Conn {
     (void)write_all(fd_, out.data(), out.size());
   }
 
-  void goaway() {
+  void goaway(uint32_t code = 0) {
     std::string p, out;
     put32(&p, last_peer_sid_.load());
-    put32(&p, 0);  // NO_ERROR
+    put32(&p, code);  // NO_ERROR unless given
     append_frame(&out, GOAWAY, 0, 0, p);
     std::lock_guard<std::mutex> lk(wmu_);
     (void)write_all(fd_, out.data(), out.size());
@@ -244,6 +259,16 @@ class H2Conn {
   void forget(uint32_t sid) {
     std::lock_guard<std::mutex> lk(mu_);
     streams_.erase(sid);
+    cv_.notify_all();
+  }
+  bool is_reset(uint32_t sid) {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = streams_.find(sid);
+    return it != streams_.end() && it->second.reset;
+  }
+  size_t stream_count() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return streams_.size();
   }
 
  private:
@@ -251,6 +276,7 @@ class H2Conn {
     int64_t send_window = 65535;
     int64_t window_delta = 0;  // SETTINGS changes before the stream opened on our side
     bool opened = false, reset = false;
+    bool discard = false;  // an oversize message was refused: drop the rest of the stream's data
     std::string rx;  // gRPC message reassembly
   };
 
@@ -322,25 +348,41 @@ class H2Conn {
       }
       switch (type) {
         case DATA: {
-          credit(sid, len);
-          std::vector<std::string> msgs;
           bool end = (flags & F_END_STREAM) != 0;
+          std::vector<std::string> msgs;
+          uint64_t oversize = 0;
+          bool known = false;
           {
             std::lock_guard<std::mutex> lk(mu_);
-            auto& st = streams_[sid];
-            st.rx.append(reinterpret_cast<const char*>(p), n);
-            size_t off = 0;
-            while (st.rx.size() - off >= 5) {
-              const uint32_t ml = be32(reinterpret_cast<const uint8_t*>(st.rx.data()) + off + 1);
-              if (st.rx.size() - off - 5 < ml) break;
-              if (st.rx[off] != 0) NNSX_LOGW("grpc", "compressed gRPC message (no codec negotiated) passed through");
-              msgs.emplace_back(st.rx.substr(off + 5, ml));
-              off += 5 + ml;
+            auto it = streams_.find(sid);
+            // data for a stream that was never opened (or already ended): flow
+            // control is still credited, nothing is buffered
+            known = it != streams_.end() && !it->second.reset;
+            if (known && !it->second.discard) {
+              Stream& st = it->second;
+              st.rx.append(reinterpret_cast<const char*>(p), n);
+              size_t off = 0;
+              while (st.rx.size() - off >= 5) {
+                const uint32_t ml = be32(reinterpret_cast<const uint8_t*>(st.rx.data()) + off + 1);
+                if (max_msg_ >= 0 && ml > static_cast<uint64_t>(max_msg_)) {  // refused before buffering it
+                  oversize = ml;
+                  st.discard = true;
+                  st.rx.clear();
+                  off = 0;
+                  break;
+                }
+                if (st.rx.size() - off - 5 < ml) break;
+                if (st.rx[off] != 0) NNSX_LOGW("grpc", "compressed gRPC message (no codec negotiated) passed through");
+                msgs.emplace_back(st.rx.substr(off + 5, ml));
+                off += 5 + ml;
+              }
+              st.rx.erase(0, off);
             }
-            st.rx.erase(0, off);
           }
+          credit(known ? sid : 0, len);
           for (auto& m : msgs) ev_->on_message(this, sid, std::move(m));
-          if (end) ev_->on_end(this, sid);
+          if (oversize) ev_->on_oversize(this, sid, oversize);
+          if (known && end) ev_->on_end(this, sid);
           break;
         }
         case HEADERS:
@@ -357,6 +399,12 @@ class H2Conn {
             ok = false;
             break;
           }
+          if (block.size() + n > kMaxHeaderList) {  // unbounded CONTINUATION chains end here
+            NNSX_LOGW("grpc", "header block above ", kMaxHeaderList, " bytes: closing the connection");
+            goaway(0xb);  // ENHANCE_YOUR_CALM
+            ok = false;
+            break;
+          }
           block.append(reinterpret_cast<const char*>(p), n);
           if (flags & F_END_HEADERS) {
             hpack::Headers hs;
@@ -366,13 +414,23 @@ class H2Conn {
               ok = false;
               break;
             }
+            bool refuse = false, fresh = false;
             {
               std::lock_guard<std::mutex> lk(mu_);
-              auto& st = streams_[block_sid];
-              if (!st.opened) {
-                st.opened = true;
-                st.send_window = peer_init_window_ + st.window_delta;
+              fresh = streams_.find(block_sid) == streams_.end();
+              if (fresh && server_ && streams_.size() >= kMaxStreams) {
+                refuse = true;
+              } else {
+                auto& st = streams_[block_sid];
+                if (!st.opened) {
+                  st.opened = true;
+                  st.send_window = peer_init_window_ + st.window_delta;
+                }
               }
+            }
+            if (refuse) {
+              send_rst(block_sid, 0x7);  // REFUSED_STREAM
+              break;
             }
             ev_->on_headers(this, block_sid, std::move(hs), block_end_stream);
             if (block_end_stream) ev_->on_end(this, block_sid);
@@ -409,20 +467,25 @@ class H2Conn {
           if (sid == 0) {
             conn_send_window_ += inc;
           } else {
-            auto& st = streams_[sid];
-            if (st.opened) st.send_window += inc;
-            else st.window_delta += inc;
+            auto it = streams_.find(sid);  // (never opened / already ended: ignored)
+            if (it != streams_.end()) {
+              if (it->second.opened) it->second.send_window += inc;
+              else it->second.window_delta += inc;
+            }
           }
           cv_.notify_all();
           break;
         }
         case RST_STREAM: {
+          bool known;
           {
             std::lock_guard<std::mutex> lk(mu_);
-            streams_[sid].reset = true;
+            auto it = streams_.find(sid);
+            known = it != streams_.end();
+            if (known) it->second.reset = true;  // erased by the endpoint (forget) once it is done with it
             cv_.notify_all();
           }
-          ev_->on_end(this, sid);
+          if (known) ev_->on_end(this, sid);
           break;
         }
         case GOAWAY:
@@ -439,6 +502,7 @@ class H2Conn {
   int fd_;
   bool server_;
   Events* ev_;
+  int64_t max_msg_;
   std::thread reader_;
   std::mutex wmu_;  // frame writes
   std::mutex mu_;   // streams + windows
@@ -463,6 +527,7 @@ class NativeGrpcEndpoint : public GrpcEndpoint, public H2Conn::Events {
     std::string idl = o.idl;
     for (auto& c : idl) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
     service_ = "/nnstreamer." + idl + ".TensorService/";
+    empty_ = idl == "flatbuf" ? kFlatbufEmpty : std::string();
   }
   ~NativeGrpcEndpoint() override { stop(); }
 
@@ -580,6 +645,31 @@ class NativeGrpcEndpoint : public GrpcEndpoint, public H2Conn::Events {
     t.emplace_back("grpc-message", "method not served by this tensor_" + std::string(o_.sending ? "sink" : "src") +
                                        "_grpc: " + (path ? *path : std::string("?")));
     c->send_headers(sid, t, true);
+    c->forget(sid);
+  }
+
+  void on_oversize(H2Conn* c, uint32_t sid, uint64_t bytes) override {
+    const std::string msg = "Received message larger than max (" + std::to_string(bytes) + " vs. " +
+                            std::to_string(o_.max_recv_bytes) + ")";
+    NNSX_LOGW("grpc", msg);
+    if (!o_.server) {  // our call's incoming stream: give up on it
+      failed_.store(true);
+      c->send_rst(sid, 0x8);  // CANCEL
+      std::lock_guard<std::mutex> lk(mu_);
+      finished_ = true;
+      cv_.notify_all();
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      calls_.erase({c, sid});
+    }
+    hpack::Headers t = response_headers();
+    t.emplace_back("grpc-status", "8");  // RESOURCE_EXHAUSTED
+    t.emplace_back("grpc-message", msg);
+    c->send_headers(sid, t, true);
+    c->send_rst(sid, 0x0);  // NO_ERROR: the rest of the request is not read
+    c->forget(sid);
   }
 
   void on_message(H2Conn* c, uint32_t sid, std::string&& m) override {
@@ -613,14 +703,24 @@ class NativeGrpcEndpoint : public GrpcEndpoint, public H2Conn::Events {
       if (kind == Call::SEND) calls_.erase(it);
     }
     if (kind == Call::SEND) {
-      // client finished its stream: reply google.protobuf.Empty + OK status
-      if (c->send_headers(sid, response_headers(), false) && c->send_message(sid, "", false)) {
+      // client finished its stream: reply Empty (per IDL) + OK status
+      if (c->send_headers(sid, response_headers(), false) && c->send_message(sid, empty_, false)) {
         hpack::Headers t{{"grpc-status", "0"}};
         c->send_headers(sid, t, true);
       }
       c->forget(sid);
+      return;
     }
     // RecvTensors: the client half-closed after its request; keep streaming
+    // unless it reset the stream
+    if (c->is_reset(sid)) {
+      drop_sub(c, sid);
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        calls_.erase({c, sid});
+      }
+      c->forget(sid);
+    }
   }
 
   void on_closed(H2Conn* c) override {
@@ -655,12 +755,14 @@ class NativeGrpcEndpoint : public GrpcEndpoint, public H2Conn::Events {
         subs_.erase(it);
         break;
       }
+    calls_.erase({c, sid});
   }
 
   void finish_call(H2Conn* c, uint32_t sid, int status, const std::string& msg) {
     hpack::Headers t{{"grpc-status", std::to_string(status)}};
     if (!msg.empty()) t.emplace_back("grpc-message", msg);
     c->send_headers(sid, t, true);
+    c->forget(sid);
   }
 
   bool start_server(std::string* err) {
@@ -703,7 +805,7 @@ class NativeGrpcEndpoint : public GrpcEndpoint, public H2Conn::Events {
       if (r <= 0 || !(pf.revents & POLLIN)) continue;
       const int cfd = ::accept4(lfd_, nullptr, nullptr, SOCK_CLOEXEC);
       if (cfd < 0) continue;
-      auto conn = std::make_shared<H2Conn>(cfd, true, this);
+      auto conn = std::make_shared<H2Conn>(cfd, true, this, o_.max_recv_bytes);
       {
         std::lock_guard<std::mutex> lk(mu_);
         conns_.push_back(conn);
@@ -751,7 +853,7 @@ class NativeGrpcEndpoint : public GrpcEndpoint, public H2Conn::Events {
       *err = "cannot connect to " + host + ":" + port;
       return false;
     }
-    conn_ = std::make_shared<H2Conn>(fd, false, this);
+    conn_ = std::make_shared<H2Conn>(fd, false, this, o_.max_recv_bytes);
     if (!conn_->start()) {
       *err = "HTTP/2 handshake failed";
       return false;
@@ -768,8 +870,8 @@ class NativeGrpcEndpoint : public GrpcEndpoint, public H2Conn::Events {
       *err = "cannot open the call";
       return false;
     }
-    // RecvTensors: the google.protobuf.Empty request, then half-close
-    if (!o_.sending && !conn_->send_message(sid_, "", true)) {
+    // RecvTensors: the Empty request (per IDL), then half-close
+    if (!o_.sending && !conn_->send_message(sid_, empty_, true)) {
       *err = "cannot send the RecvTensors request";
       return false;
     }
@@ -778,6 +880,7 @@ class NativeGrpcEndpoint : public GrpcEndpoint, public H2Conn::Events {
 
   GrpcOptions o_;
   std::string service_;
+  std::string empty_;  // the IDL's serialized Empty message
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<std::string> q_;

@@ -62,6 +62,15 @@ class GrpcElement : public Base {
     p.get = [this] { return std::to_string(ep_ && opt_.server ? ep_->port() : opt_.port); };
     this->add_prop(p);
     this->prop_readonly("out", [this] { return std::to_string(out_.load()); }, "The number of buffers sent / received");
+    PropSpec m;
+    m.name = "max-recv-message-size";
+    m.type = PropType::INT64;
+    m.blurb = "nnsx: largest gRPC message accepted in bytes (gRPC's default 4 MiB; -1 = unlimited); a larger one "
+              "ends its call with RESOURCE_EXHAUSTED";
+    m.default_value = std::to_string(4 << 20);
+    m.set = [this](const std::string& v) { opt_.max_recv_bytes = to_int(v); };
+    m.get = [this] { return std::to_string(opt_.max_recv_bytes); };
+    this->add_prop(m);
   }
 
   comm::GrpcOptions opt_;

@@ -232,3 +232,126 @@ def test_large_messages_respect_flow_control(nns):
         time.sleep(0.02)
     srv.stop()
     assert got == frames
+
+
+# ------------------------------------------------------------- ADVICE r2 ----
+FB_SERVICE = "nnstreamer.flatbuf.TensorService"
+# flatbuffers FlatBufferBuilder: CreateEmpty(b) + b.Finish() for a table with no
+# fields (root uoffset 8 | vtable {size 4, object 4} | soffset 4) -- the message the
+# reference's flatbuf peers send and verify (nnstreamer_grpc_flatbuf.cc:269-276,397-402)
+FB_EMPTY = bytes.fromhex("08000000" "04000400" "04000000")
+
+
+def test_flatbuf_empty_request_bytes(nns):
+    """idl=flatbuf RecvTensors client sends a finished empty flatbuffer, not 0 bytes."""
+    got = []
+    done = threading.Event()
+
+    def recv(req, ctx):
+        got.append(req)
+        done.set()
+        return iter(())
+
+    srv = grpc.server(futures.ThreadPoolExecutor(max_workers=2))
+    srv.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(FB_SERVICE, {
+        "RecvTensors": grpc.unary_stream_rpc_method_handler(recv, request_deserializer=_ident,
+                                                            response_serializer=_ident)}),))
+    port = srv.add_insecure_port("127.0.0.1:0")
+    srv.start()
+    try:
+        p = nns.parse_launch(f"tensor_src_grpc idl=flatbuf server=false host=127.0.0.1 port={port} ! {CAPS} "
+                             "! tensor_sink name=sink")
+        p.set_state("playing")
+        assert done.wait(10)
+        p.wait(10)
+        p.stop()
+    finally:
+        srv.stop(grace=0.2)
+    assert got == [FB_EMPTY]
+
+
+def test_flatbuf_empty_reply_bytes(nns):
+    """idl=flatbuf SendTensors server replies with the finished empty flatbuffer."""
+    srv = nns.parse_launch(f"tensor_src_grpc name=gs idl=flatbuf server=true port=0 ! {CAPS} ! fakesink")
+    srv.set_state("playing")
+    port = _wait_port(srv.get_by_name("gs"))
+    try:
+        with grpc.insecure_channel(f"127.0.0.1:{port}") as ch:
+            call = ch.stream_unary(f"/{FB_SERVICE}/SendTensors", request_serializer=_ident,
+                                   response_deserializer=_ident)
+            assert call(iter(()), timeout=10) == FB_EMPTY
+    finally:
+        srv.stop()
+
+
+def test_oversize_message_resource_exhausted(nns):
+    """A message above max-recv-message-size ends the call with RESOURCE_EXHAUSTED
+    before it is buffered; the server keeps serving new calls."""
+    srv = nns.parse_launch(f"tensor_src_grpc name=gs server=true port=0 max-recv-message-size=65536 ! {CAPS} "
+                           "! tensor_sink name=sink")
+    got = []
+    srv.get_by_name("sink").connect("new-data", lambda b: got.append(b.memory(0).bytes()))
+    srv.set_state("playing")
+    port = _wait_port(srv.get_by_name("gs"))
+    msgs = _messages_via_native(nns, _frames(1))
+    try:
+        with grpc.insecure_channel(f"127.0.0.1:{port}",
+                                   options=[("grpc.max_send_message_length", -1)]) as ch:
+            call = ch.stream_unary(f"/{SERVICE}/SendTensors", request_serializer=_ident, response_deserializer=_ident)
+            with pytest.raises(grpc.RpcError) as e:
+                call(iter([b"\x00" * (1 << 20)]), timeout=10)
+            assert e.value.code() == grpc.StatusCode.RESOURCE_EXHAUSTED
+            assert call(iter(msgs), timeout=10) == b""  # a normal call still works
+        t0 = time.time()
+        while not got and time.time() - t0 < 10:
+            time.sleep(0.02)
+    finally:
+        srv.stop()
+    assert len(got) == 1
+
+
+def test_header_block_flood_closes_connection(nns):
+    """A header block that keeps growing through CONTINUATION frames is cut off
+    at SETTINGS_MAX_HEADER_LIST_SIZE (64 KiB): GOAWAY, connection closed."""
+    import socket
+    import struct
+
+    srv = nns.parse_launch(f"tensor_src_grpc name=gs server=true port=0 ! {CAPS} ! fakesink")
+    srv.set_state("playing")
+    port = _wait_port(srv.get_by_name("gs"))
+
+    def frame(ftype, flags, sid, payload):
+        return struct.pack(">I", len(payload))[1:] + bytes([ftype, flags]) + struct.pack(">I", sid) + payload
+
+    s = socket.create_connection(("127.0.0.1", port), timeout=5)
+    try:
+        s.sendall(b"PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n" + frame(4, 0, 0, b""))
+        s.sendall(frame(1, 0, 1, b"\x82"))  # HEADERS without END_HEADERS
+        closed = False
+        goaway = False
+        buf = b""
+        for _ in range(40):  # 40 x 16 KiB of CONTINUATION
+            try:
+                s.sendall(frame(9, 0, 1, b"\x00" * 16384))
+            except OSError:
+                closed = True
+                break
+        s.settimeout(5)
+        try:
+            while True:
+                d = s.recv(65536)
+                if not d:
+                    closed = True
+                    break
+                buf += d
+        except OSError:
+            closed = True
+        i = 0
+        while i + 9 <= len(buf):
+            ln = int.from_bytes(buf[i:i + 3], "big")
+            goaway |= buf[i + 3] == 7
+            i += 9 + ln
+        assert closed and goaway
+    finally:
+        s.close()
+        srv.stop()

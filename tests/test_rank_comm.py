@@ -242,3 +242,50 @@ def test_ini_rccl_and_hip_sections(tmp_path):
     chk = subprocess.run([os.path.join(ROOT, "bin", "nnsx-check")], env=env, capture_output=True, text=True,
                          timeout=120)
     assert "[rccl]" in chk.stdout and "timeout_ms = 400" in chk.stdout and "stream_priority = -1" in chk.stdout
+
+
+def test_query_server_survives_a_crashed_client(nns, tmp_path):
+    """One client rank dies without a goodbye (SIGKILL): the query server's
+    any-source receive must keep serving the live client (a lost
+    member link used to fail every later receive)."""
+    nns.register_custom_easy("rank_double", lambda x: [x[0] * 2],
+                             [nns.TensorShape([4], np.float32)], [nns.TensorShape([4], np.float32)])
+    store = _free_port()
+    n = 3
+    server = nns.parse_launch(f"tensor_query_serversrc connect-type=RCCL id=41 topic=q2 {_rank(0, n, store)} ! {F32} "
+                              "! tensor_filter framework=custom-easy model=rank_double "
+                              "! tensor_query_serversink connect-type=RCCL id=41")
+    server.set_state("playing")
+    script = tmp_path / "crash_client.py"
+    script.write_text(textwrap.dedent(f"""
+        import os, signal, sys, time
+        sys.path.insert(0, {ROOT!r})
+        import numpy as np
+        import nnstreamer_amd as nns
+        c = nns.parse_launch("appsrc name=src caps={F32} ! tensor_query_client connect-type=RCCL topic=q2 "
+                             "max-request=1 {_rank(2, n, store)} ! tensor_sink name=sink")
+        got = []
+        c.get_by_name("sink").connect("new-data", lambda b: got.append(1))
+        c.set_state("playing")
+        c.get_by_name("src").push_buffer(np.full(4, 7, np.float32), pts=1)
+        t = time.time()
+        while not got and time.time() - t < 20:
+            time.sleep(0.01)
+        print("replied", len(got), flush=True)
+        os.kill(os.getpid(), signal.SIGKILL)
+    """))
+    crash = subprocess.Popen([sys.executable, str(script)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    c = nns.parse_launch(f"appsrc name=src caps={F32} ! tensor_query_client connect-type=RCCL topic=q2 "
+                         f"max-request=2 {_rank(1, n, store)} ! tensor_sink name=sink")
+    out = _collect(c)
+    c.set_state("playing")
+    c.get_by_name("src").push_buffer(np.full(4, 0, np.float32), pts=100)  # every member joins the reply group
+    crash_out, _ = crash.communicate(timeout=60)
+    assert "replied 1" in crash_out and crash.returncode == -9, (crash.returncode, crash_out)
+    for i in range(1, 5):
+        c.get_by_name("src").push_buffer(np.full(4, i, np.float32), pts=100 + i)
+    c.get_by_name("src").end_of_stream()
+    _wait_eos(c)
+    c.stop()
+    server.stop()
+    assert [float(m[0][0]) for _, m in out] == [2.0 * i for i in range(5)]
