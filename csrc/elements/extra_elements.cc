@@ -263,9 +263,9 @@ class TensorIf : public Element {
         const int dev = m->device();
         hip::DeviceGuard g(dev);
         hipStream_t s = streams_.get(dev);
-        if (!mean_ws_) {
+        if (!mean_ws_ || mean_ws_->device() != dev) {  // (a buffer from another GPU: its own workspace)
           mean_ws_ = Memory::alloc_device(kernels::mean_workspace_bytes(), dev, s);
-          mean_host_ = Memory::alloc_pinned(8);
+          if (!mean_host_) mean_host_ = Memory::alloc_pinned(8);
         }
         double* ws = static_cast<double*>(mean_ws_->data());
         if (!kernels::tensor_mean(m->map_device(dev, s), ti.type, n, ws, s)) return false;

@@ -63,10 +63,12 @@ class TensorFilter : public BaseTransform, public TransformAbsorber {
       props_.input_info.num_tensors = std::max(props_.input_info.num_tensors, n);
       // the rank of each tensor is the number of fields written (tensor_filter_common.c:1490-1505)
       if (inputranks_str_.empty()) props_.input_ranks = field_ranks(input_str_);
+      notify_io(true);
     });
     prop_string("inputtype", &inputtype_str_, "Type of each element of the input tensor ?", [this] {
       unsigned n = props_.input_info.parse_types(inputtype_str_);
       props_.input_info.num_tensors = std::max(props_.input_info.num_tensors, n);
+      notify_io(true);
     });
     prop_string("inputname", &inputname_str_, "The Name of Input Tensor", [this] { props_.input_info.parse_names(inputname_str_); });
     prop_string("inputlayout", &props_.input_layout, "Set channel first (NCHW) or channel last layout (NHWC) or None for input data");
@@ -75,18 +77,32 @@ class TensorFilter : public BaseTransform, public TransformAbsorber {
       unsigned n = props_.output_info.parse_dimensions(output_str_);
       props_.output_info.num_tensors = std::max(props_.output_info.num_tensors, n);
       if (outputranks_str_.empty()) props_.output_ranks = field_ranks(output_str_);
+      notify_io(false);
     });
     prop_string("outputtype", &outputtype_str_, "Type of each element of the output tensor ?", [this] {
       unsigned n = props_.output_info.parse_types(outputtype_str_);
       props_.output_info.num_tensors = std::max(props_.output_info.num_tensors, n);
+      notify_io(false);
     });
     prop_string("outputname", &outputname_str_, "The Name of Output Tensor", [this] { props_.output_info.parse_names(outputname_str_); });
     prop_string("outputlayout", &props_.output_layout, "Set channel first (NCHW) or channel last layout (NHWC) or None for output data");
     prop_string("outputranks", &outputranks_str_, "The Rank of the Out Tensor", [this] { props_.output_ranks = parse_ranks(outputranks_str_); });
-    prop_string("custom", &props_.custom_properties, "Custom properties for subplugins ?");
+    prop_string("custom", &props_.custom_properties, "Custom properties for subplugins ?", [this] {
+      // an open framework hears about it (V1 CUSTOM_PROP, tensor_filter_common.c _gtfc_setprop_CUSTOM)
+      if (inst_ && !inst_->update_custom(props_.custom_properties))
+        NNSX_LOGD(this->name(), "framework did not take the new custom properties");
+    });
     prop_readonly("sub-plugins", [] { return join(Registry::get().names(SubpluginKind::FILTER), ","); },
                   "Registrable sub-plugins list");
-    prop_string("accelerator", &props_.accl_str, "Set accelerator for the subplugin with format (true/false):(comma separated ACCELERATOR(s)). true/false determines if accelerator is to be used. list of accelerators determines the backend (ignored with false). Example, if GPU, NPU can be used but not CPU - true:npu,gpu,!cpu.");
+    prop_string("accelerator", &props_.accl_str, "Set accelerator for the subplugin with format (true/false):(comma separated ACCELERATOR(s)). true/false determines if accelerator is to be used. list of accelerators determines the backend (ignored with false). Example, if GPU, NPU can be used but not CPU - true:npu,gpu,!cpu.",
+                [this] {
+                  if (inst_ && fw_) {  // V1 SET_ACCELERATOR with the list the framework supports
+                    bool use = false;
+                    parse_accelerator(props_.accl_str, fw_->accelerators(), &use);
+                    if (!inst_->update_accelerator(use ? fw_->accelerators() : std::string("cpu")))
+                      NNSX_LOGD(this->name(), "framework did not take the accelerator change");
+                  }
+                });
     prop_bool("is-updatable", &props_.is_updatable, "Indicate whether a given model to this tensor filter is updatable in runtime. (e.g., with on-device training)");
     {
       PropSpec s;
@@ -132,6 +148,14 @@ class TensorFilter : public BaseTransform, public TransformAbsorber {
               "model when the model maps uint8 frames through an input table");
     prop_readonly("absorbed", [this] { return absorbed_from_; },
                   "nnsx: name of the tensor_transform absorbed at caps negotiation (empty: none)");
+  }
+
+  // V1 SET_INPUT_PROP / SET_OUTPUT_PROP once the framework is open
+  void notify_io(bool input) {
+    if (!inst_) return;
+    const TensorsInfo& ti = input ? props_.input_info : props_.output_info;
+    if (ti.num_tensors > 0 && ti.valid() && !inst_->update_io_info(input, ti))
+      NNSX_LOGD(name(), "framework did not take the new ", input ? "input" : "output", " info");
   }
 
   // ---- TransformAbsorber (runtime/fusion.h) ----
@@ -731,7 +755,10 @@ class TensorFilter : public BaseTransform, public TransformAbsorber {
       std::lock_guard<std::mutex> lk(stat_mu_);
       reset_stats_locked();
     }
-    if (!ensure_open()) return false;
+    if (!ensure_open()) {
+      post_error("tensor_filter: cannot open framework '" + fw_name_ + "' (model '" + model_str_ + "')");
+      return false;
+    }
     attach_absorbable();
     return true;
   }

@@ -5,12 +5,15 @@
 // registration entry points (nnstreamer_filter_probe, nnstreamer_decoder_probe,
 // registerExternalConverter).
 //
-// Reference: nnstreamer_plugin_api_filter.h:273-495 (V1 vtable),
-// nnstreamer_plugin_api_decoder.h:38-97, nnstreamer_plugin_api_converter.h:41-85,
-// and the dlopen-then-probe flow of nnstreamer_subplugin.c:108-171.
+// Reference: nnstreamer_plugin_api_filter.h:139-495 (V0 and V1 vtables, the
+// seven V1 events), nnstreamer_plugin_api_decoder.h:38-97,
+// nnstreamer_plugin_api_converter.h:41-85, nnstreamer_plugin_api_trainer.h
+// :31-141 and the dlopen-then-probe flow of nnstreamer_subplugin.c:108-171.
 #include <dlfcn.h>
 
 #include <cerrno>
+#include <condition_variable>
+#include <mutex>
 #include <cstdlib>
 #include <cstring>
 #include <nnsx/nnsx_plugin_api.h>
@@ -18,6 +21,7 @@
 #include "core/log.h"
 #include "core/registry.h"
 #include "core/util.h"
+#include "filter/filter.h"
 #include "runtime/hip_util.h"
 #include "runtime/plugin_api.h"
 
@@ -90,10 +94,17 @@ struct CFilterProps {
   NNSX_FilterProperties c;
 };
 
+int c_event(const NNSX_FilterFramework* fw, const NNSX_FilterProperties* prop, void* priv, NNSX_FilterEvent ev,
+            const NNSX_FilterEventData& d) {
+  if (!fw->eventHandler) return -ENOENT;
+  return fw->eventHandler(fw, prop, priv, ev, &d);
+}
+
 class CFilterInstance : public FilterInstance {
  public:
   CFilterInstance(const NNSX_FilterFramework* fw, FilterProperties& p, bool alloc_in_invoke)
       : fw_(fw), props_(p), cprops_(p), alloc_(alloc_in_invoke) {
+    if (fw_->version == NNSX_FILTER_FRAMEWORK_V2) priv_ = fw_->subplugin_data;  // the C++ base's class object
     if (fw_->open && fw_->open(&cprops_.c, &priv_) != 0)
       throw Error("framework " + std::string(fw_->name) + ": open failed");
   }
@@ -158,7 +169,13 @@ class CFilterInstance : public FilterInstance {
             m->wait_uses(s);
             (void)hipStreamSynchronize(s);
           }
-          if (fw->destroyNotify) fw->destroyNotify(priv, m->data());
+          if (fw->destroyNotify) {
+            fw->destroyNotify(priv, m->data());
+          } else {  // V1 DESTROY_NOTIFY event; not handled (-ENOENT): the runtime frees host data
+            NNSX_FilterEventData d{};
+            d.data = m->data();
+            if (c_event(fw, nullptr, priv, NNSX_EVENT_DESTROY_NOTIFY, d) == -ENOENT && dev < 0) std::free(m->data());
+          }
         };
         auto m = Memory::wrap(co[i].data, co[i].size, dev >= 0 ? MemPlace::DEVICE : MemPlace::HOST, dev, rel);
         if (dev >= 0) m->mark_ready(s);
@@ -183,6 +200,31 @@ class CFilterInstance : public FilterInstance {
     if (!fw_->eventHandler) return false;
     const std::string s = name + "=" + arg;
     return fw_->eventHandler(fw_, &cprops_.c, priv_, NNSX_EVENT_CUSTOM, s.c_str()) == 0;
+  }
+  bool update_custom(const std::string& custom) override {
+    NNSX_FilterEventData d{};
+    d.custom_properties = custom.c_str();
+    if (c_event(fw_, &cprops_.c, priv_, NNSX_EVENT_CUSTOM_PROP, d) != 0) return false;
+    props_.custom_properties = custom;
+    cprops_.set(props_);
+    return true;
+  }
+  bool update_io_info(bool input, const TensorsInfo& info) override {
+    NNSX_TensorsInfo ci;
+    to_c_info(info, &ci);
+    NNSX_FilterEventData d{};
+    d.info = &ci;
+    if (c_event(fw_, &cprops_.c, priv_, input ? NNSX_EVENT_SET_INPUT_PROP : NNSX_EVENT_SET_OUTPUT_PROP, d) != 0)
+      return false;
+    (input ? props_.input_info : props_.output_info) = info;
+    if (!input) out_ = info;
+    cprops_.set(props_);
+    return true;
+  }
+  bool update_accelerator(const std::string& accelerators) override {
+    NNSX_FilterEventData d{};
+    d.accelerators = accelerators.c_str();
+    return c_event(fw_, &cprops_.c, priv_, NNSX_EVENT_SET_ACCELERATOR, d) == 0;
   }
   bool wants_host_input() const override { return device() < 0; }
 
@@ -224,6 +266,14 @@ class CFilterFramework : public FilterFramework {
     return std::make_unique<CFilterInstance>(fw_, props, alloc_);
   }
   bool check_availability(Accelerator accl) const override {
+    // CHECK_HW_AVAILABILITY (no instance yet: private_data NULL); frameworks
+    // without the event answer from their static accelerator list
+    if (fw_->eventHandler && (accl == Accelerator::GPU || accl == Accelerator::CPU)) {
+      NNSX_FilterEventData d{};
+      d.hw = accl == Accelerator::GPU ? "gpu" : "cpu";
+      const int r = c_event(fw_, nullptr, nullptr, NNSX_EVENT_CHECK_HW_AVAILABILITY, d);
+      if (r != -ENOENT) return r == 0;
+    }
     if (accl == Accelerator::GPU) return accl_.find("gpu") != std::string::npos;
     return FilterFramework::check_availability(accl) || accl == Accelerator::NONE;
   }
@@ -239,6 +289,310 @@ class CFilterFramework : public FilterFramework {
   std::string accl_ = "cpu";
   std::vector<std::string> exts_;
 };
+
+// ------------------------------------------------------ filters: V0 table ----
+// The legacy V0 table (invoke_NN, get/set dimensions, reloadModel, handleEvent,
+// checkAvailability, allocateInInvoke) adapted to the runtime; V0 frameworks run
+// on host memories.
+class CFilterInstanceV0 : public FilterInstance {
+ public:
+  CFilterInstanceV0(const NNSX_FilterFrameworkV0* fw, FilterProperties& p) : fw_(fw), props_(p), cprops_(p) {
+    if (fw_->open && fw_->open(&cprops_.c, &priv_) != 0)
+      throw Error("framework " + std::string(fw_->name) + ": open failed");
+    alloc_ = fw_->allocateInInvoke ? fw_->allocateInInvoke(&priv_) == 0 : fw_->allocate_in_invoke != 0;
+  }
+  ~CFilterInstanceV0() override {
+    if (fw_->close) fw_->close(&cprops_.c, &priv_);
+  }
+  bool get_model_info(TensorsInfo* in, TensorsInfo* out) override {
+    if (!fw_->getInputDimension || !fw_->getOutputDimension) return false;
+    NNSX_TensorsInfo a, b;
+    std::memset(&a, 0, sizeof(a));
+    std::memset(&b, 0, sizeof(b));
+    if (fw_->getInputDimension(&cprops_.c, &priv_, &a) != 0 || fw_->getOutputDimension(&cprops_.c, &priv_, &b) != 0)
+      return false;
+    if (!from_c_info(a, in) || !from_c_info(b, out)) return false;
+    remember(*in, *out);
+    return true;
+  }
+  bool set_input_info(const TensorsInfo& in, TensorsInfo* out) override {
+    if (!fw_->setInputDimension) return false;
+    NNSX_TensorsInfo a, b;
+    to_c_info(in, &a);
+    std::memset(&b, 0, sizeof(b));
+    if (fw_->setInputDimension(&cprops_.c, &priv_, &a, &b) != 0 || !from_c_info(b, out)) return false;
+    remember(in, *out);
+    return true;
+  }
+  int invoke(const std::vector<MemoryPtr>& in, std::vector<MemoryPtr>* out, InvokeContext&) override {
+    NNSX_TensorMemory ci[NNSX_SIZE_LIMIT], co[NNSX_SIZE_LIMIT];
+    std::memset(ci, 0, sizeof(ci));
+    std::memset(co, 0, sizeof(co));
+    for (size_t i = 0; i < in.size() && i < NNSX_SIZE_LIMIT; ++i) {
+      ci[i].data = const_cast<void*>(in[i]->map_host());
+      ci[i].size = in[i]->size();
+    }
+    const unsigned nout = std::min<unsigned>(out_.num_tensors, NNSX_SIZE_LIMIT);
+    std::vector<MemoryPtr> allocated;
+    for (unsigned i = 0; i < nout; ++i) {
+      co[i].size = out_.size(static_cast<int>(i));
+      if (!alloc_) {
+        allocated.push_back(Memory::alloc_host(co[i].size));
+        co[i].data = allocated.back()->data();
+      }
+    }
+    const int r = fw_->invoke_NN(&cprops_.c, &priv_, ci, co);
+    if (r != 0) return r;
+    if (!alloc_) {
+      *out = std::move(allocated);
+      return 0;
+    }
+    for (unsigned i = 0; i < nout; ++i) {
+      if (!co[i].data) return -EINVAL;
+      const NNSX_FilterFrameworkV0* fw = fw_;
+      auto pv = std::make_shared<void*>(priv_);  // outlives neither the instance's data nor this output
+      out->push_back(Memory::wrap(co[i].data, co[i].size, MemPlace::HOST, -1, [fw, pv](Memory* m) {
+        if (fw->destroyNotify) fw->destroyNotify(pv.get(), m->data());
+        else std::free(m->data());  // the reference's default for V0 allocate-in-invoke
+      }));
+    }
+    return 0;
+  }
+  bool reload_model(const FilterProperties& p) override {
+    if (!fw_->reloadModel) return false;
+    CFilterProps np(p);
+    if (fw_->reloadModel(&np.c, &priv_) != 0) return false;
+    props_ = p;
+    cprops_.set(p);
+    return true;
+  }
+  bool handle_event(const std::string& name, const std::string& arg) override {
+    if (!fw_->handleEvent) return false;
+    const std::string s = name + "=" + arg;
+    return fw_->handleEvent(NNSX_EVENT_CUSTOM, &priv_, s.c_str()) == 0;
+  }
+  bool update_custom(const std::string& custom) override {
+    if (!fw_->handleEvent) return false;
+    NNSX_FilterEventData d{};
+    d.custom_properties = custom.c_str();
+    if (fw_->handleEvent(NNSX_EVENT_CUSTOM_PROP, &priv_, &d) != 0) return false;
+    props_.custom_properties = custom;
+    cprops_.set(props_);
+    return true;
+  }
+
+ private:
+  void remember(const TensorsInfo& in, const TensorsInfo& out) {
+    out_ = out;
+    props_.input_info = in;
+    props_.output_info = out;
+    to_c_info(in, &cprops_.c.input_meta);
+    to_c_info(out, &cprops_.c.output_meta);
+  }
+  const NNSX_FilterFrameworkV0* fw_;
+  FilterProperties props_;
+  CFilterProps cprops_;
+  bool alloc_ = false;
+  void* priv_ = nullptr;
+  TensorsInfo out_;
+};
+
+class CFilterFrameworkV0 : public FilterFramework {
+ public:
+  explicit CFilterFrameworkV0(const NNSX_FilterFrameworkV0* fw) : fw_(fw) {}
+  std::string name() const override { return fw_->name; }
+  std::unique_ptr<FilterInstance> open(FilterProperties& props) override {
+    props.device = -1;  // V0: host memories
+    return std::make_unique<CFilterInstanceV0>(fw_, props);
+  }
+  bool check_availability(Accelerator accl) const override {
+    if (fw_->checkAvailability && (accl == Accelerator::GPU || accl == Accelerator::CPU))
+      return fw_->checkAvailability(accl == Accelerator::GPU ? "gpu" : "cpu") == 0;
+    return FilterFramework::check_availability(accl) || accl == Accelerator::NONE;
+  }
+  bool run_without_model() const override { return fw_->run_without_model != 0; }
+  bool verify_model_path() const override { return fw_->verify_model_path != 0; }
+  bool allocate_in_invoke() const override { return fw_->allocate_in_invoke != 0; }
+
+ private:
+  const NNSX_FilterFrameworkV0* fw_;
+};
+
+// --------------------------------------------------------------- trainers ----
+// GstTensorTrainerFramework (nnstreamer_plugin_api_trainer.h:66-127) adapted to
+// TrainerInstance; the training-complete GCond becomes the notify callback.
+class CTrainerInstance : public TrainerInstance {
+ public:
+  CTrainerInstance(const NNSX_TrainerFramework* fw, const TrainerProperties& p) : fw_(fw), p_(p) {
+    cfg_ = p.model_config;
+    save_ = p.model_save_path;
+    load_ = p.model_load_path;
+    std::memset(&c_, 0, sizeof(c_));
+    to_c_info(p.input_info, &c_.input_meta);
+    c_.model_config = cfg_.c_str();
+    c_.model_save_path = save_.c_str();
+    c_.model_load_path = load_.empty() ? nullptr : load_.c_str();
+    c_.num_inputs = p.num_inputs;
+    c_.num_labels = p.num_labels;
+    c_.num_training_samples = p.num_training_samples;
+    c_.num_validation_samples = p.num_validation_samples;
+    c_.num_epochs = p.epochs;
+    c_.device = p.device;
+    c_.notify = &CTrainerInstance::notify;
+    c_.notify_handle = this;
+    if (!fw_->create || fw_->create(fw_, &c_, &priv_) != 0)
+      throw Error("trainer " + std::string(fw_->name) + ": create failed");
+  }
+  ~CTrainerInstance() override {
+    if (fw_->destroy) fw_->destroy(fw_, &c_, &priv_);
+  }
+  bool start() override { return !fw_->start || fw_->start(fw_, &c_, priv_) == 0; }
+  bool stop() override {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stopped_ = true;
+      cv_.notify_all();
+    }
+    return !fw_->stop || fw_->stop(fw_, &c_, priv_) == 0;
+  }
+  bool push_data(const std::vector<MemoryPtr>& tensors, bool) override {
+    NNSX_TensorMemory in[NNSX_SIZE_LIMIT];
+    std::memset(in, 0, sizeof(in));
+    for (size_t i = 0; i < tensors.size() && i < NNSX_SIZE_LIMIT; ++i) {
+      in[i].data = const_cast<void*>(tensors[i]->map_host());
+      in[i].size = tensors[i]->size();
+    }
+    return fw_->push_data(fw_, &c_, priv_, in) == 0;
+  }
+  TrainerStatus status() override {
+    NNSX_TrainerFrameworkInfo i;
+    std::memset(&i, 0, sizeof(i));
+    TrainerStatus st;
+    if (fw_->getFrameworkInfo(fw_, &c_, priv_, &i) != 0) return st;
+    st.training_loss = i.training_loss;
+    st.training_accuracy = i.training_accuracy;
+    st.validation_loss = i.validation_loss;
+    st.validation_accuracy = i.validation_accuracy;
+    st.epoch_count = static_cast<unsigned>(i.epoch_cnt);
+    std::lock_guard<std::mutex> lk(mu_);
+    st.complete = i.is_training_complete != 0 || complete_;
+    return st;
+  }
+  bool save(const std::string& path) override { return fw_->save && fw_->save(fw_, &c_, priv_, path.c_str()) == 0; }
+  bool wait_complete(int64_t timeout_ns) override {
+    std::unique_lock<std::mutex> lk(mu_);
+    auto done = [&] {
+      if (complete_ || stopped_) return true;
+      NNSX_TrainerFrameworkInfo i;
+      std::memset(&i, 0, sizeof(i));
+      return fw_->getFrameworkInfo(fw_, &c_, priv_, &i) == 0 && i.is_training_complete != 0;
+    };
+    if (timeout_ns < 0) {
+      // the notify wakes us; a plugin that only sets is_training_complete is polled
+      while (!cv_.wait_for(lk, std::chrono::milliseconds(50), done)) {
+      }
+      return complete_ || !stopped_;
+    }
+    return cv_.wait_for(lk, std::chrono::nanoseconds(timeout_ns), done);
+  }
+
+ private:
+  static void notify(void* h, NNSX_TrainerEvent ev) {
+    auto* self = static_cast<CTrainerInstance*>(h);
+    std::lock_guard<std::mutex> lk(self->mu_);
+    if (ev == NNSX_TRAINER_EVENT_TRAINING_COMPLETION) self->complete_ = true;
+    ++self->events_;
+    self->cv_.notify_all();
+  }
+  const NNSX_TrainerFramework* fw_;
+  TrainerProperties p_;
+  std::string cfg_, save_, load_;
+  NNSX_TrainerProperties c_;
+  void* priv_ = nullptr;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool complete_ = false, stopped_ = false;
+  uint64_t events_ = 0;
+};
+
+class CTrainer : public TrainerFramework {
+ public:
+  explicit CTrainer(const NNSX_TrainerFramework* fw) : fw_(fw) {}
+  std::string name() const override { return fw_->name; }
+  std::unique_ptr<TrainerInstance> create(const TrainerProperties& props) override {
+    return std::make_unique<CTrainerInstance>(fw_, props);
+  }
+
+ private:
+  const NNSX_TrainerFramework* fw_;
+};
+
+// ------------------------------------------------------ framework=cpp ----
+// objects of <nnsx/tensor_filter_cpp.hh>, reached through their C thunks
+class CppOpsFilter : public CppFilter {
+ public:
+  CppOpsFilter(void* obj, const NNSX_CppFilterOps* ops) : obj_(obj), ops_(ops) {}
+  bool get_model_info(TensorsInfo* in, TensorsInfo* out) override {
+    NNSX_TensorsInfo a, b;
+    std::memset(&a, 0, sizeof(a));
+    std::memset(&b, 0, sizeof(b));
+    if (ops_->getInputDim(obj_, &a) != 0 || ops_->getOutputDim(obj_, &b) != 0) return false;
+    if (!from_c_info(a, in) || !from_c_info(b, out)) return false;
+    out_ = *out;
+    return true;
+  }
+  bool set_input_info(const TensorsInfo& in, TensorsInfo* out) override {
+    NNSX_TensorsInfo a, b;
+    to_c_info(in, &a);
+    std::memset(&b, 0, sizeof(b));
+    if (ops_->setInputDim(obj_, &a, &b) != 0 || !from_c_info(b, out)) return false;
+    out_ = *out;
+    return true;
+  }
+  int invoke(const std::vector<MemoryPtr>& in, std::vector<MemoryPtr>* out, InvokeContext&) override {
+    NNSX_TensorMemory ci[NNSX_SIZE_LIMIT], co[NNSX_SIZE_LIMIT];
+    std::memset(ci, 0, sizeof(ci));
+    std::memset(co, 0, sizeof(co));
+    for (size_t i = 0; i < in.size() && i < NNSX_SIZE_LIMIT; ++i) {
+      ci[i].data = const_cast<void*>(in[i]->map_host());
+      ci[i].size = in[i]->size();
+    }
+    const bool pre = ops_->isAllocatedBeforeInvoke(obj_) != 0;
+    const unsigned nout = std::min<unsigned>(out_.num_tensors, NNSX_SIZE_LIMIT);
+    std::vector<MemoryPtr> mem;
+    for (unsigned i = 0; i < nout; ++i) {
+      co[i].size = out_.size(static_cast<int>(i));
+      if (pre) {
+        mem.push_back(Memory::alloc_host(co[i].size));
+        co[i].data = mem.back()->data();
+      }
+    }
+    const int r = ops_->invoke(obj_, ci, co);
+    if (r != 0) return r;
+    if (!pre) {
+      for (unsigned i = 0; i < nout; ++i) {
+        if (!co[i].data) return -EINVAL;
+        mem.push_back(adopt_malloc(co[i].data, co[i].size));
+      }
+    }
+    *out = std::move(mem);
+    return 0;
+  }
+
+ private:
+  void* obj_;
+  const NNSX_CppFilterOps* ops_;
+  TensorsInfo out_;
+};
+
+int reg_cpp(const char* name, void* obj, const void* ops_v) {
+  auto* ops = static_cast<const NNSX_CppFilterOps*>(ops_v);
+  if (!name || !*name || !obj || !ops || !ops->invoke || !ops->isAllocatedBeforeInvoke) return -EINVAL;
+  return register_cpp_filter(name, [obj, ops](const FilterProperties&) {
+           return std::unique_ptr<CppFilter>(new CppOpsFilter(obj, ops));
+         }) ? 0 : -EINVAL;
+}
+int unreg_cpp(const char* name) { return name && unregister_cpp_filter(name) ? 0 : -ENOENT; }
 
 // --------------------------------------------------------------- decoders ----
 class CDecoderInstance : public DecoderInstance {
@@ -356,8 +710,13 @@ class CConverter : public ConverterSubplugin {
 
 // ------------------------------------------------------------ registration ----
 int reg_filter(const NNSX_FilterFramework* fw) {
+  if (fw && fw->version == NNSX_FILTER_FRAMEWORK_V0) {  // the legacy table (same leading version word)
+    auto* v0 = reinterpret_cast<const NNSX_FilterFrameworkV0*>(fw);
+    if (!v0->name || !v0->invoke_NN) return -EINVAL;
+    return register_filter_framework(std::make_shared<CFilterFrameworkV0>(v0)) ? 0 : -EINVAL;
+  }
   if (!fw || !fw->name || !fw->invoke) return -EINVAL;
-  if (fw->version != NNSX_FILTER_FRAMEWORK_V1) {
+  if (fw->version != NNSX_FILTER_FRAMEWORK_V1 && fw->version != NNSX_FILTER_FRAMEWORK_V2) {
     NNSX_LOGE("c_plugin", "filter framework ", fw->name, ": unsupported ABI version ", fw->version);
     return -EINVAL;
   }
@@ -385,6 +744,17 @@ int reg_converter(const NNSX_Converter* c) {
 int unreg_converter(const char* name) {
   return name && Registry::get().remove(SubpluginKind::CONVERTER, name) ? 0 : -ENOENT;
 }
+int reg_trainer(const NNSX_TrainerFramework* t) {
+  if (!t || !t->name || !t->push_data || !t->getFrameworkInfo) return -EINVAL;
+  if (t->version != NNSX_TRAINER_FRAMEWORK_V1) {
+    NNSX_LOGE("c_plugin", "trainer ", t->name, ": unsupported ABI version ", t->version);
+    return -EINVAL;
+  }
+  return register_trainer(std::make_shared<CTrainer>(t)) ? 0 : -EINVAL;
+}
+int unreg_trainer(const char* name) {
+  return name && Registry::get().remove(SubpluginKind::TRAINER, name) ? 0 : -ENOENT;
+}
 void host_log(int level, const char* cat, const char* msg) {
   const char* c = cat ? cat : "subplugin";
   const char* m = msg ? msg : "";
@@ -396,8 +766,9 @@ void host_log(int level, const char* cat, const char* msg) {
   }
 }
 
-const NNSX_PluginHost kHost = {NNSX_PLUGIN_ABI_VERSION, reg_filter,    unreg_filter, reg_decoder,
-                               unreg_decoder,           reg_converter, unreg_converter, host_log};
+const NNSX_PluginHost kHost = {NNSX_PLUGIN_ABI_VERSION, reg_filter, unreg_filter,  reg_decoder,
+                               unreg_decoder,           reg_converter, unreg_converter, host_log,
+                               reg_trainer,             unreg_trainer, reg_cpp,       unreg_cpp};
 
 // every library the registry loads: run its nnsx_subplugin_init(&host), if any
 void on_library(void* handle, const std::string& path) {
@@ -432,5 +803,18 @@ __attribute__((visibility("default"))) int registerExternalConverter(const NNSX_
 }
 __attribute__((visibility("default"))) int unregisterExternalConverter(const char* name) {
   return nnsx::unreg_converter(name);
+}
+__attribute__((visibility("default"))) int nnstreamer_cpp_filter_register(const char* name, void* obj,
+                                                                          const void* ops) {
+  return nnsx::reg_cpp(name, obj, ops);
+}
+__attribute__((visibility("default"))) int nnstreamer_cpp_filter_unregister(const char* name) {
+  return nnsx::unreg_cpp(name);
+}
+__attribute__((visibility("default"))) int nnstreamer_trainer_probe(const NNSX_TrainerFramework* ttsp) {
+  return nnsx::reg_trainer(ttsp);
+}
+__attribute__((visibility("default"))) int nnstreamer_trainer_exit(const char* name) {
+  return nnsx::unreg_trainer(name);
 }
 }

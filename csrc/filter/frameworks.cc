@@ -191,15 +191,27 @@ std::map<std::string, CppFilterFactory>& cpp_table() {
 class CppInstance : public FilterInstance {
  public:
   explicit CppInstance(FilterProperties& p) {
-    // model = "ClassName" or "lib.so,ClassName" (the .so registers from a ctor)
-    std::string cls = p.model_files.back();
-    if (p.model_files.size() > 1) Registry::get().load_library(p.model_files[0]);
-    CppFilterFactory f;
-    {
+    // model = "Name", "Name,lib.so" (the reference order) or "lib.so,Name": the
+    // library registers its objects when loaded (nnsx_subplugin_init or a
+    // constructor); it is not loaded when Name is already registered
+    std::string cls, lib;
+    for (const auto& m : p.model_files) {
+      if (m.size() > 3 && m.compare(m.size() - 3, 3, ".so") == 0)
+        lib = m;
+      else
+        cls = m;
+    }
+    auto lookup = [&](CppFilterFactory* f) {
       std::lock_guard<std::mutex> lk(g_cpp_mu);
       auto it = cpp_table().find(cls);
-      if (it == cpp_table().end()) throw Error("cpp filter class '" + cls + "' is not registered");
-      f = it->second;
+      if (it == cpp_table().end()) return false;
+      *f = it->second;
+      return true;
+    };
+    CppFilterFactory f;
+    if (!lookup(&f)) {
+      if (!lib.empty()) Registry::get().load_library(lib);
+      if (!lookup(&f)) throw Error("cpp filter '" + cls + "' is not registered");
     }
     obj_ = f(p);
   }

@@ -7,7 +7,8 @@
 //   with the operand cast to it first (integer ops wrap, integer div
 //   truncates), half types round after each op.
 // * permute: transpose / dimchg as one gather pass with coalesced writes.
-// * stand: fp64 two-pass mean / population std (tensor_data.c:315-493).
+// * stand: fp64 two-pass mean / population std (tensor_data.c:315-493), a
+//   deterministic two-level reduction (no atomics, coalesced reads).
 //
 // Memory-bound: 8 elements per lane, 256-thread blocks, grid capped at
 // 8 blocks per CU x 256 CUs with a grid-stride loop (cdna_hip_programming.md G11).
@@ -188,42 +189,59 @@ __global__ void __launch_bounds__(kBlock) transpose2d_kernel(const E* __restrict
 }
 
 // -------------------------------------------------------------------- stand ----
+// Deterministic two-level reduction over the [rows][C] tensor (channel
+// innermost; C = 1 for the global statistics), no atomics: level 1 -- block b
+// owns rows [b * rpb, (b + 1) * rpb) and writes one fp64 partial per channel,
+// its threads reading the rows' contiguous bytes in order (coalesced; for C <=
+// kBlock a multiple of C threads is active, so thread t always meets channel
+// t % C); level 2 -- one thread per channel adds the block partials in block
+// order.  Same result on every run, whatever the dispatch order.
+constexpr uint32_t kStandMaxBlocks = 256;
+
 template <typename InT>
-__global__ void __launch_bounds__(kBlock) stand_sum_kernel(const InT* __restrict__ in, uint64_t n, uint32_t C,
-                                                           bool per_channel, const double* __restrict__ mean,
-                                                           double* __restrict__ acc, int pass) {
-  // grid.y = channel (per-channel) ; pass 0 sums x, pass 1 sums (x-mean)^2
-  const uint32_t ch = per_channel ? blockIdx.y : 0;
-  const uint64_t stride = per_channel ? C : 1;
-  const uint64_t count = per_channel ? n / C : n;
-  const double m = pass ? mean[ch] : 0.0;
-  double local = 0.0;
-  for (uint64_t j = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; j < count;
-       j += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
-    double x = Num<InT>::as_double(in[j * stride + ch]);
-    local += pass ? (x - m) * (x - m) : x;
-  }
-  // wave64 reduction, then one LDS slot per wave
-  for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
-  __shared__ double part[kBlock / 64];
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = local;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double s = 0;
-    for (int w = 0; w < kBlock / 64; ++w) s += part[w];
-    atomicAdd(&acc[ch], s);
+__global__ void __launch_bounds__(kBlock) stand_partial_kernel(const InT* __restrict__ in, uint64_t rows, uint32_t C,
+                                                               uint64_t rpb, const double* __restrict__ mean,
+                                                               double* __restrict__ part, int pass) {
+  __shared__ double red[kBlock];
+  const uint64_t r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
+  double* out = part + static_cast<uint64_t>(blockIdx.x) * C;
+  if (C <= kBlock) {
+    const uint32_t lanes = (kBlock / C) * C, t = threadIdx.x, ch = t % C;
+    const double m = pass ? mean[ch] : 0.0;
+    double local = 0.0;
+    if (t < lanes && r0 < r1)
+      for (uint64_t i = r0 * C + t, end = r1 * C; i < end; i += lanes) {
+        const double x = Num<InT>::as_double(in[i]);
+        local += pass ? (x - m) * (x - m) : x;
+      }
+    red[t] = local;
+    __syncthreads();
+    if (t < C) {
+      double acc = 0.0;
+      for (uint32_t j = t; j < lanes; j += C) acc += red[j];
+      out[t] = acc;
+    }
+  } else {
+    for (uint32_t ch = threadIdx.x; ch < C; ch += kBlock) {  // consecutive threads, consecutive channels
+      const double m = pass ? mean[ch] : 0.0;
+      double acc = 0.0;
+      for (uint64_t r = r0; r < r1; ++r) {
+        const double x = Num<InT>::as_double(in[r * C + ch]);
+        acc += pass ? (x - m) * (x - m) : x;
+      }
+      out[ch] = acc;
+    }
   }
 }
 
-__global__ void stand_finish_kernel(double* mean_or_std, uint32_t C, uint64_t count, int pass) {
-  uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void stand_combine_kernel(const double* __restrict__ part, uint32_t nblocks, uint32_t C, uint64_t count,
+                                     double* __restrict__ res, int pass) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  if (pass == 0) {
-    mean_or_std[c] /= static_cast<double>(count);
-  } else {
-    double v = mean_or_std[c] / static_cast<double>(count);
-    mean_or_std[c] = v != 0.0 ? sqrt(v) : 1e-10;
-  }
+  double acc = 0.0;
+  for (uint32_t b = 0; b < nblocks; ++b) acc += part[static_cast<uint64_t>(b) * C + c];
+  const double v = acc / static_cast<double>(count);
+  res[c] = pass == 0 ? v : (v != 0.0 ? sqrt(v) : 1e-10);
 }
 
 template <typename InT, typename OutT>
@@ -243,18 +261,21 @@ __global__ void __launch_bounds__(kBlock) stand_apply_kernel(const InT* __restri
 template <typename InT>
 void launch_stand(const void* in, DType out_t, void* out, uint64_t n, uint32_t C, int mode, bool per_channel,
                   void* ws, hipStream_t s) {
-  uint32_t nch = per_channel ? C : 1;
+  const uint32_t nch = per_channel ? C : 1;
   double* mean = static_cast<double*>(ws);
   double* stdv = mean + nch;
-  (void)hipMemsetAsync(ws, 0, sizeof(double) * 2 * nch, s);
-  uint64_t count = per_channel ? n / C : n;
-  dim3 grid(std::min<unsigned>(grid_for(count), 512), nch);
+  double* part = stdv + nch;
+  const uint64_t rows = n / nch;
+  const uint64_t rpb = std::max<uint64_t>(1, (rows + kStandMaxBlocks - 1) / kStandMaxBlocks);
+  const uint32_t nblocks = static_cast<uint32_t>((rows + rpb - 1) / rpb);
   const InT* a = static_cast<const InT*>(in);
-  hipLaunchKernelGGL((stand_sum_kernel<InT>), grid, dim3(kBlock), 0, s, a, n, C, per_channel, mean, mean, 0);
-  hipLaunchKernelGGL(stand_finish_kernel, dim3((nch + 63) / 64), dim3(64), 0, s, mean, nch, count, 0);
+  const dim3 fin((nch + 63) / 64);
+  hipLaunchKernelGGL((stand_partial_kernel<InT>), dim3(nblocks), dim3(kBlock), 0, s, a, rows, nch, rpb, mean, part, 0);
+  hipLaunchKernelGGL(stand_combine_kernel, fin, dim3(64), 0, s, part, nblocks, nch, rows, mean, 0);
   if (mode == 0) {
-    hipLaunchKernelGGL((stand_sum_kernel<InT>), grid, dim3(kBlock), 0, s, a, n, C, per_channel, mean, stdv, 1);
-    hipLaunchKernelGGL(stand_finish_kernel, dim3((nch + 63) / 64), dim3(64), 0, s, stdv, nch, count, 1);
+    hipLaunchKernelGGL((stand_partial_kernel<InT>), dim3(nblocks), dim3(kBlock), 0, s, a, rows, nch, rpb, mean, part,
+                       1);
+    hipLaunchKernelGGL(stand_combine_kernel, fin, dim3(64), 0, s, part, nblocks, nch, rows, stdv, 1);
   }
 #define NNSX_OUT(T)                                                                                          \
   hipLaunchKernelGGL((stand_apply_kernel<InT, T>), dim3(grid_for(n)), dim3(kBlock), 0, s, a,               \
@@ -369,7 +390,9 @@ void permute(const void* in, void* out, size_t elem_size, const uint32_t in_dim[
   }
 }
 
-size_t stand_workspace_bytes(uint32_t channels) { return sizeof(double) * 2 * (channels ? channels : 1); }
+size_t stand_workspace_bytes(uint32_t channels) {
+  return sizeof(double) * (2 + kStandMaxBlocks) * (channels ? channels : 1);
+}
 
 void stand(const void* in, DType in_t, void* out, DType out_t, uint64_t n, uint32_t channels, int mode,
            bool per_channel, void* ws, hipStream_t s) {

@@ -92,7 +92,7 @@ std::shared_ptr<FilterFramework> resolve_filter_framework(const std::string& fw_
   if ((props->accl == Accelerator::GPU || props->accl == Accelerator::AUTO ||
        (props->accl == Accelerator::DEFAULT && fw->accelerators().find("gpu") != std::string::npos &&
         Config::get().custom_bool("pytorch", "enable_use_gpu", true))) &&
-      hip::available() && fw->check_availability(Accelerator::GPU)) {
+      fw->check_availability(Accelerator::GPU) && hip::available()) {
     int dev = device_prop;
     if (dev < 0) {
       const char* lr = getenv("LOCAL_RANK");

@@ -95,6 +95,21 @@ class FilterInstance {
     (void)lut;
     return false;
   }
+  // Property changes after open (reference V1 events CUSTOM_PROP,
+  // SET_INPUT_PROP / SET_OUTPUT_PROP, SET_ACCELERATOR): true = applied.
+  virtual bool update_custom(const std::string& custom) {
+    (void)custom;
+    return false;
+  }
+  virtual bool update_io_info(bool input, const TensorsInfo& info) {
+    (void)input;
+    (void)info;
+    return false;
+  }
+  virtual bool update_accelerator(const std::string& accelerators) {
+    (void)accelerators;
+    return false;
+  }
 };
 
 class FilterFramework {

@@ -10,9 +10,10 @@
  *
  * Loading: a sub-plugin is a shared object named
  *   libnnstreamer_filter_<name>.so / libnnstreamer_decoder_<name>.so /
- *   libnnstreamer_converter_<name>.so
- * in a sub-plugin directory (ini [filter]/[decoder]/[converter] paths,
- * NNSTREAMER_FILTERS / _DECODERS / _CONVERTERS, NNSX_SUBPLUGIN_PATH).  On the
+ *   libnnstreamer_converter_<name>.so / libnnstreamer_trainer_<name>.so
+ * in a sub-plugin directory (ini [filter]/[decoder]/[converter]/[trainer]
+ * paths, NNSTREAMER_FILTERS / _DECODERS / _CONVERTERS / _TRAINERS,
+ * NNSX_SUBPLUGIN_PATH).  On the
  * first lookup of <name> the runtime dlopen()s it and calls its exported
  *
  *   int nnsx_subplugin_init(const NNSX_PluginHost *host);
@@ -36,11 +37,15 @@
 extern "C" {
 #endif
 
-#define NNSX_PLUGIN_ABI_VERSION 1u
+/* 2: register_trainer / unregister_trainer and register_cpp_filter /
+ * unregister_cpp_filter appended to the host table.  A sub-plugin checks
+ * host->abi_version >= the version whose entries it uses. */
+#define NNSX_PLUGIN_ABI_VERSION 2u
 
 typedef struct _NNSX_FilterFramework NNSX_FilterFramework;
 typedef struct _NNSX_Decoder NNSX_Decoder;
 typedef struct _NNSX_Converter NNSX_Converter;
+typedef struct _NNSX_TrainerFramework NNSX_TrainerFramework;
 
 typedef struct {
   uint32_t abi_version; /* NNSX_PLUGIN_ABI_VERSION */
@@ -52,6 +57,12 @@ typedef struct {
   int (*unregister_converter)(const char *name);
   /* level: 0 error, 1 warning, 2 info, 3 debug */
   void (*log)(int level, const char *category, const char *message);
+  /* abi_version >= 2 */
+  int (*register_trainer)(const NNSX_TrainerFramework *fw);
+  int (*unregister_trainer)(const char *name);
+  /* framework=cpp objects; ops: NNSX_CppFilterOps of <nnsx/nnsx_plugin_api_filter.h> */
+  int (*register_cpp_filter)(const char *name, void *obj, const void *ops);
+  int (*unregister_cpp_filter)(const char *name);
 } NNSX_PluginHost;
 
 /* exported by every sub-plugin shared object */
@@ -66,6 +77,8 @@ int nnstreamer_decoder_probe(const NNSX_Decoder *dec);
 int nnstreamer_decoder_exit(const char *modename);
 int registerExternalConverter(const NNSX_Converter *conv);
 int unregisterExternalConverter(const char *name);
+int nnstreamer_cpp_filter_register(const char *name, void *obj, const void *ops);
+int nnstreamer_cpp_filter_unregister(const char *name);
 
 #ifdef __cplusplus
 }
@@ -74,5 +87,6 @@ int unregisterExternalConverter(const char *name);
 #include <nnsx/nnsx_plugin_api_filter.h>
 #include <nnsx/nnsx_plugin_api_decoder.h>
 #include <nnsx/nnsx_plugin_api_converter.h>
+#include <nnsx/nnsx_plugin_api_trainer.h>
 
 #endif /* NNSX_PLUGIN_API_H */

@@ -57,7 +57,7 @@ static NNSX_FilterFramework fw = {NNSX_FILTER_FRAMEWORK_V1, "cscale", f_open, f_
                                   NULL, NULL};
 
 int nnsx_subplugin_init(const NNSX_PluginHost *host) {
-  if (host->abi_version != NNSX_PLUGIN_ABI_VERSION) return -EINVAL;
+  if (host->abi_version < 1) return -EINVAL;
   host->log(2, "cscale", "registering framework cscale");
   return host->register_filter(&fw);
 }

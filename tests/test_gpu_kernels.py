@@ -126,3 +126,23 @@ def test_stand(nns, per_ch, mode):
         mean, std = xd.mean(), xd.std(unbiased=False)
         ref = ((xd - mean) / std).abs() if mode == 0 else xd - mean
     torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("C", [1, 3, 7, 300])
+def test_stand_deterministic_large(nns, C):
+    """The device stand reduction is a fixed-order two-level sum (no atomics):
+    bitwise-identical outputs run to run, at sizes where the reduction spans
+    every level-1 block (and C > 256, the channel-loop path)."""
+    n = C * 200_003
+    x = (torch.rand(n, device="cuda") * 255).contiguous()
+    ws = torch.empty(nns.kernels.stand_workspace_bytes(C), dtype=torch.uint8, device="cuda")
+    outs = []
+    for _ in range(3):
+        out = torch.empty_like(x)
+        nns.kernels.stand(x.data_ptr(), 7, out.data_ptr(), 7, n, C, 0, True, ws.data_ptr(), _stream())
+        torch.cuda.synchronize()
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])
+    v = x.double().view(-1, C)
+    ref = ((v - v.mean(0)) / v.std(0, unbiased=False)).abs().view(-1)
+    torch.testing.assert_close(outs[0].double(), ref, rtol=1e-5, atol=1e-4)
