@@ -244,9 +244,9 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
             desc = (f"videotestsrc num-buffers={frames * workers} pattern=snow pool-size={pool} "
                     f"! video/x-raw,format=RGB,width={S},height={S},framerate=0/1 "
                     f"! tensor_converter frames-per-tensor={B} device={dev} ! queue max-size-buffers=4 "
-                    f"! edgesink {link}")
+                    f"! edgesink name=fan {link}")
         else:
-            desc = (f"edgesrc {link} peer-rank=0 ! queue max-size-buffers=2 "
+            desc = (f"edgesrc name=fan {link} peer-rank=0 ! queue max-size-buffers=2 "
                     + f"! tensor_transform name=norm mode=arithmetic option={cfg['norm']} "
                     + f"! {filt}"
                     f"! queue max-size-buffers={a.queue} ! {cfg['decoder'].format(**files)} ! tensor_sink name=sink")
@@ -277,12 +277,20 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
     gathered = pipe.get_by_name("ag").get_property("comm-bytes") if cfg.get("gather") else None
     dev_stamps = filt_el.get_property("device-stamps") if (filt_el is not None and use_gpu) else ""
     absorbed = filt_el.get_property("absorbed") if filt_el is not None else ""
+    # the nnsx rank groups this rank actually used (data plane : members)
+    groups = {}
+    if filt_el is not None and filt_el.get_property("model-broadcast"):
+        groups["model_broadcast"] = filt_el.get_property("model-broadcast")
+    for el in ("ag", "fan"):
+        e = pipe.get_by_name(el)
+        if e is not None and e.get_property("comm-group"):
+            groups["tensor_allgather" if el == "ag" else "edge_fan"] = e.get_property("comm-group")
     pipe.stop()
 
     import numpy as np
 
     rec = dict(elapsed=0.0, p50=0.0, p99=0.0, gpu_elapsed=0.0, gpu_busy_ms=0.0, wall=t_end - t_start,
-               desc=desc, fan=fan, workers=workers, absorbed=absorbed, gathered=gathered)
+               desc=desc, fan=fan, workers=workers, absorbed=absorbed, gathered=gathered, groups=groups)
     if sink is None:
         return rec  # the workers' clocks decide
     recs = [tuple(int(v) for v in e.split(":")) for e in sink.get_property("stats").split(",") if e]
@@ -502,6 +510,9 @@ def main():
             "wall_s": round(sum(r["wall"] for r in results.values()), 3),
             "numa_binding": numa,
             **({"allgather_bytes_sent_received_rank0": head["gathered"]} if head["gathered"] is not None else {}),
+            # nnsx rank groups of rank 0 ("<data plane>:<members>[:bytes]") and the RCCL world they span
+            "nnsx_groups_rank0": head["groups"],
+            "rccl_world": max([int(v.split(":")[1]) for v in head["groups"].values() if v.startswith("rccl:")] or [0]),
             "config": {
                 "model": cfg["desc"],
                 "global_batch": B * world,

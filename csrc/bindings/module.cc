@@ -8,6 +8,7 @@
 
 #include <cstring>
 
+#include "comm/group.h"
 #include "comm/hpack.h"
 #include "comm/mqtt.h"
 #include "core/caps.h"
@@ -451,6 +452,107 @@ PYBIND11_MODULE(_C, m) {
       });
 
   // in-process MQTT broker (mqttsink / mqttsrc / connect-type=HYBRID without an external broker)
+  // rank groups (comm/group.h): the multi-GPU data plane the among-device
+  // elements use, for direct tests of each collective and of p2p
+  py::class_<comm::Packet>(m, "Packet")
+      .def(py::init([](py::list blobs, int64_t pts, bool eos, const std::string& caps) {
+             comm::Packet p;
+             for (auto b : blobs) p.blobs.push_back(memory_from_python(b));
+             p.pts = pts;
+             p.eos = eos;
+             p.caps = caps;
+             return p;
+           }),
+           py::arg("blobs") = py::list(), py::arg("pts") = -1, py::arg("eos") = false, py::arg("caps") = "")
+      .def_readonly("src", &comm::Packet::src)
+      .def_readonly("pts", &comm::Packet::pts)
+      .def_readonly("eos", &comm::Packet::eos)
+      .def_readonly("caps", &comm::Packet::caps)
+      .def_property_readonly("blobs", [](const comm::Packet& p) { return p.blobs; });
+  py::class_<comm::Group, std::shared_ptr<comm::Group>>(m, "Group")
+      .def(py::init([](const std::string& name, int rank, int world, const std::string& store, int device,
+                       const std::string& backend, int timeout_ms) {
+             comm::GroupSpec s;
+             s.name = name;
+             s.rank = rank;
+             s.world = world;
+             s.store = store;
+             s.device = device;
+             s.backend = backend;
+             s.timeout_ms = timeout_ms;
+             std::string err;
+             std::shared_ptr<comm::Group> g;
+             {
+               py::gil_scoped_release r;
+               g = comm::Group::open(s, &err);
+             }
+             if (!g) throw Error("Group: " + err);
+             return g;
+           }),
+           py::arg("name"), py::arg("rank"), py::arg("world"), py::arg("store"), py::arg("device") = -1,
+           py::arg("backend") = "auto", py::arg("timeout_ms") = 60000)
+      .def_property_readonly("rank", &comm::Group::rank)
+      .def_property_readonly("size", &comm::Group::size)
+      .def_property_readonly("backend", [](const comm::Group& g) { return std::string(g.backend_name()); })
+      .def_property_readonly("bytes_sent", &comm::Group::bytes_sent)
+      .def_property_readonly("bytes_received", &comm::Group::bytes_received)
+      .def("allgather", [](comm::Group& g, const comm::Packet& mine) {
+        std::vector<comm::Packet> all;
+        MemoryPtr stacked;
+        std::string err;
+        bool ok;
+        {
+          py::gil_scoped_release r;
+          ok = g.allgather(mine, &all, &err, &stacked);
+        }
+        if (!ok) throw Error("allgather: " + err);
+        return py::make_tuple(all, stacked);
+      }, "-> (per-member packets, stacked buffer or None)")
+      .def("broadcast", [](comm::Group& g, int root, comm::Packet pkt) {
+        std::string err;
+        bool ok;
+        {
+          py::gil_scoped_release r;
+          ok = g.broadcast(root, &pkt, &err);
+        }
+        if (!ok) throw Error("broadcast: " + err);
+        return pkt;
+      })
+      .def("scatter", [](comm::Group& g, int root, std::vector<comm::Packet> parts) {
+        comm::Packet mine;
+        std::string err;
+        bool ok;
+        {
+          py::gil_scoped_release r;
+          ok = g.scatter(root, g.rank() == root ? &parts : nullptr, &mine, &err);
+        }
+        if (!ok) throw Error("scatter: " + err);
+        return mine;
+      }, py::arg("root"), py::arg("parts") = std::vector<comm::Packet>())
+      .def("send", [](comm::Group& g, int peer, const comm::Packet& p) {
+        std::string err;
+        bool ok;
+        {
+          py::gil_scoped_release r;
+          ok = g.send(peer, p, &err);
+        }
+        if (!ok) throw Error("send: " + err);
+      })
+      .def("recv", [](comm::Group& g, int timeout_ms) -> py::object {
+        comm::Packet p;
+        bool to = false, ok;
+        std::string err;
+        {
+          py::gil_scoped_release r;
+          ok = g.recv(&p, timeout_ms, &to, &err);
+        }
+        if (!ok) {
+          if (to) return py::none();
+          throw Error("recv: " + err);
+        }
+        return py::cast(p);
+      }, py::arg("timeout_ms") = 60000);
+
   py::class_<comm::MqttBroker, std::shared_ptr<comm::MqttBroker>>(m, "MqttBroker")
       .def(py::init([](int port, const std::string& host) {
              std::string err;

@@ -783,6 +783,9 @@ class EdgeSink : public BaseSink {
               "nnsx (connect-type=RCCL): broadcast every frame to all subscribers, or scatter frames round-robin");
     prop_readonly("comm-bytes", [this] { return std::to_string(g_ ? g_->bytes_sent() : 0); },
                   "nnsx: payload bytes published on the rank group");
+
+    prop_readonly("comm-group", [this] { return g_ ? strfmt(g_->backend_name(), ":", g_->size()) : std::string(); },
+                  "nnsx: data plane and member count of the rank group (e.g. rccl:8)");
   }
 
  protected:
@@ -970,6 +973,8 @@ class EdgeSrc : public BaseSrc {
     prop_enum("rccl-mode", &rccl_mode_, kRcclModes, "nnsx (connect-type=RCCL): must match the publishing edgesink");
     prop_readonly("comm-bytes", [this] { return std::to_string(g_ ? g_->bytes_received() : 0); },
                   "nnsx: payload bytes received on the rank group");
+    prop_readonly("comm-group", [this] { return g_ ? strfmt(g_->backend_name(), ":", g_->size()) : std::string(); },
+                  "nnsx: data plane and member count of the rank group (e.g. rccl:8)");
     is_live_ = true;
   }
 
@@ -1121,6 +1126,8 @@ class TensorAllGather : public Element {
     prop_readonly("comm-bytes",
                   [this] { return g_ ? strfmt(g_->bytes_sent(), ":", g_->bytes_received()) : std::string("0:0"); },
                   "nnsx: payload bytes sent:received on the rank group");
+    prop_readonly("comm-group", [this] { return g_ ? strfmt(g_->backend_name(), ":", g_->size()) : std::string(); },
+                  "nnsx: data plane and member count of the rank group (e.g. rccl:8)");
   }
 
   bool stop() override {

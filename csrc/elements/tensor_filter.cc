@@ -146,6 +146,9 @@ class TensorFilter : public BaseTransform, public TransformAbsorber {
     prop_bool("absorb-transform", &absorb_enabled_,
               "nnsx: fold an adjacent upstream tensor_transform (uint8 -> float32 elementwise arithmetic) into the "
               "model when the model maps uint8 frames through an input table");
+    prop_readonly("model-broadcast", [this] { return inst_ ? inst_->info("model-broadcast") : std::string(); },
+                  "nnsx: '<data plane>:<members>:<bytes>' when the model arrived by a rank-group broadcast "
+                  "(custom=broadcast:<root>)");
     prop_readonly("absorbed", [this] { return absorbed_from_; },
                   "nnsx: name of the tensor_transform absorbed at caps negotiation (empty: none)");
   }

@@ -95,6 +95,11 @@ class TorchInstance : public FilterInstance {
 
   bool wants_host_input() const override { return device_ < 0; }
 
+  std::string info(const std::string& key) const override {
+    if (key == "model-broadcast" && bcast_bytes_) return bcast_group_;
+    return std::string();
+  }
+
   // models exposing a float32 [256] attribute `in_lut` map a uint8 input 0
   // through it (nnstreamer_amd.models.fused: the fused stems); an upstream
   // tensor_transform's arithmetic is folded into that table (runtime/fusion.h)
@@ -271,6 +276,7 @@ class TorchInstance : public FilterInstance {
     const MemoryPtr& blob = pkt.blobs[0];
     std::string bytes(static_cast<const char*>(blob->map_host()), blob->size());
     bcast_bytes_ = bytes.size();
+    bcast_group_ = strfmt(g->backend_name(), ":", g->size(), ":", bytes.size());
     NNSX_LOGI("pytorch", "model of rank ", bcast_root_, " received over ", g->backend_name(), " (", bytes.size(),
               " bytes, group rank ", g->rank(), "/", g->size(), ")");
     hip::DeviceGuard dg(device_);
@@ -443,6 +449,7 @@ class TorchInstance : public FilterInstance {
   int bcast_root_ = -1;  // custom=broadcast:<rank>
   std::string bcast_backend_ = "auto", bcast_store_, bcast_name_;
   size_t bcast_bytes_ = 0;
+  std::string bcast_group_;  // "<data plane>:<members>:<bytes>" of the load-time broadcast
   const bool copy_out_ = [] {
     const char* e = std::getenv("NNSX_GRAPH_COPY_OUT");
     return e && e[0] == '1';

@@ -110,6 +110,11 @@ class FilterInstance {
     (void)accelerators;
     return false;
   }
+  // framework-specific read-only facts for tools / stats (e.g. "model-broadcast")
+  virtual std::string info(const std::string& key) const {
+    (void)key;
+    return std::string();
+  }
 };
 
 class FilterFramework {

@@ -47,8 +47,10 @@ from ._C import (  # noqa: E402,F401
     Buffer,
     Caps,
     Element,
+    Group,
     Memory,
     MqttBroker,
+    Packet,
     NnsxError,
     Pipeline,
     config_dump,
@@ -97,6 +99,8 @@ __all__ = [
     "Buffer",
     "Caps",
     "Element",
+    "Group",
+    "Packet",
     "Memory",
     "Pipeline",
     "TensorShape",

@@ -1,0 +1,56 @@
+"""Shared by the CPU and GPU multi-rank tests: start one tests/_rank_worker.py
+child per rank (never exec'ing from this process) and check what each member
+received against what every other member sent."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def run_ranks(world, devices, backend, timeout=240):
+    port = free_port()
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "_rank_worker.py"), str(r), str(world),
+                               str(port), str(devices[r]), backend], stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True, env=env) for r in range(world)]
+    outs = []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=timeout)
+            outs.append((p.returncode, out))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    res = []
+    for rc, out in outs:
+        assert rc == 0, out[-3000:]
+        line = [l for l in out.splitlines() if l.startswith("{")][-1]
+        res.append(json.loads(line))
+    return res
+
+
+def check(res, world, backend):
+    for r, x in enumerate(res):
+        assert x["rank"] == r and x["size"] == world and x["backend"] == backend, x
+        assert x["ag"] == [[k, 100 + k, float(k), 256] for k in range(world)], x["ag"]
+        if x["ag_stacked"] is not None:
+            assert x["ag_stacked"] == [float(k) for k in range(world)]
+        assert x["ag_ragged"] == [[10.0 * k] * (k + 1) for k in range(world)], x["ag_ragged"]
+        assert x["bcast"] == [7, "other/tensors", [1000.0, 1001.0, 1002.0]], x["bcast"]
+        assert x["scatter"] == [r, 100.0 + r, 32], x["scatter"]
+        if world > 1:
+            prv = (r - 1) % world
+            assert x["ring"] == [[prv, 0, prv * 10.0], [prv, 1, prv * 10.0 + 1]], x["ring"]
+            assert x["bytes_sent"] > 0 and x["bytes_received"] > 0, x

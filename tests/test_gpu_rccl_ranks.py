@@ -1,0 +1,52 @@
+"""RCCL data plane with one process per GPU (BASELINE.json configs 4 and 5):
+every collective and p2p call of comm::Group over RCCL/xGMI between N =
+min(#GPUs, 8) ranks, payload values checked on every member, plus the two
+multi-rank bench configs (edgesink rccl-mode=scatter fan-out, tensor_allgather).
+Reference fan-out / fan-in points: tensor_query_client.c:657-746,
+edge_sink.c:305-345, gsttensor_demux.c:469-556.  Skipped below 2 GPUs (the
+1-GPU pool); the CPU twin is tests/test_rank_collectives.py."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from rank_util import ROOT, check, run_ranks
+
+pytestmark = pytest.mark.gpu
+
+
+def _ngpu():
+    import torch
+
+    return torch.cuda.device_count()
+
+
+needs2 = pytest.mark.skipif(_ngpu() < 2, reason="needs >= 2 GPUs (one rank per GPU)")
+
+
+@needs2
+def test_group_collectives_rccl():
+    world = min(_ngpu(), 8)
+    res = run_ranks(world, list(range(world)), "rccl")
+    check(res, world, "rccl")
+    for x in res:  # payloads stayed in HBM: received blobs are device memories
+        assert all(x["ag_on_device"]), x
+
+
+@needs2
+@pytest.mark.parametrize("cfg", ["posenet_multi", "deeplab_fan"])
+def test_bench_multi_rank_configs(cfg):
+    n = 2 if cfg == "posenet_multi" else 3
+    if _ngpu() < n:
+        pytest.skip(f"{cfg} needs {n} GPUs")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--config", cfg,
+                        "--steps", "3", "--warmup", "1", "--batch", "4", "--latency-frames", "0", "--sweep", "",
+                        "--comm-backend", "rccl"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["n_gpus"] == n and rec["value"] > 0, rec
+    if cfg == "posenet_multi":
+        assert rec.get("allgather_bytes_sent_received_rank0"), rec

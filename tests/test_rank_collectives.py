@@ -1,0 +1,12 @@
+"""Rank-group collectives and p2p across processes on CPU (tcp backend): the
+same member logic the RCCL data plane runs on GPUs (tests/test_gpu_rccl_ranks.py):
+uniform / ragged all-gather, broadcast, scatter, send/recv ring, byte counters."""
+import pytest
+
+from rank_util import check, run_ranks
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_group_collectives_tcp(world):
+    res = run_ranks(world, [-1] * world, "tcp")
+    check(res, world, "tcp")
