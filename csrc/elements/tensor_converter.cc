@@ -55,6 +55,8 @@ class TensorConverter : public Element {
     prop_readonly("sub-plugins", [] { return join(Registry::get().names(SubpluginKind::CONVERTER), ","); },
                   "Registrable sub-plugins list");
     prop_int("device", &device_, "nnsx: -1 keep tensors on the host, N upload into GPU N's HBM (zero-copy downstream)");
+    prop_int("pool-size", &pool_blocks_,
+             "nnsx: device tensors come from a pool of this many recycled HBM blocks (0: one allocation per tensor)");
   }
 
   bool start() override {
@@ -312,7 +314,7 @@ class TensorConverter : public Element {
     size_t row = static_cast<size_t>(vinfo_.width) * vinfo_.channels;
     if (!remove_padding_) {
       if (dev >= 0 && frames_per_tensor_ == 1) {
-        auto out = Memory::alloc_device(frame_size_, dev, s);
+        auto out = dev_alloc(frame_size_, dev, s);
         if (m->on_device()) {
           m->wait_ready(s);
           hip::check(hipMemcpyAsync(out->data(), m->data(), frame_size_, hipMemcpyDeviceToDevice, s), "D2D");
@@ -334,7 +336,7 @@ class TensorConverter : public Element {
       return m;
     }
     if (dev >= 0 && frames_per_tensor_ == 1 && !m->on_device()) {
-      auto out = Memory::alloc_device(frame_size_, dev, s);
+      auto out = dev_alloc(frame_size_, dev, s);
       hip::check(hipMemcpy2DAsync(out->data(), row, m->data(), stride, row, vinfo_.height, hipMemcpyHostToDevice, s),
                  "H2D 2D frame");
       m->record_use(s, dev);
@@ -383,7 +385,7 @@ class TensorConverter : public Element {
       avail_ -= size;
       return out;
     }
-    out = dev >= 0 ? Memory::alloc_device(size, dev, s) : Memory::alloc_host(size);
+    out = dev >= 0 ? dev_alloc(size, dev, s) : Memory::alloc_host(size);
     size_t done = 0;
     std::vector<std::pair<const char*, size_t>> runs;
     if (dev >= 0 && dma_runs(size, &runs)) {
@@ -738,6 +740,15 @@ class TensorConverter : public Element {
   unsigned frames_per_tensor_ = 1;
   bool set_timestamp_ = true;
   int device_ = -1;
+  int pool_blocks_ = 8;
+  std::shared_ptr<DeviceBufferPool> pool_;
+  // device tensors of the steady size come from the recycled block pool
+  MemoryPtr dev_alloc(size_t size, int dev, hipStream_t s) {
+    if (pool_blocks_ <= 0) return Memory::alloc_device(size, dev, s);
+    if (!pool_ || pool_->device() != dev || pool_->block_size() != size)
+      pool_ = DeviceBufferPool::create(dev, size, static_cast<size_t>(pool_blocks_));
+    return pool_->acquire(s);
+  }
   bool configured_ = false;
   TensorsConfig config_;
   MediaType media_ = MediaType::INVALID;

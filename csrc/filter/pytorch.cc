@@ -75,6 +75,12 @@ struct GraphState {
   std::vector<at::Tensor> static_out;
   // downstream holders of static_out handed out without a copy (0 = free)
   std::shared_ptr<std::atomic<int>> out_held = std::make_shared<std::atomic<int>>(0);
+  // in place: static_in IS a pooled upstream block (DeviceBufferPool), replayed
+  // whenever that block comes back -- no input copy
+  bool in_place = false;
+  // small outputs are copied out after each replay, so the instance is free
+  // again at once (no instance count driven by downstream queue depth)
+  bool copy_out = false;
 };
 
 class TorchInstance : public FilterInstance {
@@ -85,7 +91,7 @@ class TorchInstance : public FilterInstance {
     load(p.model_files.at(0));
   }
   ~TorchInstance() override {
-    graphs_.clear();
+    clear_graphs();
     if (cap_stream_) {
       hip::DeviceGuard g(device_);
       (void)hipStreamSynchronize(cap_stream_);
@@ -116,7 +122,7 @@ class TorchInstance : public FilterInstance {
     }
     lut_ = lut;
     if (props_.input_info.num_tensors > 0) props_.input_info.at(0).type = DType::UINT8;
-    graphs_.clear();
+    clear_graphs();
     return true;
   }
 
@@ -182,7 +188,7 @@ class TorchInstance : public FilterInstance {
       if (!lut_.empty()) apply_lut(fresh, lut_);  // keep an absorbed transform
       std::lock_guard<std::mutex> lk(mu_);
       module_ = std::move(fresh);
-      graphs_.clear();  // captured graphs point at the old weights
+      clear_graphs();  // captured graphs point at the old weights
       return true;
     } catch (const std::exception& e) {
       NNSX_LOGE("pytorch", "reload failed: ", e.what());
@@ -344,14 +350,20 @@ class TorchInstance : public FilterInstance {
 
     std::vector<at::Tensor> outs;
     std::shared_ptr<std::atomic<int>> held;  // static outputs handed out as they are
-    GraphState* gs = use_graph_ && dev_idx >= 0 ? graph_for(inputs, s, dev_idx) : nullptr;
+    bool pooled = dev_idx >= 0 && !in.empty();
+    for (auto& m : in) pooled = pooled && m->on_device() && m->root()->tags().count(DeviceBufferPool::kPoolTag);
+    GraphState* gs = use_graph_ && dev_idx >= 0 ? graph_for(inputs, s, dev_idx, pooled) : nullptr;
     if (gs) {
       // an instance whose static outputs no downstream element holds: the replay
       // rewrites them and hands them out as they are (no copy); they return to
       // the instance when their last reader is done
-      for (size_t i = 0; i < gs->static_in.size(); ++i) gs->static_in[i].copy_(inputs[i], /*non_blocking=*/true);
-      gs->graph->replay();
-      if (copy_out_) {  // NNSX_GRAPH_COPY_OUT=1: one instance, private copies of its outputs
+      if (!gs->in_place)
+        for (size_t i = 0; i < gs->static_in.size(); ++i) gs->static_in[i].copy_(inputs[i], /*non_blocking=*/true);
+      // the captured executable on the element's stream (CUDAGraph::replay would
+      // first refresh RNG offsets with two fill kernels: the models here draw no
+      // random numbers)
+      hip::check(hipGraphLaunch(gs->graph->raw_cuda_graph_exec(), s), "hipGraphLaunch");
+      if (copy_out_ || gs->copy_out) {  // private copies of the outputs: the instance is free again
         for (auto& t : gs->static_out) outs.push_back(t.clone());
       } else {
         held = gs->out_held;
@@ -389,17 +401,43 @@ class TorchInstance : public FilterInstance {
   // outputs); each input shape keeps up to kInstances instances -- created in
   // the first frames, while the downstream queues fill -- and when all are
   // held the frame runs eagerly (nullptr).
+  //
+  // Pooled inputs (blocks of an upstream DeviceBufferPool) get in-place
+  // instances: one per block address, capturing the block itself as the graph
+  // input, so a replay reads the frame where the upstream element wrote it (no
+  // input copy; the block stays allocated for the pool's life and recurs only
+  // after its previous use was released).  Up to kInPlace per shape, then the
+  // copying instances take over.
   static constexpr size_t kInstances = 6;
-  GraphState* graph_for(const std::vector<at::Tensor>& inputs, hipStream_t s, int dev_idx) {
+  static constexpr size_t kInPlace = 12;
+  static constexpr size_t kCopyOutBytes = 64u << 20;
+  GraphState* graph_for(const std::vector<at::Tensor>& inputs, hipStream_t s, int dev_idx, bool pooled) {
     std::string key;
     for (auto& t : inputs) {
       for (auto d : t.sizes()) key += std::to_string(d) + "x";
       key += std::string(c10::toString(t.scalar_type())) + ";";
     }
+    if (pooled) {
+      std::string pkey = key + "@";
+      for (auto& t : inputs) pkey += std::to_string(reinterpret_cast<uintptr_t>(t.data_ptr())) + ";";
+      auto it = graphs_.find(pkey);
+      if (it != graphs_.end() && !it->second.empty()) {
+        GraphState* g = it->second.front().get();
+        if (g->copy_out || copy_out_ || g->out_held->load() == 0) return g;
+      } else if (in_place_count_[key] < kInPlace) {
+        ++in_place_count_[key];
+        return capture(graphs_[pkey], inputs, s, dev_idx, pkey, true);
+      }
+    }
     auto& set = graphs_[key];
     for (auto& g : set)
-      if (g->out_held->load() == 0) return g.get();  // (never held with copy_out_)
+      if (g->copy_out || g->out_held->load() == 0) return g.get();  // (never held with copy_out_)
     if (set.size() >= kInstances) return nullptr;
+    return capture(set, inputs, s, dev_idx, key, false);
+  }
+
+  GraphState* capture(std::vector<std::unique_ptr<GraphState>>& set, const std::vector<at::Tensor>& inputs,
+                      hipStream_t s, int dev_idx, const std::string& key, bool in_place) {
     hip::DeviceGuard dg(dev_idx);
     if (!cap_stream_) hip::check(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "capture stream");
     hipEvent_t ev;
@@ -410,12 +448,13 @@ class TorchInstance : public FilterInstance {
     {
       c10::hip::HIPStreamGuardMasqueradingAsCUDA cg(
           c10::hip::getStreamFromExternalMasqueradingAsCUDA(cap_stream_, static_cast<c10::DeviceIndex>(dev_idx)));
-      for (auto& t : inputs) gs->static_in.push_back(torch::empty_like(t, t.options()).copy_(t));
+      gs->in_place = in_place;
+      for (auto& t : inputs) gs->static_in.push_back(in_place ? t : torch::empty_like(t, t.options()).copy_(t));
       const std::vector<at::Tensor>& src = gs->static_in;
       std::vector<c10::IValue> iv;
       // warm up on the capture stream (lazy init, autotuning) before capturing;
-      // later instances of a shape need only one pass
-      for (int w = 0; w < (set.empty() ? 3 : 1); ++w) {
+      // later instances need only one pass
+      for (int w = 0; w < (graphs_captured_ == 0 ? 3 : 1); ++w) {
         iv.clear();
         for (auto& t : src) iv.push_back(prepare(t));
         std::vector<at::Tensor> tmp;
@@ -428,7 +467,11 @@ class TorchInstance : public FilterInstance {
       for (auto& t : src) iv.push_back(prepare(t));
       flatten(module_.forward(iv), &gs->static_out);
       gs->graph->capture_end();
+      size_t out_bytes = 0;
+      for (auto& t : gs->static_out) out_bytes += t.numel() * t.element_size();
+      gs->copy_out = out_bytes <= kCopyOutBytes;
     }
+    ++graphs_captured_;
     hip::check(hipEventDestroy(ev), "capture event destroy");
     // the replay runs on s, after the capture stream's work (the static outputs'
     // first contents are not handed out, but keep the streams ordered)
@@ -437,7 +480,7 @@ class TorchInstance : public FilterInstance {
     hip::check(hipEventRecord(done, cap_stream_), "capture done record");
     hip::check(hipStreamWaitEvent(s, done, 0), "capture done wait");
     hip::check(hipEventDestroy(done), "capture done destroy");
-    NNSX_LOGI("pytorch", "captured hipGraph for input shape ", key, ", instance ", set.size());
+    NNSX_LOGI("pytorch", "captured hipGraph for input ", key, in_place ? " (in place)" : "", ", instance ", set.size());
     set.push_back(std::move(gs));
     return set.back().get();
   }
@@ -460,6 +503,12 @@ class TorchInstance : public FilterInstance {
   bool has_lut_ = false;       // the model maps uint8 input 0 through attribute in_lut
   std::vector<float> lut_;     // the absorbed table (re-applied on hot reload)
   std::map<std::string, std::vector<std::unique_ptr<GraphState>>> graphs_;
+  std::map<std::string, size_t> in_place_count_;  // in-place instances per input shape
+  void clear_graphs() {
+    graphs_.clear();
+    in_place_count_.clear();
+  }
+  size_t graphs_captured_ = 0;
   hipStream_t cap_stream_ = nullptr;  // private capture stream (graph_for)
 };
 

@@ -40,6 +40,7 @@
 #include <cstdint>
 #include <cmath>
 #include <cstdlib>
+#include <vector>
 
 #include "kernels/mbv2.h"
 
@@ -700,7 +701,9 @@ struct IrwGeom {
   // plane.  xs positions are XOR-swizzled with (kq & 3) so the staging writes
   // (8 consecutive lanes = 8 k-quads of one pixel) land in 4 slots, not 1.
   static constexpr int XSP = NC16;                    // xs plane stride (quads)
-  static constexpr int PINP = (PIN + 15) / 16 * 16;   // hidden plane stride (quads)
+  // hidden plane stride (quads); the compact expand (FULL = false) needs one
+  // scratch cell past the grid for padding pixels
+  static constexpr int PINP = FULL ? (PIN + 15) / 16 * 16 : PIN / 16 * 16 + 16;
   static constexpr int KQ = KIN / 4;
   static constexpr int NPT = (TY * TX + 15) / 16;     // output pixel tiles
   static constexpr int NPX = NPT * 16;
@@ -714,7 +717,8 @@ struct IrwGeom {
   // batch 128 despite 6 spilled VGPRs; the same on the 14x14 64-channel block
   // (3, 21 spills) lost 40 -> 45 us, and on the 56x56 block (1 spill, 5
   // workgroups/CU instead of 4) 128 -> 144 us.
-  static constexpr int MINB = (KIN == 32 && S == 1) ? 4 : NOT <= 6 ? 2 : 1;
+  // (the wider 7x14 28x28 tiles hold 14 accumulators: 3 waves per SIMD)
+  static constexpr int MINB = (KIN == 32 && S == 1) ? (TY * TX <= 49 ? 4 : 3) : NOT <= 6 ? 2 : 1;
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -1463,8 +1467,31 @@ const IrwCfg kIrwCfgs[] = {
     // the project is a plain GEMM): 7x7 160 -> 960 whose project (-> 320)
     // needs more accumulators than a wave holds
     NNSX_IRW(1, 7, 7, 160, 0, 4, false),
+    // candidates with less halo / padding work (A/B with NNSX_IRW_SKIP=<indices of
+    // the defaults above>; find_irw takes the first configuration that fits)
+    NNSX_IRW(1, 7, 14, 32, 2, 4, false),   // 28x28: expand 136/98 cells, project 112/98 (7x7: 88/49, 64/49)
+    NNSX_IRW(1, 8, 16, 24, 2, 3, true),    // 56x56: expand 192/128 (8x8: 112/64)
+    NNSX_IRW(2, 4, 8, 24, 2, 3, true),     // 56 -> 28: expand 160/128 input px (4x4: 96/64)
+    NNSX_IRW(2, 8, 8, 16, 2, 3, true),     // 112 -> 56: expand 304/256 (4x8: 160/128)
 };
 #undef NNSX_IRW
+
+// indices of kIrwCfgs that find_irw skips (A/B experiments): NNSX_IRW_SKIP=1,4
+bool irw_skipped(size_t i) {
+  static const std::vector<size_t> skip = [] {
+    std::vector<size_t> v;
+    if (const char* e = std::getenv("NNSX_IRW_SKIP"))
+      for (const char* p = e; *p;) {
+        char* end = nullptr;
+        const unsigned long x = std::strtoul(p, &end, 10);
+        if (end == p) break;
+        v.push_back(x);
+        p = *end ? end + 1 : end;
+      }
+    return v;
+  }();
+  return std::find(skip.begin(), skip.end(), i) != skip.end();
+}
 
 bool irw_enabled() {
   static const bool on = [] {
@@ -1479,9 +1506,12 @@ const IrwCfg* find_irw(int S, int H, int W, int cin, int hid, int cout, bool has
   const int kin = (cin + 7) / 8 * 8;
   const int nout = (cout + 15) / 16;
   const int Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
-  for (const auto& c : kIrwCfgs)
-    if (c.S == S && c.KIN == kin && c.NOT == nout && Ho % c.TY == 0 && Wo % c.TX == 0 && c.lds(hid) <= 160 * 1024)
+  for (size_t i = 0; i < sizeof(kIrwCfgs) / sizeof(kIrwCfgs[0]); ++i) {
+    const IrwCfg& c = kIrwCfgs[i];
+    if (c.S == S && c.KIN == kin && c.NOT == nout && Ho % c.TY == 0 && Wo % c.TX == 0 &&
+        c.lds(hid) <= 160 * 1024 && !irw_skipped(i))
       return &c;
+  }
   return nullptr;
 }
 

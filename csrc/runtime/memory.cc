@@ -43,6 +43,93 @@ MemoryPtr Memory::alloc_device(size_t size, int dev, hipStream_t stream) {
   });
 }
 
+// ------------------------------------------------------- DeviceBufferPool ----
+std::shared_ptr<DeviceBufferPool> DeviceBufferPool::create(int dev, size_t size, size_t max_blocks) {
+  return std::shared_ptr<DeviceBufferPool>(new DeviceBufferPool(dev, size, max_blocks));
+}
+
+DeviceBufferPool::DeviceBufferPool(int dev, size_t size, size_t max_blocks) : dev_(dev), size_(size), max_(max_blocks) {
+  static std::atomic<uint64_t> next{1};
+  id_ = next++;
+}
+
+DeviceBufferPool::~DeviceBufferPool() {
+  // blocks still out are owned by their Memory (freed on release); free ones go now,
+  // ordered after their last readers
+  hip::DeviceGuard g(dev_);
+  hipStream_t rs = hip::release_stream(dev_);
+  for (auto& b : blocks_) {
+    if (!b.free) continue;
+    if (b.released) {
+      (void)hipStreamWaitEvent(rs, b.released, 0);
+      hip::event_put(dev_, b.released);
+    }
+    hip::device_free(dev_, b.ptr, rs);
+  }
+}
+
+size_t DeviceBufferPool::blocks() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return blocks_.size();
+}
+
+MemoryPtr DeviceBufferPool::acquire(hipStream_t stream) {
+  int slot = -1;
+  void* p = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (size_t i = 0; i < blocks_.size(); ++i)
+      if (blocks_[i].free) {
+        slot = static_cast<int>(i);
+        break;
+      }
+    if (slot < 0 && blocks_.size() < max_) {
+      Block b;
+      b.ptr = hip::device_alloc(dev_, size_, stream);
+      blocks_.push_back(b);
+      slot = static_cast<int>(blocks_.size()) - 1;
+    }
+    if (slot >= 0) {
+      Block& b = blocks_[static_cast<size_t>(slot)];
+      b.free = false;
+      p = b.ptr;
+      if (b.released) {  // previous readers first (stream-ordered, no host wait)
+        hip::DeviceGuard g(dev_);
+        hip::check(hipStreamWaitEvent(stream, b.released, 0), "pool acquire wait");
+      }
+    }
+  }
+  if (slot < 0) return Memory::alloc_device(size_, dev_, stream);  // all blocks out: no pooling
+  std::weak_ptr<DeviceBufferPool> wp = shared_from_this();
+  const int dev = dev_;
+  const size_t size = size_;
+  auto m = std::make_shared<Memory>(p, size, MemPlace::DEVICE, dev, [wp, slot, dev](Memory* mm) {
+    hip::DeviceGuard g(dev);
+    hipStream_t rs = hip::release_stream(dev);
+    mm->wait_ready(rs);
+    mm->wait_uses(rs);
+    if (auto pool = wp.lock()) {
+      hipEvent_t e = hip::event_get(dev);
+      hip::check(hipEventRecord(e, rs), "pool release");
+      pool->put_back(slot, e);
+    } else {
+      hip::device_free(dev, mm->data(), rs);  // the pool is gone: the block goes with its last user
+    }
+  });
+  (void)size;
+  m->tags()[kPoolTag] = static_cast<int64_t>(id_);
+  m->tags()[kSlotTag] = slot;
+  return m;
+}
+
+void DeviceBufferPool::put_back(int slot, hipEvent_t released) {
+  std::lock_guard<std::mutex> lk(mu_);
+  Block& b = blocks_.at(static_cast<size_t>(slot));
+  if (b.released) hip::event_put(dev_, b.released);
+  b.released = released;
+  b.free = true;
+}
+
 MemoryPtr Memory::wrap(void* data, size_t size, MemPlace place, int device, Release release) {
   return std::make_shared<Memory>(data, size, place, device, std::move(release));
 }
