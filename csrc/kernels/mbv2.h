@@ -54,8 +54,17 @@ bool ir_block(const IrBlockArgs& a, hipStream_t s);
 // y[M][N] = act(x[M][K] . wt[N][K]^T + bias) (+ res); wt zero-padded [Npad][Kpad]
 // (Kpad >= K, Kpad % 4 == 0), K % 4 == 0, N % 4 == 0.
 // tile: 0 = auto, else BM * 1000 + BN of an instantiated tile (64064, 128064, 64128, 128128, 128192)
+// Output layout of a GEMM writing into a slice of a concatenated tensor: rpb >
+// 0 -> row m goes to y + (m / rpb) * bstride + (m % rpb) * ncols, and only the
+// first ncols columns are stored (no split-K).  rpb = 0: plain y[M][N].
+struct YLayout {
+  int rpb = 0;
+  int ncols = 0;
+  int64_t bstride = 0;
+};
 void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
-                 int Kpad, int Npad, int act, hipStream_t s, int tile = 0, float* ws = nullptr);
+                 int Kpad, int Npad, int act, hipStream_t s, int tile = 0, float* ws = nullptr,
+                 const YLayout& yl = YLayout{});
 // split-K workspace the GEMM wants for this shape (0: no split; without it the
 // GEMM runs unsplit)
 size_t pw_gemm_f32_workspace_bytes(int M, int N, int Kpad, bool has_res, int tile = 0);

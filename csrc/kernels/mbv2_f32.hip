@@ -108,7 +108,8 @@ __global__ void __launch_bounds__(256) pw_gemm_f32_kernel(const float* __restric
                                                           const float* __restrict__ res,  // [M][N] or null
                                                           float* __restrict__ y,          // [M][N]
                                                           int M, int N, int K, int Kpad, int Npad, int act,
-                                                          int kchunk) {  // k-stages of this grid.z slice
+                                                          int kchunk,  // k-stages of this grid.z slice
+                                                          YLayout yl) {
   constexpr int RM = BM / 32, RN = BN / 32;  // 16-row fragments per wave (2 x 2 waves)
   constexpr int VX = BM * GKQ / 256, VW = BN * GKQ / 256;
   // k4-major images, row index XOR-swizzled with the k-quad (kq < 8): the
@@ -231,6 +232,18 @@ __global__ void __launch_bounds__(256) pw_gemm_f32_kernel(const float* __restric
       if (res) v += rv[i][j];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], act);
+      if (yl.rpb) {  // a slice of a concatenated output: row m of batch m / rpb, first ncols columns
+        if (n >= yl.ncols) continue;
+        float* yd = y + static_cast<int64_t>(m / yl.rpb) * yl.bstride + static_cast<int64_t>(m % yl.rpb) * yl.ncols + n;
+        if (n + 4 <= yl.ncols && (yl.ncols & 3) == 0) {
+          *reinterpret_cast<f32x4_t*>(yd) = v;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (n + r < yl.ncols) yd[r] = v[r];
+        }
+        continue;
+      }
       *reinterpret_cast<f32x4_t*>(yp) = v;
     }
   }
@@ -1242,18 +1255,29 @@ __global__ void __launch_bounds__(64, 2) stem_ir1w_f32_kernel(StemIr1F32Args a) 
   static_assert(PITCH <= 64, "stem_ir1w: one patch row per wave load");
   const int pcol = lane < PITCH ? lane : 0;
   const int pdx = pcol / 3, pch = pcol - 3 * pdx;
+  const int rowb = a.W * 3;  // bytes per image row
   int raw[IY];
+  // branch-free: every row's byte is loaded from a valid address (row 0 of the
+  // image for out-of-image taps) and replaced by -1 afterwards, so the IY loads
+  // issue back to back; the address is the wave-uniform image base plus a 32-bit
+  // per-lane offset (no 64-bit address math per load)
   auto fetch = [&](int tile) {
     const int b = tile / tiles_img;
     const int tyx = tile - b * tiles_img;
     const int iy0 = 2 * ((tyx / a.tiles_x) * TY - 1) - 1, ix = 2 * ((tyx % a.tiles_x) * TX - 1) - 1 + pdx;
     const bool colok = lane < PITCH && ix >= 0 && ix < a.W;
-    const uint8_t* xc = a.x + static_cast<int64_t>(b) * a.H * a.W * 3 + static_cast<int64_t>(ix) * 3 + pch;
+    const uint8_t* img = a.x + static_cast<int64_t>(b) * a.H * rowb;
+    const uint32_t col = colok ? static_cast<uint32_t>(ix * 3 + pch) : 0u;
+    uint8_t v[IY];
+    bool ok[IY];
 #pragma unroll
     for (int r = 0; r < IY; ++r) {
       const int iy = iy0 + r;
-      raw[r] = (colok && iy >= 0 && iy < a.H) ? static_cast<int>(xc[static_cast<int64_t>(iy) * a.W * 3]) : -1;
+      ok[r] = colok && iy >= 0 && iy < a.H;
+      v[r] = img[(ok[r] ? static_cast<uint32_t>(iy * rowb) : 0u) + col];
     }
+#pragma unroll
+    for (int r = 0; r < IY; ++r) raw[r] = ok[r] ? static_cast<int>(v[r]) : -1;
   };
 
   int tile = blockIdx.x;
@@ -1568,18 +1592,19 @@ static int gemm_splits(int M, int N, int Kpad, bool plain) {
 
 template <int BM, int BN>
 static void pw_gemm_f32_launch(const float* x, const float* wt, const float* bias, const float* res, float* y, int M,
-                               int N, int K, int Kpad, int Npad, int act, float* ws, hipStream_t s) {
+                               int N, int K, int Kpad, int Npad, int act, float* ws, hipStream_t s,
+                               const YLayout& yl = YLayout{}) {
   dim3 grid((M + BM - 1) / BM, (N + BN - 1) / BN);
   const int kstages = (Kpad + GKT - 1) / GKT;
-  int chunk = ws ? gemm_kchunk(static_cast<int>(grid.x * grid.y), kstages, N, !res) : kstages;
+  int chunk = (ws && !yl.rpb) ? gemm_kchunk(static_cast<int>(grid.x * grid.y), kstages, N, !res) : kstages;
   grid.z = static_cast<unsigned>((kstages + chunk - 1) / chunk);
   if (grid.z == 1) {
     hipLaunchKernelGGL((pw_gemm_f32_kernel<BM, BN>), grid, dim3(256), 0, s, x, wt, bias, res, y, M, N, K, Kpad, Npad,
-                       act, kstages);
+                       act, kstages, yl);
     return;
   }
   hipLaunchKernelGGL((pw_gemm_f32_kernel<BM, BN>), grid, dim3(256), 0, s, x, wt, bias, res, ws, M, N, K, Kpad, Npad,
-                     act, chunk);
+                     act, chunk, YLayout{});
   const int64_t nq = static_cast<int64_t>(M) * N / 4;
   const unsigned rg = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((nq + 255) / 256, 2048)));
   hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(rg), dim3(256), 0, s, ws, static_cast<int>(grid.z), M, N, bias,
@@ -1642,13 +1667,13 @@ size_t pw_gemm_f32_workspace_bytes(int M, int N, int Kpad, bool has_res, int til
 }
 
 void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
-                 int Kpad, int Npad, int act, hipStream_t s, int tile, float* ws) {
+                 int Kpad, int Npad, int act, hipStream_t s, int tile, float* ws, const YLayout& yl) {
   switch (resolve_tile(M, N, Kpad, tile)) {
-    case 64064: pw_gemm_f32_launch<64, 64>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s); break;
-    case 128064: pw_gemm_f32_launch<128, 64>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s); break;
-    case 64128: pw_gemm_f32_launch<64, 128>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s); break;
-    case 128192: pw_gemm_f32_launch<128, 192>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s); break;
-    default: pw_gemm_f32_launch<128, 128>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s); break;
+    case 64064: pw_gemm_f32_launch<64, 64>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s, yl); break;
+    case 128064: pw_gemm_f32_launch<128, 64>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s, yl); break;
+    case 64128: pw_gemm_f32_launch<64, 128>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s, yl); break;
+    case 128192: pw_gemm_f32_launch<128, 192>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s, yl); break;
+    default: pw_gemm_f32_launch<128, 128>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s, yl); break;
   }
 }
 

@@ -92,6 +92,39 @@ at::Tensor pw_conv_cpu(const at::Tensor& x, const at::Tensor& wt, const at::Tens
   return v.to(out_f32 || x.scalar_type() == at::kFloat ? at::kFloat : at::kBFloat16);
 }
 
+// pw_conv whose output goes straight into a slice of a concatenated tensor:
+// out [B, T, C]; the GEMM of x [B, H, W, K] writes rows row0 .. row0 + H*W*n/C
+// of every batch (n = the real output width, a multiple of C).  Replaces a
+// per-head output + torch.cat (the SSD heads).
+void pw_conv_into_cuda(const at::Tensor& x, const at::Tensor& wt, const at::Tensor& bias, at::Tensor& out,
+                       int64_t row0, int64_t n, int64_t act) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 4,
+              "pw_conv_into: x [B,H,W,K] f32 contiguous");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() && out.dim() == 3,
+              "pw_conv_into: out [B,T,C] f32 contiguous");
+  const int64_t B = x.size(0), HW = x.size(1) * x.size(2), K = x.size(3), C = out.size(2), T = out.size(1);
+  const int64_t N = (n + 3) / 4 * 4, Kpad = wt.size(1), Npad = wt.size(0);
+  TORCH_CHECK(out.size(0) == B && n % C == 0 && row0 + HW * (n / C) <= T, "pw_conv_into: slice out of range");
+  TORCH_CHECK(K % 4 == 0 && Kpad >= K && Npad >= N && bias.numel() >= N && wt.scalar_type() == at::kFloat,
+              "pw_conv_into: weights");
+  nnsx::kernels::YLayout yl;
+  yl.rpb = static_cast<int>(HW);
+  yl.ncols = static_cast<int>(n);
+  yl.bstride = T * C;
+  nnsx::kernels::pw_gemm_f32(x.data_ptr<float>(), wt.data_ptr<float>(), bias.data_ptr<float>(), nullptr,
+                             out.data_ptr<float>() + row0 * C, static_cast<int>(B * HW), static_cast<int>(N),
+                             static_cast<int>(K), static_cast<int>(Kpad), static_cast<int>(Npad), static_cast<int>(act),
+                             cur_stream(), 0, nullptr, yl);
+}
+
+void pw_conv_into_cpu(const at::Tensor& x, const at::Tensor& wt, const at::Tensor& bias, at::Tensor& out,
+                      int64_t row0, int64_t n, int64_t act) {
+  at::Tensor y = pw_conv_cpu(x, wt, bias, c10::nullopt, (n + 3) / 4 * 4, act, true).slice(-1, 0, n);
+  const int64_t B = x.size(0), C = out.size(2);
+  y = y.reshape({B, -1, C});
+  out.slice(1, row0, row0 + y.size(1)).copy_(y);
+}
+
 // ------------------------------------------------------------ dw_conv ----
 at::Tensor dw_conv_cuda(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int64_t stride, int64_t act,
                         int64_t dilation) {
@@ -397,6 +430,7 @@ bool ir_supported(int64_t stride, int64_t cin, int64_t hid, int64_t cout) {
 
 TORCH_LIBRARY(nnsx, m) {
   m.def("pw_conv(Tensor x, Tensor wt, Tensor bias, Tensor? res, int N, int act, bool out_f32) -> Tensor");
+  m.def("pw_conv_into(Tensor x, Tensor wt, Tensor bias, Tensor(a!) out, int row0, int n, int act) -> ()");
   m.def("dw_conv(Tensor x, Tensor w, Tensor bias, int stride, int act, int dilation=1) -> Tensor");
   m.def("stem_conv(Tensor x, Tensor w, Tensor bias, int act, bool out_f32=False) -> Tensor");
   m.def("stem_conv_u8(Tensor x, Tensor w, Tensor bias, int act, Tensor lut, bool out_f32=False) -> Tensor");
@@ -415,6 +449,7 @@ TORCH_LIBRARY(nnsx, m) {
 
 TORCH_LIBRARY_IMPL(nnsx, CUDA, m) {
   m.impl("pw_conv", pw_conv_cuda);
+  m.impl("pw_conv_into", pw_conv_into_cuda);
   m.impl("dw_conv", dw_conv_cuda);
   m.impl("stem_conv", stem_conv_cuda);
   m.impl("stem_conv_u8", stem_conv_u8_cuda);
@@ -427,6 +462,7 @@ TORCH_LIBRARY_IMPL(nnsx, CUDA, m) {
 
 TORCH_LIBRARY_IMPL(nnsx, CPU, m) {
   m.impl("pw_conv", pw_conv_cpu);
+  m.impl("pw_conv_into", pw_conv_into_cpu);
   m.impl("dw_conv", dw_conv_cpu);
   m.impl("stem_conv", stem_conv_cpu);
   m.impl("stem_conv_u8", stem_conv_u8_cpu);

@@ -139,6 +139,14 @@ class FusedSepHead(nn.Module):
             y = y[..., : self.n]
         return y.reshape(b, -1, self.k)
 
+    def into(self, x: torch.Tensor, out: torch.Tensor, row0: int) -> int:
+        """fp32: the head GEMM writes its rows of the concatenated output `out`
+        [B, rows, k] directly (no per-head tensor, no torch.cat).  Returns the
+        next free row."""
+        h = self.dw(x)
+        torch.ops.nnsx.pw_conv_into(h, self.pw.wt, self.pw.bias, out, row0, self.n, 0)
+        return row0 + h.shape[1] * h.shape[2] * (self.n // self.k)
+
 
 class FusedExtra(nn.Module):
     def __init__(self, e: Extra, precision: str = "bf16"):
@@ -191,6 +199,19 @@ class FusedSSDLite(nn.Module):
         for ex in self.extras:
             h = ex(h)
             feats.append(h)
+        if self.f32 and x.is_cuda:
+            rows = 0
+            for i, bh in enumerate(self.box_heads):
+                rows += feats[i].shape[1] * feats[i].shape[2] * (bh.n // bh.k)
+            bo = torch.empty((x.shape[0], rows, 4), dtype=torch.float32, device=x.device)
+            lo = torch.empty((x.shape[0], rows, self.cls_heads[0].k), dtype=torch.float32, device=x.device)
+            r = 0
+            for i, bh in enumerate(self.box_heads):
+                r = bh.into(feats[i], bo, r)
+            r = 0
+            for i, ch in enumerate(self.cls_heads):
+                r = ch.into(feats[i], lo, r)
+            return bo.reshape(bo.shape[0], bo.shape[1], 1, 4), lo
         boxes: List[torch.Tensor] = []
         logits: List[torch.Tensor] = []
         for i, bh in enumerate(self.box_heads):
