@@ -116,15 +116,18 @@ CONFIGS = {
                         "option4=300:300 option5=300:300", per_frame=True,
                 metric="end-to-end frames/sec + p50 per-frame latency, SSD-MobileNet 300x300 + bounding_boxes + HIP NMS",
                 desc="SSDLite-MobileNetV2 300x300 (tensor_filter + bounding_boxes decoder, HIP NMS)"),
-    "deeplab": dict(size=513, model="deeplab_fused", norm="typecast:float32,div:255.0",
-                    decoder="tensor_decoder mode=image_segment option1=tflite-deeplab", per_frame=True,
+    "deeplab": dict(size=513, model="deeplab_fused_lowres", norm="typecast:float32,div:255.0",
+                    decoder="tensor_decoder mode=image_segment option1=tflite-deeplab option3=513:513", per_frame=True,
                     metric="end-to-end frames/sec + p50 per-frame latency, DeepLabV3 513x513 segmentation pipeline",
                     desc="DeepLabV3-MobileNetV2 513x513 (tensor_filter + image_segment decoder)"),
+    # (DeepLab: the model ships its 33x33 logits; the decoder's option3 resizes
+    # them bilinearly per label inside the argmax pass -- same frames as a
+    # 513x513x21 model output, without the 22 MB-per-frame score map)
     # BASELINE.json config 4: one camera rank fans its batches out to the other ranks
     # (edgesink connect-type=RCCL rccl-mode=scatter -> ncclSend/ncclRecv over xGMI);
     # every other rank runs DeepLabV3 + image_segment on what it receives
-    "deeplab_fan": dict(size=513, model="deeplab_fused", norm="typecast:float32,div:255.0",
-                        decoder="tensor_decoder mode=image_segment option1=tflite-deeplab", per_frame=True, fan=True,
+    "deeplab_fan": dict(size=513, model="deeplab_fused_lowres", norm="typecast:float32,div:255.0",
+                        decoder="tensor_decoder mode=image_segment option1=tflite-deeplab option3=513:513", per_frame=True, fan=True,
                         metric="end-to-end frames/sec, DeepLabV3 513x513 segmentation, branches fanned over RCCL",
                         desc="DeepLabV3-MobileNetV2 513x513 on N-1 ranks fed by a camera rank (RCCL scatter)"),
     # BASELINE.json config 5: PoseNet multi-source, outputs all-gathered across ranks
@@ -367,7 +370,7 @@ def main():
     # which engines to run: (label, model name, dtype)
     base = cfg["model"]
     if a.engine == "torch" or not use_gpu:
-        plain = base.replace("_fused", "")
+        plain = base.replace("_fused", "").replace("_lowres", "")  # the plain oracle emits full-size maps
         runs = [("fp32", plain, "fp32")]
     else:
         runs = []

@@ -4,7 +4,12 @@
 // tensordec-imagesegment.c: option1 mode (tflite-deeplab: [L:W:H] label
 // probabilities, argmax with a 0.5 threshold; snpe-deeplab: [W:H:1] label
 // indices; snpe-depth: [1:W:H] grayscale normalised by the frame maximum),
-// option2 max labels (default 20).  The colour map is the deterministic
+// option2 max labels (default 20).  nnsx extension, option3 = W:H: a
+// tflite-deeplab score map smaller than W x H (e.g. DeepLab's 33 x 33 logits at
+// output stride 16) is bilinearly resized (align_corners, the rule of
+// PyTorch's upsample_bilinear2d) to W x H per label before the argmax, in the
+// same device pass -- the model then ships its low-resolution logits and the
+// full-resolution score map never exists.  The colour map is the deterministic
 // rgb_modifier * label table the reference uses on its vectorised path
 // (:200-215); its scalar path draws random colours, which no golden can pin.
 // On HBM-resident input the fused argmax + colour kernel writes the RGBA frame
@@ -59,6 +64,17 @@ class ImageSegment : public DecoderInstance {
       uint64_t m = to_uint(v);
       if (m != 0 && m <= UINT32_MAX) max_labels_ = static_cast<unsigned>(m);
     }
+    if (idx == 2) {
+      out_w_ = out_h_ = 0;
+      const size_t c = v.find(':');
+      if (c != std::string::npos) {
+        const uint64_t ow = to_uint(v.substr(0, c)), oh = to_uint(v.substr(c + 1));
+        if (ow > 0 && oh > 0 && ow <= 65535 && oh <= 65535) {
+          out_w_ = static_cast<unsigned>(ow);
+          out_h_ = static_cast<unsigned>(oh);
+        }
+      }
+    }
     return true;
   }
 
@@ -68,6 +84,10 @@ class ImageSegment : public DecoderInstance {
     if (config.info.num_tensors < 1) return Caps();
     unsigned w, h, b;
     if (!geometry(config.info.at(0), &w, &h, &b)) return Caps();
+    if (resizes(w, h)) {
+      w = out_w_;
+      h = out_h_;
+    }
     Caps c = Caps::from_string(strfmt("video/x-raw, format=(string)RGBA, width=(int)", w, ", height=(int)", h));
     set_framerate_from_config(c, config);
     return c;
@@ -81,10 +101,11 @@ class ImageSegment : public DecoderInstance {
       NNSX_LOGE("image_segment", "invalid input data format");
       return FlowReturn::ERROR;
     }
-    const uint64_t npix = static_cast<uint64_t>(w) * h;
-    const size_t fsize = npix * 4;
     const uint32_t rgb_mod = 0xFFFFFFu / (max_labels_ + 1);
     ctx.out_frames = batch;
+    if (resizes(w, h)) return decode_resized(x_of(in[0], ctx), w, h, batch, rgb_mod, in[0], out, ctx);
+    const uint64_t npix = static_cast<uint64_t>(w) * h;
+    const size_t fsize = npix * 4;
     if (ctx.device >= 0) {
       const int dev = ctx.device;
       hipStream_t s = ctx.stream;
@@ -151,6 +172,69 @@ class ImageSegment : public DecoderInstance {
  private:
   static constexpr float kThreshold = 0.5f;
 
+  bool resizes(unsigned w, unsigned h) const {
+    return mode_ == TFLITE_DEEPLAB && out_w_ && out_h_ && (out_w_ != w || out_h_ != h);
+  }
+  static const float* x_of(const MemoryPtr& m, InvokeContext& ctx) {
+    return static_cast<const float*>(ctx.device >= 0 ? m->map_device(ctx.device, ctx.stream) : m->map_host());
+  }
+
+  // option3: [B][h][w][L] scores -> W x H RGBA frames (resize + argmax fused)
+  FlowReturn decode_resized(const float* x, unsigned w, unsigned h, unsigned batch, uint32_t rgb_mod,
+                            const MemoryPtr& src, Buffer* out, InvokeContext& ctx) {
+    (void)src;
+    const unsigned W = out_w_, H = out_h_, L = max_labels_ + 1;
+    const size_t fsize = static_cast<size_t>(W) * H * 4;
+    if (ctx.device >= 0) {
+      MemoryPtr frames = Memory::alloc_device(fsize * batch, ctx.device, ctx.stream);
+      kernels::segment_upsample_argmax_color(x, static_cast<int>(L), static_cast<int>(h), static_cast<int>(w),
+                                             static_cast<int>(batch), static_cast<int>(H), static_cast<int>(W),
+                                             rgb_mod, kThreshold, static_cast<uint32_t*>(frames->data()), ctx.stream);
+      frames->mark_ready(ctx.stream);
+      for (unsigned b = 0; b < batch; ++b) out->mems.push_back(Memory::view(frames, b * fsize, fsize));
+      return FlowReturn::OK;
+    }
+    // host: the same taps and mixing order as the kernel
+    auto tap = [](unsigned dst, unsigned in, unsigned outn, unsigned* i0, unsigned* i1, float* l0, float* l1) {
+      const float scale = outn > 1 ? static_cast<float>(in - 1) / static_cast<float>(outn - 1) : 0.f;
+      const float s = scale * static_cast<float>(dst);
+      *i0 = std::min(static_cast<unsigned>(s), in - 1);
+      *l1 = s - static_cast<float>(*i0);
+      *l0 = 1.f - *l1;
+      *i1 = *i0 + (*i0 < in - 1 ? 1 : 0);
+    };
+    std::vector<unsigned> x0(W), x1(W);
+    std::vector<float> lx0(W), lx1(W);
+    for (unsigned X = 0; X < W; ++X) tap(X, w, W, &x0[X], &x1[X], &lx0[X], &lx1[X]);
+    for (unsigned b = 0; b < batch; ++b) {
+      auto m = Memory::alloc_host(fsize);
+      uint32_t* o = static_cast<uint32_t*>(m->data());
+      const float* f = x + static_cast<uint64_t>(b) * h * w * L;
+      for (unsigned Y = 0; Y < H; ++Y) {
+        unsigned y0, y1;
+        float ly0, ly1;
+        tap(Y, h, H, &y0, &y1, &ly0, &ly1);
+        const float* r0 = f + static_cast<uint64_t>(y0) * w * L;
+        const float* r1 = f + static_cast<uint64_t>(y1) * w * L;
+        for (unsigned X = 0; X < W; ++X) {
+          const float *a0 = r0 + x0[X] * L, *a1 = r0 + x1[X] * L, *c0 = r1 + x0[X] * L, *c1 = r1 + x1[X] * L;
+          float best = 0.f;
+          unsigned bi = 0;
+          for (unsigned l = 0; l < L; ++l) {
+            const float v = ly0 * (lx0[X] * a0[l] + lx1[X] * a1[l]) + ly1 * (lx0[X] * c0[l] + lx1[X] * c1[l]);
+            if (l == 0 || v > best) {
+              best = v;
+              bi = l;
+            }
+          }
+          o[static_cast<uint64_t>(Y) * W + X] = best > kThreshold ? color(bi, rgb_mod) : 0u;
+        }
+      }
+      out->mems.push_back(m);
+    }
+    return FlowReturn::OK;
+  }
+
   static uint32_t color(unsigned label, uint32_t rgb_mod) {
     return label == 0 ? 0u : ((rgb_mod * label) & 0x00ffffffu) | 0xff000000u;
   }
@@ -179,6 +263,7 @@ class ImageSegment : public DecoderInstance {
 
   int mode_ = UNKNOWN;
   unsigned max_labels_ = 20;
+  unsigned out_w_ = 0, out_h_ = 0;  // option3
   MemoryPtr ws_;
 };
 

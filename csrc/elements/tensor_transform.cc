@@ -6,9 +6,11 @@
 // Device-resident inputs (or `device>=0`) run the fused CDNA4 kernels of
 // csrc/kernels/transform.hip on this element's stream; host inputs run the C
 // reference loops below (also the numerics oracle of the kernels).
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <regex>
+#include <vector>
 
 #include "core/cpu_ops.h"
 #include "core/log.h"
@@ -91,17 +93,79 @@ inline T cpu_apply(T v, const kernels::ArithOp& op) {
   }
 }
 
+// one element through the whole op chain (the definition every path below
+// reproduces bit for bit)
+template <typename InT, typename OutT>
+inline OutT cpu_arith_one(InT x, int ch, const kernels::ArithParams& p) {
+  OutT v = cpu::Cast<OutT>::from(x);
+  for (int k = 0; k < p.nops; ++k)
+    if (!p.ch_count || p.ops[k].ch < 0 || p.ops[k].ch == ch) v = cpu_apply<OutT>(v, p.ops[k]);
+  return v;
+}
+
+// one op over a run of elements, the op kind resolved outside the loop (the
+// loop vectorises; fp32 division stays a division)
+template <typename T>
+void cpu_apply_run(T* v, size_t n, const kernels::ArithOp& op) {
+  if constexpr (std::is_same<T, float>::value || std::is_same<T, double>::value) {
+    const T c = static_cast<T>(op.fval);
+    switch (op.kind) {
+      case kernels::OP_ADD: for (size_t i = 0; i < n; ++i) v[i] = v[i] + c; return;
+      case kernels::OP_MUL: for (size_t i = 0; i < n; ++i) v[i] = v[i] * c; return;
+      case kernels::OP_DIV: for (size_t i = 0; i < n; ++i) v[i] = v[i] / c; return;
+      default: break;
+    }
+  }
+  for (size_t i = 0; i < n; ++i) v[i] = cpu_apply<T>(v[i], op);
+}
+
 template <typename InT, typename OutT>
 void cpu_arith_t(const void* in, void* out, uint64_t n, const kernels::ArithParams& p) {
   const InT* a = static_cast<const InT*>(in);
   OutT* b = static_cast<OutT*>(out);
-  for (uint64_t i = 0; i < n; ++i) {
-    OutT v = cpu::Cast<OutT>::from(a[i]);
-    int ch = p.ch_count ? static_cast<int>((i / p.ch_size) % p.ch_count) : -1;
-    for (int k = 0; k < p.nops; ++k)
-      if (!p.ch_count || p.ops[k].ch < 0 || p.ops[k].ch == ch) v = cpu_apply<OutT>(v, p.ops[k]);
-    b[i] = v;
+  const int nch = p.ch_count > 0 ? p.ch_count : 1;
+  if constexpr (sizeof(InT) == 1) {
+    // 8-bit input (camera frames): every distinct (channel, value) through the
+    // chain once, then a table lookup per element -- identical results
+    if (p.nops > 0 && n >= static_cast<uint64_t>(1024) * nch) {
+      std::vector<OutT> lut(static_cast<size_t>(256) * nch);
+      for (int c = 0; c < nch; ++c)
+        for (int x = 0; x < 256; ++x) {
+          InT xv;
+          const uint8_t byte = static_cast<uint8_t>(x);
+          std::memcpy(&xv, &byte, 1);
+          lut[static_cast<size_t>(c) * 256 + byte] = cpu_arith_one<InT, OutT>(xv, p.ch_count ? c : -1, p);
+        }
+      if (!p.ch_count) {
+        const OutT* t = lut.data();
+        for (uint64_t i = 0; i < n; ++i) {
+          uint8_t byte;
+          std::memcpy(&byte, &a[i], 1);
+          b[i] = t[byte];
+        }
+      } else {
+        for (uint64_t i = 0; i < n; ++i) {
+          uint8_t byte;
+          std::memcpy(&byte, &a[i], 1);
+          b[i] = lut[static_cast<size_t>((i / p.ch_size) % p.ch_count) * 256 + byte];
+        }
+      }
+      return;
+    }
   }
+  if (!p.ch_count) {
+    // op at a time over cache-sized runs
+    constexpr uint64_t kRun = 2048;
+    for (uint64_t i0 = 0; i0 < n; i0 += kRun) {
+      const size_t m = static_cast<size_t>(std::min<uint64_t>(kRun, n - i0));
+      OutT* v = b + i0;
+      for (size_t i = 0; i < m; ++i) v[i] = cpu::Cast<OutT>::from(a[i0 + i]);
+      for (int k = 0; k < p.nops; ++k) cpu_apply_run<OutT>(v, m, p.ops[k]);
+    }
+    return;
+  }
+  for (uint64_t i = 0; i < n; ++i)
+    b[i] = cpu_arith_one<InT, OutT>(a[i], static_cast<int>((i / p.ch_size) % p.ch_count), p);
 }
 
 template <typename InT>

@@ -24,6 +24,7 @@
 #include <atomic>
 #include <cstdlib>
 #include <fstream>
+#include <set>
 #include <sstream>
 
 #include "comm/group.h"
@@ -452,9 +453,14 @@ class TorchInstance : public FilterInstance {
       for (auto& t : inputs) gs->static_in.push_back(in_place ? t : torch::empty_like(t, t.options()).copy_(t));
       const std::vector<at::Tensor>& src = gs->static_in;
       std::vector<c10::IValue> iv;
-      // warm up on the capture stream (lazy init, autotuning) before capturing;
-      // later instances need only one pass
-      for (int w = 0; w < (graphs_captured_ == 0 ? 3 : 1); ++w) {
+      // warm up on the capture stream (lazy init, autotuning) before the first
+      // capture of this module, one pass before a copying instance; an in-place
+      // instance (one more pooled block address of a shape already run) captures
+      // straight away -- the extra eager forward cost a whole step of GPU time
+      const std::string shape = key.substr(0, key.find('@'));
+      const int warm = graphs_captured_ == 0 ? 3 : (in_place && warmed_.count(shape)) ? 0 : 1;
+      warmed_.insert(shape);
+      for (int w = 0; w < warm; ++w) {
         iv.clear();
         for (auto& t : src) iv.push_back(prepare(t));
         std::vector<at::Tensor> tmp;
@@ -504,9 +510,11 @@ class TorchInstance : public FilterInstance {
   std::vector<float> lut_;     // the absorbed table (re-applied on hot reload)
   std::map<std::string, std::vector<std::unique_ptr<GraphState>>> graphs_;
   std::map<std::string, size_t> in_place_count_;  // in-place instances per input shape
+  std::set<std::string> warmed_;                   // input shapes run eagerly before a capture
   void clear_graphs() {
     graphs_.clear();
     in_place_count_.clear();
+    warmed_.clear();  // a reloaded module runs eagerly again before its first capture
   }
   size_t graphs_captured_ = 0;
   hipStream_t cap_stream_ = nullptr;  // private capture stream (graph_for)

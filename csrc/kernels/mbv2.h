@@ -57,10 +57,13 @@ bool ir_block(const IrBlockArgs& a, hipStream_t s);
 // Output layout of a GEMM writing into a slice of a concatenated tensor: rpb >
 // 0 -> row m goes to y + (m / rpb) * bstride + (m % rpb) * ncols, and only the
 // first ncols columns are stored (no split-K).  rpb = 0: plain y[M][N].
+// brpb > 0: a per-batch bias -- bias is [M / brpb][N] and row m adds row
+// m / brpb (a spatially constant branch folded into the GEMM; no split-K).
 struct YLayout {
   int rpb = 0;
   int ncols = 0;
   int64_t bstride = 0;
+  int brpb = 0;
 };
 void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
                  int Kpad, int Npad, int act, hipStream_t s, int tile = 0, float* ws = nullptr,

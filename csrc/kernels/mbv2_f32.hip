@@ -228,7 +228,8 @@ __global__ void __launch_bounds__(256) pw_gemm_f32_kernel(const float* __restric
             acc[i][j];
         continue;
       }
-      f32x4_t v = acc[i][j] + bv[j];
+      f32x4_t v = acc[i][j] + (yl.brpb ? *reinterpret_cast<const f32x4_t*>(bias + static_cast<int64_t>(m / yl.brpb) * N + n)
+                                        : bv[j]);
       if (res) v += rv[i][j];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], act);
@@ -1205,11 +1206,13 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) stem_ir1_f32_kernel(StemIr1F3
 // table) under 20 KB, so 8 waves are resident per CU and one wave's MFMA
 // work overlaps the others' staging / depthwise VALU work.  The price is the
 // halo: 100 stem cells per 64 outputs (1.56x) against 324 per 256 (1.27x).
-// (second launch bound: 2 waves per SIMD = 256 VGPRs; 8 such waves per CU.)
+// (second launch bound: 2 waves per SIMD = 256 VGPRs; 8 such waves per CU.
+// WL: the depthwise weights live in LDS instead of 72 VGPRs, for 3 waves per
+// SIMD = 168 VGPRs.)
 // Persistent: a resident set of waves walks the tiles; the next tile's input
 // bytes are in flight while the current one computes.
-template <int TY, int TX, bool PAIR>
-__global__ void __launch_bounds__(64, 2) stem_ir1w_f32_kernel(StemIr1F32Args a) {
+template <int TY, int TX, bool PAIR, bool WL = false>
+__global__ void __launch_bounds__(64, WL ? 3 : 2) stem_ir1w_f32_kernel(StemIr1F32Args a) {
   constexpr int HY = TY + 2, HX = TX + 2, PIN = HY * HX;
   constexpr int NBT = (PIN + 15) / 16;
   constexpr int IY = 2 * HY + 1, IX = 2 * HX + 1, PITCH = IX * 3;
@@ -1220,6 +1223,7 @@ __global__ void __launch_bounds__(64, 2) stem_ir1w_f32_kernel(StemIr1F32Args a) 
   float* xin = smem;                                             // [IY][PITCH] normalised input
   float* lut = smem + XIN;                                       // [256] input table
   f32x4_t* hid = reinterpret_cast<f32x4_t*>(smem + XIN + 256);  // [8 quads][PIN] (32 channels)
+  f32x4_t* wdl = hid + 8 * PIN;                                  // WL: [2 halves][9 taps][4 quads]
 
   const int lane = threadIdx.x;
   const int li = lane & 15, g = lane >> 4;
@@ -1237,16 +1241,31 @@ __global__ void __launch_bounds__(64, 2) stem_ir1w_f32_kernel(StemIr1F32Args a) 
     sa[1][t] = k < 27 ? a.ws[k * 32 + 16 + li] : 0.f;
     off[t] = k < 27 ? (k / 9) * PITCH + ((k % 9) / 3) * 3 + (k % 3) : 0;
   }
-  f32x4_t bs4[2], bd4[2], pa[2], wd4[2][9];
+  f32x4_t bs4[2], bd4[2], pa[2], wd4[2][WL ? 1 : 9];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int ch = 16 * h + 4 * g;  // this lane's channel quad in half h
     bs4[h] = *reinterpret_cast<const f32x4_t*>(a.bs + ch);
     bd4[h] = *reinterpret_cast<const f32x4_t*>(a.bd + ch);
     pa[h] = *reinterpret_cast<const f32x4_t*>(a.wp + li * 32 + ch);  // project A: row li, k = 16h + 4g + j
+    if constexpr (!WL) {
 #pragma unroll
-    for (int t = 0; t < 9; ++t) wd4[h][t] = *reinterpret_cast<const f32x4_t*>(a.wd + t * 32 + ch);
+      for (int t = 0; t < 9; ++t) wd4[h][t] = *reinterpret_cast<const f32x4_t*>(a.wd + t * 32 + ch);
+    }
   }
+  if constexpr (WL) {
+    // quad (h, t, q) = channels 16h + 4q .. +3 of tap t (lane 0..71 one quad each)
+    for (int i = lane; i < 72; i += 64) {
+      const int h = i / 36, t = (i / 4) % 9, q = i % 4;
+      wdl[i] = *reinterpret_cast<const f32x4_t*>(a.wd + t * 32 + 16 * h + 4 * q);
+    }
+  }
+  auto wdw = [&](int h, int t) -> f32x4_t {
+    if constexpr (WL)
+      return wdl[(h * 9 + t) * 4 + g];
+    else
+      return wd4[h][WL ? 0 : t];
+  };
   const f32x4_t bp4 = *reinterpret_cast<const f32x4_t*>(a.bp + 4 * g);
   const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
@@ -1358,8 +1377,8 @@ __global__ void __launch_bounds__(64, 2) stem_ir1w_f32_kernel(StemIr1F32Args a) 
 #pragma unroll
             for (int kx = 0; kx < 3; ++kx) {
               const f32x4_t v = hp[r * HX + kx];
-              if (r < 3) d0 = __builtin_elementwise_fma(v, wd4[h][r * 3 + kx], d0);
-              if (r > 0) d1 = __builtin_elementwise_fma(v, wd4[h][(r - 1) * 3 + kx], d1);
+              if (r < 3) d0 = __builtin_elementwise_fma(v, wdw(h, r * 3 + kx), d0);
+              if (r > 0) d1 = __builtin_elementwise_fma(v, wdw(h, (r - 1) * 3 + kx), d1);
             }
           acc0 = mfma_k16(pa[h], relu6x4(d0), acc0);
           acc1 = mfma_k16(pa[h], relu6x4(d1), acc1);
@@ -1385,7 +1404,7 @@ __global__ void __launch_bounds__(64, 2) stem_ir1w_f32_kernel(StemIr1F32Args a) 
 #pragma unroll
           for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-            for (int kx = 0; kx < 3; ++kx) d = __builtin_elementwise_fma(hp[ky * HX + kx], wd4[h][ky * 3 + kx], d);
+            for (int kx = 0; kx < 3; ++kx) d = __builtin_elementwise_fma(hp[ky * HX + kx], wdw(h, ky * 3 + kx), d);
           acc = mfma_k16(pa[h], relu6x4(d), acc);
         }
         const int gy = oy0 + qq / TX, gx = ox0 + qq % TX;
@@ -1596,7 +1615,7 @@ static void pw_gemm_f32_launch(const float* x, const float* wt, const float* bia
                                const YLayout& yl = YLayout{}) {
   dim3 grid((M + BM - 1) / BM, (N + BN - 1) / BN);
   const int kstages = (Kpad + GKT - 1) / GKT;
-  int chunk = (ws && !yl.rpb) ? gemm_kchunk(static_cast<int>(grid.x * grid.y), kstages, N, !res) : kstages;
+  int chunk = (ws && !yl.rpb && !yl.brpb) ? gemm_kchunk(static_cast<int>(grid.x * grid.y), kstages, N, !res) : kstages;
   grid.z = static_cast<unsigned>((kstages + chunk - 1) / chunk);
   if (grid.z == 1) {
     hipLaunchKernelGGL((pw_gemm_f32_kernel<BM, BN>), grid, dim3(256), 0, s, x, wt, bias, res, y, M, N, K, Kpad, Npad,
@@ -1851,16 +1870,19 @@ constexpr int kStemW = 8;
 static size_t stem_ir1w_lds_bytes() {
   constexpr int HY = kStemW + 2, HX = kStemW + 2, PIN = HY * HX;
   constexpr int NIN = (2 * HY + 1) * (2 * HX + 1) * 3;
-  return static_cast<size_t>((NIN + 3) / 4 * 4 + 256) * 4 + 16 * 8 * PIN;
+  return static_cast<size_t>((NIN + 3) / 4 * 4 + 256) * 4 + 16 * 8 * PIN + 16 * 72;
 }
 
 static bool stem_ir1w_f32(StemIr1F32Args a, hipStream_t s) {
   a.tiles_y = (a.Ho + kStemW - 1) / kStemW;
   a.tiles_x = (a.Wo + kStemW - 1) / kStemW;
   const size_t lds = stem_ir1w_lds_bytes();
-  static const bool pair = irw_env("NNSX_STEM_WAVE", 2) == 2;
-  const void* fn = pair ? reinterpret_cast<const void*>(&stem_ir1w_f32_kernel<kStemW, kStemW, true>)
-                        : reinterpret_cast<const void*>(&stem_ir1w_f32_kernel<kStemW, kStemW, false>);
+  // 2: paired rows, weights in registers; 3: paired rows, dw weights in LDS (3 waves/SIMD); 1: unpaired
+  static const int mode = irw_env("NNSX_STEM_WAVE", 2);
+  const bool pair = mode >= 2, wl = mode == 3;
+  const void* fn = wl     ? reinterpret_cast<const void*>(&stem_ir1w_f32_kernel<kStemW, kStemW, true, true>)
+                   : pair ? reinterpret_cast<const void*>(&stem_ir1w_f32_kernel<kStemW, kStemW, true>)
+                          : reinterpret_cast<const void*>(&stem_ir1w_f32_kernel<kStemW, kStemW, false>);
   static const int resident = [fn, lds] {
     int dev = 0, ncu = 256, per_cu = 1;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
@@ -1869,7 +1891,9 @@ static bool stem_ir1w_f32(StemIr1F32Args a, hipStream_t s) {
   }();
   const int tiles = a.tiles_x * a.tiles_y * a.B;
   const unsigned grid = static_cast<unsigned>(std::min(tiles, resident));
-  if (pair)
+  if (wl)
+    hipLaunchKernelGGL((stem_ir1w_f32_kernel<kStemW, kStemW, true, true>), dim3(grid), dim3(64), lds, s, a);
+  else if (pair)
     hipLaunchKernelGGL((stem_ir1w_f32_kernel<kStemW, kStemW, true>), dim3(grid), dim3(64), lds, s, a);
   else
     hipLaunchKernelGGL((stem_ir1w_f32_kernel<kStemW, kStemW, false>), dim3(grid), dim3(64), lds, s, a);

@@ -13,6 +13,13 @@ namespace kernels {
 // background when max <= threshold; colour = rgb_modifier * label | alpha.
 void segment_argmax_color(const float* prob, int labels, uint64_t pixels, uint32_t rgb_modifier, float threshold,
                           uint32_t* out, hipStream_t s);
+// tflite-deeplab on a low-resolution score map: logits [B][h][w][labels] are
+// bilinearly resized (align_corners) to H x W per label, then argmax / threshold
+// / colour as above -> out [B][H][W]; the H x W x labels map is never stored.
+void segment_upsample_argmax_color(const float* logits, int labels, int h, int w, int batch, int H, int W,
+                                   uint32_t rgb_modifier, float threshold, uint32_t* out, hipStream_t s);
+// NHWC bilinear resize with align_corners: x [B][h][w][C] -> y [B][H][W][C]
+void upsample_bilinear_nhwc(const float* x, int batch, int h, int w, int C, int H, int W, float* y, hipStream_t s);
 // snpe-deeplab: label index map (float) -> RGBA
 void segment_index_color(const float* index_map, uint64_t pixels, int max_labels, uint32_t rgb_modifier,
                          uint32_t* out, hipStream_t s);

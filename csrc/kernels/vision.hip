@@ -258,6 +258,86 @@ __global__ void __launch_bounds__(256) pose_draw_kernel(PoseDrawArgs a) {
   }
 }
 
+// ------------------------------------------------ bilinear (align_corners) ----
+// Source taps of output index dst for an in -> out resize with align_corners
+// (the rule of PyTorch's upsample_bilinear2d: src = dst * (in-1)/(out-1) in
+// fp32, i1 = i0 + 1 clamped at the last row/column).
+struct BilinearTap {
+  int i0, i1;
+  float l0, l1;
+};
+__device__ __forceinline__ BilinearTap bilinear_tap(int dst, int in, int out) {
+  const float scale = out > 1 ? static_cast<float>(in - 1) / static_cast<float>(out - 1) : 0.f;
+  const float src = scale * static_cast<float>(dst);
+  const int i0 = min(static_cast<int>(src), in - 1);
+  const float l1 = src - static_cast<float>(i0);
+  return BilinearTap{i0, i0 + (i0 < in - 1 ? 1 : 0), 1.f - l1, l1};
+}
+__device__ __forceinline__ float bilinear_mix(const BilinearTap& ty, const BilinearTap& tx, float v00, float v01,
+                                              float v10, float v11) {
+  return ty.l0 * (tx.l0 * v00 + tx.l1 * v01) + ty.l1 * (tx.l0 * v10 + tx.l1 * v11);
+}
+
+// upsample + argmax + colour in one pass: one workgroup per (output row, frame)
+// stages the two source rows of label scores ([w][L] each, e.g. 33 x 21 floats
+// for DeepLab at output stride 16) in LDS; each lane then interpolates its
+// output pixel's L scores and keeps the first maximum.  The full-resolution
+// score map (H x W x L floats) is never written.
+template <bool LDS>
+__global__ void __launch_bounds__(256) seg_upsample_argmax_kernel(const float* __restrict__ logits, int h, int w,
+                                                                  int L, int H, int W, uint32_t rgb_mod, float thr,
+                                                                  uint32_t* __restrict__ out) {
+  extern __shared__ float rows[];  // [2][w * L]
+  const int Y = blockIdx.x, b = blockIdx.y;
+  const BilinearTap ty = bilinear_tap(Y, h, H);
+  const int n = w * L;
+  const float* src = logits + static_cast<int64_t>(b) * h * n;
+  const float* r0 = src + static_cast<int64_t>(ty.i0) * n;
+  const float* r1 = src + static_cast<int64_t>(ty.i1) * n;
+  if constexpr (LDS) {
+    for (int i = threadIdx.x; i < n; i += 256) {
+      rows[i] = r0[i];
+      rows[n + i] = r1[i];
+    }
+    __syncthreads();
+    r0 = rows;
+    r1 = rows + n;
+  }
+  uint32_t* o = out + (static_cast<int64_t>(b) * H + Y) * W;
+  for (int X = threadIdx.x; X < W; X += 256) {
+    const BilinearTap tx = bilinear_tap(X, w, W);
+    const float* a0 = r0 + tx.i0 * L;
+    const float* a1 = r0 + tx.i1 * L;
+    const float* c0 = r1 + tx.i0 * L;
+    const float* c1 = r1 + tx.i1 * L;
+    float best = bilinear_mix(ty, tx, a0[0], a1[0], c0[0], c1[0]);
+    int bi = 0;
+    for (int l = 1; l < L; ++l) {
+      const float v = bilinear_mix(ty, tx, a0[l], a1[l], c0[l], c1[l]);
+      if (v > best) {
+        best = v;
+        bi = l;
+      }
+    }
+    o[X] = best > thr ? label_color(static_cast<uint32_t>(bi), rgb_mod) : 0u;
+  }
+}
+
+// plain NHWC bilinear resize (align_corners): grid (row chunks of W*C, H, B)
+__global__ void __launch_bounds__(256) upsample_bilinear_nhwc_kernel(const float* __restrict__ x, int h, int w,
+                                                                     int C, int H, int W, float* __restrict__ y) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= W * C) return;
+  const int Y = blockIdx.y, b = blockIdx.z;
+  const int X = j / C, c = j - X * C;
+  const BilinearTap ty = bilinear_tap(Y, h, H), tx = bilinear_tap(X, w, W);
+  const float* src = x + static_cast<int64_t>(b) * h * w * C + c;
+  const float* r0 = src + static_cast<int64_t>(ty.i0) * w * C;
+  const float* r1 = src + static_cast<int64_t>(ty.i1) * w * C;
+  y[(static_cast<int64_t>(b) * H + Y) * W * C + j] =
+      bilinear_mix(ty, tx, r0[tx.i0 * C], r0[tx.i1 * C], r1[tx.i0 * C], r1[tx.i1 * C]);
+}
+
 }  // namespace
 
 void segment_argmax_color(const float* prob, int labels, uint64_t pixels, uint32_t rgb_modifier, float threshold,
@@ -298,6 +378,24 @@ void pose_heatmap_argmax(const float* heat, int keypoints, int grid_w, int grid_
 void pose_draw(const PoseDrawArgs& a, int batch, hipStream_t s) {
   if (batch == 0) return;
   hipLaunchKernelGGL(pose_draw_kernel, dim3(batch), dim3(256), 0, s, a);
+}
+
+void segment_upsample_argmax_color(const float* logits, int labels, int h, int w, int batch, int H, int W,
+                                   uint32_t rgb_modifier, float threshold, uint32_t* out, hipStream_t s) {
+  if (batch == 0 || H == 0 || W == 0) return;
+  const size_t lds = 2 * static_cast<size_t>(w) * labels * sizeof(float);
+  if (lds <= 64 * 1024)
+    hipLaunchKernelGGL(seg_upsample_argmax_kernel<true>, dim3(H, batch), dim3(256), lds, s, logits, h, w, labels, H, W,
+                       rgb_modifier, threshold, out);
+  else
+    hipLaunchKernelGGL(seg_upsample_argmax_kernel<false>, dim3(H, batch), dim3(256), 0, s, logits, h, w, labels, H, W,
+                       rgb_modifier, threshold, out);
+}
+
+void upsample_bilinear_nhwc(const float* x, int batch, int h, int w, int C, int H, int W, float* y, hipStream_t s) {
+  if (batch == 0 || H == 0 || W == 0 || C == 0) return;
+  hipLaunchKernelGGL(upsample_bilinear_nhwc_kernel, dim3((W * C + 255) / 256, H, batch), dim3(256), 0, s, x, h, w, C,
+                     H, W, y);
 }
 
 }  // namespace kernels

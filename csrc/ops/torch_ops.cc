@@ -8,6 +8,7 @@
 #include <torch/library.h>
 
 #include "kernels/mbv2.h"
+#include "kernels/vision.h"
 
 namespace {
 
@@ -123,6 +124,55 @@ void pw_conv_into_cpu(const at::Tensor& x, const at::Tensor& wt, const at::Tenso
   const int64_t B = x.size(0), C = out.size(2);
   y = y.reshape({B, -1, C});
   out.slice(1, row0, row0 + y.size(1)).copy_(y);
+}
+
+// pw_conv with a per-image bias: bias [B, N] (row b of it for every pixel of
+// image b).  project(cat[a, p]) with p constant over space (DeepLab's image
+// pooling branch) is W_a . a + (W_p . p + b): one GEMM on a, no concat.
+at::Tensor pw_conv_rowbias_cuda(const at::Tensor& x, const at::Tensor& wt, const at::Tensor& bias, int64_t N,
+                                int64_t act) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 4,
+              "pw_conv_rowbias: x [B,H,W,K] f32 contiguous");
+  const int64_t B = x.size(0), HW = x.size(1) * x.size(2), K = x.size(3);
+  const int64_t Kpad = wt.size(1), Npad = wt.size(0);
+  TORCH_CHECK(bias.is_cuda() && bias.scalar_type() == at::kFloat && bias.is_contiguous() && bias.numel() == B * N,
+              "pw_conv_rowbias: bias [B,N] f32");
+  TORCH_CHECK(K % 4 == 0 && N % 4 == 0 && Kpad >= K && Npad >= N && wt.scalar_type() == at::kFloat,
+              "pw_conv_rowbias: weights");
+  at::Tensor y = at::empty({B, x.size(1), x.size(2), N}, x.options());
+  nnsx::kernels::YLayout yl;
+  yl.brpb = static_cast<int>(HW);
+  nnsx::kernels::pw_gemm_f32(x.data_ptr<float>(), wt.data_ptr<float>(), bias.data_ptr<float>(), nullptr,
+                             y.data_ptr<float>(), static_cast<int>(B * HW), static_cast<int>(N), static_cast<int>(K),
+                             static_cast<int>(Kpad), static_cast<int>(Npad), static_cast<int>(act), cur_stream(), 0,
+                             nullptr, yl);
+  return y;
+}
+
+at::Tensor pw_conv_rowbias_cpu(const at::Tensor& x, const at::Tensor& wt, const at::Tensor& bias, int64_t N,
+                               int64_t act) {
+  const int64_t K = x.size(-1), B = x.size(0);
+  at::Tensor w = wt.slice(0, 0, N).slice(1, 0, K).to(at::kFloat);
+  at::Tensor v = at::matmul(x.to(at::kFloat), w.t()) + bias.reshape({B, 1, 1, N});
+  return act_ref(v, act);
+}
+
+// NHWC bilinear resize with align_corners (F.interpolate(..., "bilinear",
+// align_corners=True) on channels-last data, without the permutes)
+at::Tensor upsample_bilinear_cuda(const at::Tensor& x, int64_t H, int64_t W) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 4,
+              "upsample_bilinear: x [B,h,w,C] f32 contiguous");
+  TORCH_CHECK(H > 0 && W > 0 && W * x.size(3) < (int64_t{1} << 31), "upsample_bilinear: size");
+  at::Tensor y = at::empty({x.size(0), H, W, x.size(3)}, x.options());
+  nnsx::kernels::upsample_bilinear_nhwc(x.data_ptr<float>(), static_cast<int>(x.size(0)), static_cast<int>(x.size(1)),
+                                        static_cast<int>(x.size(2)), static_cast<int>(x.size(3)), static_cast<int>(H),
+                                        static_cast<int>(W), y.data_ptr<float>(), cur_stream());
+  return y;
+}
+
+at::Tensor upsample_bilinear_cpu(const at::Tensor& x, int64_t H, int64_t W) {
+  at::Tensor v = at::upsample_bilinear2d(x.permute({0, 3, 1, 2}), {H, W}, true);
+  return v.permute({0, 2, 3, 1}).contiguous();
 }
 
 // ------------------------------------------------------------ dw_conv ----
@@ -431,6 +481,8 @@ bool ir_supported(int64_t stride, int64_t cin, int64_t hid, int64_t cout) {
 TORCH_LIBRARY(nnsx, m) {
   m.def("pw_conv(Tensor x, Tensor wt, Tensor bias, Tensor? res, int N, int act, bool out_f32) -> Tensor");
   m.def("pw_conv_into(Tensor x, Tensor wt, Tensor bias, Tensor(a!) out, int row0, int n, int act) -> ()");
+  m.def("pw_conv_rowbias(Tensor x, Tensor wt, Tensor bias, int N, int act) -> Tensor");
+  m.def("upsample_bilinear(Tensor x, int H, int W) -> Tensor");
   m.def("dw_conv(Tensor x, Tensor w, Tensor bias, int stride, int act, int dilation=1) -> Tensor");
   m.def("stem_conv(Tensor x, Tensor w, Tensor bias, int act, bool out_f32=False) -> Tensor");
   m.def("stem_conv_u8(Tensor x, Tensor w, Tensor bias, int act, Tensor lut, bool out_f32=False) -> Tensor");
@@ -450,6 +502,8 @@ TORCH_LIBRARY(nnsx, m) {
 TORCH_LIBRARY_IMPL(nnsx, CUDA, m) {
   m.impl("pw_conv", pw_conv_cuda);
   m.impl("pw_conv_into", pw_conv_into_cuda);
+  m.impl("pw_conv_rowbias", pw_conv_rowbias_cuda);
+  m.impl("upsample_bilinear", upsample_bilinear_cuda);
   m.impl("dw_conv", dw_conv_cuda);
   m.impl("stem_conv", stem_conv_cuda);
   m.impl("stem_conv_u8", stem_conv_u8_cuda);
@@ -463,6 +517,8 @@ TORCH_LIBRARY_IMPL(nnsx, CUDA, m) {
 TORCH_LIBRARY_IMPL(nnsx, CPU, m) {
   m.impl("pw_conv", pw_conv_cpu);
   m.impl("pw_conv_into", pw_conv_into_cpu);
+  m.impl("pw_conv_rowbias", pw_conv_rowbias_cpu);
+  m.impl("upsample_bilinear", upsample_bilinear_cpu);
   m.impl("dw_conv", dw_conv_cpu);
   m.impl("stem_conv", stem_conv_cpu);
   m.impl("stem_conv_u8", stem_conv_u8_cpu);

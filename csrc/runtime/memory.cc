@@ -76,30 +76,50 @@ size_t DeviceBufferPool::blocks() const {
 MemoryPtr DeviceBufferPool::acquire(hipStream_t stream) {
   int slot = -1;
   void* p = nullptr;
+  hipEvent_t wait = nullptr;
   {
     std::lock_guard<std::mutex> lk(mu_);
-    for (size_t i = 0; i < blocks_.size(); ++i)
-      if (blocks_[i].free) {
-        slot = static_cast<int>(i);
-        break;
+    hip::DeviceGuard g(dev_);
+    // 1. a free block whose previous readers are done -- the most recently
+    // returned one, so the steady state cycles through as few addresses as it
+    // needs (a consumer keying per-address state, e.g. an in-place hipGraph
+    // instance per block, then sees every address during warm-up)
+    int oldest = -1;
+    for (size_t i = 0; i < blocks_.size(); ++i) {
+      Block& b = blocks_[i];
+      if (!b.free) continue;
+      if (!b.released || hipEventQuery(b.released) == hipSuccess) {
+        if (slot < 0 || b.seq > blocks_[static_cast<size_t>(slot)].seq) slot = static_cast<int>(i);
+      } else if (oldest < 0 || b.seq < blocks_[static_cast<size_t>(oldest)].seq) {
+        oldest = static_cast<int>(i);
       }
+    }
+    // 2. grow the pool
     if (slot < 0 && blocks_.size() < max_) {
       Block b;
       b.ptr = hip::device_alloc(dev_, size_, stream);
       blocks_.push_back(b);
       slot = static_cast<int>(blocks_.size()) - 1;
     }
+    // 3. the oldest free block, once its readers are done (host wait below)
+    if (slot < 0 && oldest >= 0) {
+      slot = oldest;
+      wait = blocks_[static_cast<size_t>(oldest)].released;
+    }
     if (slot >= 0) {
       Block& b = blocks_[static_cast<size_t>(slot)];
       b.free = false;
+      wait = b.released;  // complete (case 1) or waited for below (case 3); then recycled
+      b.released = nullptr;
       p = b.ptr;
-      if (b.released) {  // previous readers first (stream-ordered, no host wait)
-        hip::DeviceGuard g(dev_);
-        hip::check(hipStreamWaitEvent(stream, b.released, 0), "pool acquire wait");
-      }
     }
   }
   if (slot < 0) return Memory::alloc_device(size_, dev_, stream);  // all blocks out: no pooling
+  if (wait) {
+    hip::DeviceGuard g(dev_);
+    hip::check(hipEventSynchronize(wait), "pool acquire wait");
+    hip::event_put(dev_, wait);
+  }
   std::weak_ptr<DeviceBufferPool> wp = shared_from_this();
   const int dev = dev_;
   const size_t size = size_;
@@ -128,6 +148,7 @@ void DeviceBufferPool::put_back(int slot, hipEvent_t released) {
   if (b.released) hip::event_put(dev_, b.released);
   b.released = released;
   b.free = true;
+  b.seq = ++seq_;
 }
 
 MemoryPtr Memory::wrap(void* data, size_t size, MemPlace place, int device, Release release) {

@@ -119,8 +119,13 @@ class Memory : public std::enable_shared_from_this<Memory> {
 };
 
 // A pool of equal-size device blocks (the GstBufferPool of a device-producing
-// element): acquire() hands out a free block -- the acquiring stream waits for
-// the block's previous readers, so nothing ever blocks on the host -- and the
+// element): acquire() hands out a free block whose previous readers are done
+// (their release event has completed), else grows the pool, else waits on the
+// HOST for the oldest free block -- the acquiring stream never carries a
+// cross-queue wait.  (Measured: an SDMA upload queued behind a hipStreamWaitEvent
+// on the compute queue's event blocked the uploading thread inside
+// hipMemcpyAsync for ~7.8 ms and stalled a running kernel by ~0.9 ms; see
+// profiles/r3_step_stall_trace.txt.)  The
 // block returns to the pool when its last Memory reference drops, instead of
 // a hipFreeAsync per buffer (a 77 MB batch free costs milliseconds of host
 // time).  Acquired memories are tagged kPoolTag = pool id and kSlotTag = block
@@ -147,12 +152,14 @@ class DeviceBufferPool : public std::enable_shared_from_this<DeviceBufferPool> {
     void* ptr = nullptr;
     hipEvent_t released = nullptr;  // recorded after the last reader of the previous use
     bool free = true;
+    uint64_t seq = 0;  // put_back order (oldest free block = smallest)
   };
   int dev_;
   size_t size_, max_;
   uint64_t id_;
   mutable std::mutex mu_;
   std::vector<Block> blocks_;
+  uint64_t seq_ = 0;
 };
 
 // Meta a buffer carries across elements.

@@ -11,9 +11,18 @@ stride 1 + dilation 2 (33x33 at 513 input).  Head: the mobile ASPP variant
 and a bilinear (align_corners) upsample back to the input size.
 
 * ``DeepLabV3MobileNetV2`` -- plain fp32 oracle (NCHW internally).
-* ``FusedDeepLabV3``       -- BN-folded NHWC bf16 on the CDNA4 kernels
-  (dilated depthwise via ``nnsx::dw_conv(..., dilation)``), channels-last
-  bilinear upsample so the decoder input is produced without a transpose.
+* ``FusedDeepLabV3``       -- BN-folded NHWC bf16 / fp32 on the CDNA4 kernels
+  (dilated depthwise via ``nnsx::dw_conv(..., dilation)``).  fp32 head: the
+  image-pooling branch is constant over space, so ``project(cat[a, p])`` is
+  one GEMM on ``a`` with a per-image bias ``W_p . p + b`` (``pw_conv_rowbias``,
+  no concat); the classifier writes the 21 labels straight into a contiguous
+  ``[B, 33, 33, 21]`` map (``pw_conv_into``); the resize is the hand-written
+  NHWC bilinear kernel (``nnsx::upsample_bilinear``).
+* ``lowres=True`` (model names ``deeplab_fused_lowres*``) -- the model ships the
+  33x33 logits and the pipeline's decoder resizes them
+  (``tensor_decoder mode=image_segment option1=tflite-deeplab option3=513:513``:
+  upsample + argmax + colour map in one pass, kernels/vision.hip), so the
+  513x513x21 score map (22 MB per frame) never exists.  Same decoded frames.
 """
 from __future__ import annotations
 
@@ -83,10 +92,11 @@ class FusedDeepLabV3(nn.Module):
         super().__init__()
 
     @classmethod
-    def from_reference(cls, m: DeepLabV3MobileNetV2, precision: str = "bf16") -> "FusedDeepLabV3":
+    def from_reference(cls, m: DeepLabV3MobileNetV2, precision: str = "bf16", lowres: bool = False) -> "FusedDeepLabV3":
         self = cls()
         m = m.eval()
         self.f32 = precision == "fp32"
+        self.lowres = bool(lowres)
         stem: ConvBNReLU = m.features[0]
         w, b = _fold(stem[0], stem[1])
         self.register_buffer("stem_w", w.permute(2, 3, 1, 0).contiguous())
@@ -102,6 +112,11 @@ class FusedDeepLabV3(nn.Module):
         self.aspp_conv = PW(*_fold(m.aspp_conv[0], m.aspp_conv[1]), act=1, precision=precision)
         self.aspp_pool = PW(*_fold(m.aspp_pool[0], m.aspp_pool[1]), act=1, precision=precision)
         self.project = PW(*_fold(m.project[0], m.project[1]), act=1, precision=precision)
+        # fp32: project split at the concat boundary (a: the 1x1 branch, p: image pooling)
+        wpj, bpj = _fold(m.project[0], m.project[1])
+        na = int(m.aspp_conv[0].out_channels)
+        self.project_a = PW(wpj[:, :na].contiguous(), torch.zeros(wpj.shape[0]), act=1, precision=precision)
+        self.project_p = PW(wpj[:, na:].contiguous(), bpj, act=0, precision=precision)
         wc = m.classifier.weight.detach().float()
         bc = m.classifier.bias.detach().float()
         n = wc.shape[0]
@@ -119,17 +134,35 @@ class FusedDeepLabV3(nn.Module):
         h = stem(x, self.stem_w, self.stem_b, self.in_lut, self.f32)
         for blk in self.blocks:
             h = blk(h)
+        if self.f32:
+            return self._head_f32(h)
         a = self.aspp_conv(h)
         pooled = torch.ops.nnsx.avgpool(h)  # [B, 320]
         p = self.aspp_pool(pooled.view(pooled.shape[0], 1, 1, pooled.shape[1]))
         cat = torch.cat([a, p.expand(a.shape[0], a.shape[1], a.shape[2], p.shape[3])], 3).contiguous()
         y = self.classifier(self.project(cat))[..., : self.num_classes]
+        if self.lowres:
+            return y.contiguous()
         # NHWC viewed as channels-last NCHW: interpolate keeps channels-last, so the
         # final permute back is free and the decoder gets labels innermost
         y = y.permute(0, 3, 1, 2)
         y = F.interpolate(y, size=(self.out_size, self.out_size), mode="bilinear", align_corners=True)
         return y.permute(0, 2, 3, 1).contiguous()
 
+    def _head_f32(self, h: torch.Tensor) -> torch.Tensor:
+        B, hh, ww = h.shape[0], h.shape[1], h.shape[2]
+        a = self.aspp_conv(h)
+        pooled = torch.ops.nnsx.avgpool(h)  # [B, 320]
+        p = self.aspp_pool(pooled.view(B, 1, 1, pooled.shape[1]))
+        c = self.project_p(p)  # [B, 1, 1, 256] = W_p . p + b, the per-image bias
+        y = torch.ops.nnsx.pw_conv_rowbias(a, self.project_a.wt, c.view(B, c.shape[3]), self.project_a.n, 1)
+        logits = torch.empty((B, hh * ww, self.num_classes), dtype=torch.float32, device=h.device)
+        torch.ops.nnsx.pw_conv_into(y, self.classifier.wt, self.classifier.bias, logits, 0, self.num_classes, 0)
+        logits = logits.view(B, hh, ww, self.num_classes)
+        if self.lowres:
+            return logits
+        return torch.ops.nnsx.upsample_bilinear(logits, self.out_size, self.out_size)
 
-def fused_deeplabv3(seed: int = 0, precision: str = "bf16") -> FusedDeepLabV3:
-    return FusedDeepLabV3.from_reference(deeplabv3(seed), precision).eval()
+
+def fused_deeplabv3(seed: int = 0, precision: str = "bf16", lowres: bool = False) -> FusedDeepLabV3:
+    return FusedDeepLabV3.from_reference(deeplabv3(seed), precision, lowres).eval()

@@ -61,10 +61,13 @@ def build_model(name: str, seed: int = 0, layout: str = "nchw", num_classes: int
         from .deeplab import deeplabv3
 
         return deeplabv3(seed=seed).eval()
-    elif name in ("deeplabv3_fused", "deeplab_fused", "deeplab_fused_fp32"):
+    elif name in ("deeplabv3_fused", "deeplab_fused", "deeplab_fused_fp32", "deeplab_fused_lowres",
+                  "deeplab_fused_lowres_fp32"):
         from .deeplab import fused_deeplabv3
 
-        return fused_deeplabv3(seed=seed, precision="fp32" if name.endswith("_fp32") else "bf16")
+        # _lowres: 33x33 logits out; the image_segment decoder resizes (option3=513:513)
+        return fused_deeplabv3(seed=seed, precision="fp32" if name.endswith("_fp32") else "bf16",
+                               lowres="_lowres" in name)
     elif name in ("posenet", "pose"):
         from .posenet import posenet
 

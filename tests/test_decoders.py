@@ -203,6 +203,39 @@ def test_image_segment_batched(nns):
         np.testing.assert_array_equal(out[b], single[0])
 
 
+def _seg_resized_expected(prob, W, H, thr=0.5, max_labels=20):
+    """argmax of F.interpolate(bilinear, align_corners) of the label scores"""
+    import torch
+    t = torch.from_numpy(prob).permute(0, 3, 1, 2)
+    up = torch.nn.functional.interpolate(t, size=(H, W), mode="bilinear", align_corners=True).permute(0, 2, 3, 1)
+    best, idx = up.max(-1)
+    col = np.vectorize(lambda l: _seg_color(int(l), max_labels), otypes=[np.uint32])(idx.numpy())
+    return np.where(best.numpy() > thr, col, 0).astype(np.uint32), up.numpy()
+
+
+def test_image_segment_option3_resizes_before_argmax(nns):
+    """nnsx option3=W:H: a low-resolution score map is resized (bilinear,
+    align_corners) per label before the argmax -- the decoded frame equals
+    argmax(F.interpolate(...)) of the full-resolution scores"""
+    rng = np.random.default_rng(3)
+    b, h, w, L, W, H = 2, 5, 6, 21, 23, 17
+    prob = rng.uniform(0, 1, (b, h, w, L)).astype(np.float32)
+    out, caps = _seg_run(nns, "tflite-deeplab", prob, f"{L}:{w}:{h}:{b}", extra="option3=23:17")
+    assert caps.get("width") == W and caps.get("height") == H
+    exp, up = _seg_resized_expected(prob, W, H)
+    for i in range(b):
+        got = out[i].reshape(H, W)
+        diff = got != exp[i]
+        if diff.any():  # only where two labels tie to fp32 rounding (different fma order)
+            s = np.sort(up[i][diff], -1)
+            assert np.all(s[:, -1] - s[:, -2] < 1e-5), np.argwhere(diff)[:4]
+    # same size: option3 is a no-op
+    out2, caps2 = _seg_run(nns, "tflite-deeplab", prob[:1], f"{L}:{w}:{h}:1", extra=f"option3={w}:{h}")
+    ref, _ = _seg_run(nns, "tflite-deeplab", prob[:1], f"{L}:{w}:{h}:1")
+    assert caps2.get("width") == w
+    np.testing.assert_array_equal(out2[0], ref[0])
+
+
 # ---------------------------------------------------------- pose_estimation ----
 
 def test_pose_heatmap_only(nns):

@@ -146,6 +146,25 @@ def test_segment_device_matches_host(nns):
         np.testing.assert_array_equal(a, b)
 
 
+def test_segment_resize_device_matches_host(nns):
+    """option3: the fused resize + argmax + colour kernel against the host
+    decoder and argmax(F.interpolate) (ties within fp32 rounding excepted)"""
+    from test_decoders import _seg_resized_expected, _seg_run
+    rng = np.random.default_rng(6)
+    prob = rng.uniform(0, 1, (3, 33, 33, 21)).astype(np.float32)
+    host, caps = _seg_run(nns, "tflite-deeplab", prob, "21:33:33:3", dev=-1, extra="option3=513:513")
+    dev, _ = _seg_run(nns, "tflite-deeplab", prob, "21:33:33:3", dev=0, extra="option3=513:513")
+    assert caps.get("width") == 513 and len(dev) == 3
+    exp, up = _seg_resized_expected(prob, 513, 513)
+    for i, (a, b) in enumerate(zip(host, dev)):
+        for got in (a, b):
+            diff = got.reshape(513, 513) != exp[i]
+            if diff.any():
+                srt = np.sort(up[i][diff], -1)
+                assert np.all(srt[:, -1] - srt[:, -2] < 1e-5), np.argwhere(diff)[:4]
+        assert (a != b).mean() < 1e-4
+
+
 def test_pose_device_matches_host(nns):
     rng = np.random.default_rng(7)
     K, gw, gh, B = 14, 33, 33, 2

@@ -47,6 +47,30 @@ def test_deeplab_fp32_fused_matches_torch_fp32():
     assert agree > 0.995, agree
 
 
+def test_deeplab_fp32_lowres_and_kernels():
+    """the lowres export (33x33 logits; the decoder resizes) and the hand-written
+    NHWC bilinear resize / per-image-bias GEMM against their torch forms"""
+    m = deeplab.deeplabv3(seed=2)
+    f = torch.jit.script(deeplab.FusedDeepLabV3.from_reference(m, "fp32").cuda().eval())
+    lo = torch.jit.script(deeplab.FusedDeepLabV3.from_reference(m, "fp32", lowres=True).cuda().eval())
+    x = _u8(2, 513, 4)
+    with torch.no_grad():
+        fy = f(x)
+        ly = lo(x)
+    assert ly.shape == (2, 33, 33, 21)
+    up = torch.ops.nnsx.upsample_bilinear(ly, 513, 513)
+    assert torch.equal(up, fy)
+    ref = torch.nn.functional.interpolate(ly.permute(0, 3, 1, 2), size=(513, 513), mode="bilinear",
+                                          align_corners=True).permute(0, 2, 3, 1)
+    assert _rel(up, ref) < 1e-6
+    a = torch.randn(3, 33, 33, 256, device="cuda")
+    wt = torch.randn(256, 256, device="cuda")
+    bias = torch.randn(3, 256, device="cuda")
+    r = torch.ops.nnsx.pw_conv_rowbias(a, wt, bias, 256, 1)
+    exp = (a.double() @ wt.double().t() + bias.double().view(3, 1, 1, 256)).clamp(0, 6)
+    assert _rel(r, exp) < 1e-5
+
+
 def test_posenet_fp32_fused_matches_torch_fp32():
     m = posenet.posenet(seed=3).cuda().eval()
     f = torch.jit.script(posenet.FusedPoseNet.from_reference(posenet.posenet(seed=3), "fp32").cuda().eval())

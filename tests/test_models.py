@@ -51,6 +51,35 @@ def test_deeplab_shapes_and_fused():
     _close(fy, y, 0.25)
 
 
+def test_deeplab_fp32_head_folds_the_pooling_branch():
+    """fp32 head: project(cat[a, p]) as one GEMM on a + a per-image bias, the
+    classifier written into a contiguous 21-label map, the hand-written resize;
+    lowres ships the 33x33 logits the decoder resizes"""
+    m = deeplab.deeplabv3(seed=2)
+    x = (torch.rand(2, 513, 513, 3) * 255).to(torch.uint8)
+    f = deeplab.FusedDeepLabV3.from_reference(m, "fp32")
+    lo = deeplab.FusedDeepLabV3.from_reference(m, "fp32", lowres=True)
+    with torch.no_grad():
+        y = m(x.float() / 255.0)
+        fy = f(x)
+        ly = lo(x)
+    assert fy.shape == y.shape == (2, 513, 513, 21) and fy.is_contiguous()
+    rel = ((fy - y).norm() / y.norm()).item()
+    assert rel < 1e-4, rel
+    assert ly.shape == (2, 33, 33, 21) and ly.is_contiguous()
+    up = torch.ops.nnsx.upsample_bilinear(ly, 513, 513)
+    assert torch.equal(up, fy)
+    ref = torch.nn.functional.interpolate(ly.permute(0, 3, 1, 2), size=(513, 513), mode="bilinear",
+                                          align_corners=True).permute(0, 2, 3, 1)
+    assert torch.allclose(up, ref, rtol=1e-5, atol=1e-5)
+    # the per-image bias op on its own
+    a = torch.randn(2, 3, 4, 16)
+    wt = torch.randn(8, 16)
+    bias = torch.randn(2, 8)
+    r = torch.ops.nnsx.pw_conv_rowbias(a, wt, bias, 8, 0)
+    assert torch.allclose(r, a @ wt.t() + bias.view(2, 1, 1, 8), atol=1e-5)
+
+
 def test_posenet_shapes_and_fused():
     m = posenet.posenet(seed=3)
     x = torch.rand(2, 257, 257, 3)
