@@ -745,8 +745,12 @@ class TensorConverter : public Element {
   // device tensors of the steady size come from the recycled block pool
   MemoryPtr dev_alloc(size_t size, int dev, hipStream_t s) {
     if (pool_blocks_ <= 0) return Memory::alloc_device(size, dev, s);
-    if (!pool_ || pool_->device() != dev || pool_->block_size() != size)
+    if (!pool_ || pool_->device() != dev || pool_->block_size() != size) {
       pool_ = DeviceBufferPool::create(dev, size, static_cast<size_t>(pool_blocks_));
+      // every block up front: a consumer keying per-address state (in-place
+      // hipGraph instances) can prepare all of it at the first frame
+      pool_->preallocate(s);
+    }
     return pool_->acquire(s);
   }
   bool configured_ = false;

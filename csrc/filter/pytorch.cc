@@ -353,7 +353,13 @@ class TorchInstance : public FilterInstance {
     std::shared_ptr<std::atomic<int>> held;  // static outputs handed out as they are
     bool pooled = dev_idx >= 0 && !in.empty();
     for (auto& m : in) pooled = pooled && m->on_device() && m->root()->tags().count(DeviceBufferPool::kPoolTag);
-    GraphState* gs = use_graph_ && dev_idx >= 0 ? graph_for(inputs, s, dev_idx, pooled) : nullptr;
+    PoolRef pref;
+    if (pooled && in.size() == 1) {
+      Memory* root = in[0]->root();
+      pref.id = static_cast<uint64_t>(root->tags().at(DeviceBufferPool::kPoolTag));
+      pref.offset = static_cast<size_t>(static_cast<const char*>(in[0]->data()) - static_cast<const char*>(root->data()));
+    }
+    GraphState* gs = use_graph_ && dev_idx >= 0 ? graph_for(inputs, s, dev_idx, pooled, pref) : nullptr;
     if (gs) {
       // an instance whose static outputs no downstream element holds: the replay
       // rewrites them and hands them out as they are (no copy); they return to
@@ -412,7 +418,14 @@ class TorchInstance : public FilterInstance {
   static constexpr size_t kInstances = 6;
   static constexpr size_t kInPlace = 12;
   static constexpr size_t kCopyOutBytes = 64u << 20;
-  GraphState* graph_for(const std::vector<at::Tensor>& inputs, hipStream_t s, int dev_idx, bool pooled) {
+  // the pool a single pooled input came from (id 0: none) and its offset in the block
+  struct PoolRef {
+    uint64_t id = 0;
+    size_t offset = 0;
+  };
+
+  GraphState* graph_for(const std::vector<at::Tensor>& inputs, hipStream_t s, int dev_idx, bool pooled,
+                        const PoolRef& pref) {
     std::string key;
     for (auto& t : inputs) {
       for (auto d : t.sizes()) key += std::to_string(d) + "x";
@@ -427,7 +440,9 @@ class TorchInstance : public FilterInstance {
         if (g->copy_out || copy_out_ || g->out_held->load() == 0) return g;
       } else if (in_place_count_[key] < kInPlace) {
         ++in_place_count_[key];
-        return capture(graphs_[pkey], inputs, s, dev_idx, pkey, true);
+        GraphState* g = capture(graphs_[pkey], inputs, s, dev_idx, pkey, true);
+        precapture_pool(inputs, key, s, dev_idx, pref);
+        return g;
       }
     }
     auto& set = graphs_[key];
@@ -435,6 +450,28 @@ class TorchInstance : public FilterInstance {
       if (g->copy_out || g->out_held->load() == 0) return g.get();  // (never held with copy_out_)
     if (set.size() >= kInstances) return nullptr;
     return capture(set, inputs, s, dev_idx, key, false);
+  }
+
+  // the other blocks of the input's pool get their in-place instances now, at
+  // the first frame of this shape (a capture costs ~1 ms of host time: taken
+  // lazily, each new block address stalled the stream once in steady state)
+  void precapture_pool(const std::vector<at::Tensor>& inputs, const std::string& key, hipStream_t s, int dev_idx,
+                       const PoolRef& pref) {
+    if (!pref.id || inputs.size() != 1) return;
+    auto pool = DeviceBufferPool::find(pref.id);
+    if (!pool) return;
+    const size_t bytes = inputs[0].numel() * inputs[0].element_size();
+    if (pref.offset + bytes > pool->block_size()) return;
+    for (void* base : pool->block_addresses()) {
+      if (in_place_count_[key] >= kInPlace) break;
+      void* p = static_cast<char*>(base) + pref.offset;
+      const std::string pk = key + "@" + std::to_string(reinterpret_cast<uintptr_t>(p)) + ";";
+      auto it = graphs_.find(pk);
+      if (it != graphs_.end() && !it->second.empty()) continue;
+      std::vector<at::Tensor> t{torch::from_blob(p, inputs[0].sizes(), inputs[0].options())};
+      ++in_place_count_[key];
+      capture(graphs_[pk], t, s, dev_idx, pk, true);
+    }
   }
 
   GraphState* capture(std::vector<std::unique_ptr<GraphState>>& set, const std::vector<at::Tensor>& inputs,

@@ -99,10 +99,16 @@ struct IrBlockF32Args {
   int Ho = 0, Wo = 0, tiles_x = 0, tiles_y = 0;
   int hsplit = 1;  // hidden-channel parts per tile (wave-split kernel)
   float* ws = nullptr;  // partial-sum workspace (ir_block_f32_workspace_bytes; small batches)
+  // per-tile tickets, zeroed before the launch (ir_block_f32_tickets entries):
+  // the last part of a tile to finish adds the slabs in the same launch
+  // instead of a separate reduce kernel
+  int* tickets = nullptr;
 };
 bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout, bool has_expand);
 // device workspace ir_block_f32 needs for these args (0 = none)
 size_t ir_block_f32_workspace_bytes(const IrBlockF32Args& a);
+// int tickets (zeroed) the in-launch combine of hidden parts wants (0: none)
+size_t ir_block_f32_tickets(const IrBlockF32Args& a);
 // expand 1x1 + ReLU6 + depthwise 3x3 + ReLU6 in one kernel, the depthwise
 // output to y [B][Ho][Wo][hid] (the hidden map never touches HBM; the caller
 // runs the project as a GEMM).  wp / bp / cout / residual are unused.

@@ -749,6 +749,10 @@ __device__ __forceinline__ void wave_sync() {
 // index tables) and writes zeros for out-of-image cells; FULL = false (small
 // maps, where every tile touches the border): only the in-image pixels are
 // expanded (compact index, halos zeroed once per tile).
+// (A persistent variant -- a resident grid walking the tiles with the next
+// tile's input prefetched into registers -- needed 190 VGPRs on the 112 -> 56
+// block, 2 waves per SIMD instead of 3, and ran 757 vs 545 us at batch 512:
+// profiles/r3_irw_persistent_ab_b512.txt.)
 template <int S, int TY, int TX, int KIN, int NOT, int NW, bool FULL>
 __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FULL>::MINB)) irw_f32_kernel(IrBlockF32Args a) {
   using G = IrwGeom<S, TY, TX, KIN, NOT, NW, FULL>;
@@ -767,20 +771,7 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, g = lane >> 4;
   const int nparts = a.hsplit;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);  // the parts of a tile stay adjacent (same XCD / L2)
-  const int part = wg % nparts, tile = wg / nparts;
   const int tiles_img = a.tiles_x * a.tiles_y;
-  const int b = tile / tiles_img;
-  const int tyx = tile - b * tiles_img;
-  const int oy0 = (tyx / a.tiles_x) * TY, ox0 = (tyx % a.tiles_x) * TX;
-  const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
-  const int ry0 = max(iy0, 0), ry1 = min(iy0 + TIY, a.H);
-  const int rx0 = max(ix0, 0), rx1 = min(ix0 + TIX, a.W);
-  const int RW = rx1 - rx0, NC = FULL ? PIN : (ry1 - ry0) * RW;
-  // c / RW for the small compact indices (c < 1024): (c + 0.5) * (1 / RW) in
-  // fp32 is at least 0.5 / RW away from an integer, so truncation is exact
-  const float rrw = 1.f / static_cast<float>(RW);
-  const float* xb = a.x + static_cast<int64_t>(b) * a.H * a.W * a.cin;
 
   // ---- stage the input tile (coalesced reads: consecutive threads, consecutive
   // quads).  Two phases with branch-free loads: every load of the tile is
@@ -789,34 +780,55 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
   // load / s_waitcnt vmcnt(0) / store per iteration, one exposed memory
   // latency per 256 quads of the tile.
   constexpr int NSV = NC16 * KQ, NSIT = (NSV + NT - 1) / NT;
-  {
-    f32x4_t sv[NSIT];
-    bool sok[NSIT];
+  f32x4_t sv[NSIT];
+  bool sok[NSIT];
+  // c / RW for the small compact indices (c < 1024): (c + 0.5) * (1 / RW) in
+  // fp32 is at least 0.5 / RW away from an integer, so truncation is exact
+  auto load_tile = [&](int t) {
+    const int tb = t / tiles_img, tt = t - tb * tiles_img;
+    const int ty0 = (tt / a.tiles_x) * TY * S - 1, tx0 = (tt % a.tiles_x) * TX * S - 1;
+    const int qy0 = max(ty0, 0), qy1 = min(ty0 + TIY, a.H);
+    const int qx0 = max(tx0, 0), qx1 = min(tx0 + TIX, a.W);
+    const int qw = qx1 - qx0, qn = FULL ? PIN : (qy1 - qy0) * qw;
+    const float qr = 1.f / static_cast<float>(qw);
+    const float* qb = a.x + static_cast<int64_t>(tb) * a.H * a.W * a.cin;
 #pragma unroll
     for (int it = 0; it < NSIT; ++it) {
       const int v = tid + it * NT;
       const int c = v / KQ, kq = v - c * KQ;
       int yy, xx;
       if constexpr (FULL) {
-        yy = iy0 + c / TIX;
-        xx = ix0 + c % TIX;
+        yy = ty0 + c / TIX;
+        xx = tx0 + c % TIX;
       } else {
-        const int cy = static_cast<int>((static_cast<float>(c) + 0.5f) * rrw);
-        yy = ry0 + cy;
-        xx = rx0 + c - cy * RW;
+        const int cy = static_cast<int>((static_cast<float>(c) + 0.5f) * qr);
+        yy = qy0 + cy;
+        xx = qx0 + c - cy * qw;
       }
-      sok[it] = (NSV % NT == 0 || v < NSV) && c < NC && kq * 4 < a.cin && yy >= 0 && yy < a.H && xx >= 0 &&
+      sok[it] = (NSV % NT == 0 || v < NSV) && c < qn && kq * 4 < a.cin && yy >= 0 && yy < a.H && xx >= 0 &&
                 xx < a.W;
       const int64_t off = sok[it] ? (static_cast<int64_t>(yy) * a.W + xx) * a.cin + kq * 4 : 0;
-      sv[it] = *reinterpret_cast<const f32x4_t*>(xb + off);
+      sv[it] = *reinterpret_cast<const f32x4_t*>(qb + off);
     }
+  };
+
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);  // the parts of a tile stay adjacent (same XCD / L2)
+  const int part = wg % nparts, tile = wg / nparts;
+  const int b = tile / tiles_img;
+  const int tyx = tile - b * tiles_img;
+  const int oy0 = (tyx / a.tiles_x) * TY, ox0 = (tyx % a.tiles_x) * TX;
+  const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
+  const int ry0 = max(iy0, 0), ry1 = min(iy0 + TIY, a.H);
+  const int rx0 = max(ix0, 0), rx1 = min(ix0 + TIX, a.W);
+  const int RW = rx1 - rx0, NC = FULL ? PIN : (ry1 - ry0) * RW;
+  const float rrw = 1.f / static_cast<float>(RW);
+  load_tile(tile);
 #pragma unroll
-    for (int it = 0; it < NSIT; ++it) {
-      const int v = tid + it * NT;
-      if (NSV % NT != 0 && v >= NSV) break;
-      const int c = v / KQ, kq = v - c * KQ;
-      xs[kq * XSP + (c ^ (kq & 3))] = sok[it] ? sv[it] : f32x4_t{0.f, 0.f, 0.f, 0.f};
-    }
+  for (int it = 0; it < NSIT; ++it) {
+    const int v = tid + it * NT;
+    if (NSV % NT != 0 && v >= NSV) break;
+    const int c = v / KQ, kq = v - c * KQ;
+    xs[kq * XSP + (c ^ (kq & 3))] = sok[it] ? sv[it] : f32x4_t{0.f, 0.f, 0.f, 0.f};
   }
   // out-of-image halo cells of every wave's hidden image = the depthwise zero padding
   // (FULL: the expand itself writes them as zeros)
@@ -1033,6 +1045,41 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
       }
     }
   }
+  if (!a.ws || !a.tickets) return;
+
+  // ---- in-launch combine of the hidden parts: every part publishes its slab
+  // with an agent-scope release and draws a ticket; the last of the tile's
+  // parts acquires and adds the slabs in part order, + bias (+ residual) --
+  // the same sums in the same order as irw_reduce, without its launch
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave's slab stores issued and done; the LDS is free
+  int* flag = reinterpret_cast<int*>(smem);
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int t = __hip_atomic_fetch_add(a.tickets + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == nparts - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  const int64_t plane = static_cast<int64_t>(a.B) * a.Ho * a.Wo * a.cout;
+  const int nq = a.cout / 4;
+  for (int v = tid; v < TY * TX * nq; v += NT) {
+    const int q = v / nq, co = (v - q * nq) * 4;
+    const int gy = oy0 + q / TX, gx = ox0 + q % TX;
+    if (gy >= a.Ho || gx >= a.Wo) continue;
+    const int64_t e = ((static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx) * a.cout + co;
+    f32x4_t s = *reinterpret_cast<const f32x4_t*>(a.ws + e);
+    for (int p = 1; p < nparts; ++p) s += *reinterpret_cast<const f32x4_t*>(a.ws + p * plane + e);
+    s += *reinterpret_cast<const f32x4_t*>(a.bp + co);
+    if (a.residual) s += *reinterpret_cast<const f32x4_t*>(a.x + (e / a.cout) * a.cin + co);
+    *reinterpret_cast<f32x4_t*>(a.y + e) = s;
+  }
 }
 
 // --------------------------------------------------------- stem_ir1_f32 ----
@@ -1207,12 +1254,12 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) stem_ir1_f32_kernel(StemIr1F3
 // work overlaps the others' staging / depthwise VALU work.  The price is the
 // halo: 100 stem cells per 64 outputs (1.56x) against 324 per 256 (1.27x).
 // (second launch bound: 2 waves per SIMD = 256 VGPRs; 8 such waves per CU.
-// WL: the depthwise weights live in LDS instead of 72 VGPRs, for 3 waves per
-// SIMD = 168 VGPRs.)
+// Moving the depthwise weights to LDS for 3 waves per SIMD (168 VGPRs) spilled
+// 44 VGPRs and ran 642 vs 501 us at batch 512: profiles/r3_stem_variants_b512.txt.)
 // Persistent: a resident set of waves walks the tiles; the next tile's input
 // bytes are in flight while the current one computes.
-template <int TY, int TX, bool PAIR, bool WL = false>
-__global__ void __launch_bounds__(64, WL ? 3 : 2) stem_ir1w_f32_kernel(StemIr1F32Args a) {
+template <int TY, int TX, bool PAIR>
+__global__ void __launch_bounds__(64, 2) stem_ir1w_f32_kernel(StemIr1F32Args a) {
   constexpr int HY = TY + 2, HX = TX + 2, PIN = HY * HX;
   constexpr int NBT = (PIN + 15) / 16;
   constexpr int IY = 2 * HY + 1, IX = 2 * HX + 1, PITCH = IX * 3;
@@ -1223,7 +1270,6 @@ __global__ void __launch_bounds__(64, WL ? 3 : 2) stem_ir1w_f32_kernel(StemIr1F3
   float* xin = smem;                                             // [IY][PITCH] normalised input
   float* lut = smem + XIN;                                       // [256] input table
   f32x4_t* hid = reinterpret_cast<f32x4_t*>(smem + XIN + 256);  // [8 quads][PIN] (32 channels)
-  f32x4_t* wdl = hid + 8 * PIN;                                  // WL: [2 halves][9 taps][4 quads]
 
   const int lane = threadIdx.x;
   const int li = lane & 15, g = lane >> 4;
@@ -1241,31 +1287,16 @@ __global__ void __launch_bounds__(64, WL ? 3 : 2) stem_ir1w_f32_kernel(StemIr1F3
     sa[1][t] = k < 27 ? a.ws[k * 32 + 16 + li] : 0.f;
     off[t] = k < 27 ? (k / 9) * PITCH + ((k % 9) / 3) * 3 + (k % 3) : 0;
   }
-  f32x4_t bs4[2], bd4[2], pa[2], wd4[2][WL ? 1 : 9];
+  f32x4_t bs4[2], bd4[2], pa[2], wd4[2][9];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int ch = 16 * h + 4 * g;  // this lane's channel quad in half h
     bs4[h] = *reinterpret_cast<const f32x4_t*>(a.bs + ch);
     bd4[h] = *reinterpret_cast<const f32x4_t*>(a.bd + ch);
     pa[h] = *reinterpret_cast<const f32x4_t*>(a.wp + li * 32 + ch);  // project A: row li, k = 16h + 4g + j
-    if constexpr (!WL) {
 #pragma unroll
-      for (int t = 0; t < 9; ++t) wd4[h][t] = *reinterpret_cast<const f32x4_t*>(a.wd + t * 32 + ch);
-    }
+    for (int t = 0; t < 9; ++t) wd4[h][t] = *reinterpret_cast<const f32x4_t*>(a.wd + t * 32 + ch);
   }
-  if constexpr (WL) {
-    // quad (h, t, q) = channels 16h + 4q .. +3 of tap t (lane 0..71 one quad each)
-    for (int i = lane; i < 72; i += 64) {
-      const int h = i / 36, t = (i / 4) % 9, q = i % 4;
-      wdl[i] = *reinterpret_cast<const f32x4_t*>(a.wd + t * 32 + 16 * h + 4 * q);
-    }
-  }
-  auto wdw = [&](int h, int t) -> f32x4_t {
-    if constexpr (WL)
-      return wdl[(h * 9 + t) * 4 + g];
-    else
-      return wd4[h][WL ? 0 : t];
-  };
   const f32x4_t bp4 = *reinterpret_cast<const f32x4_t*>(a.bp + 4 * g);
   const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
@@ -1377,8 +1408,8 @@ __global__ void __launch_bounds__(64, WL ? 3 : 2) stem_ir1w_f32_kernel(StemIr1F3
 #pragma unroll
             for (int kx = 0; kx < 3; ++kx) {
               const f32x4_t v = hp[r * HX + kx];
-              if (r < 3) d0 = __builtin_elementwise_fma(v, wdw(h, r * 3 + kx), d0);
-              if (r > 0) d1 = __builtin_elementwise_fma(v, wdw(h, (r - 1) * 3 + kx), d1);
+              if (r < 3) d0 = __builtin_elementwise_fma(v, wd4[h][r * 3 + kx], d0);
+              if (r > 0) d1 = __builtin_elementwise_fma(v, wd4[h][(r - 1) * 3 + kx], d1);
             }
           acc0 = mfma_k16(pa[h], relu6x4(d0), acc0);
           acc1 = mfma_k16(pa[h], relu6x4(d1), acc1);
@@ -1404,7 +1435,7 @@ __global__ void __launch_bounds__(64, WL ? 3 : 2) stem_ir1w_f32_kernel(StemIr1F3
 #pragma unroll
           for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-            for (int kx = 0; kx < 3; ++kx) d = __builtin_elementwise_fma(hp[ky * HX + kx], wdw(h, ky * 3 + kx), d);
+            for (int kx = 0; kx < 3; ++kx) d = __builtin_elementwise_fma(hp[ky * HX + kx], wd4[h][ky * 3 + kx], d);
           acc = mfma_k16(pa[h], relu6x4(d), acc);
         }
         const int gy = oy0 + qq / TX, gx = ox0 + qq % TX;
@@ -1814,8 +1845,9 @@ static bool launch_irw(const IrwCfg* c, IrBlockF32Args a, hipStream_t s) {
                                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
     return false;
   if (a.hsplit == 2 && !slabs) (void)hipMemsetAsync(a.y, 0, static_cast<size_t>(plane) * sizeof(float), s);
+  if (!a.ws) a.tickets = nullptr;
   hipLaunchKernelGGL(c->kernel, dim3(static_cast<unsigned>(tiles * a.hsplit)), dim3(64 * c->NW), lds, s, a);
-  if (a.ws) {
+  if (a.ws && !a.tickets) {
     const unsigned grid = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((plane / 4 + 255) / 256, 4096)));
     hipLaunchKernelGGL(irw_reduce_kernel, dim3(grid), dim3(256), 0, s, a.ws, a.hsplit, plane, a.bp, a.x, a.cin,
                        a.cout, a.residual, a.y);
@@ -1857,6 +1889,20 @@ size_t ir_block_f32_workspace_bytes(const IrBlockF32Args& args) {
   return static_cast<size_t>(a.hsplit) * a.B * a.Ho * a.Wo * a.cout * sizeof(float);
 }
 
+// the in-launch combine (irw_f32_kernel's last-part reduction), off unless
+// NNSX_F32_IRW_INLAUNCH=1: at batch 1 it lost to the separate irw_reduce
+// launch -- 7x7 960-hidden block 48.7 vs ~22 us, each block also paying a
+// zero-fill kernel for its tickets (profiles/r3_b1_inlaunch_combine_trace.txt)
+size_t ir_block_f32_tickets(const IrBlockF32Args& args) {
+  static const bool on = irw_env("NNSX_F32_IRW_INLAUNCH", 0) != 0;
+  if (!on || !ir_block_f32_workspace_bytes(args)) return 0;
+  IrBlockF32Args a = args;
+  const IrwCfg* c = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0);
+  if (!c || c->NOT == 0) return 0;
+  irw_geometry(c, &a);
+  return static_cast<size_t>(a.tiles_x) * a.tiles_y * a.B;
+}
+
 size_t stem_ir1_lds_bytes() {
   constexpr int TY = kStemIr1TY, TX = kStemIr1TX;
   constexpr int HY = TY + 2, HX = TX + 2, PIN = HY * HX, PINP = (PIN + 15) / 16 * 16;
@@ -1870,19 +1916,16 @@ constexpr int kStemW = 8;
 static size_t stem_ir1w_lds_bytes() {
   constexpr int HY = kStemW + 2, HX = kStemW + 2, PIN = HY * HX;
   constexpr int NIN = (2 * HY + 1) * (2 * HX + 1) * 3;
-  return static_cast<size_t>((NIN + 3) / 4 * 4 + 256) * 4 + 16 * 8 * PIN + 16 * 72;
+  return static_cast<size_t>((NIN + 3) / 4 * 4 + 256) * 4 + 16 * 8 * PIN;
 }
 
 static bool stem_ir1w_f32(StemIr1F32Args a, hipStream_t s) {
   a.tiles_y = (a.Ho + kStemW - 1) / kStemW;
   a.tiles_x = (a.Wo + kStemW - 1) / kStemW;
   const size_t lds = stem_ir1w_lds_bytes();
-  // 2: paired rows, weights in registers; 3: paired rows, dw weights in LDS (3 waves/SIMD); 1: unpaired
-  static const int mode = irw_env("NNSX_STEM_WAVE", 2);
-  const bool pair = mode >= 2, wl = mode == 3;
-  const void* fn = wl     ? reinterpret_cast<const void*>(&stem_ir1w_f32_kernel<kStemW, kStemW, true, true>)
-                   : pair ? reinterpret_cast<const void*>(&stem_ir1w_f32_kernel<kStemW, kStemW, true>)
-                          : reinterpret_cast<const void*>(&stem_ir1w_f32_kernel<kStemW, kStemW, false>);
+  static const bool pair = irw_env("NNSX_STEM_WAVE", 2) == 2;
+  const void* fn = pair ? reinterpret_cast<const void*>(&stem_ir1w_f32_kernel<kStemW, kStemW, true>)
+                        : reinterpret_cast<const void*>(&stem_ir1w_f32_kernel<kStemW, kStemW, false>);
   static const int resident = [fn, lds] {
     int dev = 0, ncu = 256, per_cu = 1;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
@@ -1891,9 +1934,7 @@ static bool stem_ir1w_f32(StemIr1F32Args a, hipStream_t s) {
   }();
   const int tiles = a.tiles_x * a.tiles_y * a.B;
   const unsigned grid = static_cast<unsigned>(std::min(tiles, resident));
-  if (wl)
-    hipLaunchKernelGGL((stem_ir1w_f32_kernel<kStemW, kStemW, true, true>), dim3(grid), dim3(64), lds, s, a);
-  else if (pair)
+  if (pair)
     hipLaunchKernelGGL((stem_ir1w_f32_kernel<kStemW, kStemW, true>), dim3(grid), dim3(64), lds, s, a);
   else
     hipLaunchKernelGGL((stem_ir1w_f32_kernel<kStemW, kStemW, false>), dim3(grid), dim3(64), lds, s, a);

@@ -166,6 +166,67 @@ __global__ void __launch_bounds__(kBlock) permute_kernel(const E* __restrict__ i
   }
 }
 
+// General permute, after merging axes that stay adjacent: the input's
+// innermost axis (0) and the output's innermost axis (input axis `a`) span a
+// 32 x 32 LDS tile, every other axis is a batch index decomposed ONCE per
+// workgroup (no per-element div/mod); reads run along input axis 0 and writes
+// along input axis a, both coalesced.  a == 0 (innermost axis kept): each
+// workgroup copies whole contiguous rows.
+struct TiledPerm {
+  int nb;                      // batch axes
+  uint32_t bdim[6];            // their extents (innermost first)
+  uint64_t bin[6], bout[6];    // their input / output strides (elements)
+  uint32_t d0, da;             // extents of input axis 0 and axis a
+  uint64_t in_sa, out_s0;      // input stride of axis a, output stride of axis 0
+  uint64_t nbatch;
+};
+
+template <typename E>
+__global__ void __launch_bounds__(256) permute_tiled_kernel(const E* __restrict__ in, E* __restrict__ out,
+                                                            TiledPerm p) {
+  __shared__ E tile[32][33];
+  const uint32_t t0 = (blockIdx.x % ((p.d0 + 31) / 32)) * 32, ta = (blockIdx.x / ((p.d0 + 31) / 32)) * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (uint64_t bt = blockIdx.y; bt < p.nbatch; bt += gridDim.y) {
+    uint64_t rem = bt, bi = 0, bo = 0;
+    for (int k = 0; k < p.nb; ++k) {
+      const uint64_t c = rem % p.bdim[k];
+      rem /= p.bdim[k];
+      bi += c * p.bin[k];
+      bo += c * p.bout[k];
+    }
+    // read: rows along axis a, columns along axis 0 (contiguous in the input)
+    for (int k = ty; k < 32; k += 8) {
+      const uint32_t xa = ta + k, x0 = t0 + tx;
+      if (xa < p.da && x0 < p.d0) tile[k][tx] = in[bi + xa * p.in_sa + x0];
+    }
+    __syncthreads();
+    // write: rows along axis 0, columns along axis a (contiguous in the output)
+    for (int k = ty; k < 32; k += 8) {
+      const uint32_t x0 = t0 + k, xa = ta + tx;
+      if (xa < p.da && x0 < p.d0) out[bo + x0 * p.out_s0 + xa] = tile[tx][k];
+    }
+    __syncthreads();
+  }
+}
+
+// a == 0: rows of d0 contiguous elements; one workgroup walks rows, the row's
+// source offset decomposed once per row
+template <typename E>
+__global__ void __launch_bounds__(256) permute_rows_kernel(const E* __restrict__ in, E* __restrict__ out,
+                                                           TiledPerm p) {
+  for (uint64_t row = blockIdx.x; row < p.nbatch; row += gridDim.x) {
+    uint64_t rem = row, bi = 0, bo = 0;
+    for (int k = 0; k < p.nb; ++k) {
+      const uint64_t c = rem % p.bdim[k];
+      rem /= p.bdim[k];
+      bi += c * p.bin[k];
+      bo += c * p.bout[k];
+    }
+    for (uint32_t x = threadIdx.x; x < p.d0; x += 256) out[bo + x] = in[bi + x];
+  }
+}
+
 // HWC->CHW style transpose of the two innermost "super axes" through an LDS
 // tile (32 x 33 pad: conflict-free column reads).  in: [B][R][C] -> out: [B][C][R]
 template <typename E>
@@ -293,6 +354,104 @@ void arith(const void* in, DType in_t, void* out, DType out_t, uint64_t n, const
 #undef NNSX_IN
 }
 
+// the general case through permute_tiled / permute_rows; false when the
+// shape does not fit their limits (the per-element kernel takes it)
+static bool launch_tiled_permute(const void* in, void* out, size_t es, const uint32_t in_dim[8], const int perm[8],
+                                 hipStream_t s) {
+  // merge input axes i, i+1 that the output keeps adjacent and in order; drop unit axes
+  uint64_t dim[8], istr[8];
+  int map[8], r = 0;  // merged axis of each input axis (-1: unit)
+  uint64_t acc = 1;
+  for (int k = 0; k < 8; ++k) {
+    const uint64_t st = acc;
+    acc *= in_dim[k];
+    if (in_dim[k] == 1) {
+      map[k] = -1;
+      continue;
+    }
+    dim[r] = in_dim[k];
+    istr[r] = st;
+    map[k] = r++;
+  }
+  if (r == 0 || acc == 0) return false;
+  // the output order of merged axes
+  int oq[8], no = 0;
+  for (int k = 0; k < 8; ++k)
+    if (map[perm[k]] >= 0) oq[no++] = map[perm[k]];
+  // fuse runs (j, j+1) adjacent in both orders
+  uint64_t fdim[8], fistr[8];
+  int fid[8], nf = 0, fo[8], nfo = 0;
+  for (int k = 0; k < no; ++k) {
+    if (k > 0 && oq[k] == oq[k - 1] + 1) {
+      fdim[nf - 1] *= dim[oq[k]];
+      continue;
+    }
+    fid[oq[k]] = nf;
+    fdim[nf] = dim[oq[k]];
+    fistr[nf] = istr[oq[k]];
+    fo[nfo++] = nf++;
+  }
+  (void)fid;
+  // fused axes in input order: sort by input stride
+  int byin[8];
+  for (int k = 0; k < nf; ++k) byin[k] = k;
+  std::sort(byin, byin + nf, [&](int x, int y) { return fistr[x] < fistr[y]; });
+  // output strides of each fused axis
+  uint64_t fostr[8], oacc = 1;
+  for (int k = 0; k < nfo; ++k) {
+    fostr[fo[k]] = oacc;
+    oacc *= fdim[fo[k]];
+  }
+  if (nf > 8 || nf - 2 > 6) return false;
+  const int ax0 = byin[0], axa = fo[0];  // input-innermost, output-innermost
+  TiledPerm p{};
+  p.d0 = static_cast<uint32_t>(fdim[ax0]);
+  if (fdim[ax0] >= (1ull << 32)) return false;
+  if (axa == ax0) {
+    // innermost kept: rows
+    p.nbatch = acc / fdim[ax0];
+    for (int k = 0; k < nf; ++k) {
+      const int ax = byin[k];
+      if (ax == ax0) continue;
+      p.bdim[p.nb] = static_cast<uint32_t>(fdim[ax]);
+      p.bin[p.nb] = fistr[ax];
+      p.bout[p.nb++] = fostr[ax];
+    }
+    if (p.nb > 6) return false;
+    const unsigned g = static_cast<unsigned>(std::min<uint64_t>(p.nbatch, 65535));
+    switch (es) {
+      case 1: hipLaunchKernelGGL(permute_rows_kernel<uint8_t>, dim3(g), dim3(256), 0, s, (const uint8_t*)in, (uint8_t*)out, p); return true;
+      case 2: hipLaunchKernelGGL(permute_rows_kernel<uint16_t>, dim3(g), dim3(256), 0, s, (const uint16_t*)in, (uint16_t*)out, p); return true;
+      case 4: hipLaunchKernelGGL(permute_rows_kernel<uint32_t>, dim3(g), dim3(256), 0, s, (const uint32_t*)in, (uint32_t*)out, p); return true;
+      case 8: hipLaunchKernelGGL(permute_rows_kernel<uint64_t>, dim3(g), dim3(256), 0, s, (const uint64_t*)in, (uint64_t*)out, p); return true;
+      default: return false;
+    }
+  }
+  if (fdim[axa] >= (1ull << 32)) return false;
+  p.da = static_cast<uint32_t>(fdim[axa]);
+  p.in_sa = fistr[axa];
+  p.out_s0 = fostr[ax0];
+  p.nbatch = acc / (fdim[ax0] * fdim[axa]);
+  for (int k = 0; k < nf; ++k) {
+    const int ax = byin[k];
+    if (ax == ax0 || ax == axa) continue;
+    p.bdim[p.nb] = static_cast<uint32_t>(fdim[ax]);
+    p.bin[p.nb] = fistr[ax];
+    p.bout[p.nb++] = fostr[ax];
+  }
+  if (p.nb > 6) return false;
+  const uint64_t tiles = ((p.d0 + 31ull) / 32) * ((p.da + 31ull) / 32);
+  if (tiles > 0x7fffffffull) return false;
+  dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(std::min<uint64_t>(p.nbatch, 65535)));
+  switch (es) {
+    case 1: hipLaunchKernelGGL(permute_tiled_kernel<uint8_t>, grid, dim3(256), 0, s, (const uint8_t*)in, (uint8_t*)out, p); return true;
+    case 2: hipLaunchKernelGGL(permute_tiled_kernel<uint16_t>, grid, dim3(256), 0, s, (const uint16_t*)in, (uint16_t*)out, p); return true;
+    case 4: hipLaunchKernelGGL(permute_tiled_kernel<uint32_t>, grid, dim3(256), 0, s, (const uint32_t*)in, (uint32_t*)out, p); return true;
+    case 8: hipLaunchKernelGGL(permute_tiled_kernel<uint64_t>, grid, dim3(256), 0, s, (const uint64_t*)in, (uint64_t*)out, p); return true;
+    default: return false;
+  }
+}
+
 void permute(const void* in, void* out, size_t elem_size, const uint32_t in_dim[8], const int perm[8],
              hipStream_t s) {
   uint64_t in_stride[8];
@@ -380,6 +539,7 @@ void permute(const void* in, void* out, size_t elem_size, const uint32_t in_dim[
       }
     }
   }
+  if (launch_tiled_permute(in, out, elem_size, in_dim, perm, s)) return;
   unsigned g = grid_for(acc);
   switch (elem_size) {
     case 1: hipLaunchKernelGGL(permute_kernel<uint8_t>, dim3(g), dim3(kBlock), 0, s, (const uint8_t*)in, (uint8_t*)out, p); break;

@@ -326,6 +326,11 @@ at::Tensor ir_block_f32_cuda(const at::Tensor& x, const at::Tensor& we, const at
     ws = at::empty({static_cast<int64_t>(wsb / sizeof(float))}, x.options());  // caching allocator: graph-capture safe
     a.ws = ws.data_ptr<float>();
   }
+  at::Tensor tickets;
+  if (const size_t nt = nnsx::kernels::ir_block_f32_tickets(a)) {
+    tickets = at::zeros({static_cast<int64_t>(nt)}, x.options().dtype(at::kInt));
+    a.tickets = tickets.data_ptr<int>();
+  }
   TORCH_CHECK(nnsx::kernels::ir_block_f32(a, cur_stream()), "ir_block(f32): unsupported shape (stride ", stride, ", ",
               H, "x", W, ", cin ", C, ", hid ", hid, ", cout ", cout, ")");
   return y;

@@ -1,6 +1,7 @@
 #include "runtime/memory.h"
 
 #include <cstring>
+#include <iterator>
 
 #include "core/util.h"
 #include "runtime/hip_util.h"
@@ -44,8 +45,46 @@ MemoryPtr Memory::alloc_device(size_t size, int dev, hipStream_t stream) {
 }
 
 // ------------------------------------------------------- DeviceBufferPool ----
+namespace {
+std::mutex& pool_registry_mu() {
+  static std::mutex m;
+  return m;
+}
+std::map<uint64_t, std::weak_ptr<DeviceBufferPool>>& pool_registry() {
+  static std::map<uint64_t, std::weak_ptr<DeviceBufferPool>> r;
+  return r;
+}
+}  // namespace
+
 std::shared_ptr<DeviceBufferPool> DeviceBufferPool::create(int dev, size_t size, size_t max_blocks) {
-  return std::shared_ptr<DeviceBufferPool>(new DeviceBufferPool(dev, size, max_blocks));
+  auto p = std::shared_ptr<DeviceBufferPool>(new DeviceBufferPool(dev, size, max_blocks));
+  std::lock_guard<std::mutex> lk(pool_registry_mu());
+  auto& r = pool_registry();
+  for (auto it = r.begin(); it != r.end();) it = it->second.expired() ? r.erase(it) : std::next(it);
+  r[p->id()] = p;
+  return p;
+}
+
+std::shared_ptr<DeviceBufferPool> DeviceBufferPool::find(uint64_t id) {
+  std::lock_guard<std::mutex> lk(pool_registry_mu());
+  auto it = pool_registry().find(id);
+  return it == pool_registry().end() ? nullptr : it->second.lock();
+}
+
+void DeviceBufferPool::preallocate(hipStream_t stream) {
+  std::lock_guard<std::mutex> lk(mu_);
+  while (blocks_.size() < max_) {
+    Block b;
+    b.ptr = hip::device_alloc(dev_, size_, stream);
+    blocks_.push_back(b);
+  }
+}
+
+std::vector<void*> DeviceBufferPool::block_addresses() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<void*> v;
+  for (const auto& b : blocks_) v.push_back(b.ptr);
+  return v;
 }
 
 DeviceBufferPool::DeviceBufferPool(int dev, size_t size, size_t max_blocks) : dev_(dev), size_(size), max_(max_blocks) {

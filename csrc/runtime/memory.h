@@ -137,7 +137,13 @@ class DeviceBufferPool : public std::enable_shared_from_this<DeviceBufferPool> {
   static constexpr const char* kPoolTag = "nnsx.pool";
   static constexpr const char* kSlotTag = "nnsx.pool_slot";
   static std::shared_ptr<DeviceBufferPool> create(int dev, size_t size, size_t max_blocks);
+  // the live pool with this id (kPoolTag), or null
+  static std::shared_ptr<DeviceBufferPool> find(uint64_t id);
   ~DeviceBufferPool();
+  // allocate every block now (ordered on `stream`): the set of addresses is
+  // then fixed and known (block_addresses) before the first frame
+  void preallocate(hipStream_t stream);
+  std::vector<void*> block_addresses() const;
   // a block ordered on `stream`; past max_blocks outstanding: an unpooled alloc_device
   MemoryPtr acquire(hipStream_t stream);
   int device() const { return dev_; }

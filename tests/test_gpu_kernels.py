@@ -92,6 +92,29 @@ def test_permute(nns, dims, perm):
     torch.testing.assert_close(out, ref)
 
 
+@pytest.mark.parametrize("es,dims,perm", [
+    (4, [3, 5, 7, 11, 13], [3, 1, 4, 0, 2]),
+    (1, [4, 6, 1, 9, 2], [2, 4, 0, 3, 1]),
+    (2, [33, 2, 65, 3], [2, 3, 0, 1]),
+    (8, [7, 40, 3, 2, 5, 3], [5, 4, 1, 0, 3, 2]),
+    (4, [16, 9, 8, 5], [0, 2, 1, 3]),        # innermost kept: row copies
+    (1, [3, 64, 64, 2, 2], [2, 1, 0, 4, 3]),
+    (4, [2, 3, 4, 5, 6, 7, 2, 1], [7, 6, 5, 4, 3, 2, 1, 0]),
+])
+def test_permute_general(nns, es, dims, perm):
+    """every permutation class: the tiled (axis 0 <-> output-innermost axis
+    through LDS, batch axes decomposed per workgroup) and row-copy kernels"""
+    dt = {1: torch.uint8, 2: torch.int16, 4: torch.float32, 8: torch.float64}[es]
+    n = int(np.prod(dims))
+    x = (torch.rand(n, device="cuda") * 100).to(dt)
+    out = torch.zeros_like(x)
+    nns.kernels.permute(x.data_ptr(), out.data_ptr(), es, dims, perm, _stream())
+    r = len(dims)
+    order = [r - 1 - perm[k] for k in reversed(range(r))]
+    ref = x.view(dims[::-1]).permute(order).contiguous().view(-1)
+    assert torch.equal(out, ref)
+
+
 @pytest.mark.parametrize("t", [7, 5, 12])
 def test_argmax_rows_first_max_wins(nns, t):
     rows, n = 33, 1001
