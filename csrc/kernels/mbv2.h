@@ -95,6 +95,7 @@ struct IrBlockF32Args {
   const float* bp = nullptr;
   int B = 0, H = 0, W = 0, cin = 0, hid = 0, cout = 0, stride = 1;
   int has_expand = 1, residual = 0;
+  int dil = 1;  // depthwise dilation (padding = dil)
   // derived by ir_block_f32()
   int Ho = 0, Wo = 0, tiles_x = 0, tiles_y = 0;
   int hsplit = 1;  // hidden-channel parts per tile (wave-split kernel)
@@ -104,7 +105,7 @@ struct IrBlockF32Args {
   // instead of a separate reduce kernel
   int* tickets = nullptr;
 };
-bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout, bool has_expand);
+bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout, bool has_expand, int dil = 1);
 // device workspace ir_block_f32 needs for these args (0 = none)
 size_t ir_block_f32_workspace_bytes(const IrBlockF32Args& a);
 // int tickets (zeroed) the in-launch combine of hidden parts wants (0: none)
@@ -113,7 +114,7 @@ size_t ir_block_f32_tickets(const IrBlockF32Args& a);
 // output to y [B][Ho][Wo][hid] (the hidden map never touches HBM; the caller
 // runs the project as a GEMM).  wp / bp / cout / residual are unused.
 // (B > 0: whether it is the faster path at this batch; B = 0: supported at all)
-bool ir_expand_dw_f32_supported(int stride, int H, int W, int cin, int hid, int B = 0);
+bool ir_expand_dw_f32_supported(int stride, int H, int W, int cin, int hid, int B = 0, int dil = 1);
 bool ir_expand_dw_f32(const IrBlockF32Args& a, hipStream_t s);
 
 // stem (3x3/2 conv 3 -> 32 on the uint8 frame, mapped through lut[256],

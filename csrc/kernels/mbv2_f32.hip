@@ -433,24 +433,39 @@ __global__ void __launch_bounds__(256) stem_f32_kernel(const T* __restrict__ x, 
 
 // ------------------------------------------------------------- avgpool_f32 ----
 // one workgroup = one image x 64 channel quads; the 4 waves split the pixels
+// global average pool [B][HW][C] -> [B][C]: a workgroup = 16 channel quads x
+// 16 pixel stripes; each lane keeps 4 independent partial sums (4 loads in
+// flight), then the stripes are added in a fixed order through LDS
+// (deterministic).  DeepLab's 33x33x320 maps at batch 8: 40 workgroups instead
+// of 16 with one dependent load chain of 272 pixels per lane (67 us).
 __global__ void __launch_bounds__(256) avgpool_f32_kernel(const float* __restrict__ x, float* __restrict__ y, int HW,
                                                           int C) {
-  __shared__ f32x4_t part[4][64];
+  __shared__ f32x4_t part[16][16];
   const int cq = C >> 2;
-  const int groups = (cq + 63) / 64;
+  const int groups = (cq + 15) / 16;
   const int b = blockIdx.x / groups;
-  const int q = (blockIdx.x % groups) * 64 + (threadIdx.x & 63);
-  const int wave = threadIdx.x >> 6;
-  f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  if (q < cq)
-    for (int p = wave; p < HW; p += 4)
-      acc += *reinterpret_cast<const f32x4_t*>(x + (static_cast<int64_t>(b) * HW + p) * C + q * 4);
-  part[wave][threadIdx.x & 63] = acc;
+  const int q = (blockIdx.x % groups) * 16 + (threadIdx.x & 15);
+  const int stripe = threadIdx.x >> 4;
+  const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  f32x4_t a0 = z, a1 = z, a2 = z, a3 = z;
+  if (q < cq) {
+    const float* xb = x + static_cast<int64_t>(b) * HW * C + q * 4;
+    int p = stripe;
+    for (; p + 48 < HW; p += 64) {
+      a0 += *reinterpret_cast<const f32x4_t*>(xb + static_cast<int64_t>(p) * C);
+      a1 += *reinterpret_cast<const f32x4_t*>(xb + static_cast<int64_t>(p + 16) * C);
+      a2 += *reinterpret_cast<const f32x4_t*>(xb + static_cast<int64_t>(p + 32) * C);
+      a3 += *reinterpret_cast<const f32x4_t*>(xb + static_cast<int64_t>(p + 48) * C);
+    }
+    for (; p < HW; p += 16) a0 += *reinterpret_cast<const f32x4_t*>(xb + static_cast<int64_t>(p) * C);
+  }
+  part[stripe][threadIdx.x & 15] = (a0 + a1) + (a2 + a3);
   __syncthreads();
-  if (wave != 0 || q >= cq) return;
-  const float inv = 1.f / HW;
-  const f32x4_t s = (part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] + part[3][threadIdx.x]) * inv;
-  *reinterpret_cast<f32x4_t*>(y + static_cast<int64_t>(b) * C + q * 4) = s;
+  if (stripe != 0 || q >= cq) return;
+  f32x4_t s = part[0][threadIdx.x];
+#pragma unroll
+  for (int k = 1; k < 16; ++k) s += part[k][threadIdx.x];
+  *reinterpret_cast<f32x4_t*>(y + static_cast<int64_t>(b) * C + q * 4) = s * (1.f / HW);
 }
 
 // ------------------------------------------------------------ ir_block_f32 ----
@@ -703,9 +718,9 @@ __global__ void __launch_bounds__(256) ir_block_f32_kernel(IrBlockF32Args a) {
 // slabs in part order (deterministic).  The MFMA pipe of a SIMD then alternates between waves of
 // different workgroups that are never held at a common barrier, so one wave's
 // depthwise VALU work hides under another's matrix work.
-template <int S, int TY, int TX, int KIN, int NOT, int NW, bool FULL>
+template <int S, int TY, int TX, int KIN, int NOT, int NW, bool FULL, int DIL = 1>
 struct IrwGeom {
-  static constexpr int TIY = (TY - 1) * S + 3, TIX = (TX - 1) * S + 3;
+  static constexpr int TIY = (TY - 1) * S + 2 * DIL + 1, TIX = (TX - 1) * S + 2 * DIL + 1;
   static constexpr int PIN = TIY * TIX;               // halo grid cells
   static constexpr int NC16 = (PIN + 15) / 16 * 16;   // compact in-image pixels (max), padded
   static constexpr int NBT = NC16 / 16;               // expand pixel tiles
@@ -753,9 +768,10 @@ __device__ __forceinline__ void wave_sync() {
 // tile's input prefetched into registers -- needed 190 VGPRs on the 112 -> 56
 // block, 2 waves per SIMD instead of 3, and ran 757 vs 545 us at batch 512:
 // profiles/r3_irw_persistent_ab_b512.txt.)
-template <int S, int TY, int TX, int KIN, int NOT, int NW, bool FULL>
+// DIL: depthwise dilation (padding DIL; DeepLab's output-stride-16 blocks)
+template <int S, int TY, int TX, int KIN, int NOT, int NW, bool FULL, int DIL = 1>
 __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FULL>::MINB)) irw_f32_kernel(IrBlockF32Args a) {
-  using G = IrwGeom<S, TY, TX, KIN, NOT, NW, FULL>;
+  using G = IrwGeom<S, TY, TX, KIN, NOT, NW, FULL, DIL>;
   constexpr int NT = 64 * NW;
   constexpr int TIY = G::TIY, TIX = G::TIX, PIN = G::PIN, NC16 = G::NC16, NBT = G::NBT, XSP = G::XSP;
   constexpr int PINP = G::PINP;
@@ -786,7 +802,7 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
   // fp32 is at least 0.5 / RW away from an integer, so truncation is exact
   auto load_tile = [&](int t) {
     const int tb = t / tiles_img, tt = t - tb * tiles_img;
-    const int ty0 = (tt / a.tiles_x) * TY * S - 1, tx0 = (tt % a.tiles_x) * TX * S - 1;
+    const int ty0 = (tt / a.tiles_x) * TY * S - DIL, tx0 = (tt % a.tiles_x) * TX * S - DIL;
     const int qy0 = max(ty0, 0), qy1 = min(ty0 + TIY, a.H);
     const int qx0 = max(tx0, 0), qx1 = min(tx0 + TIX, a.W);
     const int qw = qx1 - qx0, qn = FULL ? PIN : (qy1 - qy0) * qw;
@@ -817,7 +833,7 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
   const int b = tile / tiles_img;
   const int tyx = tile - b * tiles_img;
   const int oy0 = (tyx / a.tiles_x) * TY, ox0 = (tyx % a.tiles_x) * TX;
-  const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
+  const int iy0 = oy0 * S - DIL, ix0 = ox0 * S - DIL;
   const int ry0 = max(iy0, 0), ry1 = min(iy0 + TIY, a.H);
   const int rx0 = max(ix0, 0), rx1 = min(ix0 + TIX, a.W);
   const int RW = rx1 - rx0, NC = FULL ? PIN : (ry1 - ry0) * RW;
@@ -991,7 +1007,7 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
       for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx)
-          d = __builtin_elementwise_fma(myhid[dcell[pt] + ky * TIX + kx], wd4[ky * 3 + kx], d);
+          d = __builtin_elementwise_fma(myhid[dcell[pt] + (ky * TIX + kx) * DIL], wd4[ky * 3 + kx], d);
       const f32x4_t bf = relu6x4(d);
       if constexpr (NOT == 0) {
         const int q = pt * 16 + li;
@@ -1517,11 +1533,17 @@ struct IrwCfg {
   bool full;
   void (*kernel)(IrBlockF32Args);
   size_t (*lds)(int);
+  int dil = 1;
 };
 #define NNSX_IRW(S, TY, TX, KIN, NOT, NW, F)                                                    \
   IrwCfg {                                                                                      \
     S, TY, TX, KIN, NOT, NW, F, &irw_f32_kernel<S, TY, TX, KIN, NOT, NW, F>,                    \
-        &IrwGeom<S, TY, TX, KIN, NOT, NW, F>::lds_bytes                                         \
+        &IrwGeom<S, TY, TX, KIN, NOT, NW, F>::lds_bytes, 1                                      \
+  }
+#define NNSX_IRWD(S, TY, TX, KIN, NOT, NW, F, D)                                                \
+  IrwCfg {                                                                                      \
+    S, TY, TX, KIN, NOT, NW, F, &irw_f32_kernel<S, TY, TX, KIN, NOT, NW, F, D>,                 \
+        &IrwGeom<S, TY, TX, KIN, NOT, NW, F, D>::lds_bytes, D                                   \
   }
 // (NW = waves per workgroup: a divisor of the hidden subtile count where possible,
 // so every wave walks the same number of 16-channel subtiles)
@@ -1547,8 +1569,13 @@ const IrwCfg kIrwCfgs[] = {
     NNSX_IRW(1, 8, 16, 24, 2, 3, true),    // 56x56: expand 192/128 (8x8: 112/64)
     NNSX_IRW(2, 4, 8, 24, 2, 3, true),     // 56 -> 28: expand 160/128 input px (4x4: 96/64)
     NNSX_IRW(2, 8, 8, 16, 2, 3, true),     // 112 -> 56: expand 304/256 (4x8: 160/128)
+    // dilation 2 (DeepLab output stride 16, 33x33 maps at 513 input)
+    NNSX_IRWD(1, 7, 7, 96, 10, 4, false, 2),   // 96 -> 576 -> 160
+    NNSX_IRWD(1, 7, 7, 160, 10, 4, false, 2),  // 160 -> 960 -> 160
+    NNSX_IRWD(1, 7, 7, 160, 0, 4, false, 2),   // 160 -> 960 expand + dw (project -> 320 as a GEMM)
 };
 #undef NNSX_IRW
+#undef NNSX_IRWD
 
 // indices of kIrwCfgs that find_irw skips (A/B experiments): NNSX_IRW_SKIP=1,4
 bool irw_skipped(size_t i) {
@@ -1575,27 +1602,32 @@ bool irw_enabled() {
   return on;
 }
 
-const IrwCfg* find_irw(int S, int H, int W, int cin, int hid, int cout, bool has_expand) {
+const IrwCfg* find_irw(int S, int H, int W, int cin, int hid, int cout, bool has_expand, int dil = 1) {
   if (!irw_enabled() || !has_expand || hid % 16) return nullptr;
   const int kin = (cin + 7) / 8 * 8;
   const int nout = (cout + 15) / 16;
   const int Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
-  for (size_t i = 0; i < sizeof(kIrwCfgs) / sizeof(kIrwCfgs[0]); ++i) {
-    const IrwCfg& c = kIrwCfgs[i];
-    if (c.S == S && c.KIN == kin && c.NOT == nout && Ho % c.TY == 0 && Wo % c.TX == 0 &&
-        c.lds(hid) <= 160 * 1024 && !irw_skipped(i))
-      return &c;
-  }
+  // an exact tiling first; else (odd maps: DeepLab's 129 / 65 / 33, SSD's 75 /
+  // 38 / 19) the first configuration of the shape with masked partial tiles
+  for (int exact = 1; exact >= 0; --exact)
+    for (size_t i = 0; i < sizeof(kIrwCfgs) / sizeof(kIrwCfgs[0]); ++i) {
+      const IrwCfg& c = kIrwCfgs[i];
+      if (c.S == S && c.dil == dil && c.KIN == kin && c.NOT == nout && (!exact || (Ho % c.TY == 0 && Wo % c.TX == 0)) &&
+          c.lds(hid) <= 160 * 1024 && !irw_skipped(i))
+        return &c;
+    }
   return nullptr;
 }
 
-const IrwCfg* find_irw_dw(int S, int H, int W, int cin, int hid) {
+const IrwCfg* find_irw_dw(int S, int H, int W, int cin, int hid, int dil = 1) {
   if (!irw_enabled() || hid % 16) return nullptr;
   const int kin = (cin + 7) / 8 * 8;
   const int Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
-  for (const auto& c : kIrwCfgs)
-    if (c.NOT == 0 && c.S == S && c.KIN == kin && Ho % c.TY == 0 && Wo % c.TX == 0 && c.lds(hid) <= 160 * 1024)
-      return &c;
+  for (int exact = 1; exact >= 0; --exact)
+    for (const auto& c : kIrwCfgs)
+      if (c.NOT == 0 && c.S == S && c.dil == dil && c.KIN == kin && (!exact || (Ho % c.TY == 0 && Wo % c.TX == 0)) &&
+          c.lds(hid) <= 160 * 1024)
+        return &c;
   return nullptr;
 }
 
@@ -1779,11 +1811,11 @@ void stem3x3_u8_f32(const uint8_t* x, const float* w, const float* bias, float* 
 }
 
 void avgpool_f32(const float* x, float* y, int B, int HW, int C, hipStream_t s) {
-  const int groups = (C / 4 + 63) / 64;
+  const int groups = (C / 4 + 15) / 16;
   hipLaunchKernelGGL(avgpool_f32_kernel, dim3(static_cast<unsigned>(B * groups)), dim3(256), 0, s, x, y, HW, C);
 }
 
-bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout, bool has_expand) {
+bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout, bool has_expand, int dil) {
   if (stride != 1 && stride != 2) return false;
   static const int min_ho = [] {
     const char* e = std::getenv("NNSX_F32_IR_MIN_HO");
@@ -1791,6 +1823,7 @@ bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout
   }();
   if ((H - 1) / stride + 1 < min_ho) return false;
   if (cin % 8 || cout % 4 || hid % 16) return false;
+  if (dil != 1) return find_irw(stride, H, W, cin, hid, cout, has_expand, dil) != nullptr;
   return find_irw(stride, H, W, cin, hid, cout, has_expand) != nullptr ||
          find_cfg(stride, H, W, cin, hid, cout, has_expand) != nullptr;
 }
@@ -1858,16 +1891,17 @@ static bool launch_irw(const IrwCfg* c, IrBlockF32Args a, hipStream_t s) {
 // used for small batches only: at batch 128 the 7x7 160 -> 960 expand GEMM +
 // depthwise kernel (46 us) beat this kernel (54 us); at batch 1 it saves a
 // launch and 4 us
-bool ir_expand_dw_f32_supported(int stride, int H, int W, int cin, int hid, int B) {
-  const IrwCfg* c = cin % 8 == 0 ? find_irw_dw(stride, H, W, cin, hid) : nullptr;
+bool ir_expand_dw_f32_supported(int stride, int H, int W, int cin, int hid, int B, int dil) {
+  const IrwCfg* c = cin % 8 == 0 ? find_irw_dw(stride, H, W, cin, hid, dil) : nullptr;
   if (!c) return false;
+  if (dil != 1) return true;  // (the alternative is an unfused dilated depthwise pass over the hidden map)
   const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
   return B <= 0 || B * (Ho / c->TY) * (Wo / c->TX) <= 32;
 }
 
 bool ir_expand_dw_f32(const IrBlockF32Args& args, hipStream_t s) {
   IrBlockF32Args a = args;
-  const IrwCfg* c = find_irw_dw(a.stride, a.H, a.W, a.cin, a.hid);
+  const IrwCfg* c = find_irw_dw(a.stride, a.H, a.W, a.cin, a.hid, a.dil);
   if (!c || !a.has_expand) return false;
   irw_geometry(c, &a);
   a.ws = nullptr;
@@ -1882,7 +1916,7 @@ bool ir_expand_dw_f32(const IrBlockF32Args& args, hipStream_t s) {
 
 size_t ir_block_f32_workspace_bytes(const IrBlockF32Args& args) {
   IrBlockF32Args a = args;
-  const IrwCfg* c = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0);
+  const IrwCfg* c = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0, a.dil);
   if (!c) return 0;
   irw_geometry(c, &a);
   if (a.hsplit < 2 || (a.hsplit == 2 && irw_atomic2())) return 0;
@@ -1897,7 +1931,7 @@ size_t ir_block_f32_tickets(const IrBlockF32Args& args) {
   static const bool on = irw_env("NNSX_F32_IRW_INLAUNCH", 0) != 0;
   if (!on || !ir_block_f32_workspace_bytes(args)) return 0;
   IrBlockF32Args a = args;
-  const IrwCfg* c = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0);
+  const IrwCfg* c = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0, a.dil);
   if (!c || c->NOT == 0) return 0;
   irw_geometry(c, &a);
   return static_cast<size_t>(a.tiles_x) * a.tiles_y * a.B;
@@ -1982,7 +2016,8 @@ bool stem_ir1_f32(const StemIr1F32Args& args, hipStream_t s) {
 
 bool ir_block_f32(const IrBlockF32Args& args, hipStream_t s) {
   IrBlockF32Args a = args;
-  if (const IrwCfg* w = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0)) return launch_irw(w, a, s);
+  if (const IrwCfg* w = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0, a.dil)) return launch_irw(w, a, s);
+  if (a.dil != 1) return false;
   const IrF32Cfg* c = find_cfg(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0);
   if (!c) return false;
   a.Ho = (a.H - 1) / a.stride + 1;

@@ -289,7 +289,7 @@ at::Tensor avgpool_cpu(const at::Tensor& x) { return x.to(at::kFloat).mean({1, 2
 // Fused inverted residual.  we [hid, cin32], wd [9, hid], wp [ceil16(cout), hid] bf16; biases f32.
 at::Tensor ir_block_f32_cuda(const at::Tensor& x, const at::Tensor& we, const at::Tensor& be, const at::Tensor& wd,
                              const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, int64_t stride,
-                             int64_t cout, bool has_expand, bool residual) {
+                             int64_t cout, bool has_expand, bool residual, int64_t dilation) {
   TORCH_CHECK(x.is_contiguous() && x.dim() == 4, "ir_block(f32): x [B,H,W,C] f32");
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   const int64_t hid = wd.size(1);
@@ -321,6 +321,7 @@ at::Tensor ir_block_f32_cuda(const at::Tensor& x, const at::Tensor& we, const at
   a.stride = static_cast<int>(stride);
   a.has_expand = has_expand ? 1 : 0;
   a.residual = residual ? 1 : 0;
+  a.dil = static_cast<int>(dilation);
   at::Tensor ws;
   if (const size_t wsb = nnsx::kernels::ir_block_f32_workspace_bytes(a)) {
     ws = at::empty({static_cast<int64_t>(wsb / sizeof(float))}, x.options());  // caching allocator: graph-capture safe
@@ -339,7 +340,7 @@ at::Tensor ir_block_f32_cuda(const at::Tensor& x, const at::Tensor& we, const at
 // expand + depthwise (fp32), the depthwise output [B, Ho, Wo, hid]: blocks
 // whose project runs as a plain GEMM afterwards
 at::Tensor ir_expand_dw_cuda(const at::Tensor& x, const at::Tensor& we, const at::Tensor& be, const at::Tensor& wd,
-                             const at::Tensor& bd, int64_t stride) {
+                             const at::Tensor& bd, int64_t stride, int64_t dilation) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 4,
               "ir_expand_dw: x [B,H,W,C] f32");
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
@@ -366,28 +367,33 @@ at::Tensor ir_expand_dw_cuda(const at::Tensor& x, const at::Tensor& we, const at
   a.cout = 0;
   a.stride = static_cast<int>(stride);
   a.has_expand = 1;
+  a.dil = static_cast<int>(dilation);
   TORCH_CHECK(nnsx::kernels::ir_expand_dw_f32(a, cur_stream()), "ir_expand_dw: unsupported shape (stride ", stride,
               ", ", H, "x", W, ", cin ", C, ", hid ", hid, ")");
   return y;
 }
 
 at::Tensor ir_expand_dw_cpu(const at::Tensor& x, const at::Tensor& we, const at::Tensor& be, const at::Tensor& wd,
-                            const at::Tensor& bd, int64_t stride) {
+                            const at::Tensor& bd, int64_t stride, int64_t dilation) {
   const int64_t hid = wd.size(1);
   at::Tensor h = pw_conv_cpu(x, we, be, c10::nullopt, hid, 1, false);
-  return dw_conv_cpu(h, wd, bd, stride, 1, 1);
+  return dw_conv_cpu(h, wd, bd, stride, 1, dilation);
 }
 
-bool ir_expand_dw_supported_f32(int64_t stride, int64_t H, int64_t W, int64_t cin, int64_t hid, int64_t B) {
+bool ir_expand_dw_supported_f32(int64_t stride, int64_t H, int64_t W, int64_t cin, int64_t hid, int64_t B,
+                                int64_t dilation) {
   return nnsx::kernels::ir_expand_dw_f32_supported(static_cast<int>(stride), static_cast<int>(H), static_cast<int>(W),
-                                                   static_cast<int>(cin), static_cast<int>(hid), static_cast<int>(B));
+                                                   static_cast<int>(cin), static_cast<int>(hid), static_cast<int>(B),
+                                                   static_cast<int>(dilation));
 }
 
 at::Tensor ir_block_cuda(const at::Tensor& x, const at::Tensor& we, const at::Tensor& be, const at::Tensor& wd,
                          const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, int64_t stride,
-                         int64_t cout, bool has_expand, bool residual) {
+                         int64_t cout, bool has_expand, bool residual, int64_t dilation) {
   TORCH_CHECK(x.is_cuda(), "ir_block: x must be a cuda tensor");
-  if (x.scalar_type() == at::kFloat) return ir_block_f32_cuda(x, we, be, wd, bd, wp, bp, stride, cout, has_expand, residual);
+  if (x.scalar_type() == at::kFloat)
+    return ir_block_f32_cuda(x, we, be, wd, bd, wp, bp, stride, cout, has_expand, residual, dilation);
+  TORCH_CHECK(dilation == 1, "ir_block(bf16): dilation 1 only");
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() == 4,
               "ir_block: x [B,H,W,C] bf16");
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
@@ -422,11 +428,11 @@ at::Tensor ir_block_cuda(const at::Tensor& x, const at::Tensor& we, const at::Te
 
 at::Tensor ir_block_cpu(const at::Tensor& x, const at::Tensor& we, const at::Tensor& be, const at::Tensor& wd,
                         const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, int64_t stride,
-                        int64_t cout, bool has_expand, bool residual) {
+                        int64_t cout, bool has_expand, bool residual, int64_t dilation) {
   at::Tensor h = x;
   const int64_t hid = wd.size(1);
   if (has_expand) h = pw_conv_cpu(x, we, be, c10::nullopt, hid, 1, false);
-  h = dw_conv_cpu(h, wd, bd, stride, 1, 1);
+  h = dw_conv_cpu(h, wd, bd, stride, 1, dilation);
   c10::optional<at::Tensor> res;
   if (residual) res = x;
   return pw_conv_cpu(h, wp, bp, res, cout, 0, false);  // (dtype follows x: f32 stays f32)
@@ -470,10 +476,11 @@ at::Tensor stem_ir1_cpu(const at::Tensor& x, const at::Tensor& ws, const at::Ten
   return pw_conv_cpu(h, wp, bp, c10::nullopt, 16, 0, true);
 }
 
-bool ir_supported_f32(int64_t stride, int64_t H, int64_t W, int64_t cin, int64_t hid, int64_t cout, bool has_expand) {
+bool ir_supported_f32(int64_t stride, int64_t H, int64_t W, int64_t cin, int64_t hid, int64_t cout, bool has_expand,
+                      int64_t dilation) {
   return nnsx::kernels::ir_block_f32_supported(static_cast<int>(stride), static_cast<int>(H), static_cast<int>(W),
                                                static_cast<int>(cin), static_cast<int>(hid), static_cast<int>(cout),
-                                               has_expand);
+                                               has_expand, static_cast<int>(dilation));
 }
 
 bool ir_supported(int64_t stride, int64_t cin, int64_t hid, int64_t cout) {
@@ -495,13 +502,13 @@ TORCH_LIBRARY(nnsx, m) {
   m.def("stem_ir1(Tensor x, Tensor ws, Tensor bs, Tensor wd, Tensor bd, Tensor wp, Tensor bp, Tensor lut) -> Tensor");
   m.def("pw_conv_f32_tile(Tensor x, Tensor wt, Tensor bias, Tensor? res, int N, int act, int tile) -> Tensor");
   m.def("ir_block(Tensor x, Tensor we, Tensor be, Tensor wd, Tensor bd, Tensor wp, Tensor bp, int stride, int cout, "
-        "bool has_expand, bool residual) -> Tensor");
+        "bool has_expand, bool residual, int dilation=1) -> Tensor");
   m.def("ir_supported(int stride, int cin, int hid, int cout) -> bool", ir_supported);
-  m.def("ir_supported_f32(int stride, int H, int W, int cin, int hid, int cout, bool has_expand) -> bool",
+  m.def("ir_supported_f32(int stride, int H, int W, int cin, int hid, int cout, bool has_expand, int dilation=1) -> bool",
         ir_supported_f32);
-  m.def("ir_expand_dw_supported_f32(int stride, int H, int W, int cin, int hid, int B=0) -> bool",
+  m.def("ir_expand_dw_supported_f32(int stride, int H, int W, int cin, int hid, int B=0, int dilation=1) -> bool",
         ir_expand_dw_supported_f32);
-  m.def("ir_expand_dw(Tensor x, Tensor we, Tensor be, Tensor wd, Tensor bd, int stride) -> Tensor");
+  m.def("ir_expand_dw(Tensor x, Tensor we, Tensor be, Tensor wd, Tensor bd, int stride, int dilation=1) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(nnsx, CUDA, m) {

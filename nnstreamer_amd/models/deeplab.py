@@ -30,7 +30,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .fused import DW, PW, Block, _fold, input_lut, stem
+from .fused import PW, Block, StemBlock1, _fold, input_lut
 from .mobilenet_v2 import ConvBNReLU, InvertedResidual, MobileNetV2
 
 
@@ -109,6 +109,8 @@ class FusedDeepLabV3(nn.Module):
             blk.dw.dilation = int(dwc.dilation[0])
             blocks.append(blk)
         self.blocks = nn.ModuleList(blocks)
+        # stem + block 0 (fp32, uint8 frames: one stem_ir1 kernel over the 257x257 map)
+        self.front = StemBlock1(self.stem_w.clone(), self.stem_b.clone(), self.blocks[0], self.f32)
         self.aspp_conv = PW(*_fold(m.aspp_conv[0], m.aspp_conv[1]), act=1, precision=precision)
         self.aspp_pool = PW(*_fold(m.aspp_pool[0], m.aspp_pool[1]), act=1, precision=precision)
         self.project = PW(*_fold(m.project[0], m.project[1]), act=1, precision=precision)
@@ -131,9 +133,12 @@ class FusedDeepLabV3(nn.Module):
         return self
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        h = stem(x, self.stem_w, self.stem_b, self.in_lut, self.f32)
+        h = self.front(x, self.in_lut)
+        i = 0
         for blk in self.blocks:
-            h = blk(h)
+            if i > 0:  # (block 0 is in self.front)
+                h = blk(h)
+            i += 1
         if self.f32:
             return self._head_f32(h)
         a = self.aspp_conv(h)

@@ -181,16 +181,19 @@ class Block(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.f32:
-            if self.use_ir and self.dw.dilation == 1 and bool(torch.ops.nnsx.ir_supported_f32(
-                    self.dw.stride, x.shape[1], x.shape[2], self.cin, self.hid, self.cout, self.has_expand)):
+            # (dilation 2: DeepLab's output-stride-16 blocks, instantiated for 33x33 maps)
+            if self.use_ir and bool(torch.ops.nnsx.ir_supported_f32(
+                    self.dw.stride, x.shape[1], x.shape[2], self.cin, self.hid, self.cout, self.has_expand,
+                    self.dw.dilation)):
                 return torch.ops.nnsx.ir_block(x, self.ir_we, self.ir_be, self.ir_wd, self.ir_bd, self.ir_wp,
                                                self.project.bias, self.dw.stride, self.cout, self.has_expand,
-                                               self.use_res)
-            if self.use_ir and self.has_expand and self.dw.dilation == 1 and bool(
+                                               self.use_res, self.dw.dilation)
+            if self.use_ir and self.has_expand and bool(
                     torch.ops.nnsx.ir_expand_dw_supported_f32(self.dw.stride, x.shape[1], x.shape[2], self.cin,
-                                                              self.hid, x.shape[0])):
+                                                              self.hid, x.shape[0], self.dw.dilation)):
                 # expand + depthwise in one kernel (no hidden map in HBM), project as a GEMM
-                h = torch.ops.nnsx.ir_expand_dw(x, self.ir_we, self.ir_be, self.ir_wd, self.ir_bd, self.dw.stride)
+                h = torch.ops.nnsx.ir_expand_dw(x, self.ir_we, self.ir_be, self.ir_wd, self.ir_bd, self.dw.stride,
+                                                self.dw.dilation)
             else:
                 h = self.expand(x) if self.has_expand else x
                 h = self.dw(h)
@@ -211,6 +214,32 @@ class Block(nn.Module):
         if self.use_res:
             return self.project(h, x)
         return self.project(h)
+
+
+class StemBlock1(nn.Module):
+    """A MobileNetV2 backbone's 3x3/2 stem and first block (t = 1, 32 -> 16).
+    fp32 on a uint8 frame: one `stem_ir1` kernel -- the 32-channel stem output
+    (the largest activation of the network) never leaves LDS; otherwise the
+    stem op followed by block 0.  Any frame size (partial tiles are masked)."""
+
+    def __init__(self, stem_w: torch.Tensor, stem_b: torch.Tensor, b0: Block, f32: bool):
+        super().__init__()
+        self.register_buffer("stem_w", stem_w)
+        self.register_buffer("stem_b", stem_b)
+        self.f32 = bool(f32)
+        self.fused = bool(f32 and not b0.has_expand and b0.cin == 32 and b0.cout == 16
+                          and b0.dw.stride == 1 and not b0.use_res and FUSE_STEM)
+        self.register_buffer("s1_wd", b0.dw.w.clone() if self.fused else torch.zeros(1))
+        self.register_buffer("s1_bd", b0.dw.bias.clone() if self.fused else torch.zeros(1))
+        self.register_buffer("s1_wp", b0.project.wt.clone() if self.fused else torch.zeros(1))
+        self.register_buffer("s1_bp", b0.project.bias.clone() if self.fused else torch.zeros(1))
+        self.b0 = b0
+
+    def forward(self, x: torch.Tensor, lut: torch.Tensor) -> torch.Tensor:
+        if self.fused and x.dtype == torch.uint8 and x.is_cuda:
+            return torch.ops.nnsx.stem_ir1(x.contiguous(), self.stem_w, self.stem_b, self.s1_wd, self.s1_bd,
+                                           self.s1_wp, self.s1_bp, lut)
+        return self.b0(stem(x, self.stem_w, self.stem_b, lut, self.f32))
 
 
 class FusedMobileNetV2(nn.Module):

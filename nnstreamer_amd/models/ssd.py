@@ -20,7 +20,7 @@ from typing import List, Tuple
 import torch
 import torch.nn as nn
 
-from .fused import DW, PW, Block, _fold, input_lut, stem
+from .fused import DW, PW, Block, StemBlock1, _fold, input_lut, stem
 from .mobilenet_v2 import ConvBNReLU, MobileNetV2
 
 ANCHORS = (3, 6, 6, 6, 6, 6)
@@ -176,6 +176,8 @@ class FusedSSDLite(nn.Module):
         self.register_buffer("stem_b", b.contiguous())
         self.register_buffer("in_lut", input_lut(-127.5, 127.5))  # uint8 input table (absorbable transform)
         self.blocks = nn.ModuleList([Block(ir, precision) for ir in m.features[1:-1]])  # features[1..17]
+        # stem + block 0 (fp32, uint8 frames: one stem_ir1 kernel)
+        self.front = StemBlock1(self.stem_w.clone(), self.stem_b.clone(), self.blocks[0], self.f32)
         head: ConvBNReLU = m.features[-1]
         self.head = PW(*_fold(head[0], head[1]), act=1, precision=precision)
         self.extras = nn.ModuleList([FusedExtra(e, precision) for e in m.extras])
@@ -185,14 +187,14 @@ class FusedSSDLite(nn.Module):
         return self
 
     def forward(self, x: torch.Tensor):
-        h = stem(x, self.stem_w, self.stem_b, self.in_lut, self.f32)
+        h = self.front(x, self.in_lut)
         feats: List[torch.Tensor] = []
         for i, blk in enumerate(self.blocks):
             if i == self.feat_block:
                 e = blk.expand(h)
                 feats.append(e)
                 h = blk.project(blk.dw(e))
-            else:
+            elif i > 0:  # (block 0 is in self.front)
                 h = blk(h)
         h = self.head(h)
         feats.append(h)

@@ -79,3 +79,45 @@ def test_posenet_fp32_fused_matches_torch_fp32():
         fh, fo = f(x)
         h, o = m((x.float() - 127.5) / 127.5)
     assert _rel(fh, h) < 1e-3 and _rel(fo, o) < 1e-3, (_rel(fh, h), _rel(fo, o))
+
+
+@pytest.mark.parametrize("H,cin,hid,cout,stride,dil", [
+    (33, 96, 576, 160, 1, 2),    # DeepLab output stride 16: dilated depthwise
+    (33, 160, 960, 160, 1, 2),
+    (65, 32, 192, 32, 1, 1),     # odd maps: masked partial tiles
+    (129, 24, 144, 24, 1, 1),
+    (257, 16, 96, 24, 2, 1),
+    (19, 64, 384, 64, 1, 1),     # SSD 19x19
+])
+def test_ir_block_dilated_and_partial_tiles(H, cin, hid, cout, stride, dil):
+    """the fused inverted-residual kernel on map sizes no tile divides and with
+    dilation 2, against the same op's host implementation (fp32)"""
+    g = torch.Generator().manual_seed(H + cin)
+    B = 2
+    kin = (cin + 7) // 8 * 8
+    x = torch.rand(B, H, H, cin, generator=g)
+    we = torch.randn(hid, kin, generator=g) * (2.0 / cin) ** 0.5
+    be = torch.randn(hid, generator=g) * 0.1
+    wd = torch.randn(9, hid, generator=g) * 0.3
+    bd = torch.randn(hid, generator=g) * 0.1
+    wp = torch.randn((cout + 15) // 16 * 16, hid, generator=g) * (1.0 / hid) ** 0.5
+    bp = torch.randn(wp.shape[0], generator=g) * 0.1
+    res = stride == 1 and cin == cout
+    assert torch.ops.nnsx.ir_supported_f32(stride, H, H, cin, hid, cout, True, dil)
+    args = (we, be, wd, bd, wp, bp)
+    ref = torch.ops.nnsx.ir_block(x, *args, stride, cout, True, res, dil)
+    got = torch.ops.nnsx.ir_block(x.cuda(), *[t.cuda() for t in args], stride, cout, True, res, dil).cpu()
+    assert got.shape == ref.shape
+    assert _rel(got, ref) < 1e-5, _rel(got, ref)
+    if dil == 2 and hid == 960:
+        h_ref = torch.ops.nnsx.ir_expand_dw(x, we, be, wd, bd, 1, 2)
+        h = torch.ops.nnsx.ir_expand_dw(x.cuda(), we.cuda(), be.cuda(), wd.cuda(), bd.cuda(), 1, 2).cpu()
+        assert _rel(h, h_ref) < 1e-5, _rel(h, h_ref)
+
+
+@pytest.mark.parametrize("B,HW,C", [(8, 33 * 33, 320), (512, 49, 1280), (3, 5, 12)])
+def test_avgpool_f32(B, HW, C):
+    x = torch.randn(B, HW, 1, C, device="cuda")
+    p = torch.ops.nnsx.avgpool(x)
+    assert _rel(p.cpu(), x.double().cpu().mean((1, 2))) < 1e-6
+    assert torch.equal(p, torch.ops.nnsx.avgpool(x))  # deterministic
