@@ -1569,10 +1569,14 @@ const IrwCfg kIrwCfgs[] = {
     NNSX_IRW(1, 8, 16, 24, 2, 3, true),    // 56x56: expand 192/128 (8x8: 112/64)
     NNSX_IRW(2, 4, 8, 24, 2, 3, true),     // 56 -> 28: expand 160/128 input px (4x4: 96/64)
     NNSX_IRW(2, 8, 8, 16, 2, 3, true),     // 112 -> 56: expand 304/256 (4x8: 160/128)
-    // dilation 2 (DeepLab output stride 16, 33x33 maps at 513 input)
-    NNSX_IRWD(1, 7, 7, 96, 10, 4, false, 2),   // 96 -> 576 -> 160
-    NNSX_IRWD(1, 7, 7, 160, 10, 4, false, 2),  // 160 -> 960 -> 160
-    NNSX_IRWD(1, 7, 7, 160, 0, 4, false, 2),   // 160 -> 960 expand + dw (project -> 320 as a GEMM)
+    // (dilation 2 -- DeepLab's output-stride-16 blocks on 33x33 maps -- as
+    // NNSX_IRWD(1, 7, 7, 160, 10, 4, false, 2) etc. ran 156 vs 120 us for the
+    // unfused expand GEMM + dilated depthwise + project GEMM at batch 8 (the
+    // 11x11 halo window needs 112 KB of LDS: one workgroup per CU), so the
+    // dilated blocks stay unfused: profiles/r3_config_trace_deeplab_b8.txt)
+    // (one wave per 16-channel subtile -- 6 waves on 112 -> 56, 9 on 56 -> 28 --
+    // ran 2x slower: the hidden images of all waves then limit the CU to one
+    // workgroup; profiles/r3_irw_waves_ab_b512.txt)
 };
 #undef NNSX_IRW
 #undef NNSX_IRWD
