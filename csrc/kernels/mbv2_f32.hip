@@ -61,6 +61,7 @@ constexpr int kStemIr1TY = kStemIr1Cfg[0], kStemIr1TX = kStemIr1Cfg[1], kStemIr1
 
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f32x4_t mfma4(float a, float b, f32x4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -1045,7 +1046,14 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
       const int64_t pix = (static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx;
       if (a.ws) {  // hidden parts: this part's slab of the workspace (irw_reduce adds them in order)
         const int64_t plane = static_cast<int64_t>(a.B) * a.Ho * a.Wo * a.cout;
-        *reinterpret_cast<f32x4_t*>(a.ws + part * plane + pix * a.cout + co) = v;
+        if (a.tickets) {  // in-launch combine: written through (sc1) to where every XCD reads it
+          const __amdgpu_buffer_rsrc_t slab = __builtin_amdgcn_make_buffer_rsrc(
+              a.ws, 0, static_cast<int>(nparts * plane * sizeof(float)), 0x00020000);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), slab,
+                                                 static_cast<int>((part * plane + pix * a.cout + co) * 4), 0, 16);
+        } else {
+          *reinterpret_cast<f32x4_t*>(a.ws + part * plane + pix * a.cout + co) = v;
+        }
         continue;
       }
       if (part == 0) {
@@ -1063,35 +1071,39 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
   }
   if (!a.ws || !a.tickets) return;
 
-  // ---- in-launch combine of the hidden parts: every part publishes its slab
-  // with an agent-scope release and draws a ticket; the last of the tile's
-  // parts acquires and adds the slabs in part order, + bias (+ residual) --
-  // the same sums in the same order as irw_reduce, without its launch
+  // ---- in-launch combine of the hidden parts (MI355X hand-off, counter form):
+  // every part's slab went out write-through (sc1, so no release fence); each
+  // storing wave drains it, the workgroup meets at a barrier, one lane draws a
+  // ticket; the tile's last part reads every slab with sc1 loads (so no acquire
+  // fence either) and adds them in part order, + bias (+ residual) -- the sums
+  // of irw_reduce in its order, without its launch -- then resets the ticket
+  // for the next launch (tickets start at zero: the caller's buffer is zeroed
+  // once at creation).  Correct for any placement of the parts over XCDs.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // every wave's slab stores issued and done; the LDS is free
+  __syncthreads();  // every wave's slab stores done; the LDS is free
   int* flag = reinterpret_cast<int*>(smem);
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int t = __hip_atomic_fetch_add(a.tickets + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = t == nparts - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (last) __hip_atomic_store(a.tickets + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *flag = last;
   }
   __syncthreads();
   if (!*flag) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the ticket)
   const int64_t plane = static_cast<int64_t>(a.B) * a.Ho * a.Wo * a.cout;
+  const __amdgpu_buffer_rsrc_t slab =
+      __builtin_amdgcn_make_buffer_rsrc(a.ws, 0, static_cast<int>(nparts * plane * sizeof(float)), 0x00020000);
   const int nq = a.cout / 4;
   for (int v = tid; v < TY * TX * nq; v += NT) {
     const int q = v / nq, co = (v - q * nq) * 4;
     const int gy = oy0 + q / TX, gx = ox0 + q % TX;
     if (gy >= a.Ho || gx >= a.Wo) continue;
     const int64_t e = ((static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx) * a.cout + co;
-    f32x4_t s = *reinterpret_cast<const f32x4_t*>(a.ws + e);
-    for (int p = 1; p < nparts; ++p) s += *reinterpret_cast<const f32x4_t*>(a.ws + p * plane + e);
+    f32x4_t s = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(slab, static_cast<int>(e * 4), 0, 16));
+    for (int p = 1; p < nparts; ++p)
+      s += __builtin_bit_cast(f32x4_t,
+                              __builtin_amdgcn_raw_buffer_load_b128(slab, static_cast<int>((p * plane + e) * 4), 0, 16));
     s += *reinterpret_cast<const f32x4_t*>(a.bp + co);
     if (a.residual) s += *reinterpret_cast<const f32x4_t*>(a.x + (e / a.cout) * a.cin + co);
     *reinterpret_cast<f32x4_t*>(a.y + e) = s;
@@ -1928,9 +1940,12 @@ size_t ir_block_f32_workspace_bytes(const IrBlockF32Args& args) {
 }
 
 // the in-launch combine (irw_f32_kernel's last-part reduction), off unless
-// NNSX_F32_IRW_INLAUNCH=1: at batch 1 it lost to the separate irw_reduce
-// launch -- 7x7 960-hidden block 48.7 vs ~22 us, each block also paying a
-// zero-fill kernel for its tickets (profiles/r3_b1_inlaunch_combine_trace.txt)
+// NNSX_F32_IRW_INLAUNCH=1.  Measured at batch 1 (profiles/r3_b1_inlaunch_combine_trace.txt):
+// with release/acquire fences and per-block ticket fills, 456 vs 306 us per
+// forward; with write-through slabs, no fences and self-resetting tickets,
+// still 386 us -- the last part of a tile adds all slabs alone (15 slabs x 31 KB
+// on the 7x7 960-hidden block: 50 vs 16 + 5.5 us for the kernel + irw_reduce,
+// whose grid spreads the same adds over many workgroups).
 size_t ir_block_f32_tickets(const IrBlockF32Args& args) {
   static const bool on = irw_env("NNSX_F32_IRW_INLAUNCH", 0) != 0;
   if (!on || !ir_block_f32_workspace_bytes(args)) return 0;

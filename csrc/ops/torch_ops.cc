@@ -289,7 +289,8 @@ at::Tensor avgpool_cpu(const at::Tensor& x) { return x.to(at::kFloat).mean({1, 2
 // Fused inverted residual.  we [hid, cin32], wd [9, hid], wp [ceil16(cout), hid] bf16; biases f32.
 at::Tensor ir_block_f32_cuda(const at::Tensor& x, const at::Tensor& we, const at::Tensor& be, const at::Tensor& wd,
                              const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, int64_t stride,
-                             int64_t cout, bool has_expand, bool residual, int64_t dilation) {
+                             int64_t cout, bool has_expand, bool residual, int64_t dilation,
+                             const c10::optional<at::Tensor>& tickets) {
   TORCH_CHECK(x.is_contiguous() && x.dim() == 4, "ir_block(f32): x [B,H,W,C] f32");
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   const int64_t hid = wd.size(1);
@@ -327,10 +328,14 @@ at::Tensor ir_block_f32_cuda(const at::Tensor& x, const at::Tensor& we, const at
     ws = at::empty({static_cast<int64_t>(wsb / sizeof(float))}, x.options());  // caching allocator: graph-capture safe
     a.ws = ws.data_ptr<float>();
   }
-  at::Tensor tickets;
+  // hidden-part tickets of the in-launch combine: the model's zero-initialised
+  // int32 buffer (each launch leaves it zeroed again); without one, or when
+  // too small, the parts are added by a separate reduce launch
   if (const size_t nt = nnsx::kernels::ir_block_f32_tickets(a)) {
-    tickets = at::zeros({static_cast<int64_t>(nt)}, x.options().dtype(at::kInt));
-    a.tickets = tickets.data_ptr<int>();
+    if (tickets.has_value() && tickets->defined() && tickets->is_cuda() && tickets->scalar_type() == at::kInt &&
+        tickets->is_contiguous() && static_cast<size_t>(tickets->numel()) >= nt &&
+        tickets->get_device() == x.get_device())
+      a.tickets = tickets->data_ptr<int>();
   }
   TORCH_CHECK(nnsx::kernels::ir_block_f32(a, cur_stream()), "ir_block(f32): unsupported shape (stride ", stride, ", ",
               H, "x", W, ", cin ", C, ", hid ", hid, ", cout ", cout, ")");
@@ -389,10 +394,11 @@ bool ir_expand_dw_supported_f32(int64_t stride, int64_t H, int64_t W, int64_t ci
 
 at::Tensor ir_block_cuda(const at::Tensor& x, const at::Tensor& we, const at::Tensor& be, const at::Tensor& wd,
                          const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, int64_t stride,
-                         int64_t cout, bool has_expand, bool residual, int64_t dilation) {
+                         int64_t cout, bool has_expand, bool residual, int64_t dilation,
+                         const c10::optional<at::Tensor>& tickets) {
   TORCH_CHECK(x.is_cuda(), "ir_block: x must be a cuda tensor");
   if (x.scalar_type() == at::kFloat)
-    return ir_block_f32_cuda(x, we, be, wd, bd, wp, bp, stride, cout, has_expand, residual, dilation);
+    return ir_block_f32_cuda(x, we, be, wd, bd, wp, bp, stride, cout, has_expand, residual, dilation, tickets);
   TORCH_CHECK(dilation == 1, "ir_block(bf16): dilation 1 only");
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() == 4,
               "ir_block: x [B,H,W,C] bf16");
@@ -428,7 +434,9 @@ at::Tensor ir_block_cuda(const at::Tensor& x, const at::Tensor& we, const at::Te
 
 at::Tensor ir_block_cpu(const at::Tensor& x, const at::Tensor& we, const at::Tensor& be, const at::Tensor& wd,
                         const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, int64_t stride,
-                        int64_t cout, bool has_expand, bool residual, int64_t dilation) {
+                        int64_t cout, bool has_expand, bool residual, int64_t dilation,
+                        const c10::optional<at::Tensor>& tickets) {
+  (void)tickets;
   at::Tensor h = x;
   const int64_t hid = wd.size(1);
   if (has_expand) h = pw_conv_cpu(x, we, be, c10::nullopt, hid, 1, false);
@@ -502,7 +510,7 @@ TORCH_LIBRARY(nnsx, m) {
   m.def("stem_ir1(Tensor x, Tensor ws, Tensor bs, Tensor wd, Tensor bd, Tensor wp, Tensor bp, Tensor lut) -> Tensor");
   m.def("pw_conv_f32_tile(Tensor x, Tensor wt, Tensor bias, Tensor? res, int N, int act, int tile) -> Tensor");
   m.def("ir_block(Tensor x, Tensor we, Tensor be, Tensor wd, Tensor bd, Tensor wp, Tensor bp, int stride, int cout, "
-        "bool has_expand, bool residual, int dilation=1) -> Tensor");
+        "bool has_expand, bool residual, int dilation=1, Tensor(a!)? tickets=None) -> Tensor");
   m.def("ir_supported(int stride, int cin, int hid, int cout) -> bool", ir_supported);
   m.def("ir_supported_f32(int stride, int H, int W, int cin, int hid, int cout, bool has_expand, int dilation=1) -> bool",
         ir_supported_f32);

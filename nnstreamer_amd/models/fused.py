@@ -134,6 +134,9 @@ class Block(nn.Module):
         self.hid = hid
         self.cin = cin
         self.cout = int(p[0].out_channels)
+        # tickets of the fp32 kernel's in-launch combine of hidden-channel parts
+        # (small batches): zero here, and every launch leaves them zero again
+        self.register_buffer("ir_tickets", torch.zeros(256 if self.f32 else 1, dtype=torch.int32))
         if self.f32:
             self._init_f32(cin, hid)
             return
@@ -187,7 +190,7 @@ class Block(nn.Module):
                     self.dw.dilation)):
                 return torch.ops.nnsx.ir_block(x, self.ir_we, self.ir_be, self.ir_wd, self.ir_bd, self.ir_wp,
                                                self.project.bias, self.dw.stride, self.cout, self.has_expand,
-                                               self.use_res, self.dw.dilation)
+                                               self.use_res, self.dw.dilation, self.ir_tickets)
             if self.use_ir and self.has_expand and bool(
                     torch.ops.nnsx.ir_expand_dw_supported_f32(self.dw.stride, x.shape[1], x.shape[2], self.cin,
                                                               self.hid, x.shape[0], self.dw.dilation)):
