@@ -35,6 +35,7 @@ void ensure_builtin_elements() {
     register_fault_inject();
     register_grpc_elements();
     register_host_frameworks();
+    register_lua_framework();
     register_torch_frameworks();
     register_torch_trainer();
     register_simple_decoders();

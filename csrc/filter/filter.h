@@ -26,6 +26,7 @@ bool register_cpp_filter(const std::string& name, CppFilterFactory f);
 bool unregister_cpp_filter(const std::string& name);
 
 void register_host_frameworks();   // custom, custom-easy, cpp
+void register_lua_framework();     // lua (built-in Lua 5.1 subset, filter/lua_vm.h)
 void register_torch_frameworks();  // pytorch (libtorch, ROCm) -- torch TU
 void register_torch_trainer();     // tensor_trainer framework=pytorch -- torch TU
 
