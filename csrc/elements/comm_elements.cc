@@ -10,11 +10,15 @@
 // caps before answering clients), gst/edge/edge_sink.c / edge_src.c.  The
 // reference rides on the external nnstreamer-edge library (TCP / MQTT-hybrid
 // / AITT); nnsx implements TCP and HYBRID (endpoint discovery through an MQTT
-// broker, comm/mqtt.h) natively, plus HIPIPC: the same framing with
+// broker, comm/mqtt.h) natively, MQTT / AITT for edgesink / edgesrc (the
+// frames themselves travel through the broker on the topic: pub/sub without
+// a direct socket, what nnstreamer-edge's MQTT and AITT types give an
+// application; AITT's own library is not in the image), plus HIPIPC: the same framing with
 // HBM-resident tensors handed over through an exported device ring
 // (zero-copy on the same GPU, one xGMI peer copy across GPUs; see
 // comm/transport.h), and RCCL: rank groups over xGMI (comm/group.h).
 #include <algorithm>
+#include <cstring>
 #include <atomic>
 #include <map>
 #include <thread>
@@ -43,12 +47,92 @@ const std::vector<std::string> kRcclModes = {"broadcast", "scatter"};
 constexpr uint32_t kPktCaps = 1;  // packet carries only a caps string
 
 constexpr int kHybrid = 1;
+constexpr int kMqtt = 2;
+constexpr int kAitt = 3;
 
-bool check_connect_type(Element* e, int type) {
+// broker-carried pub/sub (edgesink / edgesrc only)
+bool via_broker(int type) { return type == kMqtt || type == kAitt; }
+
+bool check_connect_type(Element* e, int type, bool pubsub = false) {
   if (type == 0 || type == kHybrid || type == kHipIpc || type == kRccl) return true;
-  e->post_error("connect-type " + kConnectTypes[static_cast<size_t>(type)] +
-                " is not supported (nnsx implements TCP, HYBRID, HIPIPC and RCCL)");
+  if (pubsub && via_broker(type)) return true;
+  e->post_error("connect-type " + kConnectTypes[static_cast<size_t>(type)] + " is not supported by " + e->name() +
+                (pubsub ? " (nnsx implements TCP, HYBRID, MQTT, AITT, HIPIPC and RCCL)"
+                        : " (nnsx implements TCP, HYBRID, HIPIPC and RCCL; MQTT / AITT are pub/sub: edgesink / edgesrc)"));
   return false;
+}
+
+// ---- connect-type=MQTT / AITT: every message is one PUBLISH on
+// nnsx/<type>/<topic>/data (QoS 0, in order over the broker connection); the
+// current caps are also retained on .../caps for subscribers that join late.
+//   u32 magic 'NXBK' | u32 type | u32 nblobs | u32 caps_len
+//   i64 pts | i64 dts | i64 duration | u64 blob_size[nblobs] | caps | blobs
+constexpr uint32_t kBrokerMagic = 0x4e58424bu;
+
+std::string broker_topic(int type, const std::string& topic, const char* leaf) {
+  return strfmt("nnsx/", type == kAitt ? "aitt" : "mqtt", "/", topic.empty() ? "default" : topic, "/", leaf);
+}
+
+std::string broker_header(const comm::Message& m) {
+  std::string h;
+  auto put = [&](const void* p, size_t n) { h.append(static_cast<const char*>(p), n); };
+  const uint32_t w[4] = {kBrokerMagic, static_cast<uint32_t>(m.type), static_cast<uint32_t>(m.blobs.size()),
+                         static_cast<uint32_t>(m.caps.size())};
+  put(w, sizeof(w));
+  const int64_t t[3] = {m.pts, m.dts, m.duration};
+  put(t, sizeof(t));
+  for (auto& b : m.blobs) {
+    const uint64_t n = b->size();
+    put(&n, sizeof(n));
+  }
+  h += m.caps;
+  return h;
+}
+
+bool broker_publish(comm::MqttClient& cli, const std::string& topic, const comm::Message& m) {
+  const std::string h = broker_header(m);
+  if (m.blobs.empty()) return cli.publish(topic, h.data(), h.size(), 0, false);
+  if (m.blobs.size() == 1) {
+    const void* p = m.blobs[0]->map_host();
+    return cli.publish2(topic, h.data(), h.size(), p, m.blobs[0]->size(), 0, false);
+  }
+  std::string body;
+  for (auto& b : m.blobs) body.append(static_cast<const char*>(b->map_host()), b->size());
+  return cli.publish2(topic, h.data(), h.size(), body.data(), body.size(), 0, false);
+}
+
+bool broker_parse(const std::string& pl, comm::Message* m) {
+  size_t at = 0;
+  auto get = [&](void* p, size_t n) {
+    if (pl.size() - at < n) return false;
+    std::memcpy(p, pl.data() + at, n);
+    at += n;
+    return true;
+  };
+  uint32_t w[4];
+  int64_t t[3];
+  if (!get(w, sizeof(w)) || w[0] != kBrokerMagic || w[2] > static_cast<uint32_t>(kSizeLimit + kSizeExtraLimit) ||
+      !get(t, sizeof(t)))
+    return false;
+  std::vector<uint64_t> sizes(w[2]);
+  for (auto& n : sizes)
+    if (!get(&n, sizeof(n))) return false;
+  if (pl.size() - at < w[3]) return false;
+  m->type = static_cast<comm::MsgType>(w[1]);
+  m->caps = pl.substr(at, w[3]);
+  at += w[3];
+  m->pts = t[0];
+  m->dts = t[1];
+  m->duration = t[2];
+  m->blobs.clear();
+  for (uint64_t n : sizes) {
+    if (pl.size() - at < n) return false;
+    auto b = Memory::alloc_host(static_cast<size_t>(n));
+    if (n) std::memcpy(b->data(), pl.data() + at, static_cast<size_t>(n));
+    at += static_cast<size_t>(n);
+    m->blobs.push_back(b);
+  }
+  return true;
 }
 
 // ---- connect-type=HYBRID: the MQTT broker at dest-host:dest-port only
@@ -791,12 +875,23 @@ class EdgeSink : public BaseSink {
  protected:
   bool start() override {
     BaseSink::start();
-    if (!check_connect_type(this, connect_type_)) return false;
+    if (!check_connect_type(this, connect_type_, true)) return false;
     if (connect_type_ == kRccl) {
       running_ = true;
       return true;
     }
     std::string err;
+    if (via_broker(connect_type_)) {
+      static std::atomic<unsigned> seq{0};
+      broker_ = std::make_unique<comm::MqttClient>();
+      if (!broker_->connect(dest_host_, static_cast<int>(dest_port_), strfmt("nnsx-edgesink-", getpid(), "-", seq++),
+                            60, true, 5000, &err)) {
+        post_error("edgesink: broker " + dest_host_ + ":" + std::to_string(dest_port_) + ": " + err);
+        return false;
+      }
+      running_ = true;
+      return true;
+    }
     if (!listener_.listen(host_, port_, &err)) {
       post_error("edgesink: " + err);
       return false;
@@ -835,6 +930,11 @@ class EdgeSink : public BaseSink {
     running_ = false;
     g_.reset();
     announcer_.reset();
+    if (broker_) {
+      if (broker_->connected()) broker_->publish(broker_topic(connect_type_, topic_, "caps"), "", 0, 1, true);
+      broker_->close();
+      broker_.reset();
+    }
     listener_.close();
     if (accept_thr_.joinable()) accept_thr_.join();
     std::vector<std::thread> rs;
@@ -866,6 +966,11 @@ class EdgeSink : public BaseSink {
     std::lock_guard<std::mutex> lk(mu_);
     caps_str_ = caps.to_string();
     m.caps = caps_str_;
+    if (broker_) {
+      const std::string h = broker_header(m);
+      return broker_->publish(broker_topic(connect_type_, topic_, "caps"), h.data(), h.size(), 1, true) &&
+             broker_publish(*broker_, broker_topic(connect_type_, topic_, "data"), m);
+    }
     for (auto& c : subs_) c->send(m);
     return true;
   }
@@ -923,6 +1028,11 @@ class EdgeSink : public BaseSink {
   }
 
   void publish(const comm::Message& m) {
+    if (broker_) {
+      if (!broker_publish(*broker_, broker_topic(connect_type_, topic_, "data"), m) && running_)
+        post_error("edgesink: lost the broker connection");
+      return;
+    }
     std::vector<std::shared_ptr<comm::Connection>> subs;
     {
       std::lock_guard<std::mutex> lk(mu_);
@@ -954,6 +1064,7 @@ class EdgeSink : public BaseSink {
   unsigned rr_ = 0;
   std::shared_ptr<comm::Group> g_;
   std::unique_ptr<HybridAnnouncer> announcer_;
+  std::unique_ptr<comm::MqttClient> broker_;  // connect-type=MQTT / AITT
 };
 
 // =============================================================== edgesrc ====
@@ -980,10 +1091,23 @@ class EdgeSrc : public BaseSrc {
 
  protected:
   bool on_start() override {
-    if (!check_connect_type(this, connect_type_)) return false;
+    if (!check_connect_type(this, connect_type_, true)) return false;
     caps_str_.clear();
     if (connect_type_ == kRccl) return true;
     std::string err;
+    if (via_broker(connect_type_)) {
+      static std::atomic<unsigned> seq{0};
+      broker_ = std::make_unique<comm::MqttClient>();
+      if (!broker_->connect(dest_host_, static_cast<int>(dest_port_), strfmt("nnsx-edgesrc-", getpid(), "-", seq++), 60,
+                            true, 5000, &err) ||
+          !broker_->subscribe(broker_topic(connect_type_, topic_, "caps"), 1) ||
+          !broker_->subscribe(broker_topic(connect_type_, topic_, "data"), 0)) {
+        post_error("edgesrc: broker " + dest_host_ + ":" + std::to_string(dest_port_) + ": " +
+                   (err.empty() ? "subscription failed" : err));
+        return false;
+      }
+      return true;
+    }
     conn_ = connect_endpoint(connect_type_, dest_host_, dest_port_, topic_, 10000, &err);
     if (!conn_) {
       post_error("edgesrc: " + err);
@@ -994,11 +1118,24 @@ class EdgeSrc : public BaseSrc {
   }
   void on_stop() override {
     if (conn_) conn_->close();
+    if (broker_) broker_->close();
     g_.reset();
   }
   void on_unlock() override {
     if (conn_) conn_->close();
     if (auto g = g_) g->cancel();
+  }
+
+  // connect-type=MQTT / AITT: next message from the topic (false: timeout / lost)
+  bool recv_broker(comm::Message* m, int timeout_ms, bool* timed_out) {
+    comm::MqttMessage mm;
+    *timed_out = false;
+    while (broker_->recv(&mm, timeout_ms, timed_out)) {
+      if (mm.payload.empty()) continue;  // a withdrawn retained caps entry
+      if (broker_parse(mm.payload, m)) return true;
+      NNSX_LOGW(name(), "dropping a malformed message on ", mm.topic);
+    }
+    return false;
   }
 
   // connect-type=RCCL: next packet from the publisher (false: cancelled / lost)
@@ -1038,7 +1175,7 @@ class EdgeSrc : public BaseSrc {
     while (caps_str_.empty()) {
       comm::Message m;
       bool timed_out = false;
-      if (!conn_->recv(&m, 100, &timed_out)) {
+      if (!(broker_ ? recv_broker(&m, 100, &timed_out) : conn_->recv(&m, 100, &timed_out))) {
         if (timed_out && !flushing_.load()) continue;
         return false;
       }
@@ -1071,7 +1208,7 @@ class EdgeSrc : public BaseSrc {
     while (true) {
       comm::Message m;
       bool timed_out = false;
-      if (!conn_->recv(&m, 100, &timed_out)) {
+      if (!(broker_ ? recv_broker(&m, 100, &timed_out) : conn_->recv(&m, 100, &timed_out))) {
         if (timed_out && !flushing_.load()) continue;
         return flushing_.load() ? FlowReturn::FLUSHING : FlowReturn::EOS;
       }
@@ -1102,6 +1239,7 @@ class EdgeSrc : public BaseSrc {
   RankProps rp_;
   int rccl_mode_ = 0;
   std::shared_ptr<comm::Group> g_;
+  std::unique_ptr<comm::MqttClient> broker_;  // connect-type=MQTT / AITT
 };
 
 // ====================================================== tensor_allgather ====

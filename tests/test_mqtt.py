@@ -233,3 +233,57 @@ def test_edge_hybrid_pubsub(nns):
     pub.stop()
     b.stop()
     assert out == [0.0, 1.0, 2.0, 3.0]
+
+
+@pytest.mark.parametrize("ctype", ["AITT", "MQTT"])
+def test_edge_broker_pubsub(nns, ctype):
+    """connect-type=AITT / MQTT: frames travel through the broker on the topic
+    (nnstreamer-edge's broker-carried types); two subscribers each get every
+    frame, one that joins late negotiates from the retained caps."""
+    b = nns.MqttBroker()
+    common = f"connect-type={ctype} dest-host=127.0.0.1 dest-port={b.port} topic=cam-{ctype}"
+    subs, outs = [], []
+    for k in range(2):
+        sub = nns.parse_launch(f"edgesrc {common} ! tensor_sink name=sink")
+        out = []
+        sub.get_by_name("sink").connect("new-data", lambda buf, out=out: out.append(
+            (float(buf.memory(0).numpy("float32")[0]), int(buf.memory(1).numpy("uint8")[1]))))
+        sub.set_state("playing")
+        subs.append(sub)
+        outs.append(out)
+    pub = nns.parse_launch(f"appsrc name=src caps={F32} ! edgesink {common}")
+    pub.set_state("playing")
+    src = pub.get_by_name("src")
+    for i in range(3):
+        src.push_buffer([np.full(4, i, np.float32), np.full(2, 10 + i, np.uint8)], pts=i)
+    t0 = time.time()
+    while min(len(o) for o in outs) < 3 and time.time() - t0 < 10:
+        time.sleep(0.01)
+    late = nns.parse_launch(f"edgesrc {common} ! tensor_sink name=sink")
+    late_out = []
+    late.get_by_name("sink").connect("new-data", lambda buf: late_out.append(float(buf.memory(0).numpy("float32")[0])))
+    late.set_state("playing")
+    for i in range(3, 5):
+        src.push_buffer([np.full(4, i, np.float32), np.full(2, 10 + i, np.uint8)], pts=i)
+    src.end_of_stream()
+    assert pub.wait(20)[0] == "eos"
+    for p in subs + [late]:
+        msg = p.wait(20)
+        assert msg and msg[0] == "eos", p.messages()
+        p.stop()
+    pub.stop()
+    b.stop()
+    for out in outs:
+        assert out == [(float(i), 10 + i) for i in range(5)]
+    assert late_out == [3.0, 4.0]
+
+
+def test_query_refuses_pubsub_connect_types(nns):
+    b = nns.MqttBroker()
+    c = nns.parse_launch(f"appsrc name=src caps={F4} ! tensor_query_client connect-type=AITT dest-host=127.0.0.1 "
+                         f"dest-port={b.port} ! tensor_sink")
+    assert c.set_state("playing") is False
+    msg = c.wait(10)
+    assert msg[0] == "error" and "pub/sub" in msg[2], msg
+    c.stop()
+    b.stop()
