@@ -8,6 +8,8 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <ctime>
+#include <random>
 #include <sstream>
 
 namespace nnsx {
@@ -535,8 +537,37 @@ struct VarargE : Expr {
   }
 };
 
-static Value index_value(Exec& x, const Value& o, const Value& k, int line) {
-  if (o.t == Value::TABLE) return o.tab()->get(k);
+// ---- metatables
+enum MetaEvent { M_INDEX, M_NEWINDEX, M_CALL, M_ADD, M_SUB, M_MUL, M_DIV, M_MOD, M_POW, M_IDIV, M_UNM, M_CONCAT,
+                 M_EQ, M_LT, M_LE, M_TOSTRING, M_METATABLE, M_COUNT };
+static const Value& meta_name(MetaEvent e) {
+  static const Value names[M_COUNT] = {
+      Value::string("__index"), Value::string("__newindex"), Value::string("__call"), Value::string("__add"),
+      Value::string("__sub"),   Value::string("__mul"),      Value::string("__div"),  Value::string("__mod"),
+      Value::string("__pow"),   Value::string("__idiv"),     Value::string("__unm"),  Value::string("__concat"),
+      Value::string("__eq"),    Value::string("__lt"),       Value::string("__le"),   Value::string("__tostring"),
+      Value::string("__metatable")};
+  return names[e];
+}
+static Value metamethod(const Value& v, MetaEvent e) {
+  if (v.t != Value::TABLE || !v.tab()->meta) return Value();
+  return v.tab()->meta->get(meta_name(e));
+}
+static Value call1(Exec& x, const Value& fn, std::vector<Value> args, int line) {
+  std::vector<Value> r = x.call(fn, args, line);
+  return r.empty() ? Value() : r[0];
+}
+
+static Value index_value(Exec& x, const Value& o, const Value& k, int line, int depth = 0) {
+  if (o.t == Value::TABLE) {
+    Value r = o.tab()->get(k);
+    if (r.t != Value::NIL || !o.tab()->meta) return r;
+    const Value h = o.tab()->meta->get(meta_name(M_INDEX));
+    if (h.t == Value::NIL) return r;
+    if (h.t == Value::FUNC || h.t == Value::NATIVE) return call1(x, h, {o, k}, line);
+    if (depth > 100) x.error(line, "'__index' chain too long; possible loop");
+    return index_value(x, h, k, line, depth + 1);
+  }
   if (o.t == Value::USERDATA) return o.ud()->index(k);
   if (o.t == Value::STR) {  // ("abc"):upper() etc. go through the string library
     auto it = x.vm.globals_.find("string");
@@ -545,8 +576,21 @@ static Value index_value(Exec& x, const Value& o, const Value& k, int line) {
   x.error(line, "attempt to index a " + o.type_name() + " value");
 }
 
-static void newindex_value(Exec& x, const Value& o, const Value& k, Value v, int line) {
+static void newindex_value(Exec& x, const Value& o, const Value& k, Value v, int line, int depth = 0) {
   if (o.t == Value::TABLE) {
+    if (o.tab()->meta && o.tab()->get(k).t == Value::NIL) {
+      const Value h = o.tab()->meta->get(meta_name(M_NEWINDEX));
+      if (h.t == Value::FUNC || h.t == Value::NATIVE) {
+        std::vector<Value> args{o, k, std::move(v)};
+        x.call(h, args, line);
+        return;
+      }
+      if (h.t != Value::NIL) {
+        if (depth > 100) x.error(line, "'__newindex' chain too long; possible loop");
+        newindex_value(x, h, k, std::move(v), line, depth + 1);
+        return;
+      }
+    }
     try {
       o.tab()->set(k, std::move(v));
     } catch (const LuaError& e) {
@@ -637,15 +681,38 @@ static double arith_num(Exec& x, const Value& v, int line, const char* what) {
   x.error(line, std::string("attempt to perform arithmetic on a ") + v.type_name() + " value" + what);
 }
 
+// a binary metamethod from either operand (Lua 5.1 order: first, then second)
+static bool try_bin_meta(Exec& x, MetaEvent e, const Value& a, const Value& b, int line, Value* out) {
+  Value h = metamethod(a, e);
+  if (h.t == Value::NIL) h = metamethod(b, e);
+  if (h.t == Value::NIL) return false;
+  *out = call1(x, h, {a, b}, line);
+  return true;
+}
+
 static bool lua_lt(Exec& x, const Value& a, const Value& b, int line) {
   if (a.t == Value::NUM && b.t == Value::NUM) return a.n < b.n;
   if (a.t == Value::STR && b.t == Value::STR) return a.str() < b.str();
+  Value r;
+  if (a.t == b.t && try_bin_meta(x, M_LT, a, b, line, &r)) return r.truthy();
   x.error(line, "attempt to compare " + a.type_name() + " with " + b.type_name());
 }
 static bool lua_le(Exec& x, const Value& a, const Value& b, int line) {
   if (a.t == Value::NUM && b.t == Value::NUM) return a.n <= b.n;
   if (a.t == Value::STR && b.t == Value::STR) return a.str() <= b.str();
+  Value r;
+  if (a.t == b.t) {
+    if (try_bin_meta(x, M_LE, a, b, line, &r)) return r.truthy();
+    if (try_bin_meta(x, M_LT, b, a, line, &r)) return !r.truthy();  // a <= b as not (b < a)
+  }
   x.error(line, "attempt to compare " + a.type_name() + " with " + b.type_name());
+}
+static bool lua_eq(Exec& x, const Value& a, const Value& b, int line) {
+  if (ValueEq()(a, b)) return true;
+  if (a.t != Value::TABLE || b.t != Value::TABLE) return false;
+  const Value ha = metamethod(a, M_EQ), hb = metamethod(b, M_EQ);
+  if (ha.t == Value::NIL || !ValueEq()(ha, hb)) return false;  // 5.1: the same __eq on both
+  return call1(x, ha, {a, b}, line).truthy();
 }
 
 enum BinOp { B_ADD, B_SUB, B_MUL, B_DIV, B_IDIV, B_MOD, B_POW, B_CONCAT, B_EQ, B_NE, B_LT, B_LE, B_GT, B_GE };
@@ -675,23 +742,32 @@ struct BinE : Expr {
       }
     }
     switch (op) {
-      case B_EQ: return Value::boolean(ValueEq()(va, vb));
-      case B_NE: return Value::boolean(!ValueEq()(va, vb));
+      case B_EQ: return Value::boolean(lua_eq(x, va, vb, line));
+      case B_NE: return Value::boolean(!lua_eq(x, va, vb, line));
       case B_LT: return Value::boolean(lua_lt(x, va, vb, line));
       case B_LE: return Value::boolean(lua_le(x, va, vb, line));
       case B_GT: return Value::boolean(lua_lt(x, vb, va, line));
       case B_GE: return Value::boolean(lua_le(x, vb, va, line));
       case B_CONCAT: {
-        auto piece = [&](const Value& v) -> std::string {
-          if (v.t == Value::STR) return v.str();
-          if (v.t == Value::NUM) return fmt_number(v.n);
-          x.error(line, "attempt to concatenate a " + v.type_name() + " value");
-        };
-        return Value::string(piece(va) + piece(vb));
+        auto plain = [](const Value& v) { return v.t == Value::STR || v.t == Value::NUM; };
+        if (!plain(va) || !plain(vb)) {
+          Value r;
+          if (try_bin_meta(x, M_CONCAT, va, vb, line, &r)) return r;
+          x.error(line, "attempt to concatenate a " + (plain(va) ? vb : va).type_name() + " value");
+        }
+        return Value::string((va.t == Value::STR ? va.str() : fmt_number(va.n)) +
+                             (vb.t == Value::STR ? vb.str() : fmt_number(vb.n)));
       }
       default: break;
     }
-    const double p = arith_num(x, va, line, ""), q = arith_num(x, vb, line, "");
+    double p, q;
+    if (!tonumber(va, &p) || !tonumber(vb, &q)) {
+      static const MetaEvent ev[] = {M_ADD, M_SUB, M_MUL, M_DIV, M_IDIV, M_MOD, M_POW};
+      Value r;
+      if (op <= B_POW && try_bin_meta(x, ev[op], va, vb, line, &r)) return r;
+      p = arith_num(x, va, line, "");
+      q = arith_num(x, vb, line, "");
+    }
     switch (op) {
       case B_ADD: return Value::number(p + q);
       case B_SUB: return Value::number(p - q);
@@ -727,7 +803,13 @@ struct UnE : Expr {
   Value eval(Exec& x, Frame& f) const override {
     Value v = a->eval(x, f);
     switch (op) {
-      case U_NEG: return Value::number(-arith_num(x, v, line, ""));
+      case U_NEG: {
+        double d;
+        if (tonumber(v, &d)) return Value::number(-d);
+        const Value h = metamethod(v, M_UNM);
+        if (h.t != Value::NIL) return call1(x, h, {v, v}, line);
+        return Value::number(-arith_num(x, v, line, ""));
+      }
       case U_NOT: return Value::boolean(!v.truthy());
       case U_LEN:
         if (v.t == Value::STR) return Value::number(static_cast<double>(v.str().size()));
@@ -963,6 +1045,12 @@ std::vector<Value> Exec::call(const Value& fn, std::vector<Value>& args, int lin
     } catch (const std::exception& e) {
       error(line, std::string(n->name) + ": " + e.what());
     }
+  }
+  if (fn.t == Value::TABLE) {  // __call: the table is the first argument
+    const Value h = metamethod(fn, M_CALL);
+    if (h.t == Value::NIL) error(line, "attempt to call a table value");
+    args.insert(args.begin(), fn);
+    return call(h, args, line);
   }
   if (fn.t != Value::FUNC) error(line, "attempt to call a " + fn.type_name() + " value");
   if (++depth > 200) {
@@ -1711,6 +1799,267 @@ std::vector<Value> table_next(Table* t, const Value& k) {
   return {Value()};
 }
 
+// ---- Lua patterns (string.find / match / gmatch / gsub): backtracking
+// matcher over single-char classes (. %a %d %l %s %u %w %x %p %c and their
+// complements), sets [...], quantifiers * + - ?, anchors, captures (incl.
+// position captures), back-references %1-%9, %b and %f
+class Pattern {
+ public:
+  static constexpr int kMaxCaps = 32;
+  static constexpr std::ptrdiff_t kPos = -2, kOpen = -1;
+
+  Pattern(const std::string& s, const std::string& p)
+      : src_(s.data()), src_end_(s.data() + s.size()), pat_(p.data()), pat_end_(p.data() + p.size()) {}
+
+  // match at s (an offset into the subject): end offset, or -1
+  std::ptrdiff_t match_at(std::ptrdiff_t s, std::ptrdiff_t p) {
+    level_ = 0;
+    depth_ = 0;
+    const char* e = match(src_ + s, pat_ + p);
+    return e ? e - src_ : -1;
+  }
+  int captures() const { return level_; }
+  // capture i (or the whole match s..e when the pattern has none and i == 0)
+  Value capture(int i, std::ptrdiff_t s, std::ptrdiff_t e) const {
+    if (i >= level_) {
+      if (i == 0) return Value::string(std::string(src_ + s, static_cast<size_t>(e - s)));
+      throw LuaError("invalid capture index");
+    }
+    if (cap_[i].len == kPos) return Value::number(static_cast<double>(cap_[i].init - src_ + 1));
+    if (cap_[i].len == kOpen) throw LuaError("unfinished capture");
+    return Value::string(std::string(cap_[i].init, static_cast<size_t>(cap_[i].len)));
+  }
+  std::vector<Value> all_captures(std::ptrdiff_t s, std::ptrdiff_t e, bool whole_if_none) const {
+    std::vector<Value> r;
+    const int n = (level_ == 0 && whole_if_none) ? 1 : level_;
+    for (int i = 0; i < n; ++i) r.push_back(capture(i, s, e));
+    return r;
+  }
+
+ private:
+  struct Cap {
+    const char* init;
+    std::ptrdiff_t len;
+  };
+
+  static bool in_class(int c, int cl) {
+    bool r;
+    switch (std::tolower(cl)) {
+      case 'a': r = std::isalpha(c); break;
+      case 'c': r = std::iscntrl(c); break;
+      case 'd': r = std::isdigit(c); break;
+      case 'l': r = std::islower(c); break;
+      case 'p': r = std::ispunct(c); break;
+      case 's': r = std::isspace(c); break;
+      case 'u': r = std::isupper(c); break;
+      case 'w': r = std::isalnum(c); break;
+      case 'x': r = std::isxdigit(c); break;
+      default: return cl == c;  // %. %% %( ...: the character itself
+    }
+    return std::isupper(cl) ? !r : r;
+  }
+  // one past the class item starting at p
+  const char* item_end(const char* p) const {
+    const char c = *p++;
+    if (c == '%') {
+      if (p >= pat_end_) throw LuaError("malformed pattern (ends with '%')");
+      return p + 1;
+    }
+    if (c == '[') {
+      if (p < pat_end_ && *p == '^') ++p;
+      do {  // (a ']' right after '[' or '[^' is a member)
+        if (p >= pat_end_) throw LuaError("malformed pattern (missing ']')");
+        const char d = *p++;
+        if (d == '%' && p < pat_end_) ++p;
+      } while (p >= pat_end_ || *p != ']');
+      return p + 1;
+    }
+    return p;
+  }
+  // set [..] from p ('[') to close (its ']')
+  static bool in_set(int c, const char* p, const char* close) {
+    bool yes = true;
+    if (p[1] == '^') {
+      yes = false;
+      ++p;
+    }
+    while (++p < close) {
+      if (*p == '%' && p + 1 < close) {
+        ++p;
+        if (in_class(c, static_cast<unsigned char>(*p))) return yes;
+      } else if (p + 2 < close && p[1] == '-') {
+        if (static_cast<unsigned char>(p[0]) <= c && c <= static_cast<unsigned char>(p[2])) return yes;
+        p += 2;
+      } else if (static_cast<unsigned char>(*p) == c) {
+        return yes;
+      }
+    }
+    return !yes;
+  }
+  bool single(const char* s, const char* p, const char* ep) const {
+    if (s >= src_end_) return false;
+    const int c = static_cast<unsigned char>(*s);
+    switch (*p) {
+      case '.': return true;
+      case '%': return in_class(c, static_cast<unsigned char>(p[1]));
+      case '[': return in_set(c, p, ep - 1);
+      default: return static_cast<unsigned char>(*p) == c;
+    }
+  }
+
+  const char* match(const char* s, const char* p) {
+    struct Depth {
+      int& d;
+      explicit Depth(int& x) : d(x) {
+        if (++d > 220) throw LuaError("pattern too complex");
+      }
+      ~Depth() { --d; }
+    } guard(depth_);
+    while (p < pat_end_) {
+      switch (*p) {
+        case '(':
+          if (p + 1 < pat_end_ && p[1] == ')') return open_capture(s, p + 2, kPos);
+          return open_capture(s, p + 1, kOpen);
+        case ')': return close_capture(s, p + 1);
+        case '$':
+          if (p + 1 == pat_end_) return s == src_end_ ? s : nullptr;
+          break;
+        case '%':
+          if (p + 1 < pat_end_ && p[1] == 'b') {
+            s = balance(s, p + 2);
+            if (!s) return nullptr;
+            p += 4;
+            continue;
+          }
+          if (p + 1 < pat_end_ && p[1] == 'f') {
+            p += 2;
+            if (p >= pat_end_ || *p != '[') throw LuaError("missing '[' after '%f' in pattern");
+            const char* ep = item_end(p);
+            const int prev = s == src_ ? 0 : static_cast<unsigned char>(s[-1]);
+            const int cur = s < src_end_ ? static_cast<unsigned char>(*s) : 0;
+            if (in_set(prev, p, ep - 1) || !in_set(cur, p, ep - 1)) return nullptr;
+            p = ep;
+            continue;
+          }
+          if (p + 1 < pat_end_ && std::isdigit(static_cast<unsigned char>(p[1]))) {
+            s = backref(s, p[1]);
+            if (!s) return nullptr;
+            p += 2;
+            continue;
+          }
+          break;
+        default: break;
+      }
+      const char* ep = item_end(p);
+      const char q = ep < pat_end_ ? *ep : '\0';
+      if (q == '?') {
+        if (single(s, p, ep))
+          if (const char* r = match(s + 1, ep + 1)) return r;
+        p = ep + 1;
+        continue;
+      }
+      if (q == '+') return single(s, p, ep) ? greedy(s + 1, p, ep) : nullptr;
+      if (q == '*') return greedy(s, p, ep);
+      if (q == '-') return lazy(s, p, ep);
+      if (!single(s, p, ep)) return nullptr;
+      ++s;
+      p = ep;
+    }
+    return s;
+  }
+  const char* greedy(const char* s, const char* p, const char* ep) {
+    std::ptrdiff_t n = 0;
+    while (single(s + n, p, ep)) ++n;
+    for (; n >= 0; --n)
+      if (const char* r = match(s + n, ep + 1)) return r;
+    return nullptr;
+  }
+  const char* lazy(const char* s, const char* p, const char* ep) {
+    for (;;) {
+      if (const char* r = match(s, ep + 1)) return r;
+      if (!single(s, p, ep)) return nullptr;
+      ++s;
+    }
+  }
+  const char* open_capture(const char* s, const char* p, std::ptrdiff_t what) {
+    if (level_ >= kMaxCaps) throw LuaError("too many captures");
+    cap_[level_] = {s, what};
+    ++level_;
+    const char* r = match(s, p);
+    if (!r) --level_;
+    return r;
+  }
+  const char* close_capture(const char* s, const char* p) {
+    int l = level_ - 1;
+    while (l >= 0 && cap_[l].len != kOpen) --l;
+    if (l < 0) throw LuaError("invalid pattern capture");
+    cap_[l].len = s - cap_[l].init;
+    const char* r = match(s, p);
+    if (!r) cap_[l].len = kOpen;
+    return r;
+  }
+  const char* balance(const char* s, const char* p) const {
+    if (p + 1 >= pat_end_) throw LuaError("missing arguments to '%b'");
+    if (s >= src_end_ || *s != p[0]) return nullptr;
+    int open = 1;
+    while (++s < src_end_) {
+      if (*s == p[1]) {
+        if (--open == 0) return s + 1;
+      } else if (*s == p[0]) {
+        ++open;
+      }
+    }
+    return nullptr;
+  }
+  const char* backref(const char* s, char d) const {
+    const int l = d - '1';
+    if (l < 0 || l >= level_ || cap_[l].len == kOpen) throw LuaError("invalid capture index");
+    const size_t n = static_cast<size_t>(cap_[l].len);
+    if (static_cast<size_t>(src_end_ - s) >= n && std::memcmp(cap_[l].init, s, n) == 0) return s + n;
+    return nullptr;
+  }
+
+  const char *src_, *src_end_, *pat_, *pat_end_;
+  int level_ = 0, depth_ = 0;
+  Cap cap_[kMaxCaps];
+};
+
+bool has_specials(const std::string& p) { return p.find_first_of("^$*+?.([%-") != std::string::npos; }
+
+// 1-based (negative from the end) string position -> 0-based offset in [0, n]
+std::ptrdiff_t str_start(double i, size_t n) {
+  std::ptrdiff_t k = static_cast<std::ptrdiff_t>(i);
+  if (k < 0) k = static_cast<std::ptrdiff_t>(n) + k + 1;
+  if (k < 1) k = 1;
+  return k - 1;
+}
+
+// string.find (find = true) / string.match
+std::vector<Value> str_find(std::vector<Value>& a, bool find) {
+  const char* fn = find ? "find" : "match";
+  const std::string s = str_arg(a, 0, fn), p = str_arg(a, 1, fn);
+  const std::ptrdiff_t init = str_start(a.size() > 2 && a[2].t != Value::NIL ? num_arg(a, 2, fn) : 1, s.size());
+  if (init > static_cast<std::ptrdiff_t>(s.size())) return {Value()};
+  if (find && ((a.size() > 3 && a[3].truthy()) || !has_specials(p))) {
+    const size_t at = s.find(p, static_cast<size_t>(init));
+    if (at == std::string::npos) return {Value()};
+    return {Value::number(static_cast<double>(at + 1)), Value::number(static_cast<double>(at + p.size()))};
+  }
+  Pattern m(s, p);
+  const bool anchor = !p.empty() && p[0] == '^';
+  for (std::ptrdiff_t i = init; i <= static_cast<std::ptrdiff_t>(s.size()); ++i) {
+    const std::ptrdiff_t e = m.match_at(i, anchor ? 1 : 0);
+    if (e >= 0) {
+      if (!find) return m.all_captures(i, e, true);
+      std::vector<Value> r{Value::number(static_cast<double>(i + 1)), Value::number(static_cast<double>(e))};
+      for (auto& c : m.all_captures(i, e, false)) r.push_back(c);
+      return r;
+    }
+    if (anchor) break;
+  }
+  return {Value()};
+}
+
 std::string lua_format(std::vector<Value>& a) {
   const std::string f = str_arg(a, 0, "format");
   std::string out;
@@ -1780,9 +2129,18 @@ void VM::open_libs() {
   auto& G = globals_;
   auto g = [&](const std::string& n, Fn f) { G[n] = Value::native(n, std::move(f)); };
 
-  g("print", [](std::vector<Value>& a) {
+  // tostring honouring __tostring
+  auto to_str = [this](const Value& v) {
+    const Value h = metamethod(v, M_TOSTRING);
+    if (h.t == Value::NIL) return tostring(v);
+    Exec x{*this, 0, chunkname_};
+    const Value r = call1(x, h, {v}, 0);
+    if (r.t != Value::STR && r.t != Value::NUM) throw LuaError("'__tostring' must return a string");
+    return tostring(r);
+  };
+  g("print", [to_str](std::vector<Value>& a) {
     std::string s;
-    for (size_t i = 0; i < a.size(); ++i) s += (i ? "\t" : "") + tostring(a[i]);
+    for (size_t i = 0; i < a.size(); ++i) s += (i ? "\t" : "") + to_str(a[i]);
     std::fprintf(stdout, "%s\n", s.c_str());
     std::fflush(stdout);
     return std::vector<Value>{};
@@ -1791,7 +2149,24 @@ void VM::open_libs() {
     if (a.empty()) throw LuaError("bad argument #1 to 'type' (value expected)");
     return std::vector<Value>{Value::string(a[0].type_name())};
   });
-  g("tostring", [](std::vector<Value>& a) { return std::vector<Value>{Value::string(tostring(arg(a, 0)))}; });
+  g("tostring", [to_str](std::vector<Value>& a) { return std::vector<Value>{Value::string(to_str(arg(a, 0)))}; });
+  g("setmetatable", [](std::vector<Value>& a) {
+    Table* t = tab_arg(a, 0, "setmetatable");
+    const Value& mt = arg(a, 1);
+    if (mt.t != Value::NIL && mt.t != Value::TABLE)
+      throw LuaError("bad argument #2 to 'setmetatable' (nil or table expected)");
+    if (t->meta && t->meta->get(meta_name(M_METATABLE)).t != Value::NIL)
+      throw LuaError("cannot change a protected metatable");
+    t->meta = mt.t == Value::TABLE ? std::static_pointer_cast<Table>(mt.o) : nullptr;
+    return std::vector<Value>{a[0]};
+  });
+  g("getmetatable", [](std::vector<Value>& a) {
+    const Value& v = arg(a, 0);
+    if (v.t != Value::TABLE || !v.tab()->meta) return std::vector<Value>{Value()};
+    const Value prot = v.tab()->meta->get(meta_name(M_METATABLE));
+    if (prot.t != Value::NIL) return std::vector<Value>{prot};
+    return std::vector<Value>{Value::table(v.tab()->meta)};
+  });
   g("tonumber", [](std::vector<Value>& a) {
     const Value& v = arg(a, 0);
     if (a.size() > 1 && arg(a, 1).t == Value::NUM) {
@@ -1915,6 +2290,22 @@ void VM::open_libs() {
     for (size_t i = 1; i < a.size(); ++i) m = std::min(m, num_arg(a, i, "min"));
     return std::vector<Value>{Value::number(m)};
   });
+  auto rng = std::make_shared<std::mt19937_64>(0x5eed);
+  reg(math.get(), "random", [rng](std::vector<Value>& a) {
+    const double u = std::uniform_real_distribution<double>(0.0, 1.0)(*rng);
+    if (a.empty()) return std::vector<Value>{Value::number(u)};
+    double lo = 1, hi = num_arg(a, 0, "random");
+    if (a.size() > 1) {
+      lo = hi;
+      hi = num_arg(a, 1, "random");
+    }
+    if (lo > hi) throw LuaError("bad argument to 'random' (interval is empty)");
+    return std::vector<Value>{Value::number(std::floor(lo + u * (std::floor(hi) - std::floor(lo) + 1)))};
+  });
+  reg(math.get(), "randomseed", [rng](std::vector<Value>& a) {
+    rng->seed(static_cast<uint64_t>(static_cast<int64_t>(num_arg(a, 0, "randomseed"))));
+    return std::vector<Value>{};
+  });
   math->set(Value::string("pi"), Value::number(M_PI));
   math->set(Value::string("huge"), Value::number(HUGE_VAL));
   G["math"] = Value::table(math);
@@ -1958,9 +2349,16 @@ void VM::open_libs() {
   });
   reg(str.get(), "byte", [](std::vector<Value>& a) {
     const std::string s = str_arg(a, 0, "byte");
-    const long i = a.size() > 1 ? static_cast<long>(num_arg(a, 1, "byte")) : 1;
-    if (i < 1 || i > static_cast<long>(s.size())) return std::vector<Value>{};
-    return std::vector<Value>{Value::number(static_cast<unsigned char>(s[static_cast<size_t>(i - 1)]))};
+    const long n = static_cast<long>(s.size());
+    long i = a.size() > 1 && a[1].t != Value::NIL ? static_cast<long>(num_arg(a, 1, "byte")) : 1;
+    long j = a.size() > 2 && a[2].t != Value::NIL ? static_cast<long>(num_arg(a, 2, "byte")) : i;
+    if (i < 0) i = n + i + 1;
+    if (j < 0) j = n + j + 1;
+    if (i < 1) i = 1;
+    if (j > n) j = n;
+    std::vector<Value> r;
+    for (long k = i; k <= j; ++k) r.push_back(Value::number(static_cast<unsigned char>(s[static_cast<size_t>(k - 1)])));
+    return r;
   });
   reg(str.get(), "char", [](std::vector<Value>& a) {
     std::string s;
@@ -1968,12 +2366,94 @@ void VM::open_libs() {
     return std::vector<Value>{Value::string(s)};
   });
   reg(str.get(), "format", [](std::vector<Value>& a) { return std::vector<Value>{Value::string(lua_format(a))}; });
-  reg(str.get(), "find", [](std::vector<Value>& a) {  // plain find (patterns are not supported)
-    const std::string s = str_arg(a, 0, "find"), p = str_arg(a, 1, "find");
-    const long init = a.size() > 2 ? static_cast<long>(num_arg(a, 2, "find")) : 1;
-    const size_t at = s.find(p, static_cast<size_t>(std::max(init, 1L) - 1));
-    if (at == std::string::npos) return std::vector<Value>{Value()};
-    return std::vector<Value>{Value::number(static_cast<double>(at + 1)), Value::number(static_cast<double>(at + p.size()))};
+  reg(str.get(), "find", [](std::vector<Value>& a) { return str_find(a, true); });
+  reg(str.get(), "match", [](std::vector<Value>& a) { return str_find(a, false); });
+  reg(str.get(), "gmatch", [](std::vector<Value>& a) {
+    struct State {
+      std::string s, p;
+      std::ptrdiff_t pos = 0;
+    };
+    auto st = std::make_shared<State>();
+    st->s = str_arg(a, 0, "gmatch");
+    st->p = str_arg(a, 1, "gmatch");
+    return std::vector<Value>{Value::native("gmatch_iter", [st](std::vector<Value>&) {
+      Pattern m(st->s, st->p);
+      for (std::ptrdiff_t i = st->pos; i <= static_cast<std::ptrdiff_t>(st->s.size()); ++i) {
+        const std::ptrdiff_t e = m.match_at(i, 0);
+        if (e >= 0) {
+          st->pos = e == i ? e + 1 : e;  // an empty match steps one character on
+          return m.all_captures(i, e, true);
+        }
+      }
+      st->pos = static_cast<std::ptrdiff_t>(st->s.size()) + 1;
+      return std::vector<Value>{Value()};
+    })};
+  });
+  reg(str.get(), "gsub", [this](std::vector<Value>& a) {
+    const std::string s = str_arg(a, 0, "gsub"), p = str_arg(a, 1, "gsub");
+    const Value repl = arg(a, 2);
+    if (repl.t != Value::STR && repl.t != Value::NUM && repl.t != Value::TABLE && repl.t != Value::FUNC &&
+        repl.t != Value::NATIVE)
+      throw LuaError("bad argument #3 to 'gsub' (string/function/table expected)");
+    const double max_n = a.size() > 3 && a[3].t != Value::NIL ? num_arg(a, 3, "gsub") : 1e300;
+    const bool anchor = !p.empty() && p[0] == '^';
+    Pattern m(s, p);
+    Exec x{*this, 0, chunkname_};
+    std::string out;
+    double n = 0;
+    std::ptrdiff_t i = 0;
+    const std::ptrdiff_t len = static_cast<std::ptrdiff_t>(s.size());
+    while (n < max_n) {
+      const std::ptrdiff_t e = m.match_at(i, anchor ? 1 : 0);
+      if (e >= 0) {
+        ++n;
+        const std::string whole = s.substr(static_cast<size_t>(i), static_cast<size_t>(e - i));
+        Value v;
+        if (repl.t == Value::STR || repl.t == Value::NUM) {
+          const std::string r = repl.t == Value::STR ? repl.str() : fmt_number(repl.n);
+          std::string add;
+          for (size_t k = 0; k < r.size(); ++k) {
+            if (r[k] != '%') {
+              add += r[k];
+              continue;
+            }
+            if (++k >= r.size()) throw LuaError("invalid use of '%' in replacement string");
+            if (r[k] == '%') {
+              add += '%';
+            } else if (std::isdigit(static_cast<unsigned char>(r[k]))) {
+              add += r[k] == '0' ? whole : tostring(m.capture(r[k] - '1', i, e));
+            } else {
+              throw LuaError("invalid use of '%' in replacement string");
+            }
+          }
+          v = Value::string(add);
+        } else {
+          const Value key = m.capture(0, i, e);
+          if (repl.t == Value::TABLE) {
+            v = index_value(x, repl, key, 0);
+          } else {
+            std::vector<Value> caps = m.all_captures(i, e, true);
+            std::vector<Value> r = x.call(repl, caps, 0);
+            v = r.empty() ? Value() : r[0];
+          }
+        }
+        if (!v.truthy())
+          out += whole;  // false / nil: keep the match
+        else if (v.t == Value::STR || v.t == Value::NUM)
+          out += tostring(v);
+        else
+          throw LuaError("invalid replacement value (a " + v.type_name() + ")");
+      }
+      if (e >= 0 && e > i)
+        i = e;
+      else if (i < len)
+        out += s[static_cast<size_t>(i++)];
+      else
+        break;
+      if (anchor) break;
+    }
+    if (i < len) out += s.substr(static_cast<size_t>(i));
+    return std::vector<Value>{Value::string(out), Value::number(n)};
   });
   G["string"] = Value::table(str);
 
@@ -2017,7 +2497,56 @@ void VM::open_libs() {
   reg(tab.get(), "getn", [](std::vector<Value>& a) {
     return std::vector<Value>{Value::number(static_cast<double>(tab_arg(a, 0, "getn")->length()))};
   });
+  // table.sort: a merge sort (well defined even for an inconsistent comparator)
+  reg(tab.get(), "sort", [this](std::vector<Value>& a) {
+    Table* t = tab_arg(a, 0, "sort");
+    const Value cmp = arg(a, 1);
+    if (cmp.t != Value::NIL && cmp.t != Value::FUNC && cmp.t != Value::NATIVE)
+      throw LuaError("bad argument #2 to 'sort' (function expected)");
+    Exec x{*this, 0, chunkname_};
+    const size_t n = t->length();
+    std::vector<Value> v(t->arr.begin(), t->arr.begin() + static_cast<std::ptrdiff_t>(n)), tmp(n);
+    auto less = [&](const Value& p, const Value& q) {
+      if (cmp.t == Value::NIL) return lua_lt(x, p, q, 0);
+      return call1(x, cmp, {p, q}, 0).truthy();
+    };
+    for (size_t w = 1; w < n; w *= 2)
+      for (size_t lo = 0; lo + w < n; lo += 2 * w) {
+        const size_t mid = lo + w, hi = std::min(n, lo + 2 * w);
+        size_t i = lo, j = mid, k = lo;
+        while (i < mid && j < hi) tmp[k++] = less(v[j], v[i]) ? v[j++] : v[i++];
+        while (i < mid) tmp[k++] = v[i++];
+        while (j < hi) tmp[k++] = v[j++];
+        std::copy(tmp.begin() + static_cast<std::ptrdiff_t>(lo), tmp.begin() + static_cast<std::ptrdiff_t>(hi),
+                  v.begin() + static_cast<std::ptrdiff_t>(lo));
+      }
+    for (size_t i = 0; i < n; ++i) t->set(Value::number(static_cast<double>(i + 1)), v[i]);
+    return std::vector<Value>{};
+  });
+  tab->set(Value::string("unpack"), G["unpack"]);
   G["table"] = Value::table(tab);
+
+  // os: the clock / time / date subset (no process or file access)
+  auto os = std::make_shared<Table>();
+  reg(os.get(), "clock", [](std::vector<Value>&) {
+    return std::vector<Value>{Value::number(static_cast<double>(std::clock()) / CLOCKS_PER_SEC)};
+  });
+  reg(os.get(), "time", [](std::vector<Value>&) {
+    return std::vector<Value>{Value::number(static_cast<double>(std::time(nullptr)))};
+  });
+  reg(os.get(), "date", [](std::vector<Value>& a) {
+    const std::string f = a.empty() || a[0].t == Value::NIL ? "%c" : str_arg(a, 0, "date");
+    const std::time_t t = a.size() > 1 ? static_cast<std::time_t>(num_arg(a, 1, "date")) : std::time(nullptr);
+    std::tm tm{};
+    if (!f.empty() && f[0] == '!')
+      gmtime_r(&t, &tm);
+    else
+      localtime_r(&t, &tm);
+    char buf[256];
+    const size_t n = std::strftime(buf, sizeof(buf), f.c_str() + (!f.empty() && f[0] == '!' ? 1 : 0), &tm);
+    return std::vector<Value>{Value::string(std::string(buf, n))};
+  });
+  G["os"] = Value::table(os);
   G["_VERSION"] = Value::string("Lua 5.1 (nnsx)");
 }
 

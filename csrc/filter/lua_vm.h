@@ -7,9 +7,11 @@
 // assignment / returns, local / global variables, if / while / repeat /
 // numeric and generic for / break / return, method calls, long strings and
 // comments, and the base / math / string / table library functions that
-// tensor scripts use.  Not covered: coroutines, metatables on tables, goto,
-// the io / os / debug libraries (a script using them fails to load or run
-// with a LuaError naming the construct).
+// tensor scripts use, metatables (__index, __newindex, __call, arithmetic,
+// comparison, __concat, __unm, __tostring, __metatable) and Lua patterns
+// (string.find / match / gmatch / gsub).  Not covered: coroutines, goto, the
+// io / debug libraries and most of os (a script using them fails to load or
+// run with a LuaError naming the construct).
 //
 // Host objects (the input / output tensors) are Userdata with virtual
 // index / newindex / length.
@@ -87,6 +89,7 @@ struct ValueEq {
 struct Table : Obj {
   std::vector<Value> arr;  // keys 1..arr.size()
   std::unordered_map<Value, Value, ValueHash, ValueEq> hash;
+  std::shared_ptr<Table> meta;  // setmetatable()
   Value get(const Value& k) const;
   void set(const Value& k, Value v);
   size_t length() const;  // the border of the array part (Lua's # on sequences)

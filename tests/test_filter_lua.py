@@ -298,3 +298,95 @@ def test_reference_model_scripts(nns, name):
         hs = np.floor(np.arange(240) * (480 / 240)).astype(int)
         ws = np.floor(np.arange(320) * (640 / 320)).astype(int)
         np.testing.assert_array_equal(y.reshape(240, 320, 3), x[hs][:, ws])
+
+
+def test_metatables_patterns_and_libraries(nns):
+    """Lua 5.1 features beyond the tensor scripts' core: metatables (OOP via
+    __index, operators, __call, __tostring, __newindex), Lua patterns
+    (find / match / gmatch / gsub with captures, sets, anchors, %b), table.sort
+    and the os / math.random subset -- results land in a float64 output."""
+    script = textwrap.dedent(r"""
+        inputTensorsInfo = { num = 1, dim = {{1}}, type = {'uint8'} }
+        outputTensorsInfo = { num = 1, dim = {{20}}, type = {'float64'} }
+        local Vec = {}
+        Vec.__index = Vec
+        function Vec.new(x, y) return setmetatable({x = x, y = y}, Vec) end
+        function Vec:len2() return self.x * self.x + self.y * self.y end
+        Vec.__add = function(a, b) return Vec.new(a.x + b.x, a.y + b.y) end
+        Vec.__eq = function(a, b) return a.x == b.x and a.y == b.y end
+        Vec.__lt = function(a, b) return a:len2() < b:len2() end
+        Vec.__le = function(a, b) return a:len2() <= b:len2() end
+        Vec.__unm = function(a) return Vec.new(-a.x, -a.y) end
+        Vec.__tostring = function(a) return "(" .. a.x .. "," .. a.y .. ")" end
+        Vec.__concat = function(a, b) return tostring(a) .. tostring(b) end
+        Vec.__call = function(self, k) return self.x * k end
+        function nnstreamer_invoke()
+          local o = output_tensor(1)
+          local v = Vec.new(1, 2) + Vec.new(3, 4)
+          o[1] = v:len2()                                             -- 16 + 36 = 52
+          o[2] = (Vec.new(1, 1) == Vec.new(1, 1)) and 1 or 0          -- 1
+          o[3] = (Vec.new(1, 1) < Vec.new(2, 2)) and 1 or 0           -- 1
+          o[4] = (-v).x                                                -- -4
+          o[5] = #tostring(v)                                          -- "(4,6)" = 5
+          o[6] = v(10)                                                 -- 40
+          o[7] = #(Vec.new(1, 2) .. Vec.new(3, 4))                     -- "(1,2)(3,4)" = 10
+          local log = {}
+          local proxy = setmetatable({}, {__newindex = function(t, k, val) rawset(t, k, val * 2); log[#log + 1] = k end})
+          proxy.a = 5
+          o[8] = proxy.a + #log                                        -- 10 + 1
+          local defaults = setmetatable({}, {__index = function(t, k) return #k end})
+          o[9] = defaults.hello                                        -- 5
+          local s, e, word = string.find("say hello world", "(%a+)", 5)
+          o[10] = s * 100 + e                                          -- 5*100 + 9
+          o[11] = tonumber(string.match("id=42;", "id=(%d+)"))         -- 42
+          local sum = 0
+          for n in string.gmatch("1, 22, 333", "%d+") do sum = sum + tonumber(n) end
+          o[12] = sum                                                  -- 356
+          local r, n = string.gsub("hello world", "(%w+)", "<%1>")
+          o[13] = #r * 10 + n                                          -- "<hello> <world>" 15 -> 152
+          local r2 = string.gsub("abc", "%w", {a = "1", b = false})   -- "1bc": false keeps the match
+          local r3 = string.gsub(r2, "%a", function(c) return c == "c" and "3" or nil end)
+          o[14] = (r3 == "1b3") and 1 or 0
+          o[15] = (string.find("f(a(b)c)d", "%b()")) or -1             -- 2
+          o[16] = (string.match("  trim me  ", "^%s*(.-)%s*$") == "trim me") and 1 or 0
+          local t = {5, 3, 9, 1}
+          table.sort(t)
+          o[17] = t[1] * 1000 + t[2] * 100 + t[3] * 10 + t[4]          -- 1359
+          table.sort(t, function(a, b) return a > b end)
+          o[18] = t[1]                                                 -- 9
+          math.randomseed(7)
+          local a1 = math.random(1, 100)
+          math.randomseed(7)
+          o[19] = (a1 == math.random(1, 100) and a1 >= 1 and a1 <= 100) and 1 or 0
+          o[20] = (os.clock() >= 0 and os.time() > 1e9 and #os.date("%Y") == 4) and 1 or 0
+        end
+    """)
+    with nns.Single(script, framework="lua") as s:
+        (y,) = s.invoke(np.zeros(1, np.uint8))
+        got = np.asarray(y).view(np.float64).reshape(-1).tolist()
+    assert got == [52, 1, 1, -4, 5, 40, 10, 11, 5, 509, 42, 356, 152, 1, 2, 1, 1359, 9, 1, 1]
+
+
+@pytest.mark.parametrize("expr,want", [
+    ('select(2, string.gsub("hello", "", "-"))', 6),                  # empty pattern matches 6 times
+    ('#(string.gsub("hello", "", "-"))', 11),                         # "-h-e-l-l-o-"
+    ('select(2, string.gsub("aaa", "^a", "b"))', 1),                  # anchored: one substitution
+    ('string.find("THE (quick) fox", "%((%a+)%)")', 5),
+    ('select(3, string.find("hello", "()ll()"))', 3),                 # position captures
+    ('select(2, string.find("abcabc", "(abc)%1"))', 6),               # back-reference
+    ('string.find("THE quick", "%f[%a]%a+", 4)', 5),                  # frontier
+    ('#string.match("key = value", "(%w+)%s*=%s*(%w+)")', 3),
+    ('string.find("a.b", ".", 1, true) + string.find("a.b", "%.")', 4),
+    ('select("#", string.match("2024-01-15", "(%d+)-(%d+)-(%d+)"))', 3),
+    ('tonumber(string.format("%.2f", 3.14159)) * 100', 314),
+    ('string.byte("AB", 1, 2) + select(2, string.byte("AB", 1, 2))', 131),
+    ('#string.rep("ab", 3) + #string.reverse("xyz")', 9),
+    ('(string.match("[[nested]]", "%[(%b[])%]")) == "[nested]" and 1 or 0', 1),
+])
+def test_lua_pattern_semantics(nns, expr, want):
+    script = ("inputTensorsInfo = { num = 1, dim = {{1}}, type = {'uint8'} }\n"
+              "outputTensorsInfo = { num = 1, dim = {{1}}, type = {'float64'} }\n"
+              f"function nnstreamer_invoke() output_tensor(1)[1] = {expr} end\n")
+    with nns.Single(script, framework="lua") as s:
+        (y,) = s.invoke(np.zeros(1, np.uint8))
+    assert np.asarray(y).view(np.float64)[0] == want
