@@ -58,6 +58,13 @@ class ImageLabeling : public DecoderInstance {
     return c;
   }
   bool supports_device() const override { return true; }
+  // the producing filter runs the argmax (runtime/fusion.h): int32 [1:B] indices arrive
+  bool accept_argmax_input(uint32_t classes) override {
+    if (labels_.empty() || classes == 0) return false;
+    indices_ = true;
+    return true;
+  }
+  void drop_argmax_input() override { indices_ = false; }
 
   FlowReturn decode(const TensorsConfig& config, const std::vector<MemoryPtr>& in, Buffer* out,
                     InvokeContext& ctx) override {
@@ -65,7 +72,20 @@ class ImageLabeling : public DecoderInstance {
     uint64_t n = ti.dim[0];
     uint32_t batch = ti.dim[1];
     std::vector<int32_t> idx(batch, 0);
-    if (ctx.device >= 0) {
+    if (indices_ && ti.type == DType::INT32 && n == 1) {
+      // only the B indices cross to the host
+      if (ctx.device >= 0 && in[0]->on_device()) {
+        if (!host_idx_ || host_idx_->size() < batch * sizeof(int32_t))
+          host_idx_ = Memory::alloc_pinned(batch * sizeof(int32_t));
+        hip::check(hipMemcpyAsync(host_idx_->data(), in[0]->map_device(ctx.device, ctx.stream),
+                                  batch * sizeof(int32_t), hipMemcpyDeviceToHost, ctx.stream),
+                   "D2H indices");
+        hip::check(hipStreamSynchronize(ctx.stream), "sync indices");
+        std::memcpy(idx.data(), host_idx_->data(), batch * sizeof(int32_t));
+      } else {
+        std::memcpy(idx.data(), in[0]->map_host(), batch * sizeof(int32_t));
+      }
+    } else if (ctx.device >= 0) {
       const void* src = in[0]->map_device(ctx.device, ctx.stream);
       if (!dev_idx_ || dev_idx_->size() < batch * sizeof(int32_t)) {
         dev_idx_ = Memory::alloc_device(batch * sizeof(int32_t), ctx.device, ctx.stream);
@@ -109,6 +129,7 @@ class ImageLabeling : public DecoderInstance {
 
  private:
   std::vector<std::string> labels_;
+  bool indices_ = false;  // argmax absorbed upstream
   MemoryPtr dev_idx_, host_idx_;
   int last_index_ = -1;
 };

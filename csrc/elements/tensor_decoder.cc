@@ -6,6 +6,7 @@
 #include "elements/elements.h"
 #include "elements/tensor_common.h"
 #include "runtime/base.h"
+#include "runtime/fusion.h"
 #include "runtime/pipeline.h"
 #include "runtime/plugin_api.h"
 
@@ -29,7 +30,7 @@ class CustomCodeDecoder : public DecoderInstance {
   DecoderCustomFn fn_;
 };
 
-class TensorDecoder : public BaseTransform {
+class TensorDecoder : public BaseTransform, public ArgmaxConsumer {
  public:
   explicit TensorDecoder(const std::string& name)
       : BaseTransform("tensor_decoder", name, Caps::from_string(tensor_caps_template_all()), Caps::Any()) {
@@ -48,6 +49,20 @@ class TensorDecoder : public BaseTransform {
       load_config_file();
     });
     prop_int("device", &device_, "nnsx: -2 follow input placement, -1 CPU, N run post-processing kernels on GPU N");
+    prop_readonly("argmax-by", [this] { return argmax_by_; },
+                  "nnsx: the upstream tensor_filter that runs this decoder's argmax inside its device work "
+                  "(runtime/fusion.h; empty: the decoder runs it)");
+  }
+
+  // ---- ArgmaxConsumer (runtime/fusion.h) ----
+  bool take_argmax(unsigned tensor, uint32_t classes, const std::string& by) override {
+    if (tensor != 0 || !inst_ || !inst_->accept_argmax_input(classes)) return false;
+    argmax_by_ = by;
+    return true;
+  }
+  void drop_argmax() override {
+    if (inst_) inst_->drop_argmax_input();
+    argmax_by_.clear();
   }
 
  protected:
@@ -191,6 +206,7 @@ class TensorDecoder : public BaseTransform {
   std::string mode_, options_[9], config_file_;
   int device_ = -2;
   std::unique_ptr<DecoderInstance> inst_;
+  std::string argmax_by_;
   TensorsConfig config_;
   StreamSet streams_;
 };

@@ -151,6 +151,11 @@ class TensorFilter : public BaseTransform, public TransformAbsorber {
                   "(custom=broadcast:<root>)");
     prop_readonly("absorbed", [this] { return absorbed_from_; },
                   "nnsx: name of the tensor_transform absorbed at caps negotiation (empty: none)");
+    prop_bool("absorb-decoder", &absorb_dec_enabled_,
+              "nnsx: run an adjacent downstream image_labeling decoder's argmax at the end of the model's device "
+              "work (inside its hipGraph); the decoder then receives int32 indices");
+    prop_readonly("absorbed-decoder", [this] { return absorbed_decoder_; },
+                  "nnsx: name of the tensor_decoder whose argmax this filter runs (empty: none)");
   }
 
   // V1 SET_INPUT_PROP / SET_OUTPUT_PROP once the framework is open
@@ -321,6 +326,54 @@ class TensorFilter : public BaseTransform, public TransformAbsorber {
     return r;
   }
 
+  // ---- argmax absorption (runtime/fusion.h ArgmaxConsumer) ----
+  // A single float score tensor [classes:B] feeding (through queues) a decoder
+  // that starts with an argmax: the framework appends the argmax to its device
+  // work and the tensor leaves as int32 indices [1:B].
+  void absorb_decoder_argmax(TensorsInfo* mout) {
+    if (!argmax_tried_) {
+      argmax_tried_ = true;
+      const bool fp = mout->num_tensors == 1 &&
+                      (mout->at(0).type == DType::FLOAT32 || mout->at(0).type == DType::FLOAT16 ||
+                       mout->at(0).type == DType::FLOAT64 || mout->at(0).type == DType::BFLOAT16);
+      bool shape_ok = fp && mout->at(0).dim[0] > 1;
+      for (int r = 2; shape_ok && r < kRankLimit; ++r) shape_ok = mout->at(0).dim[r] <= 1;
+      if (absorb_dec_enabled_ && inst_ && !shared_ && out_comb_.empty() && !props_.invoke_dynamic && shape_ok &&
+          inst_->accepts_output_argmax(0)) {
+        Pad* sp = src_pad();
+        Element* dn = sp && sp->peer() ? sp->peer()->parent() : nullptr;
+        while (dn && dn->factory() == "queue") {
+          Pad* q = dn->src_pad();
+          dn = q && q->peer() ? q->peer()->parent() : nullptr;
+        }
+        if (auto* c = dynamic_cast<ArgmaxConsumer*>(dn)) {
+          if (c->take_argmax(0, mout->at(0).dim[0], name())) {
+            if (inst_->set_output_argmax(0, true)) {
+              argmax_consumer_ = c;
+              absorbed_decoder_ = dn->name();
+              NNSX_LOGI(name(), "runs the argmax of ", absorbed_decoder_, " at the end of its device work");
+            } else {
+              c->drop_argmax();
+            }
+          }
+        }
+      }
+    }
+    if (argmax_consumer_ && mout->num_tensors >= 1) {
+      mout->at(0).type = DType::INT32;
+      mout->at(0).dim[0] = 1;
+    }
+  }
+  void release_decoder_argmax() {
+    if (argmax_consumer_) {
+      argmax_consumer_->drop_argmax();
+      if (inst_) inst_->set_output_argmax(0, false);
+    }
+    argmax_consumer_ = nullptr;
+    absorbed_decoder_.clear();
+    argmax_tried_ = false;
+  }
+
   bool output_info_for(const TensorsConfig& in, TensorsInfo* out) {
     TensorsInfo min = combined_in(in.info);
     TensorsInfo mout;
@@ -341,6 +394,7 @@ class TensorFilter : public BaseTransform, public TransformAbsorber {
       }
     }
     if (out_comb_.empty()) {
+      absorb_decoder_argmax(&mout);
       *out = mout;
       return true;
     }
@@ -768,6 +822,7 @@ class TensorFilter : public BaseTransform, public TransformAbsorber {
   bool stop() override {
     poll_device_stats(true);
     detach_absorbable();
+    release_decoder_argmax();
     return true;
   }
   void release_timing_events() {
@@ -795,6 +850,10 @@ class TensorFilter : public BaseTransform, public TransformAbsorber {
   bool latency_report_ = false;
   int latency_mode_ = 0, throughput_mode_ = 0;
   bool absorb_enabled_ = true;
+  bool absorb_dec_enabled_ = true;
+  bool argmax_tried_ = false;
+  ArgmaxConsumer* argmax_consumer_ = nullptr;
+  std::string absorbed_decoder_;
   AbsorbableElement* absorbable_up_ = nullptr;
   std::string absorbed_from_;
   int device_prop_ = -1;

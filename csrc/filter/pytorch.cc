@@ -31,6 +31,7 @@
 #include "core/log.h"
 #include "filter/filter.h"
 #include "filter/torch_util.h"
+#include "kernels/kernels.h"
 #include "runtime/hip_util.h"
 #include "runtime/plugin_api.h"
 
@@ -123,6 +124,18 @@ class TorchInstance : public FilterInstance {
     }
     lut_ = lut;
     if (props_.input_info.num_tensors > 0) props_.input_info.at(0).type = DType::UINT8;
+    clear_graphs();
+    return true;
+  }
+
+  // a downstream image_labeling decoder's argmax, run at the end of the
+  // forward (inside the captured graph): output `index` becomes the int32
+  // index of the largest score along its last dimension (runtime/fusion.h)
+  bool accepts_output_argmax(unsigned index) const override { return index == 0; }
+  bool set_output_argmax(unsigned index, bool on) override {
+    if (index != 0) return false;
+    std::lock_guard<std::mutex> lk(mu_);
+    argmax_out_ = on ? 0 : -1;
     clear_graphs();
     return true;
   }
@@ -291,6 +304,26 @@ class TorchInstance : public FilterInstance {
     return finish_module(torch::jit::load(is, dev()));
   }
 
+  // outs[argmax_out_] -> int32 index of the first largest value along the last
+  // dimension (the decoder's rule), on the device with kernels::argmax_rows
+  void apply_argmax(std::vector<at::Tensor>* outs, hipStream_t s) {
+    if (argmax_out_ < 0 || static_cast<size_t>(argmax_out_) >= outs->size()) return;
+    at::Tensor t = (*outs)[static_cast<size_t>(argmax_out_)].contiguous();
+    if (t.dim() == 0 || t.numel() == 0) return;
+    std::vector<int64_t> sizes = t.sizes().vec();
+    const int64_t n = sizes.back();
+    sizes.back() = 1;
+    at::Tensor idx;
+    if (t.is_cuda()) {
+      idx = at::empty(sizes, t.options().dtype(at::kInt));
+      kernels::argmax_rows(t.data_ptr(), from_torch(t.scalar_type()), static_cast<uint64_t>(n),
+                           static_cast<uint32_t>(t.numel() / n), idx.data_ptr<int32_t>(), s);
+    } else {
+      idx = t.argmax(-1, /*keepdim=*/true).to(at::kInt);
+    }
+    (*outs)[static_cast<size_t>(argmax_out_)] = idx;
+  }
+
   at::Tensor prepare(at::Tensor t) {
     if (compute_dtype_ != DType::END && at::isFloatingType(t.scalar_type())) t = t.to(to_torch(compute_dtype_));
     if (channels_last_ && t.dim() == 4) t = t.contiguous(at::MemoryFormat::ChannelsLast);
@@ -381,6 +414,7 @@ class TorchInstance : public FilterInstance {
       std::vector<c10::IValue> iv;
       for (auto& t : inputs) iv.push_back(prepare(t));
       flatten(module_.forward(iv), &outs);
+      apply_argmax(&outs, s);
     }
     for (auto& m : in)
       if (dev_idx >= 0) m->record_use(s, dev_idx);
@@ -509,6 +543,7 @@ class TorchInstance : public FilterInstance {
       iv.clear();
       for (auto& t : src) iv.push_back(prepare(t));
       flatten(module_.forward(iv), &gs->static_out);
+      apply_argmax(&gs->static_out, cap_stream_);
       gs->graph->capture_end();
       size_t out_bytes = 0;
       for (auto& t : gs->static_out) out_bytes += t.numel() * t.element_size();
@@ -543,6 +578,7 @@ class TorchInstance : public FilterInstance {
   bool channels_last_ = false;
   DType compute_dtype_ = DType::END;
   std::mutex mu_;
+  int argmax_out_ = -1;        // output replaced by its argmax (absorbed decoder), -1: none
   bool has_lut_ = false;       // the model maps uint8 input 0 through attribute in_lut
   std::vector<float> lut_;     // the absorbed table (re-applied on hot reload)
   std::map<std::string, std::vector<std::unique_ptr<GraphState>>> graphs_;

@@ -48,6 +48,21 @@ class AbsorbableElement {
   virtual bool absorbed() const = 0;
 };
 
+// Downstream: `tensor_filter ! [queue !] tensor_decoder mode=image_labeling`
+// classifies by an argmax over the scores.  A filter whose framework can run
+// that argmax at the end of its own device work (inside its captured hipGraph)
+// asks the decoder to take the int32 indices instead: the scores never leave
+// the graph (no copy-out of [classes x B] floats, no separate argmax launch
+// between the graph and the decoder), only B indices cross to the host.
+class ArgmaxConsumer {  // implemented by tensor_decoder
+ public:
+  virtual ~ArgmaxConsumer() = default;
+  // the producer would hand over indices of tensor `tensor` ([classes:B]
+  // scores -> int32 [1:B]); true = accepted (the decoder now expects them)
+  virtual bool take_argmax(unsigned tensor, uint32_t classes, const std::string& by) = 0;
+  virtual void drop_argmax() = 0;
+};
+
 // The transform's output for every uint8 value 0..255 (out must be FLOAT32):
 // the table an absorbing model applies.  Computed with the transform's own
 // host arithmetic (tensor_transform.cc), which its device kernel matches.

@@ -95,6 +95,18 @@ class FilterInstance {
     (void)lut;
     return false;
   }
+  // Downstream-argmax absorption (runtime/fusion.h): true when the framework
+  // can end its device work with an argmax over the innermost dimension of
+  // output `index`, producing int32 indices (that dimension becomes 1)
+  virtual bool accepts_output_argmax(unsigned index) const {
+    (void)index;
+    return false;
+  }
+  virtual bool set_output_argmax(unsigned index, bool on) {
+    (void)index;
+    (void)on;
+    return false;
+  }
   // Property changes after open (reference V1 events CUSTOM_PROP,
   // SET_INPUT_PROP / SET_OUTPUT_PROP, SET_ACCELERATOR): true = applied.
   virtual bool update_custom(const std::string& custom) {
@@ -166,6 +178,15 @@ class DecoderInstance {
   virtual FlowReturn decode(const TensorsConfig& config, const std::vector<MemoryPtr>& in, Buffer* out,
                             InvokeContext& ctx) = 0;
   virtual bool supports_device() const { return false; }
+  // Argmax absorption (runtime/fusion.h): a decoder whose first step is an
+  // argmax over the innermost dimension of tensor 0 may receive the producer's
+  // int32 indices [1:B] instead of the scores [classes:B].  true = from now on
+  // decode() takes indices.
+  virtual bool accept_argmax_input(uint32_t classes) {
+    (void)classes;
+    return false;
+  }
+  virtual void drop_argmax_input() {}
 };
 
 class DecoderSubplugin {

@@ -388,3 +388,38 @@ def test_reference_string_absorbed_at_bench_batch(nns, workdir, labels):
     agree = sum(a == b for a, b in zip(got, ref))
     assert same >= B - 2, (same, B)       # two fp32 kernel paths: ties may flip at most a frame or two
     assert agree >= 0.995 * B, (agree, B)
+
+
+@pytest.mark.parametrize("B", [16, 1])
+def test_decoder_argmax_absorbed_in_graph(nns, workdir, labels, B):
+    """tensor_filter (fused fp32, hipGraph) ! queue ! tensor_decoder
+    mode=image_labeling: the filter captures the decoder's argmax in its graph
+    (int32 indices leave the model, runtime/fusion.h ArgmaxConsumer); labels
+    equal the pipeline where the decoder runs its own argmax kernel."""
+    import os
+
+    from nnstreamer_amd.models.export import export
+
+    model = export("mobilenet_v2_fused_fp32", os.path.join(workdir, "mbv2_f32_argmax.pt"), layout="nhwc")
+
+    def run(absorb):
+        desc = (f"videotestsrc num-buffers={B * 3} pattern=snow pool-size=48 "
+                "! video/x-raw,format=RGB,width=224,height=224,framerate=0/1 "
+                f"! tensor_converter frames-per-tensor={B} device=0 "
+                f"! tensor_filter name=f framework=pytorch model={model} input=3:224:224:{B} inputtype=uint8 "
+                f"accelerator=true:gpu device=0 custom=hipgraph:true absorb-decoder={'true' if absorb else 'false'} "
+                f"! queue max-size-buffers=4 ! tensor_decoder name=dec mode=image_labeling option1={labels} "
+                "! tensor_sink name=sink")
+        p = nns.parse_launch(desc)
+        out = []
+        p.get_by_name("sink").connect("new-data", lambda b: out.append(b.memory(0).bytes().decode()))
+        p.run(timeout=120)
+        info = (p.get_by_name("f").get_property("absorbed-decoder"), p.get_by_name("dec").get_property("argmax-by"))
+        p.stop()
+        return out, info
+
+    a, info = run(True)
+    assert info == ("dec", "f")
+    b, info_b = run(False)
+    assert info_b == ("", "")
+    assert len(a) == 3 and a == b

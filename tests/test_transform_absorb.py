@@ -83,3 +83,35 @@ def test_lut_matches_transform_arithmetic():
     v = torch.arange(256, dtype=torch.float32)
     ref = (v + np.float32(-127.5)) / np.float32(127.5)
     assert torch.equal(input_lut(-127.5, 127.5), ref)
+
+
+def _run_labels(nns, model, workdir, absorb, frames=3, queue=True, dev=""):
+    from nnstreamer_amd.models.export import write_labels
+
+    labels = write_labels(os.path.join(workdir, "labels_absorb.txt"))
+    q = "queue max-size-buffers=2 ! " if queue else ""
+    desc = (f"videotestsrc num-buffers={frames} pattern=snow ! video/x-raw,format=RGB,width=224,height=224,"
+            f"framerate=30/1 ! tensor_converter frames-per-tensor={frames} {dev} ! {NORM} "
+            f"! tensor_filter name=f framework=pytorch model={model} input=3:224:224:{frames} inputtype=float32 "
+            f"absorb-decoder={'true' if absorb else 'false'} {dev} ! {q}"
+            f"tensor_decoder name=dec mode=image_labeling option1={labels} ! tensor_sink name=sink")
+    p = nns.parse_launch(desc)
+    out = []
+    p.get_by_name("sink").connect("new-data", lambda b: out.append(bytes(b.memory(0).bytes())))
+    p.run(timeout=300)
+    info = (p.get_by_name("f").get_property("absorbed-decoder"), p.get_by_name("dec").get_property("argmax-by"))
+    p.stop()
+    assert len(out) == 1
+    return out[0].decode().split("\n"), info
+
+
+@pytest.mark.parametrize("queue", [True, False])
+def test_downstream_argmax_absorbed(nns, fused_f32, workdir, queue):
+    """tensor_filter ! [queue !] tensor_decoder mode=image_labeling: the filter
+    runs the decoder's argmax after its forward (int32 indices leave the model,
+    runtime/fusion.h ArgmaxConsumer); labels equal the unabsorbed pipeline's."""
+    a, info = _run_labels(nns, fused_f32, workdir, absorb=True, queue=queue)
+    assert info == ("dec", "f")
+    b, info_b = _run_labels(nns, fused_f32, workdir, absorb=False, queue=queue)
+    assert info_b == ("", "")
+    assert a == b and len(a) == 3
