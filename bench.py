@@ -280,6 +280,7 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
     gathered = pipe.get_by_name("ag").get_property("comm-bytes") if cfg.get("gather") else None
     dev_stamps = filt_el.get_property("device-stamps") if (filt_el is not None and use_gpu) else ""
     absorbed = filt_el.get_property("absorbed") if filt_el is not None else ""
+    absorbed_dec = filt_el.get_property("absorbed-decoder") if filt_el is not None else ""
     # the nnsx rank groups this rank actually used (data plane : members)
     groups = {}
     if filt_el is not None and filt_el.get_property("model-broadcast"):
@@ -293,7 +294,8 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
     import numpy as np
 
     rec = dict(elapsed=0.0, p50=0.0, p99=0.0, gpu_elapsed=0.0, gpu_busy_ms=0.0, wall=t_end - t_start,
-               desc=desc, fan=fan, workers=workers, absorbed=absorbed, gathered=gathered, groups=groups)
+               desc=desc, fan=fan, workers=workers, absorbed=absorbed, absorbed_dec=absorbed_dec, gathered=gathered,
+               groups=groups)
     if sink is None:
         return rec  # the workers' clocks decide
     recs = [tuple(int(v) for v in e.split(":")) for e in sink.get_property("stats").split(",") if e]
@@ -510,6 +512,9 @@ def main():
             "preprocess": (f"tensor_transform (reference string) absorbed by tensor_filter into the model's uint8 "
                            f"input table ({head['absorbed']}: frames stay uint8)" if head["absorbed"]
                            else "tensor_transform element (own kernel, float32 frames into the model)"),
+            "postprocess": (f"image_labeling argmax run by tensor_filter inside its hipGraph ({head['absorbed_dec']}: "
+                            "int32 indices leave the model)" if head.get("absorbed_dec")
+                            else "tensor_decoder's own argmax kernel"),
             "wall_s": round(sum(r["wall"] for r in results.values()), 3),
             "numa_binding": numa,
             **({"allgather_bytes_sent_received_rank0": head["gathered"]} if head["gathered"] is not None else {}),
