@@ -477,8 +477,7 @@ struct Frame {
 };
 
 struct Exec {
-  VM& vm;
-  int depth = 0;
+  VM& vm;  // (its depth_ counts nested Lua calls across every Exec: pcall, gsub, sort callbacks)
   std::string chunk;
   [[noreturn]] void error(int line, const std::string& m) const {
     throw LuaError(chunk + ":" + std::to_string(line) + ": " + m);
@@ -1053,8 +1052,8 @@ std::vector<Value> Exec::call(const Value& fn, std::vector<Value>& args, int lin
     return call(h, args, line);
   }
   if (fn.t != Value::FUNC) error(line, "attempt to call a " + fn.type_name() + " value");
-  if (++depth > 200) {
-    depth = 0;
+  if (++vm.depth_ > 200) {
+    --vm.depth_;
     error(line, "stack overflow");
   }
   auto* c = static_cast<Closure*>(fn.o.get());
@@ -1070,10 +1069,10 @@ std::vector<Value> Exec::call(const Value& fn, std::vector<Value>& args, int lin
   try {
     if (exec_block(*this, fr, p->body) == Stmt::RETURN) out = std::move(fr.ret);
   } catch (...) {
-    --depth;
+    --vm.depth_;
     throw;
   }
-  --depth;
+  --vm.depth_;
   return out;
 }
 
@@ -1218,6 +1217,7 @@ class Parser {
   static bool block_end(Tok t) { return t == T_EOF || t == K_END || t == K_ELSE || t == K_ELSEIF || t == K_UNTIL; }
 
   Block block() {
+    Nest guard(*this);
     Block b;
     while (!block_end(tk_.t)) {
       if (tk_.t == K_RETURN) {
@@ -1655,7 +1655,18 @@ class Parser {
   }
   static constexpr int kUnaryPrio = 8;
 
+  // (nesting depth of expressions / blocks: a pathological script cannot
+  // recurse the parser off the C++ stack)
+  struct Nest {
+    Parser& p;
+    explicit Nest(Parser& x) : p(x) {
+      if (++p.nest_ > 200) p.error("chunk has too many syntax levels");
+    }
+    ~Nest() { --p.nest_; }
+  };
+
   ExprP expr(int limit = 0) {
+    Nest guard(*this);
     ExprP e;
     const int line = tk_.line;
     if (tk_.t == K_NOT || tk_.t == S_MINUS || tk_.t == S_HASH) {
@@ -1713,6 +1724,7 @@ class Parser {
   Token tk_, ahead_;
   bool has_ahead_ = false;
   FuncState* fs_ = nullptr;
+  int nest_ = 0;
 };
 
 }  // namespace
@@ -1742,7 +1754,7 @@ void VM::run(const std::string& source, const std::string& chunkname) {
 }
 
 std::vector<Value> VM::call(const Value& fn, std::vector<Value> args) {
-  Exec x{*this, 0, chunkname_};
+  Exec x{*this, chunkname_};
   steps_ = 0;
   return x.call(fn, args, 0);
 }
@@ -2133,7 +2145,7 @@ void VM::open_libs() {
   auto to_str = [this](const Value& v) {
     const Value h = metamethod(v, M_TOSTRING);
     if (h.t == Value::NIL) return tostring(v);
-    Exec x{*this, 0, chunkname_};
+    Exec x{*this, chunkname_};
     const Value r = call1(x, h, {v}, 0);
     if (r.t != Value::STR && r.t != Value::NUM) throw LuaError("'__tostring' must return a string");
     return tostring(r);
@@ -2230,7 +2242,7 @@ void VM::open_libs() {
   g("pcall", [this](std::vector<Value>& a) {
     if (a.empty()) throw LuaError("bad argument #1 to 'pcall' (value expected)");
     std::vector<Value> rest(a.begin() + 1, a.end());
-    Exec x{*this, 0, chunkname_};
+    Exec x{*this, chunkname_};
     try {
       std::vector<Value> r = x.call(a[0], rest, 0);
       r.insert(r.begin(), Value::boolean(true));
@@ -2398,7 +2410,7 @@ void VM::open_libs() {
     const double max_n = a.size() > 3 && a[3].t != Value::NIL ? num_arg(a, 3, "gsub") : 1e300;
     const bool anchor = !p.empty() && p[0] == '^';
     Pattern m(s, p);
-    Exec x{*this, 0, chunkname_};
+    Exec x{*this, chunkname_};
     std::string out;
     double n = 0;
     std::ptrdiff_t i = 0;
@@ -2503,7 +2515,7 @@ void VM::open_libs() {
     const Value cmp = arg(a, 1);
     if (cmp.t != Value::NIL && cmp.t != Value::FUNC && cmp.t != Value::NATIVE)
       throw LuaError("bad argument #2 to 'sort' (function expected)");
-    Exec x{*this, 0, chunkname_};
+    Exec x{*this, chunkname_};
     const size_t n = t->length();
     std::vector<Value> v(t->arr.begin(), t->arr.begin() + static_cast<std::ptrdiff_t>(n)), tmp(n);
     auto less = [&](const Value& p, const Value& q) {

@@ -128,6 +128,7 @@ class VM {
   // (interpreter internals)
   std::unordered_map<std::string, Value> globals_;
   uint64_t steps_ = 0, step_limit_ = 0;
+  int depth_ = 0;  // nested Lua calls (capped: "stack overflow")
   std::vector<std::unique_ptr<Chunk>> chunks_;
   std::string chunkname_;
 

@@ -390,3 +390,25 @@ def test_lua_pattern_semantics(nns, expr, want):
     with nns.Single(script, framework="lua") as s:
         (y,) = s.invoke(np.zeros(1, np.uint8))
     assert np.asarray(y).view(np.float64)[0] == want
+
+
+def test_runaway_recursion_and_nesting_fail_cleanly(nns):
+    """Unbounded recursion through pcall ends at the interpreter's depth cap
+    (each pcall level sees the error) instead of overflowing the C++ stack, and
+    a script nested deeper than the parser allows fails to load."""
+    script = _IO + textwrap.dedent("""
+        function nnstreamer_invoke()
+          local depth = 0
+          local function f(n) depth = math.max(depth, n); pcall(f, n + 1) end
+          f(1)
+          output_tensor(1)[1] = depth
+        end
+    """)
+    with nns.Single(script, framework="lua") as s:
+        (y,) = s.invoke(np.zeros(4, np.float32))
+        assert 100 <= np.asarray(y).view(np.float32)[0] <= 200
+        (y,) = s.invoke(np.zeros(4, np.float32))  # the depth counter was restored
+        assert 100 <= np.asarray(y).view(np.float32)[0] <= 200
+    deep = _IO + "x = " + "(" * 5000 + "1" + ")" * 5000 + "\nfunction nnstreamer_invoke() end\n"
+    with pytest.raises(Exception):
+        nns.Single(deep, framework="lua")
