@@ -80,6 +80,10 @@ void stem3x3_f32(const float* x, const float* w, const float* bias, float* y, in
 void stem3x3_u8_f32(const uint8_t* x, const float* w, const float* bias, float* y, int B, int H, int W, int act,
                     const float* lut, hipStream_t s);
 void avgpool_f32(const float* x, float* y, int B, int HW, int C, hipStream_t s);
+// head 1x1 conv + act + global average pool in one launch (small batches):
+// x [B][HW][K] -> y [B][N] = mean_p act(x[b][p] . wt^T + bias)
+void pw_pool_f32(const float* x, const float* wt, const float* bias, float* y, int B, int HW, int N, int K, int Kpad,
+                 int Npad, int act, hipStream_t s);
 
 // fused inverted residual, fp32.  we [hid][KIN] (KIN = ceil8(cin), zero
 // padded), wd [9][hid], wp [ceil16(cout)][hid] (rows zero padded); biases
@@ -100,10 +104,17 @@ struct IrBlockF32Args {
   int Ho = 0, Wo = 0, tiles_x = 0, tiles_y = 0;
   int hsplit = 1;  // hidden-channel parts per tile (wave-split kernel)
   float* ws = nullptr;  // partial-sum workspace (ir_block_f32_workspace_bytes; small batches)
-  // per-tile tickets, zeroed before the launch (ir_block_f32_tickets entries):
-  // the last part of a tile to finish adds the slabs in the same launch
-  // instead of a separate reduce kernel
+  // per-tile tickets (ir_block_f32_tickets entries, zeroed once at creation):
+  // the hidden parts are added inside the launch instead of by a separate
+  // reduce kernel (spread form below by default; NNSX_F32_IRW_INLAUNCH=1: the
+  // last part of a tile to finish adds all slabs)
   int* tickets = nullptr;
+  // spread = 1: every part of a tile waits at a per-tile arrival counter (64-bit,
+  // monotone: tickets[] read as uint64) and then adds its 1/parts share of the
+  // tile's outputs from all slabs -- the combine spread over the parts, not left
+  // to the last one.  Only launched when every workgroup of the grid is resident
+  // at once (the host checks occupancy); the wait is bounded.
+  int spread = 0;
 };
 bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout, bool has_expand, int dil = 1);
 // device workspace ir_block_f32 needs for these args (0 = none)

@@ -267,6 +267,114 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce_kernel(const float* __
   }
 }
 
+// ------------------------------------------------------------ pw_small_f32 ----
+// Small-M 1x1 conv / FC (M <= 64 rows per workgroup: batch-1 7x7 projects, the
+// head, the classifier) in ONE launch, no split-K workspace and no reduce
+// launch: a workgroup = 16 output channels x up to 64 rows, its 4 waves =
+// RT row tiles x KS k-slices (RT * KS = 4: M <= 16 -> one row tile and 4
+// k-slices, <= 32 -> 2 x 2, else 4 x 1).  Each wave runs 4 independent
+// MFMA chains (k16 steps s mod 4, added at the end) so the 40-cycle MFMA
+// dependency is hidden; k-slices are added through LDS in slice order
+// (deterministic).  A / B fragments come straight from global memory (the
+// operands are L2-resident at these sizes).
+// POOL: rows = the HW pixels of image blockIdx.y (waves walk its 16-pixel
+// tiles), output = act(.) averaged over the pixels -> y [B][N] (head conv +
+// global average pool in one pass; the pooled sum is over pixel tiles in
+// order, pixels within a tile by a fixed butterfly).
+template <bool POOL>
+__global__ void __launch_bounds__(256) pw_small_f32_kernel(const float* __restrict__ x, const float* __restrict__ wt,
+                                                           const float* __restrict__ bias,
+                                                           const float* __restrict__ res, float* __restrict__ y,
+                                                           int M, int N, int K, int Kpad, int Npad, int act, int HW) {
+  __shared__ f32x4_t red[4][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * 16;
+  int RT = 4, KS = 1;
+  if (!POOL && M <= 16) RT = 1, KS = 4;
+  else if (!POOL && M <= 32) RT = 2, KS = 2;
+  const int rt = wave % RT, ks = wave / RT;
+  const int nsteps = (K + 15) / 16;
+  const int s0 = ks * nsteps / KS, s1 = (ks + 1) * nsteps / KS;
+  const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int wrow = n0 + li;
+  const float* wp = wt + static_cast<int64_t>(wrow < Npad ? wrow : 0) * Kpad;
+  // rows of this wave: POOL -> pixel tiles rt, rt + 4, ... of image blockIdx.y;
+  // else the single tile blockIdx.y * 64 + rt * 16
+  const int ntiles = POOL ? (HW + 15) / 16 : 1;
+  f32x4_t pooled = z;
+  for (int t = POOL ? rt : 0; t < ntiles; t += (POOL ? 4 : 1)) {
+    const int m = POOL ? t * 16 + li : static_cast<int>(blockIdx.y) * 64 + rt * 16 + li;
+    const bool mok = POOL ? m < HW : m < M;
+    const float* xp = x + (POOL ? static_cast<int64_t>(blockIdx.y) * HW : 0) * K + static_cast<int64_t>(mok ? m : 0) * K;
+    // operands in chunks of U k16-steps, the next chunk's loads in flight
+    // during this chunk's MFMAs (one exposed memory latency per kernel, not
+    // one per step); out-of-range steps load nothing and add zeros
+    constexpr int U = 8;
+    f32x4_t c[4] = {z, z, z, z};
+    f32x4_t av[2][U], bv[2][U];
+    auto load = [&](int st0, int buf) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = 16 * (st0 + u) + 4 * g;
+        const bool kok = st0 + u < s1 && k < K;
+        av[buf][u] = (kok && wrow < Npad) ? *reinterpret_cast<const f32x4_t*>(wp + k) : z;
+        bv[buf][u] = (kok && mok) ? *reinterpret_cast<const f32x4_t*>(xp + k) : z;
+      }
+    };
+    auto mma = [&](int buf) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) c[u & 3] = mfma_k16(av[buf][u], bv[buf][u], c[u & 3]);
+    };
+    if (s0 < s1) load(s0, 0);
+    for (int st = s0; st < s1; st += 2 * U) {
+      if (st + U < s1) load(st + U, 1);
+      mma(0);
+      if (st + U >= s1) break;
+      if (st + 2 * U < s1) load(st + 2 * U, 0);
+      mma(1);
+    }
+    f32x4_t acc = (c[0] + c[1]) + (c[2] + c[3]);
+    if (KS > 1) {  // k-slices through LDS, added in slice order by slice 0
+      red[wave][lane] = acc;
+      __syncthreads();
+      if (ks == 0)
+        for (int q = 1; q < KS; ++q) acc += red[q * RT + rt][lane];
+    }
+    if (ks != 0) continue;
+    const int co = n0 + 4 * g;
+    const f32x4_t b4 = co < N ? *reinterpret_cast<const f32x4_t*>(bias + co) : z;
+    f32x4_t v = acc + b4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], act);
+    if constexpr (POOL) {
+      if (!mok) v = z;
+#pragma unroll
+      for (int d = 1; d < 16; d <<= 1)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += __shfl_xor(v[r], d, 64);
+      pooled += v;
+    } else {
+      if (mok && co < N) {
+        if (res) v += *reinterpret_cast<const f32x4_t*>(res + static_cast<int64_t>(m) * N + co);
+        *reinterpret_cast<f32x4_t*>(y + static_cast<int64_t>(m) * N + co) = v;
+      }
+    }
+  }
+  if constexpr (POOL) {
+    __syncthreads();
+    red[wave][lane] = pooled;  // every lane of a 16-lane group holds its group's sum
+    __syncthreads();
+    if (wave == 0 && li == 0) {
+      f32x4_t sum = red[0][lane];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) sum += red[w][lane];
+      const int co = n0 + 4 * g;
+      if (co < N) *reinterpret_cast<f32x4_t*>(y + static_cast<int64_t>(blockIdx.y) * N + co) = sum * (1.f / HW);
+    }
+  }
+}
+
 // --------------------------------------------------------------- dw3x3_f32 ----
 // one lane = one output pixel x 4 channels (float4 loads/stores)
 __global__ void __launch_bounds__(256) dw3x3_f32_kernel(const float* __restrict__ x,     // [B][H][W][C]
@@ -1081,6 +1189,50 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
   // once at creation).  Correct for any placement of the parts over XCDs.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // every wave's slab stores done; the LDS is free
+  const int64_t plane = static_cast<int64_t>(a.B) * a.Ho * a.Wo * a.cout;
+  const __amdgpu_buffer_rsrc_t slab =
+      __builtin_amdgcn_make_buffer_rsrc(a.ws, 0, static_cast<int>(nparts * plane * sizeof(float)), 0x00020000);
+  const int nq = a.cout / 4;
+  // the tile's output quads [v0, v1): all of them (last-arriver form) or this
+  // part's share (spread form), summed over the slabs in part order
+  auto combine = [&](int v0, int v1) {
+    for (int v = v0 + tid; v < v1; v += NT) {
+      const int q = v / nq, co = (v - q * nq) * 4;
+      const int gy = oy0 + q / TX, gx = ox0 + q % TX;
+      if (gy >= a.Ho || gx >= a.Wo) continue;
+      const int64_t e = ((static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx) * a.cout + co;
+      f32x4_t s =
+          __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(slab, static_cast<int>(e * 4), 0, 16));
+      for (int p = 1; p < nparts; ++p)
+        s += __builtin_bit_cast(
+            f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(slab, static_cast<int>((p * plane + e) * 4), 0, 16));
+      s += *reinterpret_cast<const f32x4_t*>(a.bp + co);
+      if (a.residual) s += *reinterpret_cast<const f32x4_t*>(a.x + (e / a.cout) * a.cin + co);
+      *reinterpret_cast<f32x4_t*>(a.y + e) = s;
+    }
+  };
+  if (a.spread) {
+    // spread form: one lane per part bumps the tile's monotone 64-bit arrival
+    // count and waits until every part of this launch has arrived (count >=
+    // the next multiple of nparts); then each part adds its 1/nparts share.
+    // The host launches this form only when the whole grid is resident at
+    // once; the wait is bounded all the same (~0.2 s), so a broken residency
+    // assumption shows up as wrong sums, never as a hung GPU.
+    if (tid == 0) {
+      unsigned long long* ctr = reinterpret_cast<unsigned long long*>(a.tickets) + tile;
+      const unsigned long long t = __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long target = (t / nparts + 1) * nparts;
+      for (int it = 0; it < (1 << 21); ++it) {
+        if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the wait)
+    const int total = TY * TX * nq, chunk = (total + nparts - 1) / nparts;
+    combine(part * chunk, min(total, (part + 1) * chunk));
+    return;
+  }
   int* flag = reinterpret_cast<int*>(smem);
   if (tid == 0) {
     const int t = __hip_atomic_fetch_add(a.tickets + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1091,23 +1243,7 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
   __syncthreads();
   if (!*flag) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the ticket)
-  const int64_t plane = static_cast<int64_t>(a.B) * a.Ho * a.Wo * a.cout;
-  const __amdgpu_buffer_rsrc_t slab =
-      __builtin_amdgcn_make_buffer_rsrc(a.ws, 0, static_cast<int>(nparts * plane * sizeof(float)), 0x00020000);
-  const int nq = a.cout / 4;
-  for (int v = tid; v < TY * TX * nq; v += NT) {
-    const int q = v / nq, co = (v - q * nq) * 4;
-    const int gy = oy0 + q / TX, gx = ox0 + q % TX;
-    if (gy >= a.Ho || gx >= a.Wo) continue;
-    const int64_t e = ((static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx) * a.cout + co;
-    f32x4_t s = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(slab, static_cast<int>(e * 4), 0, 16));
-    for (int p = 1; p < nparts; ++p)
-      s += __builtin_bit_cast(f32x4_t,
-                              __builtin_amdgcn_raw_buffer_load_b128(slab, static_cast<int>((p * plane + e) * 4), 0, 16));
-    s += *reinterpret_cast<const f32x4_t*>(a.bp + co);
-    if (a.residual) s += *reinterpret_cast<const f32x4_t*>(a.x + (e / a.cout) * a.cin + co);
-    *reinterpret_cast<f32x4_t*>(a.y + e) = s;
-  }
+  combine(0, TY * TX * nq);
 }
 
 // --------------------------------------------------------- stem_ir1_f32 ----
@@ -1752,7 +1888,18 @@ static int resolve_tile(int M, int N, int Kpad, int tile) {
   return forced > 0 ? forced : pick_gemm_tile(M, N, Kpad);
 }
 
+// small-M GEMMs (batch-1 projects / head / classifier) run pw_small_f32: one
+// launch instead of a split-K GEMM + reduce (NNSX_F32_SMALLM=0 turns it off)
+static bool use_small_m(int M, int tile, const YLayout& yl) {
+  static const bool on = [] {
+    const char* e = std::getenv("NNSX_F32_SMALLM");
+    return !(e && e[0] == '0');
+  }();
+  return on && tile == 0 && M <= 64 && !yl.rpb && !yl.brpb;
+}
+
 size_t pw_gemm_f32_workspace_bytes(int M, int N, int Kpad, bool has_res, int tile) {
+  if (use_small_m(M, tile, YLayout{})) return 0;
   int splits = 1;
   switch (resolve_tile(M, N, Kpad, tile)) {
     case 64064: splits = gemm_splits<64, 64>(M, N, Kpad, !has_res); break;
@@ -1766,6 +1913,11 @@ size_t pw_gemm_f32_workspace_bytes(int M, int N, int Kpad, bool has_res, int til
 
 void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
                  int Kpad, int Npad, int act, hipStream_t s, int tile, float* ws, const YLayout& yl) {
+  if (use_small_m(M, tile, yl)) {
+    const dim3 grid(static_cast<unsigned>((N + 15) / 16), static_cast<unsigned>((M + 63) / 64));
+    hipLaunchKernelGGL(pw_small_f32_kernel<false>, grid, dim3(256), 0, s, x, wt, bias, res, y, M, N, K, Kpad, Npad, act, 0);
+    return;
+  }
   switch (resolve_tile(M, N, Kpad, tile)) {
     case 64064: pw_gemm_f32_launch<64, 64>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s, yl); break;
     case 128064: pw_gemm_f32_launch<128, 64>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s, yl); break;
@@ -1826,6 +1978,13 @@ void stem3x3_u8_f32(const uint8_t* x, const float* w, const float* bias, float* 
   stem_f32_launch<uint8_t>(x, w, bias, y, B, H, W, act, lut, s);
 }
 
+void pw_pool_f32(const float* x, const float* wt, const float* bias, float* y, int B, int HW, int N, int K, int Kpad,
+                 int Npad, int act, hipStream_t s) {
+  const dim3 grid(static_cast<unsigned>((N + 15) / 16), static_cast<unsigned>(B));
+  hipLaunchKernelGGL(pw_small_f32_kernel<true>, grid, dim3(256), 0, s, x, wt, bias, nullptr, y, B * HW, N, K, Kpad, Npad,
+                     act, HW);
+}
+
 void avgpool_f32(const float* x, float* y, int B, int HW, int C, hipStream_t s) {
   const int groups = (C / 4 + 15) / 16;
   hipLaunchKernelGGL(avgpool_f32_kernel, dim3(static_cast<unsigned>(B * groups)), dim3(256), 0, s, x, y, HW, C);
@@ -1862,6 +2021,17 @@ static bool irw_atomic2() {
   return on;
 }
 
+// NNSX_F32_IRW_INLAUNCH: 0 = irw_reduce launch, 1 = last-arriver combine,
+// 2 = spread combine (default: every part waits for its tile's other parts,
+// then adds a 1/parts share; 64-bit monotone counters: two int32 ticket
+// entries per tile).  Batch 1 at a 500 fps live camera: filter device time
+// 317-319 vs 329-335 us, p50 356-363 vs 368-383 us with the reduce launches
+// (profiles/r3_b1_launch_count_ab.txt); back-to-back replays are unchanged.
+static int irw_inlaunch_mode() {
+  static const int m = irw_env("NNSX_F32_IRW_INLAUNCH", 2);
+  return m;
+}
+
 static int irw_parts(const IrwCfg* c, int tiles, int hid) {
   const int nsub = hid / 16;
   if (c->NOT == 0)  // depthwise output: parts need no reduction, so fill the chip
@@ -1895,6 +2065,20 @@ static bool launch_irw(const IrwCfg* c, IrBlockF32Args a, hipStream_t s) {
     return false;
   if (a.hsplit == 2 && !slabs) (void)hipMemsetAsync(a.y, 0, static_cast<size_t>(plane) * sizeof(float), s);
   if (!a.ws) a.tickets = nullptr;
+  a.spread = 0;
+  if (a.tickets && irw_inlaunch_mode() == 2) {
+    // the spread combine waits inside the launch for the other parts of a
+    // tile: only when every workgroup of the grid is resident at once (one
+    // block per CU under what the occupancy query reports, which can over-report)
+    int dev = 0, ncu = 0, per_cu = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(c->kernel), 64 * c->NW, lds) ==
+            hipSuccess &&
+        static_cast<int64_t>(tiles) * a.hsplit <= static_cast<int64_t>(ncu) * std::max(1, per_cu - 1))
+      a.spread = 1;
+    else
+      a.tickets = nullptr;  // (separate reduce launch)
+  }
   hipLaunchKernelGGL(c->kernel, dim3(static_cast<unsigned>(tiles * a.hsplit)), dim3(64 * c->NW), lds, s, a);
   if (a.ws && !a.tickets) {
     const unsigned grid = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((plane / 4 + 255) / 256, 4096)));
@@ -1939,21 +2123,22 @@ size_t ir_block_f32_workspace_bytes(const IrBlockF32Args& args) {
   return static_cast<size_t>(a.hsplit) * a.B * a.Ho * a.Wo * a.cout * sizeof(float);
 }
 
-// the in-launch combine (irw_f32_kernel's last-part reduction), off unless
-// NNSX_F32_IRW_INLAUNCH=1.  Measured at batch 1 (profiles/r3_b1_inlaunch_combine_trace.txt):
+// the in-launch combine of the hidden parts: the spread form by default
+// (irw_inlaunch_mode); the last-arriver form (NNSX_F32_IRW_INLAUNCH=1) measured at batch 1
+// (profiles/r3_b1_inlaunch_combine_trace.txt):
 // with release/acquire fences and per-block ticket fills, 456 vs 306 us per
 // forward; with write-through slabs, no fences and self-resetting tickets,
 // still 386 us -- the last part of a tile adds all slabs alone (15 slabs x 31 KB
 // on the 7x7 960-hidden block: 50 vs 16 + 5.5 us for the kernel + irw_reduce,
 // whose grid spreads the same adds over many workgroups).
 size_t ir_block_f32_tickets(const IrBlockF32Args& args) {
-  static const bool on = irw_env("NNSX_F32_IRW_INLAUNCH", 0) != 0;
-  if (!on || !ir_block_f32_workspace_bytes(args)) return 0;
+  const int mode = irw_inlaunch_mode();
+  if (!mode || !ir_block_f32_workspace_bytes(args)) return 0;
   IrBlockF32Args a = args;
   const IrwCfg* c = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0, a.dil);
   if (!c || c->NOT == 0) return 0;
   irw_geometry(c, &a);
-  return static_cast<size_t>(a.tiles_x) * a.tiles_y * a.B;
+  return static_cast<size_t>(a.tiles_x) * a.tiles_y * a.B * (mode == 2 ? 2 : 1);
 }
 
 size_t stem_ir1_lds_bytes() {

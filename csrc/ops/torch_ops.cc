@@ -285,6 +285,27 @@ at::Tensor avgpool_cuda(const at::Tensor& x) {
 
 at::Tensor avgpool_cpu(const at::Tensor& x) { return x.to(at::kFloat).mean({1, 2}).to(x.scalar_type()); }
 
+// head 1x1 conv + act + global average pool, one launch (fp32; the small-batch
+// path of the fused MobileNetV2): x [B,H,W,K] -> [B,N]
+at::Tensor pw_conv_pool_cuda(const at::Tensor& x, const at::Tensor& wt, const at::Tensor& bias, int64_t N, int64_t act) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 4,
+              "pw_conv_pool: x [B,H,W,K] f32 contiguous");
+  TORCH_CHECK(wt.scalar_type() == at::kFloat && wt.is_contiguous() && wt.dim() == 2, "pw_conv_pool: wt [Npad,Kpad] f32");
+  TORCH_CHECK(bias.scalar_type() == at::kFloat && bias.numel() >= N, "pw_conv_pool: bias f32 [N]");
+  const int64_t B = x.size(0), HW = x.size(1) * x.size(2), K = x.size(3);
+  const int64_t Kpad = wt.size(1), Npad = wt.size(0);
+  TORCH_CHECK(K % 4 == 0 && N % 4 == 0 && Kpad >= K && Npad >= N, "pw_conv_pool: shape constraints (K%4, N%4)");
+  at::Tensor y = at::empty({B, N}, x.options());
+  nnsx::kernels::pw_pool_f32(x.data_ptr<float>(), wt.data_ptr<float>(), bias.data_ptr<float>(), y.data_ptr<float>(),
+                             static_cast<int>(B), static_cast<int>(HW), static_cast<int>(N), static_cast<int>(K),
+                             static_cast<int>(Kpad), static_cast<int>(Npad), static_cast<int>(act), cur_stream());
+  return y;
+}
+
+at::Tensor pw_conv_pool_cpu(const at::Tensor& x, const at::Tensor& wt, const at::Tensor& bias, int64_t N, int64_t act) {
+  return avgpool_cpu(pw_conv_cpu(x, wt, bias, c10::nullopt, N, act, true));
+}
+
 // ----------------------------------------------------------- ir_block ----
 // Fused inverted residual.  we [hid, cin32], wd [9, hid], wp [ceil16(cout), hid] bf16; biases f32.
 at::Tensor ir_block_f32_cuda(const at::Tensor& x, const at::Tensor& we, const at::Tensor& be, const at::Tensor& wd,
@@ -507,6 +528,7 @@ TORCH_LIBRARY(nnsx, m) {
   m.def("stem_conv(Tensor x, Tensor w, Tensor bias, int act, bool out_f32=False) -> Tensor");
   m.def("stem_conv_u8(Tensor x, Tensor w, Tensor bias, int act, Tensor lut, bool out_f32=False) -> Tensor");
   m.def("avgpool(Tensor x) -> Tensor");
+  m.def("pw_conv_pool(Tensor x, Tensor wt, Tensor bias, int N, int act) -> Tensor");
   m.def("stem_ir1(Tensor x, Tensor ws, Tensor bs, Tensor wd, Tensor bd, Tensor wp, Tensor bp, Tensor lut) -> Tensor");
   m.def("pw_conv_f32_tile(Tensor x, Tensor wt, Tensor bias, Tensor? res, int N, int act, int tile) -> Tensor");
   m.def("ir_block(Tensor x, Tensor we, Tensor be, Tensor wd, Tensor bd, Tensor wp, Tensor bp, int stride, int cout, "
@@ -528,6 +550,7 @@ TORCH_LIBRARY_IMPL(nnsx, CUDA, m) {
   m.impl("stem_conv", stem_conv_cuda);
   m.impl("stem_conv_u8", stem_conv_u8_cuda);
   m.impl("avgpool", avgpool_cuda);
+  m.impl("pw_conv_pool", pw_conv_pool_cuda);
   m.impl("stem_ir1", stem_ir1_cuda);
   m.impl("pw_conv_f32_tile", pw_conv_f32_tile_cuda);
   m.impl("ir_block", ir_block_cuda);
@@ -543,6 +566,7 @@ TORCH_LIBRARY_IMPL(nnsx, CPU, m) {
   m.impl("stem_conv", stem_conv_cpu);
   m.impl("stem_conv_u8", stem_conv_u8_cpu);
   m.impl("avgpool", avgpool_cpu);
+  m.impl("pw_conv_pool", pw_conv_pool_cpu);
   m.impl("stem_ir1", stem_ir1_cpu);
   m.impl("ir_block", ir_block_cpu);
   m.impl("ir_expand_dw", ir_expand_dw_cpu);

@@ -301,8 +301,12 @@ class FusedMobileNetV2(nn.Module):
             if i >= start:
                 h = blk(h)
             i += 1
-        h = self.head(h)
-        h = torch.ops.nnsx.avgpool(h)
+        if self.f32 and h.is_cuda and h.shape[0] <= 8:
+            # small batches: head conv + ReLU6 + global average pool in one launch
+            h = torch.ops.nnsx.pw_conv_pool(h, self.head.wt, self.head.bias, self.head.n, self.head.act)
+        else:
+            h = self.head(h)
+            h = torch.ops.nnsx.avgpool(h)
         return self.fc(h)
 
 

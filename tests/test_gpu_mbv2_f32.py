@@ -176,6 +176,37 @@ def test_ir_block_f32_two_parts_deterministic(nns, H, cin, hid, cout, stride):
     _close(y, _ir_ref64(x, we, be, wd, bd, wp, bp, stride, cout, True, res), tol=5e-5)
 
 
+@pytest.mark.parametrize("H,cin,hid,cout,stride", [(56, 24, 144, 24, 1), (28, 32, 192, 64, 2), (14, 64, 384, 96, 1),
+                                                    (14, 96, 576, 160, 2), (7, 160, 960, 160, 1)])
+@pytest.mark.parametrize("B", [1, 2])
+def test_ir_block_f32_inlaunch_combine(nns, H, cin, hid, cout, stride, B):
+    """Hidden parts combined inside the launch (the model's ticket buffer;
+    NNSX_F32_IRW_INLAUNCH=1 last arriver, =2 every part adds its share after a
+    per-tile arrival count) == the separate ordered reduce launch, bitwise, over
+    repeated launches on one ticket buffer (monotone counters).  Without the
+    env variable both calls take the reduce launch."""
+    torch.manual_seed(cin + hid + B)
+    x = torch.randn(B, H, H, cin, device="cuda")
+    kin = (cin + 7) // 8 * 8
+    we = torch.zeros(hid, kin, device="cuda")
+    we[:, :cin] = torch.randn(hid, cin, device="cuda") / cin ** 0.5
+    be = torch.randn(hid, device="cuda") * 0.1
+    wd = torch.randn(9, hid, device="cuda") / 3
+    bd = torch.randn(hid, device="cuda") * 0.1
+    npad = (cout + 15) // 16 * 16
+    wp = torch.zeros(npad, hid, device="cuda")
+    wp[:cout] = torch.randn(cout, hid, device="cuda") / hid ** 0.5
+    bp = torch.zeros(npad, device="cuda")
+    bp[:cout] = torch.randn(cout, device="cuda") * 0.1
+    res = stride == 1 and cin == cout
+    tickets = torch.zeros(256, dtype=torch.int32, device="cuda")
+    ref = torch.ops.nnsx.ir_block(x, we, be, wd, bd, wp, bp, stride, cout, True, res, 1, None)
+    for _ in range(3):
+        y = torch.ops.nnsx.ir_block(x, we, be, wd, bd, wp, bp, stride, cout, True, res, 1, tickets)
+        assert torch.equal(y, ref)
+    _close(ref, _ir_ref64(x, we, be, wd, bd, wp, bp, stride, cout, True, res), tol=5e-5)
+
+
 @pytest.mark.parametrize("B", [128, 3, 1])
 def test_ir_expand_dw_f32(nns, B):
     """expand + depthwise in one kernel, depthwise output to HBM (the 7x7
@@ -192,6 +223,44 @@ def test_ir_expand_dw_f32(nns, B):
     h = (x.double().cpu() @ we.double().cpu().t() + be.double().cpu()).clamp(0, 6)
     ref = F.conv2d(h.permute(0, 3, 1, 2), wd.double().cpu().view(3, 3, hid).permute(2, 0, 1).unsqueeze(1),
                    bd.double().cpu(), padding=1, groups=hid).clamp(0, 6).permute(0, 2, 3, 1)
+    _close(y, ref, tol=5e-5)
+
+
+@pytest.mark.parametrize("M,K,N,act,use_res", [(1, 1280, 1000, 0, False), (5, 1280, 1000, 0, False),
+                                                (17, 320, 1280, 1, False), (33, 960, 320, 0, True),
+                                                (49, 960, 320, 0, False), (64, 96, 160, 1, True), (49, 36, 24, 0, False)])
+def test_pw_small_m_f32(nns, M, K, N, act, use_res):
+    """small-M GEMM path (one launch, k-slices added through LDS in order) vs fp64, bitwise repeatable"""
+    torch.manual_seed(M * K + N)
+    x = torch.randn(M, K, device="cuda")
+    kpad, npad = (K + 7) // 8 * 8, (N + 15) // 16 * 16
+    wt = torch.zeros(npad, kpad, device="cuda")
+    wt[:N, :K] = torch.randn(N, K, device="cuda") / K ** 0.5
+    bias = torch.zeros(npad, device="cuda")
+    bias[:N] = torch.randn(N, device="cuda") * 0.1
+    res = torch.randn(M, N, device="cuda") if use_res else None
+    y = torch.ops.nnsx.pw_conv(x, wt, bias, res, N, act, True)
+    y2 = torch.ops.nnsx.pw_conv(x, wt, bias, res, N, act, True)
+    assert torch.equal(y, y2)
+    ref = x.double().cpu() @ wt.double().cpu()[:N, :K].t() + bias.double().cpu()[:N]
+    if act == 1:
+        ref = ref.clamp(0, 6)
+    if use_res:
+        ref = ref + res.double().cpu()
+    _close(y, ref, tol=5e-5)
+
+
+@pytest.mark.parametrize("B,H", [(1, 7), (3, 7), (2, 10)])
+def test_pw_conv_pool_f32(nns, B, H):
+    """head 1x1 conv + ReLU6 + global average pool in one launch vs fp64"""
+    torch.manual_seed(B * 100 + H)
+    K, N = 320, 1280
+    x = torch.randn(B, H, H, K, device="cuda")
+    wt = torch.randn(N, K, device="cuda") / K ** 0.5
+    bias = torch.randn(N, device="cuda") * 0.1
+    y = torch.ops.nnsx.pw_conv_pool(x, wt, bias, N, 1)
+    assert y.shape == (B, N)
+    ref = (x.double().cpu() @ wt.double().cpu().t() + bias.double().cpu()).clamp(0, 6).mean((1, 2))
     _close(y, ref, tol=5e-5)
 
 
