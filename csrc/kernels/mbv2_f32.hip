@@ -268,8 +268,9 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce_kernel(const float* __
 }
 
 // ------------------------------------------------------------ pw_small_f32 ----
-// Small-M 1x1 conv / FC (M <= 64 rows per workgroup: batch-1 7x7 projects, the
-// head, the classifier) in ONE launch, no split-K workspace and no reduce
+// Small-M 1x1 conv / FC (M <= 16 rows, or M <= 64 with K <= 512: the
+// small-batch classifier and 1x1-map GEMMs; the head through POOL) in ONE
+// launch, no split-K workspace and no reduce
 // launch: a workgroup = 16 output channels x up to 64 rows, its 4 waves =
 // RT row tiles x KS k-slices (RT * KS = 4: M <= 16 -> one row tile and 4
 // k-slices, <= 32 -> 2 x 2, else 4 x 1).  Each wave runs 4 independent
@@ -1890,16 +1891,21 @@ static int resolve_tile(int M, int N, int Kpad, int tile) {
 
 // small-M GEMMs (batch-1 projects / head / classifier) run pw_small_f32: one
 // launch instead of a split-K GEMM + reduce (NNSX_F32_SMALLM=0 turns it off)
-static bool use_small_m(int M, int tile, const YLayout& yl) {
+static bool use_small_m(int M, int K, int tile, const YLayout& yl) {
   static const bool on = [] {
     const char* e = std::getenv("NNSX_F32_SMALLM");
     return !(e && e[0] == '0');
   }();
-  return on && tile == 0 && M <= 64 && !yl.rpb && !yl.brpb;
+  // (a workgroup streams its rows' whole K range through one CU: at M = 49,
+  // K = 960 -- the batch-1 7x7 project -- that took 16.7 us against 12 us for
+  // the split-K GEMM + reduce, so the many-row deep-K shapes keep split-K;
+  // a two-workgroup K split with order-free atomics needed a memset node
+  // that cost more than it saved: profiles/r3b_b1_forward_trace.txt)
+  return on && tile == 0 && M <= 64 && (M <= 16 || K <= 512) && !yl.rpb && !yl.brpb;
 }
 
 size_t pw_gemm_f32_workspace_bytes(int M, int N, int Kpad, bool has_res, int tile) {
-  if (use_small_m(M, tile, YLayout{})) return 0;
+  if (use_small_m(M, static_cast<int>(Kpad), tile, YLayout{})) return 0;
   int splits = 1;
   switch (resolve_tile(M, N, Kpad, tile)) {
     case 64064: splits = gemm_splits<64, 64>(M, N, Kpad, !has_res); break;
@@ -1913,7 +1919,7 @@ size_t pw_gemm_f32_workspace_bytes(int M, int N, int Kpad, bool has_res, int til
 
 void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
                  int Kpad, int Npad, int act, hipStream_t s, int tile, float* ws, const YLayout& yl) {
-  if (use_small_m(M, tile, yl)) {
+  if (use_small_m(M, Kpad, tile, yl)) {
     const dim3 grid(static_cast<unsigned>((N + 15) / 16), static_cast<unsigned>((M + 63) / 64));
     hipLaunchKernelGGL(pw_small_f32_kernel<false>, grid, dim3(256), 0, s, x, wt, bias, res, y, M, N, K, Kpad, Npad, act, 0);
     return;
