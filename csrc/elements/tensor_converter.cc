@@ -309,16 +309,6 @@ class TensorConverter : public Element {
     old_pts_ = b.pts;
   }
 
-  // NNSX_CONV_KERNEL_UPLOAD=1: single-frame uploads from pinned memory through
-  // the gather kernel instead of a copy-engine hipMemcpyAsync
-  static bool kernel_upload() {
-    static const bool on = [] {
-      const char* e = std::getenv("NNSX_CONV_KERNEL_UPLOAD");
-      return e && e[0] == '1';
-    }();
-    return on;
-  }
-
   // strip row padding (K7) and optionally upload (device path: one 2D H2D copy)
   MemoryPtr video_frame(const MemoryPtr& m, int dev, hipStream_t s) {
     size_t row = static_cast<size_t>(vinfo_.width) * vinfo_.channels;
@@ -328,12 +318,6 @@ class TensorConverter : public Element {
         if (m->on_device()) {
           m->wait_ready(s);
           hip::check(hipMemcpyAsync(out->data(), m->data(), frame_size_, hipMemcpyDeviceToDevice, s), "D2D");
-        } else if (kernel_upload() && m->place() == MemPlace::PINNED && frame_size_ <= (4u << 20)) {
-          // a single pinned frame read over the bus by the gather kernel on the
-          // CUs (no copy-engine start-up on the batch-1 latency path)
-          kernels::GatherArgs g;
-          g.seg[g.n++] = kernels::GatherSeg{m->data(), 0, frame_size_};
-          kernels::gather_copy(g, out->data(), s);
         } else {
           hip::check(hipMemcpyAsync(out->data(), m->data(), frame_size_, hipMemcpyHostToDevice, s), "H2D frame");
         }
