@@ -230,7 +230,8 @@ def test_ir_expand_dw_f32(nns, B):
                                                 (17, 320, 1280, 1, False), (33, 960, 320, 0, True),
                                                 (49, 960, 320, 0, False), (64, 96, 160, 1, True), (49, 36, 24, 0, False)])
 def test_pw_small_m_f32(nns, M, K, N, act, use_res):
-    """small-M GEMM path (one launch, k-slices added through LDS in order) vs fp64, bitwise repeatable"""
+    """small-M GEMMs vs fp64, bitwise repeatable: M <= 16 or K <= 512 take the one-launch path (k-slices
+    added through LDS in order), the deep-K many-row shapes (33 / 49 x 960) the split-K GEMM + reduce"""
     torch.manual_seed(M * K + N)
     x = torch.randn(M, K, device="cuda")
     kpad, npad = (K + 7) // 8 * 8, (N + 15) // 16 * 16
