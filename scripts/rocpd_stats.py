@@ -26,7 +26,7 @@ def main(argv):
           f"{sum(r[1] for r in rows)} dispatches, {total:.1f} us summed")
     print(f"{'total us':>12} {'share':>6} {'calls':>7} {'avg us':>9}  kernel")
     for name, n, tot, avg in rows[:top]:
-        short = name.split("(")[0].replace("nnsx::kernels::(anonymous namespace)::", "")
+        short = name.replace("nnsx::kernels::(anonymous namespace)::", "").replace("void ", "").split("(")[0]
         print(f"{tot:12.1f} {100 * tot / total:5.1f}% {n:7d} {avg:9.1f}  {short[:110]}")
 
 
