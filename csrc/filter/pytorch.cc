@@ -383,6 +383,7 @@ class TorchInstance : public FilterInstance {
     }
 
     std::vector<at::Tensor> outs;
+    std::vector<MemoryPtr> host_outs;        // outputs already copied to pinned host memory
     std::shared_ptr<std::atomic<int>> held;  // static outputs handed out as they are
     bool pooled = dev_idx >= 0 && !in.empty();
     for (auto& m : in) pooled = pooled && m->on_device() && m->root()->tags().count(DeviceBufferPool::kPoolTag);
@@ -404,7 +405,23 @@ class TorchInstance : public FilterInstance {
       // random numbers)
       hip::check(hipGraphLaunch(gs->graph->raw_cuda_graph_exec(), s), "hipGraphLaunch");
       if (copy_out_ || gs->copy_out) {  // private copies of the outputs: the instance is free again
-        for (auto& t : gs->static_out) outs.push_back(t.clone());
+        for (size_t k = 0; k < gs->static_out.size(); ++k) {
+          const at::Tensor& t = gs->static_out[k];
+          if (static_cast<int>(k) == argmax_out_ && host_argmax_ && t.scalar_type() == at::kInt && t.is_contiguous()) {
+            // the absorbed decoder's int32 label indices go straight to pinned host
+            // memory on this stream (the decoder reads them on the host): no device
+            // clone and no second copy by the decoder
+            const size_t bytes = t.numel() * t.element_size();
+            auto hm = Memory::alloc_pinned(bytes);
+            if (bytes) hip::check(hipMemcpyAsync(hm->data(), t.data_ptr(), bytes, hipMemcpyDeviceToHost, s), "argmax D2H");
+            hm->mark_ready(s);
+            host_outs.resize(gs->static_out.size());
+            host_outs[k] = hm;
+            outs.push_back(t);  // (shape and type only)
+          } else {
+            outs.push_back(t.clone());
+          }
+        }
       } else {
         held = gs->out_held;
         held->store(1);
@@ -423,7 +440,12 @@ class TorchInstance : public FilterInstance {
       for (size_t k = 0; k < outs.size(); ++k) ctx.out_info->at(static_cast<unsigned>(k)) = info_from_tensor(outs[k]);
     }
     if (held) held->store(static_cast<int>(outs.size()));  // one count per handed-out tensor
-    for (auto& t : outs) {
+    for (size_t k = 0; k < outs.size(); ++k) {
+      if (k < host_outs.size() && host_outs[k]) {
+        out->push_back(host_outs[k]);
+        continue;
+      }
+      at::Tensor& t = outs[k];
       if (dev_idx < 0 && t.is_cuda()) t = t.cpu();
       out->push_back(wrap_output(t, dev_idx, s, held));
     }
@@ -579,6 +601,13 @@ class TorchInstance : public FilterInstance {
   DType compute_dtype_ = DType::END;
   std::mutex mu_;
   int argmax_out_ = -1;        // output replaced by its argmax (absorbed decoder), -1: none
+  // NNSX_TORCH_HOST_ARGMAX=1: the absorbed argmax's indices are copied to pinned
+  // host memory after each graph replay (default: a device clone, read back by
+  // the decoder)
+  const bool host_argmax_ = [] {
+    const char* e = std::getenv("NNSX_TORCH_HOST_ARGMAX");
+    return e && e[0] == '1';
+  }();
   bool has_lut_ = false;       // the model maps uint8 input 0 through attribute in_lut
   std::vector<float> lut_;     // the absorbed table (re-applied on hot reload)
   std::map<std::string, std::vector<std::unique_ptr<GraphState>>> graphs_;

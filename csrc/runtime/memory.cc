@@ -211,8 +211,15 @@ MemoryPtr Memory::from_bytes(const void* src, size_t size) {
 void Memory::mark_ready(hipStream_t stream) {
   Memory* r = root();
   if (r->place_ == MemPlace::HOST) return;
-  int dev = r->device_ >= 0 ? r->device_ : 0;
+  // pinned host memory has no device of its own: the event belongs to the
+  // producing stream's device (the caller's current device)
+  int dev = r->device_;
+  if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
   std::lock_guard<std::mutex> lk(r->ev_mu_);
+  if (r->ready_ && r->ready_dev_ != dev) {
+    hip::event_put(r->ready_dev_, r->ready_);
+    r->ready_ = nullptr;
+  }
   if (!r->ready_) {
     r->ready_ = hip::event_get(dev);
     r->ready_dev_ = dev;
