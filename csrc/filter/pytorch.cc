@@ -601,12 +601,13 @@ class TorchInstance : public FilterInstance {
   DType compute_dtype_ = DType::END;
   std::mutex mu_;
   int argmax_out_ = -1;        // output replaced by its argmax (absorbed decoder), -1: none
-  // NNSX_TORCH_HOST_ARGMAX=1: the absorbed argmax's indices are copied to pinned
-  // host memory after each graph replay (default: a device clone, read back by
-  // the decoder)
+  // the absorbed argmax's indices are copied to pinned host memory after each
+  // graph replay (NNSX_TORCH_HOST_ARGMAX=0: a device clone, read back by the
+  // decoder).  Batch 1 at a live 500 fps camera: p50 308 vs 362-366 us, filter
+  // device time 287 vs 312-322 us (profiles/r3_b1_host_argmax_ab.txt)
   const bool host_argmax_ = [] {
     const char* e = std::getenv("NNSX_TORCH_HOST_ARGMAX");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   bool has_lut_ = false;       // the model maps uint8 input 0 through attribute in_lut
   std::vector<float> lut_;     // the absorbed table (re-applied on hot reload)
