@@ -169,6 +169,9 @@ class TensorFilter : public BaseTransform, public TransformAbsorber {
   // ---- TransformAbsorber (runtime/fusion.h) ----
   bool absorb_arith(const ArithPrefix& p, const std::string& by) override {
     if (!inst_ || !input_comb_.empty() || p.in_type != DType::UINT8 || p.out_type != DType::FLOAT32) return false;
+    // the table belongs to the model instance: rewriting it for an instance shared
+    // by key would change the input mapping of every other element using it
+    if (shared_) return false;
     if (!inst_->accepts_input_table(p.tensor)) return false;
     std::vector<float> lut;
     if (!arith_table_u8(p.params, p.out_type, &lut)) return false;
@@ -199,6 +202,14 @@ class TensorFilter : public BaseTransform, public TransformAbsorber {
   void detach_absorbable() {
     if (absorbable_up_) absorbable_up_->set_absorber(nullptr);
     absorbable_up_ = nullptr;
+    if (!absorbed_from_.empty()) {
+      // undo the absorption: the model's own input table and model-reported
+      // input info again, so a restart with another upstream negotiates afresh
+      if (inst_ && !inst_->reset_input_table(0))
+        NNSX_LOGW(name(), "could not restore the model's input table after releasing ", absorbed_from_);
+      absorbed_from_.clear();
+      if (inst_) load_model_info();
+    }
   }
 
   ~TensorFilter() override {

@@ -94,6 +94,11 @@ class TorchInstance : public FilterInstance {
   }
   ~TorchInstance() override {
     clear_graphs();
+    if (last_replay_ev_) {
+      hip::DeviceGuard g(last_replay_dev_);
+      (void)hipEventSynchronize(last_replay_ev_);
+      (void)hipEventDestroy(last_replay_ev_);
+    }
     if (cap_stream_) {
       hip::DeviceGuard g(device_);
       (void)hipStreamSynchronize(cap_stream_);
@@ -124,6 +129,23 @@ class TorchInstance : public FilterInstance {
     }
     lut_ = lut;
     if (props_.input_info.num_tensors > 0) props_.input_info.at(0).type = DType::UINT8;
+    clear_graphs();
+    return true;
+  }
+
+  // the absorbing element released the transform (stop, re-link): back to the
+  // table the model file shipped with
+  bool reset_input_table(unsigned index) override {
+    if (index != 0 || !has_lut_) return false;
+    std::lock_guard<std::mutex> lk(mu_);
+    if (lut_.empty()) return true;
+    try {
+      apply_lut(module_, default_lut_);
+    } catch (const std::exception& e) {
+      NNSX_LOGE("pytorch", "reset_input_table failed: ", e.what());
+      return false;
+    }
+    lut_.clear();
     clear_graphs();
     return true;
   }
@@ -242,6 +264,10 @@ class TorchInstance : public FilterInstance {
     if (m.hasattr("in_lut")) {
       const c10::IValue v = m.attr("in_lut");
       has_lut_ = v.isTensor() && v.toTensor().scalar_type() == torch::kFloat && v.toTensor().numel() == 256;
+      if (has_lut_ && default_lut_.empty()) {
+        at::Tensor t = v.toTensor().detach().to(torch::kCPU).contiguous();
+        default_lut_.assign(t.data_ptr<float>(), t.data_ptr<float>() + 256);
+      }
     }
     try {
       if (has_lut_)
@@ -403,6 +429,13 @@ class TorchInstance : public FilterInstance {
       // the captured executable on the element's stream (CUDAGraph::replay would
       // first refresh RNG offsets with two fill kernels: the models here draw no
       // random numbers)
+      // every graph of this instance shares one memory pool (capture) and a
+      // copy-out instance is handed back at once: replays must not overlap, nor
+      // a replay the previous one's copy-out.  Elements sharing the instance
+      // (shared-tensor-filter-key) each bring their own stream, so a replay on a
+      // new stream first waits for the last one
+      if (last_replay_ev_ && last_replay_stream_ != s)
+        hip::check(hipStreamWaitEvent(s, last_replay_ev_, 0), "replay order wait");
       hip::check(hipGraphLaunch(gs->graph->raw_cuda_graph_exec(), s), "hipGraphLaunch");
       if (copy_out_ || gs->copy_out) {  // private copies of the outputs: the instance is free again
         for (size_t k = 0; k < gs->static_out.size(); ++k) {
@@ -427,6 +460,12 @@ class TorchInstance : public FilterInstance {
         held->store(1);
         outs = gs->static_out;
       }
+      if (!last_replay_ev_) {
+        last_replay_dev_ = dev_idx;
+        hip::check(hipEventCreateWithFlags(&last_replay_ev_, hipEventDisableTiming), "replay event");
+      }
+      hip::check(hipEventRecord(last_replay_ev_, s), "replay event record");
+      last_replay_stream_ = s;
     } else {
       std::vector<c10::IValue> iv;
       for (auto& t : inputs) iv.push_back(prepare(t));
@@ -561,7 +600,11 @@ class TorchInstance : public FilterInstance {
       }
       hip::check(hipStreamSynchronize(cap_stream_), "graph warmup sync");
       gs->graph = std::make_unique<at::cuda::CUDAGraph>();
-      gs->graph->capture_begin({0, 0}, hipStreamCaptureModeThreadLocal);
+      // one memory pool for every graph of the instance: replays never overlap
+      // (replay order, do_invoke), so the activations of one instance's forward
+      // are allocated once, not once per pooled input block and output buffer
+      if (graph_pool_.first == 0 && graph_pool_.second == 0) graph_pool_ = at::cuda::graph_pool_handle();
+      gs->graph->capture_begin(graph_pool_, hipStreamCaptureModeThreadLocal);
       iv.clear();
       for (auto& t : src) iv.push_back(prepare(t));
       flatten(module_.forward(iv), &gs->static_out);
@@ -611,15 +654,21 @@ class TorchInstance : public FilterInstance {
   }();
   bool has_lut_ = false;       // the model maps uint8 input 0 through attribute in_lut
   std::vector<float> lut_;     // the absorbed table (re-applied on hot reload)
+  std::vector<float> default_lut_;  // the table of the loaded model file (reset_input_table)
   std::map<std::string, std::vector<std::unique_ptr<GraphState>>> graphs_;
   std::map<std::string, size_t> in_place_count_;  // in-place instances per input shape
   std::set<std::string> warmed_;                   // input shapes run eagerly before a capture
   void clear_graphs() {
     graphs_.clear();
+    graph_pool_ = {0, 0};  // the pool goes with its last graph
     in_place_count_.clear();
     warmed_.clear();  // a reloaded module runs eagerly again before its first capture
   }
   size_t graphs_captured_ = 0;
+  at::cuda::MempoolId_t graph_pool_{0, 0};  // shared by every captured graph (capture)
+  hipEvent_t last_replay_ev_ = nullptr;     // end of the latest replay (+ copy-out)
+  hipStream_t last_replay_stream_ = nullptr;
+  int last_replay_dev_ = 0;
   hipStream_t cap_stream_ = nullptr;  // private capture stream (graph_for)
 };
 

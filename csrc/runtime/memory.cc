@@ -26,7 +26,10 @@ MemoryPtr Memory::alloc_pinned(size_t size) {
   if (!hip::available()) return alloc_host(size);
   void* p = hip::pinned_alloc(size);
   return std::make_shared<Memory>(p, size, MemPlace::PINNED, -1, [](Memory* m) {
-    // a pending H2D may still read this block: wait for recorded readers
+    // a pending D2H may still be landing in this block (its producer's ready
+    // event), and a pending H2D may still read it (recorded readers): the block
+    // goes back to the shared pinned pool only after both
+    m->sync_ready();
     m->sync_uses();
     hip::pinned_free(m->data(), m->size());
   });

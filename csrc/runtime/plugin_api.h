@@ -95,6 +95,11 @@ class FilterInstance {
     (void)lut;
     return false;
   }
+  // Undo set_input_table: the model's own table again (absorption released)
+  virtual bool reset_input_table(unsigned index) {
+    (void)index;
+    return false;
+  }
   // Downstream-argmax absorption (runtime/fusion.h): true when the framework
   // can end its device work with an argmax over the innermost dimension of
   // output `index`, producing int32 indices (that dimension becomes 1)
