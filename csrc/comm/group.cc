@@ -442,6 +442,14 @@ std::shared_ptr<void> host_store(const std::string& host, int port, bool* in_use
 // ================================================================= group ====
 Group::~Group() {
   mesh_.reset();  // goodbyes first: peers see an orderly end of our links
+  for (auto* links : {&tx_, &rx_})
+    for (auto& l : *links) {
+      if (!l.comm) continue;
+      hip::DeviceGuard g(device_);
+      if (l.stream) (void)hipStreamSynchronize(l.stream);
+      ncclCommDestroy(static_cast<ncclComm_t>(l.comm));
+      if (l.stream) hip::stream_destroy(device_, l.stream);
+    }
   if (comm_) {
     hip::DeviceGuard g(device_);
     if (stream_) (void)hipStreamSynchronize(stream_);
@@ -526,6 +534,8 @@ bool Group::init(const GroupSpec& in, std::string* err) {
       return false;
     }
   }
+  tx_.assign(static_cast<size_t>(n), Link{});
+  rx_.assign(static_cast<size_t>(n), Link{});
   // ---- member-to-member links (headers; payloads too on the tcp backend) ----
   if (n > 1) {
     mesh_ = std::make_unique<Mesh>();
@@ -654,13 +664,15 @@ bool Group::decode(const std::string& s, Packet* p, bool inline_payload, std::ve
   return r.ok;
 }
 
-void* Group::dev_ptr(const MemoryPtr& m) {
+void* Group::dev_ptr(const MemoryPtr& m) { return dev_ptr_on(m, stream_); }
+
+void* Group::dev_ptr_on(const MemoryPtr& m, hipStream_t s) {
   if (m->on_device() && m->device() == device_) {
-    m->wait_ready(stream_);
+    m->wait_ready(s);
     return m->data();
   }
   // host blob (or another GPU's): stage it onto ours, ordered on the comm stream
-  return const_cast<void*>(m->map_device(device_, stream_));
+  return const_cast<void*>(m->map_device(device_, s));
 }
 
 std::vector<MemoryPtr> Group::alloc_recv(const std::vector<size_t>& sizes, const std::vector<std::string>& metas) {
@@ -677,9 +689,81 @@ std::vector<MemoryPtr> Group::alloc_recv(const std::vector<size_t>& sizes, const
   return out;
 }
 
-void Group::finish_inputs(const std::vector<MemoryPtr>& in) {
+void Group::finish_inputs(const std::vector<MemoryPtr>& in, hipStream_t s) {
   for (auto& m : in)
-    if (m->size()) m->record_use(stream_, device_);
+    if (m->size()) m->record_use(s ? s : stream_, device_);
+}
+
+// Per-direction pair communicator, created at the pair's first message.  The
+// sender publishes a unique id and waits (bounded, cancellable: the store) until
+// the receiver -- which learns of the pair from that first message's header --
+// has fetched it; only then do both enter the blocking ncclCommInitRank, so a
+// receiver that never reads the header costs the sender a timeout, not a hang.
+bool Group::link(int peer, bool tx, Link** out, std::string* err) {
+  Link& l = (tx ? tx_ : rx_).at(static_cast<size_t>(peer));
+  *out = &l;
+  if (l.comm) return true;
+  const int src = tx ? grank_ : peer, dst = tx ? peer : grank_;
+  const std::string k = strfmt("p2p/", src, ">", dst);
+  ncclUniqueId id;
+  if (tx) {
+    if (!nccl_ok(ncclGetUniqueId(&id), "ncclGetUniqueId", err)) return false;
+    std::string v;
+    if (!put(k + "/id", std::string(reinterpret_cast<const char*>(&id), sizeof(id)), 1) ||
+        !get(k + "/joined", &v, spec_.timeout_ms)) {
+      if (err) *err = strfmt("p2p link to member ", peer, ": the receiver did not join");
+      return false;
+    }
+  } else {
+    std::string v;
+    if (!get(k + "/id", &v, spec_.timeout_ms) || v.size() != sizeof(id)) {
+      if (err) *err = strfmt("p2p link from member ", peer, ": no RCCL unique id");
+      return false;
+    }
+    std::memcpy(&id, v.data(), sizeof(id));
+    if (!put(k + "/joined", "1", 1)) {
+      if (err) *err = "p2p link: store lost";
+      return false;
+    }
+  }
+  hip::DeviceGuard dg(device_);
+  int lo = 0, hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+  ncclComm_t c = nullptr;
+  if (!nccl_ok(ncclCommInitRank(&c, 2, id, tx ? 0 : 1), "ncclCommInitRank(p2p)", err)) return false;
+  l.stream = hip::stream_create(device_, hi);
+  l.comm = c;
+  NNSX_LOGD("comm", "group ", spec_.name, ": p2p link ", src, " -> ", dst, " up");
+  return true;
+}
+
+bool Group::self_copy(const std::vector<MemoryPtr>& in, std::vector<MemoryPtr>* out, std::string* err) {
+  hip::DeviceGuard dg(device_);
+  auto comm = static_cast<ncclComm_t>(comm_);
+  out->clear();
+  std::vector<void*> src;
+  for (auto& b : in) {
+    src.push_back(b->size() ? dev_ptr(b) : nullptr);
+    auto m = b->size() ? Memory::alloc_device(b->size(), device_, stream_) : Memory::alloc_host(0);
+    if (b->has_meta()) m->set_meta(b->meta());
+    out->push_back(m);
+  }
+  if (!nccl_ok(ncclGroupStart(), "ncclGroupStart", err)) return false;
+  for (size_t i = 0; i < in.size(); ++i) {
+    if (!in[i]->size()) continue;
+    if (!nccl_ok(ncclSend(src[i], in[i]->size(), ncclUint8, grank_, comm, stream_), "ncclSend", err) ||
+        !nccl_ok(ncclRecv((*out)[i]->data(), in[i]->size(), ncclUint8, grank_, comm, stream_), "ncclRecv", err)) {
+      ncclGroupEnd();
+      return false;
+    }
+    bytes_sent_ += in[i]->size();
+    bytes_recv_ += in[i]->size();
+  }
+  if (!nccl_ok(ncclGroupEnd(), "ncclGroupEnd", err)) return false;
+  for (auto& m : *out)
+    if (m->size()) m->mark_ready(stream_);
+  finish_inputs(in);
+  return true;
 }
 
 // ------------------------------------------------------------ messages ----
@@ -731,7 +815,9 @@ bool Group::allgather(const Packet& mine, std::vector<Packet>* all, std::string*
   (*all)[grank_] = mine;
   (*all)[grank_].src = grank_;
   if (stacked) *stacked = nullptr;
-  if (n == 1) {
+  // a group of one: nothing to exchange -- unless RCCL was forced, then the
+  // real ncclAllGather runs (one rank: a copy into the gathered buffer)
+  if (n == 1 && !rccl()) {
     if (stacked && mine.blobs.size() == 1) *stacked = mine.blobs[0];
     return true;
   }
@@ -786,6 +872,7 @@ bool Group::allgather(const Packet& mine, std::vector<Packet>* all, std::string*
         ncclGroupEnd();
         return false;
       }
+      if (n == 1) (*all)[grank_].blobs[j] = out;  // (forced RCCL: the gathered copy)
       for (int r = 0; r < n; ++r) {
         if (r == grank_) continue;
         auto v = Memory::view(out, static_cast<size_t>(r) * s, s);
@@ -833,7 +920,7 @@ bool Group::allgather(const Packet& mine, std::vector<Packet>* all, std::string*
 bool Group::broadcast(int root, Packet* pkt, std::string* err) {
   const int n = size();
   const uint64_t seq = seq_++;
-  if (n == 1) return true;
+  if (n == 1 && !rccl()) return true;  // (forced RCCL: the one-rank ncclBroadcast runs)
   const uint64_t tag = 1 + seq;
   std::vector<size_t> sizes;
   std::vector<std::string> metas;
@@ -938,6 +1025,9 @@ bool Group::send(int peer, const Packet& p, std::string* err) {
     m.caps = encode(p, false);
     m.blobs = p.blobs;
     m.flags = 1;  // in-process: blobs handed over as they are
+    // a group of one on forced RCCL: the payload goes through RCCL's p2p path
+    // (grouped ncclSend / ncclRecv to itself) like a peer's would
+    if (size() == 1 && rccl() && !self_copy(p.blobs, &m.blobs, err)) return false;
     if (!mesh_) {
       std::lock_guard<std::mutex> lk(local_mu_);
       local_.push_back(std::move(m));
@@ -950,18 +1040,23 @@ bool Group::send(int peer, const Packet& p, std::string* err) {
   if (!mesh_->send(peer, kTagP2P, to_message(p), err)) return false;
   if (!rccl()) return true;
   hip::DeviceGuard dg(device_);
-  auto comm = static_cast<ncclComm_t>(comm_);
+  Link* l = nullptr;
+  if (!link(peer, true, &l, err)) return false;
+  auto comm = static_cast<ncclComm_t>(l->comm);
+  std::vector<void*> src;
+  for (auto& b : p.blobs) src.push_back(b->size() ? dev_ptr_on(b, l->stream) : nullptr);
   if (!nccl_ok(ncclGroupStart(), "ncclGroupStart", err)) return false;
-  for (auto& b : p.blobs) {
-    if (!b->size()) continue;
-    if (!nccl_ok(ncclSend(dev_ptr(b), b->size(), ncclUint8, peer, comm, stream_), "ncclSend", err)) {
+  for (size_t i = 0; i < p.blobs.size(); ++i) {
+    const size_t sz = p.blobs[i]->size();
+    if (!sz) continue;
+    if (!nccl_ok(ncclSend(src[i], sz, ncclUint8, 1, comm, l->stream), "ncclSend", err)) {
       ncclGroupEnd();
       return false;
     }
-    bytes_sent_ += b->size();
+    bytes_sent_ += sz;
   }
   if (!nccl_ok(ncclGroupEnd(), "ncclGroupEnd", err)) return false;
-  finish_inputs(p.blobs);
+  finish_inputs(p.blobs, l->stream);
   return true;
 }
 
@@ -1007,17 +1102,28 @@ bool Group::recv(Packet* p, int timeout_ms, bool* timed_out, std::string* err) {
   }
   if (!rccl()) return true;
   hip::DeviceGuard dg(device_);
-  p->blobs = alloc_recv(sizes, metas);
-  auto comm = static_cast<ncclComm_t>(comm_);
+  Link* l = nullptr;
+  if (!link(p->src, false, &l, err)) return false;
+  auto comm = static_cast<ncclComm_t>(l->comm);
+  p->blobs.clear();
+  for (size_t i = 0; i < sizes.size(); ++i) {
+    auto m = sizes[i] ? Memory::alloc_device(sizes[i], device_, l->stream) : Memory::alloc_host(0);
+    if (!metas[i].empty()) {
+      MetaInfo mi;
+      if (MetaInfo::parse(metas[i].data(), metas[i].size(), &mi)) m->set_meta(mi);
+    }
+    bytes_recv_ += sizes[i];
+    p->blobs.push_back(m);
+  }
   if (!nccl_ok(ncclGroupStart(), "ncclGroupStart", err)) return false;
   for (auto& b : p->blobs)
-    if (b->size() && !nccl_ok(ncclRecv(b->data(), b->size(), ncclUint8, p->src, comm, stream_), "ncclRecv", err)) {
+    if (b->size() && !nccl_ok(ncclRecv(b->data(), b->size(), ncclUint8, 0, comm, l->stream), "ncclRecv", err)) {
       ncclGroupEnd();
       return false;
     }
   if (!nccl_ok(ncclGroupEnd(), "ncclGroupEnd", err)) return false;
   for (auto& b : p->blobs)
-    if (b->size()) b->mark_ready(stream_);
+    if (b->size()) b->mark_ready(l->stream);
   return true;
 }
 

@@ -28,9 +28,19 @@
 // behind its header (host bytes), so the same elements and tests run on
 // CPU-only boxes.
 //
-// Threading rule: a Group is driven by one thread at a time (RCCL
-// communicators are not thread-safe); elements that talk in both
-// directions open one group per direction.
+// Point-to-point payloads ride on per-direction links: for each ordered pair
+// (sender -> receiver) a two-rank RCCL communicator with its own stream on
+// both sides, created at the pair's first message.  A send kernel then waits
+// only for receives of the SAME direction, which its own earlier sends
+// already matched, so no cycle of GPU waits can form -- a ring or a
+// bidirectional exchange of frame-sized messages cannot deadlock the way one
+// shared comm stream does (each rank's send kernel queued ahead of the
+// receive its peer's send waits for).  Collectives keep the group
+// communicator and stream.
+//
+// Threading rule: collectives are driven by one thread at a time (RCCL
+// communicators are not thread-safe); send() and recv() use disjoint links
+// and may run on two threads (one sender, one receiver).
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -198,7 +208,18 @@ class Group {
   bool from_message(Message&& m, Packet* p, std::vector<size_t>* sizes, std::vector<std::string>* metas);
   bool recv_from(uint64_t tag, int src, Packet* p, std::vector<size_t>* sizes, std::vector<std::string>* metas,
                  std::string* err, const char* what);
-  void finish_inputs(const std::vector<MemoryPtr>& in);
+  void finish_inputs(const std::vector<MemoryPtr>& in, hipStream_t s = nullptr);
+  void* dev_ptr_on(const MemoryPtr& m, hipStream_t s);
+  // per-direction p2p links (see the header comment): the link carrying this
+  // member's messages to `peer` (tx) or `peer`'s messages to this member (rx)
+  struct Link {
+    void* comm = nullptr;  // ncclComm_t of the two-rank pair (sender = rank 0)
+    hipStream_t stream = nullptr;
+  };
+  bool link(int peer, bool tx, Link** out, std::string* err);
+  // a group of one on forced RCCL: the blobs copied through a grouped
+  // ncclSend / ncclRecv to itself (the data plane's p2p kernels, on one GPU)
+  bool self_copy(const std::vector<MemoryPtr>& in, std::vector<MemoryPtr>* out, std::string* err);
 
   GroupSpec spec_;
   std::vector<int> members_;
@@ -210,6 +231,7 @@ class Group {
   std::unique_ptr<Mesh> mesh_;  // member-to-member links (headers; tcp payloads)
   void* comm_ = nullptr;  // ncclComm_t
   hipStream_t stream_ = nullptr;
+  std::vector<Link> tx_, rx_;  // per peer (group rank): send side / receive side
   uint64_t seq_ = 0;            // collective sequence
   std::deque<Message> local_;   // a group of one: its messages to itself
   std::mutex local_mu_;

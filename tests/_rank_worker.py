@@ -3,9 +3,20 @@ uniform and ragged all-gather, broadcast, scatter and a send/recv ring.
 Run as a child process per rank (tests/test_rank_collectives.py on CPU with the
 tcp backend, tests/test_gpu_rccl_ranks.py with one GPU per rank over RCCL).
 
-    python tests/_rank_worker.py RANK WORLD STORE_PORT DEVICE BACKEND
+    python tests/_rank_worker.py RANK WORLD STORE_PORT DEVICE BACKEND [big]
 
-Prints one JSON line with what it received and the group's byte counters."""
+Prints one JSON line with what it received and the group's byte counters.
+
+`big`: frame-sized payloads instead (the real pipelines move 0.8-77 MB per
+message): a 64 MB uniform all-gather, a ragged all-gather of 3-70 MB blobs
+(odd sizes), a 64 MB broadcast and scatter, a send-first ring of 48 MB
+messages and an all-to-all exchange of 32 MB messages in which every member
+sends to every other member before receiving anything.  On one shared RCCL
+comm stream the ring and the exchange are the classic cross-rank hang (each
+send kernel queued ahead of the receive its peer waits for); comm::Group
+carries p2p on per-direction links (comm/group.h).  Each received payload is
+checked element by element against the sender's pattern (value = sender
+rank * 1000 + index % 997), only a digest goes into the JSON."""
 import json
 import os
 import sys
@@ -13,9 +24,68 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def pattern(src, n, tag=0):
+    import numpy as np
+
+    return (np.float32(src * 1000 + tag * 100) + (np.arange(n, dtype=np.int64) % 997).astype(np.float32))
+
+
+def big(g, rank, world, arr, res):
+    import numpy as np
+
+    MB = 1 << 20
+
+    def ok(m, src, n, tag=0):
+        a = m.numpy("float32")
+        return bool(a.size == n and np.array_equal(a, pattern(src, n, tag)))
+
+    n64 = 64 * MB // 4
+    all_, stacked = g.allgather(nns_packet([arr(pattern(rank, n64))]))
+    res["big_ag"] = [ok(p.blobs[0], k, n64) for k, p in enumerate(all_)]
+    if stacked is not None:
+        st = stacked.numpy("float32")
+        res["big_ag_stacked"] = all(np.array_equal(st[k * n64:(k + 1) * n64], pattern(k, n64)) for k in range(world))
+    # ragged: 3 MB .. 70 MB, sizes not a multiple of 1 KB
+    sizes = [(3 * MB + (67 * MB * k) // max(1, world - 1)) // 4 - 3 * k - 1 for k in range(world)]
+    all_, _ = g.allgather(nns_packet([arr(pattern(rank, sizes[rank], 1))]))
+    res["big_ag_ragged"] = [ok(p.blobs[0], k, sizes[k], 1) for k, p in enumerate(all_)]
+    root = world - 1
+    got = g.broadcast(root, nns_packet([arr(pattern(root, n64, 2))]) if rank == root else nns_packet())
+    res["big_bcast"] = ok(got.blobs[0], root, n64, 2)
+    parts = [nns_packet([arr(pattern(r, n64, 3))]) for r in range(world)] if rank == 0 else []
+    mine = g.scatter(0, parts)
+    res["big_scatter"] = ok(mine.blobs[0], rank, n64, 3)
+    if world > 1:
+        n48 = 48 * MB // 4
+        nxt = (rank + 1) % world
+        for k in range(2):
+            g.send(nxt, nns_packet([arr(pattern(rank, n48, 4 + k))], pts=k))
+        ring = []
+        for _ in range(2):
+            p = g.recv(120000)
+            ring.append([p.src, p.pts, ok(p.blobs[0], p.src, n48, 4 + p.pts)])
+        res["big_ring"] = ring
+        n32 = 32 * MB // 4
+        for peer in range(world):
+            if peer != rank:
+                g.send(peer, nns_packet([arr(pattern(rank, n32, 6))], pts=peer))
+        seen = []
+        for _ in range(world - 1):
+            p = g.recv(120000)
+            seen.append([p.src, p.pts == rank and ok(p.blobs[0], p.src, n32, 6)])
+        res["big_exchange"] = sorted(seen)
+
+
+def nns_packet(blobs=(), pts=-1):
+    import nnstreamer_amd as nns
+
+    return nns.Packet(list(blobs), pts=pts)
+
+
 def main():
     rank, world, port, dev, backend = (int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]),
                                        sys.argv[5])
+    mode = sys.argv[6] if len(sys.argv) > 6 else "small"
     import numpy as np
 
     import nnstreamer_amd as nns
@@ -33,6 +103,12 @@ def main():
 
     g = nns.Group("test/collectives", rank, world, f"127.0.0.1:{port}", dev, backend, 60000)
     res = {"rank": rank, "backend": g.backend, "size": g.size}
+    if mode == "big":
+        big(g, rank, world, arr, res)
+        res["bytes_sent"] = g.bytes_sent
+        res["bytes_received"] = g.bytes_received
+        print(json.dumps(res), flush=True)
+        return
 
     def vals(m):
         return m.numpy("float32").tolist()

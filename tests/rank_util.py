@@ -18,11 +18,11 @@ def free_port():
     return p
 
 
-def run_ranks(world, devices, backend, timeout=240):
+def run_ranks(world, devices, backend, timeout=240, mode="small"):
     port = free_port()
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "_rank_worker.py"), str(r), str(world),
-                               str(port), str(devices[r]), backend], stdout=subprocess.PIPE,
+                               str(port), str(devices[r]), backend, mode], stdout=subprocess.PIPE,
                               stderr=subprocess.STDOUT, text=True, env=env) for r in range(world)]
     outs = []
     try:
@@ -54,3 +54,18 @@ def check(res, world, backend):
             prv = (r - 1) % world
             assert x["ring"] == [[prv, 0, prv * 10.0], [prv, 1, prv * 10.0 + 1]], x["ring"]
             assert x["bytes_sent"] > 0 and x["bytes_received"] > 0, x
+
+
+def check_big(res, world, backend):
+    """Frame-sized payloads (_rank_worker.py big): every element of every
+    received payload equals its sender's pattern."""
+    for r, x in enumerate(res):
+        assert x["rank"] == r and x["size"] == world and x["backend"] == backend, x
+        assert x["big_ag"] == [True] * world, x
+        assert x.get("big_ag_stacked", True), x
+        assert x["big_ag_ragged"] == [True] * world, x
+        assert x["big_bcast"] and x["big_scatter"], x
+        if world > 1:
+            prv = (r - 1) % world
+            assert x["big_ring"] == [[prv, 0, True], [prv, 1, True]], x["big_ring"]
+            assert x["big_exchange"] == [[k, True] for k in range(world) if k != r], x["big_exchange"]

@@ -148,3 +148,38 @@ def test_allgather_rccl_single_member(nns):
     for (on_dev, y), x in zip(out, frames):
         assert on_dev
         np.testing.assert_array_equal(y, 2 * x)
+
+
+def _port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.parametrize("mb", [1, 64])
+def test_group_of_one_forced_rccl_runs_every_call(nns, mb):
+    """backend=rccl on a group of one runs the real RCCL calls on one GPU: the
+    one-rank ncclAllGather (a copy into the gathered buffer), ncclBroadcast and
+    a grouped ncclSend/ncclRecv to itself for p2p (comm/group.cc self_copy) --
+    the received blobs are fresh device buffers holding the sent bytes."""
+    n = mb * (1 << 20) // 4
+    g = nns.Group(f"test/one-{mb}", 0, 1, f"127.0.0.1:{_port()}", 0, "rccl", 60000)
+    assert g.backend == "rccl" and g.size == 1
+    x = torch.arange(n, dtype=torch.float32, device="cuda") % 997 + 1
+    all_, stacked = g.allgather(nns.Packet([x], pts=5))
+    assert len(all_) == 1 and all_[0].blobs[0].on_device
+    assert all_[0].blobs[0].data_ptr != x.data_ptr()  # the gathered copy, not the input
+    assert np.array_equal(all_[0].blobs[0].numpy("float32"), x.cpu().numpy())
+    assert stacked is not None and np.array_equal(stacked.numpy("float32"), x.cpu().numpy())
+    got = g.broadcast(0, nns.Packet([x], pts=6))
+    assert np.array_equal(got.blobs[0].numpy("float32"), x.cpu().numpy())
+    g.send(0, nns.Packet([x, x[: n // 3]], pts=7))
+    p = g.recv(60000)
+    assert p is not None and p.pts == 7 and len(p.blobs) == 2
+    assert all(b.on_device for b in p.blobs) and p.blobs[0].data_ptr != x.data_ptr()
+    assert np.array_equal(p.blobs[0].numpy("float32"), x.cpu().numpy())
+    assert np.array_equal(p.blobs[1].numpy("float32"), x[: n // 3].cpu().numpy())
+    assert g.bytes_sent >= 4 * (n + n // 3) and g.bytes_received >= 4 * (n + n // 3)

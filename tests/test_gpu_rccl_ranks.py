@@ -12,7 +12,7 @@ import sys
 
 import pytest
 
-from rank_util import ROOT, check, run_ranks
+from rank_util import ROOT, check, check_big, run_ranks
 
 pytestmark = pytest.mark.gpu
 
@@ -33,6 +33,17 @@ def test_group_collectives_rccl():
     check(res, world, "rccl")
     for x in res:  # payloads stayed in HBM: received blobs are device memories
         assert all(x["ag_on_device"]), x
+
+
+@needs2
+def test_group_collectives_rccl_frame_sized():
+    """Frame-sized payloads over RCCL between GPUs (_rank_worker.py big): 64 MB
+    and 3-70 MB ragged all-gathers, 64 MB broadcast / scatter, a send-first ring
+    of 48 MB messages and an all-to-all 32 MB exchange -- the patterns that hang
+    when every rank's sends and receives share one comm stream."""
+    world = min(_ngpu(), 8)
+    res = run_ranks(world, list(range(world)), "rccl", timeout=300, mode="big")
+    check_big(res, world, "rccl")
 
 
 @needs2
