@@ -404,6 +404,7 @@ class TensorConverter : public Element {
         if (p.off == p.size()) adapter_.pop_front();
       }
     }
+    if (dev >= 0 && done < size && padded_dma(size, dev, s, out)) done = size;
     if (dev >= 0 && done < size && gather_eligible(size)) {
       // one gather launch per <=128 pieces instead of one hipMemcpyAsync per frame
       kernels::GatherArgs g;
@@ -451,6 +452,58 @@ class TensorConverter : public Element {
     if (dev >= 0) out->mark_ready(s);
     avail_ -= size;
     return out;
+  }
+
+  // Padded video frames (row stride > W*C, e.g. 513x513 RGB: 1539-byte rows 1540
+  // apart; reference: gsttensor_converter.c:1062-1107) in pinned host memory:
+  // the padded bytes go to HBM on the copy engine as they are -- one DMA for a
+  // ring of equally spaced frames, else one per frame -- and one unpad_rows
+  // launch packs the rows device-side.  (The bus-reading gather kernel moved
+  // them at ~5 GB/s with 1-byte stores on a few workgroups:
+  // profiles/r3_config_trace_deeplab_b8.txt.)  Every piece must be a whole
+  // padded pinned frame of one geometry.
+  bool padded_dma(size_t size, int dev, hipStream_t s, const MemoryPtr& out) {
+    static const bool on = [] {
+      const char* e = std::getenv("NNSX_CONVERTER_PADDED_DMA");
+      return !(e && e[0] == '0');
+    }();
+    if (!on) return false;
+    std::vector<Piece*> ps;
+    size_t seen = 0;
+    for (Piece& p : adapter_) {
+      if (!p.padded() || p.off != 0 || p.mem->place() != MemPlace::PINNED) return false;
+      if (!ps.empty() && (p.row != ps[0]->row || p.stride != ps[0]->stride || p.rows != ps[0]->rows)) return false;
+      ps.push_back(&p);
+      seen += p.size();
+      if (seen >= size) break;
+    }
+    if (ps.empty() || seen != size) return false;
+    const size_t row = ps[0]->row, stride = ps[0]->stride, rows = ps[0]->rows;
+    const size_t sf = stride * (rows - 1) + row;  // padded bytes of one frame (the last row's padding may be absent)
+    // equally spaced frames (a capture ring): one DMA over all of them
+    const char* base = static_cast<const char*>(ps[0]->mem->data());
+    size_t spacing = ps.size() > 1 ? static_cast<size_t>(static_cast<const char*>(ps[1]->mem->data()) - base) : sf;
+    bool ring = ps.size() > 1 && static_cast<const char*>(ps[1]->mem->data()) > base && spacing >= sf &&
+                spacing <= 2 * sf;
+    for (size_t i = 2; ring && i < ps.size(); ++i)
+      ring = static_cast<const char*>(ps[i]->mem->data()) == base + i * spacing;
+    if (!ring) spacing = (sf + 255) / 256 * 256;
+    auto stg = Memory::alloc_device(spacing * (ps.size() - 1) + sf, dev, s);
+    char* sp = static_cast<char*>(stg->data());
+    if (ring) {
+      hip::check(hipMemcpyAsync(sp, base, spacing * (ps.size() - 1) + sf, hipMemcpyHostToDevice, s), "padded ring DMA");
+    } else {
+      for (size_t i = 0; i < ps.size(); ++i)
+        hip::check(hipMemcpyAsync(sp + i * spacing, ps[i]->mem->data(), sf, hipMemcpyHostToDevice, s), "padded DMA");
+    }
+    kernels::unpad_rows(sp, out->data(), static_cast<uint32_t>(ps.size()), static_cast<uint32_t>(row),
+                        static_cast<uint32_t>(stride), static_cast<uint32_t>(rows), spacing, s);
+    stg->record_use(s, dev);
+    for (size_t i = 0; i < ps.size(); ++i) {
+      adapter_.front().mem->record_use(s, dev);
+      adapter_.pop_front();
+    }
+    return true;
   }
 
   // the next `size` bytes as at most kMaxRuns address-contiguous runs of unpadded

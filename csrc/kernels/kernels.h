@@ -71,6 +71,12 @@ struct GatherArgs {
   GatherSeg seg[kGatherMax];
 };
 void gather_copy(const GatherArgs& g, void* dst, hipStream_t s);
+// Padded video frames staged in HBM as they were in host memory (one DMA of
+// `src_frame_bytes` per frame on the copy engine): pack `row` bytes of each of
+// the `rows` rows (`stride` apart) of every frame into dst [frames][rows][row].
+// Replaces the bus-reading gather for padded frames (K7 remove-padding).
+void unpad_rows(const void* src, void* dst, uint32_t frames, uint32_t row, uint32_t stride, uint32_t rows,
+                uint64_t src_frame_bytes, hipStream_t s);
 
 // ------------------------------------------------------------------ decode ----
 // Global argmax over n elements (first max wins).  out_index: int32 on device.

@@ -632,7 +632,57 @@ __global__ void __launch_bounds__(256) gather_kernel(GatherArgs g, char* __restr
   }
 }
 
+// padded frames already in HBM (one DMA of the padded bytes per frame): pack
+// their rows.  Each lane writes 16 consecutive output bytes with one 16-byte
+// store (the output is one packed [frames][rows][row] block) and gathers them
+// byte by byte from the staged rows, which sit in L2 right after the DMA.
+__global__ void __launch_bounds__(256) unpad_rows_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                         uint64_t total, uint32_t row, uint32_t stride, uint32_t rows,
+                                                         uint64_t src_frame) {
+  const uint64_t fsz = static_cast<uint64_t>(row) * rows;
+  for (uint64_t q = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; q * 16 < total;
+       q += static_cast<uint64_t>(gridDim.x) * 256) {
+    uint64_t o = q * 16;
+    uint64_t f = o / fsz;
+    uint64_t rem = o - f * fsz;
+    uint32_t y = static_cast<uint32_t>(rem / row);
+    uint32_t x = static_cast<uint32_t>(rem - static_cast<uint64_t>(y) * row);
+    union {
+      uint8_t b[16];
+      uint4 v;
+    } u;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      u.b[i] = o + i < total ? src[f * src_frame + static_cast<uint64_t>(y) * stride + x] : 0;
+      if (++x == row) {
+        x = 0;
+        if (++y == rows) {
+          y = 0;
+          ++f;
+        }
+      }
+    }
+    if (o + 16 <= total) {
+      *reinterpret_cast<uint4*>(dst + o) = u.v;
+    } else {
+      for (uint64_t i = o; i < total; ++i) dst[i] = u.b[i - o];
+    }
+  }
+}
+
 }  // namespace
+
+void unpad_rows(const void* src, void* dst, uint32_t frames, uint32_t row, uint32_t stride, uint32_t rows,
+                uint64_t src_frame_bytes, hipStream_t s) {
+  if (!frames || !rows || !row) return;
+  if (row > stride || src_frame_bytes < static_cast<uint64_t>(stride) * (rows - 1) + row)
+    throw std::invalid_argument("unpad_rows: row <= stride and a staged frame holds every row");
+  const uint64_t total = static_cast<uint64_t>(frames) * row * rows;
+  const uint64_t nq = (total + 15) / 16;
+  const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>((nq + 255) / 256, 8192)));
+  hipLaunchKernelGGL(unpad_rows_kernel, dim3(grid), dim3(256), 0, s, static_cast<const uint8_t*>(src),
+                     static_cast<uint8_t*>(dst), total, row, stride, rows, src_frame_bytes);
+}
 
 void gather_copy(const GatherArgs& g, void* dst, hipStream_t s) {
   if (g.n <= 0) return;

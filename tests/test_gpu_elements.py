@@ -186,9 +186,14 @@ def test_pose_device_matches_host(nns):
     assert len(res[0]) == B and res[0] == res[-1]
 
 
-@pytest.mark.parametrize("w,h,n", [(224, 224, 6), (5, 3, 7), (64, 48, 130), (257, 257, 9), (513, 11, 3), (2731, 5, 2)])
-def test_converter_batched_gather_matches_host(nns, w, h, n):
-    desc = (f"videotestsrc num-buffers={2 * n} pattern=snow pool-size=5 ! video/x-raw,format=RGB,width={w},height={h},"
+@pytest.mark.parametrize("w,h,n,pool", [(224, 224, 6, 5), (5, 3, 7, 5), (64, 48, 130, 5), (257, 257, 9, 5),
+                                         (513, 11, 3, 5), (2731, 5, 2, 5), (513, 513, 8, 64), (257, 257, 64, 128),
+                                         (513, 513, 8, 3), (7, 5, 16, 40)])
+def test_converter_batched_gather_matches_host(nns, w, h, n, pool):
+    """Batched upload (frames-per-tensor) equals the host path byte for byte.
+    Padded rows (W*3 % 4 != 0) take the DMA + unpad_rows path: one DMA over a
+    ring of equally spaced pool frames (pool >= batch) or one per frame."""
+    desc = (f"videotestsrc num-buffers={2 * n} pattern=snow pool-size={pool} ! video/x-raw,format=RGB,width={w},height={h},"
             f"framerate=30/1 ! tensor_converter frames-per-tensor={n} device={{dev}} ! tensor_sink name=sink")
     collect = lambda b: (b.memory(0).on_device, b.memory(0).bytes())
     cpu, gpu = _both(nns, desc, collect)
