@@ -123,20 +123,29 @@ CONFIGS = {
     # (DeepLab: the model ships its 33x33 logits; the decoder's option3 resizes
     # them bilinearly per label inside the argmax pass -- same frames as a
     # 513x513x21 model output, without the 22 MB-per-frame score map)
-    # BASELINE.json config 4: one camera rank fans its batches out to the other ranks
-    # (edgesink connect-type=RCCL rccl-mode=scatter -> ncclSend/ncclRecv over xGMI);
-    # every other rank runs DeepLabV3 + image_segment on what it receives
+    # BASELINE.json config 4: "8 parallel video branches fanned via tensor_demux + RCCL".
+    # Rank 0 holds the N cameras: tensor_converter per camera -> tensor_mux -> tensor_demux;
+    # demux pad 0 feeds rank 0's own DeepLab branch, pad r goes to rank r through
+    # edgesink connect-type=RCCL (a two-member group {0, r}: ncclSend / ncclRecv over
+    # xGMI on a per-direction link).  Every rank runs DeepLabV3 + image_segment.
     "deeplab_fan": dict(size=513, model="deeplab_fused_lowres", norm="typecast:float32,div:255.0",
                         decoder="tensor_decoder mode=image_segment option1=tflite-deeplab option3=513:513", per_frame=True, fan=True,
-                        metric="end-to-end frames/sec, DeepLabV3 513x513 segmentation, branches fanned over RCCL",
-                        desc="DeepLabV3-MobileNetV2 513x513 on N-1 ranks fed by a camera rank (RCCL scatter)"),
-    # BASELINE.json config 5: PoseNet multi-source, outputs all-gathered across ranks
+                        metric="end-to-end frames/sec, DeepLabV3 513x513 segmentation, N video branches fanned "
+                               "via tensor_demux + RCCL",
+                        desc="DeepLabV3-MobileNetV2 513x513, N camera branches on rank 0 demuxed to N GPUs over RCCL"),
+    # BASELINE.json config 5: "PoseNet multi-source pipeline with tensor_mux sync +
+    # nnstreamer-edge RCCL all-gather".  Every rank: camera -> PoseNet -> pose decoder,
+    # and its pose tensors published with edgesink connect-type=RCCL rccl-mode=allgather
+    # (one ncclAllGather per round over all cameras); one edgesrc per other camera feeds
+    # tensor_mux sync-mode=slowest next to the rank's own stream: every rank holds the
+    # synchronised N-camera pose set.
     "posenet_multi": dict(size=257, model="posenet_fused", norm="typecast:float32,add:-127.5,div:127.5",
                           decoder="tensor_decoder mode=pose_estimation option1=640:480 option2=257:257 "
                                   "option3={pose} option4=heatmap-offset", per_frame=True, gather=True,
-                          metric="end-to-end frames/sec + p50 per-frame latency, PoseNet multi-source "
-                                 "pipeline with RCCL all-gather",
-                          desc="PoseNet-MobileNetV1 257x257 per rank + tensor_allgather of the pose tensors"),
+                          metric="end-to-end frames/sec, PoseNet multi-source pipeline with tensor_mux sync "
+                                 "+ edge RCCL all-gather",
+                          desc="PoseNet-MobileNetV1 257x257 per rank, pose tensors all-gathered (edgesink/edgesrc "
+                               "rccl-mode=allgather) into tensor_mux sync-mode=slowest"),
     "posenet": dict(size=257, model="posenet_fused", norm="typecast:float32,add:-127.5,div:127.5",
                     decoder="tensor_decoder mode=pose_estimation option1=640:480 option2=257:257 option3={pose} "
                             "option4=heatmap-offset", per_frame=True,
@@ -216,6 +225,10 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
             f"inputtype=float32 absorb-transform={absorb} accelerator={accel} device={dev} "
             f"custom=hipgraph:{graph}{bcast} device-stats={'true' if use_gpu else 'false'} ")
     live = f"is-live=true " if live_fps > 0 else ""
+    gather = bool(cfg.get("gather"))
+    # multi-source sync: the cameras of every rank stamp the same frame clock (frame k
+    # at k ms) so tensor_mux sync-mode=slowest pairs round k of every camera
+    fr = live_fps if live_fps > 0 else (1000 if gather else 0)
     # throughput runs: queues are thread boundaries, so the next batch's upload
     # is issued while the filter thread still submits this batch's kernels, and
     # the decoder's read-back overlaps the next forward.  The live batch-1
@@ -225,34 +238,46 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
     q2 = f"! queue max-size-buffers={a.queue} " if live_fps <= 0 else ""
     desc = (
         f"videotestsrc num-buffers={frames} pattern=snow pool-size={pool} {live}"
-        f"! video/x-raw,format=RGB,width={S},height={S},framerate={live_fps}/1 "
+        f"! video/x-raw,format=RGB,width={S},height={S},framerate={fr}/1 "
         f"! tensor_converter frames-per-tensor={B} device={dev} "
         + f"! tensor_transform name=norm mode=arithmetic option={cfg['norm']} "
         + q1
         + f"! {filt}"
-        + (f"! tee name=t t. ! queue max-size-buffers={a.queue} " if cfg.get("gather") else q2)
+        + (f"! tee name=t t. ! queue max-size-buffers={a.queue} " if gather else q2)
         + f"! {cfg['decoder'].format(**files)} "
         f"! tensor_sink name=sink"
-        # multi-source: every rank's PoseNet outputs are all-gathered (RCCL over xGMI
-        # between GPUs, the TCP store on CPU) so each rank holds the synchronised
-        # multi-camera set -- one collective per batch, beside the local decoder
-        + (f" t. ! queue max-size-buffers={a.queue} ! tensor_allgather name=ag channel=posenet mode=concat "
-           f"rank={rank} world-size={world} device={dev} comm-backend={a.comm_backend} ! fakesink" if cfg.get("gather") else "")
     )
+    if gather:
+        # this camera's pose tensors go out on the topic (one all-gather round per
+        # batch); every other camera comes back through its own edgesrc, and
+        # tensor_mux pairs the N streams by timestamp (slowest policy)
+        edge = (f"connect-type=RCCL rccl-mode=allgather topic=posenet-b{B} rank={rank} world-size={world} "
+                f"comm-backend={a.comm_backend}")
+        desc += (f" t. ! queue max-size-buffers={a.queue} ! edgesink name=ag {edge} device={dev}"
+                 f" t. ! queue max-size-buffers={a.queue} ! mux.sink_{rank}"
+                 + "".join(f" edgesrc name=sub{r} {edge} peer-rank={r} device={dev} ! queue max-size-buffers="
+                           f"{a.queue} ! mux.sink_{r}" for r in range(world) if r != rank)
+                 + " tensor_mux name=mux sync-mode=slowest ! tensor_sink name=msink")
     fan = bool(cfg.get("fan")) and world > 1
-    workers = world - 1 if fan else world
+    workers = world
     if fan:
-        link = f"connect-type=RCCL rccl-mode=scatter topic=fan rank={rank} world-size={world} device={dev}"
-        if rank == 0:  # the camera rank: upload batches, scatter them round-robin to the workers
-            desc = (f"videotestsrc num-buffers={frames * workers} pattern=snow pool-size={pool} "
-                    f"! video/x-raw,format=RGB,width={S},height={S},framerate=0/1 "
-                    f"! tensor_converter frames-per-tensor={B} device={dev} ! queue max-size-buffers=4 "
-                    f"! edgesink name=fan {link}")
+        def link(r):  # the two-member group of demux branch r: rank 0 -> rank r
+            return (f"connect-type=RCCL rccl-mode=scatter topic=fan{r}-b{B} group-ranks=0,{r} rank={rank} "
+                    f"world-size={world} device={dev} comm-backend={a.comm_backend}")
+        branch = (f"! tensor_transform name=norm mode=arithmetic option={cfg['norm']} ! {filt}"
+                  f"! queue max-size-buffers={a.queue} ! {cfg['decoder'].format(**files)} ! tensor_sink name=sink")
+        if rank == 0:  # the N cameras: upload, mux, demux -> own branch + one RCCL edge per other rank
+            cam_pool = max(2 * B, min(pool, -(-128 * 2**20 // frame_bytes)))
+            desc = ("".join(f"videotestsrc num-buffers={frames} pattern=snow pool-size={cam_pool} "
+                            f"! video/x-raw,format=RGB,width={S},height={S},framerate=0/1 "
+                            f"! tensor_converter frames-per-tensor={B} device={dev} ! queue max-size-buffers=2 "
+                            f"! mux.sink_{r} " for r in range(world))
+                    + "tensor_mux name=mux sync-mode=nosync ! tensor_demux name=d "
+                    + f"d.src_0 ! queue max-size-buffers=2 {branch} "
+                    + " ".join(f"d.src_{r} ! queue max-size-buffers=2 ! edgesink name=fan{r} {link(r)}"
+                               for r in range(1, world)))
         else:
-            desc = (f"edgesrc name=fan {link} peer-rank=0 ! queue max-size-buffers=2 "
-                    + f"! tensor_transform name=norm mode=arithmetic option={cfg['norm']} "
-                    + f"! {filt}"
-                    f"! queue max-size-buffers={a.queue} ! {cfg['decoder'].format(**files)} ! tensor_sink name=sink")
+            desc = f"edgesrc name=fan {link(rank)} peer-rank=0 ! queue max-size-buffers=2 {branch}"
     per_step = B if cfg["per_frame"] else 1  # sink buffers per batch
     pipe = nns.parse_launch(desc)
     sink = pipe.get_by_name("sink")
@@ -277,7 +302,11 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
     t_end = time.perf_counter()
     if dist is not None:
         dist.barrier()
-    gathered = pipe.get_by_name("ag").get_property("comm-bytes") if cfg.get("gather") else None
+    gathered = pipe.get_by_name("ag").get_property("comm-bytes") if gather else None
+    mux_sets = None
+    if gather:
+        ms = pipe.get_by_name("msink")
+        mux_sets = int(ms.get_property("frames")) if ms is not None else None
     dev_stamps = filt_el.get_property("device-stamps") if (filt_el is not None and use_gpu) else ""
     absorbed = filt_el.get_property("absorbed") if filt_el is not None else ""
     absorbed_dec = filt_el.get_property("absorbed-decoder") if filt_el is not None else ""
@@ -285,19 +314,17 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
     groups = {}
     if filt_el is not None and filt_el.get_property("model-broadcast"):
         groups["model_broadcast"] = filt_el.get_property("model-broadcast")
-    for el in ("ag", "fan"):
+    for el in ["ag"] + [f"fan{r}" for r in range(1, world)] + ["fan"]:
         e = pipe.get_by_name(el)
         if e is not None and e.get_property("comm-group"):
-            groups["tensor_allgather" if el == "ag" else "edge_fan"] = e.get_property("comm-group")
+            groups["edge_allgather" if el == "ag" else f"edge_{el}"] = e.get_property("comm-group")
     pipe.stop()
 
     import numpy as np
 
     rec = dict(elapsed=0.0, p50=0.0, p99=0.0, gpu_elapsed=0.0, gpu_busy_ms=0.0, wall=t_end - t_start,
                desc=desc, fan=fan, workers=workers, absorbed=absorbed, absorbed_dec=absorbed_dec, gathered=gathered,
-               groups=groups)
-    if sink is None:
-        return rec  # the workers' clocks decide
+               groups=groups, mux_sets=mux_sets)
     recs = [tuple(int(v) for v in e.split(":")) for e in sink.get_property("stats").split(",") if e]
     arrivals = [t / 1e9 for i, (t, _) in enumerate(recs) if (i + 1) % per_step == 0]  # last frame of each batch
     step_lat = [[lat / 1e6 for _, lat in recs[k * per_step:(k + 1) * per_step] if lat >= 0]
@@ -309,7 +336,9 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
     t1 = arrivals[warmup + steps - 1]
     rec["elapsed"] = t1 - t0
     timed = [x for k in range(warmup, warmup + steps) for x in step_lat[k]]
-    lat = np.array(timed) if (timed and not fan) else np.array([0.0])
+    # (multi-source: the cameras stamp a shared synthetic frame clock, so sink-side
+    # latency is not a pipeline latency there)
+    lat = np.array(timed) if (timed and not fan and not gather) else np.array([0.0])
     rec["p50"] = float(np.percentile(lat, 50))
     rec["p99"] = float(np.percentile(lat, 99))
     # device-clock cross-check: the filter's end-of-invoke events of the same K batches
@@ -443,7 +472,7 @@ def main():
 
         def agg(i, B=B):
             cols = per_rank[:, i * 5:(i + 1) * 5]
-            active = cols[1:] if fan else cols  # the fan-out camera rank has no sink
+            active = cols  # every rank runs a branch (config 4: rank 0's own demux pad too)
             sink_el = float(active[:, 0].max())
             gpu_el = float(active[:, 3].max())
             # the timed window on the slower of the two clocks: sink arrivals can
@@ -474,8 +503,8 @@ def main():
             "vs_baseline": (round(h["fps"] / CPU_BASELINE_FPS, 2) if a.config == "mbv2" else None),
             "dtype": head["dtype"],
             "data": "synthetic video frames (videotestsrc pattern=snow), random-init weights",
-            "p50_latency_ms": None if fan else round(h["p50"], 3),
-            "p99_latency_ms": None if fan else round(h["p99"], 3),
+            "p50_latency_ms": None if (fan or cfg.get("gather")) else round(h["p50"], 3),
+            "p99_latency_ms": None if (fan or cfg.get("gather")) else round(h["p99"], 3),
             "gpu_event_fps": round(h["gpu_fps"], 2) if h["gpu_fps"] else None,
             "sink_fps": round(h["sink_fps"], 2),
             "timing": "value = frames / max(sink-arrival window, device-event window) of the same K batches",
@@ -517,7 +546,8 @@ def main():
                             else "tensor_decoder's own argmax kernel"),
             "wall_s": round(sum(r["wall"] for r in results.values()), 3),
             "numa_binding": numa,
-            **({"allgather_bytes_sent_received_rank0": head["gathered"]} if head["gathered"] is not None else {}),
+            **({"allgather_bytes_published_rank0": head["gathered"]} if head["gathered"] is not None else {}),
+            **({"mux_sets_rank0": head["mux_sets"]} if head.get("mux_sets") is not None else {}),
             # nnsx rank groups of rank 0 ("<data plane>:<members>[:bytes]") and the RCCL world they span
             "nnsx_groups_rank0": head["groups"],
             "rccl_world": max([int(v.split(":")[1]) for v in head["groups"].values() if v.startswith("rccl:")] or [0]),
@@ -525,7 +555,8 @@ def main():
                 "model": cfg["desc"],
                 "global_batch": B * world,
                 "seq_len": 1,
-                "parallelism": f"fan-out 1->{workers} (RCCL scatter)" if fan else f"branch-dp{world}",
+                "parallelism": (f"tensor_demux fan-out 1->{world} (RCCL p2p)" if fan else
+                                f"branch-dp{world} + edge all-gather" if cfg.get("gather") else f"branch-dp{world}"),
                 "pipeline": head["desc"],
             },
         })

@@ -43,7 +43,8 @@ namespace {
 const std::vector<std::string> kConnectTypes = {"TCP", "HYBRID", "MQTT", "AITT", "HIPIPC", "RCCL"};
 constexpr int kHipIpc = 4;
 constexpr int kRccl = 5;
-const std::vector<std::string> kRcclModes = {"broadcast", "scatter"};
+const std::vector<std::string> kRcclModes = {"broadcast", "scatter", "allgather"};
+constexpr int kRcclAllGather = 2;
 constexpr uint32_t kPktCaps = 1;  // packet carries only a caps string
 
 constexpr int kHybrid = 1;
@@ -217,6 +218,100 @@ std::string rccl_channel(const char* kind, const std::string& topic, unsigned po
 }
 
 std::vector<MemoryPtr> place_blobs(std::vector<MemoryPtr> blobs, int device, StreamSet& streams);
+
+// ---------------------------------------------------------------- EdgeHub ----
+// connect-type=RCCL rccl-mode=allgather: N->N pub/sub on one topic.  Every
+// member's edgesink publishes its stream and every member subscribes to the
+// others' with one edgesrc per source (peer-rank); a round is ONE collective
+// (comm::Group::allgather -> ncclAllGather over xGMI for equal-size frames)
+// instead of one broadcast per publisher.  The hub is the process-local
+// meeting point: the publishing edgesink runs the rounds and deals each
+// member's packet to the queue of the local edgesrc subscribed to it (sources
+// nobody subscribed to are dropped); a full queue holds the publisher back
+// (bounded, cancellable), so a slow consumer throttles the whole round.
+// Reference pub/sub: gst/edge/edge_sink.c:305-345, edge_src.c:255-412.
+class EdgeHub {
+ public:
+  static std::shared_ptr<EdgeHub> get(const std::string& key) {
+    static std::mutex mu;
+    static std::map<std::string, std::weak_ptr<EdgeHub>> hubs;
+    std::lock_guard<std::mutex> lk(mu);
+    auto h = hubs[key].lock();
+    if (!h) hubs[key] = h = std::make_shared<EdgeHub>();
+    return h;
+  }
+  void subscribe(int global_rank) {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto& q = subs_[global_rank];
+    // a subscriber that starts after the caps round still gets the caps (sticky)
+    auto c = caps_.find(global_rank);
+    if (q.empty() && c != caps_.end()) q.push_back(c->second);
+    cancelled_ = false;
+  }
+  void unsubscribe(int global_rank) {
+    std::lock_guard<std::mutex> lk(mu_);
+    subs_.erase(global_rank);
+    cv_.notify_all();
+  }
+  // one round: every member's packet, dealt to the subscribed queues
+  bool publish(comm::Group& g, const comm::Packet& mine, std::string* err) {
+    std::vector<comm::Packet> all;
+    if (!g.allgather(mine, &all, err)) return false;
+    std::unique_lock<std::mutex> lk(mu_);
+    for (size_t r = 0; r < all.size(); ++r) {
+      const int src = g.global_rank(static_cast<int>(r));
+      if (all[r].flags & kPktCaps) {
+        caps_[src] = all[r];
+        caps_[src].src = src;
+      }
+      auto it = subs_.find(src);
+      if (it == subs_.end()) continue;
+      cv_.wait(lk, [&] {
+        auto i = subs_.find(src);
+        return cancelled_ || i == subs_.end() || i->second.size() < kDepth;
+      });
+      if (cancelled_) return false;
+      it = subs_.find(src);
+      if (it == subs_.end()) continue;
+      all[r].src = src;
+      it->second.push_back(std::move(all[r]));
+    }
+    cv_.notify_all();
+    return true;
+  }
+  // next packet of member `global_rank` (false + *timed_out on timeout)
+  bool take(int global_rank, comm::Packet* p, int timeout_ms, bool* timed_out) {
+    std::unique_lock<std::mutex> lk(mu_);
+    *timed_out = false;
+    auto ready = [&] {
+      auto it = subs_.find(global_rank);
+      return cancelled_ || (it != subs_.end() && !it->second.empty());
+    };
+    if (!cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), ready)) {
+      *timed_out = true;
+      return false;
+    }
+    if (cancelled_) return false;
+    auto& q = subs_[global_rank];
+    *p = std::move(q.front());
+    q.pop_front();
+    cv_.notify_all();
+    return true;
+  }
+  void cancel() {
+    std::lock_guard<std::mutex> lk(mu_);
+    cancelled_ = true;
+    cv_.notify_all();
+  }
+
+ private:
+  static constexpr size_t kDepth = 4;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::map<int, std::deque<comm::Packet>> subs_;  // per subscribed source (global rank)
+  std::map<int, comm::Packet> caps_;              // latest caps packet per source
+  bool cancelled_ = false;
+};
 
 comm::Packet packet_of(const Buffer& b) {
   comm::Packet p;
@@ -864,7 +959,8 @@ class EdgeSink : public BaseSink {
     prop_readonly("subscribers", [this] { return std::to_string(subscribers()); }, "Connected subscribers");
     rp_.install([this](PropSpec p) -> PropSpec& { return add_prop(p); });
     prop_enum("rccl-mode", &rccl_mode_, kRcclModes,
-              "nnsx (connect-type=RCCL): broadcast every frame to all subscribers, or scatter frames round-robin");
+              "nnsx (connect-type=RCCL): broadcast every frame to all subscribers, scatter frames round-robin, "
+              "or allgather (every member publishes on the topic; one collective per round)");
     prop_readonly("comm-bytes", [this] { return std::to_string(g_ ? g_->bytes_sent() : 0); },
                   "nnsx: payload bytes published on the rank group");
 
@@ -929,6 +1025,7 @@ class EdgeSink : public BaseSink {
   bool stop() override {
     running_ = false;
     g_.reset();
+    hub_.reset();
     announcer_.reset();
     if (broker_) {
       if (broker_->connected()) broker_->publish(broker_topic(connect_type_, topic_, "caps"), "", 0, 1, true);
@@ -951,6 +1048,7 @@ class EdgeSink : public BaseSink {
   void unlock() override {
     running_ = false;
     cv_.notify_all();
+    if (auto h = hub_) h->cancel();
     if (auto g = g_) g->cancel();
   }
   bool set_caps(const Caps& caps) override {
@@ -1015,6 +1113,9 @@ class EdgeSink : public BaseSink {
     bool ok = true;
     if (rccl_mode_ == 0) {
       ok = g_->broadcast(g_->rank(), &p, &err);
+    } else if (rccl_mode_ == kRcclAllGather) {
+      if (!hub_) hub_ = EdgeHub::get(g_->name());
+      ok = hub_->publish(*g_, p, &err);
     } else if (control) {
       for (int r = 0; r < g_->size() && ok; ++r)
         if (r != g_->rank()) ok = g_->send(r, p, &err);
@@ -1063,6 +1164,7 @@ class EdgeSink : public BaseSink {
   int rccl_mode_ = 0;
   unsigned rr_ = 0;
   std::shared_ptr<comm::Group> g_;
+  std::shared_ptr<EdgeHub> hub_;  // rccl-mode=allgather
   std::unique_ptr<HybridAnnouncer> announcer_;
   std::unique_ptr<comm::MqttClient> broker_;  // connect-type=MQTT / AITT
 };
@@ -1119,10 +1221,13 @@ class EdgeSrc : public BaseSrc {
   void on_stop() override {
     if (conn_) conn_->close();
     if (broker_) broker_->close();
+    if (hub_) hub_->unsubscribe(hub_src_);
+    hub_.reset();
     g_.reset();
   }
   void on_unlock() override {
     if (conn_) conn_->close();
+    if (auto h = hub_) h->cancel();
     if (auto g = g_) g->cancel();
   }
 
@@ -1141,6 +1246,16 @@ class EdgeSrc : public BaseSrc {
   // connect-type=RCCL: next packet from the publisher (false: cancelled / lost)
   bool recv_rccl(comm::Packet* p) {
     std::string err;
+    if (rccl_mode_ == kRcclAllGather) {
+      // the local edgesink of the topic runs the rounds (EdgeHub); this source
+      // takes its publisher's share
+      while (!flushing_.load()) {
+        bool to = false;
+        if (hub_->take(hub_src_, p, 100, &to)) return true;
+        if (!to) break;
+      }
+      return false;
+    }
     if (rccl_mode_ == 0) {
       const int root = rp_.peer_in(*g_);
       if (root < 0 || root == g_->rank()) {
@@ -1162,6 +1277,24 @@ class EdgeSrc : public BaseSrc {
 
   // the publisher's caps arrive with HELLO (or a later CAPS message)
   bool negotiate() override {
+    if (connect_type_ == kRccl && rccl_mode_ == kRcclAllGather) {
+      // no group of its own: subscribe to the topic's hub (fed by the local edgesink)
+      if (rp_.peer < 0) {
+        post_error("edgesrc: rccl-mode=allgather needs peer-rank (the publishing member)");
+        return false;
+      }
+      if (!hub_) {
+        hub_src_ = rp_.peer;
+        hub_ = EdgeHub::get(rccl_channel("edge", topic_, dest_port_));
+        hub_->subscribe(hub_src_);
+      }
+      while (caps_str_.empty()) {
+        comm::Packet p;
+        if (!recv_rccl(&p) || p.eos) return false;
+        if (!p.caps.empty()) caps_str_ = p.caps;
+      }
+      return BaseSrc::negotiate();
+    }
     if (connect_type_ == kRccl) {
       rp_.device = device_;
       if (!g_ && !(g_ = rp_.open(this, rccl_channel("edge", topic_, dest_port_)))) return false;
@@ -1239,6 +1372,8 @@ class EdgeSrc : public BaseSrc {
   RankProps rp_;
   int rccl_mode_ = 0;
   std::shared_ptr<comm::Group> g_;
+  std::shared_ptr<EdgeHub> hub_;  // rccl-mode=allgather: the topic's hub
+  int hub_src_ = -1;              // the publishing member (global rank) this source takes
   std::unique_ptr<comm::MqttClient> broker_;  // connect-type=MQTT / AITT
 };
 

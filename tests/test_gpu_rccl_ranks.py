@@ -1,7 +1,7 @@
 """RCCL data plane with one process per GPU (BASELINE.json configs 4 and 5):
 every collective and p2p call of comm::Group over RCCL/xGMI between N =
 min(#GPUs, 8) ranks, payload values checked on every member, plus the two
-multi-rank bench configs (edgesink rccl-mode=scatter fan-out, tensor_allgather).
+multi-rank bench configs (tensor_demux -> edgesink RCCL fan-out; edge all-gather -> tensor_mux).
 Reference fan-out / fan-in points: tensor_query_client.c:657-746,
 edge_sink.c:305-345, gsttensor_demux.c:469-556.  Skipped below 2 GPUs (the
 1-GPU pool); the CPU twin is tests/test_rank_collectives.py."""
@@ -60,4 +60,7 @@ def test_bench_multi_rank_configs(cfg):
     rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert rec["n_gpus"] == n and rec["value"] > 0, rec
     if cfg == "posenet_multi":
-        assert rec.get("allgather_bytes_sent_received_rank0"), rec
+        assert int(rec.get("allgather_bytes_published_rank0", 0)) > 0, rec
+        assert rec.get("mux_sets_rank0") == 4, rec  # every batch a full N-camera set
+    else:
+        assert "tensor_demux" in rec["config"]["pipeline"], rec

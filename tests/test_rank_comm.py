@@ -179,7 +179,9 @@ def test_allgather_torchrun_style_processes(tmp_path):
 
 def test_bench_posenet_multi_two_ranks_cpu():
     """BASELINE.json config 5 through bench.py: two torchrun ranks, every rank's
-    PoseNet outputs all-gathered (TCP data plane on CPU; RCCL on GPUs)."""
+    PoseNet outputs published with edgesink rccl-mode=allgather and taken back by
+    one edgesrc per other camera into tensor_mux sync-mode=slowest (TCP data
+    plane on CPU; RCCL on GPUs)."""
     import json
     port = _free_port()
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
@@ -189,15 +191,16 @@ def test_bench_posenet_multi_two_ranks_cpu():
     assert r.returncode == 0, r.stderr[-3000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
     d = json.loads(line)
-    assert d["config"]["parallelism"] == "branch-dp2" and d["value"] > 0
-    sent, recv = (int(v) for v in d["allgather_bytes_sent_received_rank0"].split(":"))
-    assert sent > 0 and recv == sent  # equal-size contributions from both ranks
+    assert d["config"]["parallelism"] == "branch-dp2 + edge all-gather" and d["value"] > 0
+    assert "tensor_mux name=mux sync-mode=slowest" in d["config"]["pipeline"]
+    assert int(d["allgather_bytes_published_rank0"]) > 0
+    assert d["mux_sets_rank0"] == 3  # warmup + steps batches, every one a full 2-camera set
 
 
 def test_bench_deeplab_fan_three_ranks_cpu():
-    """BASELINE.json config 4 through bench.py: rank 0 uploads frames and scatters
-    the batches round-robin (edgesink connect-type=RCCL rccl-mode=scatter) to two
-    DeepLab worker ranks."""
+    """BASELINE.json config 4 through bench.py: rank 0 holds the three cameras,
+    tensor_mux -> tensor_demux; pad 0 feeds its own DeepLab branch, pads 1 and 2
+    go to ranks 1 and 2 through edgesink connect-type=RCCL (two-member groups)."""
     import json
     port = _free_port()
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3",
@@ -206,7 +209,8 @@ def test_bench_deeplab_fan_three_ranks_cpu():
                        capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
-    assert d["config"]["parallelism"].startswith("fan-out 1->2") and d["value"] > 0
+    assert d["config"]["parallelism"].startswith("tensor_demux fan-out 1->3") and d["value"] > 0
+    assert "tensor_demux name=d" in d["config"]["pipeline"]
 
 
 def test_ini_rccl_and_hip_sections(tmp_path):
