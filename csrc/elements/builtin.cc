@@ -17,8 +17,6 @@ void register_tensor_filter();
 void register_tensor_stream_elements();  // mux/demux/merge/split/aggregator
 void register_extra_elements();
 
-__attribute__((weak)) void register_torch_frameworks_weak() {}
-
 void ensure_builtin_elements() {
   static std::once_flag once;
   std::call_once(once, [] {

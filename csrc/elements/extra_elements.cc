@@ -1015,6 +1015,12 @@ class Join : public Element {
       std::lock_guard<std::mutex> lk(mu_);
       return active_;
     }, "The currently active sink pad");
+    // gst/join/gstjoin.c:448 (read-only; counts the requested sink pads)
+    prop_readonly("n-pads", [this] {
+      size_t n = 0;
+      for (Pad* p : sink_pads()) n += p != nullptr;
+      return std::to_string(n);
+    }, "The number of sink pads");
   }
   FlowReturn chain(Pad* pad, BufferPtr buf) override {
     std::lock_guard<std::mutex> lk(mu_);

@@ -162,6 +162,7 @@ def test_join(nns):
     p = nns.parse_launch(desc)
     out = []
     p.get_by_name("sink").connect("new-data", lambda b: out.append(int(b.memory(0).numpy()[0])))
+    assert p.get_by_name("j").get_property("n-pads") == "2"  # gstjoin.c:448, read-only
     p.set_state("playing")
     p.get_by_name("a").push_buffer(np.full(4, 1, np.uint8), pts=0)
     p.get_by_name("b").push_buffer(np.full(4, 2, np.uint8), pts=1)
