@@ -592,85 +592,130 @@ class BoundingBoxes : public DecoderInstance {
   }
 
   // ------------------------------------------------------------ device ----
-  FlowReturn decode_device(const TensorsConfig& config, const std::vector<MemoryPtr>& in, Buffer* out,
-                           InvokeContext& ctx, unsigned batch) {
-    const int dev = ctx.device;
-    hipStream_t s = ctx.stream;
-    const int n = static_cast<int>(is_ssd()                                ? std::min(max_detection_, kSsdMax)
-                                   : (mode_ == OV_PERSON || mode_ == OV_FACE) ? kOvMax
-                                                                               : max_detection_);
+  // Device decode in two parts: prepare (scratch, priors / anchors / labels
+  // uploaded once; may sync) and enqueue (kernels + one memset on `s`, no host
+  // work, no allocation) -- so the same enqueue also runs inside an upstream
+  // filter's hipGraph capture (stage_enqueue, runtime/fusion.h).
+  bool prepare_device(const TensorsConfig& config, int dev, hipStream_t s, unsigned batch) {
+    const int n = det_count();
     const int k = std::min(kNmsCap, (n + 63) / 64 * 64);
     const size_t need = kernels::det_scratch_bytes(n, k, static_cast<int>(batch));
     if (!scratch_ || scratch_->size() < need || scratch_->device() != dev) {
+      // a decode still queued on the old block keeps it alive (record_use)
       scratch_ = Memory::alloc_device(need, dev, s);
     }
-    kernels::DetScratch ds = kernels::det_scratch_carve(scratch_->data(), n, k, static_cast<int>(batch));
     ensure_labels(dev, s);
+    if (is_ssd() && (!dev_priors_ || dev_priors_->device() != dev)) {
+      // rows of n priors (the kernel's stride: the decoded box count)
+      std::vector<float> flat(4 * static_cast<size_t>(n));
+      for (int r = 0; r < 4; ++r)
+        std::memcpy(flat.data() + static_cast<size_t>(r) * n, priors_[static_cast<size_t>(r)].data(), sizeof(float) * n);
+      dev_priors_ = Memory::alloc_device(flat.size() * sizeof(float), dev, s);
+      hip::check(hipMemcpyAsync(dev_priors_->data(), flat.data(), flat.size() * sizeof(float), hipMemcpyHostToDevice, s),
+                 "priors H2D");
+      hip::check(hipStreamSynchronize(s), "priors sync");
+    }
+    if (mode_ == MP_PALM && (!dev_anchors_ || dev_anchors_->device() != dev || dev_anchor_count_ != anchors_.size())) {
+      std::vector<float> flat;
+      for (const Anchor& a : anchors_) flat.insert(flat.end(), {a.xc, a.yc, a.w, a.h});
+      dev_anchors_ = Memory::alloc_device(flat.size() * sizeof(float), dev, s);
+      hip::check(hipMemcpyAsync(dev_anchors_->data(), flat.data(), flat.size() * sizeof(float), hipMemcpyHostToDevice, s),
+                 "anchors H2D");
+      hip::check(hipStreamSynchronize(s), "anchors sync");
+      dev_anchor_count_ = anchors_.size();
+    }
+    dev_cfg_ = config;
+    dev_batch_ = batch;
+    return true;
+  }
+  int det_count() const {
+    return static_cast<int>(is_ssd()                                  ? std::min(max_detection_, kSsdMax)
+                            : (mode_ == OV_PERSON || mode_ == OV_FACE) ? kOvMax
+                                                                       : max_detection_);
+  }
+  // in: device pointers of the input tensors (config order); frames: B RGBA frames
+  void enqueue_device(const std::vector<const void*>& in, uint32_t* frames, hipStream_t s) {
+    const TensorsConfig& config = dev_cfg_;
+    const unsigned batch = dev_batch_;
+    const int n = det_count();
+    const int k = std::min(kNmsCap, (n + 63) / 64 * 64);
+    kernels::DetScratch ds = kernels::det_scratch_carve(scratch_->data(), n, k, static_cast<int>(batch));
+    auto f = [&](size_t i) { return static_cast<const float*>(in[i]); };
     if (is_ssd()) {
-      if (!dev_priors_ || dev_priors_->device() != dev) {
-        std::vector<float> flat(4 * static_cast<size_t>(n));
-        for (int r = 0; r < 4; ++r)
-          std::memcpy(flat.data() + static_cast<size_t>(r) * n, priors_[static_cast<size_t>(r)].data(), sizeof(float) * n);
-        dev_priors_ = Memory::alloc_device(flat.size() * sizeof(float), dev, s);
-        hip::check(hipMemcpyAsync(dev_priors_->data(), flat.data(), flat.size() * sizeof(float),
-                                  hipMemcpyHostToDevice, s),
-                   "priors H2D");
-        hip::check(hipStreamSynchronize(s), "priors sync");
-      }
       kernels::SsdParams p{sig_thr_, ssd_params_[1], ssd_params_[2], ssd_params_[3], ssd_params_[4],
                            static_cast<int>(i_width_), static_cast<int>(i_height_)};
-      const float* boxes = static_cast<const float*>(in[0]->map_device(dev, s));
-      const float* scores = static_cast<const float*>(in[1]->map_device(dev, s));
-      kernels::ssd_candidates(boxes, scores, static_cast<const float*>(dev_priors_->data()),
+      kernels::ssd_candidates(f(0), f(1), static_cast<const float*>(dev_priors_->data()),
                               static_cast<int>(config.info.at(1).dim[0]), static_cast<int>(batch), p, ds, s);
       kernels::sort_nms(ds, static_cast<int>(batch), ssd_params_[5], s);
     } else if (is_ssd_pp()) {
-      auto ptr = [&](int i) { return static_cast<const float*>(in[static_cast<size_t>(pp_map_[i])]->map_device(dev, s)); };
-      kernels::pp_candidates(ptr(0), ptr(1), ptr(2), ptr(3),
+      kernels::pp_candidates(f(static_cast<size_t>(pp_map_[0])), f(static_cast<size_t>(pp_map_[1])),
+                             f(static_cast<size_t>(pp_map_[2])), f(static_cast<size_t>(pp_map_[3])),
                              static_cast<int>(config.info.at(static_cast<unsigned>(pp_map_[0])).dim[0]), pp_thr_,
                              static_cast<int>(i_width_), static_cast<int>(i_height_), ds, s);
       kernels::sort_keep_all(ds, 1, s);
     } else if (mode_ == OV_PERSON || mode_ == OV_FACE) {
-      kernels::ov_candidates(static_cast<const float*>(in[0]->map_device(dev, s)), kOvConf, static_cast<int>(i_width_),
-                             static_cast<int>(i_height_), ds, s);
+      kernels::ov_candidates(f(0), kOvConf, static_cast<int>(i_width_), static_cast<int>(i_height_), ds, s);
       kernels::sort_keep_all(ds, 1, s);
     } else if (mode_ == MP_PALM) {
-      if (!dev_anchors_ || dev_anchors_->device() != dev || dev_anchor_count_ != anchors_.size()) {
-        std::vector<float> flat;
-        for (const Anchor& a : anchors_) flat.insert(flat.end(), {a.xc, a.yc, a.w, a.h});
-        dev_anchors_ = Memory::alloc_device(flat.size() * sizeof(float), dev, s);
-        hip::check(hipMemcpyAsync(dev_anchors_->data(), flat.data(), flat.size() * sizeof(float),
-                                  hipMemcpyHostToDevice, s),
-                   "anchors H2D");
-        hip::check(hipStreamSynchronize(s), "anchors sync");
-        dev_anchor_count_ = anchors_.size();
-      }
-      kernels::palm_candidates(static_cast<const float*>(in[0]->map_device(dev, s)),
-                               static_cast<const float*>(in[1]->map_device(dev, s)),
-                               static_cast<const float*>(dev_anchors_->data()),
+      kernels::palm_candidates(f(0), f(1), static_cast<const float*>(dev_anchors_->data()),
                                static_cast<int>(config.info.at(0).dim[0]), palm_thr_, static_cast<int>(i_width_),
                                static_cast<int>(i_height_), ds, s);
       kernels::sort_nms(ds, 1, 0.05f, s);
     } else {
-      const float* x = static_cast<const float*>(in[0]->map_device(dev, s));
-      kernels::yolov5_candidates(x, static_cast<int>(labels_.size()), static_cast<int>(batch), kYoloConf,
+      kernels::yolov5_candidates(f(0), static_cast<int>(labels_.size()), static_cast<int>(batch), kYoloConf,
                                  yolo_scaled_, static_cast<int>(i_width_), static_cast<int>(i_height_), ds, s);
       kernels::sort_nms(ds, static_cast<int>(batch), kYoloIou, s);
     }
     const size_t fsize = static_cast<size_t>(width_) * height_ * 4;
-    MemoryPtr frames = Memory::alloc_device(fsize * batch, dev, s);
-    hip::check(hipMemsetAsync(frames->data(), 0, fsize * batch, s), "clear frames");
-    kernels::draw_boxes(ds, static_cast<int>(batch), static_cast<uint32_t*>(frames->data()),
-                        static_cast<int>(width_), static_cast<int>(height_), static_cast<int>(i_width_),
-                        static_cast<int>(i_height_), dev_labels_ ? static_cast<const char*>(dev_labels_->data()) : nullptr,
+    hip::check(hipMemsetAsync(frames, 0, fsize * batch, s), "clear frames");
+    kernels::draw_boxes(ds, static_cast<int>(batch), frames, static_cast<int>(width_), static_cast<int>(height_),
+                        static_cast<int>(i_width_), static_cast<int>(i_height_),
+                        dev_labels_ ? static_cast<const char*>(dev_labels_->data()) : nullptr,
                         dev_label_offs_ ? static_cast<const int*>(dev_label_offs_->data()) : nullptr,
                         static_cast<int>(labels_.size()), use_labels_, label_style_, s);
+  }
+
+  FlowReturn decode_device(const TensorsConfig& config, const std::vector<MemoryPtr>& in, Buffer* out,
+                           InvokeContext& ctx, unsigned batch) {
+    const int dev = ctx.device;
+    hipStream_t s = ctx.stream;
+    prepare_device(config, dev, s, batch);
+    std::vector<const void*> ptrs;
+    for (auto& m : in) ptrs.push_back(m->map_device(dev, s));
+    const size_t fsize = static_cast<size_t>(width_) * height_ * 4;
+    MemoryPtr frames = Memory::alloc_device(fsize * batch, dev, s);
+    enqueue_device(ptrs, static_cast<uint32_t*>(frames->data()), s);
     frames->mark_ready(s);
     scratch_->record_use(s, dev);
     for (unsigned b = 0; b < batch; ++b) out->mems.push_back(Memory::view(frames, b * fsize, fsize));
     return FlowReturn::OK;
   }
 
+ public:
+  // ---- device stage (runtime/fusion.h): candidates + sort + NMS + raster in
+  // the filter's graph; output = the B RGBA frames [4:W:H:B] ----
+  bool stage_prepare(const TensorsConfig& config, int dev, hipStream_t s, TensorsInfo* out) override {
+    unsigned batch = 1;
+    if (dev < 0 || !check_config(config, &batch) || config.info.at(0).type != DType::FLOAT32 || width_ == 0 ||
+        height_ == 0 || i_width_ == 0 || i_height_ == 0)
+      return false;
+    for (unsigned i = 0; i < config.info.num_tensors; ++i)
+      if (config.info.at(i).type != DType::FLOAT32) return false;
+    use_labels_ = !labels_.empty();
+    if (!prepare_device(config, dev, s, batch)) return false;
+    out->resize(1);
+    TensorInfo& t = out->at(0);
+    t.type = DType::UINT8;
+    t.dim = make_dims({4, width_, height_, batch});
+    return true;
+  }
+  bool stage_enqueue(const std::vector<const void*>& in, const std::vector<void*>& out, hipStream_t s) override {
+    if (in.size() != dev_cfg_.info.num_tensors || out.size() != 1) return false;
+    enqueue_device(in, static_cast<uint32_t*>(out[0]), s);
+    return true;
+  }
+
+ private:
   void ensure_labels(int dev, hipStream_t s) {
     if (labels_.empty() || (dev_labels_ && dev_labels_->device() == dev)) return;
     std::string blob;
@@ -710,6 +755,8 @@ class BoundingBoxes : public DecoderInstance {
   // device state
   MemoryPtr scratch_, dev_priors_, dev_labels_, dev_label_offs_, dev_anchors_;
   size_t dev_anchor_count_ = 0;
+  TensorsConfig dev_cfg_;  // the input config prepare_device sized the scratch for
+  unsigned dev_batch_ = 1;
   std::vector<Det> last_;
 };
 

@@ -172,6 +172,49 @@ class ImageSegment : public DecoderInstance {
  private:
   static constexpr float kThreshold = 0.5f;
 
+ public:
+  // ---- device stage (runtime/fusion.h): (resize +) argmax + colour map inside
+  // the filter's graph; output = the B RGBA frames [4:W:H:B] ----
+  bool stage_prepare(const TensorsConfig& config, int dev, hipStream_t s, TensorsInfo* out) override {
+    if (dev < 0 || config.info.num_tensors < 1) return false;
+    const TensorInfo& ti = config.info.at(0);
+    unsigned w, h, batch;
+    if (!geometry(ti, &w, &h, &batch) || !sane(ti)) return false;
+    st_w_ = w;
+    st_h_ = h;
+    st_batch_ = batch;
+    if (mode_ == SNPE_DEPTH && (!ws_ || ws_->size() < batch * sizeof(uint32_t) || ws_->device() != dev))
+      ws_ = Memory::alloc_device(std::max<size_t>(batch, 64) * sizeof(uint32_t), dev, s);
+    const bool rs = resizes(w, h);
+    out->resize(1);
+    out->at(0).type = DType::UINT8;
+    out->at(0).dim = make_dims({4, rs ? out_w_ : w, rs ? out_h_ : h, batch});
+    return true;
+  }
+  bool stage_enqueue(const std::vector<const void*>& in, const std::vector<void*>& out, hipStream_t s) override {
+    if (in.empty() || out.size() != 1) return false;
+    enqueue_device(static_cast<const float*>(in[0]), st_w_, st_h_, st_batch_, static_cast<uint32_t*>(out[0]), s);
+    return true;
+  }
+
+ private:
+  // the device decode of [B] frames of w x h scores into RGBA frames (kernels only)
+  void enqueue_device(const float* x, unsigned w, unsigned h, unsigned batch, uint32_t* o, hipStream_t s) {
+    const uint32_t rgb_mod = 0xFFFFFFu / (max_labels_ + 1);
+    const uint64_t npix = static_cast<uint64_t>(w) * h;
+    if (resizes(w, h)) {
+      kernels::segment_upsample_argmax_color(x, static_cast<int>(max_labels_ + 1), static_cast<int>(h), static_cast<int>(w),
+                                             static_cast<int>(batch), static_cast<int>(out_h_), static_cast<int>(out_w_),
+                                             rgb_mod, kThreshold, o, s);
+    } else if (mode_ == TFLITE_DEEPLAB) {
+      kernels::segment_argmax_color(x, static_cast<int>(max_labels_ + 1), npix * batch, rgb_mod, kThreshold, o, s);
+    } else if (mode_ == SNPE_DEEPLAB) {
+      kernels::segment_index_color(x, npix * batch, static_cast<int>(max_labels_), rgb_mod, o, s);
+    } else {
+      kernels::segment_depth_gray(x, npix, static_cast<int>(batch), static_cast<uint32_t*>(ws_->data()), o, s);
+    }
+  }
+
   bool resizes(unsigned w, unsigned h) const {
     return mode_ == TFLITE_DEEPLAB && out_w_ && out_h_ && (out_w_ != w || out_h_ != h);
   }
@@ -265,6 +308,7 @@ class ImageSegment : public DecoderInstance {
   unsigned max_labels_ = 20;
   unsigned out_w_ = 0, out_h_ = 0;  // option3
   MemoryPtr ws_;
+  unsigned st_w_ = 0, st_h_ = 0, st_batch_ = 1;  // the geometry stage_prepare saw
 };
 
 class ImageSegmentPlugin : public DecoderSubplugin {
@@ -351,31 +395,12 @@ class PoseEstimation : public DecoderInstance {
       // all on the GPU: heatmap argmax, offset refinement and skeleton raster (no host sync)
       const int dev = ctx.device;
       hipStream_t s = ctx.stream;
-      const float* x = static_cast<const float*>(in[0]->map_device(dev, s));
-      if (!dev_kp_ || dev_kp_->size() < kp.size() * sizeof(float) || dev_kp_->device() != dev)
-        dev_kp_ = Memory::alloc_device(kp.size() * sizeof(float), dev, s);
-      ensure_device_meta(dev, s);
-      kernels::pose_heatmap_argmax(x, K, gw, gh, static_cast<int>(batch), mode_ == 1,
-                                   static_cast<float*>(dev_kp_->data()), s);
+      prepare_device(gw, gh, batch, dev, s);
       const size_t fsize = static_cast<size_t>(width_) * height_ * 4;
       MemoryPtr frames = Memory::alloc_device(fsize * batch, dev, s);
-      hip::check(hipMemsetAsync(frames->data(), 0, fsize * batch, s), "pose clear");
-      kernels::PoseDrawArgs da;
-      da.kp = static_cast<const float*>(dev_kp_->data());
-      da.offsets = mode_ == 1 ? static_cast<const float*>(in[1]->map_device(dev, s)) : nullptr;
-      da.keypoints = K;
-      da.gw = gw;
-      da.gh = gh;
-      da.i_w = static_cast<int>(i_width_);
-      da.i_h = static_cast<int>(i_height_);
-      da.W = static_cast<int>(width_);
-      da.H = static_cast<int>(height_);
-      da.edges = static_cast<const int*>(dev_edges_->data());
-      da.n_edges = n_edges_;
-      da.labels = static_cast<const char*>(dev_labels_->data());
-      da.label_offs = static_cast<const int*>(dev_label_offs_->data());
-      da.frames = static_cast<uint32_t*>(frames->data());
-      kernels::pose_draw(da, static_cast<int>(batch), s);
+      enqueue_device(static_cast<const float*>(in[0]->map_device(dev, s)),
+                     mode_ == 1 ? static_cast<const float*>(in[1]->map_device(dev, s)) : nullptr,
+                     static_cast<uint32_t*>(frames->data()), s);
       frames->mark_ready(s);
       dev_kp_->record_use(s, dev);
       ctx.out_frames = batch;
@@ -445,6 +470,65 @@ class PoseEstimation : public DecoderInstance {
  private:
   static constexpr uint32_t kPixel = 0xFFFFFFFFu;
 
+  // device decode, split so the enqueue also runs inside the filter's graph
+  // capture (stage_enqueue): prepare allocates / uploads, enqueue only launches
+  void prepare_device(int gw, int gh, unsigned batch, int dev, hipStream_t s) {
+    const size_t kp_bytes = static_cast<size_t>(batch) * meta_.size() * 3 * sizeof(float);
+    if (!dev_kp_ || dev_kp_->size() < kp_bytes || dev_kp_->device() != dev) dev_kp_ = Memory::alloc_device(kp_bytes, dev, s);
+    ensure_device_meta(dev, s);
+    st_gw_ = gw;
+    st_gh_ = gh;
+    st_batch_ = batch;
+  }
+  void enqueue_device(const float* x, const float* offsets, uint32_t* frames, hipStream_t s) {
+    const int K = static_cast<int>(meta_.size());
+    kernels::pose_heatmap_argmax(x, K, st_gw_, st_gh_, static_cast<int>(st_batch_), mode_ == 1,
+                                 static_cast<float*>(dev_kp_->data()), s);
+    const size_t fsize = static_cast<size_t>(width_) * height_ * 4;
+    hip::check(hipMemsetAsync(frames, 0, fsize * st_batch_, s), "pose clear");
+    kernels::PoseDrawArgs da;
+    da.kp = static_cast<const float*>(dev_kp_->data());
+    da.offsets = offsets;
+    da.keypoints = K;
+    da.gw = st_gw_;
+    da.gh = st_gh_;
+    da.i_w = static_cast<int>(i_width_);
+    da.i_h = static_cast<int>(i_height_);
+    da.W = static_cast<int>(width_);
+    da.H = static_cast<int>(height_);
+    da.edges = static_cast<const int*>(dev_edges_->data());
+    da.n_edges = n_edges_;
+    da.labels = static_cast<const char*>(dev_labels_->data());
+    da.label_offs = static_cast<const int*>(dev_label_offs_->data());
+    da.frames = frames;
+    kernels::pose_draw(da, static_cast<int>(st_batch_), s);
+  }
+
+ public:
+  // ---- device stage (runtime/fusion.h): heatmap argmax + offsets + skeleton
+  // raster inside the filter's graph; output = the B RGBA frames [4:W:H:B] ----
+  bool stage_prepare(const TensorsConfig& config, int dev, hipStream_t s, TensorsInfo* out) override {
+    if (dev < 0 || get_out_caps(config).is_empty()) return false;
+    const TensorInfo& hi = config.info.at(0);
+    const int K = static_cast<int>(meta_.size());
+    for (unsigned i = 0; i < config.info.num_tensors; ++i)
+      if (config.info.at(i).type != DType::FLOAT32) return false;
+    if (K > 64 || width_ == 0 || height_ == 0 || i_width_ == 0 || i_height_ == 0) return false;
+    prepare_device(static_cast<int>(hi.dim[1]), static_cast<int>(hi.dim[2]), hi.dim[3], dev, s);
+    st_tensors_ = config.info.num_tensors;
+    out->resize(1);
+    out->at(0).type = DType::UINT8;
+    out->at(0).dim = make_dims({4, width_, height_, hi.dim[3]});
+    return true;
+  }
+  bool stage_enqueue(const std::vector<const void*>& in, const std::vector<void*>& out, hipStream_t s) override {
+    if (in.size() != st_tensors_ || out.size() != 1) return false;
+    enqueue_device(static_cast<const float*>(in[0]), mode_ == 1 ? static_cast<const float*>(in[1]) : nullptr,
+                   static_cast<uint32_t*>(out[0]), s);
+    return true;
+  }
+
+ private:
   struct Point {
     bool valid = false;
     int x = 0, y = 0;
@@ -583,6 +667,8 @@ class PoseEstimation : public DecoderInstance {
   std::vector<PoseMeta> meta_;
   MemoryPtr dev_kp_, host_kp_, dev_edges_, dev_labels_, dev_label_offs_;
   int n_edges_ = 0;
+  int st_gw_ = 0, st_gh_ = 0;  // the geometry prepare_device saw
+  unsigned st_batch_ = 1, st_tensors_ = 1;
 };
 
 class PosePlugin : public DecoderSubplugin {

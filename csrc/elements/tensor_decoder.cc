@@ -30,7 +30,22 @@ class CustomCodeDecoder : public DecoderInstance {
   DecoderCustomFn fn_;
 };
 
-class TensorDecoder : public BaseTransform, public ArgmaxConsumer {
+// DecodeStage over a decoder instance: prepared on the filter's device, run by
+// the filter inside its graph capture (runtime/fusion.h)
+class InstanceStage : public DecodeStage {
+ public:
+  InstanceStage(DecoderInstance* inst, TensorsInfo out) : inst_(inst), out_(std::move(out)) {}
+  const TensorsInfo& out_info() const override { return out_; }
+  bool enqueue(const std::vector<const void*>& in, const std::vector<void*>& out, void* stream) override {
+    return inst_->stage_enqueue(in, out, static_cast<hipStream_t>(stream));
+  }
+
+ private:
+  DecoderInstance* inst_;
+  TensorsInfo out_;
+};
+
+class TensorDecoder : public BaseTransform, public ArgmaxConsumer, public DecodeStageConsumer {
  public:
   explicit TensorDecoder(const std::string& name)
       : BaseTransform("tensor_decoder", name, Caps::from_string(tensor_caps_template_all()), Caps::Any()) {
@@ -52,6 +67,9 @@ class TensorDecoder : public BaseTransform, public ArgmaxConsumer {
     prop_readonly("argmax-by", [this] { return argmax_by_; },
                   "nnsx: the upstream tensor_filter that runs this decoder's argmax inside its device work "
                   "(runtime/fusion.h; empty: the decoder runs it)");
+    prop_readonly("stage-by", [this] { return stage_by_; },
+                  "nnsx: the upstream tensor_filter that runs this decoder's device post-processing inside its "
+                  "hipGraph (runtime/fusion.h DecodeStage; empty: the decoder runs it)");
   }
 
   // ---- ArgmaxConsumer (runtime/fusion.h) ----
@@ -63,6 +81,26 @@ class TensorDecoder : public BaseTransform, public ArgmaxConsumer {
   void drop_argmax() override {
     if (inst_) inst_->drop_argmax_input();
     argmax_by_.clear();
+  }
+
+  // ---- DecodeStageConsumer (runtime/fusion.h) ----
+  std::shared_ptr<DecodeStage> take_stage(const TensorsConfig& model_out, int dev, const std::string& by) override {
+    if (!inst_ || dev < 0 || !inst_->supports_device() || !model_out.is_static()) return nullptr;
+    if (device_ != -2 && device_ != dev) return nullptr;  // pinned to another device / the host
+    if (inst_->get_out_caps(model_out).is_empty()) return nullptr;
+    TensorsInfo out;
+    hip::DeviceGuard g(dev);
+    if (!inst_->stage_prepare(model_out, dev, streams_.get(dev), &out) || out.num_tensors != 1 ||
+        out.at(0).type != DType::UINT8 || out.at(0).dim[0] != 4)
+      return nullptr;
+    stage_in_ = model_out;
+    stage_by_ = by;
+    stage_ = std::make_shared<InstanceStage>(inst_.get(), out);
+    return stage_;
+  }
+  void drop_stage() override {
+    stage_.reset();
+    stage_by_.clear();
   }
 
  protected:
@@ -121,7 +159,9 @@ class TensorDecoder : public BaseTransform, public ArgmaxConsumer {
         r = Caps::Any();
         break;
       }
-      Caps o = inst_->get_out_caps(cfg);
+      // staged: the incoming tensors are the stage's RGBA frames; the media caps
+      // follow from the model output the stage was prepared for
+      Caps o = inst_->get_out_caps(stage_ ? stage_in_ : cfg);
       if (o.is_empty()) continue;
       r.append(o);
       if (o.is_any()) break;
@@ -166,6 +206,21 @@ class TensorDecoder : public BaseTransform, public ArgmaxConsumer {
     } else {
       mems = in->mems;
     }
+    if (stage_) {
+      // the upstream filter ran this decoder's device stage: [4:W:H:B] RGBA
+      // frames, one output buffer per frame (views, no copy)
+      const TensorInfo& ti = cfg.info.at(0);
+      const unsigned n = std::max<uint32_t>(1, ti.dim[3]);
+      const size_t fsize = static_cast<size_t>(ti.dim[0]) * ti.dim[1] * ti.dim[2];
+      if (mems.size() != 1 || mems[0]->size() != fsize * n) {
+        post_error("tensor_decoder: staged input does not match the stage's output");
+        return FlowReturn::ERROR;
+      }
+      auto out = make_buffer();
+      out->copy_metadata_from(*in);
+      for (unsigned f = 0; f < n; ++f) out->mems.push_back(Memory::view(mems[0], f * fsize, fsize));
+      return push_frames(in, out, n, outbuf);
+    }
     InvokeContext ctx;
     ctx.device = inst_->supports_device() ? resolve_device(device_, *in) : -1;
     ctx.stream = ctx.device >= 0 ? streams_.get(ctx.device) : nullptr;
@@ -180,9 +235,13 @@ class TensorDecoder : public BaseTransform, public ArgmaxConsumer {
     }
     if (ctx.device >= 0)
       for (auto& m : mems) m->record_use(ctx.stream, ctx.device);
-    if (ctx.out_frames > 1 && out->n_memory() == ctx.out_frames) {
+    return push_frames(in, out, ctx.out_frames, outbuf);
+  }
+
+  FlowReturn push_frames(const BufferPtr& in, const BufferPtr& out, unsigned frames, BufferPtr* outbuf) {
+    if (frames > 1 && out->n_memory() == frames) {
       // batched input: one output buffer per frame, timestamps spread over the batch duration
-      const unsigned n = ctx.out_frames;
+      const unsigned n = frames;
       const int64_t step = in->duration > 0 ? in->duration / n : 0;
       for (unsigned f = 0; f < n; ++f) {
         auto fb = make_buffer();
@@ -207,6 +266,9 @@ class TensorDecoder : public BaseTransform, public ArgmaxConsumer {
   int device_ = -2;
   std::unique_ptr<DecoderInstance> inst_;
   std::string argmax_by_;
+  std::shared_ptr<DecodeStage> stage_;  // run upstream by stage_by_ (take_stage)
+  TensorsConfig stage_in_;              // the model output the stage was prepared for
+  std::string stage_by_;
   TensorsConfig config_;
   StreamSet streams_;
 };

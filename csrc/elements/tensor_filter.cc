@@ -375,6 +375,53 @@ class TensorFilter : public BaseTransform, public TransformAbsorber {
       mout->at(0).dim[0] = 1;
     }
   }
+
+  // ---- decode-stage absorption (runtime/fusion.h DecodeStage) ----
+  // A downstream decoder whose whole device post-processing can run inside this
+  // filter's captured graph (bounding_boxes, image_segment, pose_estimation):
+  // the model outputs never leave the graph, the decoded RGBA frames do.
+  void absorb_decoder_stage(TensorsInfo* mout, const TensorsConfig& in) {
+    if (!stage_tried_) {
+      stage_tried_ = true;
+      const int dev = inst_ ? inst_->stage_device() : -1;
+      if (absorb_dec_enabled_ && inst_ && dev >= 0 && !shared_ && !argmax_consumer_ && out_comb_.empty() &&
+          !props_.invoke_dynamic && mout->num_tensors > 0 && mout->valid()) {
+        Pad* sp = src_pad();
+        Element* dn = sp && sp->peer() ? sp->peer()->parent() : nullptr;
+        while (dn && dn->factory() == "queue") {
+          Pad* q = dn->src_pad();
+          dn = q && q->peer() ? q->peer()->parent() : nullptr;
+        }
+        if (auto* c = dynamic_cast<DecodeStageConsumer*>(dn)) {
+          TensorsConfig mc;
+          mc.info = *mout;
+          mc.info.format = Format::STATIC;
+          mc.rate_n = in.rate_n;
+          mc.rate_d = in.rate_d;
+          if (auto st = c->take_stage(mc, dev, name())) {
+            if (inst_->set_output_stage(st)) {
+              stage_consumer_ = c;
+              stage_ = st;
+              absorbed_decoder_ = dn->name();
+              NNSX_LOGI(name(), "runs the device post-processing of ", absorbed_decoder_, " inside its graph");
+            } else {
+              c->drop_stage();
+            }
+          }
+        }
+      }
+    }
+    if (stage_) *mout = stage_->out_info();
+  }
+  void release_decoder_stage() {
+    if (stage_consumer_) {
+      if (inst_) inst_->set_output_stage(nullptr);
+      stage_consumer_->drop_stage();
+    }
+    stage_consumer_ = nullptr;
+    stage_.reset();
+    stage_tried_ = false;
+  }
   void release_decoder_argmax() {
     if (argmax_consumer_) {
       argmax_consumer_->drop_argmax();
@@ -406,6 +453,7 @@ class TensorFilter : public BaseTransform, public TransformAbsorber {
     }
     if (out_comb_.empty()) {
       absorb_decoder_argmax(&mout);
+      absorb_decoder_stage(&mout, in);
       *out = mout;
       return true;
     }
@@ -834,6 +882,7 @@ class TensorFilter : public BaseTransform, public TransformAbsorber {
     poll_device_stats(true);
     detach_absorbable();
     release_decoder_argmax();
+    release_decoder_stage();
     return true;
   }
   void release_timing_events() {
@@ -864,6 +913,9 @@ class TensorFilter : public BaseTransform, public TransformAbsorber {
   bool absorb_dec_enabled_ = true;
   bool argmax_tried_ = false;
   ArgmaxConsumer* argmax_consumer_ = nullptr;
+  bool stage_tried_ = false;
+  DecodeStageConsumer* stage_consumer_ = nullptr;
+  std::shared_ptr<DecodeStage> stage_;
   std::string absorbed_decoder_;
   AbsorbableElement* absorbable_up_ = nullptr;
   std::string absorbed_from_;

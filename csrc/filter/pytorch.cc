@@ -32,6 +32,7 @@
 #include "filter/filter.h"
 #include "filter/torch_util.h"
 #include "kernels/kernels.h"
+#include "runtime/fusion.h"
 #include "runtime/hip_util.h"
 #include "runtime/plugin_api.h"
 
@@ -158,6 +159,18 @@ class TorchInstance : public FilterInstance {
     if (index != 0) return false;
     std::lock_guard<std::mutex> lk(mu_);
     argmax_out_ = on ? 0 : -1;
+    clear_graphs();
+    return true;
+  }
+
+  // a downstream decoder's device post-processing, appended to the forward
+  // (inside the captured graph): the stage's outputs replace the model's
+  // (runtime/fusion.h DecodeStage)
+  int stage_device() const override { return device_; }
+  bool set_output_stage(std::shared_ptr<DecodeStage> stage) override {
+    if (device_ < 0) return false;
+    std::lock_guard<std::mutex> lk(mu_);
+    stage_ = std::move(stage);
     clear_graphs();
     return true;
   }
@@ -350,6 +363,30 @@ class TorchInstance : public FilterInstance {
     (*outs)[static_cast<size_t>(argmax_out_)] = idx;
   }
 
+  // outs (model outputs on the device) -> the decode stage's outputs, enqueued
+  // on s (the capture stream while capturing: kernels and memsets only)
+  void apply_stage(std::vector<at::Tensor>* outs, hipStream_t s) {
+    if (!stage_) return;
+    const TensorsInfo& oi = stage_->out_info();
+    std::vector<const void*> in;
+    std::vector<at::Tensor> keep;
+    for (auto& t : *outs) {
+      at::Tensor c = t.contiguous();
+      keep.push_back(c);
+      in.push_back(c.data_ptr());
+    }
+    std::vector<at::Tensor> res;
+    std::vector<void*> optr;
+    for (unsigned k = 0; k < oi.num_tensors; ++k) {
+      at::Tensor o = at::empty(torch_sizes(oi.at(k), 0),
+                               keep.empty() ? at::TensorOptions() : keep[0].options().dtype(to_torch(oi.at(k).type)));
+      optr.push_back(o.data_ptr());
+      res.push_back(o);
+    }
+    if (!stage_->enqueue(in, optr, s)) throw Error("pytorch: the decoder stage rejected the model outputs");
+    *outs = std::move(res);
+  }
+
   at::Tensor prepare(at::Tensor t) {
     if (compute_dtype_ != DType::END && at::isFloatingType(t.scalar_type())) t = t.to(to_torch(compute_dtype_));
     if (channels_last_ && t.dim() == 4) t = t.contiguous(at::MemoryFormat::ChannelsLast);
@@ -471,6 +508,7 @@ class TorchInstance : public FilterInstance {
       for (auto& t : inputs) iv.push_back(prepare(t));
       flatten(module_.forward(iv), &outs);
       apply_argmax(&outs, s);
+      apply_stage(&outs, s);
     }
     for (auto& m : in)
       if (dev_idx >= 0) m->record_use(s, dev_idx);
@@ -609,6 +647,7 @@ class TorchInstance : public FilterInstance {
       for (auto& t : src) iv.push_back(prepare(t));
       flatten(module_.forward(iv), &gs->static_out);
       apply_argmax(&gs->static_out, cap_stream_);
+      apply_stage(&gs->static_out, cap_stream_);
       gs->graph->capture_end();
       size_t out_bytes = 0;
       for (auto& t : gs->static_out) out_bytes += t.numel() * t.element_size();
@@ -644,6 +683,7 @@ class TorchInstance : public FilterInstance {
   DType compute_dtype_ = DType::END;
   std::mutex mu_;
   int argmax_out_ = -1;        // output replaced by its argmax (absorbed decoder), -1: none
+  std::shared_ptr<DecodeStage> stage_;  // absorbed decoder's device stage (runtime/fusion.h)
   // the absorbed argmax's indices are copied to pinned host memory after each
   // graph replay (NNSX_TORCH_HOST_ARGMAX=0: a device clone, read back by the
   // decoder).  Batch 1 at a live 500 fps camera: p50 308 vs 362-366 us, filter

@@ -15,6 +15,7 @@
 // input types) keeps running in the transform's own kernel.
 #pragma once
 
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -61,6 +62,35 @@ class ArgmaxConsumer {  // implemented by tensor_decoder
   // scores -> int32 [1:B]); true = accepted (the decoder now expects them)
   virtual bool take_argmax(unsigned tensor, uint32_t classes, const std::string& by) = 0;
   virtual void drop_argmax() = 0;
+};
+
+// Downstream, generalised: the WHOLE device post-processing of a decoder
+// (bounding_boxes: candidates + sort + NMS + raster; image_segment: resize +
+// argmax + colour map; pose_estimation: heatmap argmax + skeleton raster) as
+// one capturable stage that the filter appends to its captured forward, so
+// model outputs -> decoded RGBA frames is one hipGraph replay and only the
+// frames leave it.  The decoder prepares the stage at caps negotiation
+// (scratch, uploaded tables: all allocated up front, so the captured kernels
+// keep valid pointers across replays); the filter allocates the outputs per
+// graph instance and calls enqueue() while capturing (kernels and memsets
+// only).  The decoder then receives the stage outputs and only slices them
+// into per-frame media buffers.
+class DecodeStage {
+ public:
+  virtual ~DecodeStage() = default;
+  virtual const TensorsInfo& out_info() const = 0;  // the tensors enqueue() writes
+  // in = device pointers of the model outputs (the decoder's normal input),
+  // out = device buffers sized by out_info(); capturable work on s only
+  virtual bool enqueue(const std::vector<const void*>& in, const std::vector<void*>& out, void* stream) = 0;
+};
+
+class DecodeStageConsumer {  // implemented by tensor_decoder
+ public:
+  virtual ~DecodeStageConsumer() = default;
+  // the producer's outputs (`model_out`, on GPU `dev`) would go through the
+  // decoder's device stage upstream; nullptr = the decoder has none / declines
+  virtual std::shared_ptr<DecodeStage> take_stage(const TensorsConfig& model_out, int dev, const std::string& by) = 0;
+  virtual void drop_stage() = 0;
 };
 
 // The transform's output for every uint8 value 0..255 (out must be FLOAT32):

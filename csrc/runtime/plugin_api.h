@@ -30,6 +30,8 @@ namespace nnsx {
 
 enum class Accelerator { NONE, AUTO, CPU, GPU, DEFAULT };
 
+class DecodeStage;  // runtime/fusion.h
+
 struct FilterProperties {
   std::string fwname;
   std::vector<std::string> model_files;
@@ -112,6 +114,15 @@ class FilterInstance {
     (void)on;
     return false;
   }
+  // Downstream decode-stage absorption (runtime/fusion.h DecodeStage): the
+  // framework runs `stage` after its forward (inside its captured graph) and
+  // hands out the stage's outputs instead of the model's; nullptr removes it.
+  // stage_device(): the GPU the outputs are produced on (-1: host framework)
+  virtual int stage_device() const { return -1; }
+  virtual bool set_output_stage(std::shared_ptr<DecodeStage> stage) {
+    (void)stage;
+    return false;
+  }
   // Property changes after open (reference V1 events CUSTOM_PROP,
   // SET_INPUT_PROP / SET_OUTPUT_PROP, SET_ACCELERATOR): true = applied.
   virtual bool update_custom(const std::string& custom) {
@@ -187,6 +198,25 @@ class DecoderInstance {
   // argmax over the innermost dimension of tensor 0 may receive the producer's
   // int32 indices [1:B] instead of the scores [classes:B].  true = from now on
   // decode() takes indices.
+  // Device stage (runtime/fusion.h): the decoder's device post-processing of
+  // inputs shaped `in` as one capturable enqueue on GPU `dev`.  prepare
+  // allocates every buffer the enqueue touches and uploads tables (it may
+  // synchronize) and reports the stage's output tensors; enqueue then only
+  // launches kernels / memsets on `s`.  Decoders whose stage writes RGBA frames
+  // report one uint8 [4:W:H:B] tensor, which the element slices per frame.
+  virtual bool stage_prepare(const TensorsConfig& in, int dev, hipStream_t s, TensorsInfo* out) {
+    (void)in;
+    (void)dev;
+    (void)s;
+    (void)out;
+    return false;
+  }
+  virtual bool stage_enqueue(const std::vector<const void*>& in, const std::vector<void*>& out, hipStream_t s) {
+    (void)in;
+    (void)out;
+    (void)s;
+    return false;
+  }
   virtual bool accept_argmax_input(uint32_t classes) {
     (void)classes;
     return false;

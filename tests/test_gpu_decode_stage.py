@@ -1,0 +1,71 @@
+"""Decoder device stages inside the filter's hipGraph (runtime/fusion.h
+DecodeStage): `tensor_filter ! [queue !] tensor_decoder mode=bounding_boxes |
+image_segment | pose_estimation` -- the filter appends the decoder's whole device
+post-processing (SSD candidates + sort + NMS + raster; DeepLab resize + argmax
++ colour map; PoseNet heatmap argmax + skeleton raster) to its captured
+forward and hands out the RGBA frames.  The frames must equal, byte for byte,
+the same pipeline with the decoder running its own kernels (absorb-decoder=
+false); reference decode paths: tensordec-boundingbox.c:1543-1777,
+tensordec-imagesegment.c:328-392, tensordec-pose.c:542-818."""
+import os
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _files(workdir):
+    from nnstreamer_amd.models.posenet import write_pose_labels
+    from nnstreamer_amd.models.ssd import write_box_priors, write_coco_labels
+
+    return dict(coco=write_coco_labels(os.path.join(workdir, "coco_st.txt")),
+                priors=write_box_priors(os.path.join(workdir, "priors_st.txt")),
+                pose=write_pose_labels(os.path.join(workdir, "pose17_st.txt")))
+
+
+CASES = {
+    "ssd": (300, "ssd_fused_fp32", "typecast:float32,add:-127.5,div:127.5",
+            "tensor_decoder name=dec mode=bounding_boxes option1=mobilenet-ssd option2={coco} option3={priors} "
+            "option4=300:300 option5=300:300"),
+    "deeplab": (513, "deeplab_fused_lowres_fp32", "typecast:float32,div:255.0",
+                "tensor_decoder name=dec mode=image_segment option1=tflite-deeplab option3=513:513"),
+    "posenet": (257, "posenet_fused_fp32", "typecast:float32,add:-127.5,div:127.5",
+                "tensor_decoder name=dec mode=pose_estimation option1=640:480 option2=257:257 option3={pose} "
+                "option4=heatmap-offset"),
+}
+
+
+def _run(nns, workdir, case, B, absorb, graph, queue):
+    from nnstreamer_amd.models.export import export
+
+    S, model_name, norm, dec = CASES[case]
+    model = export(model_name, os.path.join(workdir, f"{model_name}_st.pt"), layout="nhwc")
+    q = "queue max-size-buffers=2 ! " if queue else ""
+    desc = (f"videotestsrc num-buffers={3 * B} pattern=snow pool-size={3 * B} "
+            f"! video/x-raw,format=RGB,width={S},height={S},framerate=30/1 "
+            f"! tensor_converter frames-per-tensor={B} device=0 ! tensor_transform mode=arithmetic option={norm} "
+            f"! tensor_filter name=f framework=pytorch model={model} input=3:{S}:{S}:{B} inputtype=float32 "
+            f"accelerator=true:gpu device=0 custom=hipgraph:{'true' if graph else 'false'} "
+            f"absorb-decoder={'true' if absorb else 'false'} ! {q}{dec.format(**_files(workdir))} "
+            "! tensor_sink name=sink")
+    p = nns.parse_launch(desc)
+    out = []
+    p.get_by_name("sink").connect("new-data", lambda b: out.append(bytes(b.memory(0).bytes())))
+    p.run(timeout=300)
+    info = (p.get_by_name("f").get_property("absorbed-decoder"), p.get_by_name("dec").get_property("stage-by"))
+    p.stop()
+    return out, info
+
+
+@pytest.mark.parametrize("case,B,graph,queue", [("ssd", 4, True, True), ("ssd", 1, True, False),
+                                                ("deeplab", 2, True, True), ("posenet", 4, True, True),
+                                                ("posenet", 2, False, True)])
+def test_decoder_stage_in_graph_matches_own_kernels(nns, workdir, case, B, graph, queue):
+    got, info = _run(nns, workdir, case, B, True, graph, queue)
+    ref, info_ref = _run(nns, workdir, case, B, False, graph, queue)
+    assert info == ("dec", "f"), info
+    assert info_ref == ("", ""), info_ref
+    assert len(got) == len(ref) == 3 * B
+    assert got == ref
+    if case != "ssd":  # (random-init SSD may detect nothing)
+        assert any(any(x) for x in got[:4])  # something was drawn
