@@ -68,6 +68,25 @@ struct YLayout {
 void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
                  int Kpad, int Npad, int act, hipStream_t s, int tile = 0, float* ws = nullptr,
                  const YLayout& yl = YLayout{});
+// SSDLite prediction heads, all in one launch (heads_f32.hip): per head y =
+// pw(relu6(dw3x3(x) + bd)) + bias written into rows of a concatenated output.
+struct SepHead {
+  const float* x = nullptr;     // [B][H][W][K] feature map (f32 NHWC)
+  const float* wd = nullptr;    // [9][K] depthwise weights (BN folded)
+  const float* bd = nullptr;    // [K]
+  const float* wt = nullptr;    // [Npad][Kpad] predictor weights
+  const float* bias = nullptr;  // [>= N rounded to 4]
+  float* out = nullptr;         // this head's first row in image 0 of the [B][T][C] output
+  int64_t bstride = 0;          // floats between images in the output (T * C)
+  int B = 0, H = 0, W = 0, K = 0, Kpad = 0, N = 0, Npad = 0;  // N: outputs per pixel (anchors x C)
+  int tiles = 0;                // (set by sep_heads_f32)
+};
+constexpr int kSepHeadsMax = 16;
+struct SepHeadsArgs {
+  int n = 0;
+  SepHead h[kSepHeadsMax];
+};
+void sep_heads_f32(SepHeadsArgs a, hipStream_t s);
 // split-K workspace the GEMM wants for this shape (0: no split; without it the
 // GEMM runs unsplit)
 size_t pw_gemm_f32_workspace_bytes(int M, int N, int Kpad, bool has_res, int tile = 0);

@@ -126,6 +126,72 @@ void pw_conv_into_cpu(const at::Tensor& x, const at::Tensor& wt, const at::Tenso
   out.slice(1, row0, row0 + y.size(1)).copy_(y);
 }
 
+at::Tensor dw_conv_cpu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int64_t stride, int64_t act,
+                       int64_t dilation);
+
+// All SSDLite heads in one launch (kernels::sep_heads_f32): head i reads
+// feature xs[i] through its depthwise (wds[i], bds[i]) and predictor (wts[i],
+// biases[i], ns[i] outputs per pixel) into out_box (which[i] == 0) or out_cls
+// (1), its rows following the previous head's of the same output.
+void sep_heads_cuda(at::TensorList xs, at::TensorList wds, at::TensorList bds, at::TensorList wts,
+                    at::TensorList biases, at::IntArrayRef ns, at::IntArrayRef which, at::Tensor& out_box,
+                    at::Tensor& out_cls) {
+  const size_t n = xs.size();
+  TORCH_CHECK(n > 0 && n <= static_cast<size_t>(nnsx::kernels::kSepHeadsMax) && wds.size() == n && bds.size() == n &&
+                  wts.size() == n && biases.size() == n && ns.size() == n && which.size() == n,
+              "sep_heads: 1..16 heads, one entry of every list per head");
+  nnsx::kernels::SepHeadsArgs a;
+  a.n = static_cast<int>(n);
+  int64_t rows[2] = {0, 0};
+  for (size_t i = 0; i < n; ++i) {
+    const at::Tensor& x = xs[i];
+    at::Tensor& o = which[i] ? out_cls : out_box;
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 4,
+                "sep_heads: x [B,H,W,K] f32 contiguous");
+    TORCH_CHECK(o.is_cuda() && o.scalar_type() == at::kFloat && o.is_contiguous() && o.dim() == 3 && o.size(0) == x.size(0),
+                "sep_heads: outputs [B,T,C] f32");
+    const int64_t K = x.size(3), C = o.size(2), N = ns[i];
+    TORCH_CHECK(N % C == 0 && wds[i].numel() == 9 * K && bds[i].numel() >= K && wts[i].dim() == 2 &&
+                    wts[i].size(1) >= K && wts[i].size(0) >= (N + 3) / 4 * 4 && biases[i].numel() >= (N + 3) / 4 * 4,
+                "sep_heads: weights");
+    const int64_t HW = x.size(1) * x.size(2);
+    const int64_t r0 = rows[which[i] ? 1 : 0];
+    TORCH_CHECK(r0 + HW * (N / C) <= o.size(1), "sep_heads: output rows");
+    auto& h = a.h[i];
+    h.x = x.data_ptr<float>();
+    h.wd = wds[i].data_ptr<float>();
+    h.bd = bds[i].data_ptr<float>();
+    h.wt = wts[i].data_ptr<float>();
+    h.bias = biases[i].data_ptr<float>();
+    h.out = o.data_ptr<float>() + r0 * C;
+    h.bstride = o.size(1) * C;
+    h.B = static_cast<int>(x.size(0));
+    h.H = static_cast<int>(x.size(1));
+    h.W = static_cast<int>(x.size(2));
+    h.K = static_cast<int>(K);
+    h.Kpad = static_cast<int>(wts[i].size(1));
+    h.N = static_cast<int>(N);
+    h.Npad = static_cast<int>(wts[i].size(0));
+    rows[which[i] ? 1 : 0] = r0 + HW * (N / C);
+  }
+  nnsx::kernels::sep_heads_f32(a, cur_stream());
+}
+
+void sep_heads_cpu(at::TensorList xs, at::TensorList wds, at::TensorList bds, at::TensorList wts, at::TensorList biases,
+                   at::IntArrayRef ns, at::IntArrayRef which, at::Tensor& out_box, at::Tensor& out_cls) {
+  int64_t rows[2] = {0, 0};
+  for (size_t i = 0; i < xs.size(); ++i) {
+    at::Tensor& o = which[i] ? out_cls : out_box;
+    at::Tensor h = dw_conv_cpu(xs[i], wds[i], bds[i], 1, 1, 1);
+    const int64_t N = ns[i], B = h.size(0), C = o.size(2);
+    at::Tensor y = pw_conv_cpu(h, wts[i], biases[i], c10::nullopt, (N + 3) / 4 * 4, 0, true).slice(-1, 0, N);
+    y = y.reshape({B, -1, C});
+    const int64_t r0 = rows[which[i] ? 1 : 0];
+    o.slice(1, r0, r0 + y.size(1)).copy_(y);
+    rows[which[i] ? 1 : 0] = r0 + y.size(1);
+  }
+}
+
 // pw_conv with a per-image bias: bias [B, N] (row b of it for every pixel of
 // image b).  project(cat[a, p]) with p constant over space (DeepLab's image
 // pooling branch) is W_a . a + (W_p . p + b): one GEMM on a, no concat.
@@ -524,6 +590,8 @@ TORCH_LIBRARY(nnsx, m) {
   m.def("pw_conv_into(Tensor x, Tensor wt, Tensor bias, Tensor(a!) out, int row0, int n, int act) -> ()");
   m.def("pw_conv_rowbias(Tensor x, Tensor wt, Tensor bias, int N, int act) -> Tensor");
   m.def("upsample_bilinear(Tensor x, int H, int W) -> Tensor");
+  m.def("sep_heads(Tensor[] xs, Tensor[] wds, Tensor[] bds, Tensor[] wts, Tensor[] biases, int[] ns, int[] which, "
+        "Tensor(a!) out_box, Tensor(b!) out_cls) -> ()");
   m.def("dw_conv(Tensor x, Tensor w, Tensor bias, int stride, int act, int dilation=1) -> Tensor");
   m.def("stem_conv(Tensor x, Tensor w, Tensor bias, int act, bool out_f32=False) -> Tensor");
   m.def("stem_conv_u8(Tensor x, Tensor w, Tensor bias, int act, Tensor lut, bool out_f32=False) -> Tensor");
@@ -546,6 +614,7 @@ TORCH_LIBRARY_IMPL(nnsx, CUDA, m) {
   m.impl("pw_conv_into", pw_conv_into_cuda);
   m.impl("pw_conv_rowbias", pw_conv_rowbias_cuda);
   m.impl("upsample_bilinear", upsample_bilinear_cuda);
+  m.impl("sep_heads", sep_heads_cuda);
   m.impl("dw_conv", dw_conv_cuda);
   m.impl("stem_conv", stem_conv_cuda);
   m.impl("stem_conv_u8", stem_conv_u8_cuda);
@@ -562,6 +631,7 @@ TORCH_LIBRARY_IMPL(nnsx, CPU, m) {
   m.impl("pw_conv_into", pw_conv_into_cpu);
   m.impl("pw_conv_rowbias", pw_conv_rowbias_cpu);
   m.impl("upsample_bilinear", upsample_bilinear_cpu);
+  m.impl("sep_heads", sep_heads_cpu);
   m.impl("dw_conv", dw_conv_cpu);
   m.impl("stem_conv", stem_conv_cpu);
   m.impl("stem_conv_u8", stem_conv_u8_cpu);

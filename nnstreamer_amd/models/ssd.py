@@ -184,6 +184,11 @@ class FusedSSDLite(nn.Module):
         self.box_heads = nn.ModuleList([FusedSepHead(h, 4, precision) for h in m.box_heads])
         self.cls_heads = nn.ModuleList([FusedSepHead(h, m.num_classes, precision) for h in m.cls_heads])
         self.feat_block = 13  # blocks[13] == features[14]: its expansion output is SSD feature 1
+        # fp32: all 12 heads (depthwise + predictor, box and class, 6 maps) in one
+        # grouped launch (nnsx::sep_heads); NNSX_SSD_SEP_HEADS=0 keeps 2 launches per head
+        import os
+
+        self.one_launch_heads = self.f32 and os.environ.get("NNSX_SSD_SEP_HEADS", "1") != "0"
         return self
 
     def forward(self, x: torch.Tensor):
@@ -207,6 +212,33 @@ class FusedSSDLite(nn.Module):
                 rows += feats[i].shape[1] * feats[i].shape[2] * (bh.n // bh.k)
             bo = torch.empty((x.shape[0], rows, 4), dtype=torch.float32, device=x.device)
             lo = torch.empty((x.shape[0], rows, self.cls_heads[0].k), dtype=torch.float32, device=x.device)
+            if self.one_launch_heads:
+                xs: List[torch.Tensor] = []
+                wds: List[torch.Tensor] = []
+                bds: List[torch.Tensor] = []
+                wts: List[torch.Tensor] = []
+                bs: List[torch.Tensor] = []
+                ns: List[int] = []
+                which: List[int] = []
+                # the large maps first: their tiles start first, the small maps fill the tail
+                for j, hc in enumerate(self.cls_heads):
+                    xs.append(feats[j])
+                    wds.append(hc.dw.w)
+                    bds.append(hc.dw.bias)
+                    wts.append(hc.pw.wt)
+                    bs.append(hc.pw.bias)
+                    ns.append(hc.n)
+                    which.append(1)
+                for j, hb in enumerate(self.box_heads):
+                    xs.append(feats[j])
+                    wds.append(hb.dw.w)
+                    bds.append(hb.dw.bias)
+                    wts.append(hb.pw.wt)
+                    bs.append(hb.pw.bias)
+                    ns.append(hb.n)
+                    which.append(0)
+                torch.ops.nnsx.sep_heads(xs, wds, bds, wts, bs, ns, which, bo, lo)
+                return bo.reshape(bo.shape[0], bo.shape[1], 1, 4), lo
             r = 0
             for i, bh in enumerate(self.box_heads):
                 r = bh.into(feats[i], bo, r)

@@ -115,3 +115,40 @@ def test_avgpool_f32(B, HW, C):
     p = torch.ops.nnsx.avgpool(x)
     assert _rel(p.cpu(), x.double().cpu().mean((1, 2))) < 1e-6
     assert torch.equal(p, torch.ops.nnsx.avgpool(x))  # deterministic
+
+
+@pytest.mark.parametrize("B", [1, 3, 64])
+def test_sep_heads_one_launch_vs_fp64(B):
+    """All 12 SSDLite heads (depthwise 3x3 + ReLU6 + predictor, box and class, 6
+    maps) in one grouped launch (kernels/heads_f32.hip) against an fp64 oracle
+    of each head, rows of the concatenated outputs included; B = 64 is the
+    benched batch (tiles spanning images at the 3x3 .. 1x1 maps)."""
+    import torch.nn.functional as F
+
+    m = ssd.fused_ssd_mobilenet(seed=3, precision="fp32").cuda()
+    g = torch.Generator().manual_seed(5)
+    shapes = [(19, 576), (10, 1280), (5, 512), (3, 256), (2, 256), (1, 128)]
+    feats = [(torch.rand(B, s, s, c, generator=g) * 3).cuda() for s, c in shapes]
+    rows = sum(s * s * (h.n // h.k) for (s, _), h in zip(shapes, m.box_heads))
+    bo = torch.full((B, rows, 4), float("nan"), device="cuda")
+    lo = torch.full((B, rows, 91), float("nan"), device="cuda")
+    heads = list(m.cls_heads) + list(m.box_heads)
+    torch.ops.nnsx.sep_heads(feats + feats, [h.dw.w for h in heads], [h.dw.bias for h in heads],
+                             [h.pw.wt for h in heads], [h.pw.bias for h in heads], [h.n for h in heads],
+                             [1] * 6 + [0] * 6, bo, lo)
+
+    def ref(x, h):
+        C = x.shape[-1]
+        wd = h.dw.w.double().cpu().t().reshape(C, 1, 3, 3)
+        d = F.conv2d(x.double().cpu().permute(0, 3, 1, 2), wd, h.dw.bias.double().cpu(), padding=1,
+                     groups=C).clamp(0, 6)
+        w = h.pw.wt.double().cpu()[: h.n, :C]
+        y = torch.einsum("bchw,nc->bhwn", d, w) + h.pw.bias.double().cpu()[: h.n]
+        return y.reshape(x.shape[0], -1, h.k)
+
+    for out, hs in ((lo, m.cls_heads), (bo, m.box_heads)):
+        want = torch.cat([ref(x, h) for x, h in zip(feats, hs)], 1)
+        got = out.double().cpu()
+        assert not torch.isnan(got).any()
+        err = ((got - want).abs() / (want.abs() + 1)).max().item()
+        assert err < 2e-5, err
