@@ -77,9 +77,13 @@ struct SepHead {
   const float* wt = nullptr;    // [Npad][Kpad] predictor weights
   const float* bias = nullptr;  // [>= N rounded to 4]
   float* out = nullptr;         // this head's first row in image 0 of the [B][T][C] output
-  int64_t bstride = 0;          // floats between images in the output (T * C)
+  int64_t bstride = 0;          // floats between images in the output (T * C; NHWC: Ho * Wo * N)
   int B = 0, H = 0, W = 0, K = 0, Kpad = 0, N = 0, Npad = 0;  // N: outputs per pixel (anchors x C)
-  int tiles = 0;                // (set by sep_heads_f32)
+  int stride = 1;               // depthwise stride (padding 1); wd == nullptr: no depthwise (plain 1x1)
+  int act = 0;                  // 1: ReLU6 on the output
+  int Ho = 0, Wo = 0;           // output map (0: from H, W, stride)
+  int ldo = 0;                  // floats between output pixels (0: N)
+  int tiles = 0;                // (set by the launcher)
 };
 constexpr int kSepHeadsMax = 16;
 struct SepHeadsArgs {
@@ -87,6 +91,9 @@ struct SepHeadsArgs {
   SepHead h[kSepHeadsMax];
 };
 void sep_heads_f32(SepHeadsArgs a, hipStream_t s);
+// the general form (dwpw_f32.hip): depthwise (stride 1|2, optional) + pointwise
+// (+ ReLU6) problems, one grouped launch
+void dwpw_f32(SepHeadsArgs a, hipStream_t s);
 // split-K workspace the GEMM wants for this shape (0: no split; without it the
 // GEMM runs unsplit)
 size_t pw_gemm_f32_workspace_bytes(int M, int N, int Kpad, bool has_res, int tile = 0);

@@ -176,85 +176,113 @@ __constant__ int kDotY[40] = {0,  -4, 0,  4,  -1, 0,  1,  -2, -1, 0,  1,  2,  -3
                               -2, -1, 1,  2,  3,  -3, -2, -1, 0,  1,  2,  3,  -2, -1, 0,  1,  2,  -1, 0,  1};
 __constant__ uint8_t kFontPose[95][13] = NNSX_FONT8X13_DATA;
 
-__global__ void __launch_bounds__(256) pose_draw_kernel(PoseDrawArgs a) {
-  __shared__ int px[64], py[64];
-  __shared__ int valid[64];
-  const int b = blockIdx.x;
+// keypoint k of frame b: raster position and validity, exactly as the host
+// path refines it (tensordec-pose.c:760-800)
+__device__ inline void pose_point(const PoseDrawArgs& a, int b, int k, int* px, int* py, bool* valid) {
   const int K = a.keypoints;
+  const float* o = a.kp + (static_cast<uint64_t>(b) * K + k) * 3;
+  const int mx = static_cast<int>(o[0]), my = static_cast<int>(o[1]);
+  int x, y;
+  if (a.offsets) {
+    const uint64_t oi = static_cast<uint64_t>(b) * a.gw * a.gh * 2 * K + (static_cast<uint64_t>(my) * a.gw + mx) * K * 2 + k;
+    const float offy = a.offsets[oi], offx = a.offsets[oi + K];
+    const float fx = (static_cast<float>(mx) / (a.gw - 1)) * a.i_w + offx;
+    const float fy = (static_cast<float>(my) / (a.gh - 1)) * a.i_h + offy;
+    x = static_cast<int>(fx * a.W / a.i_w);
+    y = static_cast<int>(fy * a.H / a.i_h);
+  } else {
+    x = static_cast<int>((static_cast<unsigned>(mx) * a.W) / a.i_w);
+    y = static_cast<int>((static_cast<unsigned>(my) * a.H) / a.i_h);
+  }
+  *px = static_cast<int>(min(static_cast<unsigned>(a.W), static_cast<unsigned>(max(0, x))));
+  *py = static_cast<int>(min(static_cast<unsigned>(a.H), static_cast<unsigned>(max(0, y))));
+  *valid = o[2] >= 0.5f;
+}
+
+// Skeleton, one wave per connection (grid: frames x edge groups of 4): the
+// end dots by 40 lanes each, the Bresenham line by one lane.  Every pixel gets
+// the same value, so the edges of a frame need no order among themselves.
+__global__ void __launch_bounds__(256) pose_lines_kernel(PoseDrawArgs a) {
+  const int b = blockIdx.x;
+  const int e = blockIdx.y * 4 + static_cast<int>(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (e >= a.n_edges) return;
   uint32_t* f = a.frames + static_cast<uint64_t>(b) * a.W * a.H;
-  for (int k = threadIdx.x; k < K; k += blockDim.x) {
-    const float* o = a.kp + (static_cast<uint64_t>(b) * K + k) * 3;
-    const int mx = static_cast<int>(o[0]), my = static_cast<int>(o[1]);
-    int x, y;
-    if (a.offsets) {
-      const uint64_t oi = static_cast<uint64_t>(b) * a.gw * a.gh * 2 * K + (static_cast<uint64_t>(my) * a.gw + mx) * K * 2 + k;
-      const float offy = a.offsets[oi], offx = a.offsets[oi + K];
-      const float fx = (static_cast<float>(mx) / (a.gw - 1)) * a.i_w + offx;
-      const float fy = (static_cast<float>(my) / (a.gh - 1)) * a.i_h + offy;
-      x = static_cast<int>(fx * a.W / a.i_w);
-      y = static_cast<int>(fy * a.H / a.i_h);
-    } else {
-      x = static_cast<int>((static_cast<unsigned>(mx) * a.W) / a.i_w);
-      y = static_cast<int>((static_cast<unsigned>(my) * a.H) / a.i_h);
-    }
-    x = static_cast<int>(min(static_cast<unsigned>(a.W), static_cast<unsigned>(max(0, x))));
-    y = static_cast<int>(min(static_cast<unsigned>(a.H), static_cast<unsigned>(max(0, y))));
-    px[k] = x;
-    py[k] = y;
-    valid[k] = o[2] >= 0.5f;
+  const int i = a.edges[2 * e], k = a.edges[2 * e + 1];
+  int xi, yi, xk, yk;
+  bool vi, vk;
+  pose_point(a, b, i, &xi, &yi, &vi);
+  pose_point(a, b, k, &xk, &yk, &vk);
+  if (!vi || !vk) return;
+  int xs = xi, ys = yi, xe = xk, ye = yk;
+  if (xs > xe) {
+    int t = xs; xs = xe; xe = t;
+    t = ys; ys = ye; ye = t;
   }
-  __syncthreads();
-  // connections (i -> k, k > i): one per lane
-  for (int e = threadIdx.x; e < a.n_edges; e += blockDim.x) {
-    const int i = a.edges[2 * e], k = a.edges[2 * e + 1];
-    if (!valid[i] || !valid[k]) continue;
-    int xs = px[i], ys = py[i], xe = px[k], ye = py[k];
-    if (xs > xe) {
-      int t = xs; xs = xe; xe = t;
-      t = ys; ys = ye; ye = t;
+  if (lane < 40) {
+    int yy = ys + kDotY[lane], xx = xs + kDotX[lane];
+    if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) f[yy * a.W + xx] = 0xFFFFFFFFu;
+    yy = ye + kDotY[lane];
+    xx = xe + kDotX[lane];
+    if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) f[yy * a.W + xx] = 0xFFFFFFFFu;
+  }
+  if (lane != 0) return;
+  const int dx = abs(xe - xs), sx = xs < xe ? 1 : -1;
+  const int dy = abs(ye - ys), sy = ys < ye ? 1 : -1;
+  int err = (dx > dy ? dx : -dy) / 2;
+  while (true) {
+    pose_setpixel(f, a.W, a.H, xs, ys);
+    if (xs == xe && ys == ye) break;
+    const int e2 = err;
+    if (e2 > -dx) {
+      err -= dy;
+      xs += sx;
     }
-    for (int d = 0; d < 40; ++d) {
-      int yy = ys + kDotY[d], xx = xs + kDotX[d];
-      if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) f[yy * a.W + xx] = 0xFFFFFFFFu;
-      yy = ye + kDotY[d];
-      xx = xe + kDotX[d];
-      if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) f[yy * a.W + xx] = 0xFFFFFFFFu;
-    }
-    const int dx = abs(xe - xs), sx = xs < xe ? 1 : -1;
-    const int dy = abs(ye - ys), sy = ys < ye ? 1 : -1;
-    int err = (dx > dy ? dx : -dy) / 2;
-    while (true) {
-      pose_setpixel(f, a.W, a.H, xs, ys);
-      if (xs == xe && ys == ye) break;
-      const int e2 = err;
-      if (e2 > -dx) {
-        err -= dy;
-        xs += sx;
-      }
-      if (e2 < dy) {
-        err += dx;
-        ys += sy;
-      }
+    if (e2 < dy) {
+      err += dx;
+      ys += sy;
     }
   }
+}
+
+// Labels, one workgroup per (frame, keypoint), after the skeleton (stream
+// order).  The host draws them in keypoint order, a later label's cells
+// (background zeros included) overwriting an earlier one's: here a pixel of
+// label k is written only if no later valid label covers it, so every label of
+// every frame draws at once and the result is the ordered one.
+__global__ void __launch_bounds__(256) pose_labels_kernel(PoseDrawArgs a) {
+  __shared__ int px[64], py[64], fit[64];
+  __shared__ int valid[64];
+  const int b = blockIdx.x, k = blockIdx.y;
+  const int K = a.keypoints;
+  for (int j = threadIdx.x; j < K; j += blockDim.x) {
+    bool v;
+    pose_point(a, b, j, &px[j], &py[j], &v);
+    valid[j] = v;
+    const char* lab = a.labels + a.label_offs[j];
+    int len = 0;
+    while (lab[len]) ++len;
+    int n = 0;
+    while (n < len && px[j] + 9 * n + 8 <= a.W) ++n;
+    fit[j] = n;
+  }
   __syncthreads();
-  // labels, keypoint order
-  for (int k = 0; k < K; ++k) {
-    if (valid[k]) {
-      const char* lab = a.labels + a.label_offs[k];
-      int len = 0;
-      while (lab[len]) ++len;
-      int fit = 0;
-      while (fit < len && px[k] + 9 * fit + 8 <= a.W) ++fit;
-      const int ly = max(0, py[k] - 14);
-      for (int p = threadIdx.x; p < fit * 13 * 8; p += blockDim.x) {
-        const int ch = p / 104, rem = p % 104, row = rem / 8, col = rem % 8;
-        const int yy = ly + row, xx = px[k] + 9 * ch + col;
-        if (yy < a.H && xx < a.W)
-          f[yy * a.W + xx] = font::cell_on(kFontPose, static_cast<unsigned char>(lab[ch]), row, col) ? 0xFFFFFFFFu : 0u;
-      }
+  if (!valid[k]) return;
+  uint32_t* f = a.frames + static_cast<uint64_t>(b) * a.W * a.H;
+  const char* lab = a.labels + a.label_offs[k];
+  const int ly = max(0, py[k] - 14);
+  for (int p = threadIdx.x; p < fit[k] * 13 * 8; p += blockDim.x) {
+    const int ch = p / 104, rem = p % 104, row = rem / 8, col = rem % 8;
+    const int yy = ly + row, xx = px[k] + 9 * ch + col;
+    if (yy >= a.H || xx >= a.W) continue;
+    bool later = false;
+    for (int j = k + 1; j < K && !later; ++j) {
+      if (!valid[j]) continue;
+      const int jy = max(0, py[j] - 14), dxj = xx - px[j];
+      later = yy >= jy && yy < jy + 13 && dxj >= 0 && dxj < 9 * fit[j] && dxj % 9 < 8;
     }
-    __syncthreads();
+    if (!later)
+      f[yy * a.W + xx] = font::cell_on(kFontPose, static_cast<unsigned char>(lab[ch]), row, col) ? 0xFFFFFFFFu : 0u;
   }
 }
 
@@ -377,7 +405,12 @@ void pose_heatmap_argmax(const float* heat, int keypoints, int grid_w, int grid_
 
 void pose_draw(const PoseDrawArgs& a, int batch, hipStream_t s) {
   if (batch == 0) return;
-  hipLaunchKernelGGL(pose_draw_kernel, dim3(batch), dim3(256), 0, s, a);
+  if (a.keypoints > 64) throw std::invalid_argument("pose_draw: at most 64 keypoints");
+  if (a.n_edges > 0)
+    hipLaunchKernelGGL(pose_lines_kernel, dim3(static_cast<unsigned>(batch), static_cast<unsigned>((a.n_edges + 3) / 4)),
+                       dim3(256), 0, s, a);
+  hipLaunchKernelGGL(pose_labels_kernel, dim3(static_cast<unsigned>(batch), static_cast<unsigned>(a.keypoints)),
+                     dim3(256), 0, s, a);
 }
 
 void segment_upsample_argmax_color(const float* logits, int labels, int h, int w, int batch, int H, int W,

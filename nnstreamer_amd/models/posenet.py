@@ -11,6 +11,8 @@ mode (tensordec-pose.c:40-60, 760-800): heatmaps ``17:9:9:B`` and offsets
 """
 from __future__ import annotations
 
+from typing import List, Optional
+
 import torch
 import torch.nn as nn
 
@@ -110,10 +112,25 @@ class FusedPoseNet(nn.Module):
         self.heat = _padded_pw(m.heatmap, precision)
         self.offs = _padded_pw(m.offsets, precision)
         self.k = int(m.heatmap.out_channels)
+        # fp32: every depthwise + pointwise pair as one GEMM with the depthwise in
+        # its operand staging, and both 1x1 heads in one launch with exact columns
+        # (nnsx::dwpw, kernels/dwpw_f32.hip); NNSX_POSENET_DWPW=0 keeps 2 launches per pair
+        import os
+
+        self.fuse_dwpw = self.f32 and os.environ.get("NNSX_POSENET_DWPW", "1") != "0"
         return self
 
     def forward(self, x: torch.Tensor):
         h = stem(x, self.stem_w, self.stem_b, self.in_lut, self.f32)
+        if self.fuse_dwpw and h.is_cuda:
+            for d, p in zip(self.dws, self.pws):
+                wd: List[Optional[torch.Tensor]] = [d.w]
+                bd: List[Optional[torch.Tensor]] = [d.bias]
+                h = torch.ops.nnsx.dwpw([h], wd, bd, [p.wt], [p.bias], [p.n], [d.stride], 1)[0]
+            nones: List[Optional[torch.Tensor]] = [None, None]
+            o = torch.ops.nnsx.dwpw([h, h], nones, nones, [self.heat.wt, self.offs.wt], [self.heat.bias, self.offs.bias],
+                                    [self.k, 2 * self.k], [1, 1], 0)
+            return o[0], o[1]
         for d, p in zip(self.dws, self.pws):
             h = p(d(h))
         hm = self.heat(h)[..., : self.k].contiguous()

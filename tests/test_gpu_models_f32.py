@@ -152,3 +152,38 @@ def test_sep_heads_one_launch_vs_fp64(B):
         assert not torch.isnan(got).any()
         err = ((got - want).abs() / (want.abs() + 1)).max().item()
         assert err < 2e-5, err
+
+
+@pytest.mark.parametrize("B,H,K,N,S,dw", [(3, 129, 32, 64, 1, True), (2, 129, 64, 128, 2, True),
+                                          (64, 17, 512, 512, 1, True), (5, 17, 512, 1024, 2, True),
+                                          (64, 9, 1024, 1024, 1, True), (7, 9, 1024, 17, 1, False)])
+def test_dwpw_one_gemm_vs_fp64(B, H, K, N, S, dw):
+    """Depthwise 3x3 (stride S) + ReLU6 + pointwise + ReLU6 as one GEMM with the
+    depthwise in the operand staging (kernels/dwpw_f32.hip, nnsx::dwpw: the
+    PoseNet / MobileNetV1 pairs), and without a depthwise (the 1x1 heads, exact
+    columns), against fp64."""
+    import torch.nn.functional as F
+
+    g = torch.Generator().manual_seed(K + N)
+    x = (torch.rand(B, H, H, K, generator=g) * 2).cuda()
+    wd = (torch.randn(9, K, generator=g) * 0.3).cuda()
+    bd = (torch.randn(K, generator=g) * 0.1).cuda()
+    Np = (N + 63) // 64 * 64
+    wt = torch.zeros(Np, K)
+    wt[:N] = torch.randn(N, K, generator=g) / K ** 0.5
+    wt = wt.cuda()
+    bias = torch.zeros(Np)
+    bias[:N] = torch.randn(N, generator=g) * 0.1
+    bias = bias.cuda()
+    y = torch.ops.nnsx.dwpw([x], [wd if dw else None], [bd if dw else None], [wt], [bias], [N], [S], 1 if dw else 0)[0]
+    xd = x.double().cpu().permute(0, 3, 1, 2)
+    if dw:
+        xd = F.conv2d(xd, wd.double().cpu().t().reshape(K, 1, 3, 3), bd.double().cpu(), stride=S, padding=1,
+                      groups=K).clamp(0, 6)
+    ref = torch.einsum("bchw,nc->bhwn", xd, wt.double().cpu()[:N]) + bias.double().cpu()[:N]
+    if dw:
+        ref = ref.clamp(0, 6)
+    Ho = (H - 1) // S + 1
+    assert y.shape == (B, Ho, Ho, N)
+    err = ((y.double().cpu() - ref).abs() / (ref.abs() + 1)).max().item()
+    assert err < 2e-5, err
