@@ -111,14 +111,15 @@ __global__ void __launch_bounds__(256) dwpw_f32_kernel(SepHeadsArgs args) {
           acc = *reinterpret_cast<const f32x4_t*>(xb + static_cast<int64_t>(py[i] * P.W + px[i]) * P.K);
         } else {
           acc = *reinterpret_cast<const f32x4_t*>(P.bd + k);
-          const int iy = py[i] * P.stride - 1, ix = px[i] * P.stride - 1;
+          const int D = P.dil;
+          const int iy = py[i] * P.stride - D, ix = px[i] * P.stride - D;
 #pragma unroll
           for (int ky = 0; ky < 3; ++ky) {
-            const int yy = iy + ky;
+            const int yy = iy + ky * D;
             if (yy < 0 || yy >= P.H) continue;
 #pragma unroll
             for (int kx = 0; kx < 3; ++kx) {
-              const int xx = ix + kx;
+              const int xx = ix + kx * D;
               if (xx < 0 || xx >= P.W) continue;
               const f32x4_t xv = *reinterpret_cast<const f32x4_t*>(xb + static_cast<int64_t>(yy * P.W + xx) * P.K);
               const f32x4_t w4 = *reinterpret_cast<const f32x4_t*>(P.wd + (ky * 3 + kx) * P.K + k);
@@ -194,6 +195,10 @@ __global__ void __launch_bounds__(256) dwpw_f32_kernel(SepHeadsArgs args) {
       const int n = n0 + wn * (BN / 2) + j * 16 + g * 4;
       if (n >= P.N) continue;
       f32x4_t v = acc[i][j] + *reinterpret_cast<const f32x4_t*>(P.bias + n);
+      if (P.res) {  // (an inverted residual's skip: NHWC, the output's layout, N % 4 == 0)
+        const float* rrow = P.res + static_cast<int64_t>(b) * P.bstride + static_cast<int64_t>(q) * P.ldo;
+        v += *reinterpret_cast<const f32x4_t*>(rrow + n);
+      }
       if (P.act == 1) v = f32x4_t{relu6f(v[0]), relu6f(v[1]), relu6f(v[2]), relu6f(v[3])};
       if (n + 4 <= P.N && (P.ldo & 3) == 0) {
         *reinterpret_cast<f32x4_t*>(orow + n) = v;
@@ -212,13 +217,17 @@ __global__ void __launch_bounds__(256) dwpw_f32_kernel(SepHeadsArgs args) {
 // least 128 wide (fewer depthwise recomputations per pixel), else 64
 void dwpw_f32(SepHeadsArgs a, hipStream_t s) {
   if (a.n <= 0 || a.n > kSepHeadsMax) throw std::invalid_argument("dwpw_f32: 1..16 problems");
+  // 128-wide tiles recompute the depthwise half as often; worth it where the
+  // N padding stays small
   bool wide = true;
-  for (int i = 0; i < a.n; ++i) wide = wide && a.h[i].N >= 128;
+  for (int i = 0; i < a.n; ++i) wide = wide && (a.h[i].N >= 512 || a.h[i].N % 128 == 0);
   const int BN = wide ? 128 : 64;
   int64_t tiles = 0;
   for (int i = 0; i < a.n; ++i) {
     SepHead& h = a.h[i];
     if (h.stride != 1 && h.stride != 2) throw std::invalid_argument("dwpw_f32: stride 1 or 2");
+    if (h.dil < 1) throw std::invalid_argument("dwpw_f32: dilation >= 1");
+    if (h.res && (h.N % 4 || (h.ldo > 0 && h.ldo != h.N))) throw std::invalid_argument("dwpw_f32: residual needs NHWC, N % 4");
     if (h.Ho <= 0) h.Ho = (h.H - 1) / h.stride + 1;
     if (h.Wo <= 0) h.Wo = (h.W - 1) / h.stride + 1;
     if (!h.wd && (h.stride != 1 || h.Ho != h.H || h.Wo != h.W))

@@ -79,7 +79,9 @@ struct SepHead {
   float* out = nullptr;         // this head's first row in image 0 of the [B][T][C] output
   int64_t bstride = 0;          // floats between images in the output (T * C; NHWC: Ho * Wo * N)
   int B = 0, H = 0, W = 0, K = 0, Kpad = 0, N = 0, Npad = 0;  // N: outputs per pixel (anchors x C)
-  int stride = 1;               // depthwise stride (padding 1); wd == nullptr: no depthwise (plain 1x1)
+  int stride = 1;               // depthwise stride; wd == nullptr: no depthwise (plain 1x1)
+  int dil = 1;                  // depthwise dilation (padding = dil)
+  const float* res = nullptr;   // residual added before act (NHWC like the output)
   int act = 0;                  // 1: ReLU6 on the output
   int Ho = 0, Wo = 0;           // output map (0: from H, W, stride)
   int ldo = 0;                  // floats between output pixels (0: N)

@@ -197,7 +197,8 @@ void sep_heads_cpu(at::TensorList xs, at::TensorList wds, at::TensorList bds, at
 // NHWC [B, Ho, Wo, ns[i]] (exact columns).  wds[i] undefined: no depthwise.
 std::vector<at::Tensor> dwpw_cuda(at::TensorList xs, const c10::List<c10::optional<at::Tensor>>& wds,
                                   const c10::List<c10::optional<at::Tensor>>& bds, at::TensorList wts,
-                                  at::TensorList biases, at::IntArrayRef ns, at::IntArrayRef strides, int64_t act) {
+                                  at::TensorList biases, at::IntArrayRef ns, at::IntArrayRef strides, int64_t act,
+                                  int64_t dilation, const c10::optional<at::Tensor>& res) {
   const size_t n = xs.size();
   TORCH_CHECK(n > 0 && n <= static_cast<size_t>(nnsx::kernels::kSepHeadsMax) && wds.size() == n && bds.size() == n &&
                   wts.size() == n && biases.size() == n && ns.size() == n && strides.size() == n,
@@ -235,6 +236,13 @@ std::vector<at::Tensor> dwpw_cuda(at::TensorList xs, const c10::List<c10::option
     h.Npad = static_cast<int>(wts[i].size(0));
     h.stride = static_cast<int>(S);
     h.act = static_cast<int>(act);
+    h.dil = static_cast<int>(dilation);
+    if (res.has_value() && res->defined()) {
+      TORCH_CHECK(n == 1 && res->is_cuda() && res->scalar_type() == at::kFloat && res->is_contiguous() &&
+                      res->sizes() == y.sizes() && N % 4 == 0,
+                  "dwpw: residual [B,Ho,Wo,N] f32 (one problem)");
+      h.res = res->data_ptr<float>();
+    }
     outs.push_back(y);
   }
   nnsx::kernels::dwpw_f32(a, cur_stream());
@@ -243,13 +251,15 @@ std::vector<at::Tensor> dwpw_cuda(at::TensorList xs, const c10::List<c10::option
 
 std::vector<at::Tensor> dwpw_cpu(at::TensorList xs, const c10::List<c10::optional<at::Tensor>>& wds,
                                  const c10::List<c10::optional<at::Tensor>>& bds, at::TensorList wts,
-                                 at::TensorList biases, at::IntArrayRef ns, at::IntArrayRef strides, int64_t act) {
+                                 at::TensorList biases, at::IntArrayRef ns, at::IntArrayRef strides, int64_t act,
+                                 int64_t dilation, const c10::optional<at::Tensor>& res) {
   std::vector<at::Tensor> outs;
   for (size_t i = 0; i < xs.size(); ++i) {
     const c10::optional<at::Tensor> wd = wds.get(i), bd = bds.get(i);
-    at::Tensor h = (wd.has_value() && wd->defined()) ? dw_conv_cpu(xs[i], *wd, *bd, strides[i], 1, 1) : xs[i];
+    at::Tensor h = (wd.has_value() && wd->defined()) ? dw_conv_cpu(xs[i], *wd, *bd, strides[i], 1, dilation) : xs[i];
     const int64_t N = ns[i];
-    outs.push_back(pw_conv_cpu(h, wts[i], biases[i], c10::nullopt, (N + 3) / 4 * 4, act, true).slice(-1, 0, N).contiguous());
+    at::Tensor y = pw_conv_cpu(h, wts[i], biases[i], res, (N + 3) / 4 * 4, act, true).slice(-1, 0, N).contiguous();
+    outs.push_back(y);
   }
   return outs;
 }
@@ -653,7 +663,7 @@ TORCH_LIBRARY(nnsx, m) {
   m.def("pw_conv_rowbias(Tensor x, Tensor wt, Tensor bias, int N, int act) -> Tensor");
   m.def("upsample_bilinear(Tensor x, int H, int W) -> Tensor");
   m.def("dwpw(Tensor[] xs, Tensor?[] wds, Tensor?[] bds, Tensor[] wts, Tensor[] biases, int[] ns, int[] strides, "
-        "int act) -> Tensor[]");
+        "int act, int dilation=1, Tensor? res=None) -> Tensor[]");
   m.def("sep_heads(Tensor[] xs, Tensor[] wds, Tensor[] bds, Tensor[] wts, Tensor[] biases, int[] ns, int[] which, "
         "Tensor(a!) out_box, Tensor(b!) out_cls) -> ()");
   m.def("dw_conv(Tensor x, Tensor w, Tensor bias, int stride, int act, int dilation=1) -> Tensor");

@@ -137,6 +137,7 @@ class Block(nn.Module):
         # tickets of the fp32 kernel's in-launch combine of hidden-channel parts
         # (small batches): zero here, and every launch leaves them zero again
         self.register_buffer("ir_tickets", torch.zeros(256 if self.f32 else 1, dtype=torch.int32))
+        self.dwpw_dilated = False
         if self.f32:
             self._init_f32(cin, hid)
             return
@@ -181,6 +182,9 @@ class Block(nn.Module):
         self.register_buffer("ir_wp", self.project.wt[:, :hid].contiguous().clone())
         self.min_tiles = 0
         self.use_ir = FUSE_IR and hid % 16 == 0 and (self.has_expand or hid == cin)
+        # dilated blocks (DeepLab's output-stride-16 stage) that the fused kernel
+        # does not take: depthwise + project as one GEMM (NNSX_DWPW_DILATED=0: two launches)
+        self.dwpw_dilated = os.environ.get("NNSX_DWPW_DILATED", "1") != "0" and self.cout % 4 == 0
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.f32:
@@ -199,6 +203,14 @@ class Block(nn.Module):
                                                 self.dw.dilation)
             else:
                 h = self.expand(x) if self.has_expand else x
+                if self.dwpw_dilated and self.dw.dilation > 1 and h.is_cuda:
+                    # dilated depthwise inside the project GEMM's operand staging
+                    # (kernels/dwpw_f32.hip): no depthwise output map in HBM
+                    wd: List[Optional[torch.Tensor]] = [self.dw.w]
+                    bd: List[Optional[torch.Tensor]] = [self.dw.bias]
+                    r: Optional[torch.Tensor] = x if self.use_res else None
+                    return torch.ops.nnsx.dwpw([h], wd, bd, [self.project.wt], [self.project.bias], [self.cout],
+                                               [self.dw.stride], 0, self.dw.dilation, r)[0]
                 h = self.dw(h)
             if self.use_res:
                 return self.project(h, x)

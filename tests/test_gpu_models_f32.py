@@ -187,3 +187,28 @@ def test_dwpw_one_gemm_vs_fp64(B, H, K, N, S, dw):
     assert y.shape == (B, Ho, Ho, N)
     err = ((y.double().cpu() - ref).abs() / (ref.abs() + 1)).max().item()
     assert err < 2e-5, err
+
+
+def test_dwpw_dilated_residual_vs_fp64():
+    """DeepLab's dilated blocks: depthwise dilation 2 (padding 2) inside the
+    project GEMM, plus the block's residual, against fp64 (33x33 maps, B = 8)."""
+    import torch.nn.functional as F
+
+    B, H, K, N = 8, 33, 960, 160
+    g = torch.Generator().manual_seed(11)
+    x = (torch.rand(B, H, H, K, generator=g) * 2).cuda()
+    res = torch.randn(B, H, H, N, generator=g).cuda()
+    wd = (torch.randn(9, K, generator=g) * 0.3).cuda()
+    bd = (torch.randn(K, generator=g) * 0.1).cuda()
+    wt = torch.zeros(192, K)
+    wt[:N] = torch.randn(N, K, generator=g) / K ** 0.5
+    wt = wt.cuda()
+    bias = torch.zeros(192)
+    bias[:N] = torch.randn(N, generator=g) * 0.1
+    bias = bias.cuda()
+    y = torch.ops.nnsx.dwpw([x], [wd], [bd], [wt], [bias], [N], [1], 0, 2, res)[0]
+    d = F.conv2d(x.double().cpu().permute(0, 3, 1, 2), wd.double().cpu().t().reshape(K, 1, 3, 3), bd.double().cpu(),
+                 padding=2, dilation=2, groups=K).clamp(0, 6)
+    ref = torch.einsum("bchw,nc->bhwn", d, wt.double().cpu()[:N]) + bias.double().cpu()[:N] + res.double().cpu()
+    err = ((y.double().cpu() - ref).abs() / (ref.abs() + 1)).max().item()
+    assert err < 2e-5, err
