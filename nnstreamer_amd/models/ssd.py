@@ -15,7 +15,7 @@ Input for both: ``[B, 300, 300, 3]`` float32 NHWC (NNStreamer ``3:300:300:B``).
 from __future__ import annotations
 
 import math
-from typing import List, Tuple
+from typing import List, Optional, Tuple
 
 import torch
 import torch.nn as nn
@@ -156,7 +156,13 @@ class FusedExtra(nn.Module):
         self.c = PW(*_fold(e[2][0], e[2][1]), act=1, precision=precision)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return self.c(self.d(self.a(x)))
+        h = self.a(x)
+        if self.c.wt.dtype == torch.float32 and h.is_cuda:
+            # the stride-2 depthwise inside the second pointwise GEMM (kernels/dwpw_f32.hip)
+            wd: List[Optional[torch.Tensor]] = [self.d.w]
+            bd: List[Optional[torch.Tensor]] = [self.d.bias]
+            return torch.ops.nnsx.dwpw([h], wd, bd, [self.c.wt], [self.c.bias], [self.c.n], [self.d.stride], 1)[0]
+        return self.c(self.d(h))
 
 
 class FusedSSDLite(nn.Module):
@@ -198,7 +204,13 @@ class FusedSSDLite(nn.Module):
             if i == self.feat_block:
                 e = blk.expand(h)
                 feats.append(e)
-                h = blk.project(blk.dw(e))
+                if self.f32 and e.is_cuda and not blk.use_res:
+                    wd: List[Optional[torch.Tensor]] = [blk.dw.w]
+                    bd: List[Optional[torch.Tensor]] = [blk.dw.bias]
+                    h = torch.ops.nnsx.dwpw([e], wd, bd, [blk.project.wt], [blk.project.bias], [blk.cout],
+                                            [blk.dw.stride], 0)[0]
+                else:
+                    h = blk.project(blk.dw(e))
             elif i > 0:  # (block 0 is in self.front)
                 h = blk(h)
         h = self.head(h)

@@ -1,7 +1,7 @@
 """Batch-1 launch-path probe of the fp32 fused MobileNetV2: host time of a
 hipGraph replay vs. eager launches, and replay->sync latency (no profiler).
 
-    python scripts/b1_graph_probe.py
+    python scripts/b1_graph_probe.py [batch]     (default 1)
 """
 import os
 import sys
@@ -14,7 +14,8 @@ import nnstreamer_amd  # noqa: F401,E402
 from nnstreamer_amd.models.fused import fused_mobilenet_v2  # noqa: E402
 
 m = torch.jit.script(fused_mobilenet_v2(0, "fp32").cuda())
-x = torch.randint(0, 256, (1, 224, 224, 3), device="cuda", dtype=torch.uint8)
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+x = torch.randint(0, 256, (B, 224, 224, 3), device="cuda", dtype=torch.uint8)
 s = torch.cuda.Stream()
 with torch.cuda.stream(s):
     for _ in range(5):
@@ -52,4 +53,4 @@ for _ in range(100):
     g.replay()
 ev1.record()
 torch.cuda.synchronize()
-print(f"graph replay back-to-back: {ev0.elapsed_time(ev1) * 10:.1f} us per forward (device)")
+print(f"batch {B}: graph replay back-to-back: {ev0.elapsed_time(ev1) * 10:.1f} us per forward (device)")

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 4: small-batch forward traces (batch 1 and 8: back-to-back graph replays)
+# and the ATen-origin analysis of a short bench run.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+for B in 1 8; do
+  cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/fwdprof_b$B -o fwd --output-format csv -- python3 $R/scripts/b1_graph_probe.py $B > $R/gpurun_out/fwdprof_b$B.log 2>&1 || { echo "fwd prof $B failed"; tail -20 $R/gpurun_out/fwdprof_b$B.log; exit 1; }
+  grep -E "graph replay" $R/gpurun_out/fwdprof_b$B.log
+done
+cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace -d $R/gpurun_out/prof_aten -o aten -- python3 $R/bench.py --steps 10 --warmup 3 --latency-frames 50 --sweep 8 > $R/gpurun_out/prof_aten.log 2>&1 || { echo "aten prof failed"; tail -20 $R/gpurun_out/prof_aten.log; exit 1; }
+cd $R && python3 scripts/aten_origin.py gpurun_out/prof_aten/aten_results.db > gpurun_out/aten_origin.txt 2>&1; tail -30 gpurun_out/aten_origin.txt
