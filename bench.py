@@ -423,7 +423,7 @@ def main():
 
     # batch-1 latency of the headline engine (the "p50 per-frame latency" half of the metric)
     lat_b1 = None
-    if a.latency_frames > 0 and a.config == "mbv2" and not cfg.get("fan"):
+    if a.latency_frames > 0 and not cfg.get("fan") and not cfg.get("gather"):
         label, model_name, _ = runs[0]
         model_path = os.path.join(workdir, f"{model_name}.pt")
         w1 = max(10, a.latency_frames // 5)

@@ -1718,6 +1718,7 @@ const IrwCfg kIrwCfgs[] = {
     NNSX_IRW(1, 8, 16, 24, 2, 3, true),    // 56x56: expand 192/128 (8x8: 112/64)
     NNSX_IRW(2, 4, 8, 24, 2, 3, true),     // 56 -> 28: expand 160/128 input px (4x4: 96/64)
     NNSX_IRW(2, 8, 8, 16, 2, 3, true),     // 112 -> 56: expand 304/256 (4x8: 160/128)
+    NNSX_IRW(1, 7, 14, 64, 4, 4, false),   // 14x14 64 -> 384 -> 64: expand / project 112/98 cells (7x7: 64/49)
     // (dilation 2 -- DeepLab's output-stride-16 blocks on 33x33 maps -- as
     // NNSX_IRWD(1, 7, 7, 160, 10, 4, false, 2) etc. ran 156 vs 120 us for the
     // unfused expand GEMM + dilated depthwise + project GEMM at batch 8 (the
