@@ -138,6 +138,7 @@ class Block(nn.Module):
         # (small batches): zero here, and every launch leaves them zero again
         self.register_buffer("ir_tickets", torch.zeros(256 if self.f32 else 1, dtype=torch.int32))
         self.dwpw_dilated = False
+        self.dwpw_all = False
         if self.f32:
             self._init_f32(cin, hid)
             return
@@ -185,6 +186,8 @@ class Block(nn.Module):
         # dilated blocks (DeepLab's output-stride-16 stage) that the fused kernel
         # does not take: depthwise + project as one GEMM (NNSX_DWPW_DILATED=0: two launches)
         self.dwpw_dilated = os.environ.get("NNSX_DWPW_DILATED", "1") != "0" and self.cout % 4 == 0
+        # (A/B: every unfused block that way, e.g. MobileNetV2's 7x7 160 -> 960 -> 320)
+        self.dwpw_all = os.environ.get("NNSX_DWPW_ALL", "0") == "1"
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.f32:
@@ -203,7 +206,7 @@ class Block(nn.Module):
                                                 self.dw.dilation)
             else:
                 h = self.expand(x) if self.has_expand else x
-                if self.dwpw_dilated and self.dw.dilation > 1 and h.is_cuda:
+                if self.dwpw_dilated and (self.dw.dilation > 1 or self.dwpw_all) and h.is_cuda:
                     # dilated depthwise inside the project GEMM's operand staging
                     # (kernels/dwpw_f32.hip): no depthwise output map in HBM
                     wd: List[Optional[torch.Tensor]] = [self.dw.w]
