@@ -171,6 +171,7 @@ struct StemIr1F32Args {
   const float* bp = nullptr;
   int B = 0, H = 0, W = 0;
   const float* lut = nullptr;  // [256] f32, device
+  int mode = -1;               // kernel: -1 = $NNSX_STEM_WAVE policy, 0/1/2 tile kernels, 3 line buffer
   // derived
   int Ho = 0, Wo = 0, tiles_x = 0, tiles_y = 0;
 };

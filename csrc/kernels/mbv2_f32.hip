@@ -1612,6 +1612,183 @@ __global__ void __launch_bounds__(64, 2) stem_ir1w_f32_kernel(StemIr1F32Args a) 
   }
 }
 
+// ----------------------------------------------------- stem_band_f32 ----
+// Stem + block 1 as a LINE BUFFER: one workgroup (4 waves) walks a band of BR
+// output rows of a column strip (<= 112 columns) of one image top to bottom.
+// Each stem output row is computed ONCE into a 4-slot LDS ring (32 channels x
+// the strip's cells + the dw's 1-cell horizontal halo); output row y then
+// runs the depthwise over ring rows y-1, y, y+1 and the K = 32 project.  The
+// tile kernels recompute the stem on every tile's halo -- 100 stem cells per 64
+// outputs at 8 x 8 (1.56x, plus 16-pixel padding: 1.75x of the stem MFMAs) --
+// here the only recompute is 2 stem rows per band (BR = 28: 1.07x) and, with
+// several strips, 2 columns per strip.
+// Per output row: (1) the input rows of the next stem row, prefetched into
+// registers during the previous row's depthwise, go through the 256-entry
+// table into LDS; barrier; (2) stem MFMA of that row into its ring slot
+// (units = 16-cell pixel tile x 16-channel half, dealt over the waves);
+// barrier; (3) depthwise + project of the output row (pixel tiles dealt over
+// the waves).  The slot written in (2) was last read two rows earlier, so two
+// barriers per row order everything.
+constexpr int kBandWS = 112;                    // strip width (output columns)
+constexpr int kBandCells = kBandWS + 2;         // ring cells per row (dw halo)
+constexpr int kBandPitch = (2 * kBandCells + 1) * 3;  // input floats per staged row
+struct StemBandGeom {
+  static constexpr size_t ring_q = static_cast<size_t>(4) * 8 * kBandCells;  // [slot][quad][cell] f32x4
+  static constexpr size_t xin_f = static_cast<size_t>(3) * kBandPitch;
+  static constexpr size_t bytes = 16 * ring_q + 4 * ((xin_f + 3) / 4 * 4 + 256);
+};
+
+__global__ void __launch_bounds__(256, 2) stem_band_f32_kernel(StemIr1F32Args a, int BR, int strips) {
+  constexpr int PITCH = kBandPitch, CELLS = kBandCells;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  f32x4_t* ring = reinterpret_cast<f32x4_t*>(smem);                 // [4][8][CELLS]
+  float* xin = smem + 4 * StemBandGeom::ring_q;                      // [3][PITCH]
+  float* lut = xin + (StemBandGeom::xin_f + 3) / 4 * 4;              // [256]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // ---- which band / strip
+  const int nbands = (a.Ho + BR - 1) / BR;
+  int w = blockIdx.x;
+  const int strip = w % strips;
+  w /= strips;
+  const int band = w % nbands;
+  const int b = w / nbands;
+  const int y0 = band * BR, y1 = min(a.Ho, y0 + BR);
+  const int x0 = strip * kBandWS, ws = min(kBandWS, a.Wo - x0);
+  // ring cell j <-> stem column x0 - 1 + j; in-image cells [clo, chi)
+  const int clo = x0 == 0 ? 1 : 0, chi = min(ws + 2, a.Wo - x0 + 1);
+  const int nunits = 2 * ((chi - clo + 15) / 16);  // (16-cell tile, channel half)
+
+  for (int i = tid; i < 256; i += 256) lut[i] = a.lut[i];
+  // out-of-image ring cells (the dw's zero padding) are zero for every row
+  for (int v = tid; v < 4 * 8 * CELLS; v += 256) {
+    const int j = v % CELLS;
+    if (j < clo || j >= chi) ring[v] = z;
+  }
+
+  // stem weights (A: row li = channel 16h + li, k = 4t + g over the 27 taps + 1 zero)
+  float sa[2][7];
+  int off[7];
+#pragma unroll
+  for (int t = 0; t < 7; ++t) {
+    const int k = 4 * t + g;
+    sa[0][t] = k < 27 ? a.ws[k * 32 + li] : 0.f;
+    sa[1][t] = k < 27 ? a.ws[k * 32 + 16 + li] : 0.f;
+    off[t] = k < 27 ? (k / 9) * PITCH + ((k % 9) / 3) * 3 + (k % 3) : 0;
+  }
+  f32x4_t bs4[2], bd4[2], pa[2], wd4[2][9];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int ch = 16 * h + 4 * g;
+    bs4[h] = *reinterpret_cast<const f32x4_t*>(a.bs + ch);
+    bd4[h] = *reinterpret_cast<const f32x4_t*>(a.bd + ch);
+    pa[h] = *reinterpret_cast<const f32x4_t*>(a.wp + li * 32 + ch);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wd4[h][t] = *reinterpret_cast<const f32x4_t*>(a.wd + t * 32 + ch);
+  }
+  const f32x4_t bp4 = *reinterpret_cast<const f32x4_t*>(a.bp + 4 * g);
+
+  // input staging: stem row r reads input rows 2r-1 .. 2r+1, columns
+  // 2(x0-1)-1 .. (2(ws+2)+1 columns); byte v of the 3 x PITCH patch
+  const int rowb = a.W * 3;
+  const uint8_t* img = a.x + static_cast<int64_t>(b) * a.H * rowb;
+  const int col0 = (2 * (x0 - 1) - 1) * 3;
+  constexpr int NV = (3 * PITCH + 255) / 256;
+  int raw[NV];
+  auto fetch = [&](int r) {  // raw bytes (-1: outside the image = zero padding)
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = tid + i * 256;
+      const int ry = v / PITCH, rc = v - ry * PITCH;
+      const int iy = 2 * r - 1 + ry, ib = col0 + rc;
+      const bool ok = v < 3 * PITCH && r >= 0 && r < a.Ho && iy >= 0 && iy < a.H && ib >= 0 && ib < rowb;
+      const uint8_t byte = img[ok ? static_cast<int64_t>(iy) * rowb + ib : 0];
+      raw[i] = ok ? static_cast<int>(byte) : -1;
+    }
+  };
+  __syncthreads();  // lut, zeroed halo cells
+
+  // ---- prologue: stem rows y0 - 1 and y0 into their ring slots
+  auto stem_row = [&](int r) {  // input in xin -> ring slot r & 3 (zeros outside the map)
+    f32x4_t* slot = ring + (r & 3) * 8 * CELLS;
+    if (r < 0 || r >= a.Ho) {
+      for (int v = tid; v < 8 * CELLS; v += 256) slot[v] = z;
+      return;
+    }
+    for (int u = wave; u < nunits; u += 8) {
+      // two units per pass (u, u + 4): two independent MFMA chains
+      const int u1 = u + 4;
+      const bool two = u1 < nunits;
+      const int c0 = clo + (u >> 1) * 16 + li, h0 = u & 1;
+      const int c1 = clo + (u1 >> 1) * 16 + li, h1 = u1 & 1;
+      const int bb0 = 6 * (c0 < chi ? c0 : clo), bb1 = 6 * (two && c1 < chi ? c1 : clo);
+      f32x4_t e0 = z, e1 = z;
+#pragma unroll
+      for (int t = 0; t < 7; ++t) {
+        e0 = mfma4(h0 ? sa[1][t] : sa[0][t], xin[bb0 + off[t]], e0);
+        if (two) e1 = mfma4(h1 ? sa[1][t] : sa[0][t], xin[bb1 + off[t]], e1);
+      }
+      if (c0 < chi) slot[(4 * h0 + g) * CELLS + c0] = relu6x4(e0 + bs4[h0]);
+      if (two && c1 < chi) slot[(4 * h1 + g) * CELLS + c1] = relu6x4(e1 + bs4[h1]);
+    }
+  };
+  auto stage = [&]() {  // raw -> xin through the table
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = tid + i * 256;
+      if (v < 3 * PITCH) xin[v] = raw[i] >= 0 ? lut[raw[i]] : 0.f;
+    }
+  };
+  fetch(y0 - 1);
+  stage();
+  fetch(y0);
+  __syncthreads();
+  stem_row(y0 - 1);
+  __syncthreads();
+  stage();
+  fetch(y0 + 1);
+  __syncthreads();
+  stem_row(y0);
+
+  const int npt = (ws + 15) / 16;
+  for (int y = y0; y < y1; ++y) {
+    // (1) next stem row's input (fetched during the previous row) -> xin
+    __syncthreads();  // xin free (stem row y done by every wave)
+    stage();
+    if (y + 2 <= y1) fetch(y + 2);  // (the row after: in flight during this row)
+    __syncthreads();
+    // (2) stem row y + 1
+    stem_row(y + 1);
+    __syncthreads();  // ring rows y-1 .. y+1 complete
+    // (3) depthwise + project of output row y
+    const f32x4_t* r0 = ring + ((y - 1) & 3) * 8 * CELLS;
+    const f32x4_t* r1 = ring + (y & 3) * 8 * CELLS;
+    const f32x4_t* r2 = ring + ((y + 1) & 3) * 8 * CELLS;
+    for (int pt = wave; pt < npt; pt += 4) {
+      const int x = pt * 16 + li;  // strip-relative output column; cells x, x+1, x+2
+      const int xx = x < ws ? x : 0;
+      f32x4_t acc = z;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int q = (4 * h + g) * CELLS + xx;
+        f32x4_t d = bd4[h];
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          d = __builtin_elementwise_fma(r0[q + kx], wd4[h][kx], d);
+          d = __builtin_elementwise_fma(r1[q + kx], wd4[h][3 + kx], d);
+          d = __builtin_elementwise_fma(r2[q + kx], wd4[h][6 + kx], d);
+        }
+        acc = mfma_k16(pa[h], relu6x4(d), acc);
+      }
+      if (x < ws)
+        *reinterpret_cast<f32x4_t*>(a.y + ((static_cast<int64_t>(b) * a.Ho + y) * a.Wo + x0 + x) * 16 + 4 * g) =
+            acc + bp4;
+    }
+  }
+}
+
 // the hidden-split partials of irw_f32 (> 2 parts), added in part order
 // (deterministic), + bias (+ residual)
 __global__ void __launch_bounds__(256) irw_reduce_kernel(const float* __restrict__ ws, int parts, int64_t plane,
@@ -2186,8 +2363,32 @@ static bool stem_ir1w_f32(StemIr1F32Args a, hipStream_t s) {
   return true;
 }
 
+// line-buffer stem (stem_band_f32_kernel): bands of BR rows, strips of <= 112
+// columns; chosen when the grid stays large (>= 1024 workgroups at BR >= 14)
+static bool stem_band_f32(StemIr1F32Args a, hipStream_t s) {
+  a.Ho = (a.H - 1) / 2 + 1;
+  a.Wo = (a.W - 1) / 2 + 1;
+  const int strips = (a.Wo + kBandWS - 1) / kBandWS;
+  // the tallest band that keeps >= 1024 workgroups (2 resident per CU x 256 CUs x 2
+  // rounds), 14 .. 28 rows
+  int BR = 28;
+  while (BR > 14 && static_cast<int64_t>(a.B) * strips * ((a.Ho + BR - 1) / BR) < 1024) BR -= 2;
+  const int64_t wgs = static_cast<int64_t>(a.B) * strips * ((a.Ho + BR - 1) / BR);
+  const size_t lds = StemBandGeom::bytes;
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_band_f32_kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+  if (!attr || lds > 160 * 1024 || wgs <= 0 || wgs > (1ll << 31)) return false;
+  hipLaunchKernelGGL(stem_band_f32_kernel, dim3(static_cast<unsigned>(wgs)), dim3(256), lds, s, a, BR, strips);
+  return true;
+}
+
 bool stem_ir1_f32(const StemIr1F32Args& args, hipStream_t s) {
   StemIr1F32Args a = args;
+  // NNSX_STEM_WAVE=3: the line-buffer band kernel whenever the batch gives it a
+  // large grid (B >= 16 at 224 x 224); small batches keep the tile kernel
+  static const int env_mode = irw_env("NNSX_STEM_WAVE", 2);
+  if (a.mode == 3) return stem_band_f32(a, s);  // (forced: tests)
+  if (a.mode < 0 && env_mode == 3 && a.B >= 16 && stem_band_f32(a, s)) return true;
   // one wave per 8 x 8 tile with paired-row depthwise (default, 2), the same
   // without the row pairing (1), or the 8-wave 16 x 16 tile kernel (0).
   // Batch 512 on one box: 525 / 514 / 510 us for 0 / 1 / 2 (another box: 520 vs

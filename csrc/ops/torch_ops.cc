@@ -607,7 +607,8 @@ at::Tensor ir_block_cpu(const at::Tensor& x, const at::Tensor& we, const at::Ten
 
 // stem + first (t = 1) block, fused (fp32): uint8 frame -> [B, Ho, Wo, 16]
 at::Tensor stem_ir1_cuda(const at::Tensor& x, const at::Tensor& ws, const at::Tensor& bs, const at::Tensor& wd,
-                         const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, const at::Tensor& lut) {
+                         const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, const at::Tensor& lut,
+                         int64_t mode) {
   TORCH_CHECK(lut.is_cuda() && lut.scalar_type() == at::kFloat && lut.numel() == 256 && lut.is_contiguous(),
               "stem_ir1: lut [256] f32 on the device");
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kByte && x.is_contiguous() && x.dim() == 4 && x.size(3) == 3,
@@ -632,12 +633,15 @@ at::Tensor stem_ir1_cuda(const at::Tensor& x, const at::Tensor& ws, const at::Te
   a.H = static_cast<int>(H);
   a.W = static_cast<int>(W);
   a.lut = lut.data_ptr<float>();
+  a.mode = static_cast<int>(mode);
   TORCH_CHECK(nnsx::kernels::stem_ir1_f32(a, cur_stream()), "stem_ir1: launch failed");
   return y;
 }
 
 at::Tensor stem_ir1_cpu(const at::Tensor& x, const at::Tensor& ws, const at::Tensor& bs, const at::Tensor& wd,
-                        const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, const at::Tensor& lut) {
+                        const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, const at::Tensor& lut,
+                        int64_t mode) {
+  (void)mode;
   at::Tensor h = stem_conv_u8_cpu(x, ws, bs, 1, lut, true);
   h = dw_conv_cpu(h, wd, bd, 1, 1, 1);
   return pw_conv_cpu(h, wp, bp, c10::nullopt, 16, 0, true);
@@ -671,7 +675,8 @@ TORCH_LIBRARY(nnsx, m) {
   m.def("stem_conv_u8(Tensor x, Tensor w, Tensor bias, int act, Tensor lut, bool out_f32=False) -> Tensor");
   m.def("avgpool(Tensor x) -> Tensor");
   m.def("pw_conv_pool(Tensor x, Tensor wt, Tensor bias, int N, int act) -> Tensor");
-  m.def("stem_ir1(Tensor x, Tensor ws, Tensor bs, Tensor wd, Tensor bd, Tensor wp, Tensor bp, Tensor lut) -> Tensor");
+  m.def("stem_ir1(Tensor x, Tensor ws, Tensor bs, Tensor wd, Tensor bd, Tensor wp, Tensor bp, Tensor lut, "
+        "int mode=-1) -> Tensor");
   m.def("pw_conv_f32_tile(Tensor x, Tensor wt, Tensor bias, Tensor? res, int N, int act, int tile) -> Tensor");
   m.def("ir_block(Tensor x, Tensor we, Tensor be, Tensor wd, Tensor bd, Tensor wp, Tensor bp, int stride, int cout, "
         "bool has_expand, bool residual, int dilation=1, Tensor(a!)? tickets=None) -> Tensor");

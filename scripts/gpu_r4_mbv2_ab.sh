@@ -8,4 +8,4 @@ run() {  # name, env...
   env "$@" timeout -k 10 300 python bench.py --steps 30 --warmup 10 --latency-frames 0 --sweep "" > gpurun_out/ab_$name.log 2>&1 || { echo "ab $name failed"; tail -20 gpurun_out/ab_$name.log; return 1; }
   python3 -c "import json,sys; d=json.loads([l for l in open('gpurun_out/ab_$name.log') if l.startswith('{')][-1]); print('$name', d['value'], d['ms_per_step'], d['gpu_invoke_ms_median'])"
 }
-run base NNSX_NONE=1 && run tile7x14 NNSX_IRW_SKIP=6 && run dwpw_all NNSX_DWPW_ALL=1 && run gemm128 NNSX_F32_GEMM_TILE=128128 && run base2 NNSX_NONE=1
+run base NNSX_NONE=1 && run stemband NNSX_STEM_WAVE=3 && run tile7x14 NNSX_IRW_SKIP=6 && run dwpw_all NNSX_DWPW_ALL=1 && run gemm128 NNSX_F32_GEMM_TILE=128128 && run base2 NNSX_NONE=1

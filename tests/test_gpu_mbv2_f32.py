@@ -82,9 +82,13 @@ def test_stem_f32_u8_and_pool(nns, H, W):
     _close(p, y.double().cpu().mean((1, 2)))
 
 
-@pytest.mark.parametrize("H,W,B", [(224, 224, 3), (300, 300, 2), (57, 41, 2), (17, 35, 1)])
-def test_stem_ir1_f32(nns, H, W, B):
-    """stem + first block fused (uint8 frame -> 16 channels) vs the fp64 chain."""
+@pytest.mark.parametrize("H,W,B,mode", [(224, 224, 3, -1), (300, 300, 2, -1), (57, 41, 2, -1), (17, 35, 1, -1),
+                                        (224, 224, 3, 3), (300, 300, 2, 3), (513, 513, 1, 3), (57, 41, 2, 3),
+                                        (17, 35, 1, 3), (224, 224, 20, 3)])
+def test_stem_ir1_f32(nns, H, W, B, mode):
+    """stem + first block fused (uint8 frame -> 16 channels) vs the fp64 chain;
+    mode 3 = the line-buffer band kernel (stem rows computed once, strips of 112
+    columns, bands of 14-28 rows)."""
     torch.manual_seed(H + W)
     x = torch.randint(0, 256, (B, H, W, 3), device="cuda", dtype=torch.uint8)
     ws = torch.randn(3, 3, 3, 32, device="cuda") * 0.3
@@ -93,7 +97,7 @@ def test_stem_ir1_f32(nns, H, W, B):
     bd = torch.randn(32, device="cuda") * 0.1
     wp = torch.randn(16, 32, device="cuda") / 32 ** 0.5
     bp = torch.randn(16, device="cuda") * 0.1
-    y = torch.ops.nnsx.stem_ir1(x, ws, bs, wd, bd, wp, bp, input_lut(-127.5, 127.5).cuda())
+    y = torch.ops.nnsx.stem_ir1(x, ws, bs, wd, bd, wp, bp, input_lut(-127.5, 127.5).cuda(), mode)
     assert y.shape == (B, (H - 1) // 2 + 1, (W - 1) // 2 + 1, 16) and y.dtype == torch.float32
     xf = (x.double().cpu() - 127.5) / 127.5
     h = F.conv2d(xf.permute(0, 3, 1, 2), ws.double().cpu().permute(3, 2, 0, 1), bs.double().cpu(), stride=2,
