@@ -2216,6 +2216,12 @@ static int irw_inlaunch_mode() {
   return m;
 }
 
+// the model's ticket buffer (ir_block_f32_tickets ints, zeroed once): the
+// spread form's 64-bit counters in [0, kSpreadTickets), the last-arriver
+// form's self-resetting ints after them (kLastTickets).  Hidden parts > 1 only
+// below 256 tiles (irw_parts), so both regions hold every splitting launch.
+constexpr int kSpreadTickets = 512, kLastTickets = 256;
+
 static int irw_parts(const IrwCfg* c, int tiles, int hid) {
   const int nsub = hid / 16;
   if (c->NOT == 0)  // depthwise output: parts need no reduction, so fill the chip
@@ -2248,20 +2254,27 @@ static bool launch_irw(const IrwCfg* c, IrBlockF32Args a, hipStream_t s) {
                                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
     return false;
   if (a.hsplit == 2 && !slabs) (void)hipMemsetAsync(a.y, 0, static_cast<size_t>(plane) * sizeof(float), s);
-  if (!a.ws) a.tickets = nullptr;
+  if (!a.ws || tiles > kLastTickets) a.tickets = nullptr;
   a.spread = 0;
-  if (a.tickets && irw_inlaunch_mode() == 2) {
+  if (a.tickets) {
     // the spread combine waits inside the launch for the other parts of a
     // tile: only when every workgroup of the grid is resident at once (one
     // block per CU under what the occupancy query reports, which can over-report)
     int dev = 0, ncu = 0, per_cu = 0;
-    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+    if (irw_inlaunch_mode() == 2 && 2 * tiles <= kSpreadTickets && hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(c->kernel), 64 * c->NW, lds) ==
             hipSuccess &&
         static_cast<int64_t>(tiles) * a.hsplit <= static_cast<int64_t>(ncu) * std::max(1, per_cu - 1))
       a.spread = 1;
+    else if (irw_inlaunch_mode() == 1 || a.hsplit <= 4)
+      // last-arriver form (self-resetting int tickets, their own region of the
+      // buffer: the spread form's counters there only grow): a grid larger than
+      // the chip -- DeepLab's 33x33 blocks at batch 8, 200 tiles x 2 parts --
+      // has few slabs per tile, so the last part adds them alone cheaply
+      a.tickets += kSpreadTickets;
     else
-      a.tickets = nullptr;  // (separate reduce launch)
+      a.tickets = nullptr;  // (separate reduce launch: many slabs, spread over its grid)
   }
   hipLaunchKernelGGL(c->kernel, dim3(static_cast<unsigned>(tiles * a.hsplit)), dim3(64 * c->NW), lds, s, a);
   if (a.ws && !a.tickets) {
@@ -2307,8 +2320,10 @@ size_t ir_block_f32_workspace_bytes(const IrBlockF32Args& args) {
   return static_cast<size_t>(a.hsplit) * a.B * a.Ho * a.Wo * a.cout * sizeof(float);
 }
 
-// the in-launch combine of the hidden parts: the spread form by default
-// (irw_inlaunch_mode); the last-arriver form (NNSX_F32_IRW_INLAUNCH=1) measured at batch 1
+// the in-launch combine of the hidden parts: the spread form by default when
+// the grid is resident, else the last-arriver form for <= 4 parts
+// (irw_inlaunch_mode, launch_irw); the last-arriver form everywhere
+// (NNSX_F32_IRW_INLAUNCH=1) measured at batch 1
 // (profiles/r3_b1_inlaunch_combine_trace.txt):
 // with release/acquire fences and per-block ticket fills, 456 vs 306 us per
 // forward; with write-through slabs, no fences and self-resetting tickets,
@@ -2322,7 +2337,7 @@ size_t ir_block_f32_tickets(const IrBlockF32Args& args) {
   const IrwCfg* c = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0, a.dil);
   if (!c || c->NOT == 0) return 0;
   irw_geometry(c, &a);
-  return static_cast<size_t>(a.tiles_x) * a.tiles_y * a.B * (mode == 2 ? 2 : 1);
+  return a.tiles_x * a.tiles_y * a.B <= kLastTickets ? kSpreadTickets + kLastTickets : 0;
 }
 
 size_t stem_ir1_lds_bytes() {

@@ -136,7 +136,7 @@ class Block(nn.Module):
         self.cout = int(p[0].out_channels)
         # tickets of the fp32 kernel's in-launch combine of hidden-channel parts
         # (small batches): zero here, and every launch leaves them zero again
-        self.register_buffer("ir_tickets", torch.zeros(256 if self.f32 else 1, dtype=torch.int32))
+        self.register_buffer("ir_tickets", torch.zeros(768 if self.f32 else 1, dtype=torch.int32))
         self.dwpw_dilated = False
         self.dwpw_all = False
         if self.f32:

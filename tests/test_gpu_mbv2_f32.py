@@ -181,14 +181,16 @@ def test_ir_block_f32_two_parts_deterministic(nns, H, cin, hid, cout, stride):
 
 
 @pytest.mark.parametrize("H,cin,hid,cout,stride", [(56, 24, 144, 24, 1), (28, 32, 192, 64, 2), (14, 64, 384, 96, 1),
-                                                    (14, 96, 576, 160, 2), (7, 160, 960, 160, 1)])
-@pytest.mark.parametrize("B", [1, 2])
+                                                    (14, 96, 576, 160, 2), (7, 160, 960, 160, 1),
+                                                    (33, 64, 384, 64, 1)])
+@pytest.mark.parametrize("B", [1, 2, 8])
 def test_ir_block_f32_inlaunch_combine(nns, H, cin, hid, cout, stride, B):
     """Hidden parts combined inside the launch (the model's ticket buffer;
     NNSX_F32_IRW_INLAUNCH=1 last arriver, =2 every part adds its share after a
     per-tile arrival count) == the separate ordered reduce launch, bitwise, over
-    repeated launches on one ticket buffer (monotone counters).  Without the
-    env variable both calls take the reduce launch."""
+    repeated launches on one ticket buffer (monotone counters).  Batch 8 of the
+    33x33 block (DeepLab: 200 tiles x 2 parts, more than the chip holds) takes
+    the last-arriver form in its own ticket region."""
     torch.manual_seed(cin + hid + B)
     x = torch.randn(B, H, H, cin, device="cuda")
     kin = (cin + 7) // 8 * 8
@@ -203,7 +205,7 @@ def test_ir_block_f32_inlaunch_combine(nns, H, cin, hid, cout, stride, B):
     bp = torch.zeros(npad, device="cuda")
     bp[:cout] = torch.randn(cout, device="cuda") * 0.1
     res = stride == 1 and cin == cout
-    tickets = torch.zeros(256, dtype=torch.int32, device="cuda")
+    tickets = torch.zeros(768, dtype=torch.int32, device="cuda")
     ref = torch.ops.nnsx.ir_block(x, we, be, wd, bd, wp, bp, stride, cout, True, res, 1, None)
     for _ in range(3):
         y = torch.ops.nnsx.ir_block(x, we, be, wd, bd, wp, bp, stride, cout, True, res, 1, tickets)
