@@ -1751,11 +1751,12 @@ __global__ void __launch_bounds__(256, 2) stem_band_f32_kernel(StemIr1F32Args a,
   fetch(y0 + 1);
   __syncthreads();
   stem_row(y0);
+  __syncthreads();  // xin free (stem row y0 done by every wave)
 
   const int npt = (ws + 15) / 16;
   for (int y = y0; y < y1; ++y) {
-    // (1) next stem row's input (fetched during the previous row) -> xin
-    __syncthreads();  // xin free (stem row y done by every wave)
+    // (1) next stem row's input (fetched during the previous row) -> xin; the
+    // barrier before the previous row's depthwise ordered every read of xin
     stage();
     if (y + 2 <= y1) fetch(y + 2);  // (the row after: in flight during this row)
     __syncthreads();
