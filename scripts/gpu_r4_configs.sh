@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for spec in ${SPECS:-ssd:64 deeplab:8 deeplab:32 posenet:64 deeplab_fan:8 posenet_multi:64}; do
+for spec in ${SPECS:-ssd:64 deeplab:8 deeplab:16 deeplab:32 posenet:64 deeplab_fan:8 posenet_multi:64}; do
   c=${spec%%:*}; B=${spec##*:}
   timeout -k 10 300 python bench.py --config $c --batch $B --steps ${STEPS:-20} --warmup ${WARMUP:-5} --sweep "" > gpurun_out/bench_${c}_b$B.log 2>&1 || { echo "bench $c failed"; tail -30 gpurun_out/bench_${c}_b$B.log; exit 1; }
   tail -1 gpurun_out/bench_${c}_b$B.log | cut -c1-300
