@@ -9,5 +9,10 @@ for B in 1 8; do
   cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/fwdprof_b$B -o fwd --output-format csv -- python3 $R/scripts/b1_graph_probe.py $B > $R/gpurun_out/fwdprof_b$B.log 2>&1 || { echo "fwd prof $B failed"; tail -20 $R/gpurun_out/fwdprof_b$B.log; exit 1; }
   grep -E "graph replay" $R/gpurun_out/fwdprof_b$B.log
 done
+# batch 8 as the headline run (long window): pipeline ms per batch vs device ms per invoke
+cd $R && for B in 8 32; do
+  timeout -k 10 300 python3 bench.py --batch $B --steps 400 --warmup 20 --latency-frames 0 --sweep "" > gpurun_out/bench_b$B.log 2>&1 || { echo "bench b$B failed"; tail -20 gpurun_out/bench_b$B.log; exit 1; }
+  python3 -c "import json; d=json.loads([l for l in open('gpurun_out/bench_b$B.log') if l.startswith('{')][-1]); print('b$B', d['value'], d['ms_per_step'], d['gpu_invoke_ms_median'], d['p50_latency_ms'])"
+done
 cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace -d $R/gpurun_out/prof_aten -o aten -- python3 $R/bench.py --steps 10 --warmup 3 --latency-frames 50 --sweep 8 > $R/gpurun_out/prof_aten.log 2>&1 || { echo "aten prof failed"; tail -20 $R/gpurun_out/prof_aten.log; exit 1; }
 cd $R && python3 scripts/aten_origin.py gpurun_out/prof_aten/aten_results.db > gpurun_out/aten_origin.txt 2>&1; tail -30 gpurun_out/aten_origin.txt
