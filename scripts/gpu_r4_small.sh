@@ -9,6 +9,12 @@ for B in 1 8; do
   cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/fwdprof_b$B -o fwd --output-format csv -- python3 $R/scripts/b1_graph_probe.py $B > $R/gpurun_out/fwdprof_b$B.log 2>&1 || { echo "fwd prof $B failed"; tail -20 $R/gpurun_out/fwdprof_b$B.log; exit 1; }
   grep -E "graph replay" $R/gpurun_out/fwdprof_b$B.log
 done
+# padded-frame upload micro-bench (DeepLab 513 / PoseNet 257 wide): DMA + unpad vs the gather kernel
+cd $R && for w in 513:8 257:64; do
+  timeout -k 10 120 python3 scripts/upload_bench.py ${w%%:*} ${w##*:} 100 >> gpurun_out/upload_bench.txt 2>&1 && \
+  NNSX_CONVERTER_PADDED_DMA=0 timeout -k 10 120 python3 scripts/upload_bench.py ${w%%:*} ${w##*:} 100 >> gpurun_out/upload_bench.txt 2>&1 || { echo "upload bench failed"; tail -20 gpurun_out/upload_bench.txt; exit 1; }
+done
+cat gpurun_out/upload_bench.txt
 # batch 8 as the headline run (long window): pipeline ms per batch vs device ms per invoke
 cd $R && for B in 8 32; do
   timeout -k 10 300 python3 bench.py --batch $B --steps 400 --warmup 20 --latency-frames 0 --sweep "" > gpurun_out/bench_b$B.log 2>&1 || { echo "bench b$B failed"; tail -20 gpurun_out/bench_b$B.log; exit 1; }
