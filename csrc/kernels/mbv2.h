@@ -64,6 +64,10 @@ struct YLayout {
   int ncols = 0;
   int64_t bstride = 0;
   int brpb = 0;
+  // pool > 0 (BN = 64 tiles, pool <= BM, no split-K / residual): y is [M / pool][N],
+  // the mean over each image's `pool` rows of act(x . w + bias); the caller zeroes y
+  // (an image spans at most two row tiles: two addends, so the sum is order-free)
+  int pool = 0;
 };
 void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
                  int Kpad, int Npad, int act, hipStream_t s, int tile = 0, float* ws = nullptr,

@@ -197,6 +197,37 @@ __global__ void __launch_bounds__(256) pw_gemm_f32_kernel(const float* __restric
   // values are all loaded up front, branch-free: loaded at each store behind
   // the bounds checks they were fetched and waited for one at a time.
   const bool slab = gridDim.z > 1;
+  if constexpr (BN == 64) {
+    if (yl.pool && !slab) {
+      // head conv + act + global average pool: the activated tile goes through
+      // the (now free) staging LDS, quads XOR-swizzled by row; each thread sums
+      // one (image, channel) column of the tile in row order and adds sum / pool
+      float* t = &xs[0][0][0][0];  // [BM][64]
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        const int ml = wm * (BM / 2) + i * 16 + li, m = m0 + ml;
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+          const int nl = wn * (BN / 2) + j * 16 + g * 4, n = n0 + nl;
+          f32x4_t v = acc[i][j] + *reinterpret_cast<const f32x4_t*>(bias + (n < N ? n : 0));
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], act);
+          *reinterpret_cast<f32x4_t*>(t + ml * 64 + (((nl >> 2) ^ (ml & 15)) << 2)) = m < M ? v : zero;
+        }
+      }
+      __syncthreads();
+      const int hw = yl.pool, mend = min(m0 + BM, M), b0 = m0 / hw, nb = (mend - 1) / hw - b0 + 1;
+      const float inv = 1.f / static_cast<float>(hw);
+      for (int v = tid; v < nb * 64; v += 256) {
+        const int bi = b0 + v / 64, nl = v % 64, n = n0 + nl;
+        const int r0 = max(bi * hw, m0) - m0, r1 = min((bi + 1) * hw, mend) - m0;
+        float sum = 0.f;
+        for (int r = r0; r < r1; ++r) sum += t[r * 64 + (((nl >> 2) ^ (r & 15)) << 2) + (nl & 3)];
+        if (n < N) atomicAdd(y + static_cast<int64_t>(bi) * N + n, sum * inv);
+      }
+      return;
+    }
+  }
   f32x4_t bv[RN], rv[RM][RN];
 #pragma unroll
   for (int j = 0; j < RN; ++j) {
@@ -2010,7 +2041,7 @@ static void pw_gemm_f32_launch(const float* x, const float* wt, const float* bia
                                const YLayout& yl = YLayout{}) {
   dim3 grid((M + BM - 1) / BM, (N + BN - 1) / BN);
   const int kstages = (Kpad + GKT - 1) / GKT;
-  int chunk = (ws && !yl.rpb && !yl.brpb) ? gemm_kchunk(static_cast<int>(grid.x * grid.y), kstages, N, !res) : kstages;
+  int chunk = (ws && !yl.rpb && !yl.brpb && !yl.pool) ? gemm_kchunk(static_cast<int>(grid.x * grid.y), kstages, N, !res) : kstages;
   grid.z = static_cast<unsigned>((kstages + chunk - 1) / chunk);
   if (grid.z == 1) {
     hipLaunchKernelGGL((pw_gemm_f32_kernel<BM, BN>), grid, dim3(256), 0, s, x, wt, bias, res, y, M, N, K, Kpad, Npad,
@@ -2080,7 +2111,7 @@ static bool use_small_m(int M, int K, int tile, const YLayout& yl) {
   // the split-K GEMM + reduce, so the many-row deep-K shapes keep split-K;
   // a two-workgroup K split with order-free atomics needed a memset node
   // that cost more than it saved: profiles/r3b_b1_forward_trace.txt)
-  return on && tile == 0 && M <= 64 && (M <= 16 || K <= 512) && !yl.rpb && !yl.brpb;
+  return on && tile == 0 && M <= 64 && (M <= 16 || K <= 512) && !yl.rpb && !yl.brpb && !yl.pool;
 }
 
 size_t pw_gemm_f32_workspace_bytes(int M, int N, int Kpad, bool has_res, int tile) {
@@ -2165,6 +2196,19 @@ void stem3x3_u8_f32(const uint8_t* x, const float* w, const float* bias, float* 
 
 void pw_pool_f32(const float* x, const float* wt, const float* bias, float* y, int B, int HW, int N, int K, int Kpad,
                  int Npad, int act, hipStream_t s) {
+  // larger batches: the tiled GEMM with the pooling epilogue (no [B][HW][N]
+  // head output in HBM and no avgpool launch)
+  if (B > 8 && HW <= 64) {
+    (void)hipMemsetAsync(y, 0, static_cast<size_t>(B) * N * sizeof(float), s);
+    YLayout yl;
+    yl.pool = HW;
+    const int M = B * HW;
+    if (M >= 8192)
+      pw_gemm_f32_launch<128, 64>(x, wt, bias, nullptr, y, M, N, K, Kpad, Npad, act, nullptr, s, yl);
+    else
+      pw_gemm_f32_launch<64, 64>(x, wt, bias, nullptr, y, M, N, K, Kpad, Npad, act, nullptr, s, yl);
+    return;
+  }
   const dim3 grid(static_cast<unsigned>((N + 15) / 16), static_cast<unsigned>(B));
   hipLaunchKernelGGL(pw_small_f32_kernel<true>, grid, dim3(256), 0, s, x, wt, bias, nullptr, y, B * HW, N, K, Kpad, Npad,
                      act, HW);

@@ -34,6 +34,9 @@ import os
 FUSE_IR = os.environ.get("NNSX_FUSE_IR", "1") != "0"
 # NNSX_FUSE_STEM=0 keeps the fp32 stem and first block as separate kernels (A/B testing)
 FUSE_STEM = os.environ.get("NNSX_FUSE_STEM", "1") != "0"
+# NNSX_F32_HEAD_POOL=0: batches > 8 run the head GEMM and the average pool as two
+# kernels (A/B testing of the pooling GEMM epilogue)
+HEAD_POOL = os.environ.get("NNSX_F32_HEAD_POOL", "1") != "0"
 
 
 def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d):
@@ -274,6 +277,7 @@ class FusedMobileNetV2(nn.Module):
 
     def __init__(self):
         super().__init__()
+        self.head_pool = HEAD_POOL
 
     @classmethod
     def from_reference(cls, m: MobileNetV2, precision: str = "bf16") -> "FusedMobileNetV2":
@@ -316,8 +320,9 @@ class FusedMobileNetV2(nn.Module):
             if i >= start:
                 h = blk(h)
             i += 1
-        if self.f32 and h.is_cuda and h.shape[0] <= 8:
-            # small batches: head conv + ReLU6 + global average pool in one launch
+        if self.f32 and h.is_cuda and (h.shape[0] <= 8 or self.head_pool):
+            # head conv + ReLU6 + global average pool in one launch (small batches:
+            # a workgroup per image; larger: the tiled GEMM with a pooling epilogue)
             h = torch.ops.nnsx.pw_conv_pool(h, self.head.wt, self.head.bias, self.head.n, self.head.act)
         else:
             h = self.head(h)

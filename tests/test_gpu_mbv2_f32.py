@@ -271,6 +271,24 @@ def test_pw_conv_pool_f32(nns, B, H):
     _close(y, ref, tol=5e-5)
 
 
+@pytest.mark.parametrize("B,H", [(9, 7), (64, 7), (171, 7), (12, 8)])
+def test_pw_conv_pool_f32_gemm_epilogue(nns, B, H):
+    """larger batches: the tiled GEMM's pooling epilogue (64- and 128-row tiles,
+    images straddling two row tiles: two order-free addends) vs fp64, bitwise
+    repeatable, and equal within fp32 rounding to the head GEMM + avgpool pair"""
+    torch.manual_seed(B * 7 + H)
+    K, N = 320, 1280
+    x = torch.randn(B, H, H, K, device="cuda")
+    wt = torch.randn(N, K, device="cuda") / K ** 0.5
+    bias = torch.randn(N, device="cuda") * 0.1
+    ys = [torch.ops.nnsx.pw_conv_pool(x, wt, bias, N, 1) for _ in range(3)]
+    assert all(torch.equal(ys[0], y) for y in ys[1:])
+    ref = (x.double().cpu() @ wt.double().cpu().t() + bias.double().cpu()).clamp(0, 6).mean((1, 2))
+    _close(ys[0], ref, tol=5e-5)
+    two = torch.ops.nnsx.avgpool(torch.ops.nnsx.pw_conv(x, wt, bias, None, N, 1, True))
+    assert (ys[0] - two).abs().max().item() < 1e-5
+
+
 def test_classifier_split_k_deterministic(nns):
     """M = batch GEMM (split over K, slabs added in order): bitwise repeatable."""
     torch.manual_seed(5)
