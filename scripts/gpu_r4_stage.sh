@@ -2,7 +2,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_decode_stage.py tests/test_gpu_mbv2_f32.py::test_stem_ir1_f32 tests/test_gpu_mbv2_f32.py::test_ir_block_f32_inlaunch_combine tests/test_gpu_comm.py tests/test_gpu_models_f32.py tests/test_gpu_elements.py tests/test_gpu_decoders_golden.py tests/test_gpu_pipelines.py -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_stage.log 2>&1 || { echo "pytest failed"; tail -60 gpurun_out/pytest_stage.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_decode_stage.py tests/test_gpu_mbv2_f32.py tests/test_gpu_comm.py tests/test_gpu_models_f32.py tests/test_gpu_elements.py tests/test_gpu_decoders_golden.py tests/test_gpu_pipelines.py -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_stage.log 2>&1 || { echo "pytest failed"; tail -60 gpurun_out/pytest_stage.log; exit 1; }
 tail -3 gpurun_out/pytest_stage.log
 # A/B of the new fusions (env toggles) on the config benches
 for spec in "posenet:64:NNSX_POSENET_DWPW=0" "deeplab:8:NNSX_DWPW_DILATED=0" "ssd:64:NNSX_SSD_SEP_HEADS=0"; do
