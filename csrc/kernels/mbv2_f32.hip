@@ -888,7 +888,10 @@ struct IrwGeom {
   // (3, 21 spills) lost 40 -> 45 us, and on the 56x56 block (1 spill, 5
   // workgroups/CU instead of 4) 128 -> 144 us.
   // (the wider 7x14 28x28 tiles hold 14 accumulators: 3 waves per SIMD)
-  static constexpr int MINB = (KIN == 32 && S == 1) ? (TY * TX <= 49 ? 4 : 3) : NOT <= 6 ? 2 : 1;
+  // (7x14 tiles with 6 cout tiles: 42 accumulators; the LDS holds one workgroup
+  // per CU anyway, so one wave per SIMD and the accumulation registers)
+  static constexpr int MINB = (KIN == 32 && S == 1) ? (TY * TX <= 49 ? 4 : 3)
+                              : (NOT <= 4 || (NOT <= 6 && TY * TX <= 64)) ? 2 : 1;
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -1928,6 +1931,8 @@ const IrwCfg kIrwCfgs[] = {
     NNSX_IRW(2, 4, 8, 24, 2, 3, true),     // 56 -> 28: expand 160/128 input px (4x4: 96/64)
     NNSX_IRW(2, 8, 8, 16, 2, 3, true),     // 112 -> 56: expand 304/256 (4x8: 160/128)
     NNSX_IRW(1, 7, 14, 64, 4, 4, false),   // 14x14 64 -> 384 -> 64: expand / project 112/98 cells (7x7: 64/49)
+    NNSX_IRW(1, 7, 14, 64, 6, 4, false),   // 14x14 64 -> 384 -> 96
+    NNSX_IRW(1, 7, 14, 96, 6, 4, false),   // 14x14 96 -> 576 -> 96: expand 144/98 cells (7x7: 96/49), project 112/98
     // (dilation 2 -- DeepLab's output-stride-16 blocks on 33x33 maps -- as
     // NNSX_IRWD(1, 7, 7, 160, 10, 4, false, 2) etc. ran 156 vs 120 us for the
     // unfused expand GEMM + dilated depthwise + project GEMM at batch 8 (the
