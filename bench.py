@@ -344,7 +344,9 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
     # device-clock cross-check: the filter's end-of-invoke events of the same K batches
     ds = [tuple(int(v) for v in e.split(":")) for e in dev_stamps.split(",") if e]
     if len(ds) >= total and warmup > 0:
-        rec["gpu_elapsed"] = (ds[warmup + steps - 1][0] - ds[warmup - 1][0]) / 1e9
+        # (replay lanes: invokes may end out of order; the window runs from the
+        # last warmup end to the last timed end)
+        rec["gpu_elapsed"] = (max(d[0] for d in ds[:warmup + steps]) - max(d[0] for d in ds[:warmup])) / 1e9
         rec["gpu_busy_ms"] = float(np.median([d[1] for d in ds[warmup:warmup + steps]])) / 1e6
     return rec
 

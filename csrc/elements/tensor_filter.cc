@@ -637,7 +637,7 @@ class TensorFilter : public BaseTransform, public TransformAbsorber {
       } else {
         ret = inst_->invoke(model_in, &outs, ctx);
       }
-      if (dev_timing) dev_stamp_end(&ds, ctx.stream, ret);
+      if (dev_timing) dev_stamp_end(&ds, ctx.done_stream ? ctx.done_stream : ctx.stream, ret);
     }
     int64_t t1 = now_ns();
     if (!dev_timing) record_stats(t1 - t0, t1);

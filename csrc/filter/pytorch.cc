@@ -16,6 +16,10 @@
 //   broadcast:<rank>      load the model once: <rank> broadcasts the file's bytes
 //                         to every rank of the job (RCCL / TCP), see load_broadcast
 //   broadcast-backend:auto|rccl|tcp, broadcast-store:host:port, broadcast-name:<channel>
+//   lanes:<n>|auto        replay lanes (hipgraph): consecutive frames go round robin
+//                         to n streams, each with its own graphs and memory pool, so
+//                         the forwards of small batches overlap on the GPU (auto: 2
+//                         for a leading dimension of 2..32 and <= 8 MB of input, else 1)
 #include <ATen/hip/HIPGraph.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
@@ -32,6 +36,7 @@
 #include "filter/filter.h"
 #include "filter/torch_util.h"
 #include "kernels/kernels.h"
+#include "kernels/mbv2.h"
 #include "runtime/fusion.h"
 #include "runtime/hip_util.h"
 #include "runtime/plugin_api.h"
@@ -95,10 +100,17 @@ class TorchInstance : public FilterInstance {
   }
   ~TorchInstance() override {
     clear_graphs();
-    if (last_replay_ev_) {
-      hip::DeviceGuard g(last_replay_dev_);
-      (void)hipEventSynchronize(last_replay_ev_);
-      (void)hipEventDestroy(last_replay_ev_);
+    for (Lane& l : lanes_) {
+      hip::DeviceGuard g(l.dev);
+      if (l.last_ev) {
+        (void)hipEventSynchronize(l.last_ev);
+        (void)hipEventDestroy(l.last_ev);
+      }
+      if (l.in_ev) (void)hipEventDestroy(l.in_ev);
+      if (l.stream) {
+        (void)hipStreamSynchronize(l.stream);
+        (void)hipStreamDestroy(l.stream);
+      }
     }
     if (cap_stream_) {
       hip::DeviceGuard g(device_);
@@ -260,6 +272,7 @@ class TorchInstance : public FilterInstance {
       else if (k == "broadcast-backend") bcast_backend_ = v;
       else if (k == "broadcast-store") bcast_store_ = v;
       else if (k == "broadcast-name") bcast_name_ = v;
+      else if (k == "lanes") lanes_opt_ = lower(v) == "auto" ? 0 : std::max(1, std::min(kMaxLanes, static_cast<int>(to_int(v))));
     }
   }
 
@@ -445,6 +458,25 @@ class TorchInstance : public FilterInstance {
       inputs.push_back(torch::from_blob(ptr, sizes, opts));
     }
 
+    // replay lane: lane 0 runs on the element's stream, lane k > 0 on a private
+    // stream ordered after the inputs' arrival on s; everything below (replay,
+    // copy-out, output readiness, input release) is on that lane's stream
+    const int nl = dev_idx >= 0 && use_graph_ ? lane_count(inputs) : 1;
+    const int lane = nl > 1 ? static_cast<int>(invokes_++ % static_cast<uint64_t>(nl)) : 0;
+    if (lane > 0) {
+      Lane& l = lane_state(lane, dev_idx);
+      hip::check(hipEventRecord(l.in_ev, s), "lane input event");
+      hip::check(hipStreamWaitEvent(l.stream, l.in_ev, 0), "lane input wait");
+      s = l.stream;
+      ctx.done_stream = s;
+      sg.reset();  // (restores the caller's stream before the lane's guard records it)
+      sg = std::make_unique<c10::hip::HIPStreamGuardMasqueradingAsCUDA>(
+          c10::hip::getStreamFromExternalMasqueradingAsCUDA(s, static_cast<c10::DeviceIndex>(dev_idx)));
+    }
+    // more than one lane: kernels must not assume the device to themselves
+    kernels::SharedDeviceScope shared(nl > 1);
+    Lane& ln = lane_state(lane, dev_idx);
+
     std::vector<at::Tensor> outs;
     std::vector<MemoryPtr> host_outs;        // outputs already copied to pinned host memory
     std::shared_ptr<std::atomic<int>> held;  // static outputs handed out as they are
@@ -456,7 +488,7 @@ class TorchInstance : public FilterInstance {
       pref.id = static_cast<uint64_t>(root->tags().at(DeviceBufferPool::kPoolTag));
       pref.offset = static_cast<size_t>(static_cast<const char*>(in[0]->data()) - static_cast<const char*>(root->data()));
     }
-    GraphState* gs = use_graph_ && dev_idx >= 0 ? graph_for(inputs, s, dev_idx, pooled, pref) : nullptr;
+    GraphState* gs = use_graph_ && dev_idx >= 0 ? graph_for(inputs, s, dev_idx, pooled, pref, lane) : nullptr;
     if (gs) {
       // an instance whose static outputs no downstream element holds: the replay
       // rewrites them and hands them out as they are (no copy); they return to
@@ -471,8 +503,7 @@ class TorchInstance : public FilterInstance {
       // a replay the previous one's copy-out.  Elements sharing the instance
       // (shared-tensor-filter-key) each bring their own stream, so a replay on a
       // new stream first waits for the last one
-      if (last_replay_ev_ && last_replay_stream_ != s)
-        hip::check(hipStreamWaitEvent(s, last_replay_ev_, 0), "replay order wait");
+      if (ln.last_ev && ln.last_stream != s) hip::check(hipStreamWaitEvent(s, ln.last_ev, 0), "replay order wait");
       hip::check(hipGraphLaunch(gs->graph->raw_cuda_graph_exec(), s), "hipGraphLaunch");
       if (copy_out_ || gs->copy_out) {  // private copies of the outputs: the instance is free again
         for (size_t k = 0; k < gs->static_out.size(); ++k) {
@@ -497,12 +528,9 @@ class TorchInstance : public FilterInstance {
         held->store(1);
         outs = gs->static_out;
       }
-      if (!last_replay_ev_) {
-        last_replay_dev_ = dev_idx;
-        hip::check(hipEventCreateWithFlags(&last_replay_ev_, hipEventDisableTiming), "replay event");
-      }
-      hip::check(hipEventRecord(last_replay_ev_, s), "replay event record");
-      last_replay_stream_ = s;
+      if (!ln.last_ev) hip::check(hipEventCreateWithFlags(&ln.last_ev, hipEventDisableTiming), "replay event");
+      hip::check(hipEventRecord(ln.last_ev, s), "replay event record");
+      ln.last_stream = s;
     } else {
       std::vector<c10::IValue> iv;
       for (auto& t : inputs) iv.push_back(prepare(t));
@@ -558,8 +586,8 @@ class TorchInstance : public FilterInstance {
   };
 
   GraphState* graph_for(const std::vector<at::Tensor>& inputs, hipStream_t s, int dev_idx, bool pooled,
-                        const PoolRef& pref) {
-    std::string key;
+                        const PoolRef& pref, int lane) {
+    std::string key = lane ? "L" + std::to_string(lane) + "|" : std::string();
     for (auto& t : inputs) {
       for (auto d : t.sizes()) key += std::to_string(d) + "x";
       key += std::string(c10::toString(t.scalar_type())) + ";";
@@ -573,8 +601,8 @@ class TorchInstance : public FilterInstance {
         if (g->copy_out || copy_out_ || g->out_held->load() == 0) return g;
       } else if (in_place_count_[key] < kInPlace) {
         ++in_place_count_[key];
-        GraphState* g = capture(graphs_[pkey], inputs, s, dev_idx, pkey, true);
-        precapture_pool(inputs, key, s, dev_idx, pref);
+        GraphState* g = capture(graphs_[pkey], inputs, s, dev_idx, pkey, true, lane);
+        precapture_pool(inputs, key, s, dev_idx, pref, lane);
         return g;
       }
     }
@@ -582,14 +610,14 @@ class TorchInstance : public FilterInstance {
     for (auto& g : set)
       if (g->copy_out || g->out_held->load() == 0) return g.get();  // (never held with copy_out_)
     if (set.size() >= kInstances) return nullptr;
-    return capture(set, inputs, s, dev_idx, key, false);
+    return capture(set, inputs, s, dev_idx, key, false, lane);
   }
 
   // the other blocks of the input's pool get their in-place instances now, at
   // the first frame of this shape (a capture costs ~1 ms of host time: taken
   // lazily, each new block address stalled the stream once in steady state)
   void precapture_pool(const std::vector<at::Tensor>& inputs, const std::string& key, hipStream_t s, int dev_idx,
-                       const PoolRef& pref) {
+                       const PoolRef& pref, int lane) {
     if (!pref.id || inputs.size() != 1) return;
     auto pool = DeviceBufferPool::find(pref.id);
     if (!pool) return;
@@ -603,12 +631,12 @@ class TorchInstance : public FilterInstance {
       if (it != graphs_.end() && !it->second.empty()) continue;
       std::vector<at::Tensor> t{torch::from_blob(p, inputs[0].sizes(), inputs[0].options())};
       ++in_place_count_[key];
-      capture(graphs_[pk], t, s, dev_idx, pk, true);
+      capture(graphs_[pk], t, s, dev_idx, pk, true, lane);
     }
   }
 
   GraphState* capture(std::vector<std::unique_ptr<GraphState>>& set, const std::vector<at::Tensor>& inputs,
-                      hipStream_t s, int dev_idx, const std::string& key, bool in_place) {
+                      hipStream_t s, int dev_idx, const std::string& key, bool in_place, int lane) {
     hip::DeviceGuard dg(dev_idx);
     if (!cap_stream_) hip::check(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "capture stream");
     hipEvent_t ev;
@@ -627,7 +655,9 @@ class TorchInstance : public FilterInstance {
       // capture of this module, one pass before a copying instance; an in-place
       // instance (one more pooled block address of a shape already run) captures
       // straight away -- the extra eager forward cost a whole step of GPU time
-      const std::string shape = key.substr(0, key.find('@'));
+      const size_t bar = key.find('|'), at = key.find('@');
+      const size_t b0 = bar == std::string::npos ? 0 : bar + 1;
+      const std::string shape = key.substr(b0, at == std::string::npos ? std::string::npos : at - b0);
       const int warm = graphs_captured_ == 0 ? 3 : (in_place && warmed_.count(shape)) ? 0 : 1;
       warmed_.insert(shape);
       for (int w = 0; w < warm; ++w) {
@@ -638,11 +668,13 @@ class TorchInstance : public FilterInstance {
       }
       hip::check(hipStreamSynchronize(cap_stream_), "graph warmup sync");
       gs->graph = std::make_unique<at::cuda::CUDAGraph>();
-      // one memory pool for every graph of the instance: replays never overlap
-      // (replay order, do_invoke), so the activations of one instance's forward
-      // are allocated once, not once per pooled input block and output buffer
-      if (graph_pool_.first == 0 && graph_pool_.second == 0) graph_pool_ = at::cuda::graph_pool_handle();
-      gs->graph->capture_begin(graph_pool_, hipStreamCaptureModeThreadLocal);
+      // one memory pool for every graph of a lane: replays of a lane never
+      // overlap (one stream + replay order, do_invoke), so the activations of its
+      // forward are allocated once, not once per pooled input block and output
+      // buffer; lanes replay concurrently, so each has its own
+      at::cuda::MempoolId_t& pool = lanes_[static_cast<size_t>(lane)].pool;
+      if (pool.first == 0 && pool.second == 0) pool = at::cuda::graph_pool_handle();
+      gs->graph->capture_begin(pool, hipStreamCaptureModeThreadLocal);
       iv.clear();
       for (auto& t : src) iv.push_back(prepare(t));
       flatten(module_.forward(iv), &gs->static_out);
@@ -700,15 +732,48 @@ class TorchInstance : public FilterInstance {
   std::set<std::string> warmed_;                   // input shapes run eagerly before a capture
   void clear_graphs() {
     graphs_.clear();
-    graph_pool_ = {0, 0};  // the pool goes with its last graph
+    for (Lane& l : lanes_) l.pool = {0, 0};  // a pool goes with its last graph
     in_place_count_.clear();
     warmed_.clear();  // a reloaded module runs eagerly again before its first capture
   }
   size_t graphs_captured_ = 0;
-  at::cuda::MempoolId_t graph_pool_{0, 0};  // shared by every captured graph (capture)
-  hipEvent_t last_replay_ev_ = nullptr;     // end of the latest replay (+ copy-out)
-  hipStream_t last_replay_stream_ = nullptr;
-  int last_replay_dev_ = 0;
+  // replay lanes (custom=lanes): lane 0 replays on the element's stream
+  static constexpr int kMaxLanes = 4;
+  struct Lane {
+    int dev = 0;
+    hipStream_t stream = nullptr;           // lanes > 0: private stream
+    hipEvent_t in_ev = nullptr;             // lanes > 0: inputs arrived on the element's stream
+    at::cuda::MempoolId_t pool{0, 0};       // shared by every graph of the lane (capture)
+    hipEvent_t last_ev = nullptr;           // end of the lane's latest replay (+ copy-out)
+    hipStream_t last_stream = nullptr;
+  };
+  std::vector<Lane> lanes_ = std::vector<Lane>(kMaxLanes);
+  int lanes_opt_ = 0;  // custom=lanes:<n>; 0 = auto
+  uint64_t invokes_ = 0;
+  int lane_count(const std::vector<at::Tensor>& inputs) const {
+    static const int forced = [] {
+      const char* e = std::getenv("NNSX_TORCH_LANES");
+      return e ? std::max(0, std::min(kMaxLanes, std::atoi(e))) : 0;
+    }();
+    if (forced > 0) return forced;
+    if (lanes_opt_ > 0) return lanes_opt_;
+    if (inputs.empty() || inputs[0].dim() < 1) return 1;
+    size_t bytes = 0;
+    for (auto& t : inputs) bytes += t.numel() * t.element_size();
+    const int64_t b = inputs[0].size(0);
+    return b >= 2 && b <= 32 && bytes <= (8u << 20) ? 2 : 1;
+  }
+  Lane& lane_state(int lane, int dev_idx) {
+    Lane& l = lanes_[static_cast<size_t>(lane)];
+    if (lane > 0 && !l.stream) {
+      hip::DeviceGuard g(dev_idx);
+      l.dev = dev_idx;
+      hip::check(hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking), "lane stream");
+      hip::check(hipEventCreateWithFlags(&l.in_ev, hipEventDisableTiming), "lane event");
+    }
+    if (!l.last_ev) l.dev = dev_idx;
+    return l;
+  }
   hipStream_t cap_stream_ = nullptr;  // private capture stream (graph_for)
 };
 

@@ -148,6 +148,22 @@ struct IrBlockF32Args {
   // at once (the host checks occupancy); the wait is bounded.
   int spread = 0;
 };
+// Launches enqueued by this thread while a SharedDeviceScope is alive may run
+// concurrently with other kernels of the same process (a filter's replay
+// lanes): no form that waits inside a launch for other workgroups of the grid
+// (the spread combine above) -- it would assume a residency nothing guarantees.
+// Graph capture bakes the choice into the captured kernels.
+struct SharedDeviceScope {
+  explicit SharedDeviceScope(bool on);
+  ~SharedDeviceScope();
+  SharedDeviceScope(const SharedDeviceScope&) = delete;
+  SharedDeviceScope& operator=(const SharedDeviceScope&) = delete;
+
+ private:
+  bool prev_;
+};
+bool device_shared();
+
 bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout, bool has_expand, int dil = 1);
 // device workspace ir_block_f32 needs for these args (0 = none)
 size_t ir_block_f32_workspace_bytes(const IrBlockF32Args& a);

@@ -2266,6 +2266,11 @@ static int irw_inlaunch_mode() {
   return m;
 }
 
+static thread_local bool t_device_shared = false;
+SharedDeviceScope::SharedDeviceScope(bool on) : prev_(t_device_shared) { t_device_shared = prev_ || on; }
+SharedDeviceScope::~SharedDeviceScope() { t_device_shared = prev_; }
+bool device_shared() { return t_device_shared; }
+
 // the model's ticket buffer (ir_block_f32_tickets ints, zeroed once): the
 // spread form's 64-bit counters in [0, kSpreadTickets), the last-arriver
 // form's self-resetting ints after them (kLastTickets).  Hidden parts > 1 only
@@ -2311,7 +2316,7 @@ static bool launch_irw(const IrwCfg* c, IrBlockF32Args a, hipStream_t s) {
     // tile: only when every workgroup of the grid is resident at once (one
     // block per CU under what the occupancy query reports, which can over-report)
     int dev = 0, ncu = 0, per_cu = 0;
-    if (irw_inlaunch_mode() == 2 && 2 * tiles <= kSpreadTickets && hipGetDevice(&dev) == hipSuccess &&
+    if (irw_inlaunch_mode() == 2 && !device_shared() && 2 * tiles <= kSpreadTickets && hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(c->kernel), 64 * c->NW, lds) ==
             hipSuccess &&

@@ -57,6 +57,10 @@ struct InvokeContext {
   // decoders: >1 when out->mems holds one memory per frame of a batched input;
   // tensor_decoder then pushes them as consecutive buffers
   unsigned out_frames = 1;
+  // set by a filter instance whose device work for this invoke ended on another
+  // stream than `stream` (pytorch replay lanes): the element's end-of-invoke
+  // timing event goes there
+  hipStream_t done_stream = nullptr;
 };
 
 class FilterInstance {

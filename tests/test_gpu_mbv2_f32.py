@@ -419,6 +419,40 @@ def test_benched_launch_string_labels_match_torch_fp32(nns, workdir, labels, pre
     assert agree / total >= need, (agree, total)
 
 
+def test_replay_lanes_same_labels(nns, workdir, labels):
+    """custom=lanes:<n>: consecutive batches replay round robin on n streams
+    (own graphs and memory pool per lane; the in-launch combine then never
+    waits on other workgroups).  Every frame's label equals the one-lane run,
+    in order, with the absorbed argmax's indices read back on the lanes."""
+    import os
+
+    from nnstreamer_amd.models.export import export
+
+    model = export("mobilenet_v2_fused_fp32", os.path.join(workdir, "mbv2_f32_lanes.pt"), layout="nhwc")
+    B, nb = 8, 24
+
+    def run(lanes):
+        desc = (f"videotestsrc num-buffers={B * nb} pattern=snow pool-size=96 "
+                "! video/x-raw,format=RGB,width=224,height=224,framerate=0/1 "
+                f"! tensor_converter frames-per-tensor={B} device=0 ! queue max-size-buffers=2 "
+                f"! tensor_filter name=f framework=pytorch model={model} input=3:224:224:{B} inputtype=uint8 "
+                f"accelerator=true:gpu device=0 custom=hipgraph:true,lanes:{lanes} device-stats=true "
+                f"! queue max-size-buffers=4 ! tensor_decoder mode=image_labeling option1={labels} "
+                "! tensor_sink name=sink")
+        p = nns.parse_launch(desc)
+        out = []
+        p.get_by_name("sink").connect("new-data", lambda b: out.append(b.memory(0).bytes().decode()))
+        p.run(timeout=180)
+        stamps = [e for e in p.get_by_name("f").get_property("device-stamps").split(",") if e]
+        p.stop()
+        return out, stamps
+
+    one, st1 = run(1)
+    three, st3 = run(3)
+    assert len(one) == B * nb and len(st1) == nb and len(st3) == nb
+    assert three == one
+
+
 def test_filter_device_stats(nns, workdir, labels):
     """tensor_filter latency / throughput / device-stamps come from HIP events
     on the element's stream (device time), one record per invoke."""
