@@ -77,6 +77,13 @@ void flatten(const c10::IValue& v, std::vector<at::Tensor>* out) {
   }
 }
 
+// GPU model instances alive per device: with more than one, replays of
+// different filters may run at the same time, so kernels must not wait inside
+// a launch for workgroups that may not be resident (kernels::SharedDeviceScope)
+std::atomic<int> g_device_instances[64];
+
+int device_instances(int dev) { return dev >= 0 && dev < 64 ? g_device_instances[dev].load() : 0; }
+
 struct GraphState {
   std::unique_ptr<at::cuda::CUDAGraph> graph;
   std::vector<at::Tensor> static_in;  // the stable input slot the frame is copied into
@@ -97,8 +104,10 @@ class TorchInstance : public FilterInstance {
     parse_custom(p.custom_properties);
     device_ = p.device;
     load(p.model_files.at(0));
+    if (device_ >= 0 && device_ < 64) g_device_instances[device_].fetch_add(1);
   }
   ~TorchInstance() override {
+    if (device_ >= 0 && device_ < 64) g_device_instances[device_].fetch_sub(1);
     clear_graphs();
     for (Lane& l : lanes_) {
       hip::DeviceGuard g(l.dev);
@@ -473,8 +482,17 @@ class TorchInstance : public FilterInstance {
       sg = std::make_unique<c10::hip::HIPStreamGuardMasqueradingAsCUDA>(
           c10::hip::getStreamFromExternalMasqueradingAsCUDA(s, static_cast<c10::DeviceIndex>(dev_idx)));
     }
-    // more than one lane: kernels must not assume the device to themselves
-    kernels::SharedDeviceScope shared(nl > 1);
+    // more than one lane, or other model instances on the device: kernels must
+    // not assume the device to themselves.  Graphs captured under the other
+    // assumption are dropped and captured again
+    const bool shared_dev = dev_idx >= 0 && (nl > 1 || device_instances(dev_idx) > 1);
+    if (shared_dev != graphs_shared_) {
+      for (Lane& l : lanes_)
+        if (l.last_ev) hip::check(hipEventSynchronize(l.last_ev), "replays done");  // (graphs die below)
+      clear_graphs();
+      graphs_shared_ = shared_dev;
+    }
+    kernels::SharedDeviceScope shared(shared_dev);
     Lane& ln = lane_state(lane, dev_idx);
 
     std::vector<at::Tensor> outs;
@@ -749,6 +767,7 @@ class TorchInstance : public FilterInstance {
   };
   std::vector<Lane> lanes_ = std::vector<Lane>(kMaxLanes);
   int lanes_opt_ = 0;  // custom=lanes:<n>; 0 = auto
+  bool graphs_shared_ = false;  // graphs_ were captured under kernels::SharedDeviceScope
   uint64_t invokes_ = 0;
   int lane_count(const std::vector<at::Tensor>& inputs) const {
     static const int forced = [] {
