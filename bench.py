@@ -90,6 +90,7 @@ def parse_args(argv=None):
     ap.add_argument("--sweep-steps", type=int, default=10, help="timed steps per sweep point")
     ap.add_argument("--cpu", action="store_true", help="CPU reference path (device=-1, torch CPU)")
     ap.add_argument("--queue", type=int, default=4, help="queue depth between filter and decoder")
+    ap.add_argument("--queue-in", type=int, default=2, help="queue depth between converter and filter")
     ap.add_argument("--model-broadcast", default=os.environ.get("NNSX_BENCH_BCAST", "auto"),
                     choices=["off", "tcp", "rccl", "auto"],
                     help="N > 1: rank 0 broadcasts the model bytes to every rank at load over this data plane")
@@ -234,7 +235,7 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
     # the decoder's read-back overlaps the next forward.  The live batch-1
     # latency run keeps the whole chain in the source's streaming thread: no
     # queue hand-off on the path of a frame.
-    q1 = "! queue max-size-buffers=2 " if live_fps <= 0 else ""
+    q1 = f"! queue max-size-buffers={a.queue_in} " if live_fps <= 0 else ""
     q2 = f"! queue max-size-buffers={a.queue} " if live_fps <= 0 else ""
     desc = (
         f"videotestsrc num-buffers={frames} pattern=snow pool-size={pool} {live}"
