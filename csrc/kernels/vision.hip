@@ -226,22 +226,31 @@ __global__ void __launch_bounds__(256) pose_lines_kernel(PoseDrawArgs a) {
     xx = xe + kDotX[lane];
     if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) f[yy * a.W + xx] = 0xFFFFFFFFu;
   }
-  if (lane != 0) return;
+  // The host's Bresenham walk (err = (dx > dy ? dx : -dy) / 2; e2 > -dx steps
+  // x, e2 < dy steps y) in closed form, so the wave's lanes draw its pixels in
+  // parallel: with dx > dy x steps every iteration and after t steps y has
+  // stepped ceil((dy t - e0) / dx) times (e0 = dx / 2; the error stays in
+  // [0, dx) + dy t - dx ny(t) >= 0, so the x test always passes); dx <= dy is
+  // the mirror (y every step, x ceil((dx t - dy / 2) / dy) times).  The walk
+  // ends after max(dx, dy) steps: that many + 1 pixels, all the same value.
   const int dx = abs(xe - xs), sx = xs < xe ? 1 : -1;
   const int dy = abs(ye - ys), sy = ys < ye ? 1 : -1;
-  int err = (dx > dy ? dx : -dy) / 2;
-  while (true) {
-    pose_setpixel(f, a.W, a.H, xs, ys);
-    if (xs == xe && ys == ye) break;
-    const int e2 = err;
-    if (e2 > -dx) {
-      err -= dy;
-      xs += sx;
+  auto ceil_div = [](int n, int d) { return n >= 0 ? (n + d - 1) / d : -((-n) / d); };
+  const bool xmajor = dx > dy;
+  const int steps = xmajor ? dx : dy;
+  for (int t = lane; t <= steps; t += 64) {
+    int x, y;
+    if (xmajor) {
+      x = xs + sx * t;
+      y = ys + sy * ceil_div(dy * t - dx / 2, dx);
+    } else if (dy > 0) {
+      y = ys + sy * t;
+      x = xs + sx * ceil_div(dx * t - dy / 2, dy);
+    } else {  // (a single point)
+      x = xs;
+      y = ys;
     }
-    if (e2 < dy) {
-      err += dx;
-      ys += sy;
-    }
+    pose_setpixel(f, a.W, a.H, x, y);
   }
 }
 

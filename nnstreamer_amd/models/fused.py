@@ -37,6 +37,12 @@ FUSE_STEM = os.environ.get("NNSX_FUSE_STEM", "1") != "0"
 # NNSX_F32_HEAD_POOL=0: batches > 8 run the head GEMM and the average pool as two
 # kernels (A/B testing of the pooling GEMM epilogue)
 HEAD_POOL = os.environ.get("NNSX_F32_HEAD_POOL", "1") != "0"
+# NNSX_DWPW=1: depthwise + pointwise pairs as one dwpw GEMM (kernels/dwpw_f32.hip,
+# the depthwise computed in the GEMM's operand staging).  Off by default: it
+# recomputes the depthwise once per output-column tile, and measured slower
+# than the depthwise kernel + GEMM on every model (profiles/r4_dwpw_ab.txt:
+# PoseNet b64 16.2k vs 32.3k frames/s, DeepLab b8 4.5k vs 6.7k, SSD b64 20.4k vs 24.8k)
+DWPW = os.environ.get("NNSX_DWPW", "0") == "1"
 
 
 def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d):
@@ -187,8 +193,8 @@ class Block(nn.Module):
         self.min_tiles = 0
         self.use_ir = FUSE_IR and hid % 16 == 0 and (self.has_expand or hid == cin)
         # dilated blocks (DeepLab's output-stride-16 stage) that the fused kernel
-        # does not take: depthwise + project as one GEMM (NNSX_DWPW_DILATED=0: two launches)
-        self.dwpw_dilated = os.environ.get("NNSX_DWPW_DILATED", "1") != "0" and self.cout % 4 == 0
+        # does not take: depthwise + project as one GEMM with NNSX_DWPW=1 (A/B)
+        self.dwpw_dilated = DWPW and self.cout % 4 == 0
         # (A/B: every unfused block that way, e.g. MobileNetV2's 7x7 160 -> 960 -> 320)
         self.dwpw_all = os.environ.get("NNSX_DWPW_ALL", "0") == "1"
 

@@ -114,10 +114,10 @@ class FusedPoseNet(nn.Module):
         self.k = int(m.heatmap.out_channels)
         # fp32: every depthwise + pointwise pair as one GEMM with the depthwise in
         # its operand staging, and both 1x1 heads in one launch with exact columns
-        # (nnsx::dwpw, kernels/dwpw_f32.hip); NNSX_POSENET_DWPW=0 keeps 2 launches per pair
+        # (nnsx::dwpw, kernels/dwpw_f32.hip) with NNSX_DWPW=1; default: 2 launches per pair (measured faster)
         import os
 
-        self.fuse_dwpw = self.f32 and os.environ.get("NNSX_POSENET_DWPW", "1") != "0"
+        self.fuse_dwpw = self.f32 and os.environ.get("NNSX_DWPW", "0") == "1"
         return self
 
     def forward(self, x: torch.Tensor):

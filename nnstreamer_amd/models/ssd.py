@@ -20,7 +20,7 @@ from typing import List, Optional, Tuple
 import torch
 import torch.nn as nn
 
-from .fused import DW, PW, Block, StemBlock1, _fold, input_lut, stem
+from .fused import DW, DWPW, PW, Block, StemBlock1, _fold, input_lut, stem
 from .mobilenet_v2 import ConvBNReLU, MobileNetV2
 
 ANCHORS = (3, 6, 6, 6, 6, 6)
@@ -154,10 +154,11 @@ class FusedExtra(nn.Module):
         self.a = PW(*_fold(e[0][0], e[0][1]), act=1, precision=precision)
         self.d = DW(*_fold(e[1][0], e[1][1]), stride=2, precision=precision)
         self.c = PW(*_fold(e[2][0], e[2][1]), act=1, precision=precision)
+        self.dwpw = DWPW
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         h = self.a(x)
-        if self.c.wt.dtype == torch.float32 and h.is_cuda:
+        if self.dwpw and self.c.wt.dtype == torch.float32 and h.is_cuda:
             # the stride-2 depthwise inside the second pointwise GEMM (kernels/dwpw_f32.hip)
             wd: List[Optional[torch.Tensor]] = [self.d.w]
             bd: List[Optional[torch.Tensor]] = [self.d.bias]
@@ -190,11 +191,13 @@ class FusedSSDLite(nn.Module):
         self.box_heads = nn.ModuleList([FusedSepHead(h, 4, precision) for h in m.box_heads])
         self.cls_heads = nn.ModuleList([FusedSepHead(h, m.num_classes, precision) for h in m.cls_heads])
         self.feat_block = 13  # blocks[13] == features[14]: its expansion output is SSD feature 1
-        # fp32: all 12 heads (depthwise + predictor, box and class, 6 maps) in one
-        # grouped launch (nnsx::sep_heads); NNSX_SSD_SEP_HEADS=0 keeps 2 launches per head
+        # fp32 with NNSX_DWPW=1 (or NNSX_SSD_SEP_HEADS=1): all 12 heads (depthwise +
+        # predictor, box and class, 6 maps) in one grouped launch (nnsx::sep_heads);
+        # default: 2 launches per head (measured faster, fused.py DWPW)
         import os
 
-        self.one_launch_heads = self.f32 and os.environ.get("NNSX_SSD_SEP_HEADS", "1") != "0"
+        self.one_launch_heads = self.f32 and os.environ.get("NNSX_SSD_SEP_HEADS", "1" if DWPW else "0") != "0"
+        self.feat_dwpw = self.f32 and DWPW
         return self
 
     def forward(self, x: torch.Tensor):
@@ -204,7 +207,7 @@ class FusedSSDLite(nn.Module):
             if i == self.feat_block:
                 e = blk.expand(h)
                 feats.append(e)
-                if self.f32 and e.is_cuda and not blk.use_res:
+                if self.feat_dwpw and e.is_cuda and not blk.use_res:
                     wd: List[Optional[torch.Tensor]] = [blk.dw.w]
                     bd: List[Optional[torch.Tensor]] = [blk.dw.bias]
                     h = torch.ops.nnsx.dwpw([e], wd, bd, [blk.project.wt], [blk.project.bias], [blk.cout],

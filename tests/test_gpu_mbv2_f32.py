@@ -449,7 +449,9 @@ def test_replay_lanes_same_labels(nns, workdir, labels):
 
     one, st1 = run(1)
     three, st3 = run(3)
-    assert len(one) == B * nb and len(st1) == nb and len(st3) == nb
+    # (image_labeling: one buffer of B newline-separated labels per batch)
+    assert len(one) == nb and len(st1) == nb and len(st3) == nb
+    assert all(len(x.split("\n")) == B for x in one)
     assert three == one
 
 
