@@ -871,66 +871,11 @@ struct IrwGeom {
   // plane.  xs positions are XOR-swizzled with (kq & 3) so the staging writes
   // (8 consecutive lanes = 8 k-quads of one pixel) land in 4 slots, not 1.
   static constexpr int XSP = NC16;                    // xs plane stride (quads)
-  // Depthwise reads (ds_read_b128) are conflict-free when the 16 pixels of a
-  // pixel tile fall on 16 distinct 16-B bank slots (cell mod 16; a lane group
-  // mixes the lanes of two quad planes whose 16-quad-aligned strides drop out).
-  // Stride 2: the hidden image is stored column-deinterleaved -- cell (r, c) at
-  // r * RP + (c & 1) * HC + (c >> 1) -- so a tap reads consecutive cells, with a
-  // row pitch RP that puts the tile's next output row 8 (TX = 7, 8) or 4
-  // (TX = 4) slots on.  (Not the 7 x 7 stride-2 tile: its 154 KB of LDS has no
-  // room for the pitch.)  Stride 1 keeps the halo raster and orders the pixels
-  // instead (pix below).
-  static constexpr bool DEINT = S == 2 && DIL == 1 && !(TY == 7 && TX == 7);
-  static constexpr int HC = (TIX + 1) / 2;
-  static constexpr int RPM = TX == 4 ? 2 : 4;  // RP mod 8
-  static constexpr int RP = DEINT ? TIX + ((RPM - TIX % 8) + 8) % 8 : TIX;
-  static constexpr int CELLS = TIY * RP;  // hidden cells incl. the pitch padding
-  __host__ __device__ static constexpr int map(int c) {
-    return DEINT ? (c / TIX) * RP + ((c % TIX) & 1) * HC + ((c % TIX) >> 1) : c;
-  }
-  // hidden plane stride (quads); a scratch cell past the grid takes the
-  // expand's padding pixels (the compact expand, or a deinterleaved image)
-  static constexpr int PINP = (FULL && !DEINT) ? (PIN + 15) / 16 * 16 : CELLS / 16 * 16 + 16;
-  static constexpr int SCR = FULL && !DEINT ? 0 : CELLS;  // (FULL raster: padding cells are in the plane)
+  // hidden plane stride (quads); the compact expand (FULL = false) needs one
+  // scratch cell past the grid for padding pixels
+  static constexpr int PINP = FULL ? (PIN + 15) / 16 * 16 : PIN / 16 * 16 + 16;
   static constexpr int KQ = KIN / 4;
   static constexpr int NPT = (TY * TX + 15) / 16;     // output pixel tiles
-  // pixel (py, px) of lane li in pixel tile pt, valid = a real output pixel
-  // (padding lanes read the tile's first pixel: same address, a broadcast):
-  //   TX = 7: two rows per tile (slots x, x + 9 or 8), 14 lanes;  TX = 14: a row;
-  //   8 x 8, stride 1: rows pt and pt + 4 (40 cells = 8 slots apart); else raster
-  static constexpr int PMODE = TX == 7 ? 1 : TX == 14 ? 2 : (TX == 8 && TY == 8 && S == 1) ? 3 : 0;
-  static_assert(PMODE != 1 || (TY + 1) / 2 == NPT, "irw: two-row pixel tiles");
-  static_assert(PMODE != 2 || TY == NPT, "irw: one-row pixel tiles");
-  __device__ static void pix(int pt, int li, int* py, int* px, bool* valid) {
-    int y, x;
-    bool v;
-    if constexpr (PMODE == 1) {
-      const int hi = li >= 7;
-      y = 2 * pt + hi;
-      x = li - 7 * hi;
-      v = li < 14 && y < TY;
-    } else if constexpr (PMODE == 2) {
-      y = pt;
-      x = li;
-      v = li < 14;
-    } else if constexpr (PMODE == 3) {
-      y = pt + 4 * (li >> 3);
-      x = li & 7;
-      v = true;
-    } else {
-      const int q = pt * 16 + li;
-      y = q / TX;
-      x = q % TX;
-      v = q < TY * TX;
-    }
-    if (!v) {
-      y = PMODE == 3 ? pt : PMODE == 0 ? (pt * 16) / TX : PMODE == 1 ? 2 * pt : pt;
-      x = PMODE == 0 ? (pt * 16) % TX : 0;
-    }
-    *py = y;
-    *px = x;
-    *valid = v;
-  }
   static constexpr int NPX = NPT * 16;
   static constexpr size_t xs_q = static_cast<size_t>(KQ) * XSP;
   static constexpr size_t hid_q = static_cast<size_t>(4 * NW) * PINP;     // [wave][quad][cell]
@@ -1051,36 +996,28 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
     for (int v = tid; v < 4 * NW * PIN; v += NT) {
       const int pl = v / PIN, p = v - pl * PIN;
       const int yy = iy0 + p / TIX, xx = ix0 + p % TIX;
-      if (yy < ry0 || yy >= ry1 || xx < rx0 || xx >= rx1) hidw[pl * PINP + G::map(p)] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      if (yy < ry0 || yy >= ry1 || xx < rx0 || xx >= rx1) hidw[pl * PINP + p] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     }
   }
-  // expand pixel j*16+li -> its hidden cell (compact; deinterleaved FULL), or
-  // the in-image flag (FULL raster)
+  // expand pixel j*16+li -> its hidden cell (compact), or in-image flag (FULL)
   int hcell[NBT];
 #pragma unroll
   for (int j = 0; j < NBT; ++j) {
     const int c = j * 16 + li;
     if constexpr (FULL) {
       const int yy = iy0 + c / TIX, xx = ix0 + c % TIX;
-      const bool in = c < PIN && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
-      if constexpr (G::DEINT)
-        hcell[j] = (c < PIN ? G::map(c) : G::SCR) | (in ? 0 : (1 << 30));  // bit 30: write zeros
-      else
-        hcell[j] = in ? 1 : 0;
+      hcell[j] = (c < PIN && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) ? 1 : 0;
     } else {
       const int cy = static_cast<int>((static_cast<float>(c) + 0.5f) * rrw);
-      hcell[j] = c < NC ? G::map((ry0 + cy - iy0) * TIX + (rx0 + c - cy * RW - ix0)) : G::SCR;  // SCR: scratch
+      hcell[j] = c < NC ? (ry0 + cy - iy0) * TIX + (rx0 + c - cy * RW - ix0) : PIN;  // PIN: scratch cell
     }
   }
-  // depthwise window origin of each pixel tile's lane (mapped cells) and the
-  // per-tap offsets (compile time)
   int dcell[NPT];
 #pragma unroll
   for (int pt = 0; pt < NPT; ++pt) {
-    int py, px;
-    bool pv;
-    G::pix(pt, li, &py, &px, &pv);
-    dcell[pt] = G::DEINT ? S * py * G::RP + px : (py * S * TIX + px * S);
+    const int q = pt * 16 + li;
+    const int qq = q < TY * TX ? q : 0;
+    dcell[pt] = (qq / TX) * S * TIX + (qq % TX) * S;
   }
   const int nbt = (NC + 15) / 16;  // pixel tiles holding in-image pixels (wave-uniform)
 
@@ -1178,11 +1115,7 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
             e0 = mfma_k8(et, t0[g & 1], e0);
             e1 = mfma_k8(et, t1[g & 1], e1);
           }
-          if constexpr (FULL && G::DEINT) {
-            const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
-            myhid[hcell[j] & 0xffff] = (hcell[j] >> 30) ? z : relu6x4(e0 + be4);
-            if (j + 1 < NBT) myhid[hcell[j1] & 0xffff] = (hcell[j1] >> 30) ? z : relu6x4(e1 + be4);
-          } else if constexpr (FULL) {
+          if constexpr (FULL) {
             const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
             myhid[j * 16 + li] = hcell[j] ? relu6x4(e0 + be4) : z;
             if (j + 1 < NBT) myhid[j1 * 16 + li] = hcell[j1] ? relu6x4(e1 + be4) : z;
@@ -1200,10 +1133,10 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
       // t = 1: the hidden channels are the input channels
 #pragma unroll
       for (int j = 0; j < NBT; ++j) {
-        if constexpr (FULL && !G::DEINT)
+        if constexpr (FULL)
           myhid[j * 16 + li] = xs[(hs * 4 + g) * XSP + j * 16 + (li ^ g)];  // (staged zeros outside the image)
-        else
-          myhid[hcell[j] & 0xffff] = xs[(hs * 4 + g) * XSP + j * 16 + (li ^ g)];
+        else if (hcell[j] >= 0)
+          myhid[hcell[j]] = xs[(hs * 4 + g) * XSP + j * 16 + (li ^ g)];
       }
     }
     wave_sync();
@@ -1217,17 +1150,13 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
 #pragma unroll
       for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          const int toff = G::DEINT ? ky * G::RP + (kx & 1) * G::HC + (kx >> 1) : (ky * TIX + kx) * DIL;
-          d = __builtin_elementwise_fma(myhid[dcell[pt] + toff], wd4[ky * 3 + kx], d);
-        }
+        for (int kx = 0; kx < 3; ++kx)
+          d = __builtin_elementwise_fma(myhid[dcell[pt] + (ky * TIX + kx) * DIL], wd4[ky * 3 + kx], d);
       const f32x4_t bf = relu6x4(d);
       if constexpr (NOT == 0) {
-        int py, px;
-        bool pv;
-        G::pix(pt, li, &py, &px, &pv);
-        const int gy = oy0 + py, gx = ox0 + px;
-        if (pv && gy < a.Ho && gx < a.Wo)
+        const int q = pt * 16 + li;
+        const int gy = oy0 + q / TX, gx = ox0 + q % TX;
+        if (q < TY * TX && gy < a.Ho && gx < a.Wo)
           *reinterpret_cast<f32x4_t*>(a.y + ((static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx) * a.hid + ch) = bf;
         continue;
       }
@@ -1250,15 +1179,12 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
     __syncthreads();
     const int co = o * 16 + 4 * g;
     for (int pt = wave; pt < NPT; pt += NW) {
-      const int q = pt * 16 + li;  // (pixel slot)
+      const int q = pt * 16 + li;
       f32x4_t v = rb[g * NPX + q];
 #pragma unroll
       for (int w = 1; w < NW; ++w) v += rb[(4 * w + g) * NPX + q];
-      int py, px;
-      bool pv;
-      G::pix(pt, li, &py, &px, &pv);
-      if (!pv || co >= a.cout) continue;
-      const int gy = oy0 + py, gx = ox0 + px;
+      if (q >= TY * TX || co >= a.cout) continue;
+      const int gy = oy0 + q / TX, gx = ox0 + q % TX;
       if (gy >= a.Ho || gx >= a.Wo) continue;
       const int64_t pix = (static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx;
       if (a.ws) {  // hidden parts: this part's slab of the workspace (irw_reduce adds them in order)
@@ -1534,28 +1460,23 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) stem_ir1_f32_kernel(StemIr1F3
 template <int TY, int TX, bool PAIR>
 __global__ void __launch_bounds__(64, 2) stem_ir1w_f32_kernel(StemIr1F32Args a) {
   constexpr int HY = TY + 2, HX = TX + 2, PIN = HY * HX;
-  // hidden planes 16-quad aligned: a ds_read_b128 lane group of the depthwise
-  // mixes lanes of quad planes g and g + 1, whose cells then fall on distinct
-  // 16-B bank slots (PIN = 100 put half the groups 2-way on one slot)
-  constexpr int PINP = (PIN + 15) / 16 * 16;
   constexpr int NBT = (PIN + 15) / 16;
   constexpr int IY = 2 * HY + 1, IX = 2 * HX + 1, PITCH = IX * 3;
   constexpr int NIN = IY * PITCH;
   constexpr int XIN = (NIN + 3) / 4 * 4;
   constexpr int NPT = (TY * TX + 15) / 16;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* xin = smem;                                       // [IY][PITCH] normalised input
-  f32x4_t* hid = reinterpret_cast<f32x4_t*>(smem + XIN);  // [8 quads][PINP] (32 channels)
+  float* xin = smem;                                             // [IY][PITCH] normalised input
+  float* lut = smem + XIN;                                       // [256] input table
+  f32x4_t* hid = reinterpret_cast<f32x4_t*>(smem + XIN + 256);  // [8 quads][PIN] (32 channels)
 
   const int lane = threadIdx.x;
   const int li = lane & 15, g = lane >> 4;
   const int tiles_img = a.tiles_x * a.tiles_y;
   const int ntiles = tiles_img * a.B;
 
-  // (the 256-entry input table is read from global memory, L1-resident: in LDS
-  // its data-dependent gathers were bank-conflicted and it kept the hidden
-  // planes from their 16-quad alignment at 8 waves per CU)
-  const float* __restrict__ lut = a.lut;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) lut[lane * 4 + i] = a.lut[lane * 4 + i];
   float sa[2][7];  // stem weights: half h, k = 4t + g (27 taps + 1 zero); A row li = channel 16h + li
   int off[7];
 #pragma unroll
@@ -1615,9 +1536,11 @@ __global__ void __launch_bounds__(64, 2) stem_ir1w_f32_kernel(StemIr1F32Args a) 
     const int tyx = tile - b * tiles_img;
     const int oy0 = (tyx / a.tiles_x) * TY, ox0 = (tyx % a.tiles_x) * TX;
     const int hy0 = oy0 - 1, hx0 = ox0 - 1;  // hidden halo origin (stem-output coords)
-    __syncthreads();  // (one wave: orders the previous tile's LDS reads before these writes)
+    __syncthreads();  // (one wave: orders the previous tile's LDS reads before these writes; lut on entry)
     if (lane < PITCH) {
-      // all table reads first, then the stores
+      // all table reads first, then the stores: lut and xin share the LDS
+      // array, so read / store pairs in one loop were ordered one after the
+      // other (an LDS round trip per patch row)
       float nv[IY];
 #pragma unroll
       for (int r = 0; r < IY; ++r) nv[r] = lut[raw[r] >= 0 ? raw[r] : 0];
@@ -1657,8 +1580,8 @@ __global__ void __launch_bounds__(64, 2) stem_ir1w_f32_kernel(StemIr1F32Args a) 
       for (int t = 0; t < 7; ++t) xv[t] = xn[t];
       if (c < PIN) {
         const bool in = hy0 + hy >= 0 && hy0 + hy < a.Ho && hx0 + hx >= 0 && hx0 + hx < a.Wo;
-        hid[g * PINP + c] = in ? relu6x4(e0 + bs4[0]) : z;
-        hid[(4 + g) * PINP + c] = in ? relu6x4(e1 + bs4[1]) : z;
+        hid[g * PIN + c] = in ? relu6x4(e0 + bs4[0]) : z;
+        hid[(4 + g) * PIN + c] = in ? relu6x4(e1 + bs4[1]) : z;
       }
     }
     __syncthreads();
@@ -1677,7 +1600,7 @@ __global__ void __launch_bounds__(64, 2) stem_ir1w_f32_kernel(StemIr1F32Args a) 
         f32x4_t acc0 = z, acc1 = z;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const f32x4_t* hp = hid + (4 * h + g) * PINP + oy * HX + ox;
+          const f32x4_t* hp = hid + (4 * h + g) * PIN + oy * HX + ox;
           f32x4_t d0 = bd4[h], d1 = bd4[h];
 #pragma unroll
           for (int r = 0; r < 4; ++r)
@@ -1706,7 +1629,7 @@ __global__ void __launch_bounds__(64, 2) stem_ir1w_f32_kernel(StemIr1F32Args a) 
         f32x4_t acc = z;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const f32x4_t* hp = hid + (4 * h + g) * PINP + cell;
+          const f32x4_t* hp = hid + (4 * h + g) * PIN + cell;
           f32x4_t d = bd4[h];
 #pragma unroll
           for (int ky = 0; ky < 3; ++ky)
@@ -1972,19 +1895,11 @@ struct IrwCfg {
   void (*kernel)(IrBlockF32Args);
   size_t (*lds)(int);
   int dil = 1;
-  // > 0: only for exactly tiled maps and batches >= min_batch (find_irw with the
-  // launch's batch; a support query without one never picks it)
-  int min_batch = 0;
 };
 #define NNSX_IRW(S, TY, TX, KIN, NOT, NW, F)                                                    \
   IrwCfg {                                                                                      \
     S, TY, TX, KIN, NOT, NW, F, &irw_f32_kernel<S, TY, TX, KIN, NOT, NW, F>,                    \
         &IrwGeom<S, TY, TX, KIN, NOT, NW, F>::lds_bytes, 1                                      \
-  }
-#define NNSX_IRWB(S, TY, TX, KIN, NOT, NW, F, MB)                                               \
-  IrwCfg {                                                                                      \
-    S, TY, TX, KIN, NOT, NW, F, &irw_f32_kernel<S, TY, TX, KIN, NOT, NW, F>,                    \
-        &IrwGeom<S, TY, TX, KIN, NOT, NW, F>::lds_bytes, 1, MB                                  \
   }
 #define NNSX_IRWD(S, TY, TX, KIN, NOT, NW, F, D)                                                \
   IrwCfg {                                                                                      \
@@ -2000,10 +1915,6 @@ const IrwCfg kIrwCfgs[] = {
     NNSX_IRW(2, 7, 4, 24, 2, 3, true),     // 56 -> 28   24 -> 144 -> 32  (9)
     NNSX_IRW(1, 7, 7, 32, 2, 4, false),    // 28x28      32 -> 192 -> 32  (12)
     NNSX_IRW(2, 2, 7, 32, 4, 4, false),    // 28 -> 14   32 -> 192 -> 64  (12)
-    // 14x14 64 -> 384 -> 64 at batch >= 16: 7 x 14 tiles (expand 144 / 98 cells, project
-    // 112 / 98 against 96 / 49, 64 / 49 at 7 x 7), 127.9 vs 140.5 us per block at batch 512
-    // (profiles/r4_fp32_layers_b512_t714.txt); small batches keep the 7 x 7 tiles' parallelism
-    NNSX_IRWB(1, 7, 14, 64, 4, 4, false, 16),
     NNSX_IRW(1, 7, 7, 64, 4, 4, false),    // 14x14      64 -> 384 -> 64  (24)
     NNSX_IRW(1, 7, 7, 64, 6, 4, false),    // 14x14      64 -> 384 -> 96  (24)
     NNSX_IRW(1, 7, 7, 96, 6, 4, false),    // 14x14      96 -> 576 -> 96  (36)
@@ -2019,6 +1930,7 @@ const IrwCfg kIrwCfgs[] = {
     NNSX_IRW(1, 8, 16, 24, 2, 3, true),    // 56x56: expand 192/128 (8x8: 112/64)
     NNSX_IRW(2, 4, 8, 24, 2, 3, true),     // 56 -> 28: expand 160/128 input px (4x4: 96/64)
     NNSX_IRW(2, 8, 8, 16, 2, 3, true),     // 112 -> 56: expand 304/256 (4x8: 160/128)
+    NNSX_IRW(1, 7, 14, 64, 4, 4, false),   // 14x14 64 -> 384 -> 64: expand / project 112/98 cells (7x7: 64/49)
     NNSX_IRW(1, 7, 14, 64, 6, 4, false),   // 14x14 64 -> 384 -> 96
     NNSX_IRW(1, 7, 14, 96, 6, 4, false),   // 14x14 96 -> 576 -> 96: expand 144/98 cells (7x7: 96/49), project 112/98
     // (dilation 2 -- DeepLab's output-stride-16 blocks on 33x33 maps -- as
@@ -2031,7 +1943,6 @@ const IrwCfg kIrwCfgs[] = {
     // workgroup; profiles/r3_irw_waves_ab_b512.txt)
 };
 #undef NNSX_IRW
-#undef NNSX_IRWB
 #undef NNSX_IRWD
 
 // indices of kIrwCfgs that find_irw skips (A/B experiments): NNSX_IRW_SKIP=1,4
@@ -2059,7 +1970,7 @@ bool irw_enabled() {
   return on;
 }
 
-const IrwCfg* find_irw(int S, int H, int W, int cin, int hid, int cout, bool has_expand, int dil = 1, int B = 0) {
+const IrwCfg* find_irw(int S, int H, int W, int cin, int hid, int cout, bool has_expand, int dil = 1) {
   if (!irw_enabled() || !has_expand || hid % 16) return nullptr;
   const int kin = (cin + 7) / 8 * 8;
   const int nout = (cout + 15) / 16;
@@ -2070,7 +1981,7 @@ const IrwCfg* find_irw(int S, int H, int W, int cin, int hid, int cout, bool has
     for (size_t i = 0; i < sizeof(kIrwCfgs) / sizeof(kIrwCfgs[0]); ++i) {
       const IrwCfg& c = kIrwCfgs[i];
       if (c.S == S && c.dil == dil && c.KIN == kin && c.NOT == nout && (!exact || (Ho % c.TY == 0 && Wo % c.TX == 0)) &&
-          c.lds(hid) <= 160 * 1024 && !irw_skipped(i) && (c.min_batch == 0 || (exact && B >= c.min_batch)))
+          c.lds(hid) <= 160 * 1024 && !irw_skipped(i))
         return &c;
     }
   return nullptr;
@@ -2457,7 +2368,7 @@ bool ir_expand_dw_f32(const IrBlockF32Args& args, hipStream_t s) {
 
 size_t ir_block_f32_workspace_bytes(const IrBlockF32Args& args) {
   IrBlockF32Args a = args;
-  const IrwCfg* c = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0, a.dil, a.B);
+  const IrwCfg* c = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0, a.dil);
   if (!c) return 0;
   irw_geometry(c, &a);
   if (a.hsplit < 2 || (a.hsplit == 2 && irw_atomic2())) return 0;
@@ -2478,7 +2389,7 @@ size_t ir_block_f32_tickets(const IrBlockF32Args& args) {
   const int mode = irw_inlaunch_mode();
   if (!mode || !ir_block_f32_workspace_bytes(args)) return 0;
   IrBlockF32Args a = args;
-  const IrwCfg* c = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0, a.dil, a.B);
+  const IrwCfg* c = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0, a.dil);
   if (!c || c->NOT == 0) return 0;
   irw_geometry(c, &a);
   return a.tiles_x * a.tiles_y * a.B <= kLastTickets ? kSpreadTickets + kLastTickets : 0;
@@ -2495,9 +2406,9 @@ size_t stem_ir1_lds_bytes() {
 // one-wave-per-tile variant (stem_ir1w_f32_kernel): 8 x 8 tiles
 constexpr int kStemW = 8;
 static size_t stem_ir1w_lds_bytes() {
-  constexpr int HY = kStemW + 2, HX = kStemW + 2, PINP = (HY * HX + 15) / 16 * 16;
+  constexpr int HY = kStemW + 2, HX = kStemW + 2, PIN = HY * HX;
   constexpr int NIN = (2 * HY + 1) * (2 * HX + 1) * 3;
-  return static_cast<size_t>((NIN + 3) / 4 * 4) * 4 + 16 * 8 * PINP;  // 19.6 KB: 8 waves per CU
+  return static_cast<size_t>((NIN + 3) / 4 * 4 + 256) * 4 + 16 * 8 * PIN;
 }
 
 static bool stem_ir1w_f32(StemIr1F32Args a, hipStream_t s) {
@@ -2587,8 +2498,7 @@ bool stem_ir1_f32(const StemIr1F32Args& args, hipStream_t s) {
 
 bool ir_block_f32(const IrBlockF32Args& args, hipStream_t s) {
   IrBlockF32Args a = args;
-  if (const IrwCfg* w = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0, a.dil, a.B))
-    return launch_irw(w, a, s);
+  if (const IrwCfg* w = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0, a.dil)) return launch_irw(w, a, s);
   if (a.dil != 1) return false;
   const IrF32Cfg* c = find_cfg(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0);
   if (!c) return false;
