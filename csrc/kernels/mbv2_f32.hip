@@ -1895,11 +1895,19 @@ struct IrwCfg {
   void (*kernel)(IrBlockF32Args);
   size_t (*lds)(int);
   int dil = 1;
+  // > 0: only for exactly tiled maps and batches >= min_batch (find_irw with the
+  // launch's batch; a support query without one never picks it)
+  int min_batch = 0;
 };
 #define NNSX_IRW(S, TY, TX, KIN, NOT, NW, F)                                                    \
   IrwCfg {                                                                                      \
     S, TY, TX, KIN, NOT, NW, F, &irw_f32_kernel<S, TY, TX, KIN, NOT, NW, F>,                    \
         &IrwGeom<S, TY, TX, KIN, NOT, NW, F>::lds_bytes, 1                                      \
+  }
+#define NNSX_IRWB(S, TY, TX, KIN, NOT, NW, F, MB)                                               \
+  IrwCfg {                                                                                      \
+    S, TY, TX, KIN, NOT, NW, F, &irw_f32_kernel<S, TY, TX, KIN, NOT, NW, F>,                    \
+        &IrwGeom<S, TY, TX, KIN, NOT, NW, F>::lds_bytes, 1, MB                                  \
   }
 #define NNSX_IRWD(S, TY, TX, KIN, NOT, NW, F, D)                                                \
   IrwCfg {                                                                                      \
@@ -1915,6 +1923,10 @@ const IrwCfg kIrwCfgs[] = {
     NNSX_IRW(2, 7, 4, 24, 2, 3, true),     // 56 -> 28   24 -> 144 -> 32  (9)
     NNSX_IRW(1, 7, 7, 32, 2, 4, false),    // 28x28      32 -> 192 -> 32  (12)
     NNSX_IRW(2, 2, 7, 32, 4, 4, false),    // 28 -> 14   32 -> 192 -> 64  (12)
+    // 14x14 64 -> 384 -> 64 at batch >= 16: 7 x 14 tiles (expand 144 / 98 cells, project
+    // 112 / 98 against 96 / 49, 64 / 49 at 7 x 7), 127.9 vs 140.5 us per block at batch 512
+    // (profiles/r4_fp32_layers_b512_t714.txt); small batches keep the 7 x 7 tiles' parallelism
+    NNSX_IRWB(1, 7, 14, 64, 4, 4, false, 16),
     NNSX_IRW(1, 7, 7, 64, 4, 4, false),    // 14x14      64 -> 384 -> 64  (24)
     NNSX_IRW(1, 7, 7, 64, 6, 4, false),    // 14x14      64 -> 384 -> 96  (24)
     NNSX_IRW(1, 7, 7, 96, 6, 4, false),    // 14x14      96 -> 576 -> 96  (36)
@@ -1930,7 +1942,6 @@ const IrwCfg kIrwCfgs[] = {
     NNSX_IRW(1, 8, 16, 24, 2, 3, true),    // 56x56: expand 192/128 (8x8: 112/64)
     NNSX_IRW(2, 4, 8, 24, 2, 3, true),     // 56 -> 28: expand 160/128 input px (4x4: 96/64)
     NNSX_IRW(2, 8, 8, 16, 2, 3, true),     // 112 -> 56: expand 304/256 (4x8: 160/128)
-    NNSX_IRW(1, 7, 14, 64, 4, 4, false),   // 14x14 64 -> 384 -> 64: expand / project 112/98 cells (7x7: 64/49)
     NNSX_IRW(1, 7, 14, 64, 6, 4, false),   // 14x14 64 -> 384 -> 96
     NNSX_IRW(1, 7, 14, 96, 6, 4, false),   // 14x14 96 -> 576 -> 96: expand 144/98 cells (7x7: 96/49), project 112/98
     // (dilation 2 -- DeepLab's output-stride-16 blocks on 33x33 maps -- as
@@ -1943,6 +1954,7 @@ const IrwCfg kIrwCfgs[] = {
     // workgroup; profiles/r3_irw_waves_ab_b512.txt)
 };
 #undef NNSX_IRW
+#undef NNSX_IRWB
 #undef NNSX_IRWD
 
 // indices of kIrwCfgs that find_irw skips (A/B experiments): NNSX_IRW_SKIP=1,4
@@ -1970,7 +1982,7 @@ bool irw_enabled() {
   return on;
 }
 
-const IrwCfg* find_irw(int S, int H, int W, int cin, int hid, int cout, bool has_expand, int dil = 1) {
+const IrwCfg* find_irw(int S, int H, int W, int cin, int hid, int cout, bool has_expand, int dil = 1, int B = 0) {
   if (!irw_enabled() || !has_expand || hid % 16) return nullptr;
   const int kin = (cin + 7) / 8 * 8;
   const int nout = (cout + 15) / 16;
@@ -1981,7 +1993,7 @@ const IrwCfg* find_irw(int S, int H, int W, int cin, int hid, int cout, bool has
     for (size_t i = 0; i < sizeof(kIrwCfgs) / sizeof(kIrwCfgs[0]); ++i) {
       const IrwCfg& c = kIrwCfgs[i];
       if (c.S == S && c.dil == dil && c.KIN == kin && c.NOT == nout && (!exact || (Ho % c.TY == 0 && Wo % c.TX == 0)) &&
-          c.lds(hid) <= 160 * 1024 && !irw_skipped(i))
+          c.lds(hid) <= 160 * 1024 && !irw_skipped(i) && (c.min_batch == 0 || (exact && B >= c.min_batch)))
         return &c;
     }
   return nullptr;
@@ -2368,7 +2380,7 @@ bool ir_expand_dw_f32(const IrBlockF32Args& args, hipStream_t s) {
 
 size_t ir_block_f32_workspace_bytes(const IrBlockF32Args& args) {
   IrBlockF32Args a = args;
-  const IrwCfg* c = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0, a.dil);
+  const IrwCfg* c = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0, a.dil, a.B);
   if (!c) return 0;
   irw_geometry(c, &a);
   if (a.hsplit < 2 || (a.hsplit == 2 && irw_atomic2())) return 0;
@@ -2389,7 +2401,7 @@ size_t ir_block_f32_tickets(const IrBlockF32Args& args) {
   const int mode = irw_inlaunch_mode();
   if (!mode || !ir_block_f32_workspace_bytes(args)) return 0;
   IrBlockF32Args a = args;
-  const IrwCfg* c = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0, a.dil);
+  const IrwCfg* c = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0, a.dil, a.B);
   if (!c || c->NOT == 0) return 0;
   irw_geometry(c, &a);
   return a.tiles_x * a.tiles_y * a.B <= kLastTickets ? kSpreadTickets + kLastTickets : 0;
@@ -2498,7 +2510,8 @@ bool stem_ir1_f32(const StemIr1F32Args& args, hipStream_t s) {
 
 bool ir_block_f32(const IrBlockF32Args& args, hipStream_t s) {
   IrBlockF32Args a = args;
-  if (const IrwCfg* w = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0, a.dil)) return launch_irw(w, a, s);
+  if (const IrwCfg* w = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0, a.dil, a.B))
+    return launch_irw(w, a, s);
   if (a.dil != 1) return false;
   const IrF32Cfg* c = find_cfg(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0);
   if (!c) return false;

@@ -213,7 +213,7 @@ def test_ir_block_f32_inlaunch_combine(nns, H, cin, hid, cout, stride, B):
     _close(ref, _ir_ref64(x, we, be, wd, bd, wp, bp, stride, cout, True, res), tol=5e-5)
 
 
-@pytest.mark.parametrize("skip", ["6,7,8", "0,1,2,3,4"])
+@pytest.mark.parametrize("skip", ["7,8,9", "6", "0,1,2,3,4"])
 def test_irw_tile_variants(skip):
     """The A/B tile configurations of the fused block (7 x 14 tiles on the
     14 x 14 blocks; 8 x 8 / 8 x 16 / 4 x 8 / 7 x 14 tiles on the 112 / 56 / 28
@@ -223,10 +223,12 @@ def test_irw_tile_variants(skip):
     import subprocess
     import sys
 
-    shapes = ("14,64,384,64,1;14,64,384,96,1;14,96,576,96,1" if skip == "6,7,8"
+    # (kIrwCfgs indices: 6 = the 7 x 14 64 -> 384 -> 64 default for batch >= 16,
+    # 7-9 = the 7 x 7 14x14 configurations, 0-4 = the 112 / 56 / 28 defaults)
+    shapes = ("14,64,384,64,1;14,64,384,96,1;14,96,576,96,1" if skip in ("7,8,9", "6")
               else "112,16,96,24,2;56,24,144,24,1;56,24,144,32,2;28,32,192,32,1")
     here = os.path.dirname(os.path.abspath(__file__))
-    r = subprocess.run([sys.executable, os.path.join(here, "_irw_variant_check.py"), shapes, "1,3,16"],
+    r = subprocess.run([sys.executable, os.path.join(here, "_irw_variant_check.py"), shapes, "1,3,16,32"],
                        env=dict(os.environ, NNSX_IRW_SKIP=skip), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
 
