@@ -18,7 +18,7 @@
 //   broadcast-backend:auto|rccl|tcp, broadcast-store:host:port, broadcast-name:<channel>
 //   lanes:<n>|auto        replay lanes (hipgraph): consecutive frames go round robin
 //                         to n streams, each with its own graphs and memory pool, so
-//                         the forwards of small batches overlap on the GPU (auto: 2
+//                         the forwards of small batches overlap on the GPU (auto: 3
 //                         for a leading dimension of 2..32 and <= 8 MB of input, else 1)
 #include <ATen/hip/HIPGraph.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
@@ -780,7 +780,9 @@ class TorchInstance : public FilterInstance {
     size_t bytes = 0;
     for (auto& t : inputs) bytes += t.numel() * t.element_size();
     const int64_t b = inputs[0].size(0);
-    return b >= 2 && b <= 32 && bytes <= (8u << 20) ? 2 : 1;
+    // (batch 8: 1 / 2 / 3 lanes 20.8k / 20.0k / 26.6k frames/s, batch 32 50.0k / 49.3k / 54.2k:
+    // profiles/r4_lanes_ab.txt)
+    return b >= 2 && b <= 32 && bytes <= (8u << 20) ? 3 : 1;
   }
   Lane& lane_state(int lane, int dev_idx) {
     Lane& l = lanes_[static_cast<size_t>(lane)];

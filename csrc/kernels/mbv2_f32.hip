@@ -2289,6 +2289,17 @@ bool device_shared() { return t_device_shared; }
 // below 256 tiles (irw_parts), so both regions hold every splitting launch.
 constexpr int kSpreadTickets = 512, kLastTickets = 256;
 
+// workgroups of configuration c the spread combine may keep waiting at once:
+// one per CU under what the occupancy query reports (it can over-report)
+static int irw_spread_slots(const IrwCfg* c, int hid) {
+  int dev = 0, ncu = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(c->kernel), 64 * c->NW,
+                                                   c->lds(hid)) != hipSuccess)
+    return 0;
+  return ncu * std::max(1, per_cu - 1);
+}
+
 static int irw_parts(const IrwCfg* c, int tiles, int hid) {
   const int nsub = hid / 16;
   if (c->NOT == 0)  // depthwise output: parts need no reduction, so fill the chip
@@ -2298,7 +2309,16 @@ static int irw_parts(const IrwCfg* c, int tiles, int hid) {
   if (forced > 0) return std::min(forced, std::max(1, nsub / c->NW));
   if (tiles >= 128) return 2;
   const int want = (512 + tiles - 1) / tiles;
-  return std::max(2, std::min(want, nsub / c->NW));
+  int parts = std::max(2, std::min(want, nsub / c->NW));
+  // more than 4 parts combine in the launch only in the spread form, which
+  // needs the whole grid resident: trim the parts to what fits when that
+  // keeps >= 3/4 of them (batch 8, 14x14 96 -> 576 -> 96: 8 parts of 32
+  // tiles instead of 9 and an irw_reduce launch)
+  if (parts > 4 && irw_inlaunch_mode() == 2) {
+    const int fit = irw_spread_slots(c, hid) / tiles;
+    if (fit < parts && 4 * fit >= 3 * parts) parts = fit;
+  }
+  return parts;
 }
 
 static void irw_geometry(const IrwCfg* c, IrBlockF32Args* a) {

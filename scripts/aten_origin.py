@@ -14,6 +14,8 @@ import sys
 
 
 def is_aten(n):
+    if "nnsx" in n:  # (irw_reduce_kernel etc.)
+        return False
     return "at::native" in n or n.startswith("void at::") or "reduce_kernel" in n or "elementwise_kernel" in n
 
 

@@ -25,7 +25,8 @@ total = 0
 for r in step:
     d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000
     total += d
-    name = re.sub(r"\(.*", "", r["Kernel_Name"]).replace("nnsx::kernels::(anonymous namespace)::", "")
+    name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("nnsx::kernels::", "")
+    name = re.sub(r"\(.*", "", name[5:] if name.startswith("void ") else name)
     g = r.get("Grid_Size_X", r.get("Grid_Size", ""))
     print(f"{(int(r['Start_Timestamp']) - t0) / 1000:9.1f} us  {d:8.1f} us  grid {g:>8}  {name[:90]}")
 span = (int(rows[b]["Start_Timestamp"]) - t0) / 1000

@@ -25,10 +25,12 @@ def main():
 
     frame = w * w * 3
     pool = max(2 * B, -(-512 * 2**20 // frame))  # 512 MiB ring: larger than the last-level cache
+    host = os.environ.get("UPLOAD_BENCH_HOST") == "1"  # reference: the same pipeline without the upload
+    dev = "" if host else " device=0"
     for rep in range(2):  # first pass warms the pools / code objects
         desc = (f"videotestsrc num-buffers={n * B} pattern=snow pool-size={min(pool, n * B)} "
                 f"! video/x-raw,format=RGB,width={w},height={w},framerate=0/1 "
-                f"! tensor_converter frames-per-tensor={B} device=0 ! tensor_sink name=sink sync-device=true")
+                f"! tensor_converter frames-per-tensor={B}{dev} ! tensor_sink name=sink sync-device=true")
         p = nns.parse_launch(desc)
         torch.cuda.synchronize()
         t = time.perf_counter()
@@ -37,6 +39,10 @@ def main():
         el = time.perf_counter() - t
         p.stop()
     mode = "padded DMA + unpad_rows" if os.environ.get("NNSX_CONVERTER_PADDED_DMA", "1") != "0" else "gather kernel"
+    if host:
+        mode = "host only, no upload"
+    elif os.environ.get("NNSX_CONVERTER_DMA_SPLIT", "1") != "1":
+        mode += f", {os.environ['NNSX_CONVERTER_DMA_SPLIT']} copy streams"
     print(f"width {w} batch {B} ({mode}): {n} batches in {el * 1e3:.1f} ms, {el / n * 1e6:.1f} us per batch, "
           f"{n * B * frame / el / 1e9:.2f} GB/s packed frames to HBM")
 
