@@ -254,6 +254,21 @@ void Memory::sync_ready() const {
 }
 
 void Memory::record_use(hipStream_t stream, int dev) {
+  // a read on device `dev` of a memory that lives elsewhere read its device
+  // mirror (map_device): the mirror is freed / recycled in the order of the
+  // stream that mapped it, so a reader on another stream (a filter's replay
+  // lane) must hold it too
+  MemoryPtr mirror;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = dev_mirror_.find(dev);
+    if (it != dev_mirror_.end()) mirror = it->second;
+  }
+  if (mirror) mirror->record_use(stream, dev);
+  record_use_self(stream, dev);
+}
+
+void Memory::record_use_self(hipStream_t stream, int dev) {
   Memory* r = root();
   std::lock_guard<std::mutex> lk(r->ev_mu_);
   // one event per reading stream: work on a stream completes in order, so the
@@ -315,11 +330,11 @@ const void* Memory::map_device(int dev, hipStream_t stream) {
   if (place_ == MemPlace::DEVICE) {
     wait_ready(stream);  // peer copy over xGMI after the producer
     if (size_) hip::check(hipMemcpyPeerAsync(mirror->data(), dev, data_, device_, size_, stream), "P2P");
-    record_use(stream, dev);
+    record_use_self(stream, dev);  // (mu_ is held: not record_use, which looks up the mirrors)
   } else {
     if (size_) hip::check(hipMemcpyAsync(mirror->data(), data_, size_, hipMemcpyHostToDevice, stream), "H2D");
     // a pinned source is read asynchronously: it must not be recycled before the copy ran
-    if (place_ == MemPlace::PINNED) record_use(stream, dev);
+    if (place_ == MemPlace::PINNED) record_use_self(stream, dev);
   }
   mirror->mark_ready(stream);
   dev_mirror_[dev] = mirror;

@@ -93,6 +93,7 @@ class Memory : public std::enable_shared_from_this<Memory> {
   const Memory* root() const { return parent_ ? parent_->root() : this; }
 
  private:
+  void record_use_self(hipStream_t stream, int dev);  // record_use without the device mirror
   void* data_;
   size_t size_;
   MemPlace place_;
