@@ -3,7 +3,8 @@
 (pinned ring of pre-rendered RGB frames whose rows are padded to 4 bytes, as
 GStreamer lays out 513- and 257-wide RGB) -> tensor_converter
 frames-per-tensor=B device=0 -> tensor_sink sync-device.  Reports the packed
-bytes per second that reach HBM.  NNSX_CONVERTER_PADDED_DMA=0 selects the
+bytes per second that reach HBM (a queue before the sink: the sink's device
+sync does not stall the converter).  NNSX_CONVERTER_PADDED_DMA=0 selects the
 previous per-frame gather kernel for the A/B.
 
     python scripts/upload_bench.py [width] [batch] [batches]
@@ -30,7 +31,8 @@ def main():
     for rep in range(2):  # first pass warms the pools / code objects
         desc = (f"videotestsrc num-buffers={n * B} pattern=snow pool-size={min(pool, n * B)} "
                 f"! video/x-raw,format=RGB,width={w},height={w},framerate=0/1 "
-                f"! tensor_converter frames-per-tensor={B}{dev} ! tensor_sink name=sink sync-device=true")
+                f"! tensor_converter frames-per-tensor={B}{dev} ! queue max-size-buffers=4 "
+                f"! tensor_sink name=sink sync-device=true")
         p = nns.parse_launch(desc)
         torch.cuda.synchronize()
         t = time.perf_counter()
