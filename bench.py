@@ -79,8 +79,9 @@ def parse_args(argv=None):
                     help="fused = nnsx CDNA4 kernels; torch = plain TorchScript/MIOpen model (fp32)")
     ap.add_argument("--latency-frames", type=int, default=int(os.environ.get("NNSX_BENCH_LAT_FRAMES", "300")),
                     help="frames of the batch-1 latency run (0 = skip)")
-    ap.add_argument("--latency-fps", type=int, default=int(os.environ.get("NNSX_BENCH_LAT_FPS", "500")),
-                    help="frame rate of the live camera in the batch-1 latency run")
+    ap.add_argument("--latency-fps", type=int, default=int(os.environ.get("NNSX_BENCH_LAT_FPS", "0")),
+                    help="frame rate of the live camera in the batch-1 latency run (0: the config's, "
+                         "500 unless the model needs longer per frame)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-absorb", "--no-fuse-norm", dest="no_absorb", action="store_true",
                     help="tensor_filter absorb-transform=false: the tensor_transform runs its own kernel and the "
@@ -118,7 +119,7 @@ CONFIGS = {
                         "option4=300:300 option5=300:300", per_frame=True,
                 metric="end-to-end frames/sec + p50 per-frame latency, SSD-MobileNet 300x300 + bounding_boxes + HIP NMS",
                 desc="SSDLite-MobileNetV2 300x300 (tensor_filter + bounding_boxes decoder, HIP NMS)"),
-    "deeplab": dict(size=513, model="deeplab_fused_lowres", norm="typecast:float32,div:255.0",
+    "deeplab": dict(size=513, model="deeplab_fused_lowres", norm="typecast:float32,div:255.0", lat_fps=100,
                     decoder="tensor_decoder mode=image_segment option1=tflite-deeplab option3=513:513", per_frame=True,
                     metric="end-to-end frames/sec + p50 per-frame latency, DeepLabV3 513x513 segmentation pipeline",
                     desc="DeepLabV3-MobileNetV2 513x513 (tensor_filter + image_segment decoder)"),
@@ -148,7 +149,7 @@ CONFIGS = {
                                  "+ edge RCCL all-gather",
                           desc="PoseNet-MobileNetV1 257x257 per rank, pose tensors all-gathered (edgesink/edgesrc "
                                "rccl-mode=allgather) into tensor_mux sync-mode=slowest"),
-    "posenet": dict(size=257, model="posenet_fused", norm="typecast:float32,add:-127.5,div:127.5",
+    "posenet": dict(size=257, model="posenet_fused", norm="typecast:float32,add:-127.5,div:127.5", lat_fps=250,
                     decoder="tensor_decoder mode=pose_estimation option1=640:480 option2=257:257 option3={pose} "
                             "option4=heatmap-offset", per_frame=True,
                     metric="end-to-end frames/sec + p50 per-frame latency, PoseNet 257x257 pipeline",
@@ -432,7 +433,7 @@ def main():
         model_path = os.path.join(workdir, f"{model_name}.pt")
         w1 = max(10, a.latency_frames // 5)
         lat_b1 = run_pipeline(a, nns, cfg, model_name, model_path, files, 1, a.latency_frames, w1, rank, world, dev,
-                              use_gpu, dist, live_fps=a.latency_fps)
+                              use_gpu, dist, live_fps=a.latency_fps or cfg.get("lat_fps", 500))
 
     # throughput / latency trade-off at smaller batches (same engine, same pipeline)
     sweep = []
@@ -530,7 +531,7 @@ def main():
             n = len(runs)
             out.update(p50_latency_ms_b1=round(float(per_rank[:, n * 5].max()), 3),
                        p99_latency_ms_b1=round(float(per_rank[:, n * 5 + 1].max()), 3),
-                       latency_b1_source=f"live camera, {a.latency_fps} frames/s, batch 1")
+                       latency_b1_source=f"live camera, {a.latency_fps or cfg.get('lat_fps', 500)} frames/s, batch 1")
         if sweep:
             n = len(runs)
             base_i = n * 5 + 2
