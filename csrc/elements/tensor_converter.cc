@@ -328,10 +328,13 @@ class TensorConverter : public Element {
       return m->size() == frame_size_ ? m : Memory::view(m, 0, frame_size_);
     }
     size_t stride = vinfo_.stride[0];
-    if (dev >= 0 && frames_per_tensor_ > 1 && m->place() != MemPlace::HOST && stride <= kernels::kGatherMaxStride &&
-        stride % 4 == 0 && m->size() >= stride * (vinfo_.height - 1) + row) {
-      // batched upload: the gather kernel strips the padding while reading the
-      // frame over the bus (the adapter piece is flagged padded)
+    if (dev >= 0 && m->place() != MemPlace::HOST && stride <= kernels::kGatherMaxStride && stride % 4 == 0 &&
+        m->size() >= stride * (vinfo_.height - 1) + row) {
+      // the padded frame goes to HBM as it is (one DMA, padded_dma) and one
+      // unpad_rows launch strips the padding -- batch 1 too: a 2D copy (one
+      // DMA descriptor per row) took 3.6 ms for a 513 x 513 RGB frame
+      // (scripts/b1_pipeline_probe.py: DeepLab batch-1 p50 4.2 ms, of which the
+      // converter 3.6)
       padded_frame_ = true;
       return m;
     }
