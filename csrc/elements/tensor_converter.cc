@@ -771,7 +771,7 @@ class TensorConverter : public Element {
     push_segment();
     set_timestamp(*in, frames_in);
 
-    if (frames_in == frames_out) {
+    if (frames_in == frames_out && !padded_frame_) {  // (a padded frame is unpacked through the adapter)
       if (dev >= 0) {
         auto nb = make_buffer();
         nb->copy_metadata_from(*in);
