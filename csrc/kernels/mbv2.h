@@ -69,6 +69,11 @@ struct YLayout {
   // (an image spans at most two row tiles: two addends, so the sum is order-free)
   int pool = 0;
 };
+// plain fp32 pointwise GEMM on hipBLASLt (blaslt.cc): y[M][N] = act(x . wt^T + bias) (+ res);
+// false = not taken (the caller runs its own kernel).  NNSX_F32_BLASLT=0 turns it off
+bool blaslt_enabled();
+bool blaslt_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
+                     int Kpad, int act, hipStream_t s);
 void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
                  int Kpad, int Npad, int act, hipStream_t s, int tile = 0, float* ws = nullptr,
                  const YLayout& yl = YLayout{});

@@ -42,6 +42,26 @@ def test_pw_conv_f32(nns, M, K, N, act, use_res):
     _close(y, ref)
 
 
+@pytest.mark.parametrize("M,K,N,act,use_res", [(18496, 512, 512, 1, False), (25088, 960, 320, 0, True),
+                                              (8712, 160, 960, 1, False), (4096, 128, 64, 0, False)])
+def test_pw_conv_f32_library_path(nns, M, K, N, act, use_res):
+    """Plain GEMMs with K >= 128 and M >= 2048 run on hipBLASLt (bias + clamp
+    epilogue, residual as C): fp64 oracle and bitwise repeatability."""
+    torch.manual_seed(M + K)
+    x = torch.randn(M, K, device="cuda")
+    wt = torch.randn((N + 15) // 16 * 16, K, device="cuda") / K ** 0.5
+    bias = torch.randn(wt.shape[0], device="cuda")
+    res = torch.randn(M, N, device="cuda") if use_res else None
+    ys = [torch.ops.nnsx.pw_conv(x, wt, bias, res, N, act, True) for _ in range(3)]
+    assert all(torch.equal(ys[0], y) for y in ys[1:])
+    ref = x.double().cpu() @ wt[:N].double().cpu().t() + bias[:N].double().cpu()
+    if use_res:
+        ref = ref + res.double().cpu()
+    if act == 1:
+        ref = ref.clamp(0, 6)
+    _close(ys[0], ref)
+
+
 def test_pw_conv_f32_identity_asymmetric(nns):
     # A = I with an asymmetric B catches transposed fragment / k-permutation bugs exactly
     M, K, N = 192, 64, 64
