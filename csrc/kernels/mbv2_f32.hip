@@ -2146,10 +2146,12 @@ size_t pw_gemm_f32_workspace_bytes(int M, int N, int Kpad, bool has_res, int til
 
 void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
                  int Kpad, int Npad, int act, hipStream_t s, int tile, float* ws, const YLayout& yl) {
-  // plain products with a deep enough K and enough rows: the library GEMM
-  // (blaslt.cc); its residual is the C operand (act must be none then)
+  // plain linear products (no activation: the projects) with a deep enough K
+  // and enough rows: the library GEMM (blaslt.cc), the residual as its C
+  // operand.  (Its bias + clamp epilogue returned the bare product on this
+  // ROCm: scripts/blaslt_probe.py -- the ReLU6 GEMMs stay on the engine's kernel.)
   if (tile == 0 && blaslt_enabled() && !yl.rpb && !yl.brpb && !yl.pool && K >= 128 && M >= 2048 && N >= 64 &&
-      (act == 0 || (act == 1 && !res)) && blaslt_gemm_f32(x, wt, bias, res, y, M, N, K, Kpad, act, s))
+      act == 0 && blaslt_gemm_f32(x, wt, bias, res, y, M, N, K, Kpad, act, s))
     return;
   if (use_small_m(M, Kpad, tile, yl)) {
     const dim3 grid(static_cast<unsigned>((N + 15) / 16), static_cast<unsigned>((M + 63) / 64));
