@@ -415,6 +415,10 @@ __global__ void __launch_bounds__(256) dw3x3_f32_kernel(const float* __restrict_
                                                         float* __restrict__ y,           // [B][Ho][Wo][C]
                                                         int B, int H, int W, int C, int Ho, int Wo, int stride,
                                                         int dil, int act) {
+  // act bit 1: the input is a pre-activation map (a linear GEMM's output whose
+  // ReLU6 was deferred to this consumer): clamp every tap to [0, 6]
+  const bool ic = (act & 2) != 0;
+  act &= 1;
   const uint32_t cg = static_cast<uint32_t>(C) >> 2;
   const uint32_t total = static_cast<uint32_t>(B) * Ho * Wo * cg;
   for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
@@ -433,7 +437,8 @@ __global__ void __launch_bounds__(256) dw3x3_f32_kernel(const float* __restrict_
       for (int kx = 0; kx < 3; ++kx) {
         const int ix = ox * stride - dil + kx * dil;
         if (ix < 0 || ix >= W) continue;
-        const f32x4_t xv = *reinterpret_cast<const f32x4_t*>(x + ((static_cast<int64_t>(b) * H + iy) * W + ix) * C + c);
+        f32x4_t xv = *reinterpret_cast<const f32x4_t*>(x + ((static_cast<int64_t>(b) * H + iy) * W + ix) * C + c);
+        if (ic) xv = relu6x4(xv);
         const f32x4_t wv = *reinterpret_cast<const f32x4_t*>(w + (ky * 3 + kx) * C + c);
         acc = __builtin_elementwise_fma(xv, wv, acc);
       }
@@ -452,6 +457,8 @@ __global__ void __launch_bounds__(256) dw3x3_f32_col_kernel(const float* __restr
                                                             const float* __restrict__ bias, float* __restrict__ y,
                                                             int B, int H, int W, int C, int Ho, int Wo, int act) {
   constexpr int NR = (R - 1) * S + 3;
+  const bool ic = (act & 2) != 0;  // (deferred input ReLU6, dw3x3_f32_kernel)
+  act &= 1;
   const uint32_t cg = static_cast<uint32_t>(C) >> 2;
   const uint32_t rg = static_cast<uint32_t>((Ho + R - 1) / R);
   const uint32_t total = static_cast<uint32_t>(B) * rg * Wo * cg;
@@ -480,6 +487,7 @@ __global__ void __launch_bounds__(256) dw3x3_f32_col_kernel(const float* __restr
         const int ix = ox * S - 1 + kx;
         xv[kx] = (ix >= 0 && ix < W) ? *reinterpret_cast<const f32x4_t*>(xb + (static_cast<int64_t>(iy) * W + ix) * C)
                                      : f32x4_t{0.f, 0.f, 0.f, 0.f};
+        if (ic) xv[kx] = relu6x4(xv[kx]);
       }
 #pragma unroll
       for (int j = 0; j < R; ++j) {

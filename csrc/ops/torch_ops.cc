@@ -328,6 +328,7 @@ at::Tensor dw_conv_cuda(const at::Tensor& x, const at::Tensor& w, const at::Tens
                              static_cast<int>(stride), static_cast<int>(dilation), static_cast<int>(act), cur_stream());
     return y;
   }
+  TORCH_CHECK(act < 2, "dw_conv: the deferred input activation (act bit 1) is fp32 only");
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() == 4, "dw_conv: x [B,H,W,C] bf16");
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   TORCH_CHECK(C % 8 == 0 && w.numel() == 9 * C && w.scalar_type() == at::kBFloat16, "dw_conv: w [9,C] bf16, C%8==0");
@@ -343,6 +344,8 @@ at::Tensor dw_conv_cpu(const at::Tensor& x, const at::Tensor& w, const at::Tenso
                        int64_t dilation) {
   const int64_t C = x.size(3);
   at::Tensor xf = x.to(at::kFloat).permute({0, 3, 1, 2});
+  if (act & 2) xf = xf.clamp(0, 6);  // deferred input ReLU6
+  act &= 1;
   at::Tensor wf = w.to(at::kFloat).view({3, 3, C}).permute({2, 0, 1}).unsqueeze(1).contiguous();
   at::Tensor v = at::conv2d(xf, wf, bias, {stride, stride}, {dilation, dilation}, {dilation, dilation}, C);
   return act_ref(v, act).permute({0, 2, 3, 1}).contiguous().to(x.scalar_type() == at::kFloat ? at::kFloat : at::kBFloat16);

@@ -118,6 +118,11 @@ class FusedPoseNet(nn.Module):
         import os
 
         self.fuse_dwpw = self.f32 and os.environ.get("NNSX_DWPW", "0") == "1"
+        # fp32: every pointwise conv but the last runs linear (bias only) and the
+        # next depthwise applies its ReLU6 to the taps it reads (dw_conv act bit
+        # 1), so the pointwise GEMMs are plain products the library GEMM takes
+        # (kernels/blaslt.cc).  NNSX_DEFER_ACT=0: ReLU6 in the GEMM's epilogue
+        self.defer_act = self.f32 and os.environ.get("NNSX_DEFER_ACT", "1") != "0"
         return self
 
     def forward(self, x: torch.Tensor):
@@ -131,8 +136,16 @@ class FusedPoseNet(nn.Module):
             o = torch.ops.nnsx.dwpw([h, h], nones, nones, [self.heat.wt, self.offs.wt], [self.heat.bias, self.offs.bias],
                                     [self.k, 2 * self.k], [1, 1], 0)
             return o[0], o[1]
-        for d, p in zip(self.dws, self.pws):
-            h = p(d(h))
+        if self.defer_act and h.is_cuda:
+            n = len(self.pws)
+            i = 0
+            for d, p in zip(self.dws, self.pws):
+                h = torch.ops.nnsx.dw_conv(h, d.w, d.bias, d.stride, 3 if i > 0 else 1, d.dilation)
+                h = torch.ops.nnsx.pw_conv(h, p.wt, p.bias, None, p.n, 1 if i == n - 1 else 0, p.out_f32)
+                i += 1
+        else:
+            for d, p in zip(self.dws, self.pws):
+                h = p(d(h))
         hm = self.heat(h)[..., : self.k].contiguous()
         of = self.offs(h)[..., : 2 * self.k].contiguous()
         return hm, of

@@ -73,15 +73,19 @@ def test_pw_conv_f32_identity_asymmetric(nns):
 
 @pytest.mark.parametrize("B,H,W,C,stride,dil", [(2, 112, 112, 32, 1, 1), (3, 112, 112, 96, 2, 1), (1, 7, 7, 960, 1, 1),
                                                 (2, 15, 9, 144, 2, 1), (2, 33, 33, 320, 1, 2), (1, 65, 65, 64, 1, 4)])
-def test_dw_conv_f32(nns, B, H, W, C, stride, dil):
-    x = torch.randn(B, H, W, C, device="cuda")
+@pytest.mark.parametrize("act", [1, 3])
+def test_dw_conv_f32(nns, B, H, W, C, stride, dil, act):
+    """act 3 = the producer's deferred ReLU6 applied to the input taps, then ReLU6"""
+    x = torch.randn(B, H, W, C, device="cuda") * 4
     w = torch.randn(9, C, device="cuda")
     bias = torch.randn(C, device="cuda")
-    y = torch.ops.nnsx.dw_conv(x, w, bias, stride, 1, dil)
+    y = torch.ops.nnsx.dw_conv(x, w, bias, stride, act, dil)
     assert y.dtype == torch.float32
     wf = w.double().cpu().view(3, 3, C).permute(2, 0, 1).unsqueeze(1)
-    ref = F.conv2d(x.double().cpu().permute(0, 3, 1, 2), wf, bias.double().cpu(), stride=stride, padding=dil,
-                   dilation=dil, groups=C).clamp(0, 6)
+    xin = x.double().cpu().permute(0, 3, 1, 2)
+    if act == 3:
+        xin = xin.clamp(0, 6)
+    ref = F.conv2d(xin, wf, bias.double().cpu(), stride=stride, padding=dil, dilation=dil, groups=C).clamp(0, 6)
     _close(y, ref.permute(0, 2, 3, 1))
 
 
