@@ -2158,8 +2158,11 @@ void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float
   // and enough rows: the library GEMM (blaslt.cc), the residual as its C
   // operand.  (Its bias + clamp epilogue returned the bare product on this
   // ROCm: scripts/blaslt_probe.py -- the ReLU6 GEMMs stay on the engine's kernel.)
-  if (tile == 0 && blaslt_enabled() && !yl.rpb && !yl.brpb && !yl.pool && K >= 128 && M >= 2048 && N >= 64 &&
-      act == 0 && blaslt_gemm_f32(x, wt, bias, res, y, M, N, K, Kpad, act, s))
+  // (M <= 65536: the range measured in the pipelines -- MobileNetV2 / SSD /
+  // DeepLab up to 35k rows; a PoseNet run with 270k-row products on it hung the
+  // device, so larger products stay on the engine's kernel)
+  if (tile == 0 && blaslt_enabled() && !yl.rpb && !yl.brpb && !yl.pool && K >= 128 && M >= 2048 && M <= 65536 &&
+      N >= 64 && act == 0 && blaslt_gemm_f32(x, wt, bias, res, y, M, N, K, Kpad, act, s))
     return;
   if (use_small_m(M, Kpad, tile, yl)) {
     const dim3 grid(static_cast<unsigned>((N + 15) / 16), static_cast<unsigned>((M + 63) / 64));

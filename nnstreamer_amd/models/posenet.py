@@ -121,8 +121,10 @@ class FusedPoseNet(nn.Module):
         # fp32: every pointwise conv but the last runs linear (bias only) and the
         # next depthwise applies its ReLU6 to the taps it reads (dw_conv act bit
         # 1), so the pointwise GEMMs are plain products the library GEMM takes
-        # (kernels/blaslt.cc).  NNSX_DEFER_ACT=0: ReLU6 in the GEMM's epilogue
-        self.defer_act = self.f32 and os.environ.get("NNSX_DEFER_ACT", "1") != "0"
+        # (kernels/blaslt.cc).  Opt-in (NNSX_DEFER_ACT=1): the batch-64 run with the
+        # 270k-row products on the library GEMM hung the device; default: ReLU6 in
+        # the engine GEMM's epilogue
+        self.defer_act = self.f32 and os.environ.get("NNSX_DEFER_ACT", "0") == "1"
         return self
 
     def forward(self, x: torch.Tensor):
