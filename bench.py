@@ -119,7 +119,7 @@ CONFIGS = {
                         "option4=300:300 option5=300:300", per_frame=True,
                 metric="end-to-end frames/sec + p50 per-frame latency, SSD-MobileNet 300x300 + bounding_boxes + HIP NMS",
                 desc="SSDLite-MobileNetV2 300x300 (tensor_filter + bounding_boxes decoder, HIP NMS)"),
-    "deeplab": dict(size=513, model="deeplab_fused_lowres", norm="typecast:float32,div:255.0", lat_fps=100,
+    "deeplab": dict(size=513, model="deeplab_fused_lowres", norm="typecast:float32,div:255.0",
                     decoder="tensor_decoder mode=image_segment option1=tflite-deeplab option3=513:513", per_frame=True,
                     metric="end-to-end frames/sec + p50 per-frame latency, DeepLabV3 513x513 segmentation pipeline",
                     desc="DeepLabV3-MobileNetV2 513x513 (tensor_filter + image_segment decoder)"),
@@ -149,7 +149,7 @@ CONFIGS = {
                                  "+ edge RCCL all-gather",
                           desc="PoseNet-MobileNetV1 257x257 per rank, pose tensors all-gathered (edgesink/edgesrc "
                                "rccl-mode=allgather) into tensor_mux sync-mode=slowest"),
-    "posenet": dict(size=257, model="posenet_fused", norm="typecast:float32,add:-127.5,div:127.5", lat_fps=250,
+    "posenet": dict(size=257, model="posenet_fused", norm="typecast:float32,add:-127.5,div:127.5",
                     decoder="tensor_decoder mode=pose_estimation option1=640:480 option2=257:257 option3={pose} "
                             "option4=heatmap-offset", per_frame=True,
                     metric="end-to-end frames/sec + p50 per-frame latency, PoseNet 257x257 pipeline",
