@@ -102,9 +102,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int n) {
 constexpr int GKT = 32;       // k per LDS stage
 constexpr int GKQ = GKT / 4;  // k-quads per stage
 
-// PF = 2: the k-stage two ahead is loaded into a second register set, so a
-// stage's global loads have two stages of MFMAs to land in (PF = 1: one)
-template <int BM, int BN, int PF = 1>
+template <int BM, int BN>
 __global__ void __launch_bounds__(256) pw_gemm_f32_kernel(const float* __restrict__ x,    // [M][K]
                                                           const float* __restrict__ wt,   // [Npad][Kpad]
                                                           const float* __restrict__ bias, // [N]
@@ -133,36 +131,34 @@ __global__ void __launch_bounds__(256) pw_gemm_f32_kernel(const float* __restric
   const int kend = min(Kpad, kbeg + kchunk * GKT);
   const int nk = (kend - kbeg + GKT - 1) / GKT;
 
-  f32x4_t px[VX], pw[VW], qx[PF == 2 ? VX : 1], qw[PF == 2 ? VW : 1];
-  auto gload_to = [&](int k0, f32x4_t* dx, f32x4_t* dw) {
+  f32x4_t px[VX], pw[VW];
+  auto gload = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < VX; ++i) {
       const int v = tid + i * 256, kq = v & 7, row = v >> 3;
       const int m = m0 + row, k = k0 + kq * 4;
-      dx[i] = (m < M && k < K) ? *reinterpret_cast<const f32x4_t*>(x + static_cast<int64_t>(m) * K + k) : zero;
+      px[i] = (m < M && k < K) ? *reinterpret_cast<const f32x4_t*>(x + static_cast<int64_t>(m) * K + k) : zero;
     }
 #pragma unroll
     for (int i = 0; i < VW; ++i) {
       const int v = tid + i * 256, kq = v & 7, row = v >> 3;
       const int n = n0 + row, k = k0 + kq * 4;
-      dw[i] = (n < Npad && k < Kpad) ? *reinterpret_cast<const f32x4_t*>(wt + static_cast<int64_t>(n) * Kpad + k)
+      pw[i] = (n < Npad && k < Kpad) ? *reinterpret_cast<const f32x4_t*>(wt + static_cast<int64_t>(n) * Kpad + k)
                                      : zero;
     }
   };
-  auto lstore_from = [&](int buf, const f32x4_t* sx, const f32x4_t* sw) {
+  auto lstore = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < VX; ++i) {
       const int v = tid + i * 256, kq = v & 7, row = v >> 3;
-      *reinterpret_cast<f32x4_t*>(&xs[buf][kq][row ^ kq][0]) = sx[i];
+      *reinterpret_cast<f32x4_t*>(&xs[buf][kq][row ^ kq][0]) = px[i];
     }
 #pragma unroll
     for (int i = 0; i < VW; ++i) {
       const int v = tid + i * 256, kq = v & 7, row = v >> 3;
-      *reinterpret_cast<f32x4_t*>(&ws[buf][kq][row ^ kq][0]) = sw[i];
+      *reinterpret_cast<f32x4_t*>(&ws[buf][kq][row ^ kq][0]) = pw[i];
     }
   };
-  auto gload = [&](int k0) { gload_to(k0, px, pw); };
-  auto lstore = [&](int buf) { lstore_from(buf, px, pw); };
 
   f32x4_t acc[RM][RN];
 #pragma unroll
@@ -170,7 +166,14 @@ __global__ void __launch_bounds__(256) pw_gemm_f32_kernel(const float* __restric
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = zero;
 
-  auto compute = [&](int buf) {
+  if (nk > 0) {
+    gload(kbeg);
+    lstore(0);
+    __syncthreads();
+  }
+  for (int ks = 0; ks < nk; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nk) gload(kbeg + (ks + 1) * GKT);  // in flight during this stage's MFMAs
 #pragma unroll
     for (int s = 0; s < GKT / 16; ++s) {
       const int kq = 4 * s + g;
@@ -186,40 +189,8 @@ __global__ void __launch_bounds__(256) pw_gemm_f32_kernel(const float* __restric
 #pragma unroll
         for (int j = 0; j < RN; ++j) acc[i][j] = mfma_k16(a[j], b[i], acc[i][j]);
     }
-  };
-  if constexpr (PF == 2) {
-    // stages alternate LDS buffers 0 / 1 and register sets p / q: while stage
-    // ks computes, stage ks + 1 waits in registers and stage ks + 2 loads
-    if (nk > 0) {
-      gload_to(kbeg, px, pw);
-      lstore_from(0, px, pw);
-      if (nk > 1) gload_to(kbeg + GKT, qx, qw);
-      __syncthreads();
-    }
-    for (int ks = 0; ks < nk; ks += 2) {
-      if (ks + 2 < nk) gload_to(kbeg + (ks + 2) * GKT, px, pw);
-      compute(0);
-      if (ks + 1 < nk) lstore_from(1, qx, qw);  // buffer 1 was last read before the previous barrier
-      __syncthreads();
-      if (ks + 1 >= nk) break;
-      if (ks + 3 < nk) gload_to(kbeg + (ks + 3) * GKT, qx, qw);
-      compute(1);
-      if (ks + 2 < nk) lstore_from(0, px, pw);
-      __syncthreads();
-    }
-  } else {
-    if (nk > 0) {
-      gload(kbeg);
-      lstore(0);
-      __syncthreads();
-    }
-    for (int ks = 0; ks < nk; ++ks) {
-      const int buf = ks & 1;
-      if (ks + 1 < nk) gload(kbeg + (ks + 1) * GKT);  // in flight during this stage's MFMAs
-      compute(buf);
-      if (ks + 1 < nk) lstore(buf ^ 1);  // buf ^ 1 was last read before the previous barrier
-      __syncthreads();
-    }
+    if (ks + 1 < nk) lstore(buf ^ 1);  // buf ^ 1 was last read before the previous barrier
+    __syncthreads();
   }
 
   // epilogue: lane owns channels n..n+3 of pixel m.  Bias (and residual)
@@ -2097,18 +2068,9 @@ static void pw_gemm_f32_launch(const float* x, const float* wt, const float* bia
   const int kstages = (Kpad + GKT - 1) / GKT;
   int chunk = (ws && !yl.rpb && !yl.brpb && !yl.pool) ? gemm_kchunk(static_cast<int>(grid.x * grid.y), kstages, N, !res) : kstages;
   grid.z = static_cast<unsigned>((kstages + chunk - 1) / chunk);
-  // NNSX_F32_GEMM_PF=2: two k-stages of register prefetch (deep-K products)
-  static const int pf = [] {
-    const char* e = std::getenv("NNSX_F32_GEMM_PF");
-    return e && e[0] == '2' ? 2 : 1;
-  }();
   if (grid.z == 1) {
-    if (pf == 2 && kstages >= 4)
-      hipLaunchKernelGGL((pw_gemm_f32_kernel<BM, BN, 2>), grid, dim3(256), 0, s, x, wt, bias, res, y, M, N, K, Kpad,
-                         Npad, act, kstages, yl);
-    else
-      hipLaunchKernelGGL((pw_gemm_f32_kernel<BM, BN>), grid, dim3(256), 0, s, x, wt, bias, res, y, M, N, K, Kpad, Npad,
-                         act, kstages, yl);
+    hipLaunchKernelGGL((pw_gemm_f32_kernel<BM, BN>), grid, dim3(256), 0, s, x, wt, bias, res, y, M, N, K, Kpad, Npad,
+                       act, kstages, yl);
     return;
   }
   hipLaunchKernelGGL((pw_gemm_f32_kernel<BM, BN>), grid, dim3(256), 0, s, x, wt, bias, res, ws, M, N, K, Kpad, Npad,
