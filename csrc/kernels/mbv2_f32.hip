@@ -1950,6 +1950,11 @@ const IrwCfg kIrwCfgs[] = {
     NNSX_IRW(1, 8, 16, 24, 2, 3, true),    // 56x56: expand 192/128 (8x8: 112/64)
     NNSX_IRW(2, 4, 8, 24, 2, 3, true),     // 56 -> 28: expand 160/128 input px (4x4: 96/64)
     NNSX_IRW(2, 8, 8, 16, 2, 3, true),     // 112 -> 56: expand 304/256 (4x8: 160/128)
+    // SSD-300's 10x10 stage (exact 5 x 5 tiles: 2 x 2 tiles of 7 x 7 computed 196 cells
+    // per 100 outputs) -- found only for maps a multiple of 5 that no 7 x 7 tile fits
+    NNSX_IRW(1, 5, 5, 160, 10, 4, false),  // 10x10     160 -> 960 -> 160
+    NNSX_IRW(2, 5, 5, 96, 10, 4, false),   // 19 -> 10   96 -> 576 -> 160
+    NNSX_IRW(1, 5, 5, 160, 0, 4, false),   // 10x10     160 -> 960 (expand + depthwise)
     NNSX_IRW(1, 7, 14, 64, 6, 4, false),   // 14x14 64 -> 384 -> 96
     NNSX_IRW(1, 7, 14, 96, 6, 4, false),   // 14x14 96 -> 576 -> 96: expand 144/98 cells (7x7: 96/49), project 112/98
     // (dilation 2 -- DeepLab's output-stride-16 blocks on 33x33 maps -- as
