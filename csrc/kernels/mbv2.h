@@ -155,9 +155,11 @@ struct IrBlockF32Args {
 };
 // Launches enqueued by this thread while a SharedDeviceScope is alive may run
 // concurrently with other kernels of the same process (a filter's replay
-// lanes): no form that waits inside a launch for other workgroups of the grid
-// (the spread combine above) -- it would assume a residency nothing guarantees.
-// Graph capture bakes the choice into the captured kernels.
+// lanes), including other launches of the same model: no in-launch combine of
+// hidden parts -- the spread form would wait for a residency nothing
+// guarantees, and both forms count arrivals in the model's one ticket buffer,
+// which concurrent replays of a block would share.  Graph capture bakes the
+// choice into the captured kernels.
 struct SharedDeviceScope {
   explicit SharedDeviceScope(bool on);
   ~SharedDeviceScope();

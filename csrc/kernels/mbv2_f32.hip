@@ -2364,14 +2364,17 @@ static bool launch_irw(const IrwCfg* c, IrBlockF32Args a, hipStream_t s) {
                                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
     return false;
   if (a.hsplit == 2 && !slabs) (void)hipMemsetAsync(a.y, 0, static_cast<size_t>(plane) * sizeof(float), s);
-  if (!a.ws || tiles > kLastTickets) a.tickets = nullptr;
+  // (a shared device -- replay lanes, other model instances -- may run this
+  // block's launches concurrently, and the tickets are the model's one buffer:
+  // the parts are then added by a separate reduce launch)
+  if (!a.ws || tiles > kLastTickets || device_shared()) a.tickets = nullptr;
   a.spread = 0;
   if (a.tickets) {
     // the spread combine waits inside the launch for the other parts of a
     // tile: only when every workgroup of the grid is resident at once (one
     // block per CU under what the occupancy query reports, which can over-report)
     int dev = 0, ncu = 0, per_cu = 0;
-    if (irw_inlaunch_mode() == 2 && !device_shared() && 2 * tiles <= kSpreadTickets && hipGetDevice(&dev) == hipSuccess &&
+    if (irw_inlaunch_mode() == 2 && 2 * tiles <= kSpreadTickets && hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(c->kernel), 64 * c->NW, lds) ==
             hipSuccess &&
