@@ -47,6 +47,18 @@ def main():
         lds = per("SQ_INSTS_LDS")
         print(f"{n[:58]:58s} {mfma:9.3g} {valu / mfma if mfma else 0:9.2f} {conf:9.1f} {wait:6.1f} {ldsw:6.1f} "
               f"{per('FETCH_SIZE'):9.0f} {per('WRITE_SIZE'):9.0f} {lds / mfma if mfma else 0:8.2f}")
+        # wave-time split (SQ_WAVE_CYCLES counts 4-cycle units): issuing, parked on
+        # s_waitcnt / barriers, the rest stalled on dependencies; MFMA pipe busy =
+        # SQ_VALU_MFMA_BUSY_CYCLES / SQ_BUSY_CYCLES / 32 SIMDs per SE
+        wc = per("SQ_WAVE_CYCLES")
+        if wc:
+            iss = per("SQ_ACTIVE_INST_ANY") / wc
+            wt = per("SQ_WAIT_ANY") / wc
+            busy = per("SQ_VALU_MFMA_BUSY_CYCLES") / per("SQ_BUSY_CYCLES") / 32 if per("SQ_BUSY_CYCLES") else 0
+            life = 4 * wc / per("SQ_WAVES") if per("SQ_WAVES") else 0
+            salu = per("SQ_INSTS_SALU") / mfma if mfma else 0
+            print(f"{'':58s}   wave lifetime {life:.0f} cycles; issuing {iss:.2f}, waitcnt/barrier {wt:.2f}, "
+                  f"dependency stalls {max(0.0, 1 - iss - wt):.2f}; MFMA pipe busy {busy:.2f}; SALU/MFMA {salu:.2f}")
 
 
 if __name__ == "__main__":
