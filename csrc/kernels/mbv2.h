@@ -77,6 +77,28 @@ bool blaslt_gemm_f32(const float* x, const float* wt, const float* bias, const f
 void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
                  int Kpad, int Npad, int act, hipStream_t s, int tile = 0, float* ws = nullptr,
                  const YLayout& yl = YLayout{});
+// Grouped launches (the SSD prediction heads): up to kGroupMax independent
+// problems per launch.  pw_gemm_f32_group: 64 x 64 tiles, no split-K, no
+// residual, any YLayout but pool.  dw3x3_f32_group: stride 1, dilation 1,
+// y [B][H][W][C] (act as dw3x3_f32).
+constexpr int kGroupMax = 16;
+struct GemmProb {
+  const float* x = nullptr;
+  const float* wt = nullptr;
+  const float* bias = nullptr;
+  float* y = nullptr;
+  int M = 0, N = 0, K = 0, Kpad = 0, Npad = 0, act = 0;
+  YLayout yl;
+};
+struct DwProb {
+  const float* x = nullptr;
+  const float* w = nullptr;
+  const float* bias = nullptr;
+  float* y = nullptr;
+  int B = 0, H = 0, W = 0, C = 0, act = 0;
+};
+void pw_gemm_f32_group(const GemmProb* p, int n, hipStream_t s);
+void dw3x3_f32_group(const DwProb* p, int n, hipStream_t s);
 // SSDLite prediction heads, all in one launch (heads_f32.hip): per head y =
 // pw(relu6(dw3x3(x) + bd)) + bias written into rows of a concatenated output.
 struct SepHead {

@@ -40,6 +40,7 @@
 #include <cstdint>
 #include <cmath>
 #include <cstdlib>
+#include <stdexcept>
 #include <vector>
 
 #include "kernels/mbv2.h"
@@ -102,15 +103,16 @@ __device__ __forceinline__ int xcd_remap(int bid, int n) {
 constexpr int GKT = 32;       // k per LDS stage
 constexpr int GKQ = GKT / 4;  // k-quads per stage
 
+// one BM x BN output tile over k-stages [kbeg, kbeg + nk * GKT); zs / slab: this
+// block's split-K slice and whether the grid is split (then y is the slab workspace)
 template <int BM, int BN>
-__global__ void __launch_bounds__(256) pw_gemm_f32_kernel(const float* __restrict__ x,    // [M][K]
-                                                          const float* __restrict__ wt,   // [Npad][Kpad]
-                                                          const float* __restrict__ bias, // [N]
-                                                          const float* __restrict__ res,  // [M][N] or null
-                                                          float* __restrict__ y,          // [M][N]
-                                                          int M, int N, int K, int Kpad, int Npad, int act,
-                                                          int kchunk,  // k-stages of this grid.z slice
-                                                          YLayout yl) {
+__device__ __forceinline__ void pw_gemm_f32_tile(const float* __restrict__ x,     // [M][K]
+                                                 const float* __restrict__ wt,    // [Npad][Kpad]
+                                                 const float* __restrict__ bias,  // [N]
+                                                 const float* __restrict__ res,   // [M][N] or null
+                                                 float* __restrict__ y,           // [M][N]
+                                                 int M, int N, int K, int Kpad, int Npad, int act, int kbeg, int nk,
+                                                 int zs, bool slab, const YLayout& yl, int m0, int n0) {
   constexpr int RM = BM / 32, RN = BN / 32;  // 16-row fragments per wave (2 x 2 waves)
   constexpr int VX = BM * GKQ / 256, VW = BN * GKQ / 256;
   // k4-major images, row index XOR-swizzled with the k-quad (kq < 8): the
@@ -122,14 +124,7 @@ __global__ void __launch_bounds__(256) pw_gemm_f32_kernel(const float* __restric
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int li = lane & 15, g = lane >> 4;
-  const int nbx = gridDim.x, nby = gridDim.y;
-  const int flat = xcd_remap(blockIdx.y * nbx + blockIdx.x, nbx * nby);
-  const int m0 = (flat % nbx) * BM, n0 = (flat / nbx) * BN;
   const f32x4_t zero = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  const int kbeg = blockIdx.z * kchunk * GKT;
-  const int kend = min(Kpad, kbeg + kchunk * GKT);
-  const int nk = (kend - kbeg + GKT - 1) / GKT;
 
   f32x4_t px[VX], pw[VW];
   auto gload = [&](int k0) {
@@ -196,7 +191,6 @@ __global__ void __launch_bounds__(256) pw_gemm_f32_kernel(const float* __restric
   // epilogue: lane owns channels n..n+3 of pixel m.  Bias (and residual)
   // values are all loaded up front, branch-free: loaded at each store behind
   // the bounds checks they were fetched and waited for one at a time.
-  const bool slab = gridDim.z > 1;
   if constexpr (BN == 64) {
     if (yl.pool && !slab) {
       // head conv + act + global average pool: the activated tile goes through
@@ -256,8 +250,7 @@ __global__ void __launch_bounds__(256) pw_gemm_f32_kernel(const float* __restric
       if (n >= N) continue;
       float* yp = y + static_cast<int64_t>(m) * N + n;
       if (slab) {  // split-K: this slice's slab of the workspace (gemm_splitk_reduce adds them)
-        *reinterpret_cast<f32x4_t*>(y + static_cast<int64_t>(blockIdx.z) * M * N + static_cast<int64_t>(m) * N + n) =
-            acc[i][j];
+        *reinterpret_cast<f32x4_t*>(y + static_cast<int64_t>(zs) * M * N + static_cast<int64_t>(m) * N + n) = acc[i][j];
         continue;
       }
       f32x4_t v = acc[i][j] + (yl.brpb ? *reinterpret_cast<const f32x4_t*>(bias + static_cast<int64_t>(m / yl.brpb) * N + n)
@@ -280,6 +273,42 @@ __global__ void __launch_bounds__(256) pw_gemm_f32_kernel(const float* __restric
       *reinterpret_cast<f32x4_t*>(yp) = v;
     }
   }
+}
+
+template <int BM, int BN>
+__global__ void __launch_bounds__(256) pw_gemm_f32_kernel(const float* __restrict__ x, const float* __restrict__ wt,
+                                                          const float* __restrict__ bias, const float* __restrict__ res,
+                                                          float* __restrict__ y, int M, int N, int K, int Kpad, int Npad,
+                                                          int act,
+                                                          int kchunk,  // k-stages of this grid.z slice
+                                                          YLayout yl) {
+  const int nbx = gridDim.x, nby = gridDim.y;
+  const int flat = xcd_remap(blockIdx.y * nbx + blockIdx.x, nbx * nby);
+  const int kbeg = blockIdx.z * kchunk * GKT;
+  const int kend = min(Kpad, kbeg + kchunk * GKT);
+  pw_gemm_f32_tile<BM, BN>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, kbeg, (kend - kbeg + GKT - 1) / GKT,
+                           static_cast<int>(blockIdx.z), gridDim.z > 1, yl, (flat % nbx) * BM, (flat / nbx) * BN);
+}
+
+// Several independent GEMMs in one launch (the SSD prediction heads): block b
+// takes a tile of the problem whose block range holds it.  No XCD remap: the
+// dispatcher deals blocks round robin over the XCDs, so each XCD gets the same
+// mix of deep (long) and shallow tiles instead of one problem's eighth.
+struct GemmGroupArgs {
+  int n = 0;
+  int start[kGroupMax + 1] = {};
+  GemmProb p[kGroupMax];
+};
+
+template <int BM, int BN>
+__global__ void __launch_bounds__(256) pw_gemm_group_f32_kernel(GemmGroupArgs g) {
+  const int flat = blockIdx.x;
+  int i = 0;
+  while (i + 1 < g.n && flat >= g.start[i + 1]) ++i;
+  const GemmProb& p = g.p[i];
+  const int local = flat - g.start[i], gx = (p.M + BM - 1) / BM;
+  pw_gemm_f32_tile<BM, BN>(p.x, p.wt, p.bias, nullptr, p.y, p.M, p.N, p.K, p.Kpad, p.Npad, p.act, 0,
+                           (p.Kpad + GKT - 1) / GKT, 0, false, p.yl, (local % gx) * BM, (local / gx) * BN);
 }
 
 // split-K epilogue: y = act(sum_z ws[z] + bias), slabs added in z order
@@ -453,16 +482,16 @@ __global__ void __launch_bounds__(256) dw3x3_f32_kernel(const float* __restrict_
 // 4 channels, so each loaded input row feeds up to 3 of them
 // ((R-1)S+3 row loads instead of 3R)
 template <int R, int S>
-__global__ void __launch_bounds__(256) dw3x3_f32_col_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                            const float* __restrict__ bias, float* __restrict__ y,
-                                                            int B, int H, int W, int C, int Ho, int Wo, int act) {
+__device__ __forceinline__ void dw3x3_f32_col(const float* __restrict__ x, const float* __restrict__ w,
+                                              const float* __restrict__ bias, float* __restrict__ y, int B, int H,
+                                              int W, int C, int Ho, int Wo, int act, uint32_t t0, uint32_t step) {
   constexpr int NR = (R - 1) * S + 3;
   const bool ic = (act & 2) != 0;  // (deferred input ReLU6, dw3x3_f32_kernel)
   act &= 1;
   const uint32_t cg = static_cast<uint32_t>(C) >> 2;
   const uint32_t rg = static_cast<uint32_t>((Ho + R - 1) / R);
   const uint32_t total = static_cast<uint32_t>(B) * rg * Wo * cg;
-  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+  for (uint32_t t = t0; t < total; t += step) {
     const int c = static_cast<int>(t % cg) * 4;
     uint32_t p = t / cg;
     const int ox = static_cast<int>(p % Wo);
@@ -507,6 +536,32 @@ __global__ void __launch_bounds__(256) dw3x3_f32_col_kernel(const float* __restr
       *reinterpret_cast<f32x4_t*>(y + ((static_cast<int64_t>(b) * Ho + oy) * Wo + ox) * C + c) = v;
     }
   }
+}
+
+template <int R, int S>
+__global__ void __launch_bounds__(256) dw3x3_f32_col_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                            const float* __restrict__ bias, float* __restrict__ y,
+                                                            int B, int H, int W, int C, int Ho, int Wo, int act) {
+  dw3x3_f32_col<R, S>(x, w, bias, y, B, H, W, C, Ho, Wo, act, blockIdx.x * blockDim.x + threadIdx.x,
+                      gridDim.x * blockDim.x);
+}
+
+// several stride-1 depthwise problems in one launch (the SSD heads); problem i
+// owns blocks [start[i], start[i + 1]) and walks its work with that stride
+struct DwGroupArgs {
+  int n = 0;
+  int start[kGroupMax + 1] = {};
+  DwProb p[kGroupMax];
+};
+
+__global__ void __launch_bounds__(256) dw3x3_group_f32_kernel(DwGroupArgs g) {
+  const int bid = blockIdx.x;
+  int i = 0;
+  while (i + 1 < g.n && bid >= g.start[i + 1]) ++i;
+  const DwProb& p = g.p[i];
+  dw3x3_f32_col<4, 1>(p.x, p.w, p.bias, p.y, p.B, p.H, p.W, p.C, p.H, p.W, p.act,
+                      static_cast<uint32_t>(bid - g.start[i]) * 256u + threadIdx.x,
+                      static_cast<uint32_t>(g.start[i + 1] - g.start[i]) * 256u);
 }
 
 // ---------------------------------------------------------------- stem_f32 ----
@@ -2181,6 +2236,39 @@ void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float
     case 128192: pw_gemm_f32_launch<128, 192>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s, yl); break;
     default: pw_gemm_f32_launch<128, 128>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s, yl); break;
   }
+}
+
+void pw_gemm_f32_group(const GemmProb* p, int n, hipStream_t s) {
+  if (n <= 0 || n > kGroupMax) throw std::invalid_argument("pw_gemm_f32_group: 1..16 problems");
+  GemmGroupArgs g;
+  g.n = n;
+  int64_t blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    if (p[i].yl.pool || p[i].yl.brpb || p[i].K % 4 || p[i].N % 4 || p[i].Kpad < p[i].K || p[i].Npad < p[i].N)
+      throw std::invalid_argument("pw_gemm_f32_group: unsupported problem");
+    g.p[i] = p[i];
+    g.start[i] = static_cast<int>(blocks);
+    blocks += static_cast<int64_t>((p[i].M + 63) / 64) * ((p[i].N + 63) / 64);
+  }
+  if (blocks <= 0 || blocks > (1 << 30)) throw std::invalid_argument("pw_gemm_f32_group: grid");
+  g.start[n] = static_cast<int>(blocks);
+  hipLaunchKernelGGL((pw_gemm_group_f32_kernel<64, 64>), dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, g);
+}
+
+void dw3x3_f32_group(const DwProb* p, int n, hipStream_t s) {
+  if (n <= 0 || n > kGroupMax) throw std::invalid_argument("dw3x3_f32_group: 1..16 problems");
+  DwGroupArgs g;
+  g.n = n;
+  int64_t blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    if (p[i].C % 4) throw std::invalid_argument("dw3x3_f32_group: C % 4");
+    g.p[i] = p[i];
+    g.start[i] = static_cast<int>(blocks);
+    const int64_t work = static_cast<int64_t>(p[i].B) * ((p[i].H + 3) / 4) * p[i].W * (p[i].C / 4);
+    blocks += std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 16384));
+  }
+  g.start[n] = static_cast<int>(blocks);
+  hipLaunchKernelGGL(dw3x3_group_f32_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, g);
 }
 
 void dw3x3_f32(const float* x, const float* w, const float* bias, float* y, int B, int H, int W, int C, int stride,

@@ -2,6 +2,7 @@
 // TorchScript models (loaded by tensor_filter framework=pytorch) run them,
 // and hipGraph capture records them like any other kernel.  CPU
 // implementations are the fp32 numerics reference.
+#include <algorithm>
 #include <ATen/ATen.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
@@ -133,9 +134,14 @@ at::Tensor dw_conv_cpu(const at::Tensor& x, const at::Tensor& w, const at::Tenso
 // feature xs[i] through its depthwise (wds[i], bds[i]) and predictor (wts[i],
 // biases[i], ns[i] outputs per pixel) into out_box (which[i] == 0) or out_cls
 // (1), its rows following the previous head's of the same output.
+// mode 0: two grouped launches -- every head's depthwise into a scratch map
+// (kernels::dw3x3_f32_group), then every predictor GEMM
+// (kernels::pw_gemm_f32_group); mode 1: one launch with the depthwise in the
+// GEMM's operand staging (recomputed per output-column tile: slower,
+// profiles/r4_dwpw_ab.txt).
 void sep_heads_cuda(at::TensorList xs, at::TensorList wds, at::TensorList bds, at::TensorList wts,
                     at::TensorList biases, at::IntArrayRef ns, at::IntArrayRef which, at::Tensor& out_box,
-                    at::Tensor& out_cls) {
+                    at::Tensor& out_cls, int64_t mode) {
   const size_t n = xs.size();
   TORCH_CHECK(n > 0 && n <= static_cast<size_t>(nnsx::kernels::kSepHeadsMax) && wds.size() == n && bds.size() == n &&
                   wts.size() == n && biases.size() == n && ns.size() == n && which.size() == n,
@@ -174,11 +180,59 @@ void sep_heads_cuda(at::TensorList xs, at::TensorList wds, at::TensorList bds, a
     h.Npad = static_cast<int>(wts[i].size(0));
     rows[which[i] ? 1 : 0] = r0 + HW * (N / C);
   }
-  nnsx::kernels::sep_heads_f32(a, cur_stream());
+  if (mode == 1) {
+    nnsx::kernels::sep_heads_f32(a, cur_stream());
+    return;
+  }
+  TORCH_CHECK(mode == 0, "sep_heads: mode 0 (grouped depthwise + grouped GEMM) or 1 (one launch)");
+  int64_t total = 0;
+  for (size_t i = 0; i < n; ++i) total += xs[i].numel();
+  at::Tensor hid = at::empty({total}, xs[0].options());
+  // the largest maps first: their blocks start first, the small maps fill the tail
+  std::vector<size_t> order(n);
+  for (size_t i = 0; i < n; ++i) order[i] = i;
+  std::stable_sort(order.begin(), order.end(), [&](size_t p, size_t q) {
+    const auto& hp = a.h[p];
+    const auto& hq = a.h[q];
+    return static_cast<int64_t>(hp.B) * hp.H * hp.W * hp.Kpad > static_cast<int64_t>(hq.B) * hq.H * hq.W * hq.Kpad;
+  });
+  nnsx::kernels::DwProb dp[nnsx::kernels::kGroupMax];
+  nnsx::kernels::GemmProb gp[nnsx::kernels::kGroupMax];
+  int64_t off = 0;
+  for (size_t j = 0; j < n; ++j) {
+    const auto& h = a.h[order[j]];
+    float* hb = hid.data_ptr<float>() + off;
+    off += static_cast<int64_t>(h.B) * h.H * h.W * h.K;
+    dp[j].x = h.x;
+    dp[j].w = h.wd;
+    dp[j].bias = h.bd;
+    dp[j].y = hb;
+    dp[j].B = h.B;
+    dp[j].H = h.H;
+    dp[j].W = h.W;
+    dp[j].C = h.K;
+    dp[j].act = 1;
+    auto& g = gp[j];
+    g.x = hb;
+    g.wt = h.wt;
+    g.bias = h.bias;
+    g.y = h.out;
+    g.M = h.B * h.H * h.W;
+    g.N = (h.N + 3) / 4 * 4;
+    g.K = h.K;
+    g.Kpad = h.Kpad;
+    g.Npad = h.Npad;
+    g.act = 0;
+    g.yl.rpb = h.H * h.W;
+    g.yl.ncols = h.N;
+    g.yl.bstride = h.bstride;
+  }
+  nnsx::kernels::dw3x3_f32_group(dp, static_cast<int>(n), cur_stream());
+  nnsx::kernels::pw_gemm_f32_group(gp, static_cast<int>(n), cur_stream());
 }
 
 void sep_heads_cpu(at::TensorList xs, at::TensorList wds, at::TensorList bds, at::TensorList wts, at::TensorList biases,
-                   at::IntArrayRef ns, at::IntArrayRef which, at::Tensor& out_box, at::Tensor& out_cls) {
+                   at::IntArrayRef ns, at::IntArrayRef which, at::Tensor& out_box, at::Tensor& out_cls, int64_t) {
   int64_t rows[2] = {0, 0};
   for (size_t i = 0; i < xs.size(); ++i) {
     at::Tensor& o = which[i] ? out_cls : out_box;
@@ -672,7 +726,7 @@ TORCH_LIBRARY(nnsx, m) {
   m.def("dwpw(Tensor[] xs, Tensor?[] wds, Tensor?[] bds, Tensor[] wts, Tensor[] biases, int[] ns, int[] strides, "
         "int act, int dilation=1, Tensor? res=None) -> Tensor[]");
   m.def("sep_heads(Tensor[] xs, Tensor[] wds, Tensor[] bds, Tensor[] wts, Tensor[] biases, int[] ns, int[] which, "
-        "Tensor(a!) out_box, Tensor(b!) out_cls) -> ()");
+        "Tensor(a!) out_box, Tensor(b!) out_cls, int mode=0) -> ()");
   m.def("dw_conv(Tensor x, Tensor w, Tensor bias, int stride, int act, int dilation=1) -> Tensor");
   m.def("stem_conv(Tensor x, Tensor w, Tensor bias, int act, bool out_f32=False) -> Tensor");
   m.def("stem_conv_u8(Tensor x, Tensor w, Tensor bias, int act, Tensor lut, bool out_f32=False) -> Tensor");

@@ -191,12 +191,14 @@ class FusedSSDLite(nn.Module):
         self.box_heads = nn.ModuleList([FusedSepHead(h, 4, precision) for h in m.box_heads])
         self.cls_heads = nn.ModuleList([FusedSepHead(h, m.num_classes, precision) for h in m.cls_heads])
         self.feat_block = 13  # blocks[13] == features[14]: its expansion output is SSD feature 1
-        # fp32 with NNSX_DWPW=1 (or NNSX_SSD_SEP_HEADS=1): all 12 heads (depthwise +
-        # predictor, box and class, 6 maps) in one grouped launch (nnsx::sep_heads);
-        # default: 2 launches per head (measured faster, fused.py DWPW)
+        # fp32: all 12 heads (depthwise + predictor, box and class, 6 maps) through
+        # nnsx::sep_heads -- mode 0 (default): one grouped depthwise launch + one
+        # grouped GEMM launch; mode 1 (NNSX_DWPW=1): one launch, the depthwise in the
+        # GEMM's staging (slower, fused.py DWPW).  NNSX_SSD_SEP_HEADS=0: 2 launches per head.
         import os
 
-        self.one_launch_heads = self.f32 and os.environ.get("NNSX_SSD_SEP_HEADS", "1" if DWPW else "0") != "0"
+        self.one_launch_heads = self.f32 and os.environ.get("NNSX_SSD_SEP_HEADS", "1") != "0"
+        self.heads_mode = 1 if DWPW else 0
         self.feat_dwpw = self.f32 and DWPW
         return self
 
@@ -252,7 +254,7 @@ class FusedSSDLite(nn.Module):
                     bs.append(hb.pw.bias)
                     ns.append(hb.n)
                     which.append(0)
-                torch.ops.nnsx.sep_heads(xs, wds, bds, wts, bs, ns, which, bo, lo)
+                torch.ops.nnsx.sep_heads(xs, wds, bds, wts, bs, ns, which, bo, lo, self.heads_mode)
                 return bo.reshape(bo.shape[0], bo.shape[1], 1, 4), lo
             r = 0
             for i, bh in enumerate(self.box_heads):

@@ -117,12 +117,15 @@ def test_avgpool_f32(B, HW, C):
     assert torch.equal(p, torch.ops.nnsx.avgpool(x))  # deterministic
 
 
+@pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("B", [1, 3, 64])
-def test_sep_heads_one_launch_vs_fp64(B):
+def test_sep_heads_one_launch_vs_fp64(B, mode):
     """All 12 SSDLite heads (depthwise 3x3 + ReLU6 + predictor, box and class, 6
-    maps) in one grouped launch (kernels/heads_f32.hip) against an fp64 oracle
-    of each head, rows of the concatenated outputs included; B = 64 is the
-    benched batch (tiles spanning images at the 3x3 .. 1x1 maps)."""
+    maps) against an fp64 oracle of each head, rows of the concatenated outputs
+    included; mode 0: one grouped depthwise launch + one grouped GEMM launch
+    (kernels/mbv2_f32.hip dw3x3_group / pw_gemm_group), mode 1: one launch
+    (kernels/dwpw_f32.hip).  B = 64 is the benched batch (tiles spanning images
+    at the 3x3 .. 1x1 maps)."""
     import torch.nn.functional as F
 
     m = ssd.fused_ssd_mobilenet(seed=3, precision="fp32").cuda()
@@ -135,7 +138,7 @@ def test_sep_heads_one_launch_vs_fp64(B):
     heads = list(m.cls_heads) + list(m.box_heads)
     torch.ops.nnsx.sep_heads(feats + feats, [h.dw.w for h in heads], [h.dw.bias for h in heads],
                              [h.pw.wt for h in heads], [h.pw.bias for h in heads], [h.n for h in heads],
-                             [1] * 6 + [0] * 6, bo, lo)
+                             [1] * 6 + [0] * 6, bo, lo, mode)
 
     def ref(x, h):
         C = x.shape[-1]
