@@ -231,6 +231,57 @@ void sep_heads_cuda(at::TensorList xs, at::TensorList wds, at::TensorList bds, a
   nnsx::kernels::pw_gemm_f32_group(gp, static_cast<int>(n), cur_stream());
 }
 
+// Several pointwise convs in one grouped launch (kernels::pw_gemm_f32_group):
+// out[i] = act_i(xs[i] . wts[i]^T + biases[i]), NHWC [B, H, W, ns[i]] with
+// exact columns (the PoseNet heatmap + offset heads).
+std::vector<at::Tensor> pw_conv_group_cuda(at::TensorList xs, at::TensorList wts, at::TensorList biases,
+                                           at::IntArrayRef ns, at::IntArrayRef acts) {
+  const size_t n = xs.size();
+  TORCH_CHECK(n > 0 && n <= static_cast<size_t>(nnsx::kernels::kGroupMax) && wts.size() == n && biases.size() == n &&
+                  ns.size() == n && acts.size() == n,
+              "pw_conv_group: 1..16 problems, one entry of every list per problem");
+  nnsx::kernels::GemmProb gp[nnsx::kernels::kGroupMax];
+  std::vector<at::Tensor> outs;
+  for (size_t i = 0; i < n; ++i) {
+    const at::Tensor& x = xs[i];
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 4,
+                "pw_conv_group: x [B,H,W,K] f32 contiguous");
+    const int64_t K = x.size(3), M = x.numel() / K, N = ns[i], N4 = (N + 3) / 4 * 4;
+    TORCH_CHECK(K % 4 == 0 && wts[i].scalar_type() == at::kFloat && wts[i].is_contiguous() && wts[i].dim() == 2 &&
+                    wts[i].size(1) >= K && wts[i].size(0) >= N4 && biases[i].numel() >= N4 && acts[i] >= 0 &&
+                    acts[i] <= 1 && M > 0 && M < (1 << 30),
+                "pw_conv_group: weights [Npad >= N rounded to 4][Kpad >= K], bias, act 0|1");
+    at::Tensor y = at::empty({x.size(0), x.size(1), x.size(2), N}, x.options());
+    auto& g = gp[i];
+    g.x = x.data_ptr<float>();
+    g.wt = wts[i].data_ptr<float>();
+    g.bias = biases[i].data_ptr<float>();
+    g.y = y.data_ptr<float>();
+    g.M = static_cast<int>(M);
+    g.N = static_cast<int>(N4);
+    g.K = static_cast<int>(K);
+    g.Kpad = static_cast<int>(wts[i].size(1));
+    g.Npad = static_cast<int>(wts[i].size(0));
+    g.act = static_cast<int>(acts[i]);
+    g.yl.rpb = static_cast<int>(M);  // one "batch" of M rows, N exact columns each
+    g.yl.ncols = static_cast<int>(N);
+    g.yl.bstride = 0;
+    outs.push_back(y);
+  }
+  nnsx::kernels::pw_gemm_f32_group(gp, static_cast<int>(n), cur_stream());
+  return outs;
+}
+
+std::vector<at::Tensor> pw_conv_group_cpu(at::TensorList xs, at::TensorList wts, at::TensorList biases,
+                                          at::IntArrayRef ns, at::IntArrayRef acts) {
+  std::vector<at::Tensor> outs;
+  for (size_t i = 0; i < xs.size(); ++i)
+    outs.push_back(pw_conv_cpu(xs[i], wts[i], biases[i], c10::nullopt, (ns[i] + 3) / 4 * 4, acts[i], true)
+                       .slice(-1, 0, ns[i])
+                       .contiguous());
+  return outs;
+}
+
 void sep_heads_cpu(at::TensorList xs, at::TensorList wds, at::TensorList bds, at::TensorList wts, at::TensorList biases,
                    at::IntArrayRef ns, at::IntArrayRef which, at::Tensor& out_box, at::Tensor& out_cls, int64_t) {
   int64_t rows[2] = {0, 0};
@@ -727,6 +778,7 @@ TORCH_LIBRARY(nnsx, m) {
         "int act, int dilation=1, Tensor? res=None) -> Tensor[]");
   m.def("sep_heads(Tensor[] xs, Tensor[] wds, Tensor[] bds, Tensor[] wts, Tensor[] biases, int[] ns, int[] which, "
         "Tensor(a!) out_box, Tensor(b!) out_cls, int mode=0) -> ()");
+  m.def("pw_conv_group(Tensor[] xs, Tensor[] wts, Tensor[] biases, int[] ns, int[] acts) -> Tensor[]");
   m.def("dw_conv(Tensor x, Tensor w, Tensor bias, int stride, int act, int dilation=1) -> Tensor");
   m.def("stem_conv(Tensor x, Tensor w, Tensor bias, int act, bool out_f32=False) -> Tensor");
   m.def("stem_conv_u8(Tensor x, Tensor w, Tensor bias, int act, Tensor lut, bool out_f32=False) -> Tensor");
@@ -751,6 +803,7 @@ TORCH_LIBRARY_IMPL(nnsx, CUDA, m) {
   m.impl("pw_conv_rowbias", pw_conv_rowbias_cuda);
   m.impl("upsample_bilinear", upsample_bilinear_cuda);
   m.impl("sep_heads", sep_heads_cuda);
+  m.impl("pw_conv_group", pw_conv_group_cuda);
   m.impl("dwpw", dwpw_cuda);
   m.impl("dw_conv", dw_conv_cuda);
   m.impl("stem_conv", stem_conv_cuda);
@@ -769,6 +822,7 @@ TORCH_LIBRARY_IMPL(nnsx, CPU, m) {
   m.impl("pw_conv_rowbias", pw_conv_rowbias_cpu);
   m.impl("upsample_bilinear", upsample_bilinear_cpu);
   m.impl("sep_heads", sep_heads_cpu);
+  m.impl("pw_conv_group", pw_conv_group_cpu);
   m.impl("dwpw", dwpw_cpu);
   m.impl("dw_conv", dw_conv_cpu);
   m.impl("stem_conv", stem_conv_cpu);

@@ -148,6 +148,11 @@ class FusedPoseNet(nn.Module):
         else:
             for d, p in zip(self.dws, self.pws):
                 h = p(d(h))
+        if self.f32 and h.is_cuda:
+            # both 1x1 heads in one grouped GEMM launch, exact columns (no slice copies)
+            o = torch.ops.nnsx.pw_conv_group([h, h], [self.heat.wt, self.offs.wt], [self.heat.bias, self.offs.bias],
+                                             [self.k, 2 * self.k], [0, 0])
+            return o[0], o[1]
         hm = self.heat(h)[..., : self.k].contiguous()
         of = self.offs(h)[..., : 2 * self.k].contiguous()
         return hm, of

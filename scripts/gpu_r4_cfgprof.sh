@@ -7,7 +7,7 @@ R=$GRAFT_REPO_ROOT
 C=${CFG:-ssd}; B=${B:-64}
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$C -o run -- python3 $R/bench.py --config $C --batch $B --steps 10 --warmup 5 --sweep "" --latency-frames 0 > $R/gpurun_out/prof_$C.log 2>&1 || { echo "prof failed"; tail -30 $R/gpurun_out/prof_$C.log; exit 1; }
 cd $R
-db=$(find gpurun_out/prof_$C -name "*results.db" | head -1)
+db=gpurun_out/prof_$C/run_results.db
 python3 - "$db" > gpurun_out/prof_${C}_streams.txt <<'PY'
 import sqlite3, sys
 c = sqlite3.connect(sys.argv[1])

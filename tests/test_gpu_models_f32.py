@@ -157,6 +157,34 @@ def test_sep_heads_one_launch_vs_fp64(B, mode):
         assert err < 2e-5, err
 
 
+@pytest.mark.parametrize("shapes", [[(64, 17, 1024, 17, 0), (64, 17, 1024, 34, 0)],
+                                    [(3, 7, 64, 13, 1), (2, 129, 32, 64, 1), (1, 1, 128, 4, 0)]])
+def test_pw_conv_group_vs_fp64(shapes):
+    """Several pointwise convs in one grouped GEMM launch (nnsx::pw_conv_group,
+    kernels/mbv2_f32.hip pw_gemm_group_f32_kernel): exact-column NHWC outputs
+    (the PoseNet heatmap + offset heads) against fp64."""
+    g = torch.Generator().manual_seed(len(shapes))
+    xs, wts, bs, ns, acts = [], [], [], [], []
+    for B, H, K, N, act in shapes:
+        xs.append((torch.rand(B, H, H, K, generator=g) * 2).cuda())
+        w = torch.zeros((N + 7) // 8 * 8, K)
+        w[:N] = torch.randn(N, K, generator=g) * K ** -0.5
+        b = torch.zeros(w.shape[0])
+        b[:N] = torch.randn(N, generator=g)
+        wts.append(w.cuda())
+        bs.append(b.cuda())
+        ns.append(N)
+        acts.append(act)
+    outs = torch.ops.nnsx.pw_conv_group(xs, wts, bs, ns, acts)
+    for x, w, b, n, act, y in zip(xs, wts, bs, ns, acts, outs):
+        want = x.double().cpu() @ w.double().cpu()[:n].t() + b.double().cpu()[:n]
+        if act:
+            want = want.clamp(0, 6)
+        assert y.shape == x.shape[:3] + (n,)
+        err = ((y.double().cpu() - want).abs() / (want.abs() + 1)).max().item()
+        assert err < 2e-5, err
+
+
 @pytest.mark.parametrize("B,H,K,N,S,dw", [(3, 129, 32, 64, 1, True), (2, 129, 64, 128, 2, True),
                                           (64, 17, 512, 512, 1, True), (5, 17, 512, 1024, 2, True),
                                           (64, 9, 1024, 1024, 1, True), (7, 9, 1024, 17, 1, False)])
