@@ -479,41 +479,45 @@ __global__ void __launch_bounds__(256) dw3x3_f32_kernel(const float* __restrict_
 }
 
 // column form (dilation 1): one lane = R vertically adjacent output pixels x
-// 4 channels, so each loaded input row feeds up to 3 of them
-// ((R-1)S+3 row loads instead of 3R)
-template <int R, int S>
+// CW horizontally adjacent ones x 4 channels, so each loaded input row feeds up
+// to 3 of them ((R-1)S+3 row loads instead of 3R) and each loaded column up to 3
+// ((CW-1)S+3 column loads instead of 3CW)
+template <int R, int S, int CW = 1>
 __device__ __forceinline__ void dw3x3_f32_col(const float* __restrict__ x, const float* __restrict__ w,
                                               const float* __restrict__ bias, float* __restrict__ y, int B, int H,
                                               int W, int C, int Ho, int Wo, int act, uint32_t t0, uint32_t step) {
-  constexpr int NR = (R - 1) * S + 3;
+  constexpr int NR = (R - 1) * S + 3, NX = (CW - 1) * S + 3;
   const bool ic = (act & 2) != 0;  // (deferred input ReLU6, dw3x3_f32_kernel)
   act &= 1;
   const uint32_t cg = static_cast<uint32_t>(C) >> 2;
   const uint32_t rg = static_cast<uint32_t>((Ho + R - 1) / R);
-  const uint32_t total = static_cast<uint32_t>(B) * rg * Wo * cg;
+  const uint32_t wg = static_cast<uint32_t>((Wo + CW - 1) / CW);
+  const uint32_t total = static_cast<uint32_t>(B) * rg * wg * cg;
   for (uint32_t t = t0; t < total; t += step) {
     const int c = static_cast<int>(t % cg) * 4;
     uint32_t p = t / cg;
-    const int ox = static_cast<int>(p % Wo);
-    p /= Wo;
+    const int ox0 = static_cast<int>(p % wg) * CW;
+    p /= wg;
     const int oy0 = static_cast<int>(p % rg) * R;
     const int b = static_cast<int>(p / rg);
     f32x4_t wv[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) wv[k] = *reinterpret_cast<const f32x4_t*>(w + k * C + c);
     const f32x4_t bv = *reinterpret_cast<const f32x4_t*>(bias + c);
-    f32x4_t acc[R];
+    f32x4_t acc[R][CW];
 #pragma unroll
-    for (int j = 0; j < R; ++j) acc[j] = bv;
+    for (int j = 0; j < R; ++j)
+#pragma unroll
+      for (int q = 0; q < CW; ++q) acc[j][q] = bv;
     const float* xb = x + static_cast<int64_t>(b) * H * W * C + c;
 #pragma unroll
     for (int ir = 0; ir < NR; ++ir) {
       const int iy = oy0 * S - 1 + ir;
       if (iy < 0 || iy >= H) continue;
-      f32x4_t xv[3];
+      f32x4_t xv[NX];
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const int ix = ox * S - 1 + kx;
+      for (int kx = 0; kx < NX; ++kx) {
+        const int ix = ox0 * S - 1 + kx;
         xv[kx] = (ix >= 0 && ix < W) ? *reinterpret_cast<const f32x4_t*>(xb + (static_cast<int64_t>(iy) * W + ix) * C)
                                      : f32x4_t{0.f, 0.f, 0.f, 0.f};
         if (ic) xv[kx] = relu6x4(xv[kx]);
@@ -523,27 +527,35 @@ __device__ __forceinline__ void dw3x3_f32_col(const float* __restrict__ x, const
         const int ky = ir - j * S;
         if (ky < 0 || ky > 2) continue;
 #pragma unroll
-        for (int kx = 0; kx < 3; ++kx) acc[j] = __builtin_elementwise_fma(xv[kx], wv[ky * 3 + kx], acc[j]);
+        for (int q = 0; q < CW; ++q)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx)
+            acc[j][q] = __builtin_elementwise_fma(xv[q * S + kx], wv[ky * 3 + kx], acc[j][q]);
       }
     }
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       const int oy = oy0 + j;
       if (oy >= Ho) break;
-      f32x4_t v = acc[j];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], act);
-      *reinterpret_cast<f32x4_t*>(y + ((static_cast<int64_t>(b) * Ho + oy) * Wo + ox) * C + c) = v;
+      for (int q = 0; q < CW; ++q) {
+        const int ox = ox0 + q;
+        if (CW > 1 && ox >= Wo) break;
+        f32x4_t v = acc[j][q];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], act);
+        *reinterpret_cast<f32x4_t*>(y + ((static_cast<int64_t>(b) * Ho + oy) * Wo + ox) * C + c) = v;
+      }
     }
   }
 }
 
-template <int R, int S>
+template <int R, int S, int CW = 1>
 __global__ void __launch_bounds__(256) dw3x3_f32_col_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                             const float* __restrict__ bias, float* __restrict__ y,
                                                             int B, int H, int W, int C, int Ho, int Wo, int act) {
-  dw3x3_f32_col<R, S>(x, w, bias, y, B, H, W, C, Ho, Wo, act, blockIdx.x * blockDim.x + threadIdx.x,
-                      gridDim.x * blockDim.x);
+  dw3x3_f32_col<R, S, CW>(x, w, bias, y, B, H, W, C, Ho, Wo, act, blockIdx.x * blockDim.x + threadIdx.x,
+                          gridDim.x * blockDim.x);
 }
 
 // several stride-1 depthwise problems in one launch (the SSD heads); problem i
@@ -559,7 +571,7 @@ __global__ void __launch_bounds__(256) dw3x3_group_f32_kernel(DwGroupArgs g) {
   int i = 0;
   while (i + 1 < g.n && bid >= g.start[i + 1]) ++i;
   const DwProb& p = g.p[i];
-  dw3x3_f32_col<4, 1>(p.x, p.w, p.bias, p.y, p.B, p.H, p.W, p.C, p.H, p.W, p.act,
+  dw3x3_f32_col<4, 1, 4>(p.x, p.w, p.bias, p.y, p.B, p.H, p.W, p.C, p.H, p.W, p.act,
                       static_cast<uint32_t>(bid - g.start[i]) * 256u + threadIdx.x,
                       static_cast<uint32_t>(g.start[i + 1] - g.start[i]) * 256u);
 }
@@ -2264,7 +2276,7 @@ void dw3x3_f32_group(const DwProb* p, int n, hipStream_t s) {
     if (p[i].C % 4) throw std::invalid_argument("dw3x3_f32_group: C % 4");
     g.p[i] = p[i];
     g.start[i] = static_cast<int>(blocks);
-    const int64_t work = static_cast<int64_t>(p[i].B) * ((p[i].H + 3) / 4) * p[i].W * (p[i].C / 4);
+    const int64_t work = static_cast<int64_t>(p[i].B) * ((p[i].H + 3) / 4) * ((p[i].W + 3) / 4) * (p[i].C / 4);
     blocks += std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 16384));
   }
   g.start[n] = static_cast<int>(blocks);
@@ -2278,6 +2290,43 @@ void dw3x3_f32(const float* x, const float* w, const float* bias, float* y, int 
     const char* e = std::getenv("NNSX_F32_DW_ROWS");
     return e ? std::atoi(e) : 4;
   }();
+  // rows x columns per lane, R * 10 + CW (NNSX_F32_DW_S1 / NNSX_F32_DW_S2; 0 = the
+  // one-column form below).  Measured (scripts/dw_roofline.py, profiles/r4_dw_lane_shapes.txt):
+  // stride 1 4 x 4 -- 7x7x960 at batch 512 56.3 -> 39.4 us, 14x14x576 130.6 -> 96.2 us,
+  // PoseNet's 17x17x512 21.2 -> 18.7 us; stride 2 2 x 2 -- 129 -> 65 x 64 66.3 -> 60.9 us
+  static const int cfg1 = [] {
+    const char* e = std::getenv("NNSX_F32_DW_S1");
+    return e ? std::atoi(e) : 44;
+  }();
+  static const int cfg2 = [] {
+    const char* e = std::getenv("NNSX_F32_DW_S2");
+    return e ? std::atoi(e) : 22;
+  }();
+  const int cfg = stride == 1 ? cfg1 : cfg2;
+  if (dil == 1 && cfg > 0) {
+    const int R = cfg / 10, CW = cfg % 10;
+    const int64_t work = static_cast<int64_t>(B) * ((Ho + R - 1) / R) * ((Wo + CW - 1) / CW) * (C / 4);
+    const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 65535))));
+#define NNSX_DWC(RR, SS, CC)                                                                                   \
+  case RR * 100 + SS * 10 + CC:                                                                                \
+    hipLaunchKernelGGL((dw3x3_f32_col_kernel<RR, SS, CC>), grid, dim3(256), 0, s, x, w, bias, y, B, H, W, C, Ho, \
+                       Wo, act);                                                                               \
+    return;
+    switch (R * 100 + stride * 10 + CW) {
+      NNSX_DWC(4, 1, 2)
+      NNSX_DWC(4, 1, 4)
+      NNSX_DWC(8, 1, 1)
+      NNSX_DWC(8, 1, 2)
+      NNSX_DWC(2, 1, 2)
+      NNSX_DWC(2, 1, 4)
+      NNSX_DWC(2, 2, 2)
+      NNSX_DWC(1, 2, 2)
+      NNSX_DWC(1, 2, 4)
+      NNSX_DWC(4, 2, 2)
+      default: break;
+    }
+#undef NNSX_DWC
+  }
   if (dil == 1 && rows > 1) {
     const int R = rows >= 4 ? 4 : 2;
     const int64_t work = static_cast<int64_t>(B) * ((Ho + R - 1) / R) * Wo * (C / 4);

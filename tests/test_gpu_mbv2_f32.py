@@ -72,7 +72,12 @@ def test_pw_conv_f32_identity_asymmetric(nns):
 
 
 @pytest.mark.parametrize("B,H,W,C,stride,dil", [(2, 112, 112, 32, 1, 1), (3, 112, 112, 96, 2, 1), (1, 7, 7, 960, 1, 1),
-                                                (2, 15, 9, 144, 2, 1), (2, 33, 33, 320, 1, 2), (1, 65, 65, 64, 1, 4)])
+                                                (2, 15, 9, 144, 2, 1), (2, 33, 33, 320, 1, 2), (1, 65, 65, 64, 1, 4),
+                                                # partial row / column groups of the 4 x 4 (stride 1) and
+                                                # 2 x 2 (stride 2) lanes; SSD's tiny extras
+                                                (2, 13, 11, 64, 1, 1), (1, 5, 6, 16, 2, 1), (3, 17, 17, 512, 1, 1),
+                                                (2, 129, 129, 64, 2, 1), (1, 1, 1, 128, 1, 1), (2, 2, 2, 256, 2, 1),
+                                                (1, 3, 3, 256, 2, 1)])
 @pytest.mark.parametrize("act", [1, 3])
 def test_dw_conv_f32(nns, B, H, W, C, stride, dil, act):
     """act 3 = the producer's deferred ReLU6 applied to the input taps, then ReLU6"""
