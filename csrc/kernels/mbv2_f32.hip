@@ -482,11 +482,13 @@ __global__ void __launch_bounds__(256) dw3x3_f32_kernel(const float* __restrict_
 // CW horizontally adjacent ones x 4 channels, so each loaded input row feeds up
 // to 3 of them ((R-1)S+3 row loads instead of 3R) and each loaded column up to 3
 // ((CW-1)S+3 column loads instead of 3CW)
-template <int R, int S, int CW = 1>
+// D: dilation (padding D; DeepLab's output-stride-16 blocks): input row ir of
+// the lane's window feeds output row j through tap ky = (ir - j S) / D
+template <int R, int S, int CW = 1, int D = 1>
 __device__ __forceinline__ void dw3x3_f32_col(const float* __restrict__ x, const float* __restrict__ w,
                                               const float* __restrict__ bias, float* __restrict__ y, int B, int H,
                                               int W, int C, int Ho, int Wo, int act, uint32_t t0, uint32_t step) {
-  constexpr int NR = (R - 1) * S + 3, NX = (CW - 1) * S + 3;
+  constexpr int NR = (R - 1) * S + 2 * D + 1, NX = (CW - 1) * S + 2 * D + 1;
   const bool ic = (act & 2) != 0;  // (deferred input ReLU6, dw3x3_f32_kernel)
   act &= 1;
   const uint32_t cg = static_cast<uint32_t>(C) >> 2;
@@ -512,25 +514,26 @@ __device__ __forceinline__ void dw3x3_f32_col(const float* __restrict__ x, const
     const float* xb = x + static_cast<int64_t>(b) * H * W * C + c;
 #pragma unroll
     for (int ir = 0; ir < NR; ++ir) {
-      const int iy = oy0 * S - 1 + ir;
+      const int iy = oy0 * S - D + ir;
       if (iy < 0 || iy >= H) continue;
       f32x4_t xv[NX];
 #pragma unroll
       for (int kx = 0; kx < NX; ++kx) {
-        const int ix = ox0 * S - 1 + kx;
+        const int ix = ox0 * S - D + kx;
         xv[kx] = (ix >= 0 && ix < W) ? *reinterpret_cast<const f32x4_t*>(xb + (static_cast<int64_t>(iy) * W + ix) * C)
                                      : f32x4_t{0.f, 0.f, 0.f, 0.f};
         if (ic) xv[kx] = relu6x4(xv[kx]);
       }
 #pragma unroll
       for (int j = 0; j < R; ++j) {
-        const int ky = ir - j * S;
-        if (ky < 0 || ky > 2) continue;
+        const int kd = ir - j * S;
+        if (kd < 0 || kd > 2 * D || kd % D) continue;
+        const int ky = kd / D;
 #pragma unroll
         for (int q = 0; q < CW; ++q)
 #pragma unroll
           for (int kx = 0; kx < 3; ++kx)
-            acc[j][q] = __builtin_elementwise_fma(xv[q * S + kx], wv[ky * 3 + kx], acc[j][q]);
+            acc[j][q] = __builtin_elementwise_fma(xv[q * S + kx * D], wv[ky * 3 + kx], acc[j][q]);
       }
     }
 #pragma unroll
@@ -550,12 +553,12 @@ __device__ __forceinline__ void dw3x3_f32_col(const float* __restrict__ x, const
   }
 }
 
-template <int R, int S, int CW = 1>
+template <int R, int S, int CW = 1, int D = 1>
 __global__ void __launch_bounds__(256) dw3x3_f32_col_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                             const float* __restrict__ bias, float* __restrict__ y,
                                                             int B, int H, int W, int C, int Ho, int Wo, int act) {
-  dw3x3_f32_col<R, S, CW>(x, w, bias, y, B, H, W, C, Ho, Wo, act, blockIdx.x * blockDim.x + threadIdx.x,
-                          gridDim.x * blockDim.x);
+  dw3x3_f32_col<R, S, CW, D>(x, w, bias, y, B, H, W, C, Ho, Wo, act, blockIdx.x * blockDim.x + threadIdx.x,
+                             gridDim.x * blockDim.x);
 }
 
 // several stride-1 depthwise problems in one launch (the SSD heads); problem i
@@ -2303,6 +2306,19 @@ void dw3x3_f32(const float* x, const float* w, const float* bias, float* y, int 
     return e ? std::atoi(e) : 22;
   }();
   const int cfg = stride == 1 ? cfg1 : cfg2;
+  static const bool dil_col = [] {
+    const char* e = std::getenv("NNSX_F32_DW_DIL_COL");
+    return !(e && e[0] == '0');
+  }();
+  if (dil_col && cfg1 > 0 && stride == 1 && dil == 2) {
+    // dilation-2 stride-1 maps (DeepLab's output-stride-16 blocks): 4 x 4 output
+    // lanes over the dilated window, 8 x 8 loads for 16 outputs instead of 144
+    // (dilation 4 would share nothing across a 4 x 4 lane: the one-pixel form)
+    const int64_t work = static_cast<int64_t>(B) * ((Ho + 3) / 4) * ((Wo + 3) / 4) * (C / 4);
+    const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 65535))));
+    hipLaunchKernelGGL((dw3x3_f32_col_kernel<4, 1, 4, 2>), grid, dim3(256), 0, s, x, w, bias, y, B, H, W, C, Ho, Wo, act);
+    return;
+  }
   if (dil == 1 && cfg > 0) {
     const int R = cfg / 10, CW = cfg % 10;
     const int64_t work = static_cast<int64_t>(B) * ((Ho + R - 1) / R) * ((Wo + CW - 1) / CW) * (C / 4);
