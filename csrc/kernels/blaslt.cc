@@ -116,7 +116,8 @@ Plan make_plan(hipblasLtHandle_t h, int M, int N, int K, int Kpad, int act, cons
   int n = 0;
   const hipblasStatus_t st = api().heuristic(h, p.desc, p.a, p.b, p.c, p.c, pref, 4, res, &n);
   api().pref_destroy(pref);
-  if (st != HIPBLAS_STATUS_SUCCESS || n < 1 || res[0].state != HIPBLAS_STATUS_SUCCESS) return p;
+  if (st != HIPBLAS_STATUS_SUCCESS || n < 1 || res[0].state != HIPBLAS_STATUS_SUCCESS || res[0].workspaceSize != 0)
+    return p;
   p.algo = res[0].algo;
   p.ok = true;
   return p;
@@ -124,12 +125,16 @@ Plan make_plan(hipblasLtHandle_t h, int M, int N, int K, int Kpad, int act, cons
 
 }  // namespace
 
+// Opt-in (NNSX_F32_BLASLT=1, read at every call: GEMMs are issued at capture /
+// eager time, never per graph replay).  Two pipeline shapes this path had not
+// run before left the device with a memory-access fault -- PoseNet's 270k-row
+// products and DeepLab's batch-16 17k-row products with the residual as C --
+// while every shape of its tests and of the MobileNetV2 / SSD / DeepLab b8, b32
+// runs was exact; until the library's failing configuration is pinned down the
+// engine's own GEMM is the default (profiles/r4_blaslt_ab.txt: 0.6-3.8 % slower).
 bool blaslt_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("NNSX_F32_BLASLT");
-    return !(e && e[0] == '0');
-  }();
-  return on;
+  const char* e = std::getenv("NNSX_F32_BLASLT");
+  return e && e[0] == '1';
 }
 
 bool blaslt_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,

@@ -70,7 +70,7 @@ struct YLayout {
   int pool = 0;
 };
 // plain fp32 pointwise GEMM on hipBLASLt (blaslt.cc): y[M][N] = act(x . wt^T + bias) (+ res);
-// false = not taken (the caller runs its own kernel).  NNSX_F32_BLASLT=0 turns it off
+// false = not taken (the caller runs its own kernel).  Opt-in: NNSX_F32_BLASLT=1 (blaslt.cc)
 bool blaslt_enabled();
 bool blaslt_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
                      int Kpad, int act, hipStream_t s);

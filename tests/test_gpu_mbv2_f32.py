@@ -44,9 +44,11 @@ def test_pw_conv_f32(nns, M, K, N, act, use_res):
 
 @pytest.mark.parametrize("M,K,N,act,use_res", [(18496, 512, 512, 0, False), (25088, 960, 320, 0, True),
                                               (8712, 160, 960, 0, True), (4096, 128, 64, 0, False)])
-def test_pw_conv_f32_library_path(nns, M, K, N, act, use_res):
+def test_pw_conv_f32_library_path(nns, M, K, N, act, use_res, monkeypatch):
     """Plain linear GEMMs with K >= 128 and M >= 2048 run on hipBLASLt (bias
-    epilogue, residual as C): fp64 oracle and bitwise repeatability."""
+    epilogue, residual as C) when NNSX_F32_BLASLT=1 (opt-in, kernels/blaslt.cc):
+    fp64 oracle and bitwise repeatability."""
+    monkeypatch.setenv("NNSX_F32_BLASLT", "1")
     torch.manual_seed(M + K)
     x = torch.randn(M, K, device="cuda")
     wt = torch.randn((N + 15) // 16 * 16, K, device="cuda") / K ** 0.5
