@@ -780,9 +780,10 @@ class TorchInstance : public FilterInstance {
     size_t bytes = 0;
     for (auto& t : inputs) bytes += t.numel() * t.element_size();
     const int64_t b = inputs[0].size(0);
-    // (batch 8: 1 / 2 / 3 lanes 20.8k / 20.0k / 26.6k frames/s, batch 32 50.0k / 49.3k / 54.2k:
-    // profiles/r4_lanes_ab.txt)
-    return b >= 2 && b <= 32 && bytes <= (8u << 20) ? 3 : 1;
+    // (MobileNetV2 batch 8: 1 / 2 / 3 lanes 20.8k / 20.0k / 26.6k frames/s, batch 32 50.0k / 49.3k /
+    // 54.2k; DeepLab batch 8, 6.3 MB of frames, 1 / 3 lanes 7.64k / 7.21k: its forward is long
+    // enough to fill the chip alone -- profiles/r4_lanes_ab.txt)
+    return b >= 2 && b <= 32 && bytes <= (5u << 20) ? 3 : 1;
   }
   Lane& lane_state(int lane, int dev_idx) {
     Lane& l = lanes_[static_cast<size_t>(lane)];
