@@ -2305,12 +2305,20 @@ void dw3x3_f32(const float* x, const float* w, const float* bias, float* y, int 
     const char* e = std::getenv("NNSX_F32_DW_S2");
     return e ? std::atoi(e) : 22;
   }();
-  const int cfg = stride == 1 ? cfg1 : cfg2;
+  // (the multi-pixel lanes only where they still give every CU a workgroup
+  // (>= 256 x 256 lanes): at batch 1 their few long lanes leave most CUs idle --
+  // PoseNet batch-1 p50 0.36 -> 0.38 ms, DeepLab 0.525 -> 0.543 ms)
+  auto lanes = [&](int cf) {
+    return cf / 10 < 1 || cf % 10 < 1 ? int64_t{0}
+                   : static_cast<int64_t>(B) * ((Ho + cf / 10 - 1) / (cf / 10)) * ((Wo + cf % 10 - 1) / (cf % 10)) * (C / 4);
+  };
+  const bool big = lanes(stride == 1 ? cfg1 : cfg2) >= 65536;
+  const int cfg = !big ? 0 : stride == 1 ? cfg1 : cfg2;
   static const bool dil_col = [] {
     const char* e = std::getenv("NNSX_F32_DW_DIL_COL");
     return !(e && e[0] == '0');
   }();
-  if (dil_col && cfg1 > 0 && stride == 1 && dil == 2) {
+  if (dil_col && big && cfg1 > 0 && stride == 1 && dil == 2) {
     // dilation-2 stride-1 maps (DeepLab's output-stride-16 blocks): 4 x 4 output
     // lanes over the dilated window, 8 x 8 loads for 16 outputs instead of 144
     // (dilation 4 would share nothing across a 4 x 4 lane: the one-pixel form)

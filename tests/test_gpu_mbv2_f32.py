@@ -79,7 +79,10 @@ def test_pw_conv_f32_identity_asymmetric(nns):
                                                 # 2 x 2 (stride 2) lanes; SSD's tiny extras
                                                 (2, 13, 11, 64, 1, 1), (1, 5, 6, 16, 2, 1), (3, 17, 17, 512, 1, 1),
                                                 (2, 129, 129, 64, 2, 1), (1, 1, 1, 128, 1, 1), (2, 2, 2, 256, 2, 1),
-                                                (1, 3, 3, 256, 2, 1), (1, 17, 13, 64, 1, 2), (3, 5, 5, 32, 1, 2)])
+                                                (1, 3, 3, 256, 2, 1), (1, 17, 13, 64, 1, 2), (3, 5, 5, 32, 1, 2),
+                                                # (maps large enough for the multi-pixel lanes, partial groups)
+                                                (8, 45, 43, 256, 1, 1), (16, 33, 33, 288, 1, 2),
+                                                (8, 129, 129, 64, 2, 1)])
 @pytest.mark.parametrize("act", [1, 3])
 def test_dw_conv_f32(nns, B, H, W, C, stride, dil, act):
     """act 3 = the producer's deferred ReLU6 applied to the input taps, then ReLU6"""
