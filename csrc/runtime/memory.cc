@@ -12,6 +12,10 @@ Memory::Memory(void* data, size_t size, MemPlace place, int device, Release rele
     : data_(data), size_(size), place_(place), device_(device), release_(std::move(release)) {}
 
 Memory::~Memory() {
+  // host memory (pageable or pinned) read by an asynchronous H2D copy (map_device
+  // records it as a use): it is freed -- and may be handed out again at once by
+  // malloc or the pinned pool -- only after that copy ran
+  if (place_ != MemPlace::DEVICE && !uses_.empty()) sync_uses();
   if (release_) release_(this);
   if (ready_) hip::event_put(ready_dev_, ready_);
   for (auto& u : uses_) hip::event_put(u.dev, u.event);
@@ -333,8 +337,11 @@ const void* Memory::map_device(int dev, hipStream_t stream) {
     record_use_self(stream, dev);  // (mu_ is held: not record_use, which looks up the mirrors)
   } else {
     if (size_) hip::check(hipMemcpyAsync(mirror->data(), data_, size_, hipMemcpyHostToDevice, stream), "H2D");
-    // a pinned source is read asynchronously: it must not be recycled before the copy ran
-    if (place_ == MemPlace::PINNED) record_use_self(stream, dev);
+    // the source may be read asynchronously (pinned always; pageable too, for the
+    // runtime's own staging): it must not be freed / recycled before the copy ran
+    // (a pageable frame freed at once came back from malloc holding the next
+    // frame, and the queued copy read that: test_hipgraph_static_outputs_...)
+    if (size_) record_use_self(stream, dev);
   }
   mirror->mark_ready(stream);
   dev_mirror_[dev] = mirror;
