@@ -88,7 +88,15 @@ def parse_args(argv=None):
                          "model reads float32 frames")
     ap.add_argument("--sweep", default=os.environ.get("NNSX_BENCH_SWEEP", "8,32,128"),
                     help="comma-separated batch sizes of the throughput / latency sweep ('' = skip)")
-    ap.add_argument("--sweep-steps", type=int, default=10, help="timed steps per sweep point")
+    ap.add_argument("--sweep-steps", type=int, default=100, help="timed steps per sweep point")
+    ap.add_argument("--sweep-warmup", type=int, default=20,
+                    help="warm-up steps per sweep point (replay lanes reach steady state)")
+    ap.add_argument("--extra-configs", default=os.environ.get("NNSX_BENCH_EXTRA", "deeplab_fan,posenet_multi"),
+                    help="WORLD_SIZE > 1: short passes of these multi-rank configs after the headline "
+                         "(their frames/s and RCCL world as extra keys; '' = skip)")
+    ap.add_argument("--extra-steps", type=int, default=20, help="timed steps of each extra config pass")
+    ap.add_argument("--no-selfcheck", action="store_true",
+                    help="WORLD_SIZE > 1: skip the rank-group data-plane self-check before the timed run")
     ap.add_argument("--cpu", action="store_true", help="CPU reference path (device=-1, torch CPU)")
     # (depth 1 / 1: same frames/s as 4 / 2 at batch 512, p50 23 vs 37 ms: profiles/r4_mbv2_ab_b512.txt q11)
     ap.add_argument("--queue", type=int, default=1, help="queue depth between filter and decoder")
@@ -415,6 +423,24 @@ def main():
         if a.precision in ("bf16", "both"):
             runs.append(("bf16", base, "bf16"))
 
+    # WORLD_SIZE > 1: every comm::Group operation on frame-sized payloads (RCCL on
+    # GPUs) before anything is timed -- all-gather uniform / ragged, broadcast,
+    # scatter, a p2p ring and an all-to-all exchange (nnstreamer_amd/parallel/selfcheck.py)
+    selfcheck = None
+    if world > 1 and not a.no_selfcheck:
+        from nnstreamer_amd.parallel import selfcheck as sc
+
+        if use_gpu:
+            def arr(v, d=dev):
+                return torch.as_tensor(v).cuda(d)
+        else:
+            def arr(v):
+                return np.asarray(v)
+        g = nns.Group("bench/selfcheck", rank, world, "", dev, a.comm_backend if use_gpu else "tcp", 60000)
+        selfcheck = sc.run(g, rank, world, arr, scale=1.0 if use_gpu else 1.0 / 64)
+        del g
+        print(f"rank {rank}: rccl_selfcheck {selfcheck}", file=sys.stderr, flush=True)
+
     results = {}
     for label, model_name, dtype in runs:
         model_path = os.path.join(workdir, f"{model_name}.pt")
@@ -443,9 +469,27 @@ def main():
         for sb in [int(x) for x in a.sweep.split(",") if x.strip()]:
             if sb == a.batch:
                 continue
-            r = run_pipeline(a, nns, cfg, model_name, model_path, files, sb, a.sweep_steps, 3, rank, world, dev,
-                             use_gpu, dist)
+            r = run_pipeline(a, nns, cfg, model_name, model_path, files, sb, a.sweep_steps, a.sweep_warmup, rank,
+                             world, dev, use_gpu, dist)
             sweep.append((sb, r))
+
+    # WORLD_SIZE > 1: short passes of the multi-rank configs (config 4's demux fan-out
+    # over RCCL p2p, config 5's edge all-gather), so a scaling run exercises the
+    # same data plane the elements use
+    extra = []
+    if world > 1 and a.extra_configs and a.config == "mbv2":
+        for name in [x for x in a.extra_configs.split(",") if x.strip()]:
+            xc = CONFIGS[name]
+            xm = xc["model"] + ("_fp32" if use_gpu else "")
+            if not use_gpu:
+                xm = xc["model"].replace("_fused", "").replace("_lowres", "")
+            xp = os.path.join(workdir, f"{xm}.pt")
+            export(xm, xp, layout="nhwc")
+            xb = (8 if name == "deeplab_fan" else 64) if use_gpu else 1
+            xs_steps, xs_warm = (a.extra_steps, 5) if use_gpu else (2, 1)  # (CPU twin: plain models, short)
+            r = run_pipeline(a, nns, xc, xm, xp, files, xb, xs_steps, xs_warm, rank, world, dev, use_gpu, dist)
+            r["steps"] = xs_steps
+            extra.append((name, xb, r))
 
     # per-rank records, all-gathered over the job's process group (RCCL on GPUs):
     # [elapsed, p50, p99, gpu_elapsed, gpu_busy] per engine + batch-1 p50/p99
@@ -457,6 +501,11 @@ def main():
     vec += [lat_b1["p50"], lat_b1["p99"]] if lat_b1 else [0.0, 0.0]
     for _, r in sweep:
         vec += [max(r["elapsed"], r["gpu_elapsed"]), r["p50"]]
+    for _, _, r in extra:
+        vec += [max(r["elapsed"], r["gpu_elapsed"])]
+    sc_keys = ["allgather", "allgather_ragged", "broadcast", "scatter", "p2p_ring", "p2p_exchange"]
+    if selfcheck is not None:
+        vec += [1.0 if selfcheck.get(k) else 0.0 for k in sc_keys] + [float(selfcheck["seconds"])]
     stats = torch.tensor(vec, dtype=torch.float64)
     if dist is not None:
         if dist.get_backend() == "nccl":
@@ -542,6 +591,29 @@ def main():
                             "p50_latency_ms": round(float(per_rank[:, base_i + 2 * j + 1].max()), 3)})
             pts.append({"batch": B, "frames_per_s": round(h["fps"], 1), "p50_latency_ms": round(h["p50"], 3)})
             out["sweep"] = sorted(pts, key=lambda d: d["batch"])
+        col = len(runs) * 5 + 2 + 2 * len(sweep)
+        if extra:
+            xs = {}
+            for j, (name, xb, r) in enumerate(extra):
+                el = float(per_rank[:, col + j].max())
+                xs[name] = {"frames_per_s": round(r["workers"] * r["steps"] * xb / el, 1) if el > 0 else None,
+                            "batch": xb, "steps": r["steps"],
+                            "rccl_world": max([int(v.split(":")[1]) for v in r["groups"].values()
+                                               if v.startswith("rccl:")] or [0]),
+                            "groups_rank0": r["groups"]}
+            out["extra_configs"] = xs
+            col += len(extra)
+        if selfcheck is not None:
+            flags = per_rank[:, col:col + len(sc_keys)].min(0).values.tolist()
+            out["rccl_selfcheck"] = {**{k: bool(f > 0.5) for k, f in zip(sc_keys, flags)},
+                                     "backend": selfcheck["backend"], "members": selfcheck["size"],
+                                     "seconds_max": round(float(per_rank[:, col + len(sc_keys)].max()), 3),
+                                     "payloads": "64 MB all-gather / broadcast / scatter, 3-70 MB ragged all-gather, "
+                                                 "48 MB p2p ring, 32 MB all-to-all" if use_gpu else "1/64 scale (CPU)"}
+        try:
+            out["fp32_method"] = str(torch.ops.nnsx.f32_math())
+        except Exception:  # noqa: BLE001
+            out["fp32_method"] = None
         out.update({
             "preprocess": (f"tensor_transform (reference string) absorbed by tensor_filter into the model's uint8 "
                            f"input table ({head['absorbed']}: frames stay uint8)" if head["absorbed"]

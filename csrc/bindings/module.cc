@@ -27,6 +27,10 @@ namespace py = pybind11;
 using namespace nnsx;
 
 namespace nnsx {
+std::string memory_selftest(const std::string& name, int dev);  // runtime/selftest.cc
+}  // namespace nnsx
+
+namespace nnsx {
 void register_python_bridge(py::module_& m);  // python_bridge.cc
 py::object memory_to_numpy(const MemoryPtr& m, const std::string& dtype, std::vector<int64_t> shape);
 py::capsule memory_to_dlpack(const MemoryPtr& m, const TensorInfo& ti);
@@ -72,6 +76,16 @@ PYBIND11_MODULE(_C, m) {
     return py::make_tuple(a, b, c);
   });
   m.def("gpu_count", [] { return hip::device_count(); });
+  m.def("memory_selftest", [](const std::string& name, int dev) {
+    py::gil_scoped_release nogil;
+    return memory_selftest(name, dev);
+  }, py::arg("name"), py::arg("device") = 0,
+        "Deterministic device-memory lifetime regression case (runtime/selftest.cc): '' = pass");
+  m.def("memory_check_enabled", [] { return Memory::check_enabled(); });
+  m.def("memory_drain_deferred", [] {
+    py::gil_scoped_release nogil;
+    Memory::drain_deferred();
+  });
   m.def("gpu_numa_node", [](int d) { return hip::numa_node(d); }, py::arg("device") = 0);
   m.def("bind_numa", [](int d) { return hip::bind_numa(d); }, py::arg("device"),
         "Pin the process to the GPU's NUMA node (CPUs + preferred memory); call before building pipelines");

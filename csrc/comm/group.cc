@@ -582,6 +582,19 @@ bool Group::init(const GroupSpec& in, std::string* err) {
     ncclComm_t c = nullptr;
     if (!nccl_ok(ncclCommInitRank(&c, n, id, grank_), "ncclCommInitRank", err)) return false;
     comm_ = c;
+    // every per-direction p2p link, now: member pairs (a < b) in lexicographic
+    // order, a -> b then b -> a.  Each member walks its own pairs in that order,
+    // so the smallest pair not yet linked always has both members waiting on it
+    // and the walk cannot deadlock; created lazily at a pair's first message
+    // instead, a sender blocked until its peer reached recv(), and members that
+    // all send before they receive waited on each other until the timeout.
+    for (int a = 0; a < n; ++a)
+      for (int b = a + 1; b < n; ++b) {
+        if (grank_ != a && grank_ != b) continue;
+        const int peer = grank_ == a ? b : a;
+        Link* l = nullptr;
+        if (!link(peer, grank_ == a, &l, err) || !link(peer, grank_ == b, &l, err)) return false;
+      }
   }
   NNSX_LOGD("comm", "group ", spec_.name, " rank ", grank_, "/", n, " backend ", backend_name(), " store ", addr);
   return true;
@@ -694,11 +707,11 @@ void Group::finish_inputs(const std::vector<MemoryPtr>& in, hipStream_t s) {
     if (m->size()) m->record_use(s ? s : stream_, device_);
 }
 
-// Per-direction pair communicator, created at the pair's first message.  The
-// sender publishes a unique id and waits (bounded, cancellable: the store) until
-// the receiver -- which learns of the pair from that first message's header --
-// has fetched it; only then do both enter the blocking ncclCommInitRank, so a
-// receiver that never reads the header costs the sender a timeout, not a hang.
+// Per-direction pair communicator (created for every pair at init, in a fixed
+// order; see Group::init).  The sender publishes a unique id and waits
+// (bounded, cancellable: the store) until the receiver has fetched it; only
+// then do both enter the blocking ncclCommInitRank, so a member that never
+// joins costs its peer a timeout, not a hang.
 bool Group::link(int peer, bool tx, Link** out, std::string* err) {
   Link& l = (tx ? tx_ : rx_).at(static_cast<size_t>(peer));
   *out = &l;

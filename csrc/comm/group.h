@@ -30,7 +30,9 @@
 //
 // Point-to-point payloads ride on per-direction links: for each ordered pair
 // (sender -> receiver) a two-rank RCCL communicator with its own stream on
-// both sides, created at the pair's first message.  A send kernel then waits
+// both sides, all created when the group opens (pairs in lexicographic order,
+// so the creation itself cannot deadlock and no send waits for its peer to
+// reach recv()).  A send kernel then waits
 // only for receives of the SAME direction, which its own earlier sends
 // already matched, so no cycle of GPU waits can form -- a ring or a
 // bidirectional exchange of frame-sized messages cannot deadlock the way one

@@ -242,22 +242,23 @@ class EdgeHub {
   }
   void subscribe(int global_rank) {
     std::lock_guard<std::mutex> lk(mu_);
-    auto& q = subs_[global_rank];
+    auto& q = subs_[global_rank].q;
     // a subscriber that starts after the caps round still gets the caps (sticky)
     auto c = caps_.find(global_rank);
     if (q.empty() && c != caps_.end()) q.push_back(c->second);
-    cancelled_ = false;
   }
   void unsubscribe(int global_rank) {
     std::lock_guard<std::mutex> lk(mu_);
     subs_.erase(global_rank);
     cv_.notify_all();
   }
-  // one round: every member's packet, dealt to the subscribed queues
+  // one round: every member's packet, dealt to the subscribed queues.  false:
+  // the round failed, or cancel_publish() ended this call's wait for room
   bool publish(comm::Group& g, const comm::Packet& mine, std::string* err) {
     std::vector<comm::Packet> all;
     if (!g.allgather(mine, &all, err)) return false;
     std::unique_lock<std::mutex> lk(mu_);
+    const uint64_t gen = pub_gen_;
     for (size_t r = 0; r < all.size(); ++r) {
       const int src = g.global_rank(static_cast<int>(r));
       if (all[r].flags & kPktCaps) {
@@ -268,49 +269,67 @@ class EdgeHub {
       if (it == subs_.end()) continue;
       cv_.wait(lk, [&] {
         auto i = subs_.find(src);
-        return cancelled_ || i == subs_.end() || i->second.size() < kDepth;
+        return pub_gen_ != gen || i == subs_.end() || i->second.q.size() < kDepth;
       });
-      if (cancelled_) return false;
+      if (pub_gen_ != gen) return false;
       it = subs_.find(src);
       if (it == subs_.end()) continue;
       all[r].src = src;
-      it->second.push_back(std::move(all[r]));
+      it->second.q.push_back(std::move(all[r]));
     }
     cv_.notify_all();
     return true;
   }
-  // next packet of member `global_rank` (false + *timed_out on timeout)
+  // next packet of member `global_rank` (false + *timed_out on timeout; false:
+  // unsubscribed, or cancel_take(global_rank) ended this call's wait)
   bool take(int global_rank, comm::Packet* p, int timeout_ms, bool* timed_out) {
     std::unique_lock<std::mutex> lk(mu_);
     *timed_out = false;
+    auto it0 = subs_.find(global_rank);
+    if (it0 == subs_.end()) return false;
+    const uint64_t gen = it0->second.cancel_gen;
     auto ready = [&] {
       auto it = subs_.find(global_rank);
-      return cancelled_ || (it != subs_.end() && !it->second.empty());
+      return it == subs_.end() || it->second.cancel_gen != gen || !it->second.q.empty();
     };
     if (!cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), ready)) {
       *timed_out = true;
       return false;
     }
-    if (cancelled_) return false;
-    auto& q = subs_[global_rank];
-    *p = std::move(q.front());
-    q.pop_front();
+    auto it = subs_.find(global_rank);
+    if (it == subs_.end() || it->second.cancel_gen != gen) return false;
+    *p = std::move(it->second.q.front());
+    it->second.q.pop_front();
     cv_.notify_all();
     return true;
   }
-  void cancel() {
+  // Cancellation is per waiter: it ends the waits in progress of ONE party --
+  // the publishing edgesink's publish() (its unlock / flush), or one
+  // subscriber's take() (its edgesrc's unlock) -- and nothing later, so one
+  // element stopping never fails the other elements of the topic.
+  void cancel_publish() {
     std::lock_guard<std::mutex> lk(mu_);
-    cancelled_ = true;
+    ++pub_gen_;
+    cv_.notify_all();
+  }
+  void cancel_take(int global_rank) {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = subs_.find(global_rank);
+    if (it != subs_.end()) ++it->second.cancel_gen;
     cv_.notify_all();
   }
 
  private:
   static constexpr size_t kDepth = 4;
+  struct Sub {
+    std::deque<comm::Packet> q;
+    uint64_t cancel_gen = 0;
+  };
   std::mutex mu_;
   std::condition_variable cv_;
-  std::map<int, std::deque<comm::Packet>> subs_;  // per subscribed source (global rank)
-  std::map<int, comm::Packet> caps_;              // latest caps packet per source
-  bool cancelled_ = false;
+  std::map<int, Sub> subs_;           // per subscribed source (global rank)
+  std::map<int, comm::Packet> caps_;  // latest caps packet per source
+  uint64_t pub_gen_ = 0;
 };
 
 comm::Packet packet_of(const Buffer& b) {
@@ -1048,7 +1067,7 @@ class EdgeSink : public BaseSink {
   void unlock() override {
     running_ = false;
     cv_.notify_all();
-    if (auto h = hub_) h->cancel();
+    if (auto h = hub_) h->cancel_publish();
     if (auto g = g_) g->cancel();
   }
   bool set_caps(const Caps& caps) override {
@@ -1227,7 +1246,7 @@ class EdgeSrc : public BaseSrc {
   }
   void on_unlock() override {
     if (conn_) conn_->close();
-    if (auto h = hub_) h->cancel();
+    if (auto h = hub_) h->cancel_take(hub_src_);
     if (auto g = g_) g->cancel();
   }
 

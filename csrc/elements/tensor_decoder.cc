@@ -2,6 +2,9 @@
 // forwarded through set_option(idx).  Reference: gst/nnstreamer/elements/
 // gsttensor_decoder.c (registry :133-200, props :286-397, transform :666-742,
 // caps :750-907, custom register :936-974).
+#include <atomic>
+#include <mutex>
+
 #include "core/log.h"
 #include "elements/elements.h"
 #include "elements/tensor_common.h"
@@ -31,18 +34,24 @@ class CustomCodeDecoder : public DecoderInstance {
 };
 
 // DecodeStage over a decoder instance: prepared on the filter's device, run by
-// the filter inside its graph capture (runtime/fusion.h)
+// the filter inside its graph capture (runtime/fusion.h).  It shares ownership
+// of the instance (a mode change replaces the decoder's instance while the
+// filter may still hold the stage) and goes stale when the decoder's mode or
+// options change (revoke()): the filter then re-takes a stage and re-captures.
 class InstanceStage : public DecodeStage {
  public:
-  InstanceStage(DecoderInstance* inst, TensorsInfo out) : inst_(inst), out_(std::move(out)) {}
+  InstanceStage(std::shared_ptr<DecoderInstance> inst, TensorsInfo out) : inst_(std::move(inst)), out_(std::move(out)) {}
   const TensorsInfo& out_info() const override { return out_; }
   bool enqueue(const std::vector<const void*>& in, const std::vector<void*>& out, void* stream) override {
     return inst_->stage_enqueue(in, out, static_cast<hipStream_t>(stream));
   }
+  bool stale() const override { return stale_.load(); }
+  void revoke() { stale_.store(true); }
 
  private:
-  DecoderInstance* inst_;
+  std::shared_ptr<DecoderInstance> inst_;
   TensorsInfo out_;
+  std::atomic<bool> stale_{false};
 };
 
 class TensorDecoder : public BaseTransform, public ArgmaxConsumer, public DecodeStageConsumer {
@@ -54,6 +63,7 @@ class TensorDecoder : public BaseTransform, public ArgmaxConsumer, public Decode
       prop_string("option" + std::to_string(i + 1), &options_[i], "Option " + std::to_string(i + 1) + " of the decoder mode",
                   [this, i] {
                     if (i == 0 && mode_ == "custom-code") return load_mode();  // the callback's name
+                    revoke_stage();  // (options are baked into a captured stage)
                     if (inst_ && !inst_->set_option(i, options_[i]))
                       throw Error("decoder " + mode_ + " rejected option" + std::to_string(i + 1) + "=" + options_[i]);
                   });
@@ -93,18 +103,31 @@ class TensorDecoder : public BaseTransform, public ArgmaxConsumer, public Decode
     if (!inst_->stage_prepare(model_out, dev, streams_.get(dev), &out) || out.num_tensors != 1 ||
         out.at(0).type != DType::UINT8 || out.at(0).dim[0] != 4)
       return nullptr;
+    auto st = std::make_shared<InstanceStage>(inst_, out);
+    std::lock_guard<std::mutex> lk(stage_mu_);
     stage_in_ = model_out;
     stage_by_ = by;
-    stage_ = std::make_shared<InstanceStage>(inst_.get(), out);
-    return stage_;
+    stage_ = st;
+    return st;
   }
   void drop_stage() override {
+    std::lock_guard<std::mutex> lk(stage_mu_);
     stage_.reset();
     stage_by_.clear();
   }
 
  protected:
+  void revoke_stage() {
+    std::lock_guard<std::mutex> lk(stage_mu_);
+    if (auto* st = dynamic_cast<InstanceStage*>(stage_.get())) st->revoke();
+  }
+  // (the filter's thread takes / drops the stage; this element's thread reads it)
+  std::shared_ptr<DecodeStage> current_stage() {
+    std::lock_guard<std::mutex> lk(stage_mu_);
+    return stage_;
+  }
   void load_mode() {
+    revoke_stage();
     inst_.reset();
     auto parts = split(mode_, ':', 2);
     // mode=custom-code option1=<name> (the reference's spelling, gsttensor_decoder.c:469,763)
@@ -206,7 +229,7 @@ class TensorDecoder : public BaseTransform, public ArgmaxConsumer, public Decode
     } else {
       mems = in->mems;
     }
-    if (stage_) {
+    if (current_stage()) {
       // the upstream filter ran this decoder's device stage: [4:W:H:B] RGBA
       // frames, one output buffer per frame (views, no copy)
       const TensorInfo& ti = cfg.info.at(0);
@@ -264,8 +287,9 @@ class TensorDecoder : public BaseTransform, public ArgmaxConsumer, public Decode
 
   std::string mode_, options_[9], config_file_;
   int device_ = -2;
-  std::unique_ptr<DecoderInstance> inst_;
+  std::shared_ptr<DecoderInstance> inst_;
   std::string argmax_by_;
+  std::mutex stage_mu_;
   std::shared_ptr<DecodeStage> stage_;  // run upstream by stage_by_ (take_stage)
   TensorsConfig stage_in_;              // the model output the stage was prepared for
   std::string stage_by_;

@@ -402,6 +402,7 @@ class TensorFilter : public BaseTransform, public TransformAbsorber {
             if (inst_->set_output_stage(st)) {
               stage_consumer_ = c;
               stage_ = st;
+              stage_model_out_ = mc;
               absorbed_decoder_ = dn->name();
               NNSX_LOGI(name(), "runs the device post-processing of ", absorbed_decoder_, " inside its graph");
             } else {
@@ -412,6 +413,32 @@ class TensorFilter : public BaseTransform, public TransformAbsorber {
       }
     }
     if (stage_) *mout = stage_->out_info();
+  }
+  // the decoder's mode / options changed after its stage was captured: take a
+  // fresh stage for the same model outputs (the filter re-captures its graphs);
+  // false when the decoder no longer offers one with the same output
+  bool refresh_decoder_stage() {
+    const TensorsConfig mc = stage_model_out_;
+    const TensorsInfo old = stage_->out_info();
+    const int dev = inst_->stage_device();
+    inst_->set_output_stage(nullptr);
+    {
+      // replays of the old graphs may still read the stage's scratch, which
+      // re-preparing the stage replaces (a rare event: a sync is fine)
+      hip::DeviceGuard g(dev);
+      hip::check(hipDeviceSynchronize(), "decoder stage refresh");
+    }
+    stage_.reset();
+    // (the decoder swaps its stage in take_stage: it never sees none in between)
+    auto st = stage_consumer_->take_stage(mc, dev, name());
+    if (!st || !(st->out_info() == old) || !inst_->set_output_stage(st)) {
+      if (st) stage_consumer_->drop_stage();
+      stage_consumer_ = nullptr;
+      return false;
+    }
+    stage_ = st;
+    NNSX_LOGI(name(), "re-took the device post-processing of ", absorbed_decoder_, " (decoder options changed)");
+    return true;
   }
   void release_decoder_stage() {
     if (stage_consumer_) {
@@ -578,6 +605,11 @@ class TensorFilter : public BaseTransform, public TransformAbsorber {
     if (!configured_ || !inst_) {
       post_error("tensor_filter: not configured");
       return FlowReturn::NOT_NEGOTIATED;
+    }
+    if (stage_ && stage_->stale() && !refresh_decoder_stage()) {
+      post_error("tensor_filter: the absorbed decoder changed its output while playing (" + absorbed_decoder_ +
+                 "); restart the pipeline");
+      return FlowReturn::ERROR;
     }
     // QoS throttling drop (tensor_filter.c:501-552)
     if (throttle_delay_ > 0 && inbuf->pts >= 0) {
@@ -916,6 +948,7 @@ class TensorFilter : public BaseTransform, public TransformAbsorber {
   bool stage_tried_ = false;
   DecodeStageConsumer* stage_consumer_ = nullptr;
   std::shared_ptr<DecodeStage> stage_;
+  TensorsConfig stage_model_out_;  // the model outputs the stage was taken for
   std::string absorbed_decoder_;
   AbsorbableElement* absorbable_up_ = nullptr;
   std::string absorbed_from_;

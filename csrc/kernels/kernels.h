@@ -103,5 +103,8 @@ bool sparse_scatter(const void* payload, int elem_size, uint32_t nnz, void* out,
 size_t mean_workspace_bytes();
 bool tensor_mean(const void* x, DType t, uint64_t n, double* d_ws, hipStream_t s);
 
+// debug: hold stream s busy for `us` microseconds (bounded to 0.2 s; kernels/debug.hip)
+void spin_us(hipStream_t s, int us);
+
 }  // namespace kernels
 }  // namespace nnsx

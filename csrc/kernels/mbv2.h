@@ -49,6 +49,14 @@ bool ir_block_supported(int stride, int cin, int hid, int cout);
 bool ir_block(const IrBlockArgs& a, hipStream_t s);
 
 // ---------------------------------------------------------------- fp32 ----
+// How the fp32 engine computes its GEMM-shaped products: kX3 = split-bf16 MFMAs
+// (each operand = three bf16 parts, six cross products, fp32 sums; error vs an
+// fp64 oracle below the native fp32 MFMA's), kNative = v_mfma_f32_16x16x4_f32.
+// Default from NNSX_F32_MATH (x3 | fp32); x3 unless set.
+enum class F32Math { kNative = 0, kX3 = 1 };
+F32Math f32_math();
+void set_f32_math(F32Math m);
+const char* f32_math_name(F32Math m);
 // The reference-precision engine (mbv2_f32.hip): fp32 activations, weights
 // and accumulation, GEMMs on v_mfma_f32_16x16x4_f32.
 // y[M][N] = act(x[M][K] . wt[N][K]^T + bias) (+ res); wt zero-padded [Npad][Kpad]
@@ -174,6 +182,11 @@ struct IrBlockF32Args {
   // to the last one.  Only launched when every workgroup of the grid is resident
   // at once (the host checks occupancy); the wait is bounded.
   int spread = 0;
+  // split-bf16 weights (F32Math::kX3): we3 [3][hid][ceil32(cin)], wp3
+  // [3][ceil32(cout)][hid] bf16 (hi, mid, lo parts; zero padded).  Both set and
+  // the method x3: the irw_x3 kernel of the same geometry, when there is one
+  const uint16_t* we3 = nullptr;
+  const uint16_t* wp3 = nullptr;
 };
 // Launches enqueued by this thread while a SharedDeviceScope is alive may run
 // concurrently with other kernels of the same process (a filter's replay
@@ -192,6 +205,8 @@ struct SharedDeviceScope {
   bool prev_;
 };
 bool device_shared();
+// set this thread's flag directly (tests); returns the previous value
+bool set_device_shared(bool on);
 
 bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout, bool has_expand, int dil = 1);
 // device workspace ir_block_f32 needs for these args (0 = none)
@@ -226,6 +241,9 @@ struct StemIr1F32Args {
 };
 bool stem_ir1_f32(const StemIr1F32Args& a, hipStream_t s);
 bool ir_block_f32(const IrBlockF32Args& a, hipStream_t s);
+// which product method ir_block_f32 uses for this shape under the current
+// F32Math with x3 weights given: "x3", "fp32", or "" (unsupported)
+const char* ir_block_f32_method(int stride, int H, int W, int cin, int hid, int cout, int B, int dil = 1);
 
 }  // namespace kernels
 }  // namespace nnsx

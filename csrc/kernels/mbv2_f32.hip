@@ -41,9 +41,11 @@
 #include <cmath>
 #include <cstdlib>
 #include <stdexcept>
+#include <string>
 #include <vector>
 
 #include "kernels/mbv2.h"
+#include "kernels/x3.h"
 
 namespace nnsx {
 namespace kernels {
@@ -60,8 +62,6 @@ namespace {
 constexpr int kStemIr1Cfg[3] = {NNSX_STEM_TILE};
 constexpr int kStemIr1TY = kStemIr1Cfg[0], kStemIr1TX = kStemIr1Cfg[1], kStemIr1NW = kStemIr1Cfg[2];
 
-typedef float f32x4_t __attribute__((ext_vector_type(4)));
-typedef float f32x2_t __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f32x4_t mfma4(float a, float b, f32x4_t c) {
@@ -105,7 +105,9 @@ constexpr int GKQ = GKT / 4;  // k-quads per stage
 
 // one BM x BN output tile over k-stages [kbeg, kbeg + nk * GKT); zs / slab: this
 // block's split-K slice and whether the grid is split (then y is the slab workspace)
-template <int BM, int BN>
+// X3: the products on split-bf16 MFMAs (see split_x3), the LDS images and the
+// epilogue unchanged
+template <int BM, int BN, bool X3 = false>
 __device__ __forceinline__ void pw_gemm_f32_tile(const float* __restrict__ x,     // [M][K]
                                                  const float* __restrict__ wt,    // [Npad][Kpad]
                                                  const float* __restrict__ bias,  // [N]
@@ -169,8 +171,27 @@ __device__ __forceinline__ void pw_gemm_f32_tile(const float* __restrict__ x,   
   for (int ks = 0; ks < nk; ++ks) {
     const int buf = ks & 1;
     if (ks + 1 < nk) gload(kbeg + (ks + 1) * GKT);  // in flight during this stage's MFMAs
+    if constexpr (X3) {
+      static_assert(GKT == 32, "x3: one 32-k step per stage");
+      // lane (li, g): k-quads 2g, 2g + 1 of its row = k 8g .. 8g + 7
+      X3Frag a[RN];
 #pragma unroll
-    for (int s = 0; s < GKT / 16; ++s) {
+      for (int j = 0; j < RN; ++j) {
+        const int r = wn * (BN / 2) + j * 16 + li;
+        a[j] = split_x3(*reinterpret_cast<const f32x4_t*>(&ws[buf][2 * g][r ^ (2 * g)][0]),
+                        *reinterpret_cast<const f32x4_t*>(&ws[buf][2 * g + 1][r ^ (2 * g + 1)][0]));
+      }
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        const int r = wm * (BM / 2) + i * 16 + li;
+        const X3Frag b = split_x3(*reinterpret_cast<const f32x4_t*>(&xs[buf][2 * g][r ^ (2 * g)][0]),
+                                  *reinterpret_cast<const f32x4_t*>(&xs[buf][2 * g + 1][r ^ (2 * g + 1)][0]));
+#pragma unroll
+        for (int j = 0; j < RN; ++j) acc[i][j] += mfma_x3(a[j], b);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < (X3 ? 0 : GKT / 16); ++s) {
       const int kq = 4 * s + g;
       f32x4_t a[RN], b[RM];
 #pragma unroll
@@ -275,7 +296,7 @@ __device__ __forceinline__ void pw_gemm_f32_tile(const float* __restrict__ x,   
   }
 }
 
-template <int BM, int BN>
+template <int BM, int BN, bool X3 = false>
 __global__ void __launch_bounds__(256) pw_gemm_f32_kernel(const float* __restrict__ x, const float* __restrict__ wt,
                                                           const float* __restrict__ bias, const float* __restrict__ res,
                                                           float* __restrict__ y, int M, int N, int K, int Kpad, int Npad,
@@ -286,8 +307,8 @@ __global__ void __launch_bounds__(256) pw_gemm_f32_kernel(const float* __restric
   const int flat = xcd_remap(blockIdx.y * nbx + blockIdx.x, nbx * nby);
   const int kbeg = blockIdx.z * kchunk * GKT;
   const int kend = min(Kpad, kbeg + kchunk * GKT);
-  pw_gemm_f32_tile<BM, BN>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, kbeg, (kend - kbeg + GKT - 1) / GKT,
-                           static_cast<int>(blockIdx.z), gridDim.z > 1, yl, (flat % nbx) * BM, (flat / nbx) * BN);
+  pw_gemm_f32_tile<BM, BN, X3>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, kbeg, (kend - kbeg + GKT - 1) / GKT,
+                               static_cast<int>(blockIdx.z), gridDim.z > 1, yl, (flat % nbx) * BM, (flat / nbx) * BN);
 }
 
 // Several independent GEMMs in one launch (the SSD prediction heads): block b
@@ -300,14 +321,14 @@ struct GemmGroupArgs {
   GemmProb p[kGroupMax];
 };
 
-template <int BM, int BN>
+template <int BM, int BN, bool X3 = false>
 __global__ void __launch_bounds__(256) pw_gemm_group_f32_kernel(GemmGroupArgs g) {
   const int flat = blockIdx.x;
   int i = 0;
   while (i + 1 < g.n && flat >= g.start[i + 1]) ++i;
   const GemmProb& p = g.p[i];
   const int local = flat - g.start[i], gx = (p.M + BM - 1) / BM;
-  pw_gemm_f32_tile<BM, BN>(p.x, p.wt, p.bias, nullptr, p.y, p.M, p.N, p.K, p.Kpad, p.Npad, p.act, 0,
+  pw_gemm_f32_tile<BM, BN, X3>(p.x, p.wt, p.bias, nullptr, p.y, p.M, p.N, p.K, p.Kpad, p.Npad, p.act, 0,
                            (p.Kpad + GKT - 1) / GKT, 0, false, p.yl, (local % gx) * BM, (local / gx) * BN);
 }
 
@@ -991,6 +1012,78 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// In-launch combine of a tile's hidden parts (irw_f32 / irw_x3), after every
+// part wrote its slab write-through (sc1) to a.ws.
+template <int TY, int TX, int NT>
+__device__ __forceinline__ void irw_inlaunch_combine(const IrBlockF32Args& a, float* smem, int tile, int part,
+                                                     int nparts, int b, int oy0, int ox0, int tid) {
+  // ---- in-launch combine of the hidden parts (MI355X hand-off, counter form):
+  // every part's slab went out write-through (sc1, so no release fence); each
+  // storing wave drains it, the workgroup meets at a barrier, one lane draws a
+  // ticket; the tile's last part reads every slab with sc1 loads (so no acquire
+  // fence either) and adds them in part order, + bias (+ residual) -- the sums
+  // of irw_reduce in its order, without its launch -- then resets the ticket
+  // for the next launch (tickets start at zero: the caller's buffer is zeroed
+  // once at creation).  Correct for any placement of the parts over XCDs.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave's slab stores done; the LDS is free
+  const int64_t plane = static_cast<int64_t>(a.B) * a.Ho * a.Wo * a.cout;
+  const __amdgpu_buffer_rsrc_t slab =
+      __builtin_amdgcn_make_buffer_rsrc(a.ws, 0, static_cast<int>(nparts * plane * sizeof(float)), 0x00020000);
+  const int nq = a.cout / 4;
+  // the tile's output quads [v0, v1): all of them (last-arriver form) or this
+  // part's share (spread form), summed over the slabs in part order
+  auto combine = [&](int v0, int v1) {
+    for (int v = v0 + tid; v < v1; v += NT) {
+      const int q = v / nq, co = (v - q * nq) * 4;
+      const int gy = oy0 + q / TX, gx = ox0 + q % TX;
+      if (gy >= a.Ho || gx >= a.Wo) continue;
+      const int64_t e = ((static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx) * a.cout + co;
+      f32x4_t s =
+          __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(slab, static_cast<int>(e * 4), 0, 16));
+      for (int p = 1; p < nparts; ++p)
+        s += __builtin_bit_cast(
+            f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(slab, static_cast<int>((p * plane + e) * 4), 0, 16));
+      s += *reinterpret_cast<const f32x4_t*>(a.bp + co);
+      if (a.residual) s += *reinterpret_cast<const f32x4_t*>(a.x + (e / a.cout) * a.cin + co);
+      *reinterpret_cast<f32x4_t*>(a.y + e) = s;
+    }
+  };
+  if (a.spread) {
+    // spread form: one lane per part bumps the tile's monotone 64-bit arrival
+    // count and waits until every part of this launch has arrived (count >=
+    // the next multiple of nparts); then each part adds its 1/nparts share.
+    // The host launches this form only when the whole grid is resident at
+    // once; the wait is bounded all the same (~0.2 s), so a broken residency
+    // assumption shows up as wrong sums, never as a hung GPU.
+    if (tid == 0) {
+      unsigned long long* ctr = reinterpret_cast<unsigned long long*>(a.tickets) + tile;
+      const unsigned long long t = __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long target = (t / nparts + 1) * nparts;
+      for (int it = 0; it < (1 << 21); ++it) {
+        if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the wait)
+    const int total = TY * TX * nq, chunk = (total + nparts - 1) / nparts;
+    combine(part * chunk, min(total, (part + 1) * chunk));
+    return;
+  }
+  int* flag = reinterpret_cast<int*>(smem);
+  if (tid == 0) {
+    const int t = __hip_atomic_fetch_add(a.tickets + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == nparts - 1;
+    if (last) __hip_atomic_store(a.tickets + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the ticket)
+  combine(0, TY * TX * nq);
+}
+
 // (second launch bound = minimum waves per SIMD: 2 keeps every configuration
 // but the 7x7 / 160-channel one within 256 VGPRs, two workgroups per CU)
 //
@@ -1305,71 +1398,294 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
   }
   if (!a.ws || !a.tickets) return;
 
-  // ---- in-launch combine of the hidden parts (MI355X hand-off, counter form):
-  // every part's slab went out write-through (sc1, so no release fence); each
-  // storing wave drains it, the workgroup meets at a barrier, one lane draws a
-  // ticket; the tile's last part reads every slab with sc1 loads (so no acquire
-  // fence either) and adds them in part order, + bias (+ residual) -- the sums
-  // of irw_reduce in its order, without its launch -- then resets the ticket
-  // for the next launch (tickets start at zero: the caller's buffer is zeroed
-  // once at creation).  Correct for any placement of the parts over XCDs.
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // every wave's slab stores done; the LDS is free
-  const int64_t plane = static_cast<int64_t>(a.B) * a.Ho * a.Wo * a.cout;
-  const __amdgpu_buffer_rsrc_t slab =
-      __builtin_amdgcn_make_buffer_rsrc(a.ws, 0, static_cast<int>(nparts * plane * sizeof(float)), 0x00020000);
-  const int nq = a.cout / 4;
-  // the tile's output quads [v0, v1): all of them (last-arriver form) or this
-  // part's share (spread form), summed over the slabs in part order
-  auto combine = [&](int v0, int v1) {
-    for (int v = v0 + tid; v < v1; v += NT) {
-      const int q = v / nq, co = (v - q * nq) * 4;
-      const int gy = oy0 + q / TX, gx = ox0 + q % TX;
-      if (gy >= a.Ho || gx >= a.Wo) continue;
-      const int64_t e = ((static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx) * a.cout + co;
-      f32x4_t s =
-          __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(slab, static_cast<int>(e * 4), 0, 16));
-      for (int p = 1; p < nparts; ++p)
-        s += __builtin_bit_cast(
-            f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(slab, static_cast<int>((p * plane + e) * 4), 0, 16));
-      s += *reinterpret_cast<const f32x4_t*>(a.bp + co);
-      if (a.residual) s += *reinterpret_cast<const f32x4_t*>(a.x + (e / a.cout) * a.cin + co);
-      *reinterpret_cast<f32x4_t*>(a.y + e) = s;
+  irw_inlaunch_combine<TY, TX, NT>(a, smem, tile, part, nparts, b, oy0, ox0, tid);
+}
+
+// ------------------------------------------------------------- irw_x3 ----
+// The wave-split fused inverted residual with its products on split-bf16
+// MFMAs (kernels/x3.h): the same tiles, waves, hidden parts and combine as
+// irw_f32, and
+//   * the input tile is split once, while it is staged: three bf16 planes
+//     [part][k8][cell] (8 channels = 16 B per cell), cells XOR-swizzled by k8
+//     within their 16-cell group (the staging writes spread over the banks;
+//     a fragment read stays 256 contiguous bytes per 16 lanes);
+//   * expand: per 16-channel subtile, six v_mfma_f32_16x16x32_bf16 per 32 input
+//     channels (weights pre-split at export: we3 [3][hid][ceil32(cin)] bf16);
+//   * depthwise: lane = one pixel of a 32-pixel tile x 8 of the subtile's 16
+//     channels -- exactly the B operand of v_mfma_f32_32x32x16_bf16 (k = 8 (l >> 5)
+//     + j), split into its three parts in registers;
+//   * project: 32 output channels x 32 pixels x the subtile's 16 channels per
+//     six 32x32x16 MFMAs (wp3 [3][ceil32(cout)][hid] bf16), the subtile's
+//     partial added to the accumulator by the VALU (round to nearest).
+// The cross-wave reduction, hidden parts and in-launch combine are irw_f32's.
+template <int S, int TY, int TX, int KIN, int NOT, int NW, bool FULL, int DIL = 1>
+struct IrwX3Geom {
+  using Base = IrwGeom<S, TY, TX, KIN, NOT, NW, FULL, DIL>;
+  static constexpr int TIY = Base::TIY, TIX = Base::TIX, PIN = Base::PIN, NC16 = Base::NC16, NBT = Base::NBT;
+  static constexpr int PINP = Base::PINP;
+  static constexpr int KP = (KIN + 31) / 32 * 32, NK32 = KP / 32, K8 = KP / 8;
+  static constexpr int XSP = NC16;                   // cells per plane
+  static constexpr int NP32 = (TY * TX + 31) / 32;   // 32-pixel project tiles
+  static constexpr int NPX = NP32 * 32;
+  static constexpr int NO32 = (NOT * 16 + 31) / 32;  // 32-channel output tiles (rows of wp3)
+  static constexpr size_t xs_b = static_cast<size_t>(3) * K8 * XSP * 16;
+  static constexpr size_t hid_b = static_cast<size_t>(16) * 4 * NW * PINP;
+  static constexpr size_t red_b = static_cast<size_t>(16) * 8 * NW * NPX;  // [wave][cout quad][px]
+  static size_t lds_bytes(int) { return std::max(xs_b + hid_b, red_b); }
+  static constexpr int MINB = NO32 * NP32 <= 4 ? 2 : 1;
+};
+
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+
+template <int S, int TY, int TX, int KIN, int NOT, int NW, bool FULL, int DIL = 1>
+__global__ void __launch_bounds__(64 * NW, (IrwX3Geom<S, TY, TX, KIN, NOT, NW, FULL, DIL>::MINB))
+    irw_x3_kernel(IrBlockF32Args a) {
+  using G = IrwX3Geom<S, TY, TX, KIN, NOT, NW, FULL, DIL>;
+  constexpr int NT = 64 * NW;
+  constexpr int TIX = G::TIX, PIN = G::PIN, NC16 = G::NC16, NBT = G::NBT, PINP = G::PINP;
+  constexpr int KP = G::KP, K8 = G::K8, NK32 = G::NK32, XSP = G::XSP, NP32 = G::NP32, NPX = G::NPX;
+  constexpr int NO32 = G::NO32, NOA = NO32 > 0 ? NO32 : 1;
+  constexpr int KQP = KP / 4;  // fp32 quads staged per cell (zeros past cin)
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  bf16x8_t* xs = reinterpret_cast<bf16x8_t*>(smem);  // [3][K8][XSP], cell swizzled by k8
+  f32x4_t* hidw = reinterpret_cast<f32x4_t*>(reinterpret_cast<char*>(smem) + G::xs_b);  // [NW][4][PINP]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, g = lane >> 4, l32 = lane & 31, h = lane >> 5;
+  const int nparts = a.hsplit;
+  const int tiles_img = a.tiles_x * a.tiles_y;
+
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int part = wg % nparts, tile = wg / nparts;
+  const int b = tile / tiles_img;
+  const int tyx = tile - b * tiles_img;
+  const int oy0 = (tyx / a.tiles_x) * TY, ox0 = (tyx % a.tiles_x) * TX;
+  const int iy0 = oy0 * S - DIL, ix0 = ox0 * S - DIL;
+  const int ry0 = max(iy0, 0), ry1 = min(iy0 + G::TIY, a.H);
+  const int rx0 = max(ix0, 0), rx1 = min(ix0 + TIX, a.W);
+  const int RW = rx1 - rx0, NC = FULL ? PIN : (ry1 - ry0) * RW;
+  const float rrw = 1.f / static_cast<float>(RW);
+
+  // ---- stage the input tile, split into its bf16 parts on the way (loads of
+  // the whole tile issued first, branch-free, then the LDS stores)
+  {
+    constexpr int NSV = NC16 * KQP, NSIT = (NSV + NT - 1) / NT;
+    f32x4_t sv[NSIT];
+    bool sok[NSIT];
+    const float* qb = a.x + static_cast<int64_t>(b) * a.H * a.W * a.cin;
+#pragma unroll
+    for (int it = 0; it < NSIT; ++it) {
+      const int v = tid + it * NT;
+      const int c = v / KQP, kq = v - c * KQP;
+      int yy, xx;
+      if constexpr (FULL) {
+        yy = iy0 + c / TIX;
+        xx = ix0 + c % TIX;
+      } else {
+        const int cy = static_cast<int>((static_cast<float>(c) + 0.5f) * rrw);
+        yy = ry0 + cy;
+        xx = rx0 + c - cy * RW;
+      }
+      const bool ok = (NSV % NT == 0 || v < NSV) && c < NC && kq * 4 < a.cin && yy >= 0 && yy < a.H && xx >= 0 &&
+                      xx < a.W;
+      const int64_t off = ok ? (static_cast<int64_t>(yy) * a.W + xx) * a.cin + kq * 4 : 0;
+      sok[it] = ok;
+      sv[it] = *reinterpret_cast<const f32x4_t*>(qb + off);
     }
-  };
-  if (a.spread) {
-    // spread form: one lane per part bumps the tile's monotone 64-bit arrival
-    // count and waits until every part of this launch has arrived (count >=
-    // the next multiple of nparts); then each part adds its 1/nparts share.
-    // The host launches this form only when the whole grid is resident at
-    // once; the wait is bounded all the same (~0.2 s), so a broken residency
-    // assumption shows up as wrong sums, never as a hung GPU.
-    if (tid == 0) {
-      unsigned long long* ctr = reinterpret_cast<unsigned long long*>(a.tickets) + tile;
-      const unsigned long long t = __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned long long target = (t / nparts + 1) * nparts;
-      for (int it = 0; it < (1 << 21); ++it) {
-        if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
-        __builtin_amdgcn_s_sleep(2);
+#pragma unroll
+    for (int it = 0; it < NSIT; ++it) {
+      const int v = tid + it * NT;
+      if (NSV % NT != 0 && v >= NSV) break;
+      const int c = v / KQP, kq = v - c * KQP, k8 = kq >> 1;
+      if (!sok[it]) sv[it] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      bf16x2_t h0, m0, l0, h1, m1, l1;
+      split2(f32x2_t{sv[it][0], sv[it][1]}, h0, m0, l0);
+      split2(f32x2_t{sv[it][2], sv[it][3]}, h1, m1, l1);
+      char* p = reinterpret_cast<char*>(xs) + (static_cast<size_t>(k8) * XSP + (c ^ (k8 & 15))) * 16 + (kq & 1) * 8;
+      constexpr size_t PS = static_cast<size_t>(K8) * XSP * 16;  // part stride (bytes)
+      *reinterpret_cast<bf16x4_t*>(p) = __builtin_shufflevector(h0, h1, 0, 1, 2, 3);
+      *reinterpret_cast<bf16x4_t*>(p + PS) = __builtin_shufflevector(m0, m1, 0, 1, 2, 3);
+      *reinterpret_cast<bf16x4_t*>(p + 2 * PS) = __builtin_shufflevector(l0, l1, 0, 1, 2, 3);
+    }
+  }
+  if (!FULL && (ry0 > iy0 || ry1 < iy0 + G::TIY || rx0 > ix0 || rx1 < ix0 + TIX)) {
+    for (int v = tid; v < 4 * NW * PIN; v += NT) {
+      const int pl = v / PIN, p = v - pl * PIN;
+      const int yy = iy0 + p / TIX, xx = ix0 + p % TIX;
+      if (yy < ry0 || yy >= ry1 || xx < rx0 || xx >= rx1) hidw[pl * PINP + p] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  int hcell[NBT];
+#pragma unroll
+  for (int j = 0; j < NBT; ++j) {
+    const int c = j * 16 + li;
+    if constexpr (FULL) {
+      const int yy = iy0 + c / TIX, xx = ix0 + c % TIX;
+      hcell[j] = (c < PIN && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) ? 1 : 0;
+    } else {
+      const int cy = static_cast<int>((static_cast<float>(c) + 0.5f) * rrw);
+      hcell[j] = c < NC ? (ry0 + cy - iy0) * TIX + (rx0 + c - cy * RW - ix0) : PIN;
+    }
+  }
+  int dcell[NP32];
+#pragma unroll
+  for (int pt = 0; pt < NP32; ++pt) {
+    const int q = pt * 32 + l32;
+    const int qq = q < TY * TX ? q : 0;
+    dcell[pt] = (qq / TX) * S * TIX + (qq % TX) * S;
+  }
+  const int nbt = (NC + 15) / 16;
+
+  f32x16_t acc[NP32][NOA];
+#pragma unroll
+  for (int pt = 0; pt < NP32; ++pt)
+#pragma unroll
+    for (int o = 0; o < NOA; ++o) acc[pt][o] = f32x16_t{};
+
+  __syncthreads();  // xs + zeroed halos
+
+  const int nsub = a.hid >> 4;
+  const int sub0 = part * nsub / nparts, sub1 = (part + 1) * nsub / nparts;
+  f32x4_t* myhid = hidw + wave * 4 * PINP;
+  const int64_t wes = static_cast<int64_t>(a.hid) * KP;            // we3 part stride
+  const int64_t wps = static_cast<int64_t>(NOA * 32) * a.hid;      // wp3 part stride
+  for (int hs = sub0 + wave; hs < sub1; hs += NW) {
+    const int ch8 = hs * 16 + 8 * h;  // this lane's 8 depthwise / project channels
+    X3Frag ea[NK32];
+#pragma unroll
+    for (int c = 0; c < NK32; ++c)
+      ea[c] = load_x3(a.we3, wes, static_cast<int64_t>(hs * 16 + li) * KP + 32 * c + 8 * g);
+    X3Frag pa[NOA];
+#pragma unroll
+    for (int o = 0; o < NO32; ++o) pa[o] = load_x3(a.wp3, wps, static_cast<int64_t>(o * 32 + l32) * a.hid + ch8);
+    f32x4_t wdA[9], wdB[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      wdA[t] = *reinterpret_cast<const f32x4_t*>(a.wd + t * a.hid + ch8);
+      wdB[t] = *reinterpret_cast<const f32x4_t*>(a.wd + t * a.hid + ch8 + 4);
+    }
+    const f32x4_t bdA = *reinterpret_cast<const f32x4_t*>(a.bd + ch8);
+    const f32x4_t bdB = *reinterpret_cast<const f32x4_t*>(a.bd + ch8 + 4);
+    const f32x4_t be4 = *reinterpret_cast<const f32x4_t*>(a.be + hs * 16 + 4 * g);
+
+    // ---- expand -> private hidden image (lane: pixel li, channels 4g .. 4g + 3)
+#pragma unroll
+    for (int j = 0; j < NBT; j += 2) {
+      if (FULL || j < nbt) {
+        const int j1 = j + 1 < NBT ? j + 1 : j;
+        f32x4_t e0 = f32x4_t{0.f, 0.f, 0.f, 0.f}, e1 = e0;
+#pragma unroll
+        for (int c = 0; c < NK32; ++c) {
+          const int k8 = 4 * c + g;
+          const bf16x8_t* pl = xs + k8 * XSP;
+          X3Frag b0, b1;
+          const int c0 = (j * 16 + li) ^ (k8 & 15), c1 = (j1 * 16 + li) ^ (k8 & 15);
+          b0.h = pl[c0];
+          b0.m = pl[K8 * XSP + c0];
+          b0.l = pl[2 * K8 * XSP + c0];
+          b1.h = pl[c1];
+          b1.m = pl[K8 * XSP + c1];
+          b1.l = pl[2 * K8 * XSP + c1];
+          e0 += mfma_x3(ea[c], b0);
+          e1 += mfma_x3(ea[c], b1);
+        }
+        if constexpr (FULL) {
+          const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
+          myhid[g * PINP + j * 16 + li] = hcell[j] ? relu6x4(e0 + be4) : z;
+          if (j + 1 < NBT) myhid[g * PINP + j1 * 16 + li] = hcell[j1] ? relu6x4(e1 + be4) : z;
+        } else {
+          myhid[g * PINP + hcell[j]] = relu6x4(e0 + be4);
+          if (j + 1 < NBT) myhid[g * PINP + hcell[j1]] = relu6x4(e1 + be4);
+        }
       }
     }
+    wave_sync();
+
+    // ---- depthwise 3x3 + bias + ReLU6 (lane: pixel l32 of tile pt, 8 channels),
+    // split -> project
+#pragma unroll
+    for (int pt = 0; pt < NP32; ++pt) {
+      const f32x4_t* hA = myhid + (2 * h) * PINP + dcell[pt];
+      const f32x4_t* hB = hA + PINP;
+      f32x4_t dA = bdA, dB = bdB;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const int off = (ky * TIX + kx) * DIL;
+          dA = __builtin_elementwise_fma(hA[off], wdA[ky * 3 + kx], dA);
+          dB = __builtin_elementwise_fma(hB[off], wdB[ky * 3 + kx], dB);
+        }
+      dA = relu6x4(dA);
+      dB = relu6x4(dB);
+      if constexpr (NOT == 0) {
+        const int q = pt * 32 + l32;
+        const int gy = oy0 + q / TX, gx = ox0 + q % TX;
+        if (q < TY * TX && gy < a.Ho && gx < a.Wo) {
+          float* yp = a.y + ((static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx) * a.hid + ch8;
+          *reinterpret_cast<f32x4_t*>(yp) = dA;
+          *reinterpret_cast<f32x4_t*>(yp + 4) = dB;
+        }
+        continue;
+      }
+      const X3Frag bf = split_x3(dA, dB);
+#pragma unroll
+      for (int o = 0; o < NO32; ++o) acc[pt][o] += mfma32_x3(pa[o], bf);
+    }
+    wave_sync();  // this wave's hidden image is read out before the next subtile's expand
+  }
+  if constexpr (NOT == 0) return;
+
+  // ---- cross-wave reduction (fixed order) + bias + residual -> NHWC
+  // acc[pt][o] lane l: pixel pt * 32 + l32, output channels o * 32 + 8 qd + 4 h + r
+  // (register 4 qd + r) -> red [wave][cout quad 2 qd + h][pixel]
+  f32x4_t* red = reinterpret_cast<f32x4_t*>(smem);
+  for (int o = 0; o < NO32; ++o) {
+    __syncthreads();  // (o = 0: xs / hidden done; else the previous round's reads)
+#pragma unroll
+    for (int pt = 0; pt < NP32; ++pt)
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd)
+        red[(wave * 8 + 2 * qd + h) * NPX + pt * 32 + l32] =
+            f32x4_t{acc[pt][o][4 * qd], acc[pt][o][4 * qd + 1], acc[pt][o][4 * qd + 2], acc[pt][o][4 * qd + 3]};
     __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the wait)
-    const int total = TY * TX * nq, chunk = (total + nparts - 1) / nparts;
-    combine(part * chunk, min(total, (part + 1) * chunk));
-    return;
+    for (int v = tid; v < 8 * NPX; v += NT) {
+      const int cq = v / NPX, q = v - cq * NPX;
+      f32x4_t s = red[cq * NPX + q];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) s += red[(w * 8 + cq) * NPX + q];
+      const int co = o * 32 + 4 * cq;
+      if (q >= TY * TX || co >= a.cout) continue;
+      const int gy = oy0 + q / TX, gx = ox0 + q % TX;
+      if (gy >= a.Ho || gx >= a.Wo) continue;
+      const int64_t pix = (static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx;
+      if (a.ws) {
+        const int64_t plane = static_cast<int64_t>(a.B) * a.Ho * a.Wo * a.cout;
+        if (a.tickets) {
+          const __amdgpu_buffer_rsrc_t slab = __builtin_amdgcn_make_buffer_rsrc(
+              a.ws, 0, static_cast<int>(nparts * plane * sizeof(float)), 0x00020000);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, s), slab,
+                                                 static_cast<int>((part * plane + pix * a.cout + co) * 4), 0, 16);
+        } else {
+          *reinterpret_cast<f32x4_t*>(a.ws + part * plane + pix * a.cout + co) = s;
+        }
+        continue;
+      }
+      if (part == 0) {
+        s += *reinterpret_cast<const f32x4_t*>(a.bp + co);
+        if (a.residual) s += *reinterpret_cast<const f32x4_t*>(a.x + pix * a.cin + co);
+      }
+      float* yp = a.y + pix * a.cout + co;
+      if (nparts > 1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) atomicAdd(yp + r, s[r]);
+      } else {
+        *reinterpret_cast<f32x4_t*>(yp) = s;
+      }
+    }
   }
-  int* flag = reinterpret_cast<int*>(smem);
-  if (tid == 0) {
-    const int t = __hip_atomic_fetch_add(a.tickets + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = t == nparts - 1;
-    if (last) __hip_atomic_store(a.tickets + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = last;
-  }
-  __syncthreads();
-  if (!*flag) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the ticket)
-  combine(0, TY * TX * nq);
+  if (!a.ws || !a.tickets) return;
+  irw_inlaunch_combine<TY, TX, NT>(a, smem, tile, part, nparts, b, oy0, ox0, tid);
 }
 
 // --------------------------------------------------------- stem_ir1_f32 ----
@@ -2053,6 +2369,43 @@ const IrwCfg kIrwCfgs[] = {
 #undef NNSX_IRWB
 #undef NNSX_IRWD
 
+// the x3 twins (irw_x3_kernel) of the configurations above: same tiles, waves
+// and hidden parts, so workspace and tickets size the same way
+#define NNSX_IRWX(S, TY, TX, KIN, NOT, NW, F)                                                   \
+  IrwCfg {                                                                                      \
+    S, TY, TX, KIN, NOT, NW, F, &irw_x3_kernel<S, TY, TX, KIN, NOT, NW, F>,                     \
+        &IrwX3Geom<S, TY, TX, KIN, NOT, NW, F>::lds_bytes, 1                                    \
+  }
+const IrwCfg kIrwX3Cfgs[] = {
+    NNSX_IRWX(2, 4, 8, 16, 2, 3, true),   NNSX_IRWX(1, 8, 8, 24, 2, 3, true),   NNSX_IRWX(2, 4, 4, 24, 2, 3, true),
+    NNSX_IRWX(2, 7, 4, 24, 2, 3, true),   NNSX_IRWX(1, 7, 7, 32, 2, 4, false),  NNSX_IRWX(2, 2, 7, 32, 4, 4, false),
+    NNSX_IRWX(1, 7, 14, 64, 4, 4, false), NNSX_IRWX(1, 7, 7, 64, 4, 4, false),  NNSX_IRWX(1, 7, 7, 64, 6, 4, false),
+    NNSX_IRWX(1, 7, 7, 96, 6, 4, false),  NNSX_IRWX(1, 7, 7, 160, 10, 4, false), NNSX_IRWX(2, 7, 7, 96, 10, 4, false),
+    NNSX_IRWX(1, 7, 7, 160, 0, 4, false), NNSX_IRWX(1, 5, 5, 160, 10, 4, false), NNSX_IRWX(2, 5, 5, 96, 10, 4, false),
+    NNSX_IRWX(1, 5, 5, 160, 0, 4, false), NNSX_IRWX(1, 7, 14, 64, 6, 4, false), NNSX_IRWX(1, 7, 14, 96, 6, 4, false),
+};
+#undef NNSX_IRWX
+
+// NNSX_X3_IRW=1: the fused blocks on irw_x3 under x3 (off until measured on the GPU)
+bool x3_irw_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("NNSX_X3_IRW");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+// the x3 twin of a configuration, when the method is x3 and both weight
+// parts are given (the expand-only form needs no project weights)
+const IrwCfg* x3_twin(const IrwCfg* c, const IrBlockF32Args& a) {
+  if (!c || f32_math() != F32Math::kX3 || !x3_irw_enabled() || !a.we3 || (c->NOT > 0 && !a.wp3)) return nullptr;
+  for (const IrwCfg& x : kIrwX3Cfgs)
+    if (x.S == c->S && x.TY == c->TY && x.TX == c->TX && x.KIN == c->KIN && x.NOT == c->NOT && x.NW == c->NW &&
+        x.full == c->full && x.dil == c->dil && x.lds(a.hid) <= 160 * 1024)
+      return &x;
+  return nullptr;
+}
+
 // indices of kIrwCfgs that find_irw skips (A/B experiments): NNSX_IRW_SKIP=1,4
 bool irw_skipped(size_t i) {
   static const std::vector<size_t> skip = [] {
@@ -2127,6 +2480,20 @@ const IrF32Cfg* find_cfg(int S, int H, int W, int cin, int hid, int cout, bool h
 
 }  // namespace
 
+// ---- fp32 product method ----------------------------------------------------
+// kX3: the fp32 GEMM-shaped products on split-bf16 MFMAs (split_x3: error vs
+// fp64 below the native fp32 MFMA's); kNative: v_mfma_f32_16x16x4_f32.  The
+// process default comes from NNSX_F32_MATH (x3 | fp32); graph capture bakes the
+// method in at capture time.
+static F32Math g_f32_math = [] {
+  const char* e = std::getenv("NNSX_F32_MATH");
+  if (e && (std::string(e) == "fp32" || std::string(e) == "native")) return F32Math::kNative;
+  return F32Math::kX3;
+}();
+F32Math f32_math() { return g_f32_math; }
+void set_f32_math(F32Math m) { g_f32_math = m; }
+const char* f32_math_name(F32Math m) { return m == F32Math::kX3 ? "x3" : "fp32"; }
+
 // K-split slices for a small output grid (the classifier: M = batch, 32
 // tiles of 64 x 64) -- otherwise most CUs idle while each workgroup walks all
 // of K.  Returns the k-stages per slice (kstages: no split).
@@ -2156,13 +2523,22 @@ static void pw_gemm_f32_launch(const float* x, const float* wt, const float* bia
   const int kstages = (Kpad + GKT - 1) / GKT;
   int chunk = (ws && !yl.rpb && !yl.brpb && !yl.pool) ? gemm_kchunk(static_cast<int>(grid.x * grid.y), kstages, N, !res) : kstages;
   grid.z = static_cast<unsigned>((kstages + chunk - 1) / chunk);
+  const bool x3 = f32_math() == F32Math::kX3;
   if (grid.z == 1) {
-    hipLaunchKernelGGL((pw_gemm_f32_kernel<BM, BN>), grid, dim3(256), 0, s, x, wt, bias, res, y, M, N, K, Kpad, Npad,
-                       act, kstages, yl);
+    if (x3)
+      hipLaunchKernelGGL((pw_gemm_f32_kernel<BM, BN, true>), grid, dim3(256), 0, s, x, wt, bias, res, y, M, N, K, Kpad,
+                         Npad, act, kstages, yl);
+    else
+      hipLaunchKernelGGL((pw_gemm_f32_kernel<BM, BN>), grid, dim3(256), 0, s, x, wt, bias, res, y, M, N, K, Kpad, Npad,
+                         act, kstages, yl);
     return;
   }
-  hipLaunchKernelGGL((pw_gemm_f32_kernel<BM, BN>), grid, dim3(256), 0, s, x, wt, bias, res, ws, M, N, K, Kpad, Npad,
-                     act, chunk, YLayout{});
+  if (x3)
+    hipLaunchKernelGGL((pw_gemm_f32_kernel<BM, BN, true>), grid, dim3(256), 0, s, x, wt, bias, res, ws, M, N, K, Kpad,
+                       Npad, act, chunk, YLayout{});
+  else
+    hipLaunchKernelGGL((pw_gemm_f32_kernel<BM, BN>), grid, dim3(256), 0, s, x, wt, bias, res, ws, M, N, K, Kpad, Npad,
+                       act, chunk, YLayout{});
   const int64_t nq = static_cast<int64_t>(M) * N / 4;
   const unsigned rg = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((nq + 255) / 256, 2048)));
   hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(rg), dim3(256), 0, s, ws, static_cast<int>(grid.z), M, N, bias,
@@ -2280,7 +2656,10 @@ void pw_gemm_f32_group(const GemmProb* p, int n, hipStream_t s) {
   }
   if (blocks <= 0 || blocks > (1 << 30)) throw std::invalid_argument("pw_gemm_f32_group: grid");
   g.start[n] = static_cast<int>(blocks);
-  hipLaunchKernelGGL((pw_gemm_group_f32_kernel<64, 64>), dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, g);
+  if (f32_math() == F32Math::kX3)
+    hipLaunchKernelGGL((pw_gemm_group_f32_kernel<64, 64, true>), dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, g);
+  else
+    hipLaunchKernelGGL((pw_gemm_group_f32_kernel<64, 64>), dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, g);
 }
 
 void dw3x3_f32_group(const DwProb* p, int n, hipStream_t s) {
@@ -2479,6 +2858,11 @@ static thread_local bool t_device_shared = false;
 SharedDeviceScope::SharedDeviceScope(bool on) : prev_(t_device_shared) { t_device_shared = prev_ || on; }
 SharedDeviceScope::~SharedDeviceScope() { t_device_shared = prev_; }
 bool device_shared() { return t_device_shared; }
+bool set_device_shared(bool on) {
+  const bool prev = t_device_shared;
+  t_device_shared = on;
+  return prev;
+}
 
 // the model's ticket buffer (ir_block_f32_tickets ints, zeroed once): the
 // spread form's 64-bit counters in [0, kSpreadTickets), the last-arriver
@@ -2587,6 +2971,7 @@ bool ir_expand_dw_f32(const IrBlockF32Args& args, hipStream_t s) {
   IrBlockF32Args a = args;
   const IrwCfg* c = find_irw_dw(a.stride, a.H, a.W, a.cin, a.hid, a.dil);
   if (!c || !a.has_expand) return false;
+  if (const IrwCfg* x = x3_twin(c, a)) c = x;
   irw_geometry(c, &a);
   a.ws = nullptr;
   const size_t lds = c->lds(a.hid);
@@ -2599,12 +2984,19 @@ bool ir_expand_dw_f32(const IrBlockF32Args& args, hipStream_t s) {
 }
 
 size_t ir_block_f32_workspace_bytes(const IrBlockF32Args& args) {
-  IrBlockF32Args a = args;
-  const IrwCfg* c = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0, a.dil, a.B);
+  const IrwCfg* c = find_irw(args.stride, args.H, args.W, args.cin, args.hid, args.cout, args.has_expand != 0, args.dil,
+                             args.B);
   if (!c) return 0;
-  irw_geometry(c, &a);
-  if (a.hsplit < 2 || (a.hsplit == 2 && irw_atomic2())) return 0;
-  return static_cast<size_t>(a.hsplit) * a.B * a.Ho * a.Wo * a.cout * sizeof(float);
+  size_t best = 0;
+  // (the x3 twin's parts can differ where they depend on residency: size for both)
+  for (const IrwCfg* k : {c, x3_twin(c, args)}) {
+    if (!k) continue;
+    IrBlockF32Args a = args;
+    irw_geometry(k, &a);
+    if (a.hsplit < 2 || (a.hsplit == 2 && irw_atomic2())) continue;
+    best = std::max(best, static_cast<size_t>(a.hsplit) * a.B * a.Ho * a.Wo * a.cout * sizeof(float));
+  }
+  return best;
 }
 
 // the in-launch combine of the hidden parts: the spread form by default when
@@ -2728,10 +3120,22 @@ bool stem_ir1_f32(const StemIr1F32Args& args, hipStream_t s) {
   return true;
 }
 
+const char* ir_block_f32_method(int stride, int H, int W, int cin, int hid, int cout, int B, int dil) {
+  const IrwCfg* c = find_irw(stride, H, W, cin, hid, cout, true, dil, B);
+  if (!c) return ir_block_f32_supported(stride, H, W, cin, hid, cout, true, dil) ? "fp32" : "";
+  IrBlockF32Args a;
+  a.hid = hid;
+  static const uint16_t dummy[8] = {};
+  a.we3 = a.wp3 = dummy;
+  return x3_twin(c, a) ? "x3" : "fp32";
+}
+
 bool ir_block_f32(const IrBlockF32Args& args, hipStream_t s) {
   IrBlockF32Args a = args;
-  if (const IrwCfg* w = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0, a.dil, a.B))
+  if (const IrwCfg* w = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0, a.dil, a.B)) {
+    if (const IrwCfg* x = x3_twin(w, a)) return launch_irw(x, a, s);
     return launch_irw(w, a, s);
+  }
   if (a.dil != 1) return false;
   const IrF32Cfg* c = find_cfg(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0);
   if (!c) return false;

@@ -554,10 +554,20 @@ at::Tensor pw_conv_pool_cpu(const at::Tensor& x, const at::Tensor& wt, const at:
 
 // ----------------------------------------------------------- ir_block ----
 // Fused inverted residual.  we [hid, cin32], wd [9, hid], wp [ceil16(cout), hid] bf16; biases f32.
+// split-bf16 weight parts [3][rows][cols] bf16 of at least these sizes (else unused)
+static const uint16_t* x3_ptr(const c10::optional<at::Tensor>& t, const at::Tensor& x, int64_t rows, int64_t cols) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->is_contiguous() && t->dim() == 3 &&
+                  t->size(0) == 3 && t->size(1) == rows && t->size(2) == cols && t->get_device() == x.get_device(),
+              "x3 weights: [3, ", rows, ", ", cols, "] bf16 on the input's device");
+  return static_cast<const uint16_t*>(t->data_ptr());
+}
+
 at::Tensor ir_block_f32_cuda(const at::Tensor& x, const at::Tensor& we, const at::Tensor& be, const at::Tensor& wd,
                              const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, int64_t stride,
                              int64_t cout, bool has_expand, bool residual, int64_t dilation,
-                             const c10::optional<at::Tensor>& tickets) {
+                             const c10::optional<at::Tensor>& tickets, const c10::optional<at::Tensor>& we3,
+                             const c10::optional<at::Tensor>& wp3) {
   TORCH_CHECK(x.is_contiguous() && x.dim() == 4, "ir_block(f32): x [B,H,W,C] f32");
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   const int64_t hid = wd.size(1);
@@ -590,6 +600,10 @@ at::Tensor ir_block_f32_cuda(const at::Tensor& x, const at::Tensor& we, const at
   a.has_expand = has_expand ? 1 : 0;
   a.residual = residual ? 1 : 0;
   a.dil = static_cast<int>(dilation);
+  if (has_expand) {
+    a.we3 = x3_ptr(we3, x, hid, (C + 31) / 32 * 32);
+    a.wp3 = x3_ptr(wp3, x, (cout + 31) / 32 * 32, hid);
+  }
   at::Tensor ws;
   if (const size_t wsb = nnsx::kernels::ir_block_f32_workspace_bytes(a)) {
     ws = at::empty({static_cast<int64_t>(wsb / sizeof(float))}, x.options());  // caching allocator: graph-capture safe
@@ -612,7 +626,8 @@ at::Tensor ir_block_f32_cuda(const at::Tensor& x, const at::Tensor& we, const at
 // expand + depthwise (fp32), the depthwise output [B, Ho, Wo, hid]: blocks
 // whose project runs as a plain GEMM afterwards
 at::Tensor ir_expand_dw_cuda(const at::Tensor& x, const at::Tensor& we, const at::Tensor& be, const at::Tensor& wd,
-                             const at::Tensor& bd, int64_t stride, int64_t dilation) {
+                             const at::Tensor& bd, int64_t stride, int64_t dilation,
+                             const c10::optional<at::Tensor>& we3) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 4,
               "ir_expand_dw: x [B,H,W,C] f32");
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
@@ -640,13 +655,16 @@ at::Tensor ir_expand_dw_cuda(const at::Tensor& x, const at::Tensor& we, const at
   a.stride = static_cast<int>(stride);
   a.has_expand = 1;
   a.dil = static_cast<int>(dilation);
+  a.we3 = x3_ptr(we3, x, hid, (C + 31) / 32 * 32);
   TORCH_CHECK(nnsx::kernels::ir_expand_dw_f32(a, cur_stream()), "ir_expand_dw: unsupported shape (stride ", stride,
               ", ", H, "x", W, ", cin ", C, ", hid ", hid, ")");
   return y;
 }
 
 at::Tensor ir_expand_dw_cpu(const at::Tensor& x, const at::Tensor& we, const at::Tensor& be, const at::Tensor& wd,
-                            const at::Tensor& bd, int64_t stride, int64_t dilation) {
+                            const at::Tensor& bd, int64_t stride, int64_t dilation,
+                            const c10::optional<at::Tensor>& we3) {
+  (void)we3;
   const int64_t hid = wd.size(1);
   at::Tensor h = pw_conv_cpu(x, we, be, c10::nullopt, hid, 1, false);
   return dw_conv_cpu(h, wd, bd, stride, 1, dilation);
@@ -662,10 +680,12 @@ bool ir_expand_dw_supported_f32(int64_t stride, int64_t H, int64_t W, int64_t ci
 at::Tensor ir_block_cuda(const at::Tensor& x, const at::Tensor& we, const at::Tensor& be, const at::Tensor& wd,
                          const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, int64_t stride,
                          int64_t cout, bool has_expand, bool residual, int64_t dilation,
-                         const c10::optional<at::Tensor>& tickets) {
+                         const c10::optional<at::Tensor>& tickets, const c10::optional<at::Tensor>& we3,
+                         const c10::optional<at::Tensor>& wp3) {
   TORCH_CHECK(x.is_cuda(), "ir_block: x must be a cuda tensor");
   if (x.scalar_type() == at::kFloat)
-    return ir_block_f32_cuda(x, we, be, wd, bd, wp, bp, stride, cout, has_expand, residual, dilation, tickets);
+    return ir_block_f32_cuda(x, we, be, wd, bd, wp, bp, stride, cout, has_expand, residual, dilation, tickets, we3,
+                             wp3);
   TORCH_CHECK(dilation == 1, "ir_block(bf16): dilation 1 only");
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() == 4,
               "ir_block: x [B,H,W,C] bf16");
@@ -702,8 +722,11 @@ at::Tensor ir_block_cuda(const at::Tensor& x, const at::Tensor& we, const at::Te
 at::Tensor ir_block_cpu(const at::Tensor& x, const at::Tensor& we, const at::Tensor& be, const at::Tensor& wd,
                         const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, int64_t stride,
                         int64_t cout, bool has_expand, bool residual, int64_t dilation,
-                        const c10::optional<at::Tensor>& tickets) {
+                        const c10::optional<at::Tensor>& tickets, const c10::optional<at::Tensor>& we3,
+                        const c10::optional<at::Tensor>& wp3) {
   (void)tickets;
+  (void)we3;
+  (void)wp3;
   at::Tensor h = x;
   const int64_t hid = wd.size(1);
   if (has_expand) h = pw_conv_cpu(x, we, be, c10::nullopt, hid, 1, false);
@@ -767,9 +790,38 @@ bool ir_supported(int64_t stride, int64_t cin, int64_t hid, int64_t cout) {
                                            static_cast<int>(cout));
 }
 
+std::string ir_method_f32(int64_t stride, int64_t H, int64_t W, int64_t cin, int64_t hid, int64_t cout, int64_t B,
+                          int64_t dilation) {
+  return nnsx::kernels::ir_block_f32_method(static_cast<int>(stride), static_cast<int>(H), static_cast<int>(W),
+                                            static_cast<int>(cin), static_cast<int>(hid), static_cast<int>(cout),
+                                            static_cast<int>(B), static_cast<int>(dilation));
+}
+
+bool set_device_shared(bool on) { return nnsx::kernels::set_device_shared(on); }
+
+std::string f32_math() { return nnsx::kernels::f32_math_name(nnsx::kernels::f32_math()); }
+
+// returns the previous method
+std::string set_f32_math(const std::string& m) {
+  const std::string prev = f32_math();
+  if (m == "x3") {
+    nnsx::kernels::set_f32_math(nnsx::kernels::F32Math::kX3);
+  } else if (m == "fp32" || m == "native") {
+    nnsx::kernels::set_f32_math(nnsx::kernels::F32Math::kNative);
+  } else {
+    TORCH_CHECK(false, "set_f32_math: x3 | fp32, got ", m);
+  }
+  return prev;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(nnsx, m) {
+  m.def("f32_math() -> str", f32_math);
+  m.def("set_device_shared(bool on) -> bool", set_device_shared);
+  m.def("ir_method_f32(int stride, int H, int W, int cin, int hid, int cout, int B, int dilation=1) -> str",
+        ir_method_f32);
+  m.def("set_f32_math(str method) -> str", set_f32_math);
   m.def("pw_conv(Tensor x, Tensor wt, Tensor bias, Tensor? res, int N, int act, bool out_f32) -> Tensor");
   m.def("pw_conv_into(Tensor x, Tensor wt, Tensor bias, Tensor(a!) out, int row0, int n, int act) -> ()");
   m.def("pw_conv_rowbias(Tensor x, Tensor wt, Tensor bias, int N, int act) -> Tensor");
@@ -788,13 +840,15 @@ TORCH_LIBRARY(nnsx, m) {
         "int mode=-1) -> Tensor");
   m.def("pw_conv_f32_tile(Tensor x, Tensor wt, Tensor bias, Tensor? res, int N, int act, int tile) -> Tensor");
   m.def("ir_block(Tensor x, Tensor we, Tensor be, Tensor wd, Tensor bd, Tensor wp, Tensor bp, int stride, int cout, "
-        "bool has_expand, bool residual, int dilation=1, Tensor(a!)? tickets=None) -> Tensor");
+        "bool has_expand, bool residual, int dilation=1, Tensor(a!)? tickets=None, Tensor? we3=None, "
+        "Tensor? wp3=None) -> Tensor");
   m.def("ir_supported(int stride, int cin, int hid, int cout) -> bool", ir_supported);
   m.def("ir_supported_f32(int stride, int H, int W, int cin, int hid, int cout, bool has_expand, int dilation=1) -> bool",
         ir_supported_f32);
   m.def("ir_expand_dw_supported_f32(int stride, int H, int W, int cin, int hid, int B=0, int dilation=1) -> bool",
         ir_expand_dw_supported_f32);
-  m.def("ir_expand_dw(Tensor x, Tensor we, Tensor be, Tensor wd, Tensor bd, int stride, int dilation=1) -> Tensor");
+  m.def("ir_expand_dw(Tensor x, Tensor we, Tensor be, Tensor wd, Tensor bd, int stride, int dilation=1, "
+        "Tensor? we3=None) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(nnsx, CUDA, m) {

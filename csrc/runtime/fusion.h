@@ -82,6 +82,10 @@ class DecodeStage {
   // in = device pointers of the model outputs (the decoder's normal input),
   // out = device buffers sized by out_info(); capturable work on s only
   virtual bool enqueue(const std::vector<const void*>& in, const std::vector<void*>& out, void* stream) = 0;
+  // true once the decoder's mode or options changed after this stage was
+  // prepared: graphs captured with it run the old post-processing.  The filter
+  // checks it before every invoke and re-takes a fresh stage (re-capturing).
+  virtual bool stale() const { return false; }
 };
 
 class DecodeStageConsumer {  // implemented by tensor_decoder

@@ -1,42 +1,163 @@
 #include "runtime/memory.h"
 
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <iterator>
+#include <thread>
 
+#include "core/log.h"
 #include "core/util.h"
 #include "runtime/hip_util.h"
 
 namespace nnsx {
 
+bool Memory::check_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("NNSX_MEM_CHECK");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+namespace {
+
+// fill a host block with the poison pattern (MEM_CHECK)
+void poison_host(void* p, size_t n) {
+  uint32_t* w = static_cast<uint32_t*>(p);
+  for (size_t i = 0; i < n / 4; ++i) w[i] = Memory::kPoison;
+}
+
+// Deferred host releases: the last reference to a host / pinned block that an
+// asynchronous copy still reads (H2D: recorded uses) or writes (D2H: the ready
+// event) drops on some pipeline thread -- a source, the converter -- which must
+// not stall on that copy.  The block goes to this thread instead, which waits
+// for the copies' events and then frees it (pinned: back to the shared pool,
+// where the next frame may pick it up).  FIFO, one thread per process.
+class DeferredRelease {
+ public:
+  struct Item {
+    std::vector<std::pair<int, hipEvent_t>> events;
+    void* data;
+    size_t size;
+    MemPlace place;
+  };
+  static DeferredRelease& get() {
+    static DeferredRelease* d = new DeferredRelease();  // (never destroyed: process-lifetime thread)
+    return *d;
+  }
+  void push(Item it) {
+    std::lock_guard<std::mutex> lk(mu_);
+    q_.push_back(std::move(it));
+    ++queued_;
+    cv_.notify_all();
+  }
+  void drain() {
+    std::unique_lock<std::mutex> lk(mu_);
+    const uint64_t target = queued_;
+    done_cv_.wait(lk, [&] { return done_ >= target; });
+  }
+
+ private:
+  DeferredRelease() {
+    std::thread([this] { run(); }).detach();
+  }
+  void run() {
+    for (;;) {
+      Item it;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return !q_.empty(); });
+        it = std::move(q_.front());
+        q_.pop_front();
+      }
+      for (auto& e : it.events) {
+        (void)hipEventSynchronize(e.second);
+        hip::event_put(e.first, e.second);
+      }
+      if (Memory::check_enabled() && it.size) poison_host(it.data, it.size);
+      if (it.place == MemPlace::PINNED)
+        hip::pinned_free(it.data, it.size);
+      else
+        hip::host_free(it.data);
+      std::lock_guard<std::mutex> lk(mu_);
+      ++done_;
+      done_cv_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  std::deque<Item> q_;
+  uint64_t queued_ = 0, done_ = 0;
+};
+
+}  // namespace
+
+void Memory::drain_deferred() {
+  if (hip::available()) DeferredRelease::get().drain();
+}
+
 Memory::Memory(void* data, size_t size, MemPlace place, int device, Release release)
     : data_(data), size_(size), place_(place), device_(device), release_(std::move(release)) {}
 
 Memory::~Memory() {
-  // host memory (pageable or pinned) read by an asynchronous H2D copy (map_device
-  // records it as a use): it is freed -- and may be handed out again at once by
-  // malloc or the pinned pool -- only after that copy ran
-  if (place_ != MemPlace::DEVICE && !uses_.empty()) sync_uses();
-  if (release_) release_(this);
+  state_.store(1);
+  if (deferrable_) {
+    // alloc_host / alloc_pinned: a pending D2H may still be landing here (pinned:
+    // the producer's ready event) and pending H2Ds may still read it (recorded
+    // uses); the block may be handed out again at once by malloc or the pinned
+    // pool, so it is freed only after them -- by the deferred-release thread,
+    // never by blocking the thread that dropped the last reference
+    std::vector<std::pair<int, hipEvent_t>> evs;
+    for (auto& u : uses_) evs.emplace_back(u.dev, u.event);
+    uses_.clear();
+    if (ready_ && place_ == MemPlace::PINNED) {
+      evs.emplace_back(ready_dev_, ready_);
+      ready_ = nullptr;
+    }
+    if (!evs.empty()) {
+      DeferredRelease::get().push({std::move(evs), data_, size_, place_});
+    } else {
+      if (check_enabled() && size_) poison_host(data_, size_);
+      if (place_ == MemPlace::PINNED)
+        hip::pinned_free(data_, size_);
+      else
+        hip::host_free(data_);
+    }
+  } else {
+    // other host memory (wrapped buffers with their own release) read by an
+    // asynchronous H2D copy: released only after that copy ran
+    if (place_ != MemPlace::DEVICE && !uses_.empty()) sync_uses();
+    if (release_) release_(this);
+  }
   if (ready_) hip::event_put(ready_dev_, ready_);
   for (auto& u : uses_) hip::event_put(u.dev, u.event);
 }
 
+void Memory::check_live(const char* what) const {
+  if (!check_enabled()) return;
+  for (const Memory* m = this; m; m = m->parent_.get())
+    if (m->state_.load() != 0) {
+      NNSX_LOGE("memcheck", what, " of a memory whose release has begun (", data_, ", ", size_, " bytes)");
+      throw Error(std::string("NNSX_MEM_CHECK: ") + what + " of a released memory");
+    }
+}
+
 MemoryPtr Memory::alloc_host(size_t size) {
   void* p = hip::host_alloc(size);
-  return std::make_shared<Memory>(p, size, MemPlace::HOST, -1, [](Memory* m) { hip::host_free(m->data()); });
+  auto m = std::make_shared<Memory>(p, size, MemPlace::HOST, -1, nullptr);
+  m->deferrable_ = hip::available();  // (no GPU: nothing is ever in flight)
+  if (!m->deferrable_) m->release_ = [](Memory* mm) { hip::host_free(mm->data()); };
+  return m;
 }
 
 MemoryPtr Memory::alloc_pinned(size_t size) {
   if (!hip::available()) return alloc_host(size);
   void* p = hip::pinned_alloc(size);
-  return std::make_shared<Memory>(p, size, MemPlace::PINNED, -1, [](Memory* m) {
-    // a pending D2H may still be landing in this block (its producer's ready
-    // event), and a pending H2D may still read it (recorded readers): the block
-    // goes back to the shared pinned pool only after both
-    m->sync_ready();
-    m->sync_uses();
-    hip::pinned_free(m->data(), m->size());
-  });
+  auto m = std::make_shared<Memory>(p, size, MemPlace::PINNED, -1, nullptr);
+  m->deferrable_ = true;
+  return m;
 }
 
 MemoryPtr Memory::alloc_device(size_t size, int dev, hipStream_t stream) {
@@ -47,8 +168,18 @@ MemoryPtr Memory::alloc_device(size_t size, int dev, hipStream_t stream) {
     hipStream_t rs = hip::release_stream(dev);
     m->wait_ready(rs);
     m->wait_uses(rs);
+    if (check_enabled() && m->size() >= 4) {
+      hip::DeviceGuard g(dev);
+      (void)hipMemsetD32Async(m->data(), static_cast<int>(kPoison), m->size() / 4, rs);
+    }
     hip::device_free(dev, m->data(), rs);
   });
+}
+
+MemoryPtr Memory::device_mirror(int dev) {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = dev_mirror_.find(dev);
+  return it == dev_mirror_.end() ? nullptr : it->second;
 }
 
 // ------------------------------------------------------- DeviceBufferPool ----
@@ -123,6 +254,7 @@ MemoryPtr DeviceBufferPool::acquire(hipStream_t stream) {
   int slot = -1;
   void* p = nullptr;
   hipEvent_t wait = nullptr;
+  bool poisoned = false;
   {
     std::lock_guard<std::mutex> lk(mu_);
     hip::DeviceGuard g(dev_);
@@ -154,6 +286,7 @@ MemoryPtr DeviceBufferPool::acquire(hipStream_t stream) {
     }
     if (slot >= 0) {
       Block& b = blocks_[static_cast<size_t>(slot)];
+      poisoned = pool_poisoned_.erase(slot) > 0;
       b.free = false;
       wait = b.released;  // complete (case 1) or waited for below (case 3); then recycled
       b.released = nullptr;
@@ -166,6 +299,19 @@ MemoryPtr DeviceBufferPool::acquire(hipStream_t stream) {
     hip::check(hipEventSynchronize(wait), "pool acquire wait");
     hip::event_put(dev_, wait);
   }
+  if (poisoned) {
+    // the block was poisoned when its previous use was released: it must still
+    // hold the pattern, else something wrote to it after the release
+    hip::DeviceGuard g(dev_);
+    uint32_t head = 0, tail = 0;
+    hip::check(hipMemcpy(&head, p, 4, hipMemcpyDeviceToHost), "memcheck head");
+    hip::check(hipMemcpy(&tail, static_cast<char*>(p) + (size_ / 4 - 1) * 4, 4, hipMemcpyDeviceToHost),
+               "memcheck tail");
+    if (head != Memory::kPoison || tail != Memory::kPoison) {
+      NNSX_LOGE("memcheck", "pool block ", p, " (", size_, " bytes) was written after its release");
+      throw Error("NNSX_MEM_CHECK: pooled device block written after its release");
+    }
+  }
   std::weak_ptr<DeviceBufferPool> wp = shared_from_this();
   const int dev = dev_;
   const size_t size = size_;
@@ -174,7 +320,10 @@ MemoryPtr DeviceBufferPool::acquire(hipStream_t stream) {
     hipStream_t rs = hip::release_stream(dev);
     mm->wait_ready(rs);
     mm->wait_uses(rs);
+    const bool poison = Memory::check_enabled() && mm->size() >= 4;
+    if (poison) (void)hipMemsetD32Async(mm->data(), static_cast<int>(Memory::kPoison), mm->size() / 4, rs);
     if (auto pool = wp.lock()) {
+      if (poison) pool->mark_poisoned(slot);
       hipEvent_t e = hip::event_get(dev);
       hip::check(hipEventRecord(e, rs), "pool release");
       pool->put_back(slot, e);
@@ -186,6 +335,11 @@ MemoryPtr DeviceBufferPool::acquire(hipStream_t stream) {
   m->tags()[kPoolTag] = static_cast<int64_t>(id_);
   m->tags()[kSlotTag] = slot;
   return m;
+}
+
+void DeviceBufferPool::mark_poisoned(int slot) {
+  std::lock_guard<std::mutex> lk(mu_);
+  pool_poisoned_.insert(slot);
 }
 
 void DeviceBufferPool::put_back(int slot, hipEvent_t released) {
@@ -301,6 +455,7 @@ void Memory::sync_uses() const {
 }
 
 const void* Memory::map_host() {
+  check_live("map_host");
   if (place_ != MemPlace::DEVICE) {
     if (place_ == MemPlace::PINNED) sync_ready();  // a D2H may be landing here
     return data_;
@@ -319,6 +474,7 @@ const void* Memory::map_host() {
 }
 
 const void* Memory::map_device(int dev, hipStream_t stream) {
+  check_live("map_device");
   if (place_ == MemPlace::DEVICE && device_ == dev) {
     wait_ready(stream);
     return data_;

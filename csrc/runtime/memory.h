@@ -20,6 +20,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -92,8 +93,28 @@ class Memory : public std::enable_shared_from_this<Memory> {
   Memory* root() { return parent_ ? parent_->root() : this; }
   const Memory* root() const { return parent_ ? parent_->root() : this; }
 
+  // the device mirror of this memory on `dev` (map_device), if any
+  MemoryPtr device_mirror(int dev);
+
+  // NNSX_MEM_CHECK=1 (debug builds of a run, read once): released blocks are
+  // filled with kPoison (device: on the release stream, after every reader;
+  // host / pinned: after the deferred free's waits), a pooled block handed out
+  // again must still hold the poison (else something wrote to it after its
+  // release: the acquire throws), and map_host / map_device of a memory whose
+  // destruction has begun throws.  Stale reads of a recycled block then read
+  // NaNs (0x7FBADBAD as fp32) instead of plausible old data.
+  static bool check_enabled();
+  static constexpr uint32_t kPoison = 0x7FBADBADu;
+  // Wait until every deferred host / pinned release queued so far has run (tests).
+  static void drain_deferred();
+
  private:
   void record_use_self(hipStream_t stream, int dev);  // record_use without the device mirror
+  void check_live(const char* what) const;
+  // alloc_host / alloc_pinned blocks: the last release hands pending copies'
+  // events to the deferred-release thread instead of waiting on them
+  bool deferrable_ = false;
+  std::atomic<uint32_t> state_{0};  // 0 live, 1 destroying
   void* data_;
   size_t size_;
   MemPlace place_;
@@ -155,6 +176,7 @@ class DeviceBufferPool : public std::enable_shared_from_this<DeviceBufferPool> {
  private:
   DeviceBufferPool(int dev, size_t size, size_t max_blocks);
   void put_back(int slot, hipEvent_t released);
+  void mark_poisoned(int slot);  // MEM_CHECK: the block's release filled it with kPoison
   struct Block {
     void* ptr = nullptr;
     hipEvent_t released = nullptr;  // recorded after the last reader of the previous use
@@ -167,6 +189,7 @@ class DeviceBufferPool : public std::enable_shared_from_this<DeviceBufferPool> {
   mutable std::mutex mu_;
   std::vector<Block> blocks_;
   uint64_t seq_ = 0;
+  std::set<int> pool_poisoned_;  // MEM_CHECK: slots poisoned at release
 };
 
 // Meta a buffer carries across elements.

@@ -1,0 +1,158 @@
+// Deterministic regression tests of the runtime's device-memory lifetime rules
+// (exposed to Python as nnstreamer_amd._C.memory_selftest, run by
+// tests/test_gpu_memcheck.py).  Each case holds a stream busy with a bounded
+// spin kernel (kernels::spin_us) so that an asynchronous copy or read is still
+// queued when the Memory that owns its source is released, then re-allocates
+// the same storage with other bytes and checks what the delayed copy saw.  A
+// lifetime rule that frees too early fails every time, not by chance.
+//
+// Cases (the fixes they pin):
+//   pageable_h2d       a pageable host frame released while its H2D copy is
+//                      queued (7ba8684: freed at once, malloc handed the
+//                      address to the next frame, the copy read that frame)
+//   pinned_h2d         the same for a pinned block (the pinned pool recycles it)
+//   mirror_other_stream a host memory's device mirror read on a second stream
+//                      (a filter replay lane) that recorded its use on the
+//                      host memory (ee80b24: the mirror went back to the pool
+//                      ordered only on the mapping stream)
+//   device_reader      a device block read on another stream while released
+//                      (the release waits for every recorded reader)
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "kernels/kernels.h"
+#include "runtime/hip_util.h"
+#include "runtime/memory.h"
+
+namespace nnsx {
+
+namespace {
+
+constexpr size_t kBytes = 8u << 20;  // 8 MB: a few frames; one copy takes ~0.2 ms
+constexpr int kSpinUs = 20000;       // 20 ms: every release below happens inside this window
+
+std::string check_bytes(const std::vector<uint8_t>& got, uint8_t want, const char* what) {
+  size_t bad = 0;
+  for (uint8_t v : got) bad += v != want;
+  if (!bad) return "";
+  return std::string(what) + ": " + std::to_string(bad) + " of " + std::to_string(got.size()) +
+         " bytes differ from the pattern the released source held (first byte " + std::to_string(got[0]) + ")";
+}
+
+std::vector<uint8_t> d2h(const void* p, size_t n, hipStream_t s) {
+  std::vector<uint8_t> h(n);
+  hip::check(hipMemcpyAsync(h.data(), p, n, hipMemcpyDeviceToHost, s), "selftest D2H");
+  hip::check(hipStreamSynchronize(s), "selftest sync");
+  return h;
+}
+
+// host frame (pageable or pinned) -> H2D on s behind a spin; the frame is
+// released at once, its storage reused for another frame; the mirror must hold
+// the first frame's bytes
+std::string host_h2d(int dev, bool pinned) {
+  hip::DeviceGuard g(dev);
+  hipStream_t s = nullptr;
+  hip::check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "selftest stream");
+  MemoryPtr h = pinned ? Memory::alloc_pinned(kBytes) : Memory::alloc_host(kBytes);
+  std::memset(h->data(), 0x11, kBytes);
+  kernels::spin_us(s, kSpinUs);
+  (void)h->map_device(dev, s);  // queued behind the spin
+  MemoryPtr mirror = h->device_mirror(dev);
+  h.reset();  // the last reference: the copy has not run yet
+  // the next frames take the freed storage (malloc / the pinned pool hand it out again)
+  std::vector<MemoryPtr> next;
+  for (int i = 0; i < 4; ++i) {
+    next.push_back(pinned ? Memory::alloc_pinned(kBytes) : Memory::alloc_host(kBytes));
+    std::memset(next.back()->data(), 0x22, kBytes);
+  }
+  std::string r = check_bytes(d2h(mirror->data(), kBytes, s), 0x11, pinned ? "pinned_h2d" : "pageable_h2d");
+  mirror.reset();
+  next.clear();
+  hip::check(hipStreamSynchronize(s), "selftest sync");
+  (void)hipStreamDestroy(s);
+  return r;
+}
+
+// the mirror of a host memory is read on a second stream (spinning first),
+// which records its use on the HOST memory (what a filter's replay lane does);
+// the host memory and so its mirror are released; a new device block of the
+// same size, written on the release stream, must not reach the reader
+std::string mirror_other_stream(int dev) {
+  hip::DeviceGuard g(dev);
+  hipStream_t s1 = nullptr, s2 = nullptr;
+  hip::check(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking), "selftest stream");
+  hip::check(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking), "selftest stream");
+  // (pageable: its release does not wait for readers on the host -- the mirror's
+  // own release must order itself after them)
+  MemoryPtr h = Memory::alloc_host(kBytes);
+  std::memset(h->data(), 0x33, kBytes);
+  const void* mp = h->map_device(dev, s1);
+  hip::check(hipStreamSynchronize(s1), "selftest sync");
+  MemoryPtr out = Memory::alloc_device(kBytes, dev, s2);
+  kernels::spin_us(s2, kSpinUs);
+  MemoryPtr mirror = h->device_mirror(dev);
+  mirror->wait_ready(s2);
+  hip::check(hipMemcpyAsync(out->data(), mp, kBytes, hipMemcpyDeviceToDevice, s2), "selftest D2D");
+  h->record_use(s2, dev);  // the reader holds the host memory (and, through it, the mirror)
+  mirror.reset();
+  h.reset();  // mirror released: ordered on the release stream after its recorded readers
+  hipStream_t rs = hip::release_stream(dev);
+  std::vector<MemoryPtr> again;
+  for (int i = 0; i < 4; ++i) {
+    again.push_back(Memory::alloc_device(kBytes, dev, rs));
+    hip::check(hipMemsetAsync(again.back()->data(), 0x44, kBytes, rs), "selftest memset");
+  }
+  std::string r = check_bytes(d2h(out->data(), kBytes, s2), 0x33, "mirror_other_stream");
+  again.clear();
+  out.reset();
+  hip::check(hipDeviceSynchronize(), "selftest sync");
+  (void)hipStreamDestroy(s1);
+  (void)hipStreamDestroy(s2);
+  return r;
+}
+
+// a device block read on another stream (spinning first) that recorded its use
+// is released; a new block written on the release stream must not reach the reader
+std::string device_reader(int dev) {
+  hip::DeviceGuard g(dev);
+  hipStream_t s1 = nullptr, s2 = nullptr;
+  hip::check(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking), "selftest stream");
+  hip::check(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking), "selftest stream");
+  MemoryPtr d = Memory::alloc_device(kBytes, dev, s1);
+  hip::check(hipMemsetAsync(d->data(), 0x55, kBytes, s1), "selftest memset");
+  d->mark_ready(s1);
+  MemoryPtr out = Memory::alloc_device(kBytes, dev, s2);
+  kernels::spin_us(s2, kSpinUs);
+  d->wait_ready(s2);
+  hip::check(hipMemcpyAsync(out->data(), d->data(), kBytes, hipMemcpyDeviceToDevice, s2), "selftest D2D");
+  d->record_use(s2, dev);
+  d.reset();
+  hipStream_t rs = hip::release_stream(dev);
+  std::vector<MemoryPtr> again;
+  for (int i = 0; i < 4; ++i) {
+    again.push_back(Memory::alloc_device(kBytes, dev, rs));
+    hip::check(hipMemsetAsync(again.back()->data(), 0x66, kBytes, rs), "selftest memset");
+  }
+  std::string r = check_bytes(d2h(out->data(), kBytes, s2), 0x55, "device_reader");
+  again.clear();
+  out.reset();
+  hip::check(hipDeviceSynchronize(), "selftest sync");
+  (void)hipStreamDestroy(s1);
+  (void)hipStreamDestroy(s2);
+  return r;
+}
+
+}  // namespace
+
+// "" = pass, else what went wrong
+std::string memory_selftest(const std::string& name, int dev) {
+  if (!hip::available() || dev < 0 || dev >= hip::device_count()) return "memory_selftest: no such GPU";
+  if (name == "pageable_h2d") return host_h2d(dev, false);
+  if (name == "pinned_h2d") return host_h2d(dev, true);
+  if (name == "mirror_other_stream") return mirror_other_stream(dev);
+  if (name == "device_reader") return device_reader(dev);
+  return "memory_selftest: unknown case " + name;
+}
+
+}  // namespace nnsx

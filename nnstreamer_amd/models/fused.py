@@ -70,6 +70,20 @@ def _pw_weight(w: torch.Tensor, precision: str = "bf16"):
     return out if precision == "fp32" else out.to(torch.bfloat16)
 
 
+def x3_split(w: torch.Tensor, rows: int, cols: int) -> torch.Tensor:
+    """fp32 matrix -> its split-bf16 form [3, rows, cols] bf16 (hi, mid, lo;
+    zero padded): w == hi + mid + lo exactly, each part the round-to-nearest
+    bf16 of the residual before it -- the kernels' F32Math::kX3 operands
+    (csrc/kernels/x3.h)."""
+    wp = torch.zeros(rows, cols, dtype=torch.float32)
+    wp[: w.shape[0], : w.shape[1]] = w.float()
+    hi = wp.to(torch.bfloat16)
+    r = wp - hi.float()
+    mid = r.to(torch.bfloat16)
+    lo = (r - mid.float()).to(torch.bfloat16)
+    return torch.stack([hi, mid, lo]).contiguous()
+
+
 def input_lut(add: float, div: float) -> torch.Tensor:
     """256-entry table of a uint8 input: what `tensor_transform mode=arithmetic
     option=typecast:float32,add:<add>,div:<div>` computes for every byte value,
@@ -151,6 +165,9 @@ class Block(nn.Module):
         if self.f32:
             self._init_f32(cin, hid)
             return
+        # (the fp32 path's split-bf16 weights; TorchScript compiles both branches)
+        self.register_buffer("ir_we3", torch.zeros(1, dtype=torch.bfloat16))
+        self.register_buffer("ir_wp3", torch.zeros(1, dtype=torch.bfloat16))
         # hidden width padded to the kernel's 32-channel chunk with zero weights/biases
         # (padded channels stay exactly 0 through ReLU6 and contribute nothing)
         hp = (hid + 31) // 32 * 32
@@ -190,6 +207,9 @@ class Block(nn.Module):
         self.register_buffer("ir_wd", self.dw.w.clone())
         self.register_buffer("ir_bd", self.dw.bias.clone())
         self.register_buffer("ir_wp", self.project.wt[:, :hid].contiguous().clone())
+        # split-bf16 forms for the x3 kernels: we3 [3, hid, ceil32(cin)], wp3 [3, ceil32(cout), hid]
+        self.register_buffer("ir_we3", x3_split(we[:, :cin], hid, (cin + 31) // 32 * 32))
+        self.register_buffer("ir_wp3", x3_split(self.project.wt[: self.cout, :hid], (self.cout + 31) // 32 * 32, hid))
         self.min_tiles = 0
         self.use_ir = FUSE_IR and hid % 16 == 0 and (self.has_expand or hid == cin)
         # dilated blocks (DeepLab's output-stride-16 stage) that the fused kernel
@@ -206,13 +226,14 @@ class Block(nn.Module):
                     self.dw.dilation)):
                 return torch.ops.nnsx.ir_block(x, self.ir_we, self.ir_be, self.ir_wd, self.ir_bd, self.ir_wp,
                                                self.project.bias, self.dw.stride, self.cout, self.has_expand,
-                                               self.use_res, self.dw.dilation, self.ir_tickets)
+                                               self.use_res, self.dw.dilation, self.ir_tickets, self.ir_we3,
+                                               self.ir_wp3)
             if self.use_ir and self.has_expand and bool(
                     torch.ops.nnsx.ir_expand_dw_supported_f32(self.dw.stride, x.shape[1], x.shape[2], self.cin,
                                                               self.hid, x.shape[0], self.dw.dilation)):
                 # expand + depthwise in one kernel (no hidden map in HBM), project as a GEMM
                 h = torch.ops.nnsx.ir_expand_dw(x, self.ir_we, self.ir_be, self.ir_wd, self.ir_bd, self.dw.stride,
-                                                self.dw.dilation)
+                                                self.dw.dilation, self.ir_we3)
             else:
                 h = self.expand(x) if self.has_expand else x
                 if self.dwpw_dilated and (self.dw.dilation > 1 or self.dwpw_all) and h.is_cuda:

@@ -34,3 +34,29 @@ def test_bench_refuses_world_mismatch():
              env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0
     assert "WORLD_SIZE=1" in (r.stderr + r.stdout)
+
+
+def test_bench_three_ranks_selfcheck_and_extra_configs():
+    """WORLD_SIZE > 1 (the driver's scaling run): before the timed run every
+    comm::Group operation is checked on every rank (rccl_selfcheck; tcp data
+    plane on CPU, RCCL on GPUs), and after the headline short passes of the
+    multi-rank configs 4 and 5 report their frames/s and groups -- all outside
+    the timed region, well inside a minute."""
+    import time
+
+    t0 = time.time()
+    r = _run(["--cpu", "--gpus", "3", "--steps", "2", "--warmup", "1", "--batch", "1", "--latency-frames", "0",
+              "--sweep", ""])
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert time.time() - t0 < 120
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    sc = out["rccl_selfcheck"]
+    for k in ("allgather", "allgather_ragged", "broadcast", "scatter", "p2p_ring", "p2p_exchange"):
+        assert sc[k] is True, sc
+    assert sc["members"] == 3 and sc["backend"] == "tcp"
+    xs = out["extra_configs"]
+    assert set(xs) == {"deeplab_fan", "posenet_multi"}
+    assert all(v["frames_per_s"] and v["frames_per_s"] > 0 for v in xs.values()), xs
+    assert "edge_fan1" in xs["deeplab_fan"]["groups_rank0"] and "edge_allgather" in xs["posenet_multi"]["groups_rank0"]
+    assert out["fp32_method"] in ("x3", "fp32")
+    assert out["value"] > 0 and out["n_gpus"] == 0

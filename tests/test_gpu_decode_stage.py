@@ -35,7 +35,7 @@ CASES = {
 }
 
 
-def _run(nns, workdir, case, B, absorb, graph, queue):
+def _run(nns, workdir, case, B, absorb, graph, queue, lanes=0):
     from nnstreamer_amd.models.export import export
 
     S, model_name, norm, dec = CASES[case]
@@ -45,7 +45,8 @@ def _run(nns, workdir, case, B, absorb, graph, queue):
             f"! video/x-raw,format=RGB,width={S},height={S},framerate=30/1 "
             f"! tensor_converter frames-per-tensor={B} device=0 ! tensor_transform mode=arithmetic option={norm} "
             f"! tensor_filter name=f framework=pytorch model={model} input=3:{S}:{S}:{B} inputtype=float32 "
-            f"accelerator=true:gpu device=0 custom=hipgraph:{'true' if graph else 'false'} "
+            f"accelerator=true:gpu device=0 custom=hipgraph:{'true' if graph else 'false'}"
+            f"{f',lanes:{lanes}' if lanes else ''} "
             f"absorb-decoder={'true' if absorb else 'false'} ! {q}{dec.format(**_files(workdir))} "
             "! tensor_sink name=sink")
     p = nns.parse_launch(desc)
@@ -69,3 +70,15 @@ def test_decoder_stage_in_graph_matches_own_kernels(nns, workdir, case, B, graph
     assert got == ref
     if case != "ssd":  # (random-init SSD may detect nothing)
         assert any(any(x) for x in got[:4])  # something was drawn
+
+
+@pytest.mark.parametrize("case", ["ssd", "posenet"])
+def test_decoder_stage_with_replay_lanes_asked(nns, workdir, case):
+    """custom=lanes:3 with a decoder stage absorbed: the stage's scratch lives in
+    the stage object, so the filter replays on one lane (lane_count); the frames
+    equal, byte for byte, the decoder running its own kernels"""
+    got, info = _run(nns, workdir, case, 4, True, True, True, lanes=3)
+    ref, _ = _run(nns, workdir, case, 4, False, True, True, lanes=3)
+    assert info == ("dec", "f"), info
+    assert len(got) == len(ref) == 12
+    assert got == ref

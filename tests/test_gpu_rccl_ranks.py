@@ -64,3 +64,21 @@ def test_bench_multi_rank_configs(cfg):
         assert rec.get("mux_sets_rank0") == 4, rec  # every batch a full N-camera set
     else:
         assert "tensor_demux" in rec["config"]["pipeline"], rec
+
+
+@needs2
+def test_bench_headline_selfcheck_and_extra_configs():
+    """The driver's scaling command shape at N = min(#GPUs, 8): bench.py's
+    rccl_selfcheck (every comm::Group operation over RCCL on frame-sized
+    payloads) and the config-4 / config-5 passes after the headline."""
+    n = min(_ngpu(), 8)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", "5",
+                        "--warmup", "2", "--latency-frames", "0", "--sweep", ""],
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    sc = rec["rccl_selfcheck"]
+    assert sc["backend"] == "rccl" and sc["members"] == n, sc
+    assert all(sc[k] for k in ("allgather", "allgather_ragged", "broadcast", "scatter", "p2p_ring", "p2p_exchange"))
+    xs = rec["extra_configs"]
+    assert xs["deeplab_fan"]["rccl_world"] == 2 and xs["posenet_multi"]["rccl_world"] == n, xs

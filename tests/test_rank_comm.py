@@ -293,3 +293,61 @@ def test_query_server_survives_a_crashed_client(nns, tmp_path):
     c.stop()
     server.stop()
     assert [float(m[0][0]) for _, m in out] == [2.0 * i for i in range(5)]
+
+
+def test_edge_allgather_subscriber_stops_others_continue(tmp_path):
+    """edgesink/edgesrc rccl-mode=allgather (the topic's EdgeHub): one
+    subscriber of a member stops in the middle of the stream; the publisher
+    and the member's other subscriber carry on and receive every frame.
+    Cancellation is per waiter (comm_elements.cc EdgeHub::cancel_take /
+    cancel_publish): a shared flag used to fail every later publish and take."""
+    script = tmp_path / "member.py"
+    script.write_text(textwrap.dedent(f"""
+        import os, sys, time
+        sys.path.insert(0, {ROOT!r})
+        import numpy as np
+        import nnstreamer_amd as nns
+        rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+        caps = "other/tensors,format=static,num_tensors=1,dimensions=2,types=float32,framerate=0/1"
+        edge = (f"connect-type=RCCL rccl-mode=allgather topic=stopper rank={{rank}} world-size={{world}} "
+                "comm-backend=tcp comm-timeout=30000")
+        others = [r for r in range(world) if r != rank]
+        subs, outs = {{}}, {{}}
+        for r in others:
+            p = nns.parse_launch(f"edgesrc name=s {{edge}} peer-rank={{r}} ! tensor_sink name=sink")
+            outs[r] = []
+            p.get_by_name("sink").connect("new-data", lambda b, r=r: outs[r].append(
+                float(b.memory(0).numpy("float32")[0])))
+            p.set_state("playing")
+            subs[r] = p
+        pub = nns.parse_launch(f"appsrc name=src caps={{caps}} ! edgesink name=ag {{edge}}")
+        pub.set_state("playing")
+        stopped = others[0]
+        for i in range(12):
+            pub.get_by_name("src").push_buffer(np.full(2, 100 * rank + i, np.float32), pts=i)
+            if i == 4:
+                time.sleep(0.3)
+                subs[stopped].stop()
+        pub.get_by_name("src").end_of_stream()
+        msg = pub.wait(60)
+        assert msg and msg[0] == "eos", pub.messages()
+        keep = others[1]
+        msg = subs[keep].wait(60)
+        assert msg and msg[0] == "eos", subs[keep].messages()
+        subs[keep].stop()
+        pub.stop()
+        print("OUT", keep, outs[keep], flush=True)
+    """))
+    port = _free_port()
+    procs = []
+    for r in range(3):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="3", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = [p.communicate(timeout=180)[0] for p in procs]
+    for p, o in zip(procs, outs):
+        assert p.returncode == 0, o[-3000:]
+        line = [x for x in o.splitlines() if x.startswith("OUT")][0]
+        _, keep, vals = line.split(" ", 2)
+        assert eval(vals) == [100.0 * int(keep) + i for i in range(12)], o[-2000:]
