@@ -1431,8 +1431,12 @@ struct IrwX3Geom {
   static constexpr size_t xs_b = static_cast<size_t>(3) * K8 * XSP * 16;
   static constexpr size_t hid_b = static_cast<size_t>(16) * 4 * NW * PINP;
   static constexpr size_t red_b = static_cast<size_t>(16) * 8 * NW * NPX;  // [wave][cout quad][px]
-  static size_t lds_bytes(int) { return std::max(xs_b + hid_b, red_b); }
-  static constexpr int MINB = NO32 * NP32 <= 4 ? 2 : 1;
+  // + the depthwise weights and bias of the workgroup's hidden channels, [10][hid]
+  // (taps 0-8, bias), staged once: read per subtile just before the depthwise
+  static size_t lds_bytes(int hid) {
+    return std::max(xs_b + hid_b + static_cast<size_t>(40) * hid, red_b);
+  }
+  static constexpr int MINB = (NOT > 0 && NO32 * NP32 <= 4) ? 2 : 1;
 };
 
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
@@ -1542,31 +1546,38 @@ __global__ void __launch_bounds__(64 * NW, (IrwX3Geom<S, TY, TX, KIN, NOT, NW, F
 #pragma unroll
     for (int o = 0; o < NOA; ++o) acc[pt][o] = f32x16_t{};
 
-  __syncthreads();  // xs + zeroed halos
-
   const int nsub = a.hid >> 4;
   const int sub0 = part * nsub / nparts, sub1 = (part + 1) * nsub / nparts;
+  // the part's depthwise taps + bias into LDS ([10][nch], row 9 = bias)
+  const int nch = (sub1 - sub0) * 16, ch0 = sub0 * 16;
+  f32x4_t* wdl = reinterpret_cast<f32x4_t*>(reinterpret_cast<char*>(smem) + G::xs_b + G::hid_b);
+  for (int v = tid; v < 10 * (nch / 4); v += NT) {
+    const int t = v / (nch / 4), q = v - t * (nch / 4);
+    wdl[v] = *reinterpret_cast<const f32x4_t*>((t < 9 ? a.wd + t * a.hid : a.bd) + ch0 + 4 * q);
+  }
+  __syncthreads();  // xs + zeroed halos + depthwise weights
+
   f32x4_t* myhid = hidw + wave * 4 * PINP;
   const int64_t wes = static_cast<int64_t>(a.hid) * KP;            // we3 part stride
   const int64_t wps = static_cast<int64_t>(NOA * 32) * a.hid;      // wp3 part stride
-  for (int hs = sub0 + wave; hs < sub1; hs += NW) {
-    const int ch8 = hs * 16 + 8 * h;  // this lane's 8 depthwise / project channels
-    X3Frag ea[NK32];
+  // the expand weights + bias of the NEXT subtile are in flight during this
+  // subtile's depthwise + project (issued after its expand's last use of them)
+  X3Frag ea[NK32];
+  f32x4_t be4;
+  auto load_ea = [&](int hs) {
 #pragma unroll
     for (int c = 0; c < NK32; ++c)
       ea[c] = load_x3(a.we3, wes, static_cast<int64_t>(hs * 16 + li) * KP + 32 * c + 8 * g);
+    be4 = *reinterpret_cast<const f32x4_t*>(a.be + hs * 16 + 4 * g);
+  };
+  int hs = sub0 + wave;
+  if (hs < sub1) load_ea(hs);
+  for (; hs < sub1; hs += NW) {
+    const int ch8 = hs * 16 + 8 * h;  // this lane's 8 depthwise / project channels
+    // project weights: in flight during the expand
     X3Frag pa[NOA];
 #pragma unroll
     for (int o = 0; o < NO32; ++o) pa[o] = load_x3(a.wp3, wps, static_cast<int64_t>(o * 32 + l32) * a.hid + ch8);
-    f32x4_t wdA[9], wdB[9];
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      wdA[t] = *reinterpret_cast<const f32x4_t*>(a.wd + t * a.hid + ch8);
-      wdB[t] = *reinterpret_cast<const f32x4_t*>(a.wd + t * a.hid + ch8 + 4);
-    }
-    const f32x4_t bdA = *reinterpret_cast<const f32x4_t*>(a.bd + ch8);
-    const f32x4_t bdB = *reinterpret_cast<const f32x4_t*>(a.bd + ch8 + 4);
-    const f32x4_t be4 = *reinterpret_cast<const f32x4_t*>(a.be + hs * 16 + 4 * g);
 
     // ---- expand -> private hidden image (lane: pixel li, channels 4g .. 4g + 3)
 #pragma unroll
@@ -1599,36 +1610,46 @@ __global__ void __launch_bounds__(64 * NW, (IrwX3Geom<S, TY, TX, KIN, NOT, NW, F
         }
       }
     }
+    if (hs + NW < sub1) load_ea(hs + NW);
     wave_sync();
 
-    // ---- depthwise 3x3 + bias + ReLU6 (lane: pixel l32 of tile pt, 8 channels),
-    // split -> project
+    // ---- depthwise 3x3 + bias + ReLU6 (lane: pixel l32 of tile pt, 8 channels
+    // in two halves of 4, the taps from LDS), split -> project
+    f32x4_t dA[NP32], dB[NP32];
+    const int cl = ch8 - ch0;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      f32x4_t w[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) w[t] = wdl[(t * nch + cl) / 4 + half];
+      const f32x4_t bd = wdl[(9 * nch + cl) / 4 + half];
+#pragma unroll
+      for (int pt = 0; pt < NP32; ++pt) {
+        const f32x4_t* hp = myhid + (2 * h + half) * PINP + dcell[pt];
+        f32x4_t d = bd;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) d = __builtin_elementwise_fma(hp[(ky * TIX + kx) * DIL], w[ky * 3 + kx], d);
+        if (half == 0)
+          dA[pt] = relu6x4(d);
+        else
+          dB[pt] = relu6x4(d);
+      }
+    }
 #pragma unroll
     for (int pt = 0; pt < NP32; ++pt) {
-      const f32x4_t* hA = myhid + (2 * h) * PINP + dcell[pt];
-      const f32x4_t* hB = hA + PINP;
-      f32x4_t dA = bdA, dB = bdB;
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          const int off = (ky * TIX + kx) * DIL;
-          dA = __builtin_elementwise_fma(hA[off], wdA[ky * 3 + kx], dA);
-          dB = __builtin_elementwise_fma(hB[off], wdB[ky * 3 + kx], dB);
-        }
-      dA = relu6x4(dA);
-      dB = relu6x4(dB);
       if constexpr (NOT == 0) {
         const int q = pt * 32 + l32;
         const int gy = oy0 + q / TX, gx = ox0 + q % TX;
         if (q < TY * TX && gy < a.Ho && gx < a.Wo) {
           float* yp = a.y + ((static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx) * a.hid + ch8;
-          *reinterpret_cast<f32x4_t*>(yp) = dA;
-          *reinterpret_cast<f32x4_t*>(yp + 4) = dB;
+          *reinterpret_cast<f32x4_t*>(yp) = dA[pt];
+          *reinterpret_cast<f32x4_t*>(yp + 4) = dB[pt];
         }
         continue;
       }
-      const X3Frag bf = split_x3(dA, dB);
+      const X3Frag bf = split_x3(dA[pt], dB[pt]);
 #pragma unroll
       for (int o = 0; o < NO32; ++o) acc[pt][o] += mfma32_x3(pa[o], bf);
     }
@@ -2379,10 +2400,9 @@ const IrwCfg kIrwCfgs[] = {
 const IrwCfg kIrwX3Cfgs[] = {
     NNSX_IRWX(2, 4, 8, 16, 2, 3, true),   NNSX_IRWX(1, 8, 8, 24, 2, 3, true),   NNSX_IRWX(2, 4, 4, 24, 2, 3, true),
     NNSX_IRWX(2, 7, 4, 24, 2, 3, true),   NNSX_IRWX(1, 7, 7, 32, 2, 4, false),  NNSX_IRWX(2, 2, 7, 32, 4, 4, false),
-    NNSX_IRWX(1, 7, 14, 64, 4, 4, false), NNSX_IRWX(1, 7, 7, 64, 4, 4, false),  NNSX_IRWX(1, 7, 7, 64, 6, 4, false),
-    NNSX_IRWX(1, 7, 7, 96, 6, 4, false),  NNSX_IRWX(1, 7, 7, 160, 10, 4, false), NNSX_IRWX(2, 7, 7, 96, 10, 4, false),
-    NNSX_IRWX(1, 7, 7, 160, 0, 4, false), NNSX_IRWX(1, 5, 5, 160, 10, 4, false), NNSX_IRWX(2, 5, 5, 96, 10, 4, false),
-    NNSX_IRWX(1, 5, 5, 160, 0, 4, false), NNSX_IRWX(1, 7, 14, 64, 6, 4, false), NNSX_IRWX(1, 7, 14, 96, 6, 4, false),
+    NNSX_IRWX(1, 7, 7, 64, 4, 4, false),  NNSX_IRWX(1, 7, 7, 64, 6, 4, false),  NNSX_IRWX(1, 7, 7, 96, 6, 4, false),
+    NNSX_IRWX(1, 7, 7, 160, 10, 4, false), NNSX_IRWX(2, 7, 7, 96, 10, 4, false), NNSX_IRWX(1, 7, 7, 160, 0, 4, false),
+    NNSX_IRWX(1, 5, 5, 160, 10, 4, false), NNSX_IRWX(2, 5, 5, 96, 10, 4, false), NNSX_IRWX(1, 5, 5, 160, 0, 4, false),
 };
 #undef NNSX_IRWX
 
@@ -2398,11 +2418,21 @@ bool x3_irw_enabled() {
 // the x3 twin of a configuration, when the method is x3 and both weight
 // parts are given (the expand-only form needs no project weights)
 const IrwCfg* x3_twin(const IrwCfg* c, const IrBlockF32Args& a) {
-  if (!c || f32_math() != F32Math::kX3 || !x3_irw_enabled() || !a.we3 || (c->NOT > 0 && !a.wp3)) return nullptr;
-  for (const IrwCfg& x : kIrwX3Cfgs)
-    if (x.S == c->S && x.TY == c->TY && x.TX == c->TX && x.KIN == c->KIN && x.NOT == c->NOT && x.NW == c->NW &&
-        x.full == c->full && x.dil == c->dil && x.lds(a.hid) <= 160 * 1024)
-      return &x;
+  if (!c || f32_math() != F32Math::kX3 || !a.we3 || (c->NOT > 0 && !a.wp3)) return nullptr;
+  // by default only where the x3 kernel measured faster than the native one
+  // (scripts/x3_blocks_ab.py, batch 512: the 960-hidden 7 x 7 blocks 170 vs 208 us;
+  // the LDS traffic of the split operands -- 3 x 16 B per 32-channel B fragment
+  // against 2 x 16 B of fp32 -- bounds the smaller-K blocks: profiles/r5_x3_blocks_ab.txt);
+  // NNSX_X3_IRW=1: every configuration with a twin (A/B)
+  if (!x3_irw_enabled() && !(c->KIN == 160 && c->NOT == 10 && c->S == 1)) return nullptr;
+  // the same tile, else (7 x 14 tiles: their 4 32-pixel project tiles hold more
+  // accumulators than two waves per SIMD allow) the 7 x 7 tile of the shape
+  for (int pass = 0; pass < 2; ++pass)
+    for (const IrwCfg& x : kIrwX3Cfgs)
+      if (x.S == c->S && (pass == 0 ? (x.TY == c->TY && x.TX == c->TX) : (x.TY == 7 && x.TX == 7 && c->TX == 14)) &&
+          x.KIN == c->KIN && x.NOT == c->NOT && x.NW == c->NW && x.full == c->full && x.dil == c->dil &&
+          x.lds(a.hid) <= 160 * 1024)
+        return &x;
   return nullptr;
 }
 

@@ -13,7 +13,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 import nnstreamer_amd  # noqa: F401,E402
-from nnstreamer_amd.models.fused import input_lut  # noqa: E402
+from nnstreamer_amd.models.fused import input_lut, x3_split  # noqa: E402
 
 PEAK = 157.3e12
 LUT = input_lut(-127.5, 127.5).cuda() if torch.cuda.is_available() else None
@@ -75,8 +75,12 @@ for H, cin, hid, cout, st in SHAPES:
     bp = torch.zeros(npad, device="cuda")
     res = st == 1 and cin == cout
     ok = bool(torch.ops.nnsx.ir_supported_f32(st, H, H, cin, hid, cout, has_expand))
+    # split-bf16 weights: the x3 kernel runs when NNSX_F32_MATH (default x3) and NNSX_X3_IRW select it
+    we3 = x3_split(we[:, :cin].cpu(), hid, (cin + 31) // 32 * 32).cuda() if has_expand else None
+    wp3 = x3_split(wp[:cout].cpu(), (cout + 31) // 32 * 32, hid).cuda() if has_expand else None
     if ok:
-        fn = lambda: torch.ops.nnsx.ir_block(x, we, be, wd, bd, wp, bp, st, cout, has_expand, res)  # noqa: E731
+        fn = lambda: torch.ops.nnsx.ir_block(x, we, be, wd, bd, wp, bp, st, cout, has_expand, res, 1, None,  # noqa: E731
+                                             we3, wp3)
         tag = "fused"
     elif has_expand and bool(torch.ops.nnsx.ir_expand_dw_supported_f32(st, H, H, cin, hid, B)):
         def fn():
