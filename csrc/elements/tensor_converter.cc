@@ -466,11 +466,6 @@ class TensorConverter : public Element {
   // profiles/r3_config_trace_deeplab_b8.txt.)  Every piece must be a whole
   // padded pinned frame of one geometry.
   bool padded_dma(size_t size, int dev, hipStream_t s, const MemoryPtr& out) {
-    static const bool on = [] {
-      const char* e = std::getenv("NNSX_CONVERTER_PADDED_DMA");
-      return !(e && e[0] == '0');
-    }();
-    if (!on) return false;
     std::vector<Piece*> ps;
     size_t seen = 0;
     for (Piece& p : adapter_) {
@@ -493,50 +488,13 @@ class TensorConverter : public Element {
     if (!ring) spacing = (sf + 255) / 256 * 256;
     auto stg = Memory::alloc_device(spacing * (ps.size() - 1) + sf, dev, s);
     char* sp = static_cast<char*>(stg->data());
-    // NNSX_CONVERTER_DMA_SPLIT=k (1-4): the upload as k copies on k streams (more
-    // than one copy engine on the host link), joined back into s before the unpad
-    static const int split = [] {
-      const char* e = std::getenv("NNSX_CONVERTER_DMA_SPLIT");
-      return e ? std::max(1, std::min(4, std::atoi(e))) : 1;
-    }();
-    const size_t total = spacing * (ps.size() - 1) + sf;
-    const int k = total >= (4u << 20) ? split : 1;
-    hipEvent_t start = nullptr;
-    if (k > 1) {
-      hip::check(hipEventCreateWithFlags(&start, hipEventDisableTiming), "dma split event");
-      hip::check(hipEventRecord(start, s), "dma split record");
-    }
-    auto lane = [&](int i) {  // the stream of copy i (0: s itself)
-      if (i == 0) return s;
-      hipStream_t ds = dma_streams_[i - 1].get(dev);
-      hip::check(hipStreamWaitEvent(ds, start, 0), "dma split wait");
-      return ds;
-    };
-    std::vector<hipStream_t> used;
+    // (splitting the upload over 2-4 copy streams did not help: profiles/r4_upload_bench.txt)
     if (ring) {
-      const size_t chunk = ((total + k - 1) / k + 4095) / 4096 * 4096;
-      for (int i = 0; i < k && static_cast<size_t>(i) * chunk < total; ++i) {
-        const size_t off = static_cast<size_t>(i) * chunk, len = std::min(chunk, total - off);
-        hipStream_t ds = lane(i);
-        hip::check(hipMemcpyAsync(sp + off, base + off, len, hipMemcpyHostToDevice, ds), "padded ring DMA");
-        if (i) used.push_back(ds);
-      }
+      hip::check(hipMemcpyAsync(sp, base, spacing * (ps.size() - 1) + sf, hipMemcpyHostToDevice, s), "padded ring DMA");
     } else {
-      std::vector<hipStream_t> lanes;
-      for (int i = 0; i < k; ++i) lanes.push_back(lane(i));
       for (size_t i = 0; i < ps.size(); ++i)
-        hip::check(hipMemcpyAsync(sp + i * spacing, ps[i]->mem->data(), sf, hipMemcpyHostToDevice, lanes[i % k]),
-                   "padded DMA");
-      used.assign(lanes.begin() + 1, lanes.end());
+        hip::check(hipMemcpyAsync(sp + i * spacing, ps[i]->mem->data(), sf, hipMemcpyHostToDevice, s), "padded DMA");
     }
-    for (hipStream_t ds : used) {  // join the copies back into s
-      hipEvent_t done;
-      hip::check(hipEventCreateWithFlags(&done, hipEventDisableTiming), "dma join event");
-      hip::check(hipEventRecord(done, ds), "dma join record");
-      hip::check(hipStreamWaitEvent(s, done, 0), "dma join wait");
-      (void)hipEventDestroy(done);
-    }
-    if (start) (void)hipEventDestroy(start);
     kernels::unpad_rows(sp, out->data(), static_cast<uint32_t>(ps.size()), static_cast<uint32_t>(row),
                         static_cast<uint32_t>(stride), static_cast<uint32_t>(rows), spacing, s);
     stg->record_use(s, dev);
@@ -863,7 +821,6 @@ class TensorConverter : public Element {
   ConverterCustomFn custom_fn_;
   std::shared_ptr<ConverterSubplugin> external_;
   StreamSet streams_;
-  StreamSet dma_streams_[3];  // extra copy streams of a split padded-frame upload (padded_dma)
 };
 
 }  // namespace

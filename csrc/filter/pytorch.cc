@@ -735,13 +735,9 @@ class TorchInstance : public FilterInstance {
   int argmax_out_ = -1;        // output replaced by its argmax (absorbed decoder), -1: none
   std::shared_ptr<DecodeStage> stage_;  // absorbed decoder's device stage (runtime/fusion.h)
   // the absorbed argmax's indices are copied to pinned host memory after each
-  // graph replay (NNSX_TORCH_HOST_ARGMAX=0: a device clone, read back by the
-  // decoder).  Batch 1 at a live 500 fps camera: p50 308 vs 362-366 us, filter
-  // device time 287 vs 312-322 us (profiles/r3_b1_host_argmax_ab.txt)
-  const bool host_argmax_ = [] {
-    const char* e = std::getenv("NNSX_TORCH_HOST_ARGMAX");
-    return !(e && e[0] == '0');
-  }();
+  // graph replay (a device clone read back by the decoder measured slower: batch 1
+  // at a live 500 fps camera p50 308 vs 362-366 us, profiles/r3_b1_host_argmax_ab.txt)
+  const bool host_argmax_ = true;
   bool has_lut_ = false;       // the model maps uint8 input 0 through attribute in_lut
   std::vector<float> lut_;     // the absorbed table (re-applied on hot reload)
   std::vector<float> default_lut_;  // the table of the loaded model file (reset_input_table)

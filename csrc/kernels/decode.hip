@@ -6,7 +6,7 @@
 
 #include <cfloat>
 
-#include "kernels/dtype.cuh"
+#include "kernels/dtype.h"
 #include "kernels/kernels.h"
 
 namespace nnsx {

@@ -77,11 +77,6 @@ struct YLayout {
   // (an image spans at most two row tiles: two addends, so the sum is order-free)
   int pool = 0;
 };
-// plain fp32 pointwise GEMM on hipBLASLt (blaslt.cc): y[M][N] = act(x . wt^T + bias) (+ res);
-// false = not taken (the caller runs its own kernel).  Opt-in: NNSX_F32_BLASLT=1 (blaslt.cc)
-bool blaslt_enabled();
-bool blaslt_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
-                     int Kpad, int act, hipStream_t s);
 void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
                  int Kpad, int Npad, int act, hipStream_t s, int tile = 0, float* ws = nullptr,
                  const YLayout& yl = YLayout{});
@@ -131,10 +126,6 @@ struct SepHeadsArgs {
   int n = 0;
   SepHead h[kSepHeadsMax];
 };
-void sep_heads_f32(SepHeadsArgs a, hipStream_t s);
-// the general form (dwpw_f32.hip): depthwise (stride 1|2, optional) + pointwise
-// (+ ReLU6) problems, one grouped launch
-void dwpw_f32(SepHeadsArgs a, hipStream_t s);
 // split-K workspace the GEMM wants for this shape (0: no split; without it the
 // GEMM runs unsplit)
 size_t pw_gemm_f32_workspace_bytes(int M, int N, int Kpad, bool has_res, int tile = 0);
@@ -235,7 +226,7 @@ struct StemIr1F32Args {
   const float* bp = nullptr;
   int B = 0, H = 0, W = 0;
   const float* lut = nullptr;  // [256] f32, device
-  int mode = -1;               // kernel: -1 = $NNSX_STEM_WAVE policy, 0/1/2 tile kernels, 3 line buffer
+  int mode = -1;               // (unused: one kernel)
   // derived
   int Ho = 0, Wo = 0, tiles_x = 0, tiles_y = 0;
 };

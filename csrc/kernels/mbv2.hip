@@ -498,11 +498,7 @@ void pw_gemm(const void* x, const void* wt, const float* bias, const void* res, 
     const auto* wp = static_cast<const uint16_t*>(wt);
     const auto* rp = static_cast<const uint16_t*>(res);
     const int big = ((M + 127) / 128) * ((N + 127) / 128);
-    static const int big_min = [] {
-      const char* e = std::getenv("NNSX_GEMM_BIG_MIN");
-      return e ? std::atoi(e) : 256;
-    }();
-    if (big >= big_min) {
+    if (big >= 256) {
       const dim3 g((M + 127) / 128, (N + 127) / 128);
       if (out_f32)
         hipLaunchKernelGGL((pw_gemm_lds_kernel<128, 128, true>), g, dim3(256), 0, s, xp, wp, bias, rp, y, M, N, K, Kpad,

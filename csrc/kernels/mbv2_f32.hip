@@ -52,15 +52,6 @@ namespace kernels {
 
 namespace {
 
-// stem_ir1 tile (TY, TX) and waves: 16 x 16 with 8 waves measured 136 us at
-// batch 128 vs 145 (8 x 16, 4 waves) and 147 (8 x 32, 8 waves) -- the per-tile
-// fixed cost (4 barriers, patch staging; ~55 us of the kernel when every
-// compute phase is ablated) is amortised over twice the pixels
-#ifndef NNSX_STEM_TILE
-#define NNSX_STEM_TILE 16, 16, 8
-#endif
-constexpr int kStemIr1Cfg[3] = {NNSX_STEM_TILE};
-constexpr int kStemIr1TY = kStemIr1Cfg[0], kStemIr1TX = kStemIr1Cfg[1], kStemIr1NW = kStemIr1Cfg[2];
 
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
@@ -121,8 +112,15 @@ __device__ __forceinline__ void pw_gemm_f32_tile(const float* __restrict__ x,   
   // staging writes (8 lanes = 8 k-quads of one row) then spread over the
   // banks, and fragment reads stay conflict-free (16 rows of one 16-aligned
   // block, permuted)
-  __shared__ __attribute__((aligned(16))) float xs[2][GKQ][BM][4];
-  __shared__ __attribute__((aligned(16))) float ws[2][GKQ][BN][4];
+  // X3: both operands are split once, while they are staged, into three bf16
+  // planes [part][k8][row] of 8 consecutive k (16 B) -- the fragment of a
+  // 32-k step is then 3 ds_read_b128 per operand and no VALU; rows
+  // XOR-swizzled by k8 (staging writes spread, fragment reads stay 256
+  // contiguous bytes per 16 lanes)
+  __shared__ __attribute__((aligned(16))) float xs[X3 ? 1 : 2][GKQ][X3 ? 4 : BM][4];
+  __shared__ __attribute__((aligned(16))) float ws[X3 ? 1 : 2][GKQ][X3 ? 4 : BN][4];
+  __shared__ __attribute__((aligned(16))) bf16x8_t xs3[X3 ? 2 : 1][3][4][X3 ? BM : 1];
+  __shared__ __attribute__((aligned(16))) bf16x8_t ws3[X3 ? 2 : 1][3][4][X3 ? BN : 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int li = lane & 15, g = lane >> 4;
@@ -144,16 +142,39 @@ __device__ __forceinline__ void pw_gemm_f32_tile(const float* __restrict__ x,   
                                      : zero;
     }
   };
+  // (X3) a staged quad -> its three bf16 parts, 8 B into each part plane
+  auto st3 = [&](bf16x8_t* base, size_t part_stride, f32x4_t q) {
+    bf16x2_t h0, m0, l0, h1, m1, l1;
+    split2(f32x2_t{q[0], q[1]}, h0, m0, l0);
+    split2(f32x2_t{q[2], q[3]}, h1, m1, l1);
+    typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+    char* p = reinterpret_cast<char*>(base);
+    *reinterpret_cast<bf16x4_t*>(p) = __builtin_shufflevector(h0, h1, 0, 1, 2, 3);
+    *reinterpret_cast<bf16x4_t*>(p + part_stride) = __builtin_shufflevector(m0, m1, 0, 1, 2, 3);
+    *reinterpret_cast<bf16x4_t*>(p + 2 * part_stride) = __builtin_shufflevector(l0, l1, 0, 1, 2, 3);
+  };
   auto lstore = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < VX; ++i) {
       const int v = tid + i * 256, kq = v & 7, row = v >> 3;
-      *reinterpret_cast<f32x4_t*>(&xs[buf][kq][row ^ kq][0]) = px[i];
+      if constexpr (X3) {
+        const int k8 = kq >> 1;
+        st3(reinterpret_cast<bf16x8_t*>(reinterpret_cast<char*>(&xs3[buf][0][k8][row ^ k8]) + (kq & 1) * 8),
+            sizeof(xs3[0][0]), px[i]);
+      } else {
+        *reinterpret_cast<f32x4_t*>(&xs[buf][kq][row ^ kq][0]) = px[i];
+      }
     }
 #pragma unroll
     for (int i = 0; i < VW; ++i) {
       const int v = tid + i * 256, kq = v & 7, row = v >> 3;
-      *reinterpret_cast<f32x4_t*>(&ws[buf][kq][row ^ kq][0]) = pw[i];
+      if constexpr (X3) {
+        const int k8 = kq >> 1;
+        st3(reinterpret_cast<bf16x8_t*>(reinterpret_cast<char*>(&ws3[buf][0][k8][row ^ k8]) + (kq & 1) * 8),
+            sizeof(ws3[0][0]), pw[i]);
+      } else {
+        *reinterpret_cast<f32x4_t*>(&ws[buf][kq][row ^ kq][0]) = pw[i];
+      }
     }
   };
 
@@ -173,19 +194,22 @@ __device__ __forceinline__ void pw_gemm_f32_tile(const float* __restrict__ x,   
     if (ks + 1 < nk) gload(kbeg + (ks + 1) * GKT);  // in flight during this stage's MFMAs
     if constexpr (X3) {
       static_assert(GKT == 32, "x3: one 32-k step per stage");
-      // lane (li, g): k-quads 2g, 2g + 1 of its row = k 8g .. 8g + 7
+      // lane (li, g): k 8g .. 8g + 7 of its row = plane k8 = g
       X3Frag a[RN];
 #pragma unroll
       for (int j = 0; j < RN; ++j) {
-        const int r = wn * (BN / 2) + j * 16 + li;
-        a[j] = split_x3(*reinterpret_cast<const f32x4_t*>(&ws[buf][2 * g][r ^ (2 * g)][0]),
-                        *reinterpret_cast<const f32x4_t*>(&ws[buf][2 * g + 1][r ^ (2 * g + 1)][0]));
+        const int r = (wn * (BN / 2) + j * 16 + li) ^ g;
+        a[j].h = ws3[buf][0][g][r];
+        a[j].m = ws3[buf][1][g][r];
+        a[j].l = ws3[buf][2][g][r];
       }
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
-        const int r = wm * (BM / 2) + i * 16 + li;
-        const X3Frag b = split_x3(*reinterpret_cast<const f32x4_t*>(&xs[buf][2 * g][r ^ (2 * g)][0]),
-                                  *reinterpret_cast<const f32x4_t*>(&xs[buf][2 * g + 1][r ^ (2 * g + 1)][0]));
+        const int r = (wm * (BM / 2) + i * 16 + li) ^ g;
+        X3Frag b;
+        b.h = xs3[buf][0][g][r];
+        b.m = xs3[buf][1][g][r];
+        b.l = xs3[buf][2][g][r];
 #pragma unroll
         for (int j = 0; j < RN; ++j) acc[i][j] += mfma_x3(a[j], b);
       }
@@ -217,7 +241,7 @@ __device__ __forceinline__ void pw_gemm_f32_tile(const float* __restrict__ x,   
       // head conv + act + global average pool: the activated tile goes through
       // the (now free) staging LDS, quads XOR-swizzled by row; each thread sums
       // one (image, channel) column of the tile in row order and adds sum / pool
-      float* t = &xs[0][0][0][0];  // [BM][64]
+      float* t = X3 ? reinterpret_cast<float*>(&xs3[0][0][0][0]) : &xs[0][0][0][0];  // [BM][64]
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
         const int ml = wm * (BM / 2) + i * 16 + li, m = m0 + ml;
@@ -1709,169 +1733,12 @@ __global__ void __launch_bounds__(64 * NW, (IrwX3Geom<S, TY, TX, KIN, NOT, NW, F
   irw_inlaunch_combine<TY, TX, NT>(a, smem, tile, part, nparts, b, oy0, ox0, tid);
 }
 
-// --------------------------------------------------------- stem_ir1_f32 ----
-// The stem (3x3/2 conv 3 -> 32 on the raw uint8 frame, mapped in-kernel
-// through the 256-entry input table, + bias, ReLU6) fused with MobileNetV2's first block
-// (t = 1: dw 3x3 on those 32 channels + ReLU6, project 32 -> 16).  The 32-
-// channel stem output -- the largest activation of the network, 205 MB per
-// 128 frames in fp32 -- never leaves LDS.
-//
-// One workgroup = one TY x TX tile of the 112x112 block output, 4 waves =
-// (16-channel half) x (pixel half): stem MFMA over the wave's half of the
-// (TY+2) x (TX+2) halo grid into its channel half's hidden image (out-of-map
-// cells = the dw zero padding); one barrier; dw + project partial (K = the
-// 16 channels) on the wave's half of the output pixels; the two channel
-// halves' partials are added in a fixed order through LDS.  Persistent: a
-// resident set of workgroups walks all tiles, the weights / normalisation
-// table are set up once per workgroup and the next tile's input bytes are in
-// flight while the current tile computes.
-template <int TY, int TX, int NW>
-__global__ void __launch_bounds__(64 * NW, 8 / NW) stem_ir1_f32_kernel(StemIr1F32Args a) {
-  constexpr int NT = 64 * NW, NPP = NW / 2;  // waves = 2 channel halves x NPP pixel parts
-  static_assert(NW % 2 == 0 && NT >= 256, "stem_ir1: waves");
-  constexpr int HY = TY + 2, HX = TX + 2, PIN = HY * HX;
-  constexpr int NBT = (PIN + 15) / 16, PINP = NBT * 16;
-  constexpr int IY = 2 * HY + 1, IX = 2 * HX + 1, PITCH = IX * 3;
-  constexpr int NPT = (TY * TX + 15) / 16, NPX = NPT * 16;
-  constexpr int XIN = (IY * PITCH + 3) / 4 * 4;  // floats, 16-B aligned end
-  constexpr int NIN = IY * PITCH, NIT = (NIN + NT - 1) / NT;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* xin = smem;                                       // [IY][PITCH] normalised input
-  float* lut = smem + XIN;                                 // [256] input table
-  f32x4_t* hidw = reinterpret_cast<f32x4_t*>(smem + XIN + 256);  // [2 channel halves][4 quads][PINP]
-  f32x4_t* dwo = hidw + 2 * 4 * PINP;                      // [2 channel halves][4 quads][NPX]
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int li = lane & 15, g = lane >> 4;
-  const int chalf = wave & 1, phalf = wave >> 1;  // wave = (16-channel half, pixel part)
-  const int tiles_img = a.tiles_x * a.tiles_y;
-  const int ntiles = tiles_img * a.B;
-
-  // ---- once per workgroup: input table, weights in registers.  The table is
-  // the pipeline's tensor_transform arithmetic (computed by the filter in the
-  // transform's own fp32 arithmetic), 256 entries.
-  if (tid < 256) lut[tid] = a.lut[tid];
-  float sa[7];  // stem weights of this wave's 16 channels: k = 4t + g (27 taps + 1 zero)
-  int off[7];
-#pragma unroll
-  for (int t = 0; t < 7; ++t) {
-    const int k = 4 * t + g;
-    sa[t] = k < 27 ? a.ws[k * 32 + chalf * 16 + li] : 0.f;
-    off[t] = k < 27 ? (k / 9) * PITCH + ((k % 9) / 3) * 3 + (k % 3) : 0;
-  }
-  const int ch = chalf * 16 + 4 * g;  // this lane's channel quad
-  const f32x4_t bs4 = *reinterpret_cast<const f32x4_t*>(a.bs + ch);
-  const f32x4_t bd4 = *reinterpret_cast<const f32x4_t*>(a.bd + ch);
-  f32x4_t wd4[9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) wd4[t] = *reinterpret_cast<const f32x4_t*>(a.wd + t * 32 + ch);
-  const f32x4_t pa = *reinterpret_cast<const f32x4_t*>(a.wp + li * 32 + ch);
-  const f32x4_t bp4 = *reinterpret_cast<const f32x4_t*>(a.bp + 4 * g);
-  f32x4_t* myhid = hidw + (chalf * 4 + g) * PINP;
-  f32x4_t* mydwo = dwo + (chalf * 4 + g) * NPX;
-  const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  // the raw bytes of a tile's input patch, -1 outside the frame (the stem's
-  // zero padding); every load of the patch is in flight at once
-  int raw[NIT];
-  auto fetch = [&](int tile) {
-    const int b = tile / tiles_img;
-    const int tyx = tile - b * tiles_img;
-    const int iy0 = 2 * ((tyx / a.tiles_x) * TY - 1) - 1, ix0 = 2 * ((tyx % a.tiles_x) * TX - 1) - 1;
-    const uint8_t* xb = a.x + static_cast<int64_t>(b) * a.H * a.W * 3;
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int i = tid + it * NT;
-      const int r = i / PITCH, c = i - r * PITCH;
-      const int iy = iy0 + r, ix = ix0 + c / 3;
-      raw[it] = (i < NIN && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
-                    ? static_cast<int>(xb[(static_cast<int64_t>(iy) * a.W + ix) * 3 + c % 3])
-                    : -1;
-    }
-  };
-
-  // persistent: the workgroup walks tiles blockIdx.x, + gridDim.x, ...; the
-  // next tile's patch loads overlap this tile's MFMA / depthwise work
-  int tile = blockIdx.x;
-  if (tile < ntiles) fetch(tile);
-  for (; tile < ntiles; tile += gridDim.x) {
-    const int b = tile / tiles_img;
-    const int tyx = tile - b * tiles_img;
-    const int oy0 = (tyx / a.tiles_x) * TY, ox0 = (tyx % a.tiles_x) * TX;
-    const int hy0 = oy0 - 1, hx0 = ox0 - 1;  // hidden halo origin (stem-output coords)
-    __syncthreads();  // previous tile done with xin / hidden / dwo (and lut written)
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int i = tid + it * NT;
-      if (i < NIN) xin[i] = raw[it] >= 0 ? lut[raw[it]] : 0.f;
-    }
-    if (tile + static_cast<int>(gridDim.x) < ntiles) fetch(tile + gridDim.x);
-    __syncthreads();
-
-    // ---- stem MFMA over this pixel part of the halo grid, two pixel tiles at a time
-    constexpr int NBH = (NBT + NPP - 1) / NPP;
-#pragma unroll
-    for (int jj = 0; jj < NBH; jj += 2) {
-      const int j = phalf * NBH + jj;
-      if (j >= NBT) break;
-      const int j1 = (jj + 1 < NBH && j + 1 < NBT) ? j + 1 : j;
-      const int c0 = j * 16 + li, c1 = j1 * 16 + li;
-      const int hy_0 = c0 / HX, hx_0 = c0 - hy_0 * HX, hy_1 = c1 / HX, hx_1 = c1 - hy_1 * HX;
-      const int base0 = c0 < PIN ? 2 * hy_0 * PITCH + 6 * hx_0 : 0;
-      const int base1 = c1 < PIN ? 2 * hy_1 * PITCH + 6 * hx_1 : 0;
-      f32x4_t e0 = z, e1 = z;
-#pragma unroll
-      for (int t = 0; t < 7; ++t) {
-        e0 = mfma4(sa[t], xin[base0 + off[t]], e0);
-        e1 = mfma4(sa[t], xin[base1 + off[t]], e1);
-      }
-      const bool in0 = c0 < PIN && hy0 + hy_0 >= 0 && hy0 + hy_0 < a.Ho && hx0 + hx_0 >= 0 && hx0 + hx_0 < a.Wo;
-      const bool in1 = c1 < PIN && hy0 + hy_1 >= 0 && hy0 + hy_1 < a.Ho && hx0 + hx_1 >= 0 && hx0 + hx_1 < a.Wo;
-      myhid[c0] = in0 ? relu6x4(e0 + bs4) : z;
-      if (j1 != j) myhid[c1] = in1 ? relu6x4(e1 + bs4) : z;
-    }
-    __syncthreads();  // all pixel parts of each channel half's hidden image
-    // ---- depthwise 3x3 + bias + ReLU6 on this wave's output pixel part
-    constexpr int NPH = (NPT + NPP - 1) / NPP;
-#pragma unroll
-    for (int pp = 0; pp < NPH; ++pp) {
-      const int pt = phalf * NPH + pp;
-      if (pt >= NPT) break;
-      const int q = pt * 16 + li;
-      const int qq = q < TY * TX ? q : 0;
-      const int cell = (qq / TX) * HX + (qq % TX);
-      f32x4_t d = bd4;
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx)
-          d = __builtin_elementwise_fma(myhid[cell + ky * HX + kx], wd4[ky * 3 + kx], d);
-      // ---- project partial over this wave's 16 channels (K = 16 of 32): the lane
-      // holding pixel q, channel quad g is the one that feeds that k-quad of
-      // column li to the MFMA, so the dw output goes straight in
-      mydwo[pt * 16 + li] = mfma_k16(pa, relu6x4(d), z);
-    }
-    __syncthreads();
-    // ---- channel half 0 + half 1 (fixed order), + bias -> [B][Ho][Wo][16]; the
-    // waves of channel half 0 store their pixel half
-    if (chalf == 0) {
-#pragma unroll
-      for (int pp = 0; pp < NPH; ++pp) {
-        const int pt = phalf * NPH + pp;
-        if (pt >= NPT) break;
-        const int q = pt * 16 + li;
-        if (q >= TY * TX) continue;
-        const int gy = oy0 + q / TX, gx = ox0 + q % TX;
-        if (gy >= a.Ho || gx >= a.Wo) continue;
-        const f32x4_t v = dwo[g * NPX + q] + dwo[(4 + g) * NPX + q] + bp4;
-        *reinterpret_cast<f32x4_t*>(a.y + ((static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx) * 16 + 4 * g) = v;
-      }
-    }
-  }
-}
-
 // ------------------------------------------------------- stem_ir1w_f32 ----
-// The same stem + block-1 fusion as stem_ir1_f32, one WAVE per tile: a
+// The stem (3x3/2 conv 3 -> 32 on the raw uint8 frame, mapped in-kernel
+// through the 256-entry input table, + bias, ReLU6) fused with MobileNetV2's
+// first block (t = 1: dw 3x3 on those 32 channels + ReLU6, project 32 -> 16):
+// the 32-channel stem output -- the largest activation of the network -- never
+// leaves LDS.  One WAVE per tile: a
 // workgroup is a single wave that owns a TY x TX output tile end to end --
 // both 16-channel halves of the stem over the (TY+2) x (TX+2) halo grid, the
 // depthwise 3x3 over all 32 channels and the whole K = 32 project -- so there
@@ -2070,184 +1937,6 @@ __global__ void __launch_bounds__(64, 2) stem_ir1w_f32_kernel(StemIr1F32Args a) 
           *reinterpret_cast<f32x4_t*>(a.y + ((static_cast<int64_t>(b) * a.Ho + gy) * a.Wo + gx) * 16 + 4 * g) =
               acc + bp4;
       }
-    }
-  }
-}
-
-// ----------------------------------------------------- stem_band_f32 ----
-// Stem + block 1 as a LINE BUFFER: one workgroup (4 waves) walks a band of BR
-// output rows of a column strip (<= 112 columns) of one image top to bottom.
-// Each stem output row is computed ONCE into a 4-slot LDS ring (32 channels x
-// the strip's cells + the dw's 1-cell horizontal halo); output row y then
-// runs the depthwise over ring rows y-1, y, y+1 and the K = 32 project.  The
-// tile kernels recompute the stem on every tile's halo -- 100 stem cells per 64
-// outputs at 8 x 8 (1.56x, plus 16-pixel padding: 1.75x of the stem MFMAs) --
-// here the only recompute is 2 stem rows per band (BR = 28: 1.07x) and, with
-// several strips, 2 columns per strip.
-// Per output row: (1) the input rows of the next stem row, prefetched into
-// registers during the previous row's depthwise, go through the 256-entry
-// table into LDS; barrier; (2) stem MFMA of that row into its ring slot
-// (units = 16-cell pixel tile x 16-channel half, dealt over the waves);
-// barrier; (3) depthwise + project of the output row (pixel tiles dealt over
-// the waves).  The slot written in (2) was last read two rows earlier, so two
-// barriers per row order everything.
-constexpr int kBandWS = 112;                    // strip width (output columns)
-constexpr int kBandCells = kBandWS + 2;         // ring cells per row (dw halo)
-constexpr int kBandPitch = (2 * kBandCells + 1) * 3;  // input floats per staged row
-struct StemBandGeom {
-  static constexpr size_t ring_q = static_cast<size_t>(4) * 8 * kBandCells;  // [slot][quad][cell] f32x4
-  static constexpr size_t xin_f = static_cast<size_t>(3) * kBandPitch;
-  static constexpr size_t bytes = 16 * ring_q + 4 * ((xin_f + 3) / 4 * 4 + 256);
-};
-
-__global__ void __launch_bounds__(256, 2) stem_band_f32_kernel(StemIr1F32Args a, int BR, int strips) {
-  constexpr int PITCH = kBandPitch, CELLS = kBandCells;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  f32x4_t* ring = reinterpret_cast<f32x4_t*>(smem);                 // [4][8][CELLS]
-  float* xin = smem + 4 * StemBandGeom::ring_q;                      // [3][PITCH]
-  float* lut = xin + (StemBandGeom::xin_f + 3) / 4 * 4;              // [256]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int li = lane & 15, g = lane >> 4;
-  const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  // ---- which band / strip
-  const int nbands = (a.Ho + BR - 1) / BR;
-  int w = blockIdx.x;
-  const int strip = w % strips;
-  w /= strips;
-  const int band = w % nbands;
-  const int b = w / nbands;
-  const int y0 = band * BR, y1 = min(a.Ho, y0 + BR);
-  const int x0 = strip * kBandWS, ws = min(kBandWS, a.Wo - x0);
-  // ring cell j <-> stem column x0 - 1 + j; in-image cells [clo, chi)
-  const int clo = x0 == 0 ? 1 : 0, chi = min(ws + 2, a.Wo - x0 + 1);
-  const int nunits = 2 * ((chi - clo + 15) / 16);  // (16-cell tile, channel half)
-
-  for (int i = tid; i < 256; i += 256) lut[i] = a.lut[i];
-  // out-of-image ring cells (the dw's zero padding) are zero for every row
-  for (int v = tid; v < 4 * 8 * CELLS; v += 256) {
-    const int j = v % CELLS;
-    if (j < clo || j >= chi) ring[v] = z;
-  }
-
-  // stem weights (A: row li = channel 16h + li, k = 4t + g over the 27 taps + 1 zero)
-  float sa[2][7];
-  int off[7];
-#pragma unroll
-  for (int t = 0; t < 7; ++t) {
-    const int k = 4 * t + g;
-    sa[0][t] = k < 27 ? a.ws[k * 32 + li] : 0.f;
-    sa[1][t] = k < 27 ? a.ws[k * 32 + 16 + li] : 0.f;
-    off[t] = k < 27 ? (k / 9) * PITCH + ((k % 9) / 3) * 3 + (k % 3) : 0;
-  }
-  f32x4_t bs4[2], bd4[2], pa[2], wd4[2][9];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int ch = 16 * h + 4 * g;
-    bs4[h] = *reinterpret_cast<const f32x4_t*>(a.bs + ch);
-    bd4[h] = *reinterpret_cast<const f32x4_t*>(a.bd + ch);
-    pa[h] = *reinterpret_cast<const f32x4_t*>(a.wp + li * 32 + ch);
-#pragma unroll
-    for (int t = 0; t < 9; ++t) wd4[h][t] = *reinterpret_cast<const f32x4_t*>(a.wd + t * 32 + ch);
-  }
-  const f32x4_t bp4 = *reinterpret_cast<const f32x4_t*>(a.bp + 4 * g);
-
-  // input staging: stem row r reads input rows 2r-1 .. 2r+1, columns
-  // 2(x0-1)-1 .. (2(ws+2)+1 columns); byte v of the 3 x PITCH patch
-  const int rowb = a.W * 3;
-  const uint8_t* img = a.x + static_cast<int64_t>(b) * a.H * rowb;
-  const int col0 = (2 * (x0 - 1) - 1) * 3;
-  constexpr int NV = (3 * PITCH + 255) / 256;
-  int raw[NV];
-  auto fetch = [&](int r) {  // raw bytes (-1: outside the image = zero padding)
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int v = tid + i * 256;
-      const int ry = v / PITCH, rc = v - ry * PITCH;
-      const int iy = 2 * r - 1 + ry, ib = col0 + rc;
-      const bool ok = v < 3 * PITCH && r >= 0 && r < a.Ho && iy >= 0 && iy < a.H && ib >= 0 && ib < rowb;
-      const uint8_t byte = img[ok ? static_cast<int64_t>(iy) * rowb + ib : 0];
-      raw[i] = ok ? static_cast<int>(byte) : -1;
-    }
-  };
-  __syncthreads();  // lut, zeroed halo cells
-
-  // ---- prologue: stem rows y0 - 1 and y0 into their ring slots
-  auto stem_row = [&](int r) {  // input in xin -> ring slot r & 3 (zeros outside the map)
-    f32x4_t* slot = ring + (r & 3) * 8 * CELLS;
-    if (r < 0 || r >= a.Ho) {
-      for (int v = tid; v < 8 * CELLS; v += 256) slot[v] = z;
-      return;
-    }
-    for (int u = wave; u < nunits; u += 8) {
-      // two units per pass (u, u + 4): two independent MFMA chains
-      const int u1 = u + 4;
-      const bool two = u1 < nunits;
-      const int c0 = clo + (u >> 1) * 16 + li, h0 = u & 1;
-      const int c1 = clo + (u1 >> 1) * 16 + li, h1 = u1 & 1;
-      const int bb0 = 6 * (c0 < chi ? c0 : clo), bb1 = 6 * (two && c1 < chi ? c1 : clo);
-      f32x4_t e0 = z, e1 = z;
-#pragma unroll
-      for (int t = 0; t < 7; ++t) {
-        e0 = mfma4(h0 ? sa[1][t] : sa[0][t], xin[bb0 + off[t]], e0);
-        if (two) e1 = mfma4(h1 ? sa[1][t] : sa[0][t], xin[bb1 + off[t]], e1);
-      }
-      if (c0 < chi) slot[(4 * h0 + g) * CELLS + c0] = relu6x4(e0 + bs4[h0]);
-      if (two && c1 < chi) slot[(4 * h1 + g) * CELLS + c1] = relu6x4(e1 + bs4[h1]);
-    }
-  };
-  auto stage = [&]() {  // raw -> xin through the table
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int v = tid + i * 256;
-      if (v < 3 * PITCH) xin[v] = raw[i] >= 0 ? lut[raw[i]] : 0.f;
-    }
-  };
-  fetch(y0 - 1);
-  stage();
-  fetch(y0);
-  __syncthreads();
-  stem_row(y0 - 1);
-  __syncthreads();
-  stage();
-  fetch(y0 + 1);
-  __syncthreads();
-  stem_row(y0);
-  __syncthreads();  // xin free (stem row y0 done by every wave)
-
-  const int npt = (ws + 15) / 16;
-  for (int y = y0; y < y1; ++y) {
-    // (1) next stem row's input (fetched during the previous row) -> xin; the
-    // barrier before the previous row's depthwise ordered every read of xin
-    stage();
-    if (y + 2 <= y1) fetch(y + 2);  // (the row after: in flight during this row)
-    __syncthreads();
-    // (2) stem row y + 1
-    stem_row(y + 1);
-    __syncthreads();  // ring rows y-1 .. y+1 complete
-    // (3) depthwise + project of output row y
-    const f32x4_t* r0 = ring + ((y - 1) & 3) * 8 * CELLS;
-    const f32x4_t* r1 = ring + (y & 3) * 8 * CELLS;
-    const f32x4_t* r2 = ring + ((y + 1) & 3) * 8 * CELLS;
-    for (int pt = wave; pt < npt; pt += 4) {
-      const int x = pt * 16 + li;  // strip-relative output column; cells x, x+1, x+2
-      const int xx = x < ws ? x : 0;
-      f32x4_t acc = z;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int q = (4 * h + g) * CELLS + xx;
-        f32x4_t d = bd4[h];
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          d = __builtin_elementwise_fma(r0[q + kx], wd4[h][kx], d);
-          d = __builtin_elementwise_fma(r1[q + kx], wd4[h][3 + kx], d);
-          d = __builtin_elementwise_fma(r2[q + kx], wd4[h][6 + kx], d);
-        }
-        acc = mfma_k16(pa[h], relu6x4(d), acc);
-      }
-      if (x < ws)
-        *reinterpret_cast<f32x4_t*>(a.y + ((static_cast<int64_t>(b) * a.Ho + y) * a.Wo + x0 + x) * 16 + 4 * g) =
-            acc + bp4;
     }
   }
 }
@@ -2453,16 +2142,8 @@ bool irw_skipped(size_t i) {
   return std::find(skip.begin(), skip.end(), i) != skip.end();
 }
 
-bool irw_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("NNSX_F32_IRW");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 const IrwCfg* find_irw(int S, int H, int W, int cin, int hid, int cout, bool has_expand, int dil = 1, int B = 0) {
-  if (!irw_enabled() || !has_expand || hid % 16) return nullptr;
+  if (!has_expand || hid % 16) return nullptr;
   const int kin = (cin + 7) / 8 * 8;
   const int nout = (cout + 15) / 16;
   const int Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
@@ -2479,7 +2160,7 @@ const IrwCfg* find_irw(int S, int H, int W, int cin, int hid, int cout, bool has
 }
 
 const IrwCfg* find_irw_dw(int S, int H, int W, int cin, int hid, int dil = 1) {
-  if (!irw_enabled() || hid % 16) return nullptr;
+  if (hid % 16) return nullptr;
   const int kin = (cin + 7) / 8 * 8;
   const int Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
   for (int exact = 1; exact >= 0; --exact)
@@ -2528,11 +2209,7 @@ const char* f32_math_name(F32Math m) { return m == F32Math::kX3 ? "x3" : "fp32";
 // tiles of 64 x 64) -- otherwise most CUs idle while each workgroup walks all
 // of K.  Returns the k-stages per slice (kstages: no split).
 static int gemm_kchunk(int tiles, int kstages, int N, bool plain) {
-  static const bool splitk = [] {
-    const char* e = std::getenv("NNSX_F32_SPLITK");
-    return !(e && e[0] == '0');
-  }();
-  if (!splitk || !plain || tiles >= 128 || kstages < 8 || N % 4) return kstages;
+  if (!plain || tiles >= 128 || kstages < 8 || N % 4) return kstages;
   const int splits = std::min(kstages / 4, (512 + tiles - 1) / tiles);
   return (kstages + splits - 1) / splits;
 }
@@ -2609,28 +2286,18 @@ static int pick_gemm_tile(int M, int N, int Kpad) {
   return cand[best][0] * 1000 + cand[best][1];
 }
 
-static int resolve_tile(int M, int N, int Kpad, int tile) {
-  if (tile > 0) return tile;
-  static const int forced = [] {
-    const char* e = std::getenv("NNSX_F32_GEMM_TILE");
-    return e ? std::atoi(e) : 0;
-  }();
-  return forced > 0 ? forced : pick_gemm_tile(M, N, Kpad);
-}
+// (tile > 0: an instantiated tile asked for by the caller -- pw_conv_f32_tile, A/B tools)
+static int resolve_tile(int M, int N, int Kpad, int tile) { return tile > 0 ? tile : pick_gemm_tile(M, N, Kpad); }
 
 // small-M GEMMs (batch-1 projects / head / classifier) run pw_small_f32: one
-// launch instead of a split-K GEMM + reduce (NNSX_F32_SMALLM=0 turns it off)
+// launch instead of a split-K GEMM + reduce
 static bool use_small_m(int M, int K, int tile, const YLayout& yl) {
-  static const bool on = [] {
-    const char* e = std::getenv("NNSX_F32_SMALLM");
-    return !(e && e[0] == '0');
-  }();
   // (a workgroup streams its rows' whole K range through one CU: at M = 49,
   // K = 960 -- the batch-1 7x7 project -- that took 16.7 us against 12 us for
   // the split-K GEMM + reduce, so the many-row deep-K shapes keep split-K;
   // a two-workgroup K split with order-free atomics needed a memset node
   // that cost more than it saved: profiles/r3b_b1_forward_trace.txt)
-  return on && tile == 0 && M <= 64 && (M <= 16 || K <= 512) && !yl.rpb && !yl.brpb && !yl.pool;
+  return tile == 0 && M <= 64 && (M <= 16 || K <= 512) && !yl.rpb && !yl.brpb && !yl.pool;
 }
 
 size_t pw_gemm_f32_workspace_bytes(int M, int N, int Kpad, bool has_res, int tile) {
@@ -2648,16 +2315,6 @@ size_t pw_gemm_f32_workspace_bytes(int M, int N, int Kpad, bool has_res, int til
 
 void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
                  int Kpad, int Npad, int act, hipStream_t s, int tile, float* ws, const YLayout& yl) {
-  // plain linear products (no activation: the projects) with a deep enough K
-  // and enough rows: the library GEMM (blaslt.cc), the residual as its C
-  // operand.  (Its bias + clamp epilogue returned the bare product on this
-  // ROCm: scripts/blaslt_probe.py -- the ReLU6 GEMMs stay on the engine's kernel.)
-  // (M <= 65536: the range measured in the pipelines -- MobileNetV2 / SSD /
-  // DeepLab up to 35k rows; a PoseNet run with 270k-row products on it hung the
-  // device, so larger products stay on the engine's kernel)
-  if (tile == 0 && blaslt_enabled() && !yl.rpb && !yl.brpb && !yl.pool && K >= 128 && M >= 2048 && M <= 65536 &&
-      N >= 64 && act == 0 && blaslt_gemm_f32(x, wt, bias, res, y, M, N, K, Kpad, act, s))
-    return;
   if (use_small_m(M, Kpad, tile, yl)) {
     const dim3 grid(static_cast<unsigned>((N + 15) / 16), static_cast<unsigned>((M + 63) / 64));
     hipLaunchKernelGGL(pw_small_f32_kernel<false>, grid, dim3(256), 0, s, x, wt, bias, res, y, M, N, K, Kpad, Npad, act, 0);
@@ -2711,80 +2368,41 @@ void dw3x3_f32_group(const DwProb* p, int n, hipStream_t s) {
 void dw3x3_f32(const float* x, const float* w, const float* bias, float* y, int B, int H, int W, int C, int stride,
                int dil, int act, hipStream_t s) {
   const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
-  static const int rows = [] {
-    const char* e = std::getenv("NNSX_F32_DW_ROWS");
-    return e ? std::atoi(e) : 4;
-  }();
-  // rows x columns per lane, R * 10 + CW (NNSX_F32_DW_S1 / NNSX_F32_DW_S2; 0 = the
-  // one-column form below).  Measured (scripts/dw_roofline.py, profiles/r4_dw_lane_shapes.txt):
-  // stride 1 4 x 4 -- 7x7x960 at batch 512 56.3 -> 39.4 us, 14x14x576 130.6 -> 96.2 us,
-  // PoseNet's 17x17x512 21.2 -> 18.7 us; stride 2 2 x 2 -- 129 -> 65 x 64 66.3 -> 60.9 us
-  static const int cfg1 = [] {
-    const char* e = std::getenv("NNSX_F32_DW_S1");
-    return e ? std::atoi(e) : 44;
-  }();
-  static const int cfg2 = [] {
-    const char* e = std::getenv("NNSX_F32_DW_S2");
-    return e ? std::atoi(e) : 22;
-  }();
-  // (the multi-pixel lanes only where they still give every CU a workgroup
+  // Lane shapes (rows x columns of outputs per lane), measured with
+  // scripts/dw_roofline.py (profiles/r4_dw_lane_shapes.txt): stride 1 4 x 4 --
+  // 7x7x960 at batch 512 56.3 -> 39.4 us, 14x14x576 130.6 -> 96.2 us, PoseNet's
+  // 17x17x512 21.2 -> 18.7 us; stride 2 2 x 2 -- 129 -> 65 x 64 66.3 -> 60.9 us;
+  // dilation 2 4 x 4 over the dilated window (8 x 8 loads for 16 outputs).
+  // The multi-pixel lanes only where they still give every CU a workgroup
   // (>= 256 x 256 lanes): at batch 1 their few long lanes leave most CUs idle --
-  // PoseNet batch-1 p50 0.36 -> 0.38 ms, DeepLab 0.525 -> 0.543 ms)
-  auto lanes = [&](int cf) {
-    return cf / 10 < 1 || cf % 10 < 1 ? int64_t{0}
-                   : static_cast<int64_t>(B) * ((Ho + cf / 10 - 1) / (cf / 10)) * ((Wo + cf % 10 - 1) / (cf % 10)) * (C / 4);
-  };
-  const bool big = lanes(stride == 1 ? cfg1 : cfg2) >= 65536;
-  const int cfg = !big ? 0 : stride == 1 ? cfg1 : cfg2;
-  static const bool dil_col = [] {
-    const char* e = std::getenv("NNSX_F32_DW_DIL_COL");
-    return !(e && e[0] == '0');
-  }();
-  if (dil_col && big && cfg1 > 0 && stride == 1 && dil == 2) {
-    // dilation-2 stride-1 maps (DeepLab's output-stride-16 blocks): 4 x 4 output
-    // lanes over the dilated window, 8 x 8 loads for 16 outputs instead of 144
-    // (dilation 4 would share nothing across a 4 x 4 lane: the one-pixel form)
+  // PoseNet batch-1 p50 0.36 -> 0.38 ms, DeepLab 0.525 -> 0.543 ms.
+  constexpr int rows = 4;
+  const int R2 = stride == 1 ? 4 : 2, C2 = stride == 1 ? 4 : 2;
+  const int64_t lanes = static_cast<int64_t>(B) * ((Ho + R2 - 1) / R2) * ((Wo + C2 - 1) / C2) * (C / 4);
+  const bool big = lanes >= 65536;
+  if (big && stride == 1 && dil == 2) {
     const int64_t work = static_cast<int64_t>(B) * ((Ho + 3) / 4) * ((Wo + 3) / 4) * (C / 4);
     const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 65535))));
     hipLaunchKernelGGL((dw3x3_f32_col_kernel<4, 1, 4, 2>), grid, dim3(256), 0, s, x, w, bias, y, B, H, W, C, Ho, Wo, act);
     return;
   }
-  if (dil == 1 && cfg > 0) {
-    const int R = cfg / 10, CW = cfg % 10;
-    const int64_t work = static_cast<int64_t>(B) * ((Ho + R - 1) / R) * ((Wo + CW - 1) / CW) * (C / 4);
-    const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 65535))));
-#define NNSX_DWC(RR, SS, CC)                                                                                   \
-  case RR * 100 + SS * 10 + CC:                                                                                \
-    hipLaunchKernelGGL((dw3x3_f32_col_kernel<RR, SS, CC>), grid, dim3(256), 0, s, x, w, bias, y, B, H, W, C, Ho, \
-                       Wo, act);                                                                               \
-    return;
-    switch (R * 100 + stride * 10 + CW) {
-      NNSX_DWC(4, 1, 2)
-      NNSX_DWC(4, 1, 4)
-      NNSX_DWC(8, 1, 1)
-      NNSX_DWC(8, 1, 2)
-      NNSX_DWC(2, 1, 2)
-      NNSX_DWC(2, 1, 4)
-      NNSX_DWC(2, 2, 2)
-      NNSX_DWC(1, 2, 2)
-      NNSX_DWC(1, 2, 4)
-      NNSX_DWC(4, 2, 2)
-      default: break;
-    }
-#undef NNSX_DWC
-  }
-  if (dil == 1 && rows > 1) {
-    const int R = rows >= 4 ? 4 : 2;
-    const int64_t work = static_cast<int64_t>(B) * ((Ho + R - 1) / R) * Wo * (C / 4);
-    const unsigned grid = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 65535)));
-    if (R == 4 && stride == 1)
-      hipLaunchKernelGGL((dw3x3_f32_col_kernel<4, 1>), dim3(grid), dim3(256), 0, s, x, w, bias, y, B, H, W, C, Ho, Wo, act);
-    else if (R == 4)
-      hipLaunchKernelGGL((dw3x3_f32_col_kernel<4, 2>), dim3(grid), dim3(256), 0, s, x, w, bias, y, B, H, W, C, Ho, Wo, act);
-    else if (stride == 1)
-      hipLaunchKernelGGL((dw3x3_f32_col_kernel<2, 1>), dim3(grid), dim3(256), 0, s, x, w, bias, y, B, H, W, C, Ho, Wo, act);
+  if (big && dil == 1) {
+    const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((lanes + 255) / 256, 65535))));
+    if (stride == 1)
+      hipLaunchKernelGGL((dw3x3_f32_col_kernel<4, 1, 4>), grid, dim3(256), 0, s, x, w, bias, y, B, H, W, C, Ho, Wo, act);
     else
-      hipLaunchKernelGGL((dw3x3_f32_col_kernel<2, 2>), dim3(grid), dim3(256), 0, s, x, w, bias, y, B, H, W, C, Ho, Wo, act);
+      hipLaunchKernelGGL((dw3x3_f32_col_kernel<2, 2, 2>), grid, dim3(256), 0, s, x, w, bias, y, B, H, W, C, Ho, Wo, act);
+    return;
+  }
+  if (dil == 1) {  // (small grids: 4 rows per lane)
+    const int64_t work = static_cast<int64_t>(B) * ((Ho + rows - 1) / rows) * Wo * (C / 4);
+    const unsigned grid = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 65535)));
+    if (stride == 1)
+      hipLaunchKernelGGL((dw3x3_f32_col_kernel<rows, 1>), dim3(grid), dim3(256), 0, s, x, w, bias, y, B, H, W, C, Ho, Wo,
+                         act);
+    else
+      hipLaunchKernelGGL((dw3x3_f32_col_kernel<rows, 2>), dim3(grid), dim3(256), 0, s, x, w, bias, y, B, H, W, C, Ho, Wo,
+                         act);
     return;
   }
   const int64_t work = static_cast<int64_t>(B) * Ho * Wo * (C / 4);
@@ -2844,11 +2462,6 @@ void avgpool_f32(const float* x, float* y, int B, int HW, int C, hipStream_t s) 
 
 bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout, bool has_expand, int dil) {
   if (stride != 1 && stride != 2) return false;
-  static const int min_ho = [] {
-    const char* e = std::getenv("NNSX_F32_IR_MIN_HO");
-    return e ? std::atoi(e) : 0;
-  }();
-  if ((H - 1) / stride + 1 < min_ho) return false;
   if (cin % 8 || cout % 4 || hid % 16) return false;
   if (dil != 1) return find_irw(stride, H, W, cin, hid, cout, has_expand, dil) != nullptr;
   return find_irw(stride, H, W, cin, hid, cout, has_expand) != nullptr ||
@@ -2858,7 +2471,7 @@ bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout
 // Hidden-channel parts per tile.  Fewer tiles than CUs: split the hidden
 // channels over workgroups (every wave keeps >= 1 subtile).  The parts write
 // workspace slabs that irw_reduce adds in part order.  (Adding two parts into a
-// zeroed output with fp32 atomics, NNSX_F32_IRW_ATOMIC2=1, is also
+// zeroed output with fp32 atomics was also
 // deterministic but measured 86 vs 71 us on the 7x7 960-hidden block at batch
 // 128: the L2 atomic unit, 4 B per request, is the bottleneck.)
 static int irw_env(const char* name, int dflt) {
@@ -2866,12 +2479,9 @@ static int irw_env(const char* name, int dflt) {
   return e ? std::atoi(e) : dflt;
 }
 
-// two hidden parts: add into a zeroed output with fp32 atomics (1) or write
-// workspace slabs + irw_reduce like more parts (0)
-static bool irw_atomic2() {
-  static const bool on = irw_env("NNSX_F32_IRW_ATOMIC2", 0) != 0;
-  return on;
-}
+// two hidden parts write workspace slabs like more parts (adding them into a
+// zeroed output with fp32 atomics measured slower, above)
+static bool irw_atomic2() { return false; }
 
 // NNSX_F32_IRW_INLAUNCH: 0 = irw_reduce launch, 1 = last-arriver combine,
 // 2 = spread combine (default: every part waits for its tile's other parts,
@@ -2915,9 +2525,7 @@ static int irw_parts(const IrwCfg* c, int tiles, int hid) {
   const int nsub = hid / 16;
   if (c->NOT == 0)  // depthwise output: parts need no reduction, so fill the chip
     return std::max(1, std::min((1024 + tiles - 1) / tiles, nsub / c->NW));
-  static const int forced = irw_env("NNSX_F32_IRW_PARTS", 0);  // (tuning: blocks that split at all)
   if (tiles >= 256 || nsub < 8) return 1;
-  if (forced > 0) return std::min(forced, std::max(1, nsub / c->NW));
   if (tiles >= 128) return 2;
   const int want = (512 + tiles - 1) / tiles;
   int parts = std::max(2, std::min(want, nsub / c->NW));
@@ -3049,15 +2657,7 @@ size_t ir_block_f32_tickets(const IrBlockF32Args& args) {
   return a.tiles_x * a.tiles_y * a.B <= kLastTickets ? kSpreadTickets + kLastTickets : 0;
 }
 
-size_t stem_ir1_lds_bytes() {
-  constexpr int TY = kStemIr1TY, TX = kStemIr1TX;
-  constexpr int HY = TY + 2, HX = TX + 2, PIN = HY * HX, PINP = (PIN + 15) / 16 * 16;
-  constexpr int IY = 2 * HY + 1, PITCH = (2 * HX + 1) * 3;
-  constexpr int NPX = (TY * TX + 15) / 16 * 16;
-  return static_cast<size_t>((IY * PITCH + 3) / 4 * 4 + 256) * 4 + 16 * (8 * PINP + 8 * NPX);
-}
-
-// one-wave-per-tile variant (stem_ir1w_f32_kernel): 8 x 8 tiles
+// one wave per 8 x 8 tile (stem_ir1w_f32_kernel)
 constexpr int kStemW = 8;
 static size_t stem_ir1w_lds_bytes() {
   constexpr int HY = kStemW + 2, HX = kStemW + 2, PIN = HY * HX;
@@ -3065,13 +2665,19 @@ static size_t stem_ir1w_lds_bytes() {
   return static_cast<size_t>((NIN + 3) / 4 * 4 + 256) * 4 + 16 * 8 * PIN;
 }
 
-static bool stem_ir1w_f32(StemIr1F32Args a, hipStream_t s) {
+// (variants measured and removed: the 8-wave 16 x 16 tile kernel -- 510-525 us
+// against 492-514 at batch 512, profiles/r2_pmc_stem_ir1.txt -- and the
+// line-buffer band kernel -- 552.6 vs 471.0 us, barrier-bound,
+// profiles/r4_fp32_layers_b512_final.txt)
+bool stem_ir1_f32(const StemIr1F32Args& args, hipStream_t s) {
+  StemIr1F32Args a = args;
+  a.Ho = (a.H - 1) / 2 + 1;
+  a.Wo = (a.W - 1) / 2 + 1;
   a.tiles_y = (a.Ho + kStemW - 1) / kStemW;
   a.tiles_x = (a.Wo + kStemW - 1) / kStemW;
   const size_t lds = stem_ir1w_lds_bytes();
-  static const bool pair = irw_env("NNSX_STEM_WAVE", 2) == 2;
-  const void* fn = pair ? reinterpret_cast<const void*>(&stem_ir1w_f32_kernel<kStemW, kStemW, true>)
-                        : reinterpret_cast<const void*>(&stem_ir1w_f32_kernel<kStemW, kStemW, false>);
+  const void* fn = reinterpret_cast<const void*>(&stem_ir1w_f32_kernel<kStemW, kStemW, true>);
+  // persistent grid: exactly the waves that fit resident at once
   static const int resident = [fn, lds] {
     int dev = 0, ncu = 256, per_cu = 1;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
@@ -3080,73 +2686,7 @@ static bool stem_ir1w_f32(StemIr1F32Args a, hipStream_t s) {
   }();
   const int tiles = a.tiles_x * a.tiles_y * a.B;
   const unsigned grid = static_cast<unsigned>(std::min(tiles, resident));
-  if (pair)
-    hipLaunchKernelGGL((stem_ir1w_f32_kernel<kStemW, kStemW, true>), dim3(grid), dim3(64), lds, s, a);
-  else
-    hipLaunchKernelGGL((stem_ir1w_f32_kernel<kStemW, kStemW, false>), dim3(grid), dim3(64), lds, s, a);
-  return true;
-}
-
-// line-buffer stem (stem_band_f32_kernel): bands of BR rows, strips of <= 112
-// columns; chosen when the grid stays large (>= 1024 workgroups at BR >= 14)
-static bool stem_band_f32(StemIr1F32Args a, hipStream_t s) {
-  a.Ho = (a.H - 1) / 2 + 1;
-  a.Wo = (a.W - 1) / 2 + 1;
-  const int strips = (a.Wo + kBandWS - 1) / kBandWS;
-  // the tallest band that keeps >= 1024 workgroups (2 resident per CU x 256 CUs x 2
-  // rounds), 14 .. 28 rows
-  int BR = 28;
-  while (BR > 14 && static_cast<int64_t>(a.B) * strips * ((a.Ho + BR - 1) / BR) < 1024) BR -= 2;
-  const int64_t wgs = static_cast<int64_t>(a.B) * strips * ((a.Ho + BR - 1) / BR);
-  const size_t lds = StemBandGeom::bytes;
-  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_band_f32_kernel),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
-  if (!attr || lds > 160 * 1024 || wgs <= 0 || wgs > (1ll << 31)) return false;
-  hipLaunchKernelGGL(stem_band_f32_kernel, dim3(static_cast<unsigned>(wgs)), dim3(256), lds, s, a, BR, strips);
-  return true;
-}
-
-bool stem_ir1_f32(const StemIr1F32Args& args, hipStream_t s) {
-  StemIr1F32Args a = args;
-  // NNSX_STEM_WAVE=3: the line-buffer band kernel whenever the batch gives it a
-  // large grid (B >= 16 at 224 x 224); small batches keep the tile kernel
-  static const int env_mode = irw_env("NNSX_STEM_WAVE", 2);
-  if (a.mode == 3) return stem_band_f32(a, s);  // (forced: tests)
-  if (a.mode < 0 && env_mode == 3 && a.B >= 16 && stem_band_f32(a, s)) return true;
-  // one wave per 8 x 8 tile with paired-row depthwise (default, 2), the same
-  // without the row pairing (1), or the 8-wave 16 x 16 tile kernel (0).
-  // Batch 512 on one box: 525 / 514 / 510 us for 0 / 1 / 2 (another box: 520 vs
-  // 492 us for 0 vs 1); PMC (profiles/r2_pmc_stem_ir1.txt): wait cycles 39 -> 31 %
-  static const bool wave_tiles = irw_env("NNSX_STEM_WAVE", 2) != 0;
-  if (wave_tiles) {
-    a.Ho = (a.H - 1) / 2 + 1;
-    a.Wo = (a.W - 1) / 2 + 1;
-    return stem_ir1w_f32(a, s);
-  }
-  a.Ho = (a.H - 1) / 2 + 1;
-  a.Wo = (a.W - 1) / 2 + 1;
-  a.tiles_y = (a.Ho + kStemIr1TY - 1) / kStemIr1TY;
-  a.tiles_x = (a.Wo + kStemIr1TX - 1) / kStemIr1TX;
-  const size_t lds = stem_ir1_lds_bytes();
-  if (lds > 160 * 1024) return false;
-  const void* fn = reinterpret_cast<const void*>(&stem_ir1_f32_kernel<kStemIr1TY, kStemIr1TX, kStemIr1NW>);
-  if (lds > 64 * 1024 &&
-      hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-    return false;
-  // persistent grid: exactly the workgroups that fit resident at once (LDS and
-  // registers decide; a workgroup that has to wait for a slot would serialise
-  // its whole tile loop behind the others)
-  static const int resident = [fn, lds] {
-    int dev = 0, ncu = 256, per_cu = 1;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * kStemIr1NW, lds) != hipSuccess || per_cu < 1)
-      per_cu = 1;
-    return ncu * per_cu;
-  }();
-  const int tiles = a.tiles_x * a.tiles_y * a.B;
-  const unsigned grid = static_cast<unsigned>(std::min(tiles, resident));
-  hipLaunchKernelGGL((stem_ir1_f32_kernel<kStemIr1TY, kStemIr1TX, kStemIr1NW>), dim3(grid), dim3(64 * kStemIr1NW), lds,
-                     s, a);
+  hipLaunchKernelGGL((stem_ir1w_f32_kernel<kStemW, kStemW, true>), dim3(grid), dim3(64), lds, s, a);
   return true;
 }
 

@@ -18,7 +18,7 @@
 #include <algorithm>
 #include <cstdint>
 
-#include "kernels/dtype.cuh"
+#include "kernels/dtype.h"
 #include "kernels/kernels.h"
 #include "runtime/hip_util.h"
 

@@ -18,7 +18,7 @@
 #include <stdexcept>
 #include <type_traits>
 
-#include "kernels/dtype.cuh"
+#include "kernels/dtype.h"
 #include "kernels/kernels.h"
 
 namespace nnsx {

@@ -136,9 +136,9 @@ at::Tensor dw_conv_cpu(const at::Tensor& x, const at::Tensor& w, const at::Tenso
 // (1), its rows following the previous head's of the same output.
 // mode 0: two grouped launches -- every head's depthwise into a scratch map
 // (kernels::dw3x3_f32_group), then every predictor GEMM
-// (kernels::pw_gemm_f32_group); mode 1: one launch with the depthwise in the
-// GEMM's operand staging (recomputed per output-column tile: slower,
-// profiles/r4_dwpw_ab.txt).
+// (kernels::pw_gemm_f32_group).  (The one-launch form with the depthwise in
+// the GEMM's operand staging measured slower and was removed:
+// profiles/r4_dwpw_ab.txt.)
 void sep_heads_cuda(at::TensorList xs, at::TensorList wds, at::TensorList bds, at::TensorList wts,
                     at::TensorList biases, at::IntArrayRef ns, at::IntArrayRef which, at::Tensor& out_box,
                     at::Tensor& out_cls, int64_t mode) {
@@ -180,11 +180,7 @@ void sep_heads_cuda(at::TensorList xs, at::TensorList wds, at::TensorList bds, a
     h.Npad = static_cast<int>(wts[i].size(0));
     rows[which[i] ? 1 : 0] = r0 + HW * (N / C);
   }
-  if (mode == 1) {
-    nnsx::kernels::sep_heads_f32(a, cur_stream());
-    return;
-  }
-  TORCH_CHECK(mode == 0, "sep_heads: mode 0 (grouped depthwise + grouped GEMM) or 1 (one launch)");
+  TORCH_CHECK(mode == 0, "sep_heads: mode 0 (grouped depthwise + grouped GEMM)");
   int64_t total = 0;
   for (size_t i = 0; i < n; ++i) total += xs[i].numel();
   at::Tensor hid = at::empty({total}, xs[0].options());
@@ -297,77 +293,6 @@ void sep_heads_cpu(at::TensorList xs, at::TensorList wds, at::TensorList bds, at
   }
 }
 
-// Depthwise-separable pairs as one GEMM each, several problems per launch
-// (kernels::dwpw_f32): out[i] = act(pw_i(relu6(dw3x3_{s_i}(x_i) + bd_i))),
-// NHWC [B, Ho, Wo, ns[i]] (exact columns).  wds[i] undefined: no depthwise.
-std::vector<at::Tensor> dwpw_cuda(at::TensorList xs, const c10::List<c10::optional<at::Tensor>>& wds,
-                                  const c10::List<c10::optional<at::Tensor>>& bds, at::TensorList wts,
-                                  at::TensorList biases, at::IntArrayRef ns, at::IntArrayRef strides, int64_t act,
-                                  int64_t dilation, const c10::optional<at::Tensor>& res) {
-  const size_t n = xs.size();
-  TORCH_CHECK(n > 0 && n <= static_cast<size_t>(nnsx::kernels::kSepHeadsMax) && wds.size() == n && bds.size() == n &&
-                  wts.size() == n && biases.size() == n && ns.size() == n && strides.size() == n,
-              "dwpw: 1..16 problems, one entry of every list per problem");
-  nnsx::kernels::SepHeadsArgs a;
-  a.n = static_cast<int>(n);
-  std::vector<at::Tensor> outs;
-  for (size_t i = 0; i < n; ++i) {
-    const at::Tensor& x = xs[i];
-    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 4,
-                "dwpw: x [B,H,W,K] f32 contiguous");
-    const int64_t K = x.size(3), N = ns[i], S = strides[i];
-    const c10::optional<at::Tensor> wd = wds.get(i), bd = bds.get(i);
-    const bool has_dw = wd.has_value() && wd->defined();
-    TORCH_CHECK(!has_dw || (wd->numel() == 9 * K && bd.has_value() && bd->numel() >= K), "dwpw: depthwise [9,K]");
-    TORCH_CHECK(wts[i].dim() == 2 && wts[i].size(1) >= K && wts[i].size(0) >= (N + 3) / 4 * 4 &&
-                    biases[i].numel() >= (N + 3) / 4 * 4 && (S == 1 || S == 2) && (has_dw || S == 1),
-                "dwpw: weights / stride");
-    const int64_t Ho = (x.size(1) - 1) / S + 1, Wo = (x.size(2) - 1) / S + 1;
-    at::Tensor y = at::empty({x.size(0), Ho, Wo, N}, x.options());
-    auto& h = a.h[i];
-    h.x = x.data_ptr<float>();
-    h.wd = has_dw ? wd->data_ptr<float>() : nullptr;
-    h.bd = has_dw ? bd->data_ptr<float>() : nullptr;
-    h.wt = wts[i].data_ptr<float>();
-    h.bias = biases[i].data_ptr<float>();
-    h.out = y.data_ptr<float>();
-    h.bstride = Ho * Wo * N;
-    h.B = static_cast<int>(x.size(0));
-    h.H = static_cast<int>(x.size(1));
-    h.W = static_cast<int>(x.size(2));
-    h.K = static_cast<int>(K);
-    h.Kpad = static_cast<int>(wts[i].size(1));
-    h.N = static_cast<int>(N);
-    h.Npad = static_cast<int>(wts[i].size(0));
-    h.stride = static_cast<int>(S);
-    h.act = static_cast<int>(act);
-    h.dil = static_cast<int>(dilation);
-    if (res.has_value() && res->defined()) {
-      TORCH_CHECK(n == 1 && res->is_cuda() && res->scalar_type() == at::kFloat && res->is_contiguous() &&
-                      res->sizes() == y.sizes() && N % 4 == 0,
-                  "dwpw: residual [B,Ho,Wo,N] f32 (one problem)");
-      h.res = res->data_ptr<float>();
-    }
-    outs.push_back(y);
-  }
-  nnsx::kernels::dwpw_f32(a, cur_stream());
-  return outs;
-}
-
-std::vector<at::Tensor> dwpw_cpu(at::TensorList xs, const c10::List<c10::optional<at::Tensor>>& wds,
-                                 const c10::List<c10::optional<at::Tensor>>& bds, at::TensorList wts,
-                                 at::TensorList biases, at::IntArrayRef ns, at::IntArrayRef strides, int64_t act,
-                                 int64_t dilation, const c10::optional<at::Tensor>& res) {
-  std::vector<at::Tensor> outs;
-  for (size_t i = 0; i < xs.size(); ++i) {
-    const c10::optional<at::Tensor> wd = wds.get(i), bd = bds.get(i);
-    at::Tensor h = (wd.has_value() && wd->defined()) ? dw_conv_cpu(xs[i], *wd, *bd, strides[i], 1, dilation) : xs[i];
-    const int64_t N = ns[i];
-    at::Tensor y = pw_conv_cpu(h, wts[i], biases[i], res, (N + 3) / 4 * 4, act, true).slice(-1, 0, N).contiguous();
-    outs.push_back(y);
-  }
-  return outs;
-}
 
 // pw_conv with a per-image bias: bias [B, N] (row b of it for every pixel of
 // image b).  project(cat[a, p]) with p constant over space (DeepLab's image
@@ -826,8 +751,6 @@ TORCH_LIBRARY(nnsx, m) {
   m.def("pw_conv_into(Tensor x, Tensor wt, Tensor bias, Tensor(a!) out, int row0, int n, int act) -> ()");
   m.def("pw_conv_rowbias(Tensor x, Tensor wt, Tensor bias, int N, int act) -> Tensor");
   m.def("upsample_bilinear(Tensor x, int H, int W) -> Tensor");
-  m.def("dwpw(Tensor[] xs, Tensor?[] wds, Tensor?[] bds, Tensor[] wts, Tensor[] biases, int[] ns, int[] strides, "
-        "int act, int dilation=1, Tensor? res=None) -> Tensor[]");
   m.def("sep_heads(Tensor[] xs, Tensor[] wds, Tensor[] bds, Tensor[] wts, Tensor[] biases, int[] ns, int[] which, "
         "Tensor(a!) out_box, Tensor(b!) out_cls, int mode=0) -> ()");
   m.def("pw_conv_group(Tensor[] xs, Tensor[] wts, Tensor[] biases, int[] ns, int[] acts) -> Tensor[]");
@@ -858,7 +781,6 @@ TORCH_LIBRARY_IMPL(nnsx, CUDA, m) {
   m.impl("upsample_bilinear", upsample_bilinear_cuda);
   m.impl("sep_heads", sep_heads_cuda);
   m.impl("pw_conv_group", pw_conv_group_cuda);
-  m.impl("dwpw", dwpw_cuda);
   m.impl("dw_conv", dw_conv_cuda);
   m.impl("stem_conv", stem_conv_cuda);
   m.impl("stem_conv_u8", stem_conv_u8_cuda);
@@ -877,7 +799,6 @@ TORCH_LIBRARY_IMPL(nnsx, CPU, m) {
   m.impl("upsample_bilinear", upsample_bilinear_cpu);
   m.impl("sep_heads", sep_heads_cpu);
   m.impl("pw_conv_group", pw_conv_group_cpu);
-  m.impl("dwpw", dwpw_cpu);
   m.impl("dw_conv", dw_conv_cpu);
   m.impl("stem_conv", stem_conv_cpu);
   m.impl("stem_conv_u8", stem_conv_u8_cpu);

@@ -30,19 +30,12 @@ from .mobilenet_v2 import ConvBNReLU, InvertedResidual, MobileNetV2
 
 import os
 
-# NNSX_FUSE_IR=0 keeps every inverted residual on the three-kernel path (A/B testing)
-FUSE_IR = os.environ.get("NNSX_FUSE_IR", "1") != "0"
-# NNSX_FUSE_STEM=0 keeps the fp32 stem and first block as separate kernels (A/B testing)
-FUSE_STEM = os.environ.get("NNSX_FUSE_STEM", "1") != "0"
-# NNSX_F32_HEAD_POOL=0: batches > 8 run the head GEMM and the average pool as two
-# kernels (A/B testing of the pooling GEMM epilogue)
-HEAD_POOL = os.environ.get("NNSX_F32_HEAD_POOL", "1") != "0"
-# NNSX_DWPW=1: depthwise + pointwise pairs as one dwpw GEMM (kernels/dwpw_f32.hip,
-# the depthwise computed in the GEMM's operand staging).  Off by default: it
-# recomputes the depthwise once per output-column tile, and measured slower
-# than the depthwise kernel + GEMM on every model (profiles/r4_dwpw_ab.txt:
-# PoseNet b64 16.2k vs 32.3k frames/s, DeepLab b8 4.5k vs 6.7k, SSD b64 20.4k vs 24.8k)
-DWPW = os.environ.get("NNSX_DWPW", "0") == "1"
+# (the A/B switches of earlier rounds -- unfused blocks / stem, head GEMM + pool
+# as two kernels, depthwise inside the project GEMM's staging -- are gone; their
+# measurements: profiles/r4_dwpw_ab.txt, r4_fp32_layers_b512_final.txt)
+FUSE_IR = True
+FUSE_STEM = True
+HEAD_POOL = True
 
 
 def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d):
@@ -160,8 +153,6 @@ class Block(nn.Module):
         # tickets of the fp32 kernel's in-launch combine of hidden-channel parts
         # (small batches): zero here, and every launch leaves them zero again
         self.register_buffer("ir_tickets", torch.zeros(768 if self.f32 else 1, dtype=torch.int32))
-        self.dwpw_dilated = False
-        self.dwpw_all = False
         if self.f32:
             self._init_f32(cin, hid)
             return
@@ -189,7 +180,7 @@ class Block(nn.Module):
         self.register_buffer("ir_wp", wp)
         # measured on MI355X (scripts/bench_ir.py, batch 256): the fused kernel wins on every
         # MobileNetV2 block except the 7x7 160->960->320 one (too few tiles, 20 output tiles/lane)
-        self.min_tiles = int(os.environ.get("NNSX_IR_MIN_TILES", "256"))
+        self.min_tiles = 256
         self.use_ir = (bool(torch.ops.nnsx.ir_supported(int(ir.stride), cin, hp, self.cout)) and FUSE_IR
                        and (self.has_expand or hid == hp) and self.cout < 320)
 
@@ -212,11 +203,6 @@ class Block(nn.Module):
         self.register_buffer("ir_wp3", x3_split(self.project.wt[: self.cout, :hid], (self.cout + 31) // 32 * 32, hid))
         self.min_tiles = 0
         self.use_ir = FUSE_IR and hid % 16 == 0 and (self.has_expand or hid == cin)
-        # dilated blocks (DeepLab's output-stride-16 stage) that the fused kernel
-        # does not take: depthwise + project as one GEMM with NNSX_DWPW=1 (A/B)
-        self.dwpw_dilated = DWPW and self.cout % 4 == 0
-        # (A/B: every unfused block that way, e.g. MobileNetV2's 7x7 160 -> 960 -> 320)
-        self.dwpw_all = os.environ.get("NNSX_DWPW_ALL", "0") == "1"
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.f32:
@@ -236,14 +222,6 @@ class Block(nn.Module):
                                                 self.dw.dilation, self.ir_we3)
             else:
                 h = self.expand(x) if self.has_expand else x
-                if self.dwpw_dilated and (self.dw.dilation > 1 or self.dwpw_all) and h.is_cuda:
-                    # dilated depthwise inside the project GEMM's operand staging
-                    # (kernels/dwpw_f32.hip): no depthwise output map in HBM
-                    wd: List[Optional[torch.Tensor]] = [self.dw.w]
-                    bd: List[Optional[torch.Tensor]] = [self.dw.bias]
-                    r: Optional[torch.Tensor] = x if self.use_res else None
-                    return torch.ops.nnsx.dwpw([h], wd, bd, [self.project.wt], [self.project.bias], [self.cout],
-                                               [self.dw.stride], 0, self.dw.dilation, r)[0]
                 h = self.dw(h)
             if self.use_res:
                 return self.project(h, x)

@@ -112,42 +112,12 @@ class FusedPoseNet(nn.Module):
         self.heat = _padded_pw(m.heatmap, precision)
         self.offs = _padded_pw(m.offsets, precision)
         self.k = int(m.heatmap.out_channels)
-        # fp32: every depthwise + pointwise pair as one GEMM with the depthwise in
-        # its operand staging, and both 1x1 heads in one launch with exact columns
-        # (nnsx::dwpw, kernels/dwpw_f32.hip) with NNSX_DWPW=1; default: 2 launches per pair (measured faster)
-        import os
-
-        self.fuse_dwpw = self.f32 and os.environ.get("NNSX_DWPW", "0") == "1"
-        # fp32: every pointwise conv but the last runs linear (bias only) and the
-        # next depthwise applies its ReLU6 to the taps it reads (dw_conv act bit
-        # 1), so the pointwise GEMMs are plain products the library GEMM takes
-        # (kernels/blaslt.cc).  Opt-in (NNSX_DEFER_ACT=1): the batch-64 run with the
-        # 270k-row products on the library GEMM hung the device; default: ReLU6 in
-        # the engine GEMM's epilogue
-        self.defer_act = self.f32 and os.environ.get("NNSX_DEFER_ACT", "0") == "1"
         return self
 
     def forward(self, x: torch.Tensor):
         h = stem(x, self.stem_w, self.stem_b, self.in_lut, self.f32)
-        if self.fuse_dwpw and h.is_cuda:
-            for d, p in zip(self.dws, self.pws):
-                wd: List[Optional[torch.Tensor]] = [d.w]
-                bd: List[Optional[torch.Tensor]] = [d.bias]
-                h = torch.ops.nnsx.dwpw([h], wd, bd, [p.wt], [p.bias], [p.n], [d.stride], 1)[0]
-            nones: List[Optional[torch.Tensor]] = [None, None]
-            o = torch.ops.nnsx.dwpw([h, h], nones, nones, [self.heat.wt, self.offs.wt], [self.heat.bias, self.offs.bias],
-                                    [self.k, 2 * self.k], [1, 1], 0)
-            return o[0], o[1]
-        if self.defer_act and h.is_cuda:
-            n = len(self.pws)
-            i = 0
-            for d, p in zip(self.dws, self.pws):
-                h = torch.ops.nnsx.dw_conv(h, d.w, d.bias, d.stride, 3 if i > 0 else 1, d.dilation)
-                h = torch.ops.nnsx.pw_conv(h, p.wt, p.bias, None, p.n, 1 if i == n - 1 else 0, p.out_f32)
-                i += 1
-        else:
-            for d, p in zip(self.dws, self.pws):
-                h = p(d(h))
+        for d, p in zip(self.dws, self.pws):
+            h = p(d(h))
         if self.f32 and h.is_cuda:
             # both 1x1 heads in one grouped GEMM launch, exact columns (no slice copies)
             o = torch.ops.nnsx.pw_conv_group([h, h], [self.heat.wt, self.offs.wt], [self.heat.bias, self.offs.bias],

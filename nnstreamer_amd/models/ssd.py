@@ -20,7 +20,7 @@ from typing import List, Optional, Tuple
 import torch
 import torch.nn as nn
 
-from .fused import DW, DWPW, PW, Block, StemBlock1, _fold, input_lut, stem
+from .fused import DW, PW, Block, StemBlock1, _fold, input_lut, stem
 from .mobilenet_v2 import ConvBNReLU, MobileNetV2
 
 ANCHORS = (3, 6, 6, 6, 6, 6)
@@ -154,16 +154,9 @@ class FusedExtra(nn.Module):
         self.a = PW(*_fold(e[0][0], e[0][1]), act=1, precision=precision)
         self.d = DW(*_fold(e[1][0], e[1][1]), stride=2, precision=precision)
         self.c = PW(*_fold(e[2][0], e[2][1]), act=1, precision=precision)
-        self.dwpw = DWPW
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        h = self.a(x)
-        if self.dwpw and self.c.wt.dtype == torch.float32 and h.is_cuda:
-            # the stride-2 depthwise inside the second pointwise GEMM (kernels/dwpw_f32.hip)
-            wd: List[Optional[torch.Tensor]] = [self.d.w]
-            bd: List[Optional[torch.Tensor]] = [self.d.bias]
-            return torch.ops.nnsx.dwpw([h], wd, bd, [self.c.wt], [self.c.bias], [self.c.n], [self.d.stride], 1)[0]
-        return self.c(self.d(h))
+        return self.c(self.d(self.a(x)))
 
 
 class FusedSSDLite(nn.Module):
@@ -192,14 +185,11 @@ class FusedSSDLite(nn.Module):
         self.cls_heads = nn.ModuleList([FusedSepHead(h, m.num_classes, precision) for h in m.cls_heads])
         self.feat_block = 13  # blocks[13] == features[14]: its expansion output is SSD feature 1
         # fp32: all 12 heads (depthwise + predictor, box and class, 6 maps) through
-        # nnsx::sep_heads -- mode 0 (default): one grouped depthwise launch + one
-        # grouped GEMM launch; mode 1 (NNSX_DWPW=1): one launch, the depthwise in the
-        # GEMM's staging (slower, fused.py DWPW).  NNSX_SSD_SEP_HEADS=0: 2 launches per head.
-        import os
-
-        self.one_launch_heads = self.f32 and os.environ.get("NNSX_SSD_SEP_HEADS", "1") != "0"
-        self.heads_mode = 1 if DWPW else 0
-        self.feat_dwpw = self.f32 and DWPW
+        # nnsx::sep_heads: one grouped depthwise launch + one grouped GEMM launch
+        # (the depthwise inside the GEMM's staging measured slower and was removed:
+        # profiles/r4_dwpw_ab.txt)
+        self.one_launch_heads = self.f32
+        self.heads_mode = 0
         return self
 
     def forward(self, x: torch.Tensor):
@@ -209,13 +199,7 @@ class FusedSSDLite(nn.Module):
             if i == self.feat_block:
                 e = blk.expand(h)
                 feats.append(e)
-                if self.feat_dwpw and e.is_cuda and not blk.use_res:
-                    wd: List[Optional[torch.Tensor]] = [blk.dw.w]
-                    bd: List[Optional[torch.Tensor]] = [blk.dw.bias]
-                    h = torch.ops.nnsx.dwpw([e], wd, bd, [blk.project.wt], [blk.project.bias], [blk.cout],
-                                            [blk.dw.stride], 0)[0]
-                else:
-                    h = blk.project(blk.dw(e))
+                h = blk.project(blk.dw(e))
             elif i > 0:  # (block 0 is in self.front)
                 h = blk(h)
         h = self.head(h)

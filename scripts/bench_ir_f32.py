@@ -43,12 +43,11 @@ def row(name, us, flop):
 
 
 ONLY = os.environ.get("NNSX_IR_ONLY")
-if ONLY in ("stem", "stemband"):  # only the fused stem + block 1 (for rocprof); stemband: the line-buffer kernel
+if ONLY == "stem":  # only the fused stem + block 1 (for rocprof)
     xu = torch.randint(0, 256, (B, 224, 224, 3), device="cuda", dtype=torch.uint8)
     w = [torch.randn(3, 3, 3, 32, device="cuda"), torch.zeros(32, device="cuda"), torch.randn(9, 32, device="cuda"),
          torch.zeros(32, device="cuda"), torch.randn(16, 32, device="cuda") * 0.1, torch.zeros(16, device="cuda")]
-    mode = 3 if ONLY == "stemband" else -1
-    us1 = timeit(lambda: torch.ops.nnsx.stem_ir1(xu, *w, LUT, mode))
+    us1 = timeit(lambda: torch.ops.nnsx.stem_ir1(xu, *w, LUT))
     print(f"stem+block1 fused ({ONLY}) {us1:.1f} us at batch {B}")
     sys.exit(0)
 if ONLY:
@@ -113,8 +112,6 @@ if not ONLY:
     row("stem+block1 fused (replaces both)", us1,
         2 * B * 112 * 112 * (32 * 27 + 32 * 9 + 32 * 16))
     print(f"  fused saves {us + seen[(112, 32, 32, 16, 1)] - us1:.1f} us")
-    us2 = timeit(lambda: torch.ops.nnsx.stem_ir1(xu, ws, bs, wd1, bd1, wp1, bp1, LUT, 3))
-    row("stem+block1 line buffer (band)", us2, 2 * B * 112 * 112 * (32 * 27 + 32 * 9 + 32 * 16))
     xh = torch.randn(B * 49, 320, device="cuda")
     wh = torch.randn(1280, 320, device="cuda") * 0.05
     bh = torch.zeros(1280, device="cuda")

@@ -4,8 +4,7 @@
 GStreamer lays out 513- and 257-wide RGB) -> tensor_converter
 frames-per-tensor=B device=0 -> tensor_sink sync-device.  Reports the packed
 bytes per second that reach HBM (a queue before the sink: the sink's device
-sync does not stall the converter).  NNSX_CONVERTER_PADDED_DMA=0 selects the
-previous per-frame gather kernel for the A/B.
+sync does not stall the converter).
 
     python scripts/upload_bench.py [width] [batch] [batches]
 """
@@ -40,11 +39,9 @@ def main():
         torch.cuda.synchronize()
         el = time.perf_counter() - t
         p.stop()
-    mode = "padded DMA + unpad_rows" if os.environ.get("NNSX_CONVERTER_PADDED_DMA", "1") != "0" else "gather kernel"
+    mode = "padded DMA + unpad_rows"
     if host:
         mode = "host only, no upload"
-    elif os.environ.get("NNSX_CONVERTER_DMA_SPLIT", "1") != "1":
-        mode += f", {os.environ['NNSX_CONVERTER_DMA_SPLIT']} copy streams"
     print(f"width {w} batch {B} ({mode}): {n} batches in {el * 1e3:.1f} ms, {el / n * 1e6:.1f} us per batch, "
           f"{n * B * frame / el / 1e9:.2f} GB/s packed frames to HBM")
 

@@ -117,15 +117,13 @@ def test_avgpool_f32(B, HW, C):
     assert torch.equal(p, torch.ops.nnsx.avgpool(x))  # deterministic
 
 
-@pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("B", [1, 3, 64])
-def test_sep_heads_one_launch_vs_fp64(B, mode):
+def test_sep_heads_one_launch_vs_fp64(B):
     """All 12 SSDLite heads (depthwise 3x3 + ReLU6 + predictor, box and class, 6
     maps) against an fp64 oracle of each head, rows of the concatenated outputs
-    included; mode 0: one grouped depthwise launch + one grouped GEMM launch
-    (kernels/mbv2_f32.hip dw3x3_group / pw_gemm_group), mode 1: one launch
-    (kernels/dwpw_f32.hip).  B = 64 is the benched batch (tiles spanning images
-    at the 3x3 .. 1x1 maps)."""
+    included: one grouped depthwise launch + one grouped GEMM launch
+    (kernels/mbv2_f32.hip dw3x3_group / pw_gemm_group).  B = 64 is the benched
+    batch (tiles spanning images at the 3x3 .. 1x1 maps)."""
     import torch.nn.functional as F
 
     m = ssd.fused_ssd_mobilenet(seed=3, precision="fp32").cuda()
@@ -138,7 +136,7 @@ def test_sep_heads_one_launch_vs_fp64(B, mode):
     heads = list(m.cls_heads) + list(m.box_heads)
     torch.ops.nnsx.sep_heads(feats + feats, [h.dw.w for h in heads], [h.dw.bias for h in heads],
                              [h.pw.wt for h in heads], [h.pw.bias for h in heads], [h.n for h in heads],
-                             [1] * 6 + [0] * 6, bo, lo, mode)
+                             [1] * 6 + [0] * 6, bo, lo, 0)
 
     def ref(x, h):
         C = x.shape[-1]
@@ -183,63 +181,3 @@ def test_pw_conv_group_vs_fp64(shapes):
         assert y.shape == x.shape[:3] + (n,)
         err = ((y.double().cpu() - want).abs() / (want.abs() + 1)).max().item()
         assert err < 2e-5, err
-
-
-@pytest.mark.parametrize("B,H,K,N,S,dw", [(3, 129, 32, 64, 1, True), (2, 129, 64, 128, 2, True),
-                                          (64, 17, 512, 512, 1, True), (5, 17, 512, 1024, 2, True),
-                                          (64, 9, 1024, 1024, 1, True), (7, 9, 1024, 17, 1, False)])
-def test_dwpw_one_gemm_vs_fp64(B, H, K, N, S, dw):
-    """Depthwise 3x3 (stride S) + ReLU6 + pointwise + ReLU6 as one GEMM with the
-    depthwise in the operand staging (kernels/dwpw_f32.hip, nnsx::dwpw: the
-    PoseNet / MobileNetV1 pairs), and without a depthwise (the 1x1 heads, exact
-    columns), against fp64."""
-    import torch.nn.functional as F
-
-    g = torch.Generator().manual_seed(K + N)
-    x = (torch.rand(B, H, H, K, generator=g) * 2).cuda()
-    wd = (torch.randn(9, K, generator=g) * 0.3).cuda()
-    bd = (torch.randn(K, generator=g) * 0.1).cuda()
-    Np = (N + 63) // 64 * 64
-    wt = torch.zeros(Np, K)
-    wt[:N] = torch.randn(N, K, generator=g) / K ** 0.5
-    wt = wt.cuda()
-    bias = torch.zeros(Np)
-    bias[:N] = torch.randn(N, generator=g) * 0.1
-    bias = bias.cuda()
-    y = torch.ops.nnsx.dwpw([x], [wd if dw else None], [bd if dw else None], [wt], [bias], [N], [S], 1 if dw else 0)[0]
-    xd = x.double().cpu().permute(0, 3, 1, 2)
-    if dw:
-        xd = F.conv2d(xd, wd.double().cpu().t().reshape(K, 1, 3, 3), bd.double().cpu(), stride=S, padding=1,
-                      groups=K).clamp(0, 6)
-    ref = torch.einsum("bchw,nc->bhwn", xd, wt.double().cpu()[:N]) + bias.double().cpu()[:N]
-    if dw:
-        ref = ref.clamp(0, 6)
-    Ho = (H - 1) // S + 1
-    assert y.shape == (B, Ho, Ho, N)
-    err = ((y.double().cpu() - ref).abs() / (ref.abs() + 1)).max().item()
-    assert err < 2e-5, err
-
-
-def test_dwpw_dilated_residual_vs_fp64():
-    """DeepLab's dilated blocks: depthwise dilation 2 (padding 2) inside the
-    project GEMM, plus the block's residual, against fp64 (33x33 maps, B = 8)."""
-    import torch.nn.functional as F
-
-    B, H, K, N = 8, 33, 960, 160
-    g = torch.Generator().manual_seed(11)
-    x = (torch.rand(B, H, H, K, generator=g) * 2).cuda()
-    res = torch.randn(B, H, H, N, generator=g).cuda()
-    wd = (torch.randn(9, K, generator=g) * 0.3).cuda()
-    bd = (torch.randn(K, generator=g) * 0.1).cuda()
-    wt = torch.zeros(192, K)
-    wt[:N] = torch.randn(N, K, generator=g) / K ** 0.5
-    wt = wt.cuda()
-    bias = torch.zeros(192)
-    bias[:N] = torch.randn(N, generator=g) * 0.1
-    bias = bias.cuda()
-    y = torch.ops.nnsx.dwpw([x], [wd], [bd], [wt], [bias], [N], [1], 0, 2, res)[0]
-    d = F.conv2d(x.double().cpu().permute(0, 3, 1, 2), wd.double().cpu().t().reshape(K, 1, 3, 3), bd.double().cpu(),
-                 padding=2, dilation=2, groups=K).clamp(0, 6)
-    ref = torch.einsum("bchw,nc->bhwn", d, wt.double().cpu()[:N]) + bias.double().cpu()[:N] + res.double().cpu()
-    err = ((y.double().cpu() - ref).abs() / (ref.abs() + 1)).max().item()
-    assert err < 2e-5, err
