@@ -478,22 +478,28 @@ class TensorConverter : public Element {
     if (ps.empty() || seen != size) return false;
     const size_t row = ps[0]->row, stride = ps[0]->stride, rows = ps[0]->rows;
     const size_t sf = stride * (rows - 1) + row;  // padded bytes of one frame (the last row's padding may be absent)
-    // equally spaced frames (a capture ring): one DMA over all of them
-    const char* base = static_cast<const char*>(ps[0]->mem->data());
-    size_t spacing = ps.size() > 1 ? static_cast<size_t>(static_cast<const char*>(ps[1]->mem->data()) - base) : sf;
-    bool ring = ps.size() > 1 && static_cast<const char*>(ps[1]->mem->data()) > base && spacing >= sf &&
-                spacing <= 2 * sf;
-    for (size_t i = 2; ring && i < ps.size(); ++i)
-      ring = static_cast<const char*>(ps[i]->mem->data()) == base + i * spacing;
-    if (!ring) spacing = (sf + 255) / 256 * 256;
-    auto stg = Memory::alloc_device(spacing * (ps.size() - 1) + sf, dev, s);
+    // Frames of a capture ring sit `spacing` apart: the staging copy keeps that
+    // spacing and every run of adjacent frames goes up as ONE DMA -- a batch
+    // that wraps around the ring is two.  A lone frame is one DMA of its own.
+    // (Per-frame DMAs of 790 KB ran at ~23 GB/s with the queue gaps between
+    // them, one 25 MB ring DMA at the 50 GB/s link rate:
+    // profiles/r5_fan_ingest_1gpu.txt.)
+    auto at = [&](size_t i) { return static_cast<const char*>(ps[i]->mem->data()); };
+    size_t spacing = 0;
+    for (size_t i = 1; i < ps.size() && !spacing; ++i)
+      if (at(i) > at(i - 1) && static_cast<size_t>(at(i) - at(i - 1)) >= sf &&
+          static_cast<size_t>(at(i) - at(i - 1)) <= 2 * sf)
+        spacing = static_cast<size_t>(at(i) - at(i - 1));
+    if (!spacing) spacing = (sf + 255) / 256 * 256;
+    auto stg = stage_alloc(spacing * (ps.size() - 1) + sf, dev, s);
     char* sp = static_cast<char*>(stg->data());
     // (splitting the upload over 2-4 copy streams did not help: profiles/r4_upload_bench.txt)
-    if (ring) {
-      hip::check(hipMemcpyAsync(sp, base, spacing * (ps.size() - 1) + sf, hipMemcpyHostToDevice, s), "padded ring DMA");
-    } else {
-      for (size_t i = 0; i < ps.size(); ++i)
-        hip::check(hipMemcpyAsync(sp + i * spacing, ps[i]->mem->data(), sf, hipMemcpyHostToDevice, s), "padded DMA");
+    for (size_t i = 0; i < ps.size();) {
+      size_t j = i + 1;
+      while (j < ps.size() && at(j) == at(i) + (j - i) * spacing) ++j;
+      hip::check(hipMemcpyAsync(sp + i * spacing, at(i), spacing * (j - i - 1) + sf, hipMemcpyHostToDevice, s),
+                 "padded DMA");
+      i = j;
     }
     kernels::unpad_rows(sp, out->data(), static_cast<uint32_t>(ps.size()), static_cast<uint32_t>(row),
                         static_cast<uint32_t>(stride), static_cast<uint32_t>(rows), spacing, s);
@@ -804,6 +810,16 @@ class TensorConverter : public Element {
       pool_->preallocate(s);
     }
     return pool_->acquire(s);
+  }
+  // the padded upload's staging blocks: recycled too (a hipFreeAsync per batch
+  // held the converter thread 90-210 us, a third of a batch-8 camera's budget:
+  // profiles/r5_fan_ingest_1gpu.txt)
+  std::shared_ptr<DeviceBufferPool> stage_pool_;
+  MemoryPtr stage_alloc(size_t size, int dev, hipStream_t s) {
+    if (pool_blocks_ <= 0) return Memory::alloc_device(size, dev, s);
+    if (!stage_pool_ || stage_pool_->device() != dev || stage_pool_->block_size() != size)
+      stage_pool_ = DeviceBufferPool::create(dev, size, static_cast<size_t>(pool_blocks_));
+    return stage_pool_->acquire(s);
   }
   bool configured_ = false;
   TensorsConfig config_;

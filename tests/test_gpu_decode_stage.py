@@ -82,3 +82,48 @@ def test_decoder_stage_with_replay_lanes_asked(nns, workdir, case):
     assert info == ("dec", "f"), info
     assert len(got) == len(ref) == 12
     assert got == ref
+
+
+def test_decoder_option_change_retakes_stage(nns, workdir):
+    """A decoder option set while playing (pose_estimation option4
+    heatmap-offset -> heatmap-only) after the filter captured the decoder's stage
+    in its graph: the stage goes stale (tensor_decoder.cc InstanceStage::revoke),
+    the filter re-takes it and re-captures, and the later frames equal a run
+    that had the new option from the start -- no frozen options, no freed
+    decoder instance under a live graph."""
+    from nnstreamer_amd.models.export import export
+
+    S, model_name, norm, dec = CASES["posenet"]
+    model = export(model_name, os.path.join(workdir, f"{model_name}_opt.pt"), layout="nhwc")
+    B, nb = 2, 8
+
+    def run(option4, switch_after=None):
+        d = dec.format(**_files(workdir)).replace("option4=heatmap-offset", f"option4={option4}")
+        desc = (f"videotestsrc num-buffers={nb * B} pattern=snow pool-size={nb * B} "
+                f"! video/x-raw,format=RGB,width={S},height={S},framerate=30/1 "
+                f"! tensor_converter frames-per-tensor={B} device=0 ! tensor_transform mode=arithmetic option={norm} "
+                f"! tensor_filter name=f framework=pytorch model={model} input=3:{S}:{S}:{B} inputtype=float32 "
+                "accelerator=true:gpu device=0 custom=hipgraph:true ! queue max-size-buffers=2 "
+                f"! {d} ! tensor_sink name=sink")
+        p = nns.parse_launch(desc)
+        out = []
+
+        def on(b):
+            out.append(bytes(b.memory(0).bytes()))
+            if switch_after is not None and len(out) == switch_after:
+                p.get_by_name("dec").set_property("option4", "heatmap-only")
+
+        p.get_by_name("sink").connect("new-data", on)
+        p.run(timeout=300)
+        info = p.get_by_name("f").get_property("absorbed-decoder")
+        p.stop()
+        return out, info
+
+    switched, info = run("heatmap-offset", switch_after=2)
+    ref, _ = run("heatmap-only")
+    off, _ = run("heatmap-offset")
+    assert info == "dec"
+    assert len(switched) == len(ref) == nb * B
+    assert switched[-4:] == ref[-4:]      # the last two batches ran the new option
+    assert switched[:2] == off[:2]        # the first frames ran the old one
+    assert ref != off                     # (the option changes the frames)

@@ -189,11 +189,12 @@ def test_pose_device_matches_host(nns):
 @pytest.mark.parametrize("w,h,n,pool", [(224, 224, 6, 5), (5, 3, 7, 5), (64, 48, 130, 5), (257, 257, 9, 5),
                                          (513, 11, 3, 5), (2731, 5, 2, 5), (513, 513, 8, 64), (257, 257, 64, 128),
                                          (513, 513, 8, 3), (7, 5, 16, 40), (513, 513, 1, 5), (257, 257, 1, 5),
-                                         (5, 3, 1, 5)])
+                                         (5, 3, 1, 5), (513, 513, 8, 12), (257, 257, 16, 20)])
 def test_converter_batched_gather_matches_host(nns, w, h, n, pool):
     """Batched upload (frames-per-tensor) equals the host path byte for byte.
     Padded rows (W*3 % 4 != 0) take the DMA + unpad_rows path: one DMA over a
-    ring of equally spaced pool frames (pool >= batch) or one per frame -- at
+    run of equally spaced pool frames (a batch that wraps around the pool is
+    two runs: pool 12 / batch 8, pool 20 / batch 16) or one per frame -- at
     batch 1 too (it replaced a per-row 2D copy)."""
     desc = (f"videotestsrc num-buffers={2 * n} pattern=snow pool-size={pool} ! video/x-raw,format=RGB,width={w},height={h},"
             f"framerate=30/1 ! tensor_converter frames-per-tensor={n} device={{dev}} ! tensor_sink name=sink")
