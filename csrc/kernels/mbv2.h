@@ -77,9 +77,25 @@ struct YLayout {
   // (an image spans at most two row tiles: two addends, so the sum is order-free)
   int pool = 0;
 };
+// The weights of an fp32 GEMM already split into their three bf16 parts
+// (x3_split_weights), laid out the way a k-stage of the x3 GEMM stages them:
+// [stages][rows][3 parts][32 k] bf16 -- a tile's rows of one stage are one
+// contiguous block (192 B per row).  rows >= Npad, stages * 32 >= Kpad.  Given,
+// the x3 GEMM stages them as they are (no per-tile split of the weight operand);
+// absent (p null), it splits the fp32 weights per tile.
+struct X3W {
+  const uint16_t* p = nullptr;
+  int stages = 0, rows = 0;
+};
 void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
                  int Kpad, int Npad, int act, hipStream_t s, int tile = 0, float* ws = nullptr,
-                 const YLayout& yl = YLayout{});
+                 const YLayout& yl = YLayout{}, X3W w3 = X3W{});
+// fp32 weights [rows][cols] -> out [ceil(cols / 32)][x3_split_rows(rows)][3][32]
+// bf16 (hi, mid, lo; zero past rows / cols): the X3W layout.  Rows are padded
+// to a multiple of every tile width (64, 128, 192), so a tile's weight loads
+// need no bounds checks.
+int x3_split_rows(int rows);
+void x3_split_weights(const float* w, int rows, int cols, uint16_t* out, hipStream_t s);
 // Grouped launches (the SSD prediction heads): up to kGroupMax independent
 // problems per launch.  pw_gemm_f32_group: 64 x 64 tiles, no split-K, no
 // residual, any YLayout but pool.  dw3x3_f32_group: stride 1, dilation 1,
@@ -92,6 +108,7 @@ struct GemmProb {
   float* y = nullptr;
   int M = 0, N = 0, K = 0, Kpad = 0, Npad = 0, act = 0;
   YLayout yl;
+  X3W w3;  // (the x3 launch stages pre-split weights only if every problem has them)
 };
 struct DwProb {
   const float* x = nullptr;
@@ -141,7 +158,7 @@ void avgpool_f32(const float* x, float* y, int B, int HW, int C, hipStream_t s);
 // head 1x1 conv + act + global average pool in one launch (small batches):
 // x [B][HW][K] -> y [B][N] = mean_p act(x[b][p] . wt^T + bias)
 void pw_pool_f32(const float* x, const float* wt, const float* bias, float* y, int B, int HW, int N, int K, int Kpad,
-                 int Npad, int act, hipStream_t s);
+                 int Npad, int act, hipStream_t s, X3W w3 = X3W{});
 
 // fused inverted residual, fp32.  we [hid][KIN] (KIN = ceil8(cin), zero
 // padded), wd [9][hid], wp [ceil16(cout)][hid] (rows zero padded); biases

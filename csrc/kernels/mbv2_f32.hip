@@ -44,6 +44,7 @@
 #include <string>
 #include <vector>
 
+#include "kernels/gemm_f32.h"
 #include "kernels/mbv2.h"
 #include "kernels/x3.h"
 
@@ -52,309 +53,6 @@ namespace kernels {
 
 namespace {
 
-
-typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ f32x4_t mfma4(float a, float b, f32x4_t c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-// one 16-k step: lane (li, g) holds k = 16s + 4g + j in component j of a and b
-__device__ __forceinline__ f32x4_t mfma_k16(f32x4_t a, f32x4_t b, f32x4_t c) {
-  c = mfma4(a[0], b[0], c);
-  c = mfma4(a[1], b[1], c);
-  c = mfma4(a[2], b[2], c);
-  return mfma4(a[3], b[3], c);
-}
-// an 8-k tail step: lane (li, g) holds k = 2g + j in component j
-__device__ __forceinline__ f32x4_t mfma_k8(f32x2_t a, f32x2_t b, f32x4_t c) {
-  c = mfma4(a[0], b[0], c);
-  return mfma4(a[1], b[1], c);
-}
-
-__device__ __forceinline__ float act_fn(float v, int act) {
-  if (act == 1) return fminf(fmaxf(v, 0.f), 6.f);  // ReLU6
-  if (act == 2) return fmaxf(v, 0.f);                // ReLU
-  return v;
-}
-__device__ __forceinline__ float relu6(float v) { return fminf(fmaxf(v, 0.f), 6.f); }
-__device__ __forceinline__ f32x4_t relu6x4(f32x4_t v) {
-  return f32x4_t{relu6(v[0]), relu6(v[1]), relu6(v[2]), relu6(v[3])};
-}
-
-// XCD-aware workgroup order: the dispatcher places consecutive workgroup ids
-// round-robin over the 8 XCDs (each with its own L2).  Renumber so that each
-// XCD walks a contiguous range of tiles: neighbouring tiles share halo rows
-// and the same image, and stay in one L2.
-__device__ __forceinline__ int xcd_remap(int bid, int n) {
-  if (n % 8) return bid;
-  return (bid % 8) * (n / 8) + bid / 8;
-}
-
-// ------------------------------------------------------------- pw_gemm_f32 ----
-constexpr int GKT = 32;       // k per LDS stage
-constexpr int GKQ = GKT / 4;  // k-quads per stage
-
-// one BM x BN output tile over k-stages [kbeg, kbeg + nk * GKT); zs / slab: this
-// block's split-K slice and whether the grid is split (then y is the slab workspace)
-// X3: the products on split-bf16 MFMAs (see split_x3), the LDS images and the
-// epilogue unchanged
-template <int BM, int BN, bool X3 = false>
-__device__ __forceinline__ void pw_gemm_f32_tile(const float* __restrict__ x,     // [M][K]
-                                                 const float* __restrict__ wt,    // [Npad][Kpad]
-                                                 const float* __restrict__ bias,  // [N]
-                                                 const float* __restrict__ res,   // [M][N] or null
-                                                 float* __restrict__ y,           // [M][N]
-                                                 int M, int N, int K, int Kpad, int Npad, int act, int kbeg, int nk,
-                                                 int zs, bool slab, const YLayout& yl, int m0, int n0) {
-  constexpr int RM = BM / 32, RN = BN / 32;  // 16-row fragments per wave (2 x 2 waves)
-  constexpr int VX = BM * GKQ / 256, VW = BN * GKQ / 256;
-  // k4-major images, row index XOR-swizzled with the k-quad (kq < 8): the
-  // staging writes (8 lanes = 8 k-quads of one row) then spread over the
-  // banks, and fragment reads stay conflict-free (16 rows of one 16-aligned
-  // block, permuted)
-  // X3: both operands are split once, while they are staged, into three bf16
-  // planes [part][k8][row] of 8 consecutive k (16 B) -- the fragment of a
-  // 32-k step is then 3 ds_read_b128 per operand and no VALU; rows
-  // XOR-swizzled by k8 (staging writes spread, fragment reads stay 256
-  // contiguous bytes per 16 lanes)
-  __shared__ __attribute__((aligned(16))) float xs[X3 ? 1 : 2][GKQ][X3 ? 4 : BM][4];
-  __shared__ __attribute__((aligned(16))) float ws[X3 ? 1 : 2][GKQ][X3 ? 4 : BN][4];
-  __shared__ __attribute__((aligned(16))) bf16x8_t xs3[X3 ? 2 : 1][3][4][X3 ? BM : 1];
-  __shared__ __attribute__((aligned(16))) bf16x8_t ws3[X3 ? 2 : 1][3][4][X3 ? BN : 1];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int li = lane & 15, g = lane >> 4;
-  const f32x4_t zero = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  f32x4_t px[VX], pw[VW];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < VX; ++i) {
-      const int v = tid + i * 256, kq = v & 7, row = v >> 3;
-      const int m = m0 + row, k = k0 + kq * 4;
-      px[i] = (m < M && k < K) ? *reinterpret_cast<const f32x4_t*>(x + static_cast<int64_t>(m) * K + k) : zero;
-    }
-#pragma unroll
-    for (int i = 0; i < VW; ++i) {
-      const int v = tid + i * 256, kq = v & 7, row = v >> 3;
-      const int n = n0 + row, k = k0 + kq * 4;
-      pw[i] = (n < Npad && k < Kpad) ? *reinterpret_cast<const f32x4_t*>(wt + static_cast<int64_t>(n) * Kpad + k)
-                                     : zero;
-    }
-  };
-  // (X3) a staged quad -> its three bf16 parts, 8 B into each part plane
-  auto st3 = [&](bf16x8_t* base, size_t part_stride, f32x4_t q) {
-    bf16x2_t h0, m0, l0, h1, m1, l1;
-    split2(f32x2_t{q[0], q[1]}, h0, m0, l0);
-    split2(f32x2_t{q[2], q[3]}, h1, m1, l1);
-    typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-    char* p = reinterpret_cast<char*>(base);
-    *reinterpret_cast<bf16x4_t*>(p) = __builtin_shufflevector(h0, h1, 0, 1, 2, 3);
-    *reinterpret_cast<bf16x4_t*>(p + part_stride) = __builtin_shufflevector(m0, m1, 0, 1, 2, 3);
-    *reinterpret_cast<bf16x4_t*>(p + 2 * part_stride) = __builtin_shufflevector(l0, l1, 0, 1, 2, 3);
-  };
-  auto lstore = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < VX; ++i) {
-      const int v = tid + i * 256, kq = v & 7, row = v >> 3;
-      if constexpr (X3) {
-        const int k8 = kq >> 1;
-        st3(reinterpret_cast<bf16x8_t*>(reinterpret_cast<char*>(&xs3[buf][0][k8][row ^ k8]) + (kq & 1) * 8),
-            sizeof(xs3[0][0]), px[i]);
-      } else {
-        *reinterpret_cast<f32x4_t*>(&xs[buf][kq][row ^ kq][0]) = px[i];
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < VW; ++i) {
-      const int v = tid + i * 256, kq = v & 7, row = v >> 3;
-      if constexpr (X3) {
-        const int k8 = kq >> 1;
-        st3(reinterpret_cast<bf16x8_t*>(reinterpret_cast<char*>(&ws3[buf][0][k8][row ^ k8]) + (kq & 1) * 8),
-            sizeof(ws3[0][0]), pw[i]);
-      } else {
-        *reinterpret_cast<f32x4_t*>(&ws[buf][kq][row ^ kq][0]) = pw[i];
-      }
-    }
-  };
-
-  f32x4_t acc[RM][RN];
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < RN; ++j) acc[i][j] = zero;
-
-  if (nk > 0) {
-    gload(kbeg);
-    lstore(0);
-    __syncthreads();
-  }
-  for (int ks = 0; ks < nk; ++ks) {
-    const int buf = ks & 1;
-    if (ks + 1 < nk) gload(kbeg + (ks + 1) * GKT);  // in flight during this stage's MFMAs
-    if constexpr (X3) {
-      static_assert(GKT == 32, "x3: one 32-k step per stage");
-      // lane (li, g): k 8g .. 8g + 7 of its row = plane k8 = g
-      X3Frag a[RN];
-#pragma unroll
-      for (int j = 0; j < RN; ++j) {
-        const int r = (wn * (BN / 2) + j * 16 + li) ^ g;
-        a[j].h = ws3[buf][0][g][r];
-        a[j].m = ws3[buf][1][g][r];
-        a[j].l = ws3[buf][2][g][r];
-      }
-#pragma unroll
-      for (int i = 0; i < RM; ++i) {
-        const int r = (wm * (BM / 2) + i * 16 + li) ^ g;
-        X3Frag b;
-        b.h = xs3[buf][0][g][r];
-        b.m = xs3[buf][1][g][r];
-        b.l = xs3[buf][2][g][r];
-#pragma unroll
-        for (int j = 0; j < RN; ++j) acc[i][j] += mfma_x3(a[j], b);
-      }
-    }
-#pragma unroll
-    for (int s = 0; s < (X3 ? 0 : GKT / 16); ++s) {
-      const int kq = 4 * s + g;
-      f32x4_t a[RN], b[RM];
-#pragma unroll
-      for (int j = 0; j < RN; ++j)
-        a[j] = *reinterpret_cast<const f32x4_t*>(&ws[buf][kq][(wn * (BN / 2) + j * 16 + li) ^ kq][0]);
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
-        b[i] = *reinterpret_cast<const f32x4_t*>(&xs[buf][kq][(wm * (BM / 2) + i * 16 + li) ^ kq][0]);
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
-#pragma unroll
-        for (int j = 0; j < RN; ++j) acc[i][j] = mfma_k16(a[j], b[i], acc[i][j]);
-    }
-    if (ks + 1 < nk) lstore(buf ^ 1);  // buf ^ 1 was last read before the previous barrier
-    __syncthreads();
-  }
-
-  // epilogue: lane owns channels n..n+3 of pixel m.  Bias (and residual)
-  // values are all loaded up front, branch-free: loaded at each store behind
-  // the bounds checks they were fetched and waited for one at a time.
-  if constexpr (BN == 64) {
-    if (yl.pool && !slab) {
-      // head conv + act + global average pool: the activated tile goes through
-      // the (now free) staging LDS, quads XOR-swizzled by row; each thread sums
-      // one (image, channel) column of the tile in row order and adds sum / pool
-      float* t = X3 ? reinterpret_cast<float*>(&xs3[0][0][0][0]) : &xs[0][0][0][0];  // [BM][64]
-#pragma unroll
-      for (int i = 0; i < RM; ++i) {
-        const int ml = wm * (BM / 2) + i * 16 + li, m = m0 + ml;
-#pragma unroll
-        for (int j = 0; j < RN; ++j) {
-          const int nl = wn * (BN / 2) + j * 16 + g * 4, n = n0 + nl;
-          f32x4_t v = acc[i][j] + *reinterpret_cast<const f32x4_t*>(bias + (n < N ? n : 0));
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], act);
-          *reinterpret_cast<f32x4_t*>(t + ml * 64 + (((nl >> 2) ^ (ml & 15)) << 2)) = m < M ? v : zero;
-        }
-      }
-      __syncthreads();
-      const int hw = yl.pool, mend = min(m0 + BM, M), b0 = m0 / hw, nb = (mend - 1) / hw - b0 + 1;
-      const float inv = 1.f / static_cast<float>(hw);
-      for (int v = tid; v < nb * 64; v += 256) {
-        const int bi = b0 + v / 64, nl = v % 64, n = n0 + nl;
-        const int r0 = max(bi * hw, m0) - m0, r1 = min((bi + 1) * hw, mend) - m0;
-        float sum = 0.f;
-        for (int r = r0; r < r1; ++r) sum += t[r * 64 + (((nl >> 2) ^ (r & 15)) << 2) + (nl & 3)];
-        if (n < N) atomicAdd(y + static_cast<int64_t>(bi) * N + n, sum * inv);
-      }
-      return;
-    }
-  }
-  f32x4_t bv[RN], rv[RM][RN];
-#pragma unroll
-  for (int j = 0; j < RN; ++j) {
-    const int n = n0 + wn * (BN / 2) + j * 16 + g * 4;
-    bv[j] = slab ? zero : *reinterpret_cast<const f32x4_t*>(bias + (n < N ? n : 0));
-  }
-  if (res && !slab) {
-#pragma unroll
-    for (int i = 0; i < RM; ++i) {
-      const int m = m0 + wm * (BM / 2) + i * 16 + li;
-#pragma unroll
-      for (int j = 0; j < RN; ++j) {
-        const int n = n0 + wn * (BN / 2) + j * 16 + g * 4;
-        const int64_t off = (m < M && n < N) ? static_cast<int64_t>(m) * N + n : 0;
-        rv[i][j] = *reinterpret_cast<const f32x4_t*>(res + off);
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < RM; ++i) {
-    const int m = m0 + wm * (BM / 2) + i * 16 + li;
-    if (m >= M) continue;
-#pragma unroll
-    for (int j = 0; j < RN; ++j) {
-      const int n = n0 + wn * (BN / 2) + j * 16 + g * 4;
-      if (n >= N) continue;
-      float* yp = y + static_cast<int64_t>(m) * N + n;
-      if (slab) {  // split-K: this slice's slab of the workspace (gemm_splitk_reduce adds them)
-        *reinterpret_cast<f32x4_t*>(y + static_cast<int64_t>(zs) * M * N + static_cast<int64_t>(m) * N + n) = acc[i][j];
-        continue;
-      }
-      f32x4_t v = acc[i][j] + (yl.brpb ? *reinterpret_cast<const f32x4_t*>(bias + static_cast<int64_t>(m / yl.brpb) * N + n)
-                                        : bv[j]);
-      if (res) v += rv[i][j];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], act);
-      if (yl.rpb) {  // a slice of a concatenated output: row m of batch m / rpb, first ncols columns
-        if (n >= yl.ncols) continue;
-        float* yd = y + static_cast<int64_t>(m / yl.rpb) * yl.bstride + static_cast<int64_t>(m % yl.rpb) * yl.ncols + n;
-        if (n + 4 <= yl.ncols && (yl.ncols & 3) == 0) {
-          *reinterpret_cast<f32x4_t*>(yd) = v;
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (n + r < yl.ncols) yd[r] = v[r];
-        }
-        continue;
-      }
-      *reinterpret_cast<f32x4_t*>(yp) = v;
-    }
-  }
-}
-
-template <int BM, int BN, bool X3 = false>
-__global__ void __launch_bounds__(256) pw_gemm_f32_kernel(const float* __restrict__ x, const float* __restrict__ wt,
-                                                          const float* __restrict__ bias, const float* __restrict__ res,
-                                                          float* __restrict__ y, int M, int N, int K, int Kpad, int Npad,
-                                                          int act,
-                                                          int kchunk,  // k-stages of this grid.z slice
-                                                          YLayout yl) {
-  const int nbx = gridDim.x, nby = gridDim.y;
-  const int flat = xcd_remap(blockIdx.y * nbx + blockIdx.x, nbx * nby);
-  const int kbeg = blockIdx.z * kchunk * GKT;
-  const int kend = min(Kpad, kbeg + kchunk * GKT);
-  pw_gemm_f32_tile<BM, BN, X3>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, kbeg, (kend - kbeg + GKT - 1) / GKT,
-                               static_cast<int>(blockIdx.z), gridDim.z > 1, yl, (flat % nbx) * BM, (flat / nbx) * BN);
-}
-
-// Several independent GEMMs in one launch (the SSD prediction heads): block b
-// takes a tile of the problem whose block range holds it.  No XCD remap: the
-// dispatcher deals blocks round robin over the XCDs, so each XCD gets the same
-// mix of deep (long) and shallow tiles instead of one problem's eighth.
-struct GemmGroupArgs {
-  int n = 0;
-  int start[kGroupMax + 1] = {};
-  GemmProb p[kGroupMax];
-};
-
-template <int BM, int BN, bool X3 = false>
-__global__ void __launch_bounds__(256) pw_gemm_group_f32_kernel(GemmGroupArgs g) {
-  const int flat = blockIdx.x;
-  int i = 0;
-  while (i + 1 < g.n && flat >= g.start[i + 1]) ++i;
-  const GemmProb& p = g.p[i];
-  const int local = flat - g.start[i], gx = (p.M + BM - 1) / BM;
-  pw_gemm_f32_tile<BM, BN, X3>(p.x, p.wt, p.bias, nullptr, p.y, p.M, p.N, p.K, p.Kpad, p.Npad, p.act, 0,
-                           (p.Kpad + GKT - 1) / GKT, 0, false, p.yl, (local % gx) * BM, (local / gx) * BN);
-}
 
 // split-K epilogue: y = act(sum_z ws[z] + bias), slabs added in z order
 // (deterministic, unlike fp32 atomics whose arrival order varies)
@@ -2225,27 +1923,25 @@ static int gemm_splits(int M, int N, int Kpad, bool plain) {
 template <int BM, int BN>
 static void pw_gemm_f32_launch(const float* x, const float* wt, const float* bias, const float* res, float* y, int M,
                                int N, int K, int Kpad, int Npad, int act, float* ws, hipStream_t s,
-                               const YLayout& yl = YLayout{}) {
+                               const YLayout& yl = YLayout{}, X3W w3 = X3W{}) {
   dim3 grid((M + BM - 1) / BM, (N + BN - 1) / BN);
   const int kstages = (Kpad + GKT - 1) / GKT;
   int chunk = (ws && !yl.rpb && !yl.brpb && !yl.pool) ? gemm_kchunk(static_cast<int>(grid.x * grid.y), kstages, N, !res) : kstages;
   grid.z = static_cast<unsigned>((kstages + chunk - 1) / chunk);
   const bool x3 = f32_math() == F32Math::kX3;
-  if (grid.z == 1) {
-    if (x3)
-      hipLaunchKernelGGL((pw_gemm_f32_kernel<BM, BN, true>), grid, dim3(256), 0, s, x, wt, bias, res, y, M, N, K, Kpad,
-                         Npad, act, kstages, yl);
-    else
-      hipLaunchKernelGGL((pw_gemm_f32_kernel<BM, BN>), grid, dim3(256), 0, s, x, wt, bias, res, y, M, N, K, Kpad, Npad,
-                         act, kstages, yl);
-    return;
-  }
+  // pre-split weights must cover every row and k-stage a tile reads
+  const bool w3ok = x3 && w3.p && w3.stages >= kstages && w3.rows >= static_cast<int>(grid.y) * BN;
+  const bool split = grid.z > 1;
+  float* out = split ? ws : y;
+  const YLayout ylo = split ? YLayout{} : yl;
+  const int kc = split ? chunk : kstages;
   if (x3)
-    hipLaunchKernelGGL((pw_gemm_f32_kernel<BM, BN, true>), grid, dim3(256), 0, s, x, wt, bias, res, ws, M, N, K, Kpad,
-                       Npad, act, chunk, YLayout{});
+    pw_gemm_x3_launch(BM, BN, w3ok, grid, s, x, wt, w3ok ? w3 : X3W{}, bias, res, out, M, N, K, Kpad, Npad, act, kc,
+                      ylo);
   else
-    hipLaunchKernelGGL((pw_gemm_f32_kernel<BM, BN>), grid, dim3(256), 0, s, x, wt, bias, res, ws, M, N, K, Kpad, Npad,
-                       act, chunk, YLayout{});
+    hipLaunchKernelGGL((pw_gemm_f32_kernel<BM, BN>), grid, dim3(256), 0, s, x, wt, X3W{}, bias, res, out, M, N, K, Kpad,
+                       Npad, act, kc, ylo);
+  if (!split) return;
   const int64_t nq = static_cast<int64_t>(M) * N / 4;
   const unsigned rg = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((nq + 255) / 256, 2048)));
   hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3(rg), dim3(256), 0, s, ws, static_cast<int>(grid.z), M, N, bias,
@@ -2257,6 +1953,17 @@ static void pw_gemm_f32_launch(const float* x, const float* wt, const float* bia
 // prologue/epilogue share, and the grid runs in rounds of 512 co-resident
 // workgroups (256 CUs x 2; every tile here fits two per CU in LDS).
 static int pick_gemm_tile(int M, int N, int Kpad) {
+  // x3: 64 x 64 tiles, but 128 x 64 for deep products (K >= 768) on large grids.
+  // Measured (profiles/r5_x3_tiles_w3.txt, pre-split weights): 64 x 64 is the
+  // best or within 0.5 % on every benched shape but the 7x7 chain's 960 -> 320
+  // (122 vs 113.5 us at 128 x 64); DeepLab's 8712 x 320 x 256 19.0 vs 22.9 us,
+  // MobileNetV2's 100352 x 96 x 576 118.8 vs 125.3, PoseNet's 69696 x 256 x 256
+  // 74.7 vs 79.5.
+  // (the batch-512 classifier, 512 x 1280 x 1000, keeps 128 x 64 as below)
+  if (f32_math() == F32Math::kX3 && M >= 64) {
+    const bool big = static_cast<int64_t>((M + 63) / 64) * ((N + 63) / 64) >= 128;
+    return big && ((M >= 8192 && Kpad >= 768) || (M >= 512 && Kpad >= 1024)) ? 128064 : 64064;
+  }
   // Large grids (>= 128 tiles of 64 x 64; M >= 8192, or M >= 512 with a deep
   // K): 128 x 64 tiles, which re-read the weights half as often per output.
   // The round model below ties them with 64 x 64 there; measured at batch 512
@@ -2314,18 +2021,18 @@ size_t pw_gemm_f32_workspace_bytes(int M, int N, int Kpad, bool has_res, int til
 }
 
 void pw_gemm_f32(const float* x, const float* wt, const float* bias, const float* res, float* y, int M, int N, int K,
-                 int Kpad, int Npad, int act, hipStream_t s, int tile, float* ws, const YLayout& yl) {
+                 int Kpad, int Npad, int act, hipStream_t s, int tile, float* ws, const YLayout& yl, X3W w3) {
   if (use_small_m(M, Kpad, tile, yl)) {
     const dim3 grid(static_cast<unsigned>((N + 15) / 16), static_cast<unsigned>((M + 63) / 64));
     hipLaunchKernelGGL(pw_small_f32_kernel<false>, grid, dim3(256), 0, s, x, wt, bias, res, y, M, N, K, Kpad, Npad, act, 0);
     return;
   }
   switch (resolve_tile(M, N, Kpad, tile)) {
-    case 64064: pw_gemm_f32_launch<64, 64>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s, yl); break;
-    case 128064: pw_gemm_f32_launch<128, 64>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s, yl); break;
-    case 64128: pw_gemm_f32_launch<64, 128>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s, yl); break;
-    case 128192: pw_gemm_f32_launch<128, 192>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s, yl); break;
-    default: pw_gemm_f32_launch<128, 128>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s, yl); break;
+    case 64064: pw_gemm_f32_launch<64, 64>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s, yl, w3); break;
+    case 128064: pw_gemm_f32_launch<128, 64>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s, yl, w3); break;
+    case 64128: pw_gemm_f32_launch<64, 128>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s, yl, w3); break;
+    case 128192: pw_gemm_f32_launch<128, 192>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s, yl, w3); break;
+    default: pw_gemm_f32_launch<128, 128>(x, wt, bias, res, y, M, N, K, Kpad, Npad, act, ws, s, yl, w3); break;
   }
 }
 
@@ -2343,8 +2050,11 @@ void pw_gemm_f32_group(const GemmProb* p, int n, hipStream_t s) {
   }
   if (blocks <= 0 || blocks > (1 << 30)) throw std::invalid_argument("pw_gemm_f32_group: grid");
   g.start[n] = static_cast<int>(blocks);
+  bool w3ok = true;
+  for (int i = 0; i < n; ++i)
+    w3ok = w3ok && p[i].w3.p && p[i].w3.stages >= (p[i].Kpad + GKT - 1) / GKT && p[i].w3.rows >= (p[i].N + 63) / 64 * 64;
   if (f32_math() == F32Math::kX3)
-    hipLaunchKernelGGL((pw_gemm_group_f32_kernel<64, 64, true>), dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, g);
+    pw_gemm_group_x3_launch(w3ok, static_cast<unsigned>(blocks), s, g);
   else
     hipLaunchKernelGGL((pw_gemm_group_f32_kernel<64, 64>), dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, g);
 }
@@ -2435,8 +2145,42 @@ void stem3x3_u8_f32(const uint8_t* x, const float* w, const float* bias, float* 
   stem_f32_launch<uint8_t>(x, w, bias, y, B, H, W, act, lut, s);
 }
 
+namespace {
+__global__ void __launch_bounds__(256) x3_split_weights_kernel(const float* __restrict__ w, int rows, int cols,
+                                                               uint16_t* __restrict__ out, int stages, int rows3) {
+  // pairs (r, c), (r, c + 1) of consecutive k, c even; rows past `rows` are zeros
+  const int64_t npair = static_cast<int64_t>(stages) * rows3 * 16;
+  for (int64_t q = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; q < npair;
+       q += static_cast<int64_t>(gridDim.x) * 256) {
+    const int kp = static_cast<int>(q % 16);
+    const int64_t rs = q / 16;
+    const int r = static_cast<int>(rs % rows3), ks = static_cast<int>(rs / rows3);
+    const int c = ks * 32 + 2 * kp;
+    f32x2_t v;
+    v[0] = r < rows && c < cols ? w[static_cast<int64_t>(r) * cols + c] : 0.f;
+    v[1] = r < rows && c + 1 < cols ? w[static_cast<int64_t>(r) * cols + c + 1] : 0.f;
+    bf16x2_t h, m, l;
+    split2(v, h, m, l);
+    uint16_t* o = out + (static_cast<int64_t>(ks) * rows3 + r) * 96 + 2 * kp;
+    *reinterpret_cast<bf16x2_t*>(o) = h;
+    *reinterpret_cast<bf16x2_t*>(o + 32) = m;
+    *reinterpret_cast<bf16x2_t*>(o + 64) = l;
+  }
+}
+}  // namespace
+
+int x3_split_rows(int rows) { return (rows + 383) / 384 * 384; }
+
+void x3_split_weights(const float* w, int rows, int cols, uint16_t* out, hipStream_t s) {
+  if (rows <= 0 || cols <= 0) throw std::invalid_argument("x3_split_weights: empty weights");
+  const int stages = (cols + GKT - 1) / GKT, rows3 = x3_split_rows(rows);
+  const int64_t npair = static_cast<int64_t>(stages) * rows3 * 16;
+  const unsigned grid = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((npair + 255) / 256, 4096)));
+  hipLaunchKernelGGL(x3_split_weights_kernel, dim3(grid), dim3(256), 0, s, w, rows, cols, out, stages, rows3);
+}
+
 void pw_pool_f32(const float* x, const float* wt, const float* bias, float* y, int B, int HW, int N, int K, int Kpad,
-                 int Npad, int act, hipStream_t s) {
+                 int Npad, int act, hipStream_t s, X3W w3) {
   // larger batches: the tiled GEMM with the pooling epilogue (no [B][HW][N]
   // head output in HBM and no avgpool launch)
   if (B > 8 && HW <= 64) {
@@ -2445,9 +2189,9 @@ void pw_pool_f32(const float* x, const float* wt, const float* bias, float* y, i
     yl.pool = HW;
     const int M = B * HW;
     if (M >= 8192)
-      pw_gemm_f32_launch<128, 64>(x, wt, bias, nullptr, y, M, N, K, Kpad, Npad, act, nullptr, s, yl);
+      pw_gemm_f32_launch<128, 64>(x, wt, bias, nullptr, y, M, N, K, Kpad, Npad, act, nullptr, s, yl, w3);
     else
-      pw_gemm_f32_launch<64, 64>(x, wt, bias, nullptr, y, M, N, K, Kpad, Npad, act, nullptr, s, yl);
+      pw_gemm_f32_launch<64, 64>(x, wt, bias, nullptr, y, M, N, K, Kpad, Npad, act, nullptr, s, yl, w3);
     return;
   }
   const dim3 grid(static_cast<unsigned>((N + 15) / 16), static_cast<unsigned>(B));

@@ -3,6 +3,8 @@
 // and hipGraph capture records them like any other kernel.  CPU
 // implementations are the fp32 numerics reference.
 #include <algorithm>
+#include <mutex>
+#include <unordered_map>
 #include <ATen/ATen.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
@@ -19,6 +21,64 @@ at::Tensor act_ref(at::Tensor v, int64_t act) {
   if (act == 1) return v.clamp(0, 6);
   if (act == 2) return v.clamp_min(0);
   return v;
+}
+
+// ------------------------------------------------- pre-split x3 weights ----
+// The x3 GEMMs stage weights that are already split into their bf16 parts
+// (kernels::X3W): each fp32 weight matrix is split once, at its first GEMM
+// outside a graph capture (tensor_filter runs a model eagerly before it
+// captures), and kept with a reference to the weights -- so the address cannot
+// be reused by another tensor while cached -- and the weights' version, so an
+// in-place update is split again.  Entries whose weights nobody else holds any
+// more (an unloaded model) are dropped at the next miss.
+struct X3Cached {
+  at::Tensor src, parts;
+  int64_t version = -1;
+  nnsx::kernels::X3W w3;
+};
+std::mutex g_x3_mu;
+std::unordered_map<const void*, X3Cached> g_x3;
+bool g_x3_cache_on = true;
+
+// tests: off = every x3 GEMM splits its weights per tile (the capture fallback)
+bool x3_weight_cache(bool on) {
+  std::lock_guard<std::mutex> lk(g_x3_mu);
+  const bool prev = g_x3_cache_on;
+  g_x3_cache_on = on;
+  if (!on) g_x3.clear();
+  return prev;
+}
+
+nnsx::kernels::X3W x3_weights(const at::Tensor& wt) {
+  if (nnsx::kernels::f32_math() != nnsx::kernels::F32Math::kX3 || !wt.is_cuda() || wt.scalar_type() != at::kFloat ||
+      wt.dim() != 2 || !wt.is_contiguous() || wt.numel() == 0)
+    return {};
+  std::lock_guard<std::mutex> lk(g_x3_mu);
+  if (!g_x3_cache_on) return {};
+  auto it = g_x3.find(wt.data_ptr());
+  if (it != g_x3.end() && it->second.src.sizes() == wt.sizes() && it->second.src.device() == wt.device() &&
+      it->second.version == wt._version())
+    return it->second.w3;
+  hipStream_t s = cur_stream();
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return {};  // (per-tile split)
+  for (auto e = g_x3.begin(); e != g_x3.end();) e = e->second.src.use_count() == 1 ? g_x3.erase(e) : std::next(e);
+  const int64_t rows = wt.size(0), cols = wt.size(1), stages = (cols + 31) / 32;
+  X3Cached c;
+  c.src = wt;
+  c.version = wt._version();
+  const int64_t rows3 = nnsx::kernels::x3_split_rows(static_cast<int>(rows));
+  c.parts = at::empty({stages, rows3, 3, 32}, wt.options().dtype(at::kBFloat16));
+  nnsx::kernels::x3_split_weights(wt.data_ptr<float>(), static_cast<int>(rows), static_cast<int>(cols),
+                                  reinterpret_cast<uint16_t*>(c.parts.data_ptr()), s);
+  // other streams (replay lanes) read the parts later: done before first use
+  TORCH_CHECK(hipStreamSynchronize(s) == hipSuccess, "x3 weight split");
+  c.w3.p = reinterpret_cast<const uint16_t*>(c.parts.data_ptr());
+  c.w3.stages = static_cast<int>(stages);
+  c.w3.rows = static_cast<int>(rows3);
+  const nnsx::kernels::X3W w3 = c.w3;
+  g_x3[wt.data_ptr()] = std::move(c);
+  return w3;
 }
 
 // ------------------------------------------------------------ pw_conv ----
@@ -47,7 +107,7 @@ at::Tensor pw_conv_f32_cuda(const at::Tensor& x, const at::Tensor& wt, const at:
   nnsx::kernels::pw_gemm_f32(x.data_ptr<float>(), wt.data_ptr<float>(), bias.data_ptr<float>(), r, y.data_ptr<float>(),
                              static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), static_cast<int>(Kpad),
                              static_cast<int>(Npad), static_cast<int>(act), cur_stream(), static_cast<int>(tile),
-                             wsb ? ws.data_ptr<float>() : nullptr);
+                             wsb ? ws.data_ptr<float>() : nullptr, nnsx::kernels::YLayout{}, x3_weights(wt));
   return y;
 }
 
@@ -116,7 +176,7 @@ void pw_conv_into_cuda(const at::Tensor& x, const at::Tensor& wt, const at::Tens
   nnsx::kernels::pw_gemm_f32(x.data_ptr<float>(), wt.data_ptr<float>(), bias.data_ptr<float>(), nullptr,
                              out.data_ptr<float>() + row0 * C, static_cast<int>(B * HW), static_cast<int>(N),
                              static_cast<int>(K), static_cast<int>(Kpad), static_cast<int>(Npad), static_cast<int>(act),
-                             cur_stream(), 0, nullptr, yl);
+                             cur_stream(), 0, nullptr, yl, x3_weights(wt));
 }
 
 void pw_conv_into_cpu(const at::Tensor& x, const at::Tensor& wt, const at::Tensor& bias, at::Tensor& out,
@@ -222,6 +282,7 @@ void sep_heads_cuda(at::TensorList xs, at::TensorList wds, at::TensorList bds, a
     g.yl.rpb = h.H * h.W;
     g.yl.ncols = h.N;
     g.yl.bstride = h.bstride;
+    g.w3 = x3_weights(wts[order[j]]);
   }
   nnsx::kernels::dw3x3_f32_group(dp, static_cast<int>(n), cur_stream());
   nnsx::kernels::pw_gemm_f32_group(gp, static_cast<int>(n), cur_stream());
@@ -262,6 +323,7 @@ std::vector<at::Tensor> pw_conv_group_cuda(at::TensorList xs, at::TensorList wts
     g.yl.rpb = static_cast<int>(M);  // one "batch" of M rows, N exact columns each
     g.yl.ncols = static_cast<int>(N);
     g.yl.bstride = 0;
+    g.w3 = x3_weights(wts[i]);
     outs.push_back(y);
   }
   nnsx::kernels::pw_gemm_f32_group(gp, static_cast<int>(n), cur_stream());
@@ -313,7 +375,7 @@ at::Tensor pw_conv_rowbias_cuda(const at::Tensor& x, const at::Tensor& wt, const
   nnsx::kernels::pw_gemm_f32(x.data_ptr<float>(), wt.data_ptr<float>(), bias.data_ptr<float>(), nullptr,
                              y.data_ptr<float>(), static_cast<int>(B * HW), static_cast<int>(N), static_cast<int>(K),
                              static_cast<int>(Kpad), static_cast<int>(Npad), static_cast<int>(act), cur_stream(), 0,
-                             nullptr, yl);
+                             nullptr, yl, x3_weights(wt));
   return y;
 }
 
@@ -469,7 +531,8 @@ at::Tensor pw_conv_pool_cuda(const at::Tensor& x, const at::Tensor& wt, const at
   at::Tensor y = at::empty({B, N}, x.options());
   nnsx::kernels::pw_pool_f32(x.data_ptr<float>(), wt.data_ptr<float>(), bias.data_ptr<float>(), y.data_ptr<float>(),
                              static_cast<int>(B), static_cast<int>(HW), static_cast<int>(N), static_cast<int>(K),
-                             static_cast<int>(Kpad), static_cast<int>(Npad), static_cast<int>(act), cur_stream());
+                             static_cast<int>(Kpad), static_cast<int>(Npad), static_cast<int>(act), cur_stream(),
+                             x3_weights(wt));
   return y;
 }
 
@@ -744,6 +807,7 @@ std::string set_f32_math(const std::string& m) {
 TORCH_LIBRARY(nnsx, m) {
   m.def("f32_math() -> str", f32_math);
   m.def("set_device_shared(bool on) -> bool", set_device_shared);
+  m.def("x3_weight_cache(bool on) -> bool", x3_weight_cache);
   m.def("ir_method_f32(int stride, int H, int W, int cin, int hid, int cout, int B, int dilation=1) -> str",
         ir_method_f32);
   m.def("set_f32_math(str method) -> str", set_f32_math);

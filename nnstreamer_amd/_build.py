@@ -27,6 +27,8 @@ CXX = os.environ.get("NNSX_CXX", "/opt/rocm/lib/llvm/bin/clang++")
 TORCH_SOURCES = {"filter/pytorch.cc", "filter/torch_trainer.cc", "ops/torch_ops.cc"}
 # pybind11 sources
 PY_SOURCES = {"bindings/module.cc", "bindings/python_bridge.cc"}
+# per-unit code generation: the x3 GEMMs keep MFMA results in VGPRs (kernels/gemm_f32.h)
+UNIT_FLAGS = {"kernels/gemm_x3.hip": "-mllvm -amdgpu-mfma-vgpr-form"}
 
 
 def ext_suffix() -> str:
@@ -117,6 +119,8 @@ def write_ninja(debug: bool = False) -> str:
             extra = torch_flags
         if rel in PY_SOURCES:
             extra += " " + py_flags
+        if rel in UNIT_FLAGS:
+            extra += " " + UNIT_FLAGS[rel]
         rule = "hip" if rel.endswith(".hip") else "cxx"
         lines.append(f"build {obj}: {rule} {os.path.join(CSRC, rel)}")
         if extra:

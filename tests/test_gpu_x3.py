@@ -100,6 +100,78 @@ def test_x3_split_is_exact_for_fp32_operands(nns, method):
     torch.testing.assert_close(y, x, rtol=0, atol=0)
 
 
+@pytest.fixture
+def x3_cache():
+    prev = torch.ops.nnsx.x3_weight_cache(True)
+    yield lambda on: torch.ops.nnsx.x3_weight_cache(on)
+    torch.ops.nnsx.x3_weight_cache(prev)
+
+
+@pytest.mark.parametrize("tile", [0, 64064, 128064, 64128, 128128, 128192])
+@pytest.mark.parametrize("M,K,N", [(6272, 960, 320), (4225, 64, 128), (1000, 24, 144), (130, 1280, 1000)])
+def test_x3_presplit_weights_match_per_tile_split(nns, method, x3_cache, tile, M, K, N):
+    """The pre-split weight path (weights split once, staged as bf16 parts) and
+    the per-tile split give the same bits: same RNE parts, same products"""
+    method("x3")
+    torch.manual_seed(M + K + N + tile)
+    x = (torch.randn(M, K, device="cuda") * 2).clamp(0, 6)
+    npad, kpad = (N + 15) // 16 * 16, (K + 7) // 8 * 8
+    wt = torch.zeros(npad, kpad, device="cuda")
+    wt[:N, :K] = torch.randn(N, K, device="cuda") / K ** 0.5
+    bias = torch.randn(npad, device="cuda") * 0.1
+    x3_cache(False)
+    y0 = torch.ops.nnsx.pw_conv_f32_tile(x, wt, bias, None, N, 1, tile)
+    x3_cache(True)
+    y1 = torch.ops.nnsx.pw_conv_f32_tile(x, wt, bias, None, N, 1, tile)
+    y2 = torch.ops.nnsx.pw_conv_f32_tile(x, wt, bias, None, N, 1, tile)  # (cache hit)
+    assert torch.equal(y0, y1) and torch.equal(y1, y2)
+
+
+def test_x3_presplit_weights_follow_in_place_updates(nns, method, x3_cache):
+    """An in-place change of the weights is split again (version check), and a
+    new weight tensor is never served another's parts"""
+    method("x3")
+    torch.manual_seed(5)
+    x = torch.randn(2048, 96, device="cuda")
+    wt = torch.randn(160, 96, device="cuda") / 10
+    bias = torch.zeros(160, device="cuda")
+    y1 = torch.ops.nnsx.pw_conv(x, wt, bias, None, 160, 0, True)
+    wt.mul_(2)
+    y2 = torch.ops.nnsx.pw_conv(x, wt, bias, None, 160, 0, True)
+    torch.testing.assert_close(y2, 2 * y1, rtol=1e-6, atol=1e-6)
+    wt2 = torch.randn(160, 96, device="cuda") / 10
+    ref = (x.double() @ wt2.double().t()).float()
+    torch.testing.assert_close(torch.ops.nnsx.pw_conv(x, wt2, bias, None, 160, 0, True), ref, rtol=1e-5, atol=1e-5)
+
+
+def test_x3_presplit_weights_grouped_and_pooled(nns, method, x3_cache):
+    """pw_conv_group (PoseNet heads), pw_conv_pool (head + pool), pw_conv_into
+    and pw_conv_rowbias: the same bits with and without the pre-split weights"""
+    method("x3")
+    torch.manual_seed(9)
+    xs = [torch.randn(4, 17, 17, 64, device="cuda").clamp(0, 6), torch.randn(4, 9, 9, 128, device="cuda").clamp(0, 6)]
+    wts = [torch.randn(48, 64, device="cuda") / 8, torch.randn(32, 128, device="cuda") / 11]
+    bs = [torch.randn(48, device="cuda"), torch.randn(32, device="cuda")]
+    xp = torch.randn(64, 7, 7, 320, device="cuda").clamp(0, 6)
+    wp = torch.randn(1280, 320, device="cuda") / 18
+    bp = torch.randn(1280, device="cuda")
+    rb = torch.randn(4, 256, device="cuda")
+    wr = torch.randn(256, 64, device="cuda") / 8
+
+    def run():
+        out = torch.zeros(4, 17 * 17 * 2 + 5, 24, device="cuda")
+        torch.ops.nnsx.pw_conv_into(xs[0], wts[0], bs[0], out, 5, 48, 0)
+        return (torch.ops.nnsx.pw_conv_group(xs, wts, bs, [48, 32], [0, 1])
+                + [torch.ops.nnsx.pw_conv_pool(xp, wp, bp, 1280, 1), out,
+                   torch.ops.nnsx.pw_conv_rowbias(xs[0], wr, rb, 256, 1)])
+    x3_cache(False)
+    a = run()
+    x3_cache(True)
+    b = run()
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
+
+
 @pytest.mark.parametrize("B,H", [(9, 7), (64, 7), (171, 7)])
 def test_x3_head_pool_no_worse_than_native(nns, method, B, H):
     torch.manual_seed(B * 7 + H)
