@@ -28,7 +28,7 @@ TORCH_SOURCES = {"filter/pytorch.cc", "filter/torch_trainer.cc", "ops/torch_ops.
 # pybind11 sources
 PY_SOURCES = {"bindings/module.cc", "bindings/python_bridge.cc"}
 # per-unit code generation: the x3 GEMMs keep MFMA results in VGPRs (kernels/gemm_f32.h)
-UNIT_FLAGS = {"kernels/gemm_x3.hip": "-mllvm -amdgpu-mfma-vgpr-form"}
+UNIT_FLAGS = {"kernels/gemm_x3.hip": "-mllvm -amdgpu-mfma-vgpr-form", "kernels/irw_x3.hip": "-mllvm -amdgpu-mfma-vgpr-form"}
 
 
 def ext_suffix() -> str:

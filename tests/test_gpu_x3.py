@@ -256,7 +256,7 @@ def test_x3_ir_block_hidden_parts(nns, method, H, cin, hid, cout, stride, B):
 
 @pytest.mark.parametrize("B", [128, 3, 1])
 def test_x3_ir_expand_dw(nns, method, B):
-    """the expand + depthwise kernel (the x3 twin runs under NNSX_X3_IRW=1 only)"""
+    """the expand + depthwise kernel (7x7 160 -> 960: the x3 twin is the default)"""
     import torch.nn.functional as F
 
     cin, hid, H = 160, 960, 7
