@@ -30,6 +30,8 @@ struct IrwCfg {
   // > 0: only for exactly tiled maps and batches >= min_batch (find_irw with the
   // launch's batch; a support query without one never picks it)
   int min_batch = 0;
+  // > 0: only for batches <= max_batch (a support query must name its batch)
+  int max_batch = 0;
 };
 
 // the x3 twins of the fused-block configurations (kernels/irw_x3.hip)

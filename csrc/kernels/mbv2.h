@@ -216,7 +216,8 @@ bool device_shared();
 // set this thread's flag directly (tests); returns the previous value
 bool set_device_shared(bool on);
 
-bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout, bool has_expand, int dil = 1);
+bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout, bool has_expand, int dil = 1,
+                            int B = 0);
 // device workspace ir_block_f32 needs for these args (0 = none)
 size_t ir_block_f32_workspace_bytes(const IrBlockF32Args& a);
 // int tickets (zeroed) the in-launch combine of hidden parts wants (0: none)

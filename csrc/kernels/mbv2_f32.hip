@@ -707,9 +707,24 @@ __global__ void __launch_bounds__(256) ir_block_f32_kernel(IrBlockF32Args a) {
 // block, 2 waves per SIMD instead of 3, and ran 757 vs 545 us at batch 512:
 // profiles/r3_irw_persistent_ab_b512.txt.)
 // DIL: depthwise dilation (padding DIL; DeepLab's output-stride-16 blocks)
-template <int S, int TY, int TX, int KIN, int NOT, int NW, bool FULL, int DIL = 1>
+// XE: the expand on split-bf16 MFMAs (x3, kernels/x3.h) -- the input tile split
+// into three bf16 planes while it is staged (as irw_x3 does), the expand
+// weights pre-split (we3), 6 v_mfma_f32_16x16x32_bf16 per 32 input channels
+// against 8 x 4 v_mfma_f32_16x16x4_f32; the depthwise and the project stay
+// native fp32.  (irw_x3 also moves the project to x3, which costs a register
+// split of every depthwise output and 32x32 accumulators.)
+template <int S, int TY, int TX, int KIN, int NOT, int NW, bool FULL, int DIL = 1, bool XE = false>
+struct IrwXEGeom {
+  using Base = IrwGeom<S, TY, TX, KIN, NOT, NW, FULL, DIL>;
+  static constexpr int KP = (KIN + 31) / 32 * 32, K8 = KP / 8, NK32 = KP / 32;
+  static constexpr size_t xs_b = XE ? static_cast<size_t>(3) * K8 * Base::XSP * 16 : 16 * Base::xs_q;
+  static size_t lds_bytes(int) { return std::max(xs_b + 16 * Base::hid_q, 16 * Base::red_q); }
+};
+
+template <int S, int TY, int TX, int KIN, int NOT, int NW, bool FULL, int DIL = 1, bool XE = false>
 __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FULL>::MINB)) irw_f32_kernel(IrBlockF32Args a) {
   using G = IrwGeom<S, TY, TX, KIN, NOT, NW, FULL, DIL>;
+  using GX = IrwXEGeom<S, TY, TX, KIN, NOT, NW, FULL, DIL, XE>;
   constexpr int NT = 64 * NW;
   constexpr int TIY = G::TIY, TIX = G::TIX, PIN = G::PIN, NC16 = G::NC16, NBT = G::NBT, XSP = G::XSP;
   constexpr int PINP = G::PINP;
@@ -717,10 +732,12 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
   constexpr int KQ = G::KQ, NPT = G::NPT, NPX = G::NPX;
   constexpr int NS16 = KIN / 16;
   constexpr bool KT8 = (KIN % 16) != 0;
+  constexpr int KP = GX::KP, K8 = GX::K8, NK32 = GX::NK32;
   static_assert(KIN % 8 == 0, "irw_f32: KIN % 8");
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  f32x4_t* xs = reinterpret_cast<f32x4_t*>(smem);  // [KQ][XSP]
-  f32x4_t* hidw = xs + G::xs_q;                     // [NW waves][4 quads][PINP]
+  f32x4_t* xs = reinterpret_cast<f32x4_t*>(smem);     // [KQ][XSP] (fp32 expand)
+  bf16x8_t* xs3 = reinterpret_cast<bf16x8_t*>(smem);  // [3][K8][XSP] (XE), cell swizzled by k8
+  f32x4_t* hidw = reinterpret_cast<f32x4_t*>(reinterpret_cast<char*>(smem) + GX::xs_b);  // [NW][4][PINP]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, g = lane >> 4;
@@ -733,7 +750,8 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
   // select zero), then the LDS stores.  A load under a branch became
   // load / s_waitcnt vmcnt(0) / store per iteration, one exposed memory
   // latency per 256 quads of the tile.
-  constexpr int NSV = NC16 * KQ, NSIT = (NSV + NT - 1) / NT;
+  constexpr int KQS = XE ? KP / 4 : KQ;  // quads staged per cell (XE: zeros up to the 32-channel pad)
+  constexpr int NSV = NC16 * KQS, NSIT = (NSV + NT - 1) / NT;
   f32x4_t sv[NSIT];
   bool sok[NSIT];
   // c / RW for the small compact indices (c < 1024): (c + 0.5) * (1 / RW) in
@@ -749,7 +767,7 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
 #pragma unroll
     for (int it = 0; it < NSIT; ++it) {
       const int v = tid + it * NT;
-      const int c = v / KQ, kq = v - c * KQ;
+      const int c = v / KQS, kq = v - c * KQS;
       int yy, xx;
       if constexpr (FULL) {
         yy = ty0 + c / TIX;
@@ -781,8 +799,24 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
   for (int it = 0; it < NSIT; ++it) {
     const int v = tid + it * NT;
     if (NSV % NT != 0 && v >= NSV) break;
-    const int c = v / KQ, kq = v - c * KQ;
-    xs[kq * XSP + (c ^ (kq & 3))] = sok[it] ? sv[it] : f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const int c = v / KQS, kq = v - c * KQS;
+    const f32x4_t q = sok[it] ? sv[it] : f32x4_t{0.f, 0.f, 0.f, 0.f};
+    if constexpr (XE) {
+      // three bf16 planes [part][k8][cell], 8 channels (16 B) per cell, cells
+      // XOR-swizzled by k8 within their 16-cell group (irw_x3's layout)
+      typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+      const int k8 = kq >> 1;
+      bf16x2_t h0, m0, l0, h1, m1, l1;
+      split2(f32x2_t{q[0], q[1]}, h0, m0, l0);
+      split2(f32x2_t{q[2], q[3]}, h1, m1, l1);
+      char* p = reinterpret_cast<char*>(xs3) + (static_cast<size_t>(k8) * XSP + (c ^ (k8 & 15))) * 16 + (kq & 1) * 8;
+      constexpr size_t PS = static_cast<size_t>(K8) * XSP * 16;  // part stride (bytes)
+      *reinterpret_cast<bf16x4_t*>(p) = __builtin_shufflevector(h0, h1, 0, 1, 2, 3);
+      *reinterpret_cast<bf16x4_t*>(p + PS) = __builtin_shufflevector(m0, m1, 0, 1, 2, 3);
+      *reinterpret_cast<bf16x4_t*>(p + 2 * PS) = __builtin_shufflevector(l0, l1, 0, 1, 2, 3);
+    } else {
+      xs[kq * XSP + (c ^ (kq & 3))] = q;
+    }
   }
   // out-of-image halo cells of every wave's hidden image = the depthwise zero padding
   // (FULL: the expand itself writes them as zeros)
@@ -829,7 +863,8 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
   const int nsub = a.hid >> 4;
   const int sub0 = part * nsub / nparts, sub1 = (part + 1) * nsub / nparts;
   f32x4_t* myhid = hidw + (wave * 4 + g) * PINP;
-  f32x4_t ea[NS16 > 0 ? NS16 : 1];
+  f32x4_t ea[XE ? 1 : (NS16 > 0 ? NS16 : 1)];
+  X3Frag ea3[XE ? NK32 : 1];
   f32x2_t et = f32x2_t{0.f, 0.f};
   f32x4_t be4 = f32x4_t{0.f, 0.f, 0.f, 0.f};
   // PREB: the expand bias is fetched one subtile ahead with the expand
@@ -843,10 +878,18 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
   // large-map 3-wave configurations use it.
   constexpr bool PREB = FULL && NW == 3 && TY * TX >= 32;
   auto load_ea = [&](int hs) {
-    const float* wrow = a.we + static_cast<int64_t>(hs * 16 + li) * KIN;
+    if constexpr (XE) {
+      // we3 [3][hid][KP] bf16: lane (li, g) holds k 8g .. 8g + 7 of each 32-k step of row hs * 16 + li
+      const int64_t wes = static_cast<int64_t>(a.hid) * KP;
 #pragma unroll
-    for (int s = 0; s < NS16; ++s) ea[s] = *reinterpret_cast<const f32x4_t*>(wrow + 16 * s + 4 * g);
-    if constexpr (KT8) et = *reinterpret_cast<const f32x2_t*>(wrow + 16 * NS16 + 2 * g);
+      for (int c = 0; c < NK32; ++c)
+        ea3[c] = load_x3(a.we3, wes, static_cast<int64_t>(hs * 16 + li) * KP + 32 * c + 8 * g);
+    } else {
+      const float* wrow = a.we + static_cast<int64_t>(hs * 16 + li) * KIN;
+#pragma unroll
+      for (int s = 0; s < NS16; ++s) ea[s] = *reinterpret_cast<const f32x4_t*>(wrow + 16 * s + 4 * g);
+      if constexpr (KT8) et = *reinterpret_cast<const f32x2_t*>(wrow + 16 * NS16 + 2 * g);
+    }
     if constexpr (PREB) be4 = *reinterpret_cast<const f32x4_t*>(a.be + hs * 16 + 4 * g);
   };
   int hs = sub0 + wave;
@@ -871,7 +914,7 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
       // read before this pair's MFMAs and hidden stores -- xs and the hidden
       // images share the LDS array, so reads placed after the stores cannot be
       // hoisted above them and each pair waited for its own LDS round trip
-      constexpr bool PREX = FULL && NS16 == 1;
+      constexpr bool PREX = FULL && NS16 == 1 && !XE;
       f32x4_t bx0 = f32x4_t{0.f, 0.f, 0.f, 0.f}, bx1 = bx0;
       if constexpr (PREX) {
         bx0 = xs[g * XSP + (li ^ g)];
@@ -882,7 +925,23 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
         if (FULL || j < nbt) {
           const int j1 = j + 1 < NBT ? j + 1 : j;
           f32x4_t e0 = f32x4_t{0.f, 0.f, 0.f, 0.f}, e1 = e0;
-          if constexpr (PREX) {
+          if constexpr (XE) {
+#pragma unroll
+            for (int c = 0; c < NK32; ++c) {
+              const int k8 = 4 * c + g;
+              const bf16x8_t* pl = xs3 + k8 * XSP;
+              const int c0 = (j * 16 + li) ^ (k8 & 15), c1 = (j1 * 16 + li) ^ (k8 & 15);
+              X3Frag b0, b1;
+              b0.h = pl[c0];
+              b0.m = pl[K8 * XSP + c0];
+              b0.l = pl[2 * K8 * XSP + c0];
+              b1.h = pl[c1];
+              b1.m = pl[K8 * XSP + c1];
+              b1.l = pl[2 * K8 * XSP + c1];
+              e0 += mfma_x3(ea3[c], b0);
+              e1 += mfma_x3(ea3[c], b1);
+            }
+          } else if constexpr (PREX) {
             f32x4_t n0 = bx0, n1 = bx1;
             if (j + 2 < NBT) {
               const int k1 = j + 3 < NBT ? j + 3 : j + 2;
@@ -900,7 +959,7 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
               e1 = mfma_k16(ea[s], xs[(4 * s + g) * XSP + j1 * 16 + (li ^ g)], e1);
             }
           }
-          if constexpr (KT8) {
+          if constexpr (KT8 && !XE) {
             // tail plane kq = 4 NS16 + g/2: swizzle (kq & 3) = g >> 1
             const f32x2_t* t0 =
                 reinterpret_cast<const f32x2_t*>(&xs[(4 * NS16 + g / 2) * XSP + j * 16 + (li ^ (g >> 1))]);
@@ -1293,10 +1352,10 @@ int tile_pref(int S, int H, int W, int TY, int TX) {
     S, TY, TX, KIN, NOT, NW, F, &irw_f32_kernel<S, TY, TX, KIN, NOT, NW, F>,                    \
         &IrwGeom<S, TY, TX, KIN, NOT, NW, F>::lds_bytes, 1, MB                                  \
   }
-#define NNSX_IRWD(S, TY, TX, KIN, NOT, NW, F, D)                                                \
+#define NNSX_IRWD(S, TY, TX, KIN, NOT, NW, F, D, MAXB)                                          \
   IrwCfg {                                                                                      \
     S, TY, TX, KIN, NOT, NW, F, &irw_f32_kernel<S, TY, TX, KIN, NOT, NW, F, D>,                 \
-        &IrwGeom<S, TY, TX, KIN, NOT, NW, F, D>::lds_bytes, D                                   \
+        &IrwGeom<S, TY, TX, KIN, NOT, NW, F, D>::lds_bytes, D, 0, MAXB                          \
   }
 // (NW = waves per workgroup: a divisor of the hidden subtile count where possible,
 // so every wave walks the same number of 16-channel subtiles)
@@ -1336,8 +1395,10 @@ const IrwCfg kIrwCfgs[] = {
     // (dilation 2 -- DeepLab's output-stride-16 blocks on 33x33 maps -- as
     // NNSX_IRWD(1, 7, 7, 160, 10, 4, false, 2) etc. ran 156 vs 120 us for the
     // unfused expand GEMM + dilated depthwise + project GEMM at batch 8 (the
-    // 11x11 halo window needs 112 KB of LDS: one workgroup per CU), so the
-    // dilated blocks stay unfused: profiles/r3_config_trace_deeplab_b8.txt)
+    // 11x11 halo window needs 112 KB of LDS: one workgroup per CU), and at
+    // batch 1 / 2 0.499 / 0.654 vs 0.488 / 0.565 ms per step, so the dilated
+    // blocks stay unfused: profiles/r3_config_trace_deeplab_b8.txt,
+    // profiles/r5_deeplab_b1.txt)
     // (one wave per 16-channel subtile -- 6 waves on 112 -> 56, 9 on 56 -> 28 --
     // ran 2x slower: the hidden images of all waves then limit the CU to one
     // workgroup; profiles/r3_irw_waves_ab_b512.txt)
@@ -1346,13 +1407,44 @@ const IrwCfg kIrwCfgs[] = {
 #undef NNSX_IRWB
 #undef NNSX_IRWD
 
-// NNSX_X3_IRW=1: the fused blocks on irw_x3 under x3 (off until measured on the GPU)
-bool x3_irw_enabled() {
-  static const bool on = [] {
+// NNSX_X3_IRW (A/B): 1 = every fused block on its irw_x3 twin, 2 = every
+// block with an expand-x3 twin (irw_f32 XE) on it; unset = the measured defaults
+static int x3_irw_mode() {
+  static const int m = [] {
     const char* e = std::getenv("NNSX_X3_IRW");
-    return e && e[0] == '1';
+    return e && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : 0;
   }();
-  return on;
+  return m;
+}
+bool x3_irw_enabled() { return x3_irw_mode() == 1; }
+
+// the expand-x3 twins (irw_f32_kernel<..., XE = true>) of the native configurations
+#define NNSX_IRWE(S, TY, TX, KIN, NOT, NW, F)                                                   \
+  IrwCfg {                                                                                      \
+    S, TY, TX, KIN, NOT, NW, F, &irw_f32_kernel<S, TY, TX, KIN, NOT, NW, F, 1, true>,           \
+        &IrwXEGeom<S, TY, TX, KIN, NOT, NW, F, 1, true>::lds_bytes, 1                           \
+  }
+const IrwCfg kIrwXECfgs[] = {
+    NNSX_IRWE(2, 4, 8, 16, 2, 3, true),   NNSX_IRWE(1, 8, 8, 24, 2, 3, true),   NNSX_IRWE(2, 4, 4, 24, 2, 3, true),
+    NNSX_IRWE(2, 2, 7, 32, 4, 4, false),  NNSX_IRWE(1, 7, 14, 64, 4, 4, false), NNSX_IRWE(1, 7, 7, 64, 4, 4, false),
+    NNSX_IRWE(1, 7, 7, 64, 6, 4, false),  NNSX_IRWE(1, 7, 7, 96, 6, 4, false),  NNSX_IRWE(2, 7, 7, 96, 10, 4, false),
+};
+#undef NNSX_IRWE
+
+// the expand-x3 twin of a native configuration (same tile, waves and parts)
+static const IrwCfg* xe_twin(const IrwCfg* c, const IrBlockF32Args& a) {
+  if (!c || f32_math() != F32Math::kX3 || !a.we3 || !a.has_expand) return nullptr;
+  // by default where measured faster (scripts/x3_blocks_ab.py with NNSX_X3_IRW=2,
+  // batch 512, profiles/r5_xe_blocks_ab.txt): 56 -> 28 265 -> 244 us, 28 -> 14
+  // 129 -> 121 us; 56x56 and the 14x14 blocks lost 6-27 % (the split planes'
+  // LDS and the extra registers; the 14x14 configurations spill)
+  const bool dflt = c->S == 2 && ((c->KIN == 24 && c->TY == 4 && c->TX == 4) || (c->KIN == 32 && c->NOT == 4));
+  if (x3_irw_mode() != 2 && !dflt) return nullptr;
+  for (const IrwCfg& x : kIrwXECfgs)
+    if (x.S == c->S && x.TY == c->TY && x.TX == c->TX && x.KIN == c->KIN && x.NOT == c->NOT && x.NW == c->NW &&
+        x.full == c->full && x.dil == c->dil && x.lds(a.hid) <= 160 * 1024)
+      return &x;
+  return nullptr;
 }
 
 // the x3 twin of a configuration, when the method is x3 and both weight
@@ -1369,7 +1461,7 @@ const IrwCfg* x3_twin(const IrwCfg* c, const IrBlockF32Args& a) {
   // the native kernel's -- the accuracy gate of test_gpu_x3.py.)
   // NNSX_X3_IRW=1: every configuration with a twin (A/B)
   const bool dflt = c->S == 1 && ((c->KIN == 160 && (c->NOT == 10 || c->NOT == 0)) || (c->KIN == 32 && c->NOT == 2));
-  if (!x3_irw_enabled() && !dflt) return nullptr;
+  if (x3_irw_mode() == 2 || (!x3_irw_enabled() && !dflt)) return xe_twin(c, a);
   // the same tile, else (7 x 14 tiles: their 4 32-pixel project tiles hold more
   // accumulators than two waves per SIMD allow) the 7 x 7 tile of the shape
   for (int pass = 0; pass < 2; ++pass)
@@ -1409,21 +1501,24 @@ const IrwCfg* find_irw(int S, int H, int W, int cin, int hid, int cout, bool has
     for (size_t i = 0; i < sizeof(kIrwCfgs) / sizeof(kIrwCfgs[0]); ++i) {
       const IrwCfg& c = kIrwCfgs[i];
       if (c.S == S && c.dil == dil && c.KIN == kin && c.NOT == nout && (!exact || (Ho % c.TY == 0 && Wo % c.TX == 0)) &&
-          c.lds(hid) <= 160 * 1024 && !irw_skipped(i) && (c.min_batch == 0 || (exact && B >= c.min_batch)))
+          c.lds(hid) <= 160 * 1024 && !irw_skipped(i) && (c.min_batch == 0 || (exact && B >= c.min_batch)) &&
+          (c.max_batch == 0 || (B > 0 && B <= c.max_batch)))
         return &c;
     }
   return nullptr;
 }
 
-const IrwCfg* find_irw_dw(int S, int H, int W, int cin, int hid, int dil = 1) {
+const IrwCfg* find_irw_dw(int S, int H, int W, int cin, int hid, int dil = 1, int B = 0) {
   if (hid % 16) return nullptr;
   const int kin = (cin + 7) / 8 * 8;
   const int Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
   for (int exact = 1; exact >= 0; --exact)
-    for (const auto& c : kIrwCfgs)
+    for (size_t i = 0; i < sizeof(kIrwCfgs) / sizeof(kIrwCfgs[0]); ++i) {
+      const IrwCfg& c = kIrwCfgs[i];
       if (c.NOT == 0 && c.S == S && c.dil == dil && c.KIN == kin && (!exact || (Ho % c.TY == 0 && Wo % c.TX == 0)) &&
-          c.lds(hid) <= 160 * 1024)
+          c.lds(hid) <= 160 * 1024 && !irw_skipped(i) && (c.max_batch == 0 || (B > 0 && B <= c.max_batch)))
         return &c;
+    }
   return nullptr;
 }
 
@@ -1465,7 +1560,9 @@ const char* f32_math_name(F32Math m) { return m == F32Math::kX3 ? "x3" : "fp32";
 // tiles of 64 x 64) -- otherwise most CUs idle while each workgroup walks all
 // of K.  Returns the k-stages per slice (kstages: no split).
 static int gemm_kchunk(int tiles, int kstages, int N, bool plain) {
-  if (!plain || tiles >= 128 || kstages < 8 || N % 4) return kstages;
+  // (K < 384: the reduce launch costs about what the split saves -- DeepLab's
+  // batch-1 ASPP 1x1 conv, K = 320, runs unsplit: one launch fewer)
+  if (!plain || tiles >= 128 || kstages < 12 || N % 4) return kstages;
   const int splits = std::min(kstages / 4, (512 + tiles - 1) / tiles);
   return (kstages + splits - 1) / splits;
 }
@@ -1762,10 +1859,10 @@ void avgpool_f32(const float* x, float* y, int B, int HW, int C, hipStream_t s) 
   hipLaunchKernelGGL(avgpool_f32_kernel, dim3(static_cast<unsigned>(B * groups)), dim3(256), 0, s, x, y, HW, C);
 }
 
-bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout, bool has_expand, int dil) {
+bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout, bool has_expand, int dil, int B) {
   if (stride != 1 && stride != 2) return false;
   if (cin % 8 || cout % 4 || hid % 16) return false;
-  if (dil != 1) return find_irw(stride, H, W, cin, hid, cout, has_expand, dil) != nullptr;
+  if (dil != 1) return find_irw(stride, H, W, cin, hid, cout, has_expand, dil, B) != nullptr;
   return find_irw(stride, H, W, cin, hid, cout, has_expand) != nullptr ||
          find_cfg(stride, H, W, cin, hid, cout, has_expand) != nullptr;
 }
@@ -1900,7 +1997,7 @@ static bool launch_irw(const IrwCfg* c, IrBlockF32Args a, hipStream_t s) {
 // depthwise kernel (46 us) beat this kernel (54 us); at batch 1 it saves a
 // launch and 4 us
 bool ir_expand_dw_f32_supported(int stride, int H, int W, int cin, int hid, int B, int dil) {
-  const IrwCfg* c = cin % 8 == 0 ? find_irw_dw(stride, H, W, cin, hid, dil) : nullptr;
+  const IrwCfg* c = cin % 8 == 0 ? find_irw_dw(stride, H, W, cin, hid, dil, B) : nullptr;
   if (!c) return false;
   if (dil != 1) return true;  // (the alternative is an unfused dilated depthwise pass over the hidden map)
   const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
@@ -1909,7 +2006,7 @@ bool ir_expand_dw_f32_supported(int stride, int H, int W, int cin, int hid, int 
 
 bool ir_expand_dw_f32(const IrBlockF32Args& args, hipStream_t s) {
   IrBlockF32Args a = args;
-  const IrwCfg* c = find_irw_dw(a.stride, a.H, a.W, a.cin, a.hid, a.dil);
+  const IrwCfg* c = find_irw_dw(a.stride, a.H, a.W, a.cin, a.hid, a.dil, a.B);
   if (!c || !a.has_expand) return false;
   if (const IrwCfg* x = x3_twin(c, a)) c = x;
   irw_geometry(c, &a);

@@ -767,10 +767,10 @@ at::Tensor stem_ir1_cpu(const at::Tensor& x, const at::Tensor& ws, const at::Ten
 }
 
 bool ir_supported_f32(int64_t stride, int64_t H, int64_t W, int64_t cin, int64_t hid, int64_t cout, bool has_expand,
-                      int64_t dilation) {
+                      int64_t dilation, int64_t B) {
   return nnsx::kernels::ir_block_f32_supported(static_cast<int>(stride), static_cast<int>(H), static_cast<int>(W),
                                                static_cast<int>(cin), static_cast<int>(hid), static_cast<int>(cout),
-                                               has_expand, static_cast<int>(dilation));
+                                               has_expand, static_cast<int>(dilation), static_cast<int>(B));
 }
 
 bool ir_supported(int64_t stride, int64_t cin, int64_t hid, int64_t cout) {
@@ -830,7 +830,8 @@ TORCH_LIBRARY(nnsx, m) {
         "bool has_expand, bool residual, int dilation=1, Tensor(a!)? tickets=None, Tensor? we3=None, "
         "Tensor? wp3=None) -> Tensor");
   m.def("ir_supported(int stride, int cin, int hid, int cout) -> bool", ir_supported);
-  m.def("ir_supported_f32(int stride, int H, int W, int cin, int hid, int cout, bool has_expand, int dilation=1) -> bool",
+  m.def("ir_supported_f32(int stride, int H, int W, int cin, int hid, int cout, bool has_expand, int dilation=1, "
+        "int B=0) -> bool",
         ir_supported_f32);
   m.def("ir_expand_dw_supported_f32(int stride, int H, int W, int cin, int hid, int B=0, int dilation=1) -> bool",
         ir_expand_dw_supported_f32);

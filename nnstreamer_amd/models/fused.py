@@ -209,7 +209,7 @@ class Block(nn.Module):
             # (dilation 2: DeepLab's output-stride-16 blocks, instantiated for 33x33 maps)
             if self.use_ir and bool(torch.ops.nnsx.ir_supported_f32(
                     self.dw.stride, x.shape[1], x.shape[2], self.cin, self.hid, self.cout, self.has_expand,
-                    self.dw.dilation)):
+                    self.dw.dilation, x.shape[0])):
                 return torch.ops.nnsx.ir_block(x, self.ir_we, self.ir_be, self.ir_wd, self.ir_bd, self.ir_wp,
                                                self.project.bias, self.dw.stride, self.cout, self.has_expand,
                                                self.use_res, self.dw.dilation, self.ir_tickets, self.ir_we3,

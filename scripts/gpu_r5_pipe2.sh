@@ -1,0 +1,12 @@
+#!/bin/bash
+set -eo pipefail
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+timeout -k 10 120 python -u scripts/x3_check.py > gpurun_out/chk_new.txt 2>&1
+grep -c "e-0[67]" gpurun_out/chk_new.txt
+grep -v "e-0[67]" gpurun_out/chk_new.txt | head -5
+timeout -k 10 600 python -u -m pytest tests/test_gpu_x3.py tests/test_gpu_mbv2_f32.py tests/test_gpu_models_f32.py -q -x --timeout 300 --timeout-method thread > gpurun_out/pp_tests.txt 2>&1
+tail -2 gpurun_out/pp_tests.txt
+timeout -k 10 300 python -u scripts/x3_tiles.py > gpurun_out/pp_tiles_new.txt 2>&1
+timeout -k 10 300 python -u variants/base/scripts/x3_tiles.py > gpurun_out/pp_tiles_base.txt 2>&1
+SPECS="mbv2:512 posenet:64 deeplab:8" bash scripts/gpu_ab_variant.sh

@@ -133,7 +133,7 @@ IR_F32_SHAPES = [(112, 32, 32, 16, 1, False), (112, 16, 96, 24, 2, True), (56, 2
                  (10, 160, 960, 160, 1, True), (19, 96, 576, 160, 2, True)]
 
 
-def _ir_ref64(x, we, be, wd, bd, wp, bp, stride, cout, has_expand, residual):
+def _ir_ref64(x, we, be, wd, bd, wp, bp, stride, cout, has_expand, residual, dil=1):
     x64 = x.double().cpu()
     cin = x.shape[-1]
     hid = wd.shape[1]
@@ -141,7 +141,8 @@ def _ir_ref64(x, we, be, wd, bd, wp, bp, stride, cout, has_expand, residual):
     if has_expand:
         h = (x64 @ we.double().cpu()[:, :cin].t() + be.double().cpu()).clamp(0, 6)
     wdf = wd.double().cpu().view(3, 3, hid).permute(2, 0, 1).unsqueeze(1)
-    h = F.conv2d(h.permute(0, 3, 1, 2), wdf, bd.double().cpu(), stride=stride, padding=1, groups=hid).clamp(0, 6)
+    h = F.conv2d(h.permute(0, 3, 1, 2), wdf, bd.double().cpu(), stride=stride, padding=dil, dilation=dil,
+                 groups=hid).clamp(0, 6)
     h = h.permute(0, 2, 3, 1)
     y = h @ wp.double().cpu()[:cout].t() + bp.double().cpu()[:cout]
     if residual:
