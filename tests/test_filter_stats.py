@@ -91,8 +91,9 @@ def test_stats_disabled_read_minus_one(nns, sleeper):
 
 
 def test_latency_report_rules(nns, sleeper):
-    # 20 ms for 8 invokes, then 60 ms
-    p, src, f, got = _start(nns, sleeper, [0.02] * 9 + [0.06], "latency-report=true")
+    # 50 ms for 8 invokes, then 150 ms (long enough that sleep overshoot on a
+    # loaded host -- a few ms per invoke -- stays inside the 5 % headroom)
+    p, src, f, got = _start(nns, sleeper, [0.05] * 9 + [0.15], "latency-report=true")
     sink = p.get_by_name("sink")
 
     def posts():
@@ -101,10 +102,10 @@ def test_latency_report_rules(nns, sleeper):
     _push(src, got, 3)  # first sample ignored; then estimate > reported (0): posted
     assert posts() >= 1
     q = sink.query_latency()  # reported := estimate x 1.05, added to the pipeline latency
-    assert q is not None and q[1] >= 19_000_000, q
-    _push(src, got, 4)  # steady 20 ms: inside the headroom, within 25 %: nothing posted
+    assert q is not None and q[1] >= 48_000_000, q
+    _push(src, got, 4)  # steady 50 ms: inside the headroom, within 25 %: nothing posted
     assert posts() == 0
-    _push(src, got, 3)  # 60 ms invokes: estimate above the reported value: posted again
+    _push(src, got, 3)  # 150 ms invokes: estimate above the reported value: posted again
     assert posts() >= 1
     src.end_of_stream()
     p.wait(timeout=10)
