@@ -1392,6 +1392,9 @@ const IrwCfg kIrwCfgs[] = {
     NNSX_IRW(1, 5, 5, 160, 0, 4, false),   // 10x10     160 -> 960 (expand + depthwise)
     NNSX_IRW(1, 7, 14, 64, 6, 4, false),   // 14x14 64 -> 384 -> 96
     NNSX_IRW(1, 7, 14, 96, 6, 4, false),   // 14x14 96 -> 576 -> 96: expand 144/98 cells (7x7: 96/49), project 112/98
+    NNSX_IRW(1, 5, 5, 96, 6, 4, false),    // SSD's 19x19 96 -> 576 -> 96: 5 x 5 tiles (least padding)
+    NNSX_IRW(1, 5, 5, 64, 4, 4, false),    // SSD's 19x19 64 -> 384 -> 64
+    NNSX_IRW(1, 5, 5, 64, 6, 4, false),    // SSD's 19x19 64 -> 384 -> 96
     // (dilation 2 -- DeepLab's output-stride-16 blocks on 33x33 maps -- as
     // NNSX_IRWD(1, 7, 7, 160, 10, 4, false, 2) etc. ran 156 vs 120 us for the
     // unfused expand GEMM + dilated depthwise + project GEMM at batch 8 (the
@@ -1496,16 +1499,28 @@ const IrwCfg* find_irw(int S, int H, int W, int cin, int hid, int cout, bool has
   const int nout = (cout + 15) / 16;
   const int Ho = (H - 1) / S + 1, Wo = (W - 1) / S + 1;
   // an exact tiling first; else (odd maps: DeepLab's 129 / 65 / 33, SSD's 75 /
-  // 38 / 19) the first configuration of the shape with masked partial tiles
-  for (int exact = 1; exact >= 0; --exact)
+  // 38 / 19) the configuration of the shape with masked partial tiles that
+  // computes the fewest padded outputs, the first in order on a tie (SSD's 19x19
+  // 96 -> 576 -> 96 blocks: 5 x 5 tiles, 400 outputs per 361, against 441 on
+  // 7 x 7; with the 64-channel 19x19 blocks on 5 x 5 too, 1.917 -> 1.886 ms per
+  // batch-64 step, profiles/r5_ssd_tiles.txt)
+  const IrwCfg* best = nullptr;
+  int64_t best_area = 0;
+  for (int exact = 1; exact >= 0 && !best; --exact)
     for (size_t i = 0; i < sizeof(kIrwCfgs) / sizeof(kIrwCfgs[0]); ++i) {
       const IrwCfg& c = kIrwCfgs[i];
       if (c.S == S && c.dil == dil && c.KIN == kin && c.NOT == nout && (!exact || (Ho % c.TY == 0 && Wo % c.TX == 0)) &&
           c.lds(hid) <= 160 * 1024 && !irw_skipped(i) && (c.min_batch == 0 || (exact && B >= c.min_batch)) &&
-          (c.max_batch == 0 || (B > 0 && B <= c.max_batch)))
-        return &c;
+          (c.max_batch == 0 || (B > 0 && B <= c.max_batch))) {
+        if (exact) return &c;
+        const int64_t area = static_cast<int64_t>((Ho + c.TY - 1) / c.TY * c.TY) * ((Wo + c.TX - 1) / c.TX * c.TX);
+        if (!best || area < best_area) {
+          best = &c;
+          best_area = area;
+        }
+      }
     }
-  return nullptr;
+  return best;
 }
 
 const IrwCfg* find_irw_dw(int S, int H, int W, int cin, int hid, int dil = 1, int B = 0) {

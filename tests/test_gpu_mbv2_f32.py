@@ -130,7 +130,9 @@ IR_F32_SHAPES = [(112, 32, 32, 16, 1, False), (112, 16, 96, 24, 2, True), (56, 2
                  # 14 -> 7 stride-2 block (B14): one 7x7 image per tile, 3 waves
                  (14, 96, 576, 160, 2, True),
                  # SSD-300's 10x10 stage on exact 5x5 tiles
-                 (10, 160, 960, 160, 1, True), (19, 96, 576, 160, 2, True)]
+                 (10, 160, 960, 160, 1, True), (19, 96, 576, 160, 2, True),
+                 # SSD-300's 19x19 stage on masked 5x5 tiles (the least-padding pick)
+                 (19, 64, 384, 64, 1, True), (19, 64, 384, 96, 1, True), (19, 96, 576, 96, 1, True)]
 
 
 def _ir_ref64(x, we, be, wd, bd, wp, bp, stride, cout, has_expand, residual, dil=1):
