@@ -1630,9 +1630,16 @@ static int pick_gemm_tile(int M, int N, int Kpad) {
   // MobileNetV2's 100352 x 96 x 576 118.8 vs 125.3, PoseNet's 69696 x 256 x 256
   // 74.7 vs 79.5.
   // (the batch-512 classifier, 512 x 1280 x 1000, keeps 128 x 64 as below)
+  // Deep products take 128 x 64 only on a grid of >= 3 workgroups per CU (or a
+  // split-K grid): under that the 64 x 64 grid's two resident workgroups per CU
+  // win -- DeepLab b8's 8712 x 960 -> 160 / 320 projects 40.7 -> 34.5 / 55.3 ->
+  // 47.3 us, SSD b64's 6400 x 1280 -> 256 47.2 -> 40.4, PoseNet b64's 5184 x
+  // 1024 -> 1024 even (profiles/r5_gemm_fill.txt)
   if (f32_math() == F32Math::kX3 && M >= 64) {
     const bool big = static_cast<int64_t>((M + 63) / 64) * ((N + 63) / 64) >= 128;
-    return big && ((M >= 8192 && Kpad >= 768) || (M >= 512 && Kpad >= 1024)) ? 128064 : 64064;
+    const int64_t t128 = static_cast<int64_t>((M + 127) / 128) * ((N + 63) / 64);
+    const bool deep = (M >= 8192 && Kpad >= 768) || (M >= 512 && Kpad >= 1024);
+    return big && deep && (t128 >= 768 || t128 < 128) ? 128064 : 64064;
   }
   // Large grids (>= 128 tiles of 64 x 64; M >= 8192, or M >= 512 with a deep
   // K): 128 x 64 tiles, which re-read the weights half as often per output.
