@@ -226,13 +226,11 @@ __global__ void __launch_bounds__(256) dw3x3_f32_kernel(const float* __restrict_
 // CW horizontally adjacent ones x 4 channels, so each loaded input row feeds up
 // to 3 of them ((R-1)S+3 row loads instead of 3R) and each loaded column up to 3
 // ((CW-1)S+3 column loads instead of 3CW)
-// D: dilation (padding D; DeepLab's output-stride-16 blocks): input row ir of
-// the lane's window feeds output row j through tap ky = (ir - j S) / D
-template <int R, int S, int CW = 1, int D = 1>
+template <int R, int S, int CW = 1>
 __device__ __forceinline__ void dw3x3_f32_col(const float* __restrict__ x, const float* __restrict__ w,
                                               const float* __restrict__ bias, float* __restrict__ y, int B, int H,
                                               int W, int C, int Ho, int Wo, int act, uint32_t t0, uint32_t step) {
-  constexpr int NR = (R - 1) * S + 2 * D + 1, NX = (CW - 1) * S + 2 * D + 1;
+  constexpr int NR = (R - 1) * S + 3, NX = (CW - 1) * S + 3;
   const bool ic = (act & 2) != 0;  // (deferred input ReLU6, dw3x3_f32_kernel)
   act &= 1;
   const uint32_t cg = static_cast<uint32_t>(C) >> 2;
@@ -258,26 +256,25 @@ __device__ __forceinline__ void dw3x3_f32_col(const float* __restrict__ x, const
     const float* xb = x + static_cast<int64_t>(b) * H * W * C + c;
 #pragma unroll
     for (int ir = 0; ir < NR; ++ir) {
-      const int iy = oy0 * S - D + ir;
+      const int iy = oy0 * S - 1 + ir;
       if (iy < 0 || iy >= H) continue;
       f32x4_t xv[NX];
 #pragma unroll
       for (int kx = 0; kx < NX; ++kx) {
-        const int ix = ox0 * S - D + kx;
+        const int ix = ox0 * S - 1 + kx;
         xv[kx] = (ix >= 0 && ix < W) ? *reinterpret_cast<const f32x4_t*>(xb + (static_cast<int64_t>(iy) * W + ix) * C)
                                      : f32x4_t{0.f, 0.f, 0.f, 0.f};
         if (ic) xv[kx] = relu6x4(xv[kx]);
       }
 #pragma unroll
       for (int j = 0; j < R; ++j) {
-        const int kd = ir - j * S;
-        if (kd < 0 || kd > 2 * D || kd % D) continue;
-        const int ky = kd / D;
+        const int ky = ir - j * S;
+        if (ky < 0 || ky > 2) continue;
 #pragma unroll
         for (int q = 0; q < CW; ++q)
 #pragma unroll
           for (int kx = 0; kx < 3; ++kx)
-            acc[j][q] = __builtin_elementwise_fma(xv[q * S + kx * D], wv[ky * 3 + kx], acc[j][q]);
+            acc[j][q] = __builtin_elementwise_fma(xv[q * S + kx], wv[ky * 3 + kx], acc[j][q]);
       }
     }
 #pragma unroll
@@ -297,12 +294,104 @@ __device__ __forceinline__ void dw3x3_f32_col(const float* __restrict__ x, const
   }
 }
 
-template <int R, int S, int CW = 1, int D = 1>
+template <int R, int S, int CW = 1>
 __global__ void __launch_bounds__(256) dw3x3_f32_col_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                             const float* __restrict__ bias, float* __restrict__ y,
                                                             int B, int H, int W, int C, int Ho, int Wo, int act) {
-  dw3x3_f32_col<R, S, CW, D>(x, w, bias, y, B, H, W, C, Ho, Wo, act, blockIdx.x * blockDim.x + threadIdx.x,
+  dw3x3_f32_col<R, S, CW>(x, w, bias, y, B, H, W, C, Ho, Wo, act, blockIdx.x * blockDim.x + threadIdx.x,
                              gridDim.x * blockDim.x);
+}
+
+// Dilated stride-1 depthwise (DeepLab's output-stride-16 blocks), parity form:
+// output (oy, ox) reads only inputs of its own residue (oy mod D, ox mod D), so
+// the map is D x D independent plain 3x3 convolutions on its residue grids.  A
+// lane owns R x CW outputs D apart inside one residue grid: (R + 2) x (CW + 2)
+// loads for R x CW outputs -- 36 per 16 at 4 x 4 against 64 for the contiguous
+// 4 x 4 block over the dilated window (dw3x3_f32_col<4, 1, 4, 2>).  Row blocks
+// are numbered residue by residue (residue r has ceil((H - r) / D) rows).
+template <int R, int CW, int D>
+__global__ void __launch_bounds__(256) dw3x3_f32_dil_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                            const float* __restrict__ bias, float* __restrict__ y,
+                                                            int B, int H, int W, int C, int act) {
+  const bool ic = (act & 2) != 0;  // (deferred input ReLU6, dw3x3_f32_kernel)
+  act &= 1;
+  auto blocks = [](int n, int r, int per) { return ((n - r + D - 1) / D + per - 1) / per; };
+  int rbt = 0, cbt = 0;
+#pragma unroll
+  for (int r = 0; r < D; ++r) {
+    rbt += blocks(H, r, R);
+    cbt += blocks(W, r, CW);
+  }
+  const uint32_t cg = static_cast<uint32_t>(C) >> 2;
+  const uint32_t total = static_cast<uint32_t>(B) * rbt * cbt * cg;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const int c = static_cast<int>(t % cg) * 4;
+    uint32_t p = t / cg;
+    int kx = static_cast<int>(p % cbt);
+    p /= cbt;
+    int ky = static_cast<int>(p % rbt);
+    const int b = static_cast<int>(p / rbt);
+    int py = 0, px = 0;
+#pragma unroll
+    for (int r = 0; r < D - 1; ++r) {
+      const int nr = blocks(H, py, R), nc = blocks(W, px, CW);
+      if (ky >= nr) {
+        ky -= nr;
+        ++py;
+      }
+      if (kx >= nc) {
+        kx -= nc;
+        ++px;
+      }
+    }
+    const int oy0 = py + ky * R * D, ox0 = px + kx * CW * D;
+    f32x4_t wv[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) wv[k] = *reinterpret_cast<const f32x4_t*>(w + k * C + c);
+    const f32x4_t bv = *reinterpret_cast<const f32x4_t*>(bias + c);
+    f32x4_t acc[R][CW];
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+#pragma unroll
+      for (int q = 0; q < CW; ++q) acc[j][q] = bv;
+    const float* xb = x + static_cast<int64_t>(b) * H * W * C + c;
+#pragma unroll
+    for (int ir = 0; ir < R + 2; ++ir) {
+      const int iy = oy0 + (ir - 1) * D;
+      if (iy < 0 || iy >= H) continue;
+      f32x4_t xv[CW + 2];
+#pragma unroll
+      for (int k = 0; k < CW + 2; ++k) {
+        const int ix = ox0 + (k - 1) * D;
+        xv[k] = (ix >= 0 && ix < W) ? *reinterpret_cast<const f32x4_t*>(xb + (static_cast<int64_t>(iy) * W + ix) * C)
+                                    : f32x4_t{0.f, 0.f, 0.f, 0.f};
+        if (ic) xv[k] = relu6x4(xv[k]);
+      }
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        const int tap = ir - j;
+        if (tap < 0 || tap > 2) continue;
+#pragma unroll
+        for (int q = 0; q < CW; ++q)
+#pragma unroll
+          for (int k = 0; k < 3; ++k) acc[j][q] = __builtin_elementwise_fma(xv[q + k], wv[tap * 3 + k], acc[j][q]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int oy = oy0 + j * D;
+      if (oy >= H) break;
+#pragma unroll
+      for (int q = 0; q < CW; ++q) {
+        const int ox = ox0 + q * D;
+        if (ox >= W) break;
+        f32x4_t v = acc[j][q];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], act);
+        *reinterpret_cast<f32x4_t*>(y + ((static_cast<int64_t>(b) * H + oy) * W + ox) * C + c) = v;
+      }
+    }
+  }
 }
 
 // several stride-1 depthwise problems in one launch (the SSD heads); problem i
@@ -1352,11 +1441,6 @@ int tile_pref(int S, int H, int W, int TY, int TX) {
     S, TY, TX, KIN, NOT, NW, F, &irw_f32_kernel<S, TY, TX, KIN, NOT, NW, F>,                    \
         &IrwGeom<S, TY, TX, KIN, NOT, NW, F>::lds_bytes, 1, MB                                  \
   }
-#define NNSX_IRWD(S, TY, TX, KIN, NOT, NW, F, D, MAXB)                                          \
-  IrwCfg {                                                                                      \
-    S, TY, TX, KIN, NOT, NW, F, &irw_f32_kernel<S, TY, TX, KIN, NOT, NW, F, D>,                 \
-        &IrwGeom<S, TY, TX, KIN, NOT, NW, F, D>::lds_bytes, D, 0, MAXB                          \
-  }
 // (NW = waves per workgroup: a divisor of the hidden subtile count where possible,
 // so every wave walks the same number of 16-channel subtiles)
 const IrwCfg kIrwCfgs[] = {
@@ -1392,9 +1476,15 @@ const IrwCfg kIrwCfgs[] = {
     NNSX_IRW(1, 5, 5, 160, 0, 4, false),   // 10x10     160 -> 960 (expand + depthwise)
     NNSX_IRW(1, 7, 14, 64, 6, 4, false),   // 14x14 64 -> 384 -> 96
     NNSX_IRW(1, 7, 14, 96, 6, 4, false),   // 14x14 96 -> 576 -> 96: expand 144/98 cells (7x7: 96/49), project 112/98
-    NNSX_IRW(1, 5, 5, 96, 6, 4, false),    // SSD's 19x19 96 -> 576 -> 96: 5 x 5 tiles (least padding)
-    NNSX_IRW(1, 5, 5, 64, 4, 4, false),    // SSD's 19x19 64 -> 384 -> 64
-    NNSX_IRW(1, 5, 5, 64, 6, 4, false),    // SSD's 19x19 64 -> 384 -> 96
+    // SSD's 19x19 blocks (least padding: 20 x 20 outputs per 19 x 19): 5 x 10 tiles -- the
+    // 7 x 7 tile's LDS and registers, 525 expand cells per image against 625 on 5 x 5 --
+    // and the 5 x 5 tiles
+    NNSX_IRW(1, 5, 10, 96, 6, 4, false),   // 96 -> 576 -> 96
+    NNSX_IRW(1, 5, 10, 64, 4, 4, false),   // 64 -> 384 -> 64
+    NNSX_IRW(1, 5, 10, 64, 6, 4, false),   // 64 -> 384 -> 96
+    NNSX_IRW(1, 5, 5, 96, 6, 4, false),
+    NNSX_IRW(1, 5, 5, 64, 4, 4, false),
+    NNSX_IRW(1, 5, 5, 64, 6, 4, false),
     // (dilation 2 -- DeepLab's output-stride-16 blocks on 33x33 maps -- as
     // NNSX_IRWD(1, 7, 7, 160, 10, 4, false, 2) etc. ran 156 vs 120 us for the
     // unfused expand GEMM + dilated depthwise + project GEMM at batch 8 (the
@@ -1408,7 +1498,6 @@ const IrwCfg kIrwCfgs[] = {
 };
 #undef NNSX_IRW
 #undef NNSX_IRWB
-#undef NNSX_IRWD
 
 // NNSX_X3_IRW (A/B): 1 = every fused block on its irw_x3 twin, 2 = every
 // block with an expand-x3 twin (irw_f32 XE) on it; unset = the measured defaults
@@ -1501,9 +1590,9 @@ const IrwCfg* find_irw(int S, int H, int W, int cin, int hid, int cout, bool has
   // an exact tiling first; else (odd maps: DeepLab's 129 / 65 / 33, SSD's 75 /
   // 38 / 19) the configuration of the shape with masked partial tiles that
   // computes the fewest padded outputs, the first in order on a tie (SSD's 19x19
-  // 96 -> 576 -> 96 blocks: 5 x 5 tiles, 400 outputs per 361, against 441 on
-  // 7 x 7; with the 64-channel 19x19 blocks on 5 x 5 too, 1.917 -> 1.886 ms per
-  // batch-64 step, profiles/r5_ssd_tiles.txt)
+  // blocks: 400 outputs per 361 on 5 x 5 tiles against 441 on 7 x 7, 1.917 ->
+  // 1.886 ms per batch-64 step, profiles/r5_ssd_tiles.txt; on 5 x 10 tiles
+  // (also 400, fewer halo cells) 1.864 -> 1.758 ms, profiles/r5_dw_dil.txt)
   const IrwCfg* best = nullptr;
   int64_t best_area = 0;
   for (int exact = 1; exact >= 0 && !best; --exact)
@@ -1758,8 +1847,9 @@ void dw3x3_f32(const float* x, const float* w, const float* bias, float* y, int 
   // Lane shapes (rows x columns of outputs per lane), measured with
   // scripts/dw_roofline.py (profiles/r4_dw_lane_shapes.txt): stride 1 4 x 4 --
   // 7x7x960 at batch 512 56.3 -> 39.4 us, 14x14x576 130.6 -> 96.2 us, PoseNet's
-  // 17x17x512 21.2 -> 18.7 us; stride 2 2 x 2 -- 129 -> 65 x 64 66.3 -> 60.9 us;
-  // dilation 2 4 x 4 over the dilated window (8 x 8 loads for 16 outputs).
+  // 17x17x512 21.2 -> 18.7 us; stride 2 2 x 2 -- 129 -> 65 x 64 66.3 -> 60.9 us.
+  // Dilation 2: residue-grid lanes (dw3x3_f32_dil), DeepLab b8's 33x33x960 24.3 ->
+  // 16.9 us, batch 1 6.0 -> 5.3 us (profiles/r5_dw_dil.txt).
   // The multi-pixel lanes only where they still give every CU a workgroup
   // (>= 256 x 256 lanes): at batch 1 their few long lanes leave most CUs idle --
   // PoseNet batch-1 p50 0.36 -> 0.38 ms, DeepLab 0.525 -> 0.543 ms.
@@ -1767,10 +1857,14 @@ void dw3x3_f32(const float* x, const float* w, const float* bias, float* y, int 
   const int R2 = stride == 1 ? 4 : 2, C2 = stride == 1 ? 4 : 2;
   const int64_t lanes = static_cast<int64_t>(B) * ((Ho + R2 - 1) / R2) * ((Wo + C2 - 1) / C2) * (C / 4);
   const bool big = lanes >= 65536;
-  if (big && stride == 1 && dil == 2) {
-    const int64_t work = static_cast<int64_t>(B) * ((Ho + 3) / 4) * ((Wo + 3) / 4) * (C / 4);
+  if (stride == 1 && dil == 2) {  // residue-grid lanes: 4 x 4 on large grids, else 2 x 2
+    const int r = big ? 4 : 2;
+    const int64_t work = static_cast<int64_t>(B) * ((H + 1) / 2 / r + 2) * ((W + 1) / 2 / r + 2) * (C / 4) * 4;
     const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 65535))));
-    hipLaunchKernelGGL((dw3x3_f32_col_kernel<4, 1, 4, 2>), grid, dim3(256), 0, s, x, w, bias, y, B, H, W, C, Ho, Wo, act);
+    if (big)
+      hipLaunchKernelGGL((dw3x3_f32_dil_kernel<4, 4, 2>), grid, dim3(256), 0, s, x, w, bias, y, B, H, W, C, act);
+    else
+      hipLaunchKernelGGL((dw3x3_f32_dil_kernel<2, 2, 2>), grid, dim3(256), 0, s, x, w, bias, y, B, H, W, C, act);
     return;
   }
   if (big && dil == 1) {

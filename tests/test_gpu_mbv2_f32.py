@@ -60,7 +60,11 @@ def test_pw_conv_f32_identity_asymmetric(nns):
                                                 (1, 3, 3, 256, 2, 1), (1, 17, 13, 64, 1, 2), (3, 5, 5, 32, 1, 2),
                                                 # (maps large enough for the multi-pixel lanes, partial groups)
                                                 (8, 45, 43, 256, 1, 1), (16, 33, 33, 288, 1, 2),
-                                                (8, 129, 129, 64, 2, 1)])
+                                                (8, 129, 129, 64, 2, 1),
+                                                # dilation 2 residue-grid lanes (4 x 4 large, 2 x 2 small;
+                                                # even / odd extents)
+                                                (8, 33, 33, 960, 1, 2), (16, 34, 31, 256, 1, 2),
+                                                (1, 33, 33, 960, 1, 2), (2, 34, 31, 64, 1, 2)])
 @pytest.mark.parametrize("act", [1, 3])
 def test_dw_conv_f32(nns, B, H, W, C, stride, dil, act):
     """act 3 = the producer's deferred ReLU6 applied to the input taps, then ReLU6"""
