@@ -70,7 +70,10 @@ struct IrwGeom {
   // (the wider 7x14 28x28 tiles hold 14 accumulators: 3 waves per SIMD)
   // (7x14 tiles with 6 cout tiles: 42 accumulators; the LDS holds one workgroup
   // per CU anyway, so one wave per SIMD and the accumulation registers)
+  // (5 x 15 tiles on 24 channels: 170 VGPRs at 2, two waves per SIMD where the LDS
+  // holds three)
   static constexpr int MINB = (KIN == 32 && S == 1) ? (TY * TX <= 49 ? 4 : 3)
+                              : (KIN == 24 && S == 1 && TY == 5) ? 3
                               : (NOT <= 4 || (NOT <= 6 && TY * TX <= 64)) ? 2 : 1;
 };
 

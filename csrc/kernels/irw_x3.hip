@@ -329,6 +329,7 @@ const std::vector<IrwCfg> kIrwX3Cfgs = {
     NNSX_IRWX(1, 7, 7, 64, 4, 4, false),  NNSX_IRWX(1, 7, 7, 64, 6, 4, false),  NNSX_IRWX(1, 7, 7, 96, 6, 4, false),
     NNSX_IRWX(1, 7, 7, 160, 10, 4, false), NNSX_IRWX(2, 7, 7, 96, 10, 4, false), NNSX_IRWX(1, 7, 7, 160, 0, 4, false),
     NNSX_IRWX(1, 5, 5, 160, 10, 4, false), NNSX_IRWX(2, 5, 5, 96, 10, 4, false), NNSX_IRWX(1, 5, 5, 160, 0, 4, false),
+    NNSX_IRWX(1, 5, 10, 32, 2, 4, false),
 };
 #undef NNSX_IRWX
 

@@ -1485,6 +1485,14 @@ const IrwCfg kIrwCfgs[] = {
     NNSX_IRW(1, 5, 5, 96, 6, 4, false),
     NNSX_IRW(1, 5, 5, 64, 4, 4, false),
     NNSX_IRW(1, 5, 5, 64, 6, 4, false),
+    // 32 -> 192 -> 32 on SSD's 38x38 and DeepLab's 65x65 maps (1600 / 4550 outputs against
+    // 1764 / 4900 on 7 x 7) and 24 -> 144 -> 24 on SSD's 75x75 (exact) and DeepLab's 129x129:
+    // SSD b64 1.786 -> 1.758 ms, DeepLab b8 0.947 -> 0.944 ms.  (Measured and dropped: 11 x 5
+    // tiles on DeepLab's 33x33 blocks -- 1155 outputs per 1089, no gain -- and exact 5 x 13
+    // tiles on 65x65, +1 % there: its x3 twin's 32-pixel project tiles hold 96 per 65;
+    // profiles/r5_odd_map_tiles.txt)
+    NNSX_IRW(1, 5, 10, 32, 2, 4, false),
+    NNSX_IRW(1, 5, 15, 24, 2, 3, true),
     // (dilation 2 -- DeepLab's output-stride-16 blocks on 33x33 maps -- as
     // NNSX_IRWD(1, 7, 7, 160, 10, 4, false, 2) etc. ran 156 vs 120 us for the
     // unfused expand GEMM + dilated depthwise + project GEMM at batch 8 (the

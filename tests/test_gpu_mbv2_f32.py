@@ -136,7 +136,10 @@ IR_F32_SHAPES = [(112, 32, 32, 16, 1, False), (112, 16, 96, 24, 2, True), (56, 2
                  # SSD-300's 10x10 stage on exact 5x5 tiles
                  (10, 160, 960, 160, 1, True), (19, 96, 576, 160, 2, True),
                  # SSD-300's 19x19 stage on masked 5x5 tiles (the least-padding pick)
-                 (19, 64, 384, 64, 1, True), (19, 64, 384, 96, 1, True), (19, 96, 576, 96, 1, True)]
+                 (19, 64, 384, 64, 1, True), (19, 64, 384, 96, 1, True), (19, 96, 576, 96, 1, True),
+                 # DeepLab's 33x33, 65x65 and 129x129 maps, SSD's 38x38 and 75x75 (5 x 10 / 5 x 15 tiles)
+                 (33, 64, 384, 64, 1, True), (33, 96, 576, 96, 1, True), (65, 32, 192, 32, 1, True),
+                 (38, 32, 192, 32, 1, True), (75, 24, 144, 24, 1, True), (129, 24, 144, 24, 1, True)]
 
 
 def _ir_ref64(x, we, be, wd, bd, wp, bp, stride, cout, has_expand, residual, dil=1):
