@@ -1558,9 +1558,11 @@ const IrwCfg* x3_twin(const IrwCfg* c, const IrBlockF32Args& a) {
   // The LDS traffic of the split operands -- 3 x 16 B per 32-channel B fragment
   // against 2 x 16 B of fp32 -- bounds the other blocks.  (56 x 56 24 -> 144 ->
   // 24, 430 vs 447 us, stays native: at batch 1 its max error vs fp64 is 1.16x
-  // the native kernel's -- the accuracy gate of test_gpu_x3.py.)
+  // the native kernel's -- the accuracy gate of test_gpu_x3.py.  The 5 x 10
+  // 32-channel tiles stay native too: DeepLab b8's 65x65 blocks 22.4 vs 23.2-23.7
+  // us, profiles/r5_deeplab_twins.txt, r5_parts3_n510.txt.)
   // NNSX_X3_IRW=1: every configuration with a twin (A/B)
-  const bool dflt = c->S == 1 && ((c->KIN == 160 && (c->NOT == 10 || c->NOT == 0)) || (c->KIN == 32 && c->NOT == 2));
+  const bool dflt = c->S == 1 && ((c->KIN == 160 && (c->NOT == 10 || c->NOT == 0)) || (c->KIN == 32 && c->NOT == 2 && c->TX != 10));
   if (x3_irw_mode() == 2 || (!x3_irw_enabled() && !dflt)) return xe_twin(c, a);
   // the same tile, else (7 x 14 tiles: their 4 32-pixel project tiles hold more
   // accumulators than two waves per SIMD allow) the 7 x 7 tile of the shape
@@ -2049,6 +2051,9 @@ static int irw_parts(const IrwCfg* c, int tiles, int hid) {
   if (c->NOT == 0)  // depthwise output: parts need no reduction, so fill the chip
     return std::max(1, std::min((1024 + tiles - 1) / tiles, nsub / c->NW));
   if (tiles >= 256 || nsub < 8) return 1;
+  // (three parts where two leave the waves unevenly loaded -- DeepLab b8's 33x33
+  // 96 -> 576 -> 96, 18 subtiles = 5 / 5 / 4 / 4 per wave -- measured slower:
+  // DeepLab b8 +1.6 %, MobileNetV2 b128 -5.5 %, profiles/r5_parts3_n510.txt)
   if (tiles >= 128) return 2;
   const int want = (512 + tiles - 1) / tiles;
   int parts = std::max(2, std::min(want, nsub / c->NW));
