@@ -503,33 +503,39 @@ __global__ void __launch_bounds__(256) stem_f32_kernel(const T* __restrict__ x, 
 // flight), then the stripes are added in a fixed order through LDS
 // (deterministic).  DeepLab's 33x33x320 maps at batch 8: 40 workgroups instead
 // of 16 with one dependent load chain of 272 pixels per lane (67 us).
+// Q channel quads x (256 / Q) pixel stripes per workgroup; the stripes' sums are
+// added in a fixed order (bitwise repeatable).  Q = 4 where 16-quad groups would
+// leave most CUs idle: DeepLab b8's 8 x 1089 x 320 map, 40 workgroups of 16
+// quads, read at 1.4 TB/s.
+template <int Q>
 __global__ void __launch_bounds__(256) avgpool_f32_kernel(const float* __restrict__ x, float* __restrict__ y, int HW,
                                                           int C) {
-  __shared__ f32x4_t part[16][16];
+  constexpr int S = 256 / Q;
+  __shared__ f32x4_t part[S][Q];
   const int cq = C >> 2;
-  const int groups = (cq + 15) / 16;
+  const int groups = (cq + Q - 1) / Q;
   const int b = blockIdx.x / groups;
-  const int q = (blockIdx.x % groups) * 16 + (threadIdx.x & 15);
-  const int stripe = threadIdx.x >> 4;
+  const int q = (blockIdx.x % groups) * Q + (threadIdx.x % Q);
+  const int stripe = threadIdx.x / Q;
   const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
   f32x4_t a0 = z, a1 = z, a2 = z, a3 = z;
   if (q < cq) {
     const float* xb = x + static_cast<int64_t>(b) * HW * C + q * 4;
     int p = stripe;
-    for (; p + 48 < HW; p += 64) {
+    for (; p + 3 * S < HW; p += 4 * S) {
       a0 += *reinterpret_cast<const f32x4_t*>(xb + static_cast<int64_t>(p) * C);
-      a1 += *reinterpret_cast<const f32x4_t*>(xb + static_cast<int64_t>(p + 16) * C);
-      a2 += *reinterpret_cast<const f32x4_t*>(xb + static_cast<int64_t>(p + 32) * C);
-      a3 += *reinterpret_cast<const f32x4_t*>(xb + static_cast<int64_t>(p + 48) * C);
+      a1 += *reinterpret_cast<const f32x4_t*>(xb + static_cast<int64_t>(p + S) * C);
+      a2 += *reinterpret_cast<const f32x4_t*>(xb + static_cast<int64_t>(p + 2 * S) * C);
+      a3 += *reinterpret_cast<const f32x4_t*>(xb + static_cast<int64_t>(p + 3 * S) * C);
     }
-    for (; p < HW; p += 16) a0 += *reinterpret_cast<const f32x4_t*>(xb + static_cast<int64_t>(p) * C);
+    for (; p < HW; p += S) a0 += *reinterpret_cast<const f32x4_t*>(xb + static_cast<int64_t>(p) * C);
   }
-  part[stripe][threadIdx.x & 15] = (a0 + a1) + (a2 + a3);
+  part[stripe][threadIdx.x % Q] = (a0 + a1) + (a2 + a3);
   __syncthreads();
   if (stripe != 0 || q >= cq) return;
   f32x4_t s = part[0][threadIdx.x];
 #pragma unroll
-  for (int k = 1; k < 16; ++k) s += part[k][threadIdx.x];
+  for (int k = 1; k < S; ++k) s += part[k][threadIdx.x];
   *reinterpret_cast<f32x4_t*>(y + static_cast<int64_t>(b) * C + q * 4) = s * (1.f / HW);
 }
 
@@ -1982,7 +1988,12 @@ void pw_pool_f32(const float* x, const float* wt, const float* bias, float* y, i
 
 void avgpool_f32(const float* x, float* y, int B, int HW, int C, hipStream_t s) {
   const int groups = (C / 4 + 15) / 16;
-  hipLaunchKernelGGL(avgpool_f32_kernel, dim3(static_cast<unsigned>(B * groups)), dim3(256), 0, s, x, y, HW, C);
+  if (B * groups >= 512 || HW < 256) {
+    hipLaunchKernelGGL(avgpool_f32_kernel<16>, dim3(static_cast<unsigned>(B * groups)), dim3(256), 0, s, x, y, HW, C);
+    return;
+  }
+  const int g4 = (C / 4 + 3) / 4;
+  hipLaunchKernelGGL(avgpool_f32_kernel<4>, dim3(static_cast<unsigned>(B * g4)), dim3(256), 0, s, x, y, HW, C);
 }
 
 bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout, bool has_expand, int dil, int B) {

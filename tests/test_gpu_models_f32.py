@@ -109,7 +109,7 @@ def test_ir_block_dilated_and_partial_tiles(H, cin, hid, cout, stride, dil):
     assert _rel(got, ref) < 1e-5, _rel(got, ref)
 
 
-@pytest.mark.parametrize("B,HW,C", [(8, 33 * 33, 320), (512, 49, 1280), (3, 5, 12)])
+@pytest.mark.parametrize("B,HW,C", [(8, 33 * 33, 320), (512, 49, 1280), (3, 5, 12), (2, 1000, 36), (1, 300, 20)])
 def test_avgpool_f32(B, HW, C):
     x = torch.randn(B, HW, 1, C, device="cuda")
     p = torch.ops.nnsx.avgpool(x)
