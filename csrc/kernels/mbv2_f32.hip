@@ -1741,6 +1741,13 @@ static int pick_gemm_tile(int M, int N, int Kpad) {
   // 47.3 us, SSD b64's 6400 x 1280 -> 256 47.2 -> 40.4, PoseNet b64's 5184 x
   // 1024 -> 1024 even (profiles/r5_gemm_fill.txt)
   if (f32_math() == F32Math::kX3 && M >= 64) {
+    // wide products on large grids: 64 x 128 tiles (each staged, split activation
+    // tile feeds twice the columns) -- MobileNetV2 b512's 25088 x 320 -> 1280 head
+    // 164.5 -> 149.7 us, PoseNet b64's 18496 x 512 -> 512 75.1 -> 72.0 and 5184 x
+    // 1024 -> 1024 86.3 -> 81.9 (profiles/r5_gemm_fill.txt)
+    if (N >= 512 && Kpad >= 256 && (M >= 16384 || Kpad >= 1024) &&
+        static_cast<int64_t>((M + 63) / 64) * ((N + 127) / 128) >= 256)
+      return 64128;
     const bool big = static_cast<int64_t>((M + 63) / 64) * ((N + 63) / 64) >= 128;
     const int64_t t128 = static_cast<int64_t>((M + 127) / 128) * ((N + 63) / 64);
     const bool deep = (M >= 8192 && Kpad >= 768) || (M >= 512 && Kpad >= 1024);

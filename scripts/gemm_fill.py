@@ -28,7 +28,7 @@ SHAPES = [
     ("mbv2 b512 classifier 1280->1000", 512, 1280, 1000, 0, False),
     ("mbv2 b512 head 320->1280", 25088, 320, 1280, 1, False),
 ]
-TILES = [0, 64064, 128064]
+TILES = [int(t) for t in os.environ.get("TILES", "0,64064,128064").split(",")]
 
 
 def timeit(fn, n=50):
