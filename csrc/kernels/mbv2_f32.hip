@@ -888,6 +888,7 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
   const int ry0 = max(iy0, 0), ry1 = min(iy0 + TIY, a.H);
   const int rx0 = max(ix0, 0), rx1 = min(ix0 + TIX, a.W);
   const int RW = rx1 - rx0, NC = FULL ? PIN : (ry1 - ry0) * RW;
+  const bool tile_in = iy0 >= 0 && ix0 >= 0 && iy0 + TIY <= a.H && ix0 + TIX <= a.W;  // whole halo grid in the image
   const float rrw = 1.f / static_cast<float>(RW);
   load_tile(tile);
 #pragma unroll
@@ -1064,9 +1065,14 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
             e1 = mfma_k8(et, t1[g & 1], e1);
           }
           if constexpr (FULL) {
-            const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
-            myhid[j * 16 + li] = hcell[j] ? relu6x4(e0 + be4) : z;
-            if (j + 1 < NBT) myhid[j1 * 16 + li] = hcell[j1] ? relu6x4(e1 + be4) : z;
+            if (tile_in) {  // (wave-uniform: no per-cell select; cells past PIN are never read)
+              myhid[j * 16 + li] = relu6x4(e0 + be4);
+              if (j + 1 < NBT) myhid[j1 * 16 + li] = relu6x4(e1 + be4);
+            } else {
+              const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
+              myhid[j * 16 + li] = hcell[j] ? relu6x4(e0 + be4) : z;
+              if (j + 1 < NBT) myhid[j1 * 16 + li] = hcell[j1] ? relu6x4(e1 + be4) : z;
+            }
           } else {
             // branch-free: padding pixels store to the unused cell PIN (a per-lane
             // `if` compiled to exec-mask branches that kept the next pair's LDS
@@ -1263,6 +1269,8 @@ __global__ void __launch_bounds__(64, 2) stem_ir1w_f32_kernel(StemIr1F32Args a) 
     const int tyx = tile - b * tiles_img;
     const int oy0 = (tyx / a.tiles_x) * TY, ox0 = (tyx % a.tiles_x) * TX;
     const int hy0 = oy0 - 1, hx0 = ox0 - 1;  // hidden halo origin (stem-output coords)
+    // every halo cell inside the stem output (most tiles of a 112x112 map)
+    const bool interior = hy0 >= 0 && hx0 >= 0 && hy0 + HY <= a.Ho && hx0 + HX <= a.Wo;
     __syncthreads();  // (one wave: orders the previous tile's LDS reads before these writes; lut on entry)
     if (lane < PITCH) {
       // all table reads first, then the stores: lut and xin share the LDS
@@ -1306,9 +1314,14 @@ __global__ void __launch_bounds__(64, 2) stem_ir1w_f32_kernel(StemIr1F32Args a) 
 #pragma unroll
       for (int t = 0; t < 7; ++t) xv[t] = xn[t];
       if (c < PIN) {
-        const bool in = hy0 + hy >= 0 && hy0 + hy < a.Ho && hx0 + hx >= 0 && hx0 + hx < a.Wo;
-        hid[g * PIN + c] = in ? relu6x4(e0 + bs4[0]) : z;
-        hid[(4 + g) * PIN + c] = in ? relu6x4(e1 + bs4[1]) : z;
+        if (interior) {  // (wave-uniform: no per-cell bounds test and selects)
+          hid[g * PIN + c] = relu6x4(e0 + bs4[0]);
+          hid[(4 + g) * PIN + c] = relu6x4(e1 + bs4[1]);
+        } else {
+          const bool in = hy0 + hy >= 0 && hy0 + hy < a.Ho && hx0 + hx >= 0 && hx0 + hx < a.Wo;
+          hid[g * PIN + c] = in ? relu6x4(e0 + bs4[0]) : z;
+          hid[(4 + g) * PIN + c] = in ? relu6x4(e1 + bs4[1]) : z;
+        }
       }
     }
     __syncthreads();
