@@ -859,6 +859,20 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
     const int qw = qx1 - qx0, qn = FULL ? PIN : (qy1 - qy0) * qw;
     const float qr = 1.f / static_cast<float>(qw);
     const float* qb = a.x + static_cast<int64_t>(tb) * a.H * a.W * a.cin;
+    // FULL tile whose halo grid lies inside the image (wave-uniform): no per-cell
+    // bounds tests
+    if (FULL && ty0 >= 0 && tx0 >= 0 && ty0 + TIY <= a.H && tx0 + TIX <= a.W) {
+#pragma unroll
+      for (int it = 0; it < NSIT; ++it) {
+        const int v = tid + it * NT;
+        const int c = v / KQS, kq = v - c * KQS;
+        sok[it] = (NSV % NT == 0 || v < NSV) && c < PIN && kq * 4 < a.cin;
+        const int64_t off =
+            sok[it] ? (static_cast<int64_t>(ty0 + c / TIX) * a.W + (tx0 + c % TIX)) * a.cin + kq * 4 : 0;
+        sv[it] = *reinterpret_cast<const f32x4_t*>(qb + off);
+      }
+      return;
+    }
 #pragma unroll
     for (int it = 0; it < NSIT; ++it) {
       const int v = tid + it * NT;

@@ -1,5 +1,5 @@
 #!/bin/bash
-# wave-uniform interior-tile epilogues (stem_ir1w, FULL irw_f32) in the HEAD tree vs variants/base, same box
+# wave-uniform interior-tile fast paths (HEAD tree) vs variants/base, same box
 set -eo pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
