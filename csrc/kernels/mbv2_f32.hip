@@ -859,9 +859,9 @@ __global__ void __launch_bounds__(64 * NW, (IrwGeom<S, TY, TX, KIN, NOT, NW, FUL
     const int qw = qx1 - qx0, qn = FULL ? PIN : (qy1 - qy0) * qw;
     const float qr = 1.f / static_cast<float>(qw);
     const float* qb = a.x + static_cast<int64_t>(tb) * a.H * a.W * a.cin;
-    // FULL tile whose halo grid lies inside the image (wave-uniform): no per-cell
-    // bounds tests
-    if (FULL && ty0 >= 0 && tx0 >= 0 && ty0 + TIY <= a.H && tx0 + TIX <= a.W) {
+    // a tile whose halo grid lies inside the image (wave-uniform; its compact
+    // index is the grid index): no per-cell bounds tests
+    if (ty0 >= 0 && tx0 >= 0 && ty0 + TIY <= a.H && tx0 + TIX <= a.W) {
 #pragma unroll
       for (int it = 0; it < NSIT; ++it) {
         const int v = tid + it * NT;
