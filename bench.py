@@ -96,7 +96,12 @@ def parse_args(argv=None):
                          "(their frames/s and RCCL world as extra keys; '' = skip)")
     ap.add_argument("--extra-steps", type=int, default=20, help="timed steps of each extra config pass")
     ap.add_argument("--no-selfcheck", action="store_true",
-                    help="WORLD_SIZE > 1: skip the rank-group data-plane self-check before the timed run")
+                    help="WORLD_SIZE > 1: skip the rank-group data-plane self-check (run after the headline)")
+    ap.add_argument("--selfcheck-timeout-ms", type=int, default=60000,
+                    help="group timeout of the self-check (a missing member fails an operation after this)")
+    ap.add_argument("--aux-timeout", type=float, default=float(os.environ.get("NNSX_BENCH_AUX_TIMEOUT", "300")),
+                    help="seconds for the whole self-check + extra-config phase; on expiry the headline is "
+                         "printed with aux_timeout and every rank exits 0")
     ap.add_argument("--cpu", action="store_true", help="CPU reference path (device=-1, torch CPU)")
     # (depth 1 / 1: same frames/s as 4 / 2 at batch 512, p50 23 vs 37 ms: profiles/r4_mbv2_ab_b512.txt q11)
     ap.add_argument("--queue", type=int, default=1, help="queue depth between filter and decoder")
@@ -423,24 +428,6 @@ def main():
         if a.precision in ("bf16", "both"):
             runs.append(("bf16", base, "bf16"))
 
-    # WORLD_SIZE > 1: every comm::Group operation on frame-sized payloads (RCCL on
-    # GPUs) before anything is timed -- all-gather uniform / ragged, broadcast,
-    # scatter, a p2p ring and an all-to-all exchange (nnstreamer_amd/parallel/selfcheck.py)
-    selfcheck = None
-    if world > 1 and not a.no_selfcheck:
-        from nnstreamer_amd.parallel import selfcheck as sc
-
-        if use_gpu:
-            def arr(v, d=dev):
-                return torch.as_tensor(v).cuda(d)
-        else:
-            def arr(v):
-                return np.asarray(v)
-        g = nns.Group("bench/selfcheck", rank, world, "", dev, a.comm_backend if use_gpu else "tcp", 60000)
-        selfcheck = sc.run(g, rank, world, arr, scale=1.0 if use_gpu else 1.0 / 64)
-        del g
-        print(f"rank {rank}: rccl_selfcheck {selfcheck}", file=sys.stderr, flush=True)
-
     results = {}
     for label, model_name, dtype in runs:
         model_path = os.path.join(workdir, f"{model_name}.pt")
@@ -473,24 +460,6 @@ def main():
                              world, dev, use_gpu, dist)
             sweep.append((sb, r))
 
-    # WORLD_SIZE > 1: short passes of the multi-rank configs (config 4's demux fan-out
-    # over RCCL p2p, config 5's edge all-gather), so a scaling run exercises the
-    # same data plane the elements use
-    extra = []
-    if world > 1 and a.extra_configs and a.config == "mbv2":
-        for name in [x for x in a.extra_configs.split(",") if x.strip()]:
-            xc = CONFIGS[name]
-            xm = xc["model"] + ("_fp32" if use_gpu else "")
-            if not use_gpu:
-                xm = xc["model"].replace("_fused", "").replace("_lowres", "")
-            xp = os.path.join(workdir, f"{xm}.pt")
-            export(xm, xp, layout="nhwc")
-            xb = (8 if name == "deeplab_fan" else 64) if use_gpu else 1
-            xs_steps, xs_warm = (a.extra_steps, 5) if use_gpu else (2, 1)  # (CPU twin: plain models, short)
-            r = run_pipeline(a, nns, xc, xm, xp, files, xb, xs_steps, xs_warm, rank, world, dev, use_gpu, dist)
-            r["steps"] = xs_steps
-            extra.append((name, xb, r))
-
     # per-rank records, all-gathered over the job's process group (RCCL on GPUs):
     # [elapsed, p50, p99, gpu_elapsed, gpu_busy] per engine + batch-1 p50/p99
     # + [max(sink, device) elapsed, p50] per sweep batch
@@ -501,145 +470,250 @@ def main():
     vec += [lat_b1["p50"], lat_b1["p99"]] if lat_b1 else [0.0, 0.0]
     for _, r in sweep:
         vec += [max(r["elapsed"], r["gpu_elapsed"]), r["p50"]]
-    for _, _, r in extra:
-        vec += [max(r["elapsed"], r["gpu_elapsed"])]
-    sc_keys = ["allgather", "allgather_ragged", "broadcast", "scatter", "p2p_ring", "p2p_exchange"]
-    if selfcheck is not None:
-        vec += [1.0 if selfcheck.get(k) else 0.0 for k in sc_keys] + [float(selfcheck["seconds"])]
-    stats = torch.tensor(vec, dtype=torch.float64)
-    if dist is not None:
-        if dist.get_backend() == "nccl":
-            stats = stats.cuda()
-        gathered = [torch.zeros_like(stats) for _ in range(world)]
-        dist.all_gather(gathered, stats)
-        per_rank = torch.stack([g.cpu() for g in gathered])  # [world, len]
-        pg_world, pg_backend = len(gathered), ("rccl" if dist.get_backend() == "nccl" else dist.get_backend())
-    else:
-        per_rank = stats.view(1, -1)
-        pg_world, pg_backend = 1, None
+    per_rank, pg_world, pg_backend = gather_rows(vec, world, dist, torch)
+    out = None
     if rank == 0:
-        head_label = runs[0][0]
-        head = results[head_label]
-        workers = head["workers"]
-        fan = head["fan"]
-        B = a.batch
+        out = headline_record(a, cfg, runs, results, lat_b1, sweep, per_rank, world, use_gpu, numa,
+                              pg_world, pg_backend, torch)
 
-        def agg(i, B=B):
-            cols = per_rank[:, i * 5:(i + 1) * 5]
-            active = cols  # every rank runs a branch (config 4: rank 0's own demux pad too)
-            sink_el = float(active[:, 0].max())
-            gpu_el = float(active[:, 3].max())
-            # the timed window on the slower of the two clocks: sink arrivals can
-            # run ahead of the device when batches computed during warmup are
-            # still queued at the window's start (up to queue-depth / K)
-            eff = torch.maximum(active[:, 0], active[:, 3])
-            elapsed = float(eff.max())
-            per = [round(a.steps * B / float(e), 2) if e > 0 else None for e in eff.tolist()]
-            return dict(
-                fps=workers * a.steps * B / elapsed if elapsed > 0 else 0.0,
-                sink_fps=workers * a.steps * B / sink_el if sink_el > 0 else 0.0,
-                ms=elapsed / a.steps * 1e3,
-                p50=float(active[:, 1].max()), p99=float(active[:, 2].max()),
-                gpu_fps=(workers * a.steps * B / gpu_el) if gpu_el > 0 else None,
-                gpu_busy=float(active[:, 4].max()), per_rank=per)
-
-        h = agg(0)
-        out = {
-            "metric": cfg["metric"],
-            "value": round(h["fps"], 2),
-            "unit": "frames/s",
-            "n_gpus": world if use_gpu else 0,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(h["ms"], 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": (round(h["fps"] / CPU_BASELINE_FPS, 2) if a.config == "mbv2" else None),
-            "dtype": head["dtype"],
-            "data": "synthetic video frames (videotestsrc pattern=snow), random-init weights",
-            "p50_latency_ms": None if (fan or cfg.get("gather")) else round(h["p50"], 3),
-            "p99_latency_ms": None if (fan or cfg.get("gather")) else round(h["p99"], 3),
-            "gpu_event_fps": round(h["gpu_fps"], 2) if h["gpu_fps"] else None,
-            "sink_fps": round(h["sink_fps"], 2),
-            "timing": "value = frames / max(sink-arrival window, device-event window) of the same K batches",
-            "gpu_invoke_ms_median": round(h["gpu_busy"], 4),
-            "per_rank_fps": h["per_rank"],
-            # the per-rank records above travelled through one all_gather on this process group
-            "pg_world": pg_world,
-            "pg_backend": pg_backend,
-            "frames_per_step_per_gpu": B,
-        }
-        if "bf16" in results and head_label != "bf16":
-            bb = results["bf16"]["batch"]
-            b = agg(1, bb)
-            out.update(value_bf16=round(b["fps"], 2), ms_per_step_bf16=round(b["ms"], 4), batch_bf16=bb,
-                       p50_latency_ms_bf16=None if fan else round(b["p50"], 3),
-                       gpu_event_fps_bf16=round(b["gpu_fps"], 2) if b["gpu_fps"] else None,
-                       per_rank_fps_bf16=b["per_rank"])
-        if lat_b1:
-            n = len(runs)
-            out.update(p50_latency_ms_b1=round(float(per_rank[:, n * 5].max()), 3),
-                       p99_latency_ms_b1=round(float(per_rank[:, n * 5 + 1].max()), 3),
-                       latency_b1_source=f"live camera, {a.latency_fps or cfg.get('lat_fps', 500)} frames/s, batch 1")
-        if sweep:
-            n = len(runs)
-            base_i = n * 5 + 2
-            pts = []
-            for j, (sb, _) in enumerate(sweep):
-                el = float(per_rank[:, base_i + 2 * j].max())
-                pts.append({"batch": sb, "frames_per_s": round(workers * a.sweep_steps * sb / el, 1) if el > 0 else None,
-                            "p50_latency_ms": round(float(per_rank[:, base_i + 2 * j + 1].max()), 3)})
-            pts.append({"batch": B, "frames_per_s": round(h["fps"], 1), "p50_latency_ms": round(h["p50"], 3)})
-            out["sweep"] = sorted(pts, key=lambda d: d["batch"])
-        col = len(runs) * 5 + 2 + 2 * len(sweep)
-        if extra:
-            xs = {}
-            for j, (name, xb, r) in enumerate(extra):
-                el = float(per_rank[:, col + j].max())
-                xs[name] = {"frames_per_s": round(r["workers"] * r["steps"] * xb / el, 1) if el > 0 else None,
-                            "batch": xb, "steps": r["steps"],
-                            "rccl_world": max([int(v.split(":")[1]) for v in r["groups"].values()
-                                               if v.startswith("rccl:")] or [0]),
-                            "groups_rank0": r["groups"]}
-            out["extra_configs"] = xs
-            col += len(extra)
-        if selfcheck is not None:
-            flags = per_rank[:, col:col + len(sc_keys)].min(0).values.tolist()
-            out["rccl_selfcheck"] = {**{k: bool(f > 0.5) for k, f in zip(sc_keys, flags)},
-                                     "backend": selfcheck["backend"], "members": selfcheck["size"],
-                                     "seconds_max": round(float(per_rank[:, col + len(sc_keys)].max()), 3),
-                                     "payloads": "64 MB all-gather / broadcast / scatter, 3-70 MB ragged all-gather, "
-                                                 "48 MB p2p ring, 32 MB all-to-all" if use_gpu else "1/64 scale (CPU)"}
-        try:
-            out["fp32_method"] = str(torch.ops.nnsx.f32_math())
-        except Exception:  # noqa: BLE001
-            out["fp32_method"] = None
-        out.update({
-            "preprocess": (f"tensor_transform (reference string) absorbed by tensor_filter into the model's uint8 "
-                           f"input table ({head['absorbed']}: frames stay uint8)" if head["absorbed"]
-                           else "tensor_transform element (own kernel, float32 frames into the model)"),
-            "postprocess": (f"image_labeling argmax run by tensor_filter inside its hipGraph ({head['absorbed_dec']}: "
-                            "int32 indices leave the model)" if head.get("absorbed_dec")
-                            else "tensor_decoder's own argmax kernel"),
-            "wall_s": round(sum(r["wall"] for r in results.values()), 3),
-            "numa_binding": numa,
-            **({"allgather_bytes_published_rank0": head["gathered"]} if head["gathered"] is not None else {}),
-            **({"mux_sets_rank0": head["mux_sets"]} if head.get("mux_sets") is not None else {}),
-            # nnsx rank groups of rank 0 ("<data plane>:<members>[:bytes]") and the RCCL world they span
-            "nnsx_groups_rank0": head["groups"],
-            "rccl_world": max([int(v.split(":")[1]) for v in head["groups"].values() if v.startswith("rccl:")] or [0]),
-            "config": {
-                "model": cfg["desc"],
-                "global_batch": B * world,
-                "seq_len": 1,
-                "parallelism": (f"tensor_demux fan-out 1->{world} (RCCL p2p)" if fan else
-                                f"branch-dp{world} + edge all-gather" if cfg.get("gather") else f"branch-dp{world}"),
-                "pipeline": head["desc"],
-            },
-        })
+    # WORLD_SIZE > 1, AFTER the headline is recorded: the rank-group data-plane
+    # self-check (every comm::Group operation on frame-sized payloads) and short
+    # passes of the multi-rank configs (config 4's demux fan-out over RCCL p2p,
+    # config 5's edge all-gather).  Each is guarded on its own (an exception is
+    # recorded, not raised) and a watchdog bounds the whole auxiliary phase: if
+    # it expires, rank 0 prints the headline with `aux_timeout` and every rank
+    # exits 0, so no auxiliary pass can cost the headline record.
+    if world > 1 and (not a.no_selfcheck or a.extra_configs):
+        run_aux(a, nns, cfg, files, rank, world, dev, use_gpu, dist, workdir, out, torch, np)
+    if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+SC_KEYS = ["allgather", "allgather_ragged", "broadcast", "scatter", "p2p_ring", "p2p_exchange"]
+
+
+def gather_rows(vec, world, dist, torch):
+    """One all_gather of a per-rank float vector over the job's process group."""
+    stats = torch.tensor(vec, dtype=torch.float64)
+    if dist is None:
+        return stats.view(1, -1), 1, None
+    if dist.get_backend() == "nccl":
+        stats = stats.cuda()
+    gathered = [torch.zeros_like(stats) for _ in range(world)]
+    dist.all_gather(gathered, stats)
+    per_rank = torch.stack([g.cpu() for g in gathered])  # [world, len]
+    return per_rank, len(gathered), ("rccl" if dist.get_backend() == "nccl" else dist.get_backend())
+
+
+def headline_record(a, cfg, runs, results, lat_b1, sweep, per_rank, world, use_gpu, numa, pg_world, pg_backend,
+                    torch):
+    head_label = runs[0][0]
+    head = results[head_label]
+    workers = head["workers"]
+    fan = head["fan"]
+    B = a.batch
+
+    def agg(i, B=B):
+        cols = per_rank[:, i * 5:(i + 1) * 5]
+        active = cols  # every rank runs a branch (config 4: rank 0's own demux pad too)
+        sink_el = float(active[:, 0].max())
+        gpu_el = float(active[:, 3].max())
+        # the timed window on the slower of the two clocks: sink arrivals can
+        # run ahead of the device when batches computed during warmup are
+        # still queued at the window's start (up to queue-depth / K)
+        eff = torch.maximum(active[:, 0], active[:, 3])
+        elapsed = float(eff.max())
+        per = [round(a.steps * B / float(e), 2) if e > 0 else None for e in eff.tolist()]
+        return dict(
+            fps=workers * a.steps * B / elapsed if elapsed > 0 else 0.0,
+            sink_fps=workers * a.steps * B / sink_el if sink_el > 0 else 0.0,
+            ms=elapsed / a.steps * 1e3,
+            p50=float(active[:, 1].max()), p99=float(active[:, 2].max()),
+            gpu_fps=(workers * a.steps * B / gpu_el) if gpu_el > 0 else None,
+            gpu_busy=float(active[:, 4].max()), per_rank=per)
+
+    h = agg(0)
+    out = {
+        "metric": cfg["metric"],
+        "value": round(h["fps"], 2),
+        "unit": "frames/s",
+        "n_gpus": world if use_gpu else 0,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(h["ms"], 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": (round(h["fps"] / CPU_BASELINE_FPS, 2) if a.config == "mbv2" else None),
+        "dtype": head["dtype"],
+        "data": "synthetic video frames (videotestsrc pattern=snow), random-init weights",
+        "p50_latency_ms": None if (fan or cfg.get("gather")) else round(h["p50"], 3),
+        "p99_latency_ms": None if (fan or cfg.get("gather")) else round(h["p99"], 3),
+        "gpu_event_fps": round(h["gpu_fps"], 2) if h["gpu_fps"] else None,
+        "sink_fps": round(h["sink_fps"], 2),
+        "timing": "value = frames / max(sink-arrival window, device-event window) of the same K batches",
+        "gpu_invoke_ms_median": round(h["gpu_busy"], 4),
+        "per_rank_fps": h["per_rank"],
+        # the per-rank records above travelled through one all_gather on this process group
+        "pg_world": pg_world,
+        "pg_backend": pg_backend,
+        "frames_per_step_per_gpu": B,
+    }
+    if "bf16" in results and head_label != "bf16":
+        bb = results["bf16"]["batch"]
+        b = agg(1, bb)
+        out.update(value_bf16=round(b["fps"], 2), ms_per_step_bf16=round(b["ms"], 4), batch_bf16=bb,
+                   p50_latency_ms_bf16=None if fan else round(b["p50"], 3),
+                   gpu_event_fps_bf16=round(b["gpu_fps"], 2) if b["gpu_fps"] else None,
+                   per_rank_fps_bf16=b["per_rank"])
+    if lat_b1:
+        n = len(runs)
+        out.update(p50_latency_ms_b1=round(float(per_rank[:, n * 5].max()), 3),
+                   p99_latency_ms_b1=round(float(per_rank[:, n * 5 + 1].max()), 3),
+                   latency_b1_source=f"live camera, {a.latency_fps or cfg.get('lat_fps', 500)} frames/s, batch 1")
+    if sweep:
+        n = len(runs)
+        base_i = n * 5 + 2
+        pts = []
+        for j, (sb, _) in enumerate(sweep):
+            el = float(per_rank[:, base_i + 2 * j].max())
+            pts.append({"batch": sb, "frames_per_s": round(workers * a.sweep_steps * sb / el, 1) if el > 0 else None,
+                        "p50_latency_ms": round(float(per_rank[:, base_i + 2 * j + 1].max()), 3)})
+        pts.append({"batch": B, "frames_per_s": round(h["fps"], 1), "p50_latency_ms": round(h["p50"], 3)})
+        out["sweep"] = sorted(pts, key=lambda d: d["batch"])
+    try:
+        out["fp32_method"] = str(torch.ops.nnsx.f32_math())
+    except Exception:  # noqa: BLE001
+        out["fp32_method"] = None
+    out.update({
+        "preprocess": (f"tensor_transform (reference string) absorbed by tensor_filter into the model's uint8 "
+                       f"input table ({head['absorbed']}: frames stay uint8)" if head["absorbed"]
+                       else "tensor_transform element (own kernel, float32 frames into the model)"),
+        "postprocess": (f"image_labeling argmax run by tensor_filter inside its hipGraph ({head['absorbed_dec']}: "
+                        "int32 indices leave the model)" if head.get("absorbed_dec")
+                        else "tensor_decoder's own argmax kernel"),
+        "wall_s": round(sum(r["wall"] for r in results.values()), 3),
+        "numa_binding": numa,
+        **({"allgather_bytes_published_rank0": head["gathered"]} if head["gathered"] is not None else {}),
+        **({"mux_sets_rank0": head["mux_sets"]} if head.get("mux_sets") is not None else {}),
+        # nnsx rank groups of rank 0 ("<data plane>:<members>[:bytes]") and the RCCL world they span
+        "nnsx_groups_rank0": head["groups"],
+        "rccl_world": max([int(v.split(":")[1]) for v in head["groups"].values() if v.startswith("rccl:")] or [0]),
+        "config": {
+            "model": cfg["desc"],
+            "global_batch": B * world,
+            "seq_len": 1,
+            "parallelism": (f"tensor_demux fan-out 1->{world} (RCCL p2p)" if fan else
+                            f"branch-dp{world} + edge all-gather" if cfg.get("gather") else f"branch-dp{world}"),
+            "pipeline": head["desc"],
+        },
+    })
+    return out
+
+
+def run_aux(a, nns, cfg, files, rank, world, dev, use_gpu, dist, workdir, out, torch, np):
+    """Self-check + extra multi-rank configs after the headline (see main)."""
+    import threading
+
+    printed = threading.Lock()
+    done = threading.Event()
+
+    def expire():
+        if done.is_set():
+            return
+        with printed:
+            if rank == 0 and out is not None:
+                out["aux_timeout"] = (f"the self-check / extra configs did not finish within {a.aux_timeout} s; "
+                                      "the headline above is complete")
+                print(json.dumps(out), flush=True)
+            print(f"rank {rank}: auxiliary phase timed out after {a.aux_timeout} s", file=sys.stderr, flush=True)
+            os._exit(0)
+
+    watchdog = threading.Timer(a.aux_timeout, expire)
+    watchdog.daemon = True
+    watchdog.start()
+    selfcheck, sc_error = None, None
+    if not a.no_selfcheck:
+        from nnstreamer_amd.parallel import selfcheck as sc
+
+        if use_gpu:
+            def arr(v, d=dev):
+                return torch.as_tensor(v).cuda(d)
+        else:
+            def arr(v):
+                return np.asarray(v)
+        try:
+            g = nns.Group("bench/selfcheck", rank, world, "", dev, a.comm_backend if use_gpu else "tcp",
+                          a.selfcheck_timeout_ms)
+            selfcheck = sc.run(g, rank, world, arr, scale=1.0 if use_gpu else 1.0 / 64,
+                               recv_timeout_ms=a.selfcheck_timeout_ms)
+            del g
+        except Exception as e:  # noqa: BLE001
+            sc_error = str(e)[:300]
+        print(f"rank {rank}: rccl_selfcheck {selfcheck or sc_error}", file=sys.stderr, flush=True)
+    extra = []
+    if a.extra_configs and a.config == "mbv2":
+        for name in [x for x in a.extra_configs.split(",") if x.strip()]:
+            xb = (8 if name == "deeplab_fan" else 64) if use_gpu else 1
+            xs_steps, xs_warm = (a.extra_steps, 5) if use_gpu else (2, 1)  # (CPU twin: plain models, short)
+            try:
+                xc = CONFIGS[name]
+                xm = xc["model"] + "_fp32" if use_gpu else xc["model"].replace("_fused", "").replace("_lowres", "")
+                xp = os.path.join(workdir, f"{xm}.pt")
+                from nnstreamer_amd.models.export import export
+
+                export(xm, xp, layout="nhwc")
+                r = run_pipeline(a, nns, xc, xm, xp, files, xb, xs_steps, xs_warm, rank, world, dev, use_gpu, dist)
+                r["steps"] = xs_steps
+                extra.append((name, xb, r, None))
+            except BaseException as e:  # noqa: BLE001 -- (SystemExit from run_pipeline included)
+                extra.append((name, xb, None, str(e)[:300]))
+    # [self-check flags, seconds, ok] + [elapsed or -1] per extra config
+    vec = ([1.0 if (selfcheck or {}).get(k) else 0.0 for k in SC_KEYS]
+           + [float((selfcheck or {}).get("seconds", 0.0)), 1.0 if selfcheck is not None else 0.0])
+    vec += [max(r["elapsed"], r["gpu_elapsed"]) if r is not None else -1.0 for _, _, r, _ in extra]
+    try:
+        per_rank, _, _ = gather_rows(vec, world, dist, torch)
+    except Exception as e:  # noqa: BLE001
+        per_rank = None
+        if out is not None:
+            out["aux_error"] = f"gathering the auxiliary records failed: {str(e)[:200]}"
+    done.set()
+    watchdog.cancel()
+    if rank != 0 or out is None or per_rank is None:
+        return
+    nk = len(SC_KEYS)
+    if not a.no_selfcheck:
+        ran = bool(float(per_rank[:, nk + 1].min()) > 0.5)
+        flags = per_rank[:, :nk].min(0).values.tolist()
+        rec = {**{k: bool(f > 0.5) for k, f in zip(SC_KEYS, flags)},
+               "backend": (selfcheck or {}).get("backend"), "members": (selfcheck or {}).get("size"),
+               "seconds_max": round(float(per_rank[:, nk].max()), 3),
+               "payloads": ("64 MB all-gather / broadcast / scatter, 3-70 MB ragged all-gather, 48 MB p2p ring, "
+                            "32 MB all-to-all" if use_gpu else "1/64 scale (CPU)")}
+        rec["ok"] = ran and all(rec[k] for k in SC_KEYS)
+        if selfcheck and selfcheck.get("errors"):
+            rec["errors_rank0"] = selfcheck["errors"]
+        if sc_error:
+            rec["error_rank0"] = sc_error
+        if not ran:
+            rec["error"] = "the self-check did not run on every rank"
+        out["rccl_selfcheck"] = rec
+    if extra:
+        xs = {}
+        for j, (name, xb, r, e) in enumerate(extra):
+            col = per_rank[:, nk + 2 + j]
+            if float(col.min()) < 0 or r is None:
+                xs[name] = {"frames_per_s": None, "batch": xb, "error_rank0": e or "failed on another rank"}
+                continue
+            el = float(col.max())
+            xs[name] = {"frames_per_s": round(r["workers"] * r["steps"] * xb / el, 1) if el > 0 else None,
+                        "batch": xb, "steps": r["steps"],
+                        "rccl_world": max([int(v.split(":")[1]) for v in r["groups"].values()
+                                           if v.startswith("rccl:")] or [0]),
+                        "groups_rank0": r["groups"]}
+        out["extra_configs"] = xs
 
 
 if __name__ == "__main__":

@@ -188,10 +188,8 @@ constexpr uint32_t kPktMagic = 0x4b50584eu;  // "NXPK"
 std::mutex g_groups_mu;
 std::map<std::string, std::weak_ptr<Group>> g_groups;
 
-// Process-local hand-off for point-to-point sends to oneself (a query client
-// and server in the same process): the header still goes through the store so
-// the FIFO order is shared with remote senders; the blobs stay zero-copy.
-constexpr uint64_t kTagP2P = 0;  // mesh tags: p2p messages; collectives use 1 + their sequence
+// manifests of round r travel with mesh tag r + 1
+constexpr uint32_t kRoundMagic = 0x44525851u;  // "QXRD"
 
 }  // namespace
 
@@ -304,65 +302,71 @@ void Mesh::reader(std::shared_ptr<Connection> c) {
   }
   while (true) {
     Message m;
-    if (!c->recv(&m, -1, nullptr)) {
-      std::lock_guard<std::mutex> lk(mu_);
-      if (!closed_.load()) lost_[static_cast<size_t>(src)] = 1;  // broke without a goodbye
+    const bool got = c->recv(&m, -1, nullptr);
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!got || m.type == MsgType::BYE) {
+      // everything the member sent before is already queued (one ordered stream)
+      if (!closed_.load()) lost_[static_cast<size_t>(src)] = got ? 3 : 1;
       cv_.notify_all();
       return;
     }
-    if (m.type == MsgType::BYE) return;
-    std::lock_guard<std::mutex> lk(mu_);
-    const uint64_t tag = m.seq;
-    inbox_.push_back(Item{src, tag, std::move(m)});
+    inbox_.push_back(Item{src, m.seq, std::move(m)});
     cv_.notify_all();
   }
 }
 
+bool Mesh::ensure_link(int peer, std::string* err) {
+  auto& c = out_[static_cast<size_t>(peer)];
+  if (c) return true;
+  std::string addr, host;
+  int port = 0;
+  if (!store_->get(strfmt(prefix_, "/mesh/", peer), &addr, timeout_ms_) || !split_hostport(addr, &host, &port)) {
+    if (err) *err = strfmt("mesh: no link address of member ", peer);
+    return false;
+  }
+  c = Connection::connect(host, port, timeout_ms_, err);
+  if (!c) return false;
+  Message h;
+  h.type = MsgType::HELLO;
+  h.client_id = static_cast<uint64_t>(grank_);
+  if (!c->send(h)) {
+    c.reset();
+    if (err) *err = strfmt("mesh: cannot greet member ", peer);
+    return false;
+  }
+  return true;
+}
+
+bool Mesh::connect_all(std::string* err) {
+  for (int r = 0; r < n_; ++r) {
+    if (r == grank_) continue;
+    std::lock_guard<std::mutex> lk(out_mu_[static_cast<size_t>(r)]);
+    if (!ensure_link(r, err)) return false;
+  }
+  return true;
+}
+
 bool Mesh::send(int peer, uint64_t tag, Message m, std::string* err) {
   std::lock_guard<std::mutex> lk(out_mu_[static_cast<size_t>(peer)]);
-  auto& c = out_[static_cast<size_t>(peer)];
-  if (!c) {
-    std::string addr, host;
-    int port = 0;
-    if (!store_->get(strfmt(prefix_, "/mesh/", peer), &addr, timeout_ms_) || !split_hostport(addr, &host, &port)) {
-      if (err) *err = strfmt("mesh: no link address of member ", peer);
-      return false;
-    }
-    c = Connection::connect(host, port, timeout_ms_, err);
-    if (!c) return false;
-    Message h;
-    h.type = MsgType::HELLO;
-    h.client_id = static_cast<uint64_t>(grank_);
-    if (!c->send(h)) {
-      c.reset();
-      if (err) *err = strfmt("mesh: cannot greet member ", peer);
-      return false;
-    }
-  }
+  if (!ensure_link(peer, err)) return false;
   m.type = MsgType::DATA;
   m.seq = tag;
-  if (!c->send(m)) {
+  if (!out_[static_cast<size_t>(peer)]->send(m)) {
     if (err) *err = strfmt("mesh: the link to member ", peer, " broke");
     return false;
   }
   return true;
 }
 
-void Mesh::deliver_local(uint64_t tag, Message m) {
-  std::lock_guard<std::mutex> lk(mu_);
-  inbox_.push_back(Item{grank_, tag, std::move(m)});
-  cv_.notify_all();
-}
-
-bool Mesh::recv(uint64_t tag, int src, Message* m, int* from, int timeout_ms, bool* timed_out, std::string* err) {
+bool Mesh::recv(uint64_t tag, int src, Message* m, int timeout_ms, bool* timed_out, int* gone, std::string* err) {
   if (timed_out) *timed_out = false;
+  if (gone) *gone = 0;
   const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(std::max(0, timeout_ms));
   std::unique_lock<std::mutex> lk(mu_);
   while (true) {
     for (auto it = inbox_.begin(); it != inbox_.end(); ++it)
-      if (it->tag == tag && (src < 0 || it->src == src)) {
+      if (it->tag == tag && it->src == src) {
         *m = std::move(it->m);
-        if (from) *from = it->src;
         inbox_.erase(it);
         return true;
       }
@@ -370,30 +374,10 @@ bool Mesh::recv(uint64_t tag, int src, Message* m, int* from, int timeout_ms, bo
       if (err) *err = "mesh: closed";
       return false;
     }
-    if (src >= 0) {
-      if (lost_[static_cast<size_t>(src)]) {
-        if (err) *err = strfmt("lost the link to member ", src);
-        return false;
-      }
-    } else {
-      // any-source: one member's broken link must not stop the traffic of the
-      // live ones (a query server keeps serving its other clients).  The loss
-      // is reported once per member; the receive fails only when no other
-      // member is left that could still send.
-      int alive = 0;
-      for (int r = 0; r < n_; ++r) {
-        if (r == grank_) continue;
-        if (!lost_[static_cast<size_t>(r)]) {
-          ++alive;
-        } else if (lost_[static_cast<size_t>(r)] == 1) {
-          lost_[static_cast<size_t>(r)] = 2;  // reported
-          NNSX_LOGW("mesh", "lost the link to member ", r, " (any-source receives continue with the others)");
-        }
-      }
-      if (alive == 0 && n_ > 1) {
-        if (err) *err = "mesh: lost the links to every other member";
-        return false;
-      }
+    if (const int l = lost_[static_cast<size_t>(src)]) {
+      if (gone) *gone = l;
+      if (err) *err = l == 3 ? strfmt("member ", src, " left") : strfmt("lost the link to member ", src);
+      return false;
     }
     if (timeout_ms < 0) {
       cv_.wait(lk);
@@ -402,6 +386,23 @@ bool Mesh::recv(uint64_t tag, int src, Message* m, int* from, int timeout_ms, bo
       return false;
     }
   }
+}
+
+int Mesh::wait_tag(uint64_t tag, const std::function<bool()>& wake, int timeout_ms) {
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(std::max(0, timeout_ms));
+  std::unique_lock<std::mutex> lk(mu_);
+  while (true) {
+    if (closed_.load()) return -1;
+    for (auto& it : inbox_)
+      if (it.tag == tag) return 1;
+    if (wake()) return 0;
+    if (cv_.wait_until(lk, deadline) == std::cv_status::timeout) return 0;
+  }
+}
+
+void Mesh::poke() {
+  std::lock_guard<std::mutex> lk(mu_);
+  cv_.notify_all();
 }
 
 void Mesh::close() {
@@ -413,7 +414,7 @@ void Mesh::close() {
     if (!out_[r]) continue;
     Message bye;
     bye.type = MsgType::BYE;
-    (void)out_[r]->send(bye);  // orderly goodbye: the peer's reader ends without a "lost" mark
+    (void)out_[r]->send(bye);  // orderly goodbye: the peer drops us from later rounds
     out_[r]->close();
   }
   std::vector<std::thread> readers;
@@ -440,22 +441,47 @@ std::shared_ptr<void> host_store(const std::string& host, int port, bool* in_use
 }
 
 // ================================================================= group ====
-Group::~Group() {
-  mesh_.reset();  // goodbyes first: peers see an orderly end of our links
-  for (auto* links : {&tx_, &rx_})
-    for (auto& l : *links) {
-      if (!l.comm) continue;
-      hip::DeviceGuard g(device_);
-      if (l.stream) (void)hipStreamSynchronize(l.stream);
-      ncclCommDestroy(static_cast<ncclComm_t>(l.comm));
-      if (l.stream) hip::stream_destroy(device_, l.stream);
+namespace {
+void set_metas(std::vector<MemoryPtr>* blobs, const std::vector<std::string>& metas) {
+  for (size_t i = 0; i < blobs->size() && i < metas.size(); ++i)
+    if (!metas[i].empty()) {
+      MetaInfo mi;
+      if (MetaInfo::parse(metas[i].data(), metas[i].size(), &mi)) (*blobs)[i]->set_meta(mi);
     }
+}
+}  // namespace
+
+Group::~Group() {
+  stop_engine();
+  mesh_.reset();  // (already closed by the progress thread: goodbyes)
   if (comm_) {
     hip::DeviceGuard g(device_);
-    if (stream_) (void)hipStreamSynchronize(stream_);
-    ncclCommDestroy(static_cast<ncclComm_t>(comm_));
+    // the issued rounds must finish before the communicator goes; one that
+    // cannot (a member died mid-round) is aborted instead of hanging here
+    const int64_t deadline = now_ns() + static_cast<int64_t>(op_timeout_ms_) * 1000000;
+    while (!inflight_.empty() && !aborted_.load()) {
+      const hipError_t q = hipEventQuery(inflight_.front().ev);
+      if (q == hipErrorNotReady && now_ns() < deadline) {
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+        continue;
+      }
+      if (q != hipSuccess) {
+        NNSX_LOGE("comm", "group ", spec_.name, ": round ", inflight_.front().round,
+                  " did not complete before the group closed; aborting the communicator");
+        ncclCommAbort(static_cast<ncclComm_t>(comm_));
+        aborted_ = true;
+        break;
+      }
+      hip::event_put(device_, inflight_.front().ev);
+      inflight_.pop_front();
+    }
+    if (!aborted_.load()) {
+      if (stream_) (void)hipStreamSynchronize(stream_);
+      ncclCommDestroy(static_cast<ncclComm_t>(comm_));
+    }
   }
-  if (stream_) hip::stream_destroy(device_, stream_);
+  for (auto& f : inflight_) (void)hipEventDestroy(f.ev);
+  if (stream_ && !aborted_.load()) hip::stream_destroy(device_, stream_);
   if (store_) store_->close();
 }
 
@@ -482,12 +508,13 @@ bool Group::init(const GroupSpec& in, std::string* err) {
   device_ = spec_.device;
   // [rccl] section (ini / NNSTREAMER_rccl_<key>): job-wide defaults for what
   // an element or spec leaves unset -- backend (auto|rccl|tcp), store
-  // (host:port of the control-plane store), timeout_ms (rendezvous and
-  // control-plane waits)
+  // (host:port of the control-plane store), timeout_ms (rendezvous, manifest
+  // and collective waits), op_timeout_ms (device completion of a round)
   const Config& cfg = Config::get();
   if (spec_.backend.empty() || spec_.backend == "auto") spec_.backend = cfg.custom_value("rccl", "backend", "auto");
   if (spec_.timeout_ms <= 0)
     spec_.timeout_ms = static_cast<int>(to_int(cfg.custom_value("rccl", "timeout_ms", "60000"), 60000));
+  op_timeout_ms_ = static_cast<int>(to_int(cfg.custom_value("rccl", "op_timeout_ms", ""), spec_.timeout_ms));
   // ---- control plane ----
   std::string addr = spec_.store;
   if (addr.empty()) addr = cfg.custom_value("rccl", "store", "");
@@ -534,12 +561,11 @@ bool Group::init(const GroupSpec& in, std::string* err) {
       return false;
     }
   }
-  tx_.assign(static_cast<size_t>(n), Link{});
-  rx_.assign(static_cast<size_t>(n), Link{});
-  // ---- member-to-member links (headers; payloads too on the tcp backend) ----
+  // ---- member-to-member links (manifests; payloads too on the tcp backend) ----
   if (n > 1) {
     mesh_ = std::make_unique<Mesh>();
-    if (!mesh_->start(store_.get(), prefix_, grank_, n, spec_.timeout_ms, err)) return false;
+    if (!mesh_->start(store_.get(), prefix_, grank_, n, spec_.timeout_ms, err) || !mesh_->connect_all(err))
+      return false;
   }
   // ---- data plane: RCCL when every member holds a GPU ----
   bool all_dev = device_ >= 0 && hip::available();
@@ -582,36 +608,54 @@ bool Group::init(const GroupSpec& in, std::string* err) {
     ncclComm_t c = nullptr;
     if (!nccl_ok(ncclCommInitRank(&c, n, id, grank_), "ncclCommInitRank", err)) return false;
     comm_ = c;
-    // every per-direction p2p link, now: member pairs (a < b) in lexicographic
-    // order, a -> b then b -> a.  Each member walks its own pairs in that order,
-    // so the smallest pair not yet linked always has both members waiting on it
-    // and the walk cannot deadlock; created lazily at a pair's first message
-    // instead, a sender blocked until its peer reached recv(), and members that
-    // all send before they receive waited on each other until the timeout.
-    for (int a = 0; a < n; ++a)
-      for (int b = a + 1; b < n; ++b) {
-        if (grank_ != a && grank_ != b) continue;
-        const int peer = grank_ == a ? b : a;
-        Link* l = nullptr;
-        if (!link(peer, grank_ == a, &l, err) || !link(peer, grank_ == b, &l, err)) return false;
-      }
   }
+  outbox_.assign(static_cast<size_t>(n), {});
+  unconsumed_.assign(static_cast<size_t>(n), 0);
+  allowed_.assign(static_cast<size_t>(n), kWindow);
+  granted_.assign(static_cast<size_t>(n), kWindow);
+  active_.assign(static_cast<size_t>(n), 1);
+  listed_upto_.assign(static_cast<size_t>(n), 0);
+  engine_ = n > 1 || rccl();
+  if (engine_) thr_ = std::thread([this] { progress(); });
   NNSX_LOGD("comm", "group ", spec_.name, " rank ", grank_, "/", n, " backend ", backend_name(), " store ", addr);
   return true;
 }
 
+std::string Group::failure() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return failed_;
+}
+
+void Group::poke() {
+  if (mesh_) {
+    mesh_->poke();
+  } else {
+    std::lock_guard<std::mutex> lk(mu_);
+    cv_.notify_all();
+  }
+}
+
+void Group::stop_engine() {
+  stop_ = true;
+  poke();
+  if (thr_.joinable()) thr_.join();
+}
+
 void Group::cancel() {
   if (store_) store_->close();
-  if (mesh_) mesh_->close();
-  std::lock_guard<std::mutex> lk(local_mu_);
-  cancelled_.store(true);
-  local_cv_.notify_all();
+  cancelled_ = true;
+  stop_ = true;  // the progress thread finishes the round it is in, then says goodbye
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    cv_.notify_all();
+  }
+  poke();
 }
 
 bool Group::put(const std::string& k, const std::string& v, int readers) { return store_->set(key(k), v, readers); }
 bool Group::get(const std::string& k, std::string* v, int timeout_ms) { return store_->get(key(k), v, timeout_ms); }
 
-std::string Group::encode(const Packet& p, bool inline_payload) {
+std::string Group::encode(const Packet& p) {
   std::string s;
   put_u32(s, kPktMagic);
   put_u32(s, static_cast<uint32_t>(p.blobs.size()));
@@ -633,16 +677,10 @@ std::string Group::encode(const Packet& p, bool inline_payload) {
       s.append(h, kMetaHeaderSize);
     }
   }
-  if (inline_payload)
-    for (auto& b : p.blobs) {
-      if (b->size()) s.append(static_cast<const char*>(b->map_host()), b->size());
-      bytes_sent_ += b->size();
-    }
   return s;
 }
 
-bool Group::decode(const std::string& s, Packet* p, bool inline_payload, std::vector<size_t>* sizes,
-                   std::vector<std::string>* metas) {
+bool Group::decode(const std::string& s, Packet* p, std::vector<size_t>* sizes, std::vector<std::string>* metas) {
   Reader r{s};
   if (r.get<uint32_t>() != kPktMagic) return false;
   const uint32_t nb = r.get<uint32_t>();
@@ -661,340 +699,545 @@ bool Group::decode(const std::string& s, Packet* p, bool inline_payload, std::ve
     metas->push_back(r.get<uint32_t>() ? r.bytes(kMetaHeaderSize) : std::string());
   }
   p->blobs.clear();
-  if (inline_payload) {
-    for (uint32_t i = 0; i < nb && r.ok; ++i) {
-      auto m = Memory::alloc_pinned((*sizes)[i]);
-      const std::string b = r.bytes((*sizes)[i]);
-      if (!b.empty()) std::memcpy(m->data(), b.data(), b.size());
-      if (!(*metas)[i].empty()) {
-        MetaInfo mi;
-        if (MetaInfo::parse((*metas)[i].data(), (*metas)[i].size(), &mi)) m->set_meta(mi);
-      }
-      bytes_recv_ += m->size();
-      p->blobs.push_back(m);
-    }
-  }
   return r.ok;
 }
 
-void* Group::dev_ptr(const MemoryPtr& m) { return dev_ptr_on(m, stream_); }
-
-void* Group::dev_ptr_on(const MemoryPtr& m, hipStream_t s) {
+void* Group::dev_ptr(const MemoryPtr& m) {
   if (m->on_device() && m->device() == device_) {
-    m->wait_ready(s);
+    m->wait_ready(stream_);
     return m->data();
   }
   // host blob (or another GPU's): stage it onto ours, ordered on the comm stream
-  return const_cast<void*>(m->map_device(device_, s));
+  return const_cast<void*>(m->map_device(device_, stream_));
 }
 
 std::vector<MemoryPtr> Group::alloc_recv(const std::vector<size_t>& sizes, const std::vector<std::string>& metas) {
   std::vector<MemoryPtr> out;
   for (size_t i = 0; i < sizes.size(); ++i) {
-    auto m = sizes[i] ? Memory::alloc_device(sizes[i], device_, stream_) : Memory::alloc_host(0);
-    if (!metas[i].empty()) {
-      MetaInfo mi;
-      if (MetaInfo::parse(metas[i].data(), metas[i].size(), &mi)) m->set_meta(mi);
-    }
+    out.push_back(sizes[i] ? Memory::alloc_device(sizes[i], device_, stream_) : Memory::alloc_host(0));
     bytes_recv_ += sizes[i];
-    out.push_back(m);
   }
+  set_metas(&out, metas);
   return out;
 }
 
-void Group::finish_inputs(const std::vector<MemoryPtr>& in, hipStream_t s) {
+void Group::finish_inputs(const std::vector<MemoryPtr>& in) {
   for (auto& m : in)
-    if (m->size()) m->record_use(s ? s : stream_, device_);
+    if (m->size()) m->record_use(stream_, device_);
 }
 
-// Per-direction pair communicator (created for every pair at init, in a fixed
-// order; see Group::init).  The sender publishes a unique id and waits
-// (bounded, cancellable: the store) until the receiver has fetched it; only
-// then do both enter the blocking ncclCommInitRank, so a member that never
-// joins costs its peer a timeout, not a hang.
-bool Group::link(int peer, bool tx, Link** out, std::string* err) {
-  Link& l = (tx ? tx_ : rx_).at(static_cast<size_t>(peer));
-  *out = &l;
-  if (l.comm) return true;
-  const int src = tx ? grank_ : peer, dst = tx ? peer : grank_;
-  const std::string k = strfmt("p2p/", src, ">", dst);
-  ncclUniqueId id;
-  if (tx) {
-    if (!nccl_ok(ncclGetUniqueId(&id), "ncclGetUniqueId", err)) return false;
-    std::string v;
-    if (!put(k + "/id", std::string(reinterpret_cast<const char*>(&id), sizeof(id)), 1) ||
-        !get(k + "/joined", &v, spec_.timeout_ms)) {
-      if (err) *err = strfmt("p2p link to member ", peer, ": the receiver did not join");
-      return false;
-    }
-  } else {
-    std::string v;
-    if (!get(k + "/id", &v, spec_.timeout_ms) || v.size() != sizeof(id)) {
-      if (err) *err = strfmt("p2p link from member ", peer, ": no RCCL unique id");
-      return false;
-    }
-    std::memcpy(&id, v.data(), sizeof(id));
-    if (!put(k + "/joined", "1", 1)) {
-      if (err) *err = "p2p link: store lost";
-      return false;
-    }
-  }
-  hip::DeviceGuard dg(device_);
-  int lo = 0, hi = 0;
-  (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-  ncclComm_t c = nullptr;
-  if (!nccl_ok(ncclCommInitRank(&c, 2, id, tx ? 0 : 1), "ncclCommInitRank(p2p)", err)) return false;
-  l.stream = hip::stream_create(device_, hi);
-  l.comm = c;
-  NNSX_LOGD("comm", "group ", spec_.name, ": p2p link ", src, " -> ", dst, " up");
-  return true;
-}
-
-bool Group::self_copy(const std::vector<MemoryPtr>& in, std::vector<MemoryPtr>* out, std::string* err) {
-  hip::DeviceGuard dg(device_);
-  auto comm = static_cast<ncclComm_t>(comm_);
-  out->clear();
-  std::vector<void*> src;
-  for (auto& b : in) {
-    src.push_back(b->size() ? dev_ptr(b) : nullptr);
-    auto m = b->size() ? Memory::alloc_device(b->size(), device_, stream_) : Memory::alloc_host(0);
-    if (b->has_meta()) m->set_meta(b->meta());
-    out->push_back(m);
-  }
-  if (!nccl_ok(ncclGroupStart(), "ncclGroupStart", err)) return false;
-  for (size_t i = 0; i < in.size(); ++i) {
-    if (!in[i]->size()) continue;
-    if (!nccl_ok(ncclSend(src[i], in[i]->size(), ncclUint8, grank_, comm, stream_), "ncclSend", err) ||
-        !nccl_ok(ncclRecv((*out)[i]->data(), in[i]->size(), ncclUint8, grank_, comm, stream_), "ncclRecv", err)) {
-      ncclGroupEnd();
-      return false;
-    }
-    bytes_sent_ += in[i]->size();
-    bytes_recv_ += in[i]->size();
-  }
-  if (!nccl_ok(ncclGroupEnd(), "ncclGroupEnd", err)) return false;
-  for (auto& m : *out)
-    if (m->size()) m->mark_ready(stream_);
-  finish_inputs(in);
-  return true;
-}
-
-// ------------------------------------------------------------ messages ----
-// packet -> mesh message: the encoded header rides in `caps`; on the tcp
-// backend the payload blobs follow it on the same link
-Message Group::to_message(const Packet& p) {
+// ------------------------------------------------------------ manifests ----
+// u32 magic | u64 round | u32 grant | u32 ncoll | per collective: u64 seq,
+// u32 kind, u32 root, u32 has_header, [u32 len, header] | u32 nsend | per
+// message: u32 len, header.  On tcp the payload blobs follow in the same
+// order (collective headers first, then the messages).
+Message Group::manifest_for(int d, uint32_t grant, const std::vector<std::shared_ptr<CollOp>>& colls,
+                            const std::vector<Packet>& sends) {
   Message m;
-  m.caps = encode(p, false);
-  if (!rccl()) {
-    m.blobs = p.blobs;
-    for (auto& b : p.blobs) bytes_sent_ += b->size();
+  std::string s;
+  put_u32(s, kRoundMagic);
+  put_u64(s, round_);
+  put_u32(s, grant);
+  put_u32(s, static_cast<uint32_t>(colls.size()));
+  for (auto& op : colls) {
+    put_u64(s, op->seq);
+    put_u32(s, op->kind);
+    put_u32(s, static_cast<uint32_t>(op->root));
+    const Packet* h = nullptr;
+    if (op->kind == CollOp::kAllGather || (op->kind == CollOp::kBroadcast && op->root == grank_)) h = &op->mine;
+    if (op->kind == CollOp::kScatter && op->root == grank_) h = &op->parts.at(static_cast<size_t>(d));
+    put_u32(s, h ? 1u : 0u);
+    if (!h) continue;
+    const std::string e = encode(*h);
+    put_u32(s, static_cast<uint32_t>(e.size()));
+    s += e;
+    if (!rccl()) m.blobs.insert(m.blobs.end(), h->blobs.begin(), h->blobs.end());
   }
+  put_u32(s, static_cast<uint32_t>(sends.size()));
+  for (auto& p : sends) {
+    const std::string e = encode(p);
+    put_u32(s, static_cast<uint32_t>(e.size()));
+    s += e;
+    if (!rccl()) m.blobs.insert(m.blobs.end(), p.blobs.begin(), p.blobs.end());
+  }
+  m.caps = std::move(s);
   return m;
 }
 
-// mesh message -> packet header (+ payload on the tcp backend)
-bool Group::from_message(Message&& m, Packet* p, std::vector<size_t>* sizes, std::vector<std::string>* metas) {
-  if (!decode(m.caps, p, false, sizes, metas)) return false;
-  if (rccl()) return true;
-  if (m.blobs.size() != sizes->size()) return false;
-  for (size_t i = 0; i < m.blobs.size(); ++i) {
-    if (!(*metas)[i].empty()) {
-      MetaInfo mi;
-      if (MetaInfo::parse((*metas)[i].data(), (*metas)[i].size(), &mi)) m.blobs[i]->set_meta(mi);
+bool Group::parse_manifest(Message&& m, Manifest* out) {
+  Reader r{m.caps};
+  if (r.get<uint32_t>() != kRoundMagic || r.get<uint64_t>() != round_) return false;
+  out->grant = r.get<uint32_t>();
+  size_t next_blob = 0;
+  auto take = [&](ManifestEntry* e) {
+    if (!decode(r.bytes(r.get<uint32_t>()), &e->hdr, &e->sizes, &e->metas)) return false;
+    if (rccl()) return true;
+    if (next_blob + e->sizes.size() > m.blobs.size()) return false;
+    e->hdr.blobs.assign(m.blobs.begin() + static_cast<std::ptrdiff_t>(next_blob),
+                        m.blobs.begin() + static_cast<std::ptrdiff_t>(next_blob + e->sizes.size()));
+    next_blob += e->sizes.size();
+    for (size_t i = 0; i < e->sizes.size(); ++i)
+      if (e->hdr.blobs[i]->size() != e->sizes[i]) return false;
+    set_metas(&e->hdr.blobs, e->metas);
+    return true;
+  };
+  const uint32_t nc = r.get<uint32_t>();
+  for (uint32_t i = 0; i < nc && r.ok; ++i) {
+    ManifestColl c;
+    c.seq = r.get<uint64_t>();
+    c.kind = r.get<uint32_t>();
+    c.root = static_cast<int>(r.get<uint32_t>());
+    c.has_hdr = r.get<uint32_t>() != 0;
+    if (c.has_hdr && !take(&c.e)) return false;
+    out->colls.push_back(std::move(c));
+  }
+  const uint32_t ns = r.get<uint32_t>();
+  for (uint32_t i = 0; i < ns && r.ok; ++i) {
+    ManifestEntry e;
+    if (!take(&e)) return false;
+    out->sends.push_back(std::move(e));
+  }
+  return r.ok;
+}
+
+// ---------------------------------------------------------- the engine ----
+void Group::progress() {
+  if (rccl()) (void)hipSetDevice(device_);
+  while (wait_trigger()) {
+    std::string e;
+    if (!reap(true, &e) || !run_round(&e)) {
+      fail(e);
+      break;
     }
-    bytes_recv_ += m.blobs[i]->size();
   }
-  p->blobs = std::move(m.blobs);
+  // leaving (stop / cancel / failure): an orderly goodbye on every link, so
+  // the other members drop this one from their next round
+  if (mesh_) mesh_->close();
+  std::lock_guard<std::mutex> lk(mu_);
+  const std::string why = !failed_.empty() ? failed_ : cancelled_.load() ? "cancelled" : "the group closed";
+  for (auto& op : colls_) {
+    op->done = true;
+    op->ok = false;
+    op->err = why;
+  }
+  colls_.clear();
+  cv_.notify_all();
+}
+
+bool Group::wait_trigger() {
+  while (!stop_.load()) {
+    if (work_.load()) return true;
+    if (mesh_) {
+      const int st = mesh_->wait_tag(round_ + 1, [this] { return work_.load() || stop_.load(); }, 100);
+      if (st < 0) return false;
+      if (st == 1) return true;
+    } else {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait_for(lk, std::chrono::milliseconds(100), [this] { return work_.load() || stop_.load(); });
+    }
+    std::string e;
+    if (!reap(false, &e)) {
+      fail(e);
+      return false;
+    }
+  }
+  return false;
+}
+
+// Completion of issued rounds, oldest first.  need_room: wait (bounded by the
+// operation deadline) until fewer than kInflight rounds are outstanding.  A
+// round past its deadline aborts the communicator: RCCL's kernels exit, and
+// the group fails with the round's operations and peers in the error.
+bool Group::reap(bool need_room, std::string* err) {
+  while (!inflight_.empty()) {
+    Inflight& f = inflight_.front();
+    const hipError_t q = hipEventQuery(f.ev);
+    if (q == hipSuccess) {
+      hip::event_put(device_, f.ev);
+      inflight_.pop_front();
+      continue;
+    }
+    if (q != hipErrorNotReady) {
+      *err = strfmt("round ", f.round, " (", f.what, "): ", hipGetErrorString(q));
+      return false;
+    }
+    if (now_ns() - f.t0 > static_cast<int64_t>(op_timeout_ms_) * 1000000) {
+      ncclCommAbort(static_cast<ncclComm_t>(comm_));
+      aborted_ = true;
+      *err = strfmt("round ", f.round, " (", f.what, ") did not complete on the device within ", op_timeout_ms_,
+                    " ms: a member stopped progressing; the communicator was aborted");
+      return false;
+    }
+    if (!need_room || inflight_.size() < kInflight) break;
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
   return true;
 }
 
-bool Group::recv_from(uint64_t tag, int src, Packet* p, std::vector<size_t>* sizes, std::vector<std::string>* metas,
-                      std::string* err, const char* what) {
-  Message m;
-  bool to = false;
-  std::string e;
-  if (!mesh_->recv(tag, src, &m, nullptr, spec_.timeout_ms, &to, &e) || !from_message(std::move(m), p, sizes, metas)) {
-    if (err) *err = strfmt(what, ": no message from member ", src, to ? " (timed out)" : (e.empty() ? "" : " (" + e + ")"));
-    return false;
+void Group::fail(const std::string& why) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!failed_.empty()) return;
+  failed_ = why.empty() ? std::string("the group failed") : why;
+  NNSX_LOGE("comm", "group ", spec_.name, " (member ", grank_, "): ", failed_);
+  for (auto& op : colls_) {
+    op->done = true;
+    op->ok = false;
+    op->err = failed_;
   }
-  return true;
+  colls_.clear();
+  for (auto& q : outbox_) q.clear();
+  cv_.notify_all();
 }
 
-// ----------------------------------------------------------- allgather ----
-bool Group::allgather(const Packet& mine, std::vector<Packet>* all, std::string* err, MemoryPtr* stacked) {
+void Group::drop_member(int m, bool orderly) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!active_[static_cast<size_t>(m)]) return;
+  active_[static_cast<size_t>(m)] = 0;
+  const std::string why = strfmt("member ", m, " (rank ", global_rank(m), ") left the group",
+                                 orderly ? "" : " without a goodbye");
+  if (orderly)
+    NNSX_LOGD("comm", "group ", spec_.name, ": ", why);
+  else
+    NNSX_LOGW("comm", "group ", spec_.name, ": ", why, " (p2p with the other members continues)");
+  if (coll_dead_.empty()) coll_dead_ = why;
+  for (auto& op : colls_) {
+    op->done = true;
+    op->ok = false;
+    op->err = coll_dead_;
+  }
+  colls_.clear();
+  if (!outbox_[static_cast<size_t>(m)].empty())
+    NNSX_LOGW("comm", "group ", spec_.name, ": dropping ", outbox_[static_cast<size_t>(m)].size(),
+              " queued message(s) to member ", m);
+  outbox_[static_cast<size_t>(m)].clear();
+  cv_.notify_all();
+}
+
+bool Group::run_round(std::string* err) {
   const int n = size();
-  const uint64_t seq = seq_++;
-  all->assign(static_cast<size_t>(n), Packet());
-  (*all)[grank_] = mine;
-  (*all)[grank_].src = grank_;
-  if (stacked) *stacked = nullptr;
-  // a group of one: nothing to exchange -- unless RCCL was forced, then the
-  // real ncclAllGather runs (one rank: a copy into the gathered buffer)
-  if (n == 1 && !rccl()) {
-    if (stacked && mine.blobs.size() == 1) *stacked = mine.blobs[0];
-    return true;
-  }
-  const uint64_t tag = 1 + seq;
-  for (int r = 0; r < n; ++r)
-    if (r != grank_ && !mesh_->send(r, tag, to_message(mine), err)) return false;
-  std::vector<std::vector<size_t>> sizes(n);
-  std::vector<std::vector<std::string>> metas(n);
-  for (int r = 0; r < n; ++r) {
-    if (r == grank_) {
-      for (auto& b : mine.blobs) {
-        sizes[r].push_back(b->size());
-        metas[r].push_back(std::string());
+  const uint64_t r = round_;
+  work_ = false;  // work arriving from now on triggers the next round
+  std::vector<std::shared_ptr<CollOp>> colls;
+  std::vector<std::vector<Packet>> sends(static_cast<size_t>(n));
+  std::vector<uint32_t> grant(static_cast<size_t>(n), 0);
+  std::vector<char> act;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    act = active_;
+    if (coll_dead_.empty()) colls.assign(colls_.begin(), colls_.end());
+    for (int d = 0; d < n; ++d) {
+      auto& q = outbox_[static_cast<size_t>(d)];
+      while (!q.empty() && static_cast<int>(sends[static_cast<size_t>(d)].size()) < allowed_[static_cast<size_t>(d)]) {
+        sends[static_cast<size_t>(d)].push_back(std::move(q.front()));
+        q.pop_front();
       }
-      continue;
-    }
-    if (!recv_from(tag, r, &(*all)[r], &sizes[r], &metas[r], err, "allgather")) return false;
-  }
-  bool one_uniform = true;
-  for (int r = 0; r < n; ++r)
-    one_uniform = one_uniform && sizes[r].size() == 1 && sizes[r][0] == sizes[0][0] && sizes[0][0] > 0;
-  if (!rccl()) {
-    if (stacked && one_uniform) {
-      const size_t s = sizes[0][0];
-      auto out = Memory::alloc_pinned(s * n);
-      for (int r = 0; r < n; ++r)
-        std::memcpy(static_cast<char*>(out->data()) + static_cast<size_t>(r) * s, (*all)[r].blobs[0]->map_host(), s);
-      *stacked = out;
-    }
-    return true;
-  }
-  // ---- RCCL payload ----
-  hip::DeviceGuard dg(device_);
-  size_t nb = 0;
-  for (auto& s : sizes) nb = std::max(nb, s.size());
-  std::vector<MemoryPtr> outs;
-  for (int r = 0; r < n; ++r)
-    if (r != grank_) (*all)[r].blobs.assign(sizes[r].size(), nullptr);
-  std::vector<void*> srcs(mine.blobs.size());
-  for (size_t j = 0; j < mine.blobs.size(); ++j) srcs[j] = mine.blobs[j]->size() ? dev_ptr(mine.blobs[j]) : nullptr;
-  auto comm = static_cast<ncclComm_t>(comm_);
-  if (!nccl_ok(ncclGroupStart(), "ncclGroupStart", err)) return false;
-  for (size_t j = 0; j < nb; ++j) {
-    bool uniform = true;
-    for (int r = 0; r < n; ++r) uniform = uniform && j < sizes[r].size() && sizes[r][j] == sizes[0][j];
-    if (uniform && sizes[0][j] > 0) {
-      const size_t s = sizes[0][j];
-      auto out = Memory::alloc_device(s * n, device_, stream_);
-      outs.push_back(out);
-      if (stacked && one_uniform) *stacked = out;
-      if (!nccl_ok(ncclAllGather(srcs[j], out->data(), s, ncclUint8, comm, stream_), "ncclAllGather", err)) {
-        ncclGroupEnd();
-        return false;
+      if (d != grank_) {
+        grant[static_cast<size_t>(d)] = static_cast<uint32_t>(std::max(0, kWindow - unconsumed_[static_cast<size_t>(d)]));
+        granted_[static_cast<size_t>(d)] = static_cast<int>(grant[static_cast<size_t>(d)]);
       }
-      if (n == 1) (*all)[grank_].blobs[j] = out;  // (forced RCCL: the gathered copy)
-      for (int r = 0; r < n; ++r) {
-        if (r == grank_) continue;
-        auto v = Memory::view(out, static_cast<size_t>(r) * s, s);
-        if (!metas[r][j].empty()) {
-          MetaInfo mi;
-          if (MetaInfo::parse(metas[r][j].data(), metas[r][j].size(), &mi)) v->set_meta(mi);
-        }
-        (*all)[r].blobs[j] = v;
-        bytes_recv_ += s;
-      }
-      bytes_sent_ += s;
-      continue;
     }
-    // ragged: one broadcast per owner of blob j
-    for (int r = 0; r < n; ++r) {
-      if (j >= sizes[r].size() || sizes[r][j] == 0) {
-        if (r != grank_ && j < sizes[r].size()) (*all)[r].blobs[j] = Memory::alloc_host(0);
+  }
+  cv_.notify_all();  // room in the outboxes
+  // ---- manifests out, then in ----
+  std::vector<Manifest> man(static_cast<size_t>(n));
+  for (int d = 0; d < n; ++d) {
+    if (d == grank_ || !act[static_cast<size_t>(d)]) continue;
+    std::string e;
+    if (!mesh_->send(d, r + 1, manifest_for(d, grant[static_cast<size_t>(d)], colls, sends[static_cast<size_t>(d)]), &e)) {
+      drop_member(d, false);
+      act[static_cast<size_t>(d)] = 0;
+    }
+  }
+  const int64_t deadline = now_ns() + static_cast<int64_t>(spec_.timeout_ms) * 1000000;
+  for (int d = 0; d < n; ++d) {
+    if (d == grank_ || !act[static_cast<size_t>(d)]) continue;
+    Message m;
+    bool to = false;
+    int gone = 0;
+    std::string e;
+    const int left_ms = static_cast<int>(std::max<int64_t>(0, (deadline - now_ns()) / 1000000));
+    if (!mesh_->recv(r + 1, d, &m, left_ms, &to, &gone, &e)) {
+      if (gone) {
+        drop_member(d, gone == 3);
+        act[static_cast<size_t>(d)] = 0;
         continue;
       }
-      const size_t s = sizes[r][j];
-      if (r == grank_) {
-        if (!nccl_ok(ncclBroadcast(srcs[j], srcs[j], s, ncclUint8, r, comm, stream_), "ncclBroadcast", err)) {
+      *err = to ? strfmt("round ", r, ": member ", d, " (rank ", global_rank(d), ") sent no manifest within ",
+                         spec_.timeout_ms, " ms")
+                : strfmt("round ", r, ": ", e);
+      return false;
+    }
+    if (!parse_manifest(std::move(m), &man[static_cast<size_t>(d)])) {
+      *err = strfmt("round ", r, ": malformed manifest from member ", d);
+      return false;
+    }
+  }
+  for (int d = 0; d < n; ++d)
+    if (!act[static_cast<size_t>(d)]) sends[static_cast<size_t>(d)].clear();  // (dropped with the member)
+  // ---- the collectives every member listed (a common prefix of the sequence) ----
+  bool everyone = true;
+  for (int d = 0; d < n; ++d) everyone = everyone && act[static_cast<size_t>(d)];
+  std::vector<std::shared_ptr<CollOp>> run;
+  std::vector<std::vector<const ManifestColl*>> ents;
+  std::string mismatch;
+  std::vector<size_t> pos(static_cast<size_t>(n), 0);
+  for (auto& op : colls) {
+    if (!everyone) break;
+    std::vector<const ManifestColl*> ent(static_cast<size_t>(n), nullptr);
+    bool listed = true;
+    for (int d = 0; d < n && listed; ++d) {
+      if (d == grank_) continue;
+      const auto& cs = man[static_cast<size_t>(d)].colls;
+      size_t& k = pos[static_cast<size_t>(d)];
+      while (k < cs.size() && cs[k].seq < op->seq) ++k;
+      if (k >= cs.size() || cs[k].seq != op->seq) {
+        listed = false;
+        break;
+      }
+      if (cs[k].kind != op->kind || cs[k].root != op->root) {
+        mismatch = strfmt("collective ", op->seq, ": member ", d, " called ", CollOp::name(cs[k].kind), "(root ",
+                          cs[k].root, ") where member ", grank_, " called ", CollOp::name(op->kind), "(root ", op->root,
+                          ")");
+        listed = false;
+        break;
+      }
+      ent[static_cast<size_t>(d)] = &cs[k];
+    }
+    if (!listed) break;
+    run.push_back(op);
+    ents.push_back(std::move(ent));
+  }
+  // ---- data plane: the collectives in sequence order, then the p2p group ----
+  std::string what;
+  std::vector<Packet> got;
+  if (rccl()) hip::check(hipSetDevice(device_), "hipSetDevice");
+  for (size_t i = 0; i < run.size(); ++i)
+    if (!issue_collective(*run[i], ents[i], &what, err)) return false;
+  if (!issue_p2p(sends, man, &got, &what, err)) return false;
+  if (rccl() && !what.empty()) {
+    Inflight f;
+    f.ev = hip::event_get(device_);
+    hip::check(hipEventRecord(f.ev, stream_), "hipEventRecord(round)");
+    f.t0 = now_ns();
+    f.round = r;
+    f.what = what;
+    inflight_.push_back(std::move(f));
+  }
+  // ---- publish ----
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (auto& op : run) {
+      op->done = true;
+      op->ok = op->err.empty();
+      colls_.erase(std::remove(colls_.begin(), colls_.end(), op), colls_.end());
+    }
+    if (!mismatch.empty() && coll_dead_.empty()) {
+      coll_dead_ = mismatch;
+      for (auto& op : colls_) {
+        op->done = true;
+        op->ok = false;
+        op->err = mismatch;
+      }
+      colls_.clear();
+    }
+    for (auto& p : got) {
+      if (p.src != grank_) ++unconsumed_[static_cast<size_t>(p.src)];
+      inbox_.push_back(std::move(p));
+    }
+    for (int d = 0; d < n; ++d) {
+      if (d == grank_) {
+        allowed_[static_cast<size_t>(d)] = kWindow;  // (forced RCCL group of one: the round receives its own)
+      } else if (act[static_cast<size_t>(d)]) {
+        const auto& mm = man[static_cast<size_t>(d)];
+        allowed_[static_cast<size_t>(d)] =
+            std::max(0, static_cast<int>(mm.grant) - static_cast<int>(sends[static_cast<size_t>(d)].size()));
+        listed_upto_[static_cast<size_t>(d)] = mm.colls.empty() ? 0 : mm.colls.back().seq + 1;
+      }
+      if (!outbox_[static_cast<size_t>(d)].empty() && allowed_[static_cast<size_t>(d)] > 0) work_ = true;
+    }
+  }
+  cv_.notify_all();
+  ++round_;
+  return true;
+}
+
+// One collective of the round.  ent[m]: member m's manifest entry for it
+// (nullptr for this member).  RCCL: one ncclGroupStart/End on the comm
+// stream; tcp: the payloads came inline with the manifests.
+bool Group::issue_collective(CollOp& op, const std::vector<const ManifestColl*>& ent, std::string* what,
+                             std::string* err) {
+  const int n = size();
+  what->append(strfmt(what->empty() ? "" : ", ", CollOp::name(op.kind), "#", op.seq));
+  auto comm = static_cast<ncclComm_t>(comm_);
+  auto header_of = [&](int m) -> const ManifestEntry* {
+    const ManifestColl* c = ent[static_cast<size_t>(m)];
+    return c && c->has_hdr ? &c->e : nullptr;
+  };
+  if (op.kind == CollOp::kAllGather) {
+    op.all.assign(static_cast<size_t>(n), Packet());
+    std::vector<std::vector<size_t>> sizes(static_cast<size_t>(n));
+    for (int m = 0; m < n; ++m) {
+      if (m == grank_) {
+        op.all[static_cast<size_t>(m)] = op.mine;
+        for (auto& b : op.mine.blobs) sizes[static_cast<size_t>(m)].push_back(b->size());
+        continue;
+      }
+      const ManifestEntry* h = header_of(m);
+      if (!h) {
+        op.err = strfmt("allgather: no packet from member ", m);
+        return true;
+      }
+      op.all[static_cast<size_t>(m)] = h->hdr;
+      op.all[static_cast<size_t>(m)].src = m;
+      sizes[static_cast<size_t>(m)] = h->sizes;
+    }
+    bool one_uniform = true;
+    for (int m = 0; m < n; ++m)
+      one_uniform = one_uniform && sizes[static_cast<size_t>(m)].size() == 1 &&
+                    sizes[static_cast<size_t>(m)][0] == sizes[0][0] && sizes[0][0] > 0;
+    if (!rccl()) {
+      for (int m = 0; m < n; ++m)
+        if (m != grank_)
+          for (auto& b : op.all[static_cast<size_t>(m)].blobs) bytes_recv_ += b->size();
+      if (op.want_stacked && one_uniform) {
+        const size_t s = sizes[0][0];
+        auto out = Memory::alloc_pinned(s * static_cast<size_t>(n));
+        for (int m = 0; m < n; ++m)
+          std::memcpy(static_cast<char*>(out->data()) + static_cast<size_t>(m) * s,
+                      op.all[static_cast<size_t>(m)].blobs[0]->map_host(), s);
+        op.stacked = out;
+      }
+      for (auto& b : op.mine.blobs) bytes_sent_ += b->size() * static_cast<size_t>(n - 1);
+      return true;
+    }
+    size_t nb = 0;
+    for (auto& s : sizes) nb = std::max(nb, s.size());
+    std::vector<MemoryPtr> outs;
+    for (int m = 0; m < n; ++m)
+      if (m != grank_) op.all[static_cast<size_t>(m)].blobs.assign(sizes[static_cast<size_t>(m)].size(), nullptr);
+    std::vector<void*> srcs(op.mine.blobs.size());
+    for (size_t j = 0; j < op.mine.blobs.size(); ++j)
+      srcs[j] = op.mine.blobs[j]->size() ? dev_ptr(op.mine.blobs[j]) : nullptr;
+    if (!nccl_ok(ncclGroupStart(), "ncclGroupStart", err)) return false;
+    for (size_t j = 0; j < nb; ++j) {
+      bool uniform = true;
+      for (int m = 0; m < n; ++m)
+        uniform = uniform && j < sizes[static_cast<size_t>(m)].size() && sizes[static_cast<size_t>(m)][j] == sizes[0][j];
+      if (uniform && sizes[0][j] > 0) {
+        const size_t s = sizes[0][j];
+        auto out = Memory::alloc_device(s * static_cast<size_t>(n), device_, stream_);
+        outs.push_back(out);
+        if (op.want_stacked && one_uniform) op.stacked = out;
+        if (!nccl_ok(ncclAllGather(srcs[j], out->data(), s, ncclUint8, comm, stream_), "ncclAllGather", err)) {
           ncclGroupEnd();
           return false;
+        }
+        if (n == 1) op.all[static_cast<size_t>(grank_)].blobs[j] = out;  // (forced RCCL: the gathered copy)
+        for (int m = 0; m < n; ++m) {
+          if (m == grank_) continue;
+          auto v = Memory::view(out, static_cast<size_t>(m) * s, s);
+          const std::string& meta = header_of(m)->metas[j];
+          if (!meta.empty()) {
+            MetaInfo mi;
+            if (MetaInfo::parse(meta.data(), meta.size(), &mi)) v->set_meta(mi);
+          }
+          op.all[static_cast<size_t>(m)].blobs[j] = v;
+          bytes_recv_ += s;
         }
         bytes_sent_ += s;
         continue;
       }
-      auto out = alloc_recv({s}, {metas[r][j]})[0];
-      outs.push_back(out);
-      (*all)[r].blobs[j] = out;
-      if (!nccl_ok(ncclBroadcast(out->data(), out->data(), s, ncclUint8, r, comm, stream_), "ncclBroadcast", err)) {
+      // ragged: one broadcast per owner of blob j
+      for (int m = 0; m < n; ++m) {
+        const auto& sm = sizes[static_cast<size_t>(m)];
+        if (j >= sm.size() || sm[j] == 0) {
+          if (m != grank_ && j < sm.size()) op.all[static_cast<size_t>(m)].blobs[j] = Memory::alloc_host(0);
+          continue;
+        }
+        const size_t s = sm[j];
+        if (m == grank_) {
+          if (!nccl_ok(ncclBroadcast(srcs[j], srcs[j], s, ncclUint8, m, comm, stream_), "ncclBroadcast", err)) {
+            ncclGroupEnd();
+            return false;
+          }
+          bytes_sent_ += s;
+          continue;
+        }
+        auto out = alloc_recv({s}, {header_of(m)->metas[j]})[0];
+        outs.push_back(out);
+        op.all[static_cast<size_t>(m)].blobs[j] = out;
+        if (!nccl_ok(ncclBroadcast(out->data(), out->data(), s, ncclUint8, m, comm, stream_), "ncclBroadcast", err)) {
+          ncclGroupEnd();
+          return false;
+        }
+      }
+    }
+    if (!nccl_ok(ncclGroupEnd(), "ncclGroupEnd", err)) return false;
+    for (auto& o : outs) o->mark_ready(stream_);
+    finish_inputs(op.mine.blobs);
+    return true;
+  }
+  if (op.kind == CollOp::kBroadcast) {
+    const int root = op.root;
+    if (root == grank_) {
+      op.out = op.mine;
+    } else {
+      const ManifestEntry* h = header_of(root);
+      if (!h) {
+        op.err = "broadcast: no packet from the root";
+        return true;
+      }
+      op.out = h->hdr;
+      op.out.src = root;
+      if (!rccl()) {
+        for (auto& b : op.out.blobs) bytes_recv_ += b->size();
+        return true;
+      }
+      op.out.blobs = alloc_recv(h->sizes, h->metas);
+    }
+    if (!rccl()) {
+      for (auto& b : op.out.blobs) bytes_sent_ += b->size() * static_cast<size_t>(n - 1);
+      return true;
+    }
+    std::vector<void*> ptrs;
+    for (auto& b : op.out.blobs) ptrs.push_back(!b->size() ? nullptr : root == grank_ ? dev_ptr(b) : b->data());
+    if (!nccl_ok(ncclGroupStart(), "ncclGroupStart", err)) return false;
+    for (size_t j = 0; j < op.out.blobs.size(); ++j) {
+      const size_t s = op.out.blobs[j]->size();
+      if (!s) continue;
+      if (!nccl_ok(ncclBroadcast(ptrs[j], ptrs[j], s, ncclUint8, root, comm, stream_), "ncclBroadcast", err)) {
         ncclGroupEnd();
         return false;
       }
+      if (root == grank_) bytes_sent_ += s;
     }
-  }
-  if (!nccl_ok(ncclGroupEnd(), "ncclGroupEnd", err)) return false;
-  for (auto& o : outs) o->mark_ready(stream_);
-  finish_inputs(mine.blobs);
-  return true;
-}
-
-// ----------------------------------------------------------- broadcast ----
-bool Group::broadcast(int root, Packet* pkt, std::string* err) {
-  const int n = size();
-  const uint64_t seq = seq_++;
-  if (n == 1 && !rccl()) return true;  // (forced RCCL: the one-rank ncclBroadcast runs)
-  const uint64_t tag = 1 + seq;
-  std::vector<size_t> sizes;
-  std::vector<std::string> metas;
-  if (grank_ == root) {
-    for (int r = 0; r < n; ++r)
-      if (r != root && !mesh_->send(r, tag, to_message(*pkt), err)) return false;
-    for (auto& b : pkt->blobs) sizes.push_back(b->size());
-  } else if (!recv_from(tag, root, pkt, &sizes, &metas, err, "broadcast")) {
-    return false;
-  }
-  if (!rccl()) return true;
-  hip::DeviceGuard dg(device_);
-  auto comm = static_cast<ncclComm_t>(comm_);
-  std::vector<MemoryPtr> outs;
-  std::vector<void*> ptrs;
-  if (grank_ == root) {
-    for (auto& b : pkt->blobs) ptrs.push_back(b->size() ? dev_ptr(b) : nullptr);
-  } else {
-    pkt->blobs = alloc_recv(sizes, metas);
-    for (auto& b : pkt->blobs) ptrs.push_back(b->size() ? b->data() : nullptr);
-    outs = pkt->blobs;
-  }
-  if (!nccl_ok(ncclGroupStart(), "ncclGroupStart", err)) return false;
-  for (size_t j = 0; j < sizes.size(); ++j) {
-    if (!sizes[j]) continue;
-    if (!nccl_ok(ncclBroadcast(ptrs[j], ptrs[j], sizes[j], ncclUint8, root, comm, stream_), "ncclBroadcast", err)) {
-      ncclGroupEnd();
-      return false;
+    if (!nccl_ok(ncclGroupEnd(), "ncclGroupEnd", err)) return false;
+    if (root == grank_) {
+      finish_inputs(op.out.blobs);
+    } else {
+      for (auto& b : op.out.blobs)
+        if (b->size()) b->mark_ready(stream_);
     }
-    if (grank_ == root) bytes_sent_ += sizes[j];
+    return true;
   }
-  if (!nccl_ok(ncclGroupEnd(), "ncclGroupEnd", err)) return false;
-  for (auto& o : outs)
-    if (o->size()) o->mark_ready(stream_);
-  if (grank_ == root) finish_inputs(pkt->blobs);
-  return true;
-}
-
-// ------------------------------------------------------------- scatter ----
-bool Group::scatter(int root, const std::vector<Packet>* parts, Packet* mine, std::string* err) {
-  const int n = size();
-  const uint64_t seq = seq_++;
-  const uint64_t tag = 1 + seq;
-  if (grank_ == root) {
-    if (!parts || static_cast<int>(parts->size()) != n) {
-      if (err) *err = "scatter: the root needs one part per member";
-      return false;
+  // scatter
+  const int root = op.root;
+  if (root == grank_) {
+    op.out = op.parts.at(static_cast<size_t>(root));
+    op.out.src = root;
+    if (!rccl()) {
+      for (int m = 0; m < n; ++m)
+        if (m != root)
+          for (auto& b : op.parts[static_cast<size_t>(m)].blobs) bytes_sent_ += b->size();
+      return true;
     }
-    *mine = (*parts)[root];
-    mine->src = root;
-    for (int r = 0; r < n; ++r)
-      if (r != root && !mesh_->send(r, tag, to_message((*parts)[r]), err)) return false;
-    if (!rccl() || n == 1) return true;
-    hip::DeviceGuard dg(device_);
-    auto comm = static_cast<ncclComm_t>(comm_);
+    if (n == 1) return true;
     if (!nccl_ok(ncclGroupStart(), "ncclGroupStart", err)) return false;
-    for (int r = 0; r < n; ++r) {
-      if (r == root) continue;
-      for (auto& b : (*parts)[r].blobs) {
+    for (int m = 0; m < n; ++m) {
+      if (m == root) continue;
+      for (auto& b : op.parts[static_cast<size_t>(m)].blobs) {
         if (!b->size()) continue;
-        if (!nccl_ok(ncclSend(dev_ptr(b), b->size(), ncclUint8, r, comm, stream_), "ncclSend", err)) {
+        if (!nccl_ok(ncclSend(dev_ptr(b), b->size(), ncclUint8, m, comm, stream_), "ncclSend", err)) {
           ncclGroupEnd();
           return false;
         }
@@ -1002,141 +1245,309 @@ bool Group::scatter(int root, const std::vector<Packet>* parts, Packet* mine, st
       }
     }
     if (!nccl_ok(ncclGroupEnd(), "ncclGroupEnd", err)) return false;
-    for (int r = 0; r < n; ++r)
-      if (r != root) finish_inputs((*parts)[r].blobs);
+    for (int m = 0; m < n; ++m)
+      if (m != root) finish_inputs(op.parts[static_cast<size_t>(m)].blobs);
     return true;
   }
-  std::vector<size_t> sizes;
-  std::vector<std::string> metas;
-  if (!recv_from(tag, root, mine, &sizes, &metas, err, "scatter")) return false;
-  if (!rccl()) return true;
-  hip::DeviceGuard dg(device_);
-  mine->blobs = alloc_recv(sizes, metas);
-  auto comm = static_cast<ncclComm_t>(comm_);
+  const ManifestEntry* h = header_of(root);
+  if (!h) {
+    op.err = "scatter: no part from the root";
+    return true;
+  }
+  op.out = h->hdr;
+  op.out.src = root;
+  if (!rccl()) {
+    for (auto& b : op.out.blobs) bytes_recv_ += b->size();
+    return true;
+  }
+  op.out.blobs = alloc_recv(h->sizes, h->metas);
   if (!nccl_ok(ncclGroupStart(), "ncclGroupStart", err)) return false;
-  for (auto& b : mine->blobs)
+  for (auto& b : op.out.blobs)
     if (b->size() && !nccl_ok(ncclRecv(b->data(), b->size(), ncclUint8, root, comm, stream_), "ncclRecv", err)) {
       ncclGroupEnd();
       return false;
     }
   if (!nccl_ok(ncclGroupEnd(), "ncclGroupEnd", err)) return false;
-  for (auto& b : mine->blobs)
+  for (auto& b : op.out.blobs)
     if (b->size()) b->mark_ready(stream_);
   return true;
 }
 
-// -------------------------------------------------------- point to point ----
-// header (and tcp payload) on the direct link to the peer; a member's message
-// to itself goes straight into its own inbox with the blobs as they are
+// Every p2p message of the round, in ONE ncclGroupStart/End: this member's
+// sends (peer order, FIFO per peer) and the receives of every message the
+// other members listed for it (sender order, FIFO per sender).
+bool Group::issue_p2p(std::vector<std::vector<Packet>>& sends, const std::vector<Manifest>& man,
+                      std::vector<Packet>* got, std::string* what, std::string* err) {
+  const int n = size();
+  size_t nsend = 0, nrecv = 0;
+  for (auto& s : sends) nsend += s.size();
+  for (int m = 0; m < n; ++m)
+    if (m != grank_) nrecv += man[static_cast<size_t>(m)].sends.size();
+  if (nsend + nrecv == 0) return true;
+  if (!rccl()) {
+    for (auto& s : sends)
+      for (auto& p : s)
+        for (auto& b : p.blobs) bytes_sent_ += b->size();
+    for (int m = 0; m < n; ++m) {
+      if (m == grank_) continue;
+      for (auto& e : man[static_cast<size_t>(m)].sends) {
+        Packet p = e.hdr;
+        p.src = m;
+        for (auto& b : p.blobs) bytes_recv_ += b->size();
+        got->push_back(std::move(p));
+      }
+    }
+    return true;
+  }
+  std::string peers;
+  for (int m = 0; m < n; ++m) {
+    const size_t k = sends[static_cast<size_t>(m)].size() + (m == grank_ ? 0 : man[static_cast<size_t>(m)].sends.size());
+    if (k) peers += strfmt(peers.empty() ? "" : ",", m, "(rank ", global_rank(m), ")");
+  }
+  what->append(strfmt(what->empty() ? "" : ", ", "p2p ", nsend, " out / ", nrecv, " in with members ", peers));
+  auto comm = static_cast<ncclComm_t>(comm_);
+  std::vector<std::vector<void*>> src(static_cast<size_t>(n));
+  for (int d = 0; d < n; ++d)
+    for (auto& p : sends[static_cast<size_t>(d)])
+      for (auto& b : p.blobs) src[static_cast<size_t>(d)].push_back(b->size() ? dev_ptr(b) : nullptr);
+  // receive buffers: a group of one (forced RCCL) receives its own messages
+  for (int m = 0; m < n; ++m) {
+    if (m == grank_) {
+      for (auto& p : sends[static_cast<size_t>(m)]) {
+        Packet q = p;
+        q.src = m;
+        q.blobs.clear();
+        for (auto& b : p.blobs) {
+          auto o = b->size() ? Memory::alloc_device(b->size(), device_, stream_) : Memory::alloc_host(0);
+          if (b->has_meta()) o->set_meta(b->meta());
+          bytes_recv_ += b->size();
+          q.blobs.push_back(o);
+        }
+        got->push_back(std::move(q));
+      }
+      continue;
+    }
+    for (auto& e : man[static_cast<size_t>(m)].sends) {
+      Packet q = e.hdr;
+      q.src = m;
+      q.blobs = alloc_recv(e.sizes, e.metas);
+      got->push_back(std::move(q));
+    }
+  }
+  if (!nccl_ok(ncclGroupStart(), "ncclGroupStart", err)) return false;
+  for (int d = 0; d < n; ++d) {
+    size_t k = 0;
+    for (auto& p : sends[static_cast<size_t>(d)])
+      for (auto& b : p.blobs) {
+        void* ptr = src[static_cast<size_t>(d)][k++];
+        if (!b->size()) continue;
+        if (!nccl_ok(ncclSend(ptr, b->size(), ncclUint8, d, comm, stream_), "ncclSend", err)) {
+          ncclGroupEnd();
+          return false;
+        }
+        bytes_sent_ += b->size();
+      }
+  }
+  for (auto& q : *got)
+    for (auto& b : q.blobs)
+      if (b->size() && !nccl_ok(ncclRecv(b->data(), b->size(), ncclUint8, q.src, comm, stream_), "ncclRecv", err)) {
+        ncclGroupEnd();
+        return false;
+      }
+  if (!nccl_ok(ncclGroupEnd(), "ncclGroupEnd", err)) return false;
+  for (auto& q : *got)
+    for (auto& b : q.blobs)
+      if (b->size()) b->mark_ready(stream_);
+  for (auto& s : sends)
+    for (auto& p : s) finish_inputs(p.blobs);
+  return true;
+}
+
+// ------------------------------------------------------------ callers ----
+bool Group::collective(const std::shared_ptr<CollOp>& op, std::string* err) {
+  std::unique_lock<std::mutex> lk(mu_);
+  auto bail = [&](const std::string& why) {
+    colls_.erase(std::remove(colls_.begin(), colls_.end(), op), colls_.end());
+    if (err) *err = why;
+    return false;
+  };
+  if (!failed_.empty()) return bail(failed_);
+  if (!coll_dead_.empty()) return bail(coll_dead_);
+  if (cancelled_.load()) return bail("cancelled");
+  op->seq = coll_seq_++;
+  colls_.push_back(op);
+  work_ = true;
+  lk.unlock();
+  poke();
+  lk.lock();
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(spec_.timeout_ms);
+  while (!op->done) {
+    if (!failed_.empty()) return bail(failed_);
+    if (!coll_dead_.empty()) return bail(coll_dead_);
+    if (cancelled_.load()) return bail("cancelled");
+    if (cv_.wait_until(lk, deadline) == std::cv_status::timeout && !op->done) {
+      std::string who;
+      for (int m = 0; m < size(); ++m)
+        if (m != grank_ && active_[static_cast<size_t>(m)] && listed_upto_[static_cast<size_t>(m)] <= op->seq)
+          who += strfmt(who.empty() ? "" : ",", m);
+      coll_dead_ = strfmt(CollOp::name(op->kind), " (collective ", op->seq, "): member(s) ",
+                          who.empty() ? std::string("?") : who, " did not enter it within ", spec_.timeout_ms, " ms");
+      for (auto& o : colls_)
+        if (o != op) {
+          o->done = true;
+          o->ok = false;
+          o->err = coll_dead_;
+        }
+      colls_.clear();
+      cv_.notify_all();
+      if (err) *err = coll_dead_;
+      return false;
+    }
+  }
+  if (!op->ok) {
+    if (err) *err = op->err;
+    return false;
+  }
+  return true;
+}
+
+bool Group::allgather(const Packet& mine, std::vector<Packet>* all, std::string* err, MemoryPtr* stacked) {
+  if (stacked) *stacked = nullptr;
+  if (!engine_) {  // a group of one: nothing to exchange
+    all->assign(1, mine);
+    (*all)[0].src = grank_;
+    if (stacked && mine.blobs.size() == 1) *stacked = mine.blobs[0];
+    return true;
+  }
+  auto op = std::make_shared<CollOp>();
+  op->kind = CollOp::kAllGather;
+  op->mine = mine;
+  op->mine.src = grank_;
+  op->want_stacked = stacked != nullptr;
+  if (!collective(op, err)) return false;
+  *all = std::move(op->all);
+  if (stacked) *stacked = op->stacked;
+  return true;
+}
+
+bool Group::broadcast(int root, Packet* pkt, std::string* err) {
+  if (root < 0 || root >= size()) {
+    if (err) *err = strfmt("broadcast: no member ", root);
+    return false;
+  }
+  if (!engine_) return true;  // (forced RCCL: the one-rank ncclBroadcast runs)
+  auto op = std::make_shared<CollOp>();
+  op->kind = CollOp::kBroadcast;
+  op->root = root;
+  if (root == grank_) op->mine = *pkt;
+  if (!collective(op, err)) return false;
+  *pkt = std::move(op->out);
+  return true;
+}
+
+bool Group::scatter(int root, const std::vector<Packet>* parts, Packet* mine, std::string* err) {
+  const int n = size();
+  if (root < 0 || root >= n) {
+    if (err) *err = strfmt("scatter: no member ", root);
+    return false;
+  }
+  if (grank_ == root && (!parts || static_cast<int>(parts->size()) != n)) {
+    if (err) *err = "scatter: the root needs one part per member";
+    return false;
+  }
+  if (!engine_) {
+    *mine = (*parts)[static_cast<size_t>(root)];
+    mine->src = root;
+    return true;
+  }
+  auto op = std::make_shared<CollOp>();
+  op->kind = CollOp::kScatter;
+  op->root = root;
+  if (grank_ == root) op->parts = *parts;
+  if (!collective(op, err)) return false;
+  *mine = std::move(op->out);
+  return true;
+}
+
 bool Group::send(int peer, const Packet& p, std::string* err) {
   if (peer < 0 || peer >= size()) {
     if (err) *err = strfmt("send: no member ", peer);
     return false;
   }
-  if (peer == grank_) {
-    Message m;
-    m.caps = encode(p, false);
-    m.blobs = p.blobs;
-    m.flags = 1;  // in-process: blobs handed over as they are
-    // a group of one on forced RCCL: the payload goes through RCCL's p2p path
-    // (grouped ncclSend / ncclRecv to itself) like a peer's would
-    if (size() == 1 && rccl() && !self_copy(p.blobs, &m.blobs, err)) return false;
-    if (!mesh_) {
-      std::lock_guard<std::mutex> lk(local_mu_);
-      local_.push_back(std::move(m));
-      local_cv_.notify_all();
-    } else {
-      mesh_->deliver_local(kTagP2P, std::move(m));
-    }
+  std::unique_lock<std::mutex> lk(mu_);
+  if (!failed_.empty()) {
+    if (err) *err = failed_;
+    return false;
+  }
+  if (cancelled_.load()) {
+    if (err) *err = "send: cancelled";
+    return false;
+  }
+  Packet q = p;
+  q.src = grank_;
+  // to oneself: handed over in-process, blobs as they are -- except in a group
+  // of one on forced RCCL, whose round runs the grouped ncclSend / ncclRecv to
+  // itself (the data plane's p2p kernels, on one GPU)
+  if (peer == grank_ && !(engine_ && size() == 1)) {
+    inbox_.push_back(std::move(q));
+    cv_.notify_all();
     return true;
   }
-  if (!mesh_->send(peer, kTagP2P, to_message(p), err)) return false;
-  if (!rccl()) return true;
-  hip::DeviceGuard dg(device_);
-  Link* l = nullptr;
-  if (!link(peer, true, &l, err)) return false;
-  auto comm = static_cast<ncclComm_t>(l->comm);
-  std::vector<void*> src;
-  for (auto& b : p.blobs) src.push_back(b->size() ? dev_ptr_on(b, l->stream) : nullptr);
-  if (!nccl_ok(ncclGroupStart(), "ncclGroupStart", err)) return false;
-  for (size_t i = 0; i < p.blobs.size(); ++i) {
-    const size_t sz = p.blobs[i]->size();
-    if (!sz) continue;
-    if (!nccl_ok(ncclSend(src[i], sz, ncclUint8, 1, comm, l->stream), "ncclSend", err)) {
-      ncclGroupEnd();
-      return false;
-    }
-    bytes_sent_ += sz;
+  auto& box = outbox_[static_cast<size_t>(peer)];
+  while (box.size() >= static_cast<size_t>(kOutbox)) {  // backpressure: the peer has not taken its window
+    if (!failed_.empty() || cancelled_.load() || !active_[static_cast<size_t>(peer)]) break;
+    cv_.wait_for(lk, std::chrono::milliseconds(100));
   }
-  if (!nccl_ok(ncclGroupEnd(), "ncclGroupEnd", err)) return false;
-  finish_inputs(p.blobs, l->stream);
+  if (!failed_.empty() || cancelled_.load()) {
+    if (err) *err = !failed_.empty() ? failed_ : std::string("send: cancelled");
+    return false;
+  }
+  if (!active_[static_cast<size_t>(peer)]) {
+    if (err) *err = strfmt("send: member ", peer, " (rank ", global_rank(peer), ") left the group");
+    return false;
+  }
+  box.push_back(std::move(q));
+  work_ = true;
+  lk.unlock();
+  poke();
   return true;
 }
 
 bool Group::recv(Packet* p, int timeout_ms, bool* timed_out, std::string* err) {
   if (timed_out) *timed_out = false;
-  Message m;
-  if (!mesh_) {  // a group of one: only its own messages
-    std::unique_lock<std::mutex> lk(local_mu_);
-    auto ready = [&] { return !local_.empty() || cancelled_.load(); };
-    if (timeout_ms < 0) {
-      local_cv_.wait(lk, ready);
-    } else {
-      local_cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), ready);
-    }
-    if (local_.empty()) {
-      if (timed_out) *timed_out = !cancelled_.load();
-      if (err && cancelled_.load()) *err = "recv: cancelled";
-      return false;
-    }
-    m = std::move(local_.front());
-    local_.pop_front();
+  std::unique_lock<std::mutex> lk(mu_);
+  auto ready = [&] { return !inbox_.empty() || cancelled_.load() || !failed_.empty(); };
+  if (timeout_ms < 0) {
+    cv_.wait(lk, ready);
   } else {
-    bool to = false;
-    std::string e;
-    if (!mesh_->recv(kTagP2P, -1, &m, nullptr, timeout_ms, &to, &e)) {
-      // only the wait running out is a timeout; a broken link (the member died)
-      // or a closed mesh is an error, so callers stop instead of retrying
-      if (timed_out) *timed_out = to;
-      if (err && !to) *err = "recv: " + e;
-      return false;
-    }
+    cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), ready);
   }
-  std::vector<size_t> sizes;
-  std::vector<std::string> metas;
-  if (m.flags & 1) {  // in-process
-    if (!decode(m.caps, p, false, &sizes, &metas)) return false;
-    p->blobs = std::move(m.blobs);
-    return true;
-  }
-  if (!from_message(std::move(m), p, &sizes, &metas)) {
-    if (err) *err = "recv: bad header";
+  if (!failed_.empty()) {
+    if (err) *err = "recv: " + failed_;
     return false;
   }
-  if (!rccl()) return true;
-  hip::DeviceGuard dg(device_);
-  Link* l = nullptr;
-  if (!link(p->src, false, &l, err)) return false;
-  auto comm = static_cast<ncclComm_t>(l->comm);
-  p->blobs.clear();
-  for (size_t i = 0; i < sizes.size(); ++i) {
-    auto m = sizes[i] ? Memory::alloc_device(sizes[i], device_, l->stream) : Memory::alloc_host(0);
-    if (!metas[i].empty()) {
-      MetaInfo mi;
-      if (MetaInfo::parse(metas[i].data(), metas[i].size(), &mi)) m->set_meta(mi);
+  if (inbox_.empty()) {
+    if (cancelled_.load()) {
+      if (err) *err = "recv: cancelled";
+    } else if (timed_out) {
+      *timed_out = true;
     }
-    bytes_recv_ += sizes[i];
-    p->blobs.push_back(m);
+    return false;
   }
-  if (!nccl_ok(ncclGroupStart(), "ncclGroupStart", err)) return false;
-  for (auto& b : p->blobs)
-    if (b->size() && !nccl_ok(ncclRecv(b->data(), b->size(), ncclUint8, 0, comm, l->stream), "ncclRecv", err)) {
-      ncclGroupEnd();
-      return false;
-    }
-  if (!nccl_ok(ncclGroupEnd(), "ncclGroupEnd", err)) return false;
-  for (auto& b : p->blobs)
-    if (b->size()) b->mark_ready(l->stream);
+  *p = std::move(inbox_.front());
+  inbox_.pop_front();
+  bool wake = false;
+  const int s = p->src;
+  if (engine_ && s != grank_ && s >= 0 && s < size()) {
+    --unconsumed_[static_cast<size_t>(s)];
+    // the sender may be held back by the last grant: advertise the room
+    wake = granted_[static_cast<size_t>(s)] < kWindow;
+  }
+  lk.unlock();
+  if (wake) {
+    work_ = true;
+    poke();
+  }
   return true;
 }
 

@@ -570,7 +570,7 @@ class QueryServerSrc : public BaseSrc {
 
   FlowReturn create(BufferPtr* out) override {
     if (connect_type_ == kRccl) {
-      if (!req_ && !(req_ = rp_.open(this, server_->channel + "/req"))) return FlowReturn::ERROR;
+      if (!req_ && !(req_ = rp_.open(this, server_->channel))) return FlowReturn::ERROR;
       comm::Packet p;
       std::string err;
       const int64_t t0 = now_ns();
@@ -673,7 +673,7 @@ class QueryServerSink : public BaseSink {
       post_error("tensor_query_serversink: no connect-type=RCCL tensor_query_serversrc with the same id");
       return false;
     }
-    return (rep_ = rp.open(this, ch + "/rep")) != nullptr;
+    return (rep_ = rp.open(this, ch)) != nullptr;  // (the serversrc's group: one per query channel)
   }
   FlowReturn render(const BufferPtr& buf) override {
     const uint64_t cid = buf->meta.client_id;
@@ -819,9 +819,10 @@ class QueryClient : public Element {
     if (req_) return true;
     rp_.device = device_;
     const std::string ch = rccl_channel("query", topic_, dest_port_);
-    // same order as the server: its serversink joins "rep" while the caps
-    // event travels (on the serversrc thread), before serversrc joins "req"
-    if (!(rep_ = rp_.open(this, ch + "/rep")) || !(req_ = rp_.open(this, ch + "/req"))) return false;
+    // requests and replies share ONE group (one round sequence: a reply can
+    // never queue on the device behind a request of another group's round)
+    if (!(rep_ = rp_.open(this, ch))) return false;
+    req_ = rep_;
     server_ = rp_.peer_in(*req_);
     if (server_ < 0 || server_ == req_->rank()) {
       post_error("tensor_query_client: peer-rank is not another member of the group");

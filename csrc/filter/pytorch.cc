@@ -131,7 +131,7 @@ class TorchInstance : public FilterInstance {
   bool wants_host_input() const override { return device_ < 0; }
 
   std::string info(const std::string& key) const override {
-    if (key == "model-broadcast" && bcast_bytes_) return bcast_group_;
+    if (key == "model-broadcast" && !bcast_group_.empty()) return bcast_group_;
     return std::string();
   }
 
@@ -322,7 +322,24 @@ class TorchInstance : public FilterInstance {
     t.copy_(src.to(t.device()));
     if (device_ >= 0) hip::check(hipDeviceSynchronize(), "in_lut upload");
   }
-  void load(const std::string& path) { module_ = bcast_root_ >= 0 ? load_broadcast(path) : load_module(path); }
+  void load(const std::string& path) {
+    if (bcast_root_ < 0) {
+      module_ = load_module(path);
+      return;
+    }
+    try {
+      module_ = load_broadcast(path);
+    } catch (const std::exception& e) {
+      // the data plane must never cost a rank its model: when the broadcast
+      // fails (a member missing, an aborted communicator) and this rank has
+      // the file itself, it loads it and reports the failure in model-broadcast
+      std::ifstream f(path, std::ios::binary);
+      if (!f) throw;
+      NNSX_LOGW("pytorch", e.what(), "; loading ", path, " locally");
+      bcast_group_ = strfmt("failed:", e.what());
+      module_ = load_module(path);
+    }
+  }
 
   // custom=broadcast:<root rank>: one-process-per-GPU deployments load the
   // model once -- rank <root> reads the TorchScript file and broadcasts its

@@ -37,11 +37,11 @@ def test_bench_refuses_world_mismatch():
 
 
 def test_bench_three_ranks_selfcheck_and_extra_configs():
-    """WORLD_SIZE > 1 (the driver's scaling run): before the timed run every
+    """WORLD_SIZE > 1 (the driver's scaling run): after the headline every
     comm::Group operation is checked on every rank (rccl_selfcheck; tcp data
-    plane on CPU, RCCL on GPUs), and after the headline short passes of the
-    multi-rank configs 4 and 5 report their frames/s and groups -- all outside
-    the timed region, well inside a minute."""
+    plane on CPU, RCCL on GPUs) and short passes of the multi-rank configs 4
+    and 5 report their frames/s and groups -- all outside the timed region,
+    well inside a minute."""
     import time
 
     t0 = time.time()
@@ -53,6 +53,7 @@ def test_bench_three_ranks_selfcheck_and_extra_configs():
     sc = out["rccl_selfcheck"]
     for k in ("allgather", "allgather_ragged", "broadcast", "scatter", "p2p_ring", "p2p_exchange"):
         assert sc[k] is True, sc
+    assert sc["ok"] is True
     assert sc["members"] == 3 and sc["backend"] == "tcp"
     xs = out["extra_configs"]
     assert set(xs) == {"deeplab_fan", "posenet_multi"}
@@ -60,3 +61,39 @@ def test_bench_three_ranks_selfcheck_and_extra_configs():
     assert "edge_fan1" in xs["deeplab_fan"]["groups_rank0"] and "edge_allgather" in xs["posenet_multi"]["groups_rank0"]
     assert out["fp32_method"] in ("x3", "fp32")
     assert out["value"] > 0 and out["n_gpus"] == 0
+
+
+def test_bench_selfcheck_fault_never_blocks_headline():
+    """One member skips the broadcast (NNSX_SELFCHECK_FAULT): the other members'
+    broadcast fails within the self-check's deadline with an error naming the
+    mismatch / the missing member, later collectives fail fast, p2p still
+    checks out, and the headline JSON is printed with exit code 0."""
+    import time
+
+    t0 = time.time()
+    r = _run(["--cpu", "--gpus", "3", "--steps", "2", "--warmup", "1", "--batch", "1", "--latency-frames", "0",
+              "--sweep", "", "--extra-configs", "", "--selfcheck-timeout-ms", "4000"],
+             env={"NNSX_SELFCHECK_FAULT": "1:broadcast"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert time.time() - t0 < 150
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["value"] > 0 and out["pg_world"] == 3
+    sc = out["rccl_selfcheck"]
+    assert sc["ok"] is False and sc["broadcast"] is False, sc
+    assert sc["allgather"] is True and sc["allgather_ragged"] is True, sc
+    assert sc["p2p_ring"] is True and sc["p2p_exchange"] is True, sc
+    err = sc["errors_rank0"]["broadcast"]
+    assert "member 1" in err or "member(s) 1" in err, err
+    assert sc["seconds_max"] < 60
+
+
+def test_bench_aux_watchdog_prints_headline(tmp_path):
+    """A hung auxiliary phase (watchdog at 1 s while the extra configs run)
+    still yields the headline line and exit code 0 on every rank."""
+    r = _run(["--cpu", "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "1", "--latency-frames", "0",
+              "--sweep", "", "--aux-timeout", "1"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["value"] > 0 and "aux_timeout" in out
