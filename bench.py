@@ -75,8 +75,11 @@ def parse_args(argv=None):
     ap.add_argument("--precision", default=os.environ.get("NNSX_BENCH_PRECISION", "fp32"),
                     choices=["fp32", "bf16", "both"],
                     help="fp32 = reference precision (headline); bf16 = secondary; both = fp32 headline + bf16")
-    ap.add_argument("--engine", default=os.environ.get("NNSX_BENCH_ENGINE", "fused"), choices=["fused", "torch"],
-                    help="fused = nnsx CDNA4 kernels; torch = plain TorchScript/MIOpen model (fp32)")
+    ap.add_argument("--engine", default=os.environ.get("NNSX_BENCH_ENGINE", "fused"),
+                    choices=["fused", "lowered", "torch"],
+                    help="fused = nnsx's exported model on the CDNA4 kernels; lowered = the plain TorchScript model, "
+                         "lowered onto the same kernels by tensor_filter at load (custom=lower:auto); torch = the "
+                         "plain model on PyTorch/MIOpen (custom=lower:off)")
     ap.add_argument("--latency-frames", type=int, default=int(os.environ.get("NNSX_BENCH_LAT_FRAMES", "300")),
                     help="frames of the batch-1 latency run (0 = skip)")
     ap.add_argument("--latency-fps", type=int, default=int(os.environ.get("NNSX_BENCH_LAT_FPS", "0")),
@@ -237,9 +240,10 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
     bcast = ""
     if world > 1 and a.model_broadcast != "off" and not cfg.get("fan"):  # (fan-out: rank 0 runs no filter)
         bcast = f",broadcast:0,broadcast-backend:{a.model_broadcast},broadcast-name:{model_name}-b{B}"
+    lower = ",lower:off" if a.engine == "torch" else ""
     filt = (f"tensor_filter name=filt framework=pytorch model={model_path} input=3:{S}:{S}:{B} "
             f"inputtype=float32 absorb-transform={absorb} accelerator={accel} device={dev} "
-            f"custom=hipgraph:{graph}{bcast} device-stats={'true' if use_gpu else 'false'} ")
+            f"custom=hipgraph:{graph}{bcast}{lower} device-stats={'true' if use_gpu else 'false'} ")
     live = f"is-live=true " if live_fps > 0 else ""
     gather = bool(cfg.get("gather"))
     # multi-source sync: the cameras of every rank stamp the same frame clock (frame k
@@ -325,6 +329,7 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
         mux_sets = int(ms.get_property("frames")) if ms is not None else None
     dev_stamps = filt_el.get_property("device-stamps") if (filt_el is not None and use_gpu) else ""
     absorbed = filt_el.get_property("absorbed") if filt_el is not None else ""
+    lowered = filt_el.get_property("lowered") if filt_el is not None else ""
     absorbed_dec = filt_el.get_property("absorbed-decoder") if filt_el is not None else ""
     # the nnsx rank groups this rank actually used (data plane : members)
     groups = {}
@@ -340,6 +345,7 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
 
     rec = dict(elapsed=0.0, p50=0.0, p99=0.0, gpu_elapsed=0.0, gpu_busy_ms=0.0, wall=t_end - t_start,
                desc=desc, fan=fan, workers=workers, absorbed=absorbed, absorbed_dec=absorbed_dec, gathered=gathered,
+               lowered=lowered,
                groups=groups, mux_sets=mux_sets)
     recs = [tuple(int(v) for v in e.split(":")) for e in sink.get_property("stats").split(",") if e]
     arrivals = [t / 1e9 for i, (t, _) in enumerate(recs) if (i + 1) % per_step == 0]  # last frame of each batch
@@ -418,7 +424,7 @@ def main():
 
     # which engines to run: (label, model name, dtype)
     base = cfg["model"]
-    if a.engine == "torch" or not use_gpu:
+    if a.engine in ("torch", "lowered") or not use_gpu:
         plain = base.replace("_fused", "").replace("_lowres", "")  # the plain oracle emits full-size maps
         runs = [("fp32", plain, "fp32")]
     else:
@@ -594,6 +600,8 @@ def headline_record(a, cfg, runs, results, lat_b1, sweep, per_rank, world, use_g
                         "int32 indices leave the model)" if head.get("absorbed_dec")
                         else "tensor_decoder's own argmax kernel"),
         "wall_s": round(sum(r["wall"] for r in results.values()), 3),
+        "engine": a.engine,
+        **({"lowered": head["lowered"]} if head.get("lowered") else {}),
         "numa_binding": numa,
         **({"allgather_bytes_published_rank0": head["gathered"]} if head["gathered"] is not None else {}),
         **({"mux_sets_rank0": head["mux_sets"]} if head.get("mux_sets") is not None else {}),

@@ -28,6 +28,7 @@ using namespace nnsx;
 
 namespace nnsx {
 std::string memory_selftest(const std::string& name, int dev);  // runtime/selftest.cc
+std::string lower_torchscript_file(const std::string& in, const std::string& out, int device);  // filter/torch_lower.cc
 }  // namespace nnsx
 
 namespace nnsx {
@@ -584,6 +585,12 @@ PYBIND11_MODULE(_C, m) {
       });
 
   m.def("parse_launch", [](const std::string& d) { return parse_launch(d); });
+  m.def("lower_torchscript", [](const std::string& in, const std::string& out, int device) {
+    py::gil_scoped_release r;
+    return lower_torchscript_file(in, out, device);
+  }, py::arg("path"), py::arg("out"), py::arg("device") = -1,
+        "Freeze and lower a TorchScript file onto the nnsx kernels (what tensor_filter framework=pytorch does at "
+        "load); saves the result and returns the report");
   m.def("tracer_enable", [](const std::string& spec) { trace::enable(spec); }, py::arg("spec"),
         "Enable built-in tracers: 'proctime;interlatency;framerate;roctx' ('' disables)");
   m.def("tracer_reset", [] { trace::reset(); });

@@ -146,6 +146,9 @@ class TensorFilter : public BaseTransform, public TransformAbsorber {
     prop_bool("absorb-transform", &absorb_enabled_,
               "nnsx: fold an adjacent upstream tensor_transform (uint8 -> float32 elementwise arithmetic) into the "
               "model when the model maps uint8 frames through an input table");
+    prop_readonly("lowered", [this] { return inst_ ? inst_->info("lowered") : std::string(); },
+                  "nnsx (framework=pytorch): what the load-time lowering of a plain model onto the nnsx kernels "
+                  "did ('' = not lowered)");
     prop_readonly("model-broadcast", [this] { return inst_ ? inst_->info("model-broadcast") : std::string(); },
                   "nnsx: '<data plane>:<members>:<bytes>' when the model arrived by a rank-group broadcast "
                   "(custom=broadcast:<root>)");

@@ -16,6 +16,9 @@
 //   broadcast:<rank>      load the model once: <rank> broadcasts the file's bytes
 //                         to every rank of the job (RCCL / TCP), see load_broadcast
 //   broadcast-backend:auto|rccl|tcp, broadcast-store:host:port, broadcast-name:<channel>
+//   lower:auto|off        load-time lowering of a plain model onto the nnsx kernels
+//                         (filter/torch_lower.cc): auto = on a GPU, verified against
+//                         the original on a 2-frame input at load (NNSX_LOWER=0: off)
 //   lanes:<n>|auto        replay lanes (hipgraph): consecutive frames go round robin
 //                         to n streams, each with its own graphs and memory pool, so
 //                         the forwards of small batches overlap on the GPU (auto: 3
@@ -34,6 +37,7 @@
 #include "comm/group.h"
 #include "core/log.h"
 #include "filter/filter.h"
+#include "filter/torch_lower.h"
 #include "filter/torch_util.h"
 #include "kernels/kernels.h"
 #include "kernels/mbv2.h"
@@ -132,6 +136,7 @@ class TorchInstance : public FilterInstance {
 
   std::string info(const std::string& key) const override {
     if (key == "model-broadcast" && !bcast_group_.empty()) return bcast_group_;
+    if (key == "lowered") return lowered_;
     return std::string();
   }
 
@@ -281,14 +286,102 @@ class TorchInstance : public FilterInstance {
       else if (k == "broadcast-backend") bcast_backend_ = v;
       else if (k == "broadcast-store") bcast_store_ = v;
       else if (k == "broadcast-name") bcast_name_ = v;
+      else if (k == "lower") lower_opt_ = lower(v);
       else if (k == "lanes") lanes_opt_ = lower(v) == "auto" ? 0 : std::max(1, std::min(kMaxLanes, static_cast<int>(to_int(v))));
     }
   }
 
   torch::jit::Module load_module(const std::string& path) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) throw Error("pytorch: cannot read " + path);
+    return load_bytes(std::string((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>()));
+  }
+
+  torch::jit::Module load_bytes(const std::string& bytes) {
     hip::DeviceGuard g(device_);
-    torch::jit::Module m = torch::jit::load(path, dev());
-    return finish_module(std::move(m));
+    std::istringstream is(bytes);
+    torch::jit::Module m = finish_module(torch::jit::load(is, dev()));
+    lowered_.clear();
+    if (!want_lowering(m)) return m;
+    // a second, independent copy is rewritten; the original stays the fallback
+    std::istringstream is2(bytes);
+    torch::jit::Module low = finish_module(torch::jit::load(is2, dev()));
+    LowerReport rep;
+    std::string why;
+    if (!lower_to_engine(low, dev(), &rep, &why)) {
+      NNSX_LOGI("pytorch", "model not lowered onto the nnsx kernels: ", why);
+      return m;
+    }
+    if (!verify_lowering(m, low, &why)) {
+      NNSX_LOGW("pytorch", "lowered model rejected (", why, "); running the model as loaded");
+      lowered_ = "rejected: " + why;
+      return m;
+    }
+    lowered_ = rep.summary();
+    NNSX_LOGI("pytorch", "model lowered onto the nnsx kernels: ", lowered_);
+    has_lut_ = low.hasattr("in_lut");
+    if (has_lut_ && default_lut_.empty()) {
+      at::Tensor t = low.attr("in_lut").toTensor().detach().to(torch::kCPU).contiguous();
+      default_lut_.assign(t.data_ptr<float>(), t.data_ptr<float>() + 256);
+    }
+    return low;
+  }
+
+  // plain models on a GPU: not nnsx's own exports (those call torch.ops.nnsx
+  // already, or expose in_lut), and only with a known input shape to verify on
+  bool want_lowering(const torch::jit::Module& m) const {
+    if (device_ < 0 || lower_opt_ == "off" || lower_opt_ == "false" || has_lut_) return false;
+    if (const char* e = std::getenv("NNSX_LOWER"))
+      if (e[0] == '0') return false;
+    if (props_.input_info.num_tensors != 1 || !props_.input_info.valid()) return false;
+    try {
+      for (const torch::jit::Node* n : m.get_method("forward").graph()->nodes())
+        if (std::string(n->kind().toQualString()).rfind("nnsx::", 0) == 0) return false;
+    } catch (...) {
+      return false;
+    }
+    return true;
+  }
+
+  // the lowered module must reproduce the original on a 2-frame random input
+  // (max |diff| <= 1e-3 of the output scale, every output)
+  bool verify_lowering(torch::jit::Module& orig, torch::jit::Module& low, std::string* why) {
+    try {
+      torch::InferenceMode guard;
+      const TensorInfo& ti = props_.input_info.at(0);
+      if (ti.type != DType::FLOAT32) {
+        *why = "input type is not float32";
+        return false;
+      }
+      const int rk = !props_.input_ranks.empty() ? props_.input_ranks[0] : 0;
+      std::vector<int64_t> sz = torch_sizes(ti, rk);
+      if (sz.size() == 4) sz[0] = 2;
+      at::Tensor x = torch::randn(sz, torch::TensorOptions().dtype(torch::kFloat).device(dev()));
+      std::vector<at::Tensor> a, b;
+      flatten(orig.forward({x}), &a);
+      flatten(low.forward({x}), &b);
+      if (device_ >= 0) hip::check(hipDeviceSynchronize(), "lowering check");
+      if (a.size() != b.size()) {
+        *why = "output count differs";
+        return false;
+      }
+      for (size_t i = 0; i < a.size(); ++i) {
+        if (a[i].sizes() != b[i].sizes()) {
+          *why = strfmt("output ", i, " shape differs");
+          return false;
+        }
+        const double scale = std::max(1.0, a[i].abs().max().item<double>());
+        const double d = (a[i].to(torch::kFloat) - b[i].to(torch::kFloat)).abs().max().item<double>() / scale;
+        if (!(d <= 1e-3)) {
+          *why = strfmt("output ", i, " differs by ", d, " of its scale");
+          return false;
+        }
+      }
+      return true;
+    } catch (const std::exception& e) {
+      *why = e.what();
+      return false;
+    }
   }
 
   // eval + freeze (constant-folds attributes); `in_lut` stays a mutable
@@ -377,9 +470,7 @@ class TorchInstance : public FilterInstance {
     bcast_group_ = strfmt(g->backend_name(), ":", g->size(), ":", bytes.size());
     NNSX_LOGI("pytorch", "model of rank ", bcast_root_, " received over ", g->backend_name(), " (", bytes.size(),
               " bytes, group rank ", g->rank(), "/", g->size(), ")");
-    hip::DeviceGuard dg(device_);
-    std::istringstream is(bytes);
-    return finish_module(torch::jit::load(is, dev()));
+    return load_bytes(bytes);
   }
 
   // outs[argmax_out_] -> int32 index of the first largest value along the last
@@ -742,6 +833,8 @@ class TorchInstance : public FilterInstance {
   std::string bcast_backend_ = "auto", bcast_store_, bcast_name_;
   size_t bcast_bytes_ = 0;
   std::string bcast_group_;  // "<data plane>:<members>:<bytes>" of the load-time broadcast
+  std::string lower_opt_ = "auto";  // custom=lower:auto|off
+  std::string lowered_;             // what the load-time lowering did ("" = not lowered)
   const bool copy_out_ = [] {
     const char* e = std::getenv("NNSX_GRAPH_COPY_OUT");
     return e && e[0] == '1';

@@ -36,6 +36,10 @@ struct IrwCfg {
 
 // the x3 twins of the fused-block configurations (kernels/irw_x3.hip)
 const std::vector<IrwCfg>& x3_irw_cfgs();
+// 14 x 14 blocks, one image per workgroup, split-bf16 (kernels/irp_x3.hip);
+// needs a.we3 / a.wp3.  false: not this shape (or NNSX_IRP=0)
+bool irp_x3_supported(const IrBlockF32Args& a);
+bool irp_x3(const IrBlockF32Args& a, hipStream_t s);
 
 namespace {
 

@@ -2198,6 +2198,7 @@ bool ir_expand_dw_f32(const IrBlockF32Args& args, hipStream_t s) {
 }
 
 size_t ir_block_f32_workspace_bytes(const IrBlockF32Args& args) {
+  if (f32_math() == F32Math::kX3 && irp_x3_supported(args)) return 0;  // (one image per workgroup: no parts)
   const IrwCfg* c = find_irw(args.stride, args.H, args.W, args.cin, args.hid, args.cout, args.has_expand != 0, args.dil,
                              args.B);
   if (!c) return 0;
@@ -2267,6 +2268,20 @@ bool stem_ir1_f32(const StemIr1F32Args& args, hipStream_t s) {
 }
 
 const char* ir_block_f32_method(int stride, int H, int W, int cin, int hid, int cout, int B, int dil) {
+  {
+    IrBlockF32Args q;
+    q.stride = stride;
+    q.H = H;
+    q.W = W;
+    q.cin = cin;
+    q.hid = hid;
+    q.cout = cout;
+    q.B = B;
+    q.dil = dil;
+    static const uint16_t dummy[8] = {};
+    q.we3 = q.wp3 = dummy;
+    if (f32_math() == F32Math::kX3 && irp_x3_supported(q)) return "x3";
+  }
   const IrwCfg* c = find_irw(stride, H, W, cin, hid, cout, true, dil, B);
   if (!c) return ir_block_f32_supported(stride, H, W, cin, hid, cout, true, dil) ? "fp32" : "";
   IrBlockF32Args a;
@@ -2278,6 +2293,8 @@ const char* ir_block_f32_method(int stride, int H, int W, int cin, int hid, int 
 
 bool ir_block_f32(const IrBlockF32Args& args, hipStream_t s) {
   IrBlockF32Args a = args;
+  // 14 x 14 blocks on the x3 method: one image per workgroup (kernels/irp_x3.hip)
+  if (f32_math() == F32Math::kX3 && irp_x3(a, s)) return true;
   if (const IrwCfg* w = find_irw(a.stride, a.H, a.W, a.cin, a.hid, a.cout, a.has_expand != 0, a.dil, a.B)) {
     if (const IrwCfg* x = x3_twin(w, a)) return launch_irw(x, a, s);
     return launch_irw(w, a, s);

@@ -724,6 +724,73 @@ at::Tensor ir_block_cpu(const at::Tensor& x, const at::Tensor& we, const at::Ten
   return pw_conv_cpu(h, wp, bp, res, cout, 0, false);  // (dtype follows x: f32 stays f32)
 }
 
+// ------------------------------------------------- lowered-graph ops ----
+// Composite ops the load-time lowering (filter/torch_lower.cc) emits for a
+// plain TorchScript model: each takes the fused kernel when the shape, dtype
+// and device allow it and otherwise runs the same arithmetic on the unfused
+// nnsx ops, so a lowered graph never fails on a shape the kernels lack.
+at::Tensor ir_block_any(const at::Tensor& x, const at::Tensor& we, const at::Tensor& be, const at::Tensor& wd,
+                        const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, int64_t stride, int64_t cout,
+                        bool has_expand, bool residual, int64_t dilation, const c10::optional<at::Tensor>& tickets,
+                        const c10::optional<at::Tensor>& we3, const c10::optional<at::Tensor>& wp3) {
+  if (!x.is_cuda() || x.scalar_type() != at::kFloat)
+    return ir_block_cpu(x.to(at::kFloat), we, be, wd, bd, wp, bp, stride, cout, has_expand, residual, dilation,
+                        tickets, we3, wp3);
+  at::Tensor xc = x.contiguous();
+  const int64_t B = xc.size(0), H = xc.size(1), W = xc.size(2), C = xc.size(3), hid = wd.size(1);
+  if (nnsx::kernels::ir_block_f32_supported(static_cast<int>(stride), static_cast<int>(H), static_cast<int>(W),
+                                            static_cast<int>(C), static_cast<int>(hid), static_cast<int>(cout),
+                                            has_expand, static_cast<int>(dilation), static_cast<int>(B)))
+    return ir_block_f32_cuda(xc, we, be, wd, bd, wp, bp, stride, cout, has_expand, residual, dilation, tickets, we3,
+                             wp3);
+  at::Tensor h;
+  if (has_expand && nnsx::kernels::ir_expand_dw_f32_supported(static_cast<int>(stride), static_cast<int>(H),
+                                                             static_cast<int>(W), static_cast<int>(C),
+                                                             static_cast<int>(hid), static_cast<int>(B),
+                                                             static_cast<int>(dilation))) {
+    h = ir_expand_dw_cuda(xc, we, be, wd, bd, stride, dilation, we3);
+  } else {
+    h = has_expand ? pw_conv_f32_cuda(xc, we, be, c10::nullopt, hid, 1) : xc;
+    h = dw_conv_cuda(h, wd, bd, stride, 1, dilation);
+  }
+  c10::optional<at::Tensor> res;
+  if (residual) res = xc;
+  return pw_conv_f32_cuda(h, wp, bp, res, cout, 0);
+}
+
+// stem conv + act from a uint8 frame (through the input table) or a float one
+at::Tensor stem_any(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, const at::Tensor& lut,
+                    int64_t act) {
+  if (x.scalar_type() == at::kByte)
+    return x.is_cuda() ? stem_conv_u8_cuda(x.contiguous(), w, bias, act, lut, true)
+                       : stem_conv_u8_cpu(x, w, bias, act, lut, true);
+  at::Tensor xf = x.to(at::kFloat).contiguous();
+  return xf.is_cuda() ? stem_conv_cuda(xf, w, bias, act, true) : stem_conv_cpu(xf, w, bias, act, true);
+}
+
+at::Tensor stem_ir1_cuda(const at::Tensor& x, const at::Tensor& ws, const at::Tensor& bs, const at::Tensor& wd,
+                         const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, const at::Tensor& lut,
+                         int64_t mode);
+at::Tensor stem_ir1_cpu(const at::Tensor& x, const at::Tensor& ws, const at::Tensor& bs, const at::Tensor& wd,
+                        const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, const at::Tensor& lut,
+                        int64_t mode);
+
+// stem + a t = 1 first block (32 -> dw -> 16): one kernel on a uint8 frame,
+// else the stem, depthwise and project ops
+at::Tensor stem_ir1_any(const at::Tensor& x, const at::Tensor& ws, const at::Tensor& bs, const at::Tensor& wd,
+                        const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, const at::Tensor& lut,
+                        int64_t cout) {
+  if (x.scalar_type() == at::kByte && x.is_cuda() && cout == 16 && wp.size(0) >= 16 && wp.size(1) == 32)
+    return stem_ir1_cuda(x.contiguous(), ws, bs, wd, bd, wp, bp, lut, -1);
+  at::Tensor h = stem_any(x, ws, bs, lut, 1);
+  if (h.is_cuda()) {
+    h = dw_conv_cuda(h, wd, bd, 1, 1, 1);
+    return pw_conv_f32_cuda(h, wp, bp, c10::nullopt, cout, 0);
+  }
+  h = dw_conv_cpu(h, wd, bd, 1, 1, 1);
+  return pw_conv_cpu(h, wp, bp, c10::nullopt, cout, 0, true);
+}
+
 // stem + first (t = 1) block, fused (fp32): uint8 frame -> [B, Ho, Wo, 16]
 at::Tensor stem_ir1_cuda(const at::Tensor& x, const at::Tensor& ws, const at::Tensor& bs, const at::Tensor& wd,
                          const at::Tensor& bd, const at::Tensor& wp, const at::Tensor& bp, const at::Tensor& lut,
@@ -830,6 +897,13 @@ TORCH_LIBRARY(nnsx, m) {
         "bool has_expand, bool residual, int dilation=1, Tensor(a!)? tickets=None, Tensor? we3=None, "
         "Tensor? wp3=None) -> Tensor");
   m.def("ir_supported(int stride, int cin, int hid, int cout) -> bool", ir_supported);
+  // composite ops of the load-time lowering of plain TorchScript models (filter/torch_lower.cc)
+  m.def("ir_block_any(Tensor x, Tensor we, Tensor be, Tensor wd, Tensor bd, Tensor wp, Tensor bp, int stride, "
+        "int cout, bool has_expand, bool residual, int dilation=1, Tensor(a!)? tickets=None, Tensor? we3=None, "
+        "Tensor? wp3=None) -> Tensor", ir_block_any);
+  m.def("stem_any(Tensor x, Tensor w, Tensor bias, Tensor lut, int act) -> Tensor", stem_any);
+  m.def("stem_ir1_any(Tensor x, Tensor ws, Tensor bs, Tensor wd, Tensor bd, Tensor wp, Tensor bp, Tensor lut, "
+        "int cout) -> Tensor", stem_ir1_any);
   m.def("ir_supported_f32(int stride, int H, int W, int cin, int hid, int cout, bool has_expand, int dilation=1, "
         "int B=0) -> bool",
         ir_supported_f32);

@@ -24,11 +24,12 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("NNSX_CXX", "/opt/rocm/lib/llvm/bin/clang++")
 
 # sources that include libtorch headers (slow to compile)
-TORCH_SOURCES = {"filter/pytorch.cc", "filter/torch_trainer.cc", "ops/torch_ops.cc"}
+TORCH_SOURCES = {"filter/pytorch.cc", "filter/torch_trainer.cc", "filter/torch_lower.cc", "ops/torch_ops.cc"}
 # pybind11 sources
 PY_SOURCES = {"bindings/module.cc", "bindings/python_bridge.cc"}
 # per-unit code generation: the x3 GEMMs keep MFMA results in VGPRs (kernels/gemm_f32.h)
-UNIT_FLAGS = {"kernels/gemm_x3.hip": "-mllvm -amdgpu-mfma-vgpr-form", "kernels/irw_x3.hip": "-mllvm -amdgpu-mfma-vgpr-form"}
+UNIT_FLAGS = {"kernels/gemm_x3.hip": "-mllvm -amdgpu-mfma-vgpr-form", "kernels/irw_x3.hip": "-mllvm -amdgpu-mfma-vgpr-form",
+              "kernels/irp_x3.hip": "-mllvm -amdgpu-mfma-vgpr-form"}
 
 
 def ext_suffix() -> str:
