@@ -308,6 +308,9 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
         sink.set_property("emit-signal", "false")
         sink.set_property("sync-device", "true")
         sink.set_property("stats-every", "1")
+        # roctx marks at the timed window's ends (the arrivals of batch W and W + K):
+        # scripts/kstats.py --window keeps only the kernels that ran between them
+        sink.set_property("roctx-marks", f"{warmup * per_step},{(warmup + steps) * per_step}")
 
     import torch
 

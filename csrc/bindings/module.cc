@@ -83,6 +83,9 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("name"), py::arg("device") = 0,
         "Deterministic device-memory lifetime regression case (runtime/selftest.cc): '' = pass");
   m.def("memory_check_enabled", [] { return Memory::check_enabled(); });
+  m.def("memory_test_mutation", [](int m) { return Memory::set_test_mutation(m); }, py::arg("mutation"),
+        "Lifetime self-tests only: 1 = undo the pageable-H2D use (7ba8684), 2 = undo the mirror hold (ee80b24), "
+        "0 = none; returns the previous value");
   m.def("memory_drain_deferred", [] {
     py::gil_scoped_release nogil;
     Memory::drain_deferred();

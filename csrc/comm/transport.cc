@@ -17,6 +17,7 @@
 #include <map>
 #include <thread>
 
+#include "comm/shm.h"
 #include "core/log.h"
 #include "core/util.h"
 #include "runtime/hip_util.h"
@@ -62,6 +63,7 @@ bool resolve(const std::string& host, int port, sockaddr_in* out) {
 }
 
 constexpr uint32_t kFlagIpc = 1u << 31;       // DATA: a u64 ring offset per blob follows the sizes
+constexpr uint32_t kFlagShm = 1u << 30;       // DATA: a u64 shared-memory reference per blob follows the sizes
 constexpr uint64_t kInline = ~0ull;           // offset of a blob that travels as bytes
 constexpr uint64_t kMinIpcBytes = 4096;       // smaller device blobs are cheaper inline
 constexpr size_t kDefaultRing = 256ull << 20;  // per sending end; HBM is 288 GB
@@ -295,6 +297,14 @@ bool Connection::send_ipc_hello(size_t ring_bytes) {
   return send(m);
 }
 
+bool Connection::send_shm_hello() {
+  if (boot_id().empty()) return false;
+  Message m;
+  m.type = MsgType::SHM_HELLO;
+  m.caps = strfmt("boot=", boot_id());
+  return send(m);
+}
+
 void Connection::send_ack(uint64_t off, uint64_t bytes) {
   Message m;
   m.type = MsgType::IPC_ACK;
@@ -345,6 +355,27 @@ bool Connection::handle_control(const Message& m) {
     case MsgType::IPC_ACK:
       if (ring_) ring_->release(m.seq);
       return true;
+    case MsgType::SHM_HELLO:
+      if (parse_kv(m.caps)["boot"] == boot_id()) peer_shm_ = true;
+      return true;
+    case MsgType::SHM_SEG: {
+      auto kv = parse_kv(m.caps);
+      std::string e;
+      auto seg = ShmSegment::open(kv["name"], static_cast<size_t>(to_uint(kv["size"])), &e);
+      if (!seg) {
+        NNSX_LOGE("comm", "cannot map the shared segment of ", peer_, ": ", e);
+        return false;
+      }
+      std::lock_guard<std::mutex> lk(shm_mu_);
+      shm_peer_[static_cast<uint32_t>(to_uint(kv["id"]))] = seg;
+      return true;
+    }
+    case MsgType::SHM_ACK: {
+      std::lock_guard<std::mutex> lk(shm_mu_);
+      auto it = shm_held_.find(m.seq);
+      if (it != shm_held_.end()) shm_held_.erase(it);
+      return true;
+    }
     default:
       return true;
   }
@@ -389,23 +420,51 @@ bool Connection::send(const Message& m) {
       if (!any) offs.clear();
     }
   }
+  // same-host shared memory: host blobs inside one of our segments go as
+  // references, held until the peer releases them
+  std::vector<Message> segs;
+  bool shm = false;
+  if (m.type == MsgType::DATA && peer_shm_ && offs.empty()) {
+    std::lock_guard<std::mutex> lk(shm_mu_);
+    for (size_t i = 0; i < m.blobs.size(); ++i) {
+      const MemoryPtr& b = m.blobs[i];
+      size_t off = 0;
+      std::shared_ptr<ShmSegment> seg;
+      if (b->on_device() || !b->size() || !(seg = ShmSegment::find(b->data(), b->size(), &off))) continue;
+      auto id = shm_ids_.find(seg->name());
+      if (id == shm_ids_.end()) {
+        id = shm_ids_.emplace(seg->name(), static_cast<uint32_t>(shm_ids_.size())).first;
+        Message r;
+        r.type = MsgType::SHM_SEG;
+        r.caps = strfmt("id=", id->second, ";name=", seg->name(), ";size=", seg->size());
+        segs.push_back(std::move(r));
+      }
+      if (offs.empty()) offs.assign(m.blobs.size(), kInline);
+      offs[i] = (static_cast<uint64_t>(id->second) << 48) | static_cast<uint64_t>(off);
+      shm_held_.emplace(offs[i], b);
+      shm = true;
+    }
+  }
   std::lock_guard<std::mutex> lk(send_mu_);
+  for (auto& r : segs)
+    if (!send_locked(r, nullptr)) return false;
   if (announce) {
     Message r;
     r.type = MsgType::IPC_RING;
     r.caps = ring_->desc;
     if (!send_locked(r, nullptr)) return false;
   }
-  if (!send_locked(m, offs.empty() ? nullptr : &offs)) return false;
+  if (!send_locked(m, offs.empty() ? nullptr : &offs, shm)) return false;
   if (!offs.empty())
-    for (auto o : offs) ipc_sent_ += o != kInline;
+    for (auto o : offs) (shm ? shm_sent_ : ipc_sent_) += o != kInline;
   return true;
 }
 
-bool Connection::send_locked(const Message& m, const std::vector<uint64_t>* offs) {
+bool Connection::send_locked(const Message& m, const std::vector<uint64_t>* offs, bool shm) {
+  const uint32_t flags = m.flags & ~(kFlagIpc | kFlagShm);
   WireHeader h{kMagic, kVersion, static_cast<uint32_t>(m.type), static_cast<uint32_t>(m.blobs.size()),
                m.client_id, m.seq, m.pts, m.dts, m.duration, static_cast<uint32_t>(m.caps.size()),
-               offs ? (m.flags | kFlagIpc) : (m.flags & ~kFlagIpc)};
+               offs ? (flags | (shm ? kFlagShm : kFlagIpc)) : flags};
   std::vector<uint64_t> sizes;
   std::vector<const void*> ptrs;
   for (size_t i = 0; i < m.blobs.size(); ++i) {
@@ -440,10 +499,11 @@ bool Connection::recv(Message* m, int timeout_ms, bool* timed_out) {
     m->pts = h.pts;
     m->dts = h.dts;
     m->duration = h.duration;
-    m->flags = h.flags & ~kFlagIpc;
+    m->flags = h.flags & ~(kFlagIpc | kFlagShm);
     std::vector<uint64_t> sizes(h.nblobs), offs;
     if (h.nblobs && !read_all(sizes.data(), sizes.size() * sizeof(uint64_t), -1, nullptr)) return false;
-    if (h.flags & kFlagIpc) {
+    const bool shm = (h.flags & kFlagShm) != 0;
+    if (h.flags & (kFlagIpc | kFlagShm)) {
       offs.resize(h.nblobs);
       if (h.nblobs && !read_all(offs.data(), offs.size() * sizeof(uint64_t), -1, nullptr)) return false;
     }
@@ -452,6 +512,34 @@ bool Connection::recv(Message* m, int timeout_ms, bool* timed_out) {
     m->blobs.clear();
     for (size_t i = 0; i < sizes.size(); ++i) {
       const uint64_t sz = sizes[i];
+      if (shm && offs[i] != kInline) {
+        const uint64_t ref = offs[i];
+        std::shared_ptr<ShmSegment> seg;
+        {
+          std::lock_guard<std::mutex> lk(shm_mu_);
+          auto it = shm_peer_.find(static_cast<uint32_t>(ref >> 48));
+          if (it != shm_peer_.end()) seg = std::static_pointer_cast<ShmSegment>(it->second);
+        }
+        const uint64_t off = ref & ((1ull << 48) - 1);
+        if (!seg || off + sz > seg->size()) {
+          NNSX_LOGE("comm", "shared-memory blob outside a mapped segment from ", peer_);
+          alive_ = false;
+          return false;
+        }
+        std::weak_ptr<Connection> w = self_;
+        // zero-copy: downstream reads the producer's frame in place; releasing it hands it back
+        m->blobs.push_back(seg->view(off, sz, [w, ref, sz](Memory*) {
+          if (auto c = w.lock()) {
+            Message a;
+            a.type = MsgType::SHM_ACK;
+            a.seq = ref;
+            a.duration = static_cast<int64_t>(sz);
+            (void)c->send(a);
+          }
+        }));
+        ++shm_recv_;
+        continue;
+      }
       if (!offs.empty() && offs[i] != kInline) {
         auto pr = peer_ring_;
         if (!pr || offs[i] + sz > pr->size) {
@@ -473,7 +561,8 @@ bool Connection::recv(Message* m, int timeout_ms, bool* timed_out) {
       if (sz && !read_all(mem->data(), sz, -1, nullptr)) return false;
       m->blobs.push_back(mem);
     }
-    if (m->type == MsgType::IPC_HELLO || m->type == MsgType::IPC_RING || m->type == MsgType::IPC_ACK) {
+    if (m->type == MsgType::IPC_HELLO || m->type == MsgType::IPC_RING || m->type == MsgType::IPC_ACK ||
+        m->type == MsgType::SHM_HELLO || m->type == MsgType::SHM_SEG || m->type == MsgType::SHM_ACK) {
       if (!handle_control(*m)) {
         alive_ = false;
         return false;
@@ -489,6 +578,10 @@ void Connection::shutdown() {
 }
 
 void Connection::close() {
+  {
+    std::lock_guard<std::mutex> lk(shm_mu_);
+    shm_held_.clear();  // (the peer can no longer release them)
+  }
   bool was = alive_.exchange(false);
   if (fd_ >= 0) {
     if (was) ::shutdown(fd_, SHUT_RDWR);

@@ -28,6 +28,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -43,6 +44,9 @@ enum class MsgType : uint32_t {
   IPC_HELLO = 7,  // caps: "boot=<id>;pid=<n>" -- the sender can receive ring blobs
   IPC_RING = 8,   // caps: ring description (handle, size, PCI bus id); precedes its first use
   IPC_ACK = 9,    // seq = ring offset, duration = bytes: the receiver released a slot
+  SHM_HELLO = 10,  // caps: "boot=<id>": the sender maps shared-memory segments of this host
+  SHM_SEG = 11,    // caps: "id=<n>;name=<shm path>;size=<bytes>": a segment, before its first blob
+  SHM_ACK = 12,    // seq = blob reference: the receiver released a shared-memory blob
 };
 
 struct IpcRing;      // transport.cc
@@ -89,13 +93,27 @@ class Connection {
   uint64_t ipc_blobs_sent() const { return ipc_sent_.load(); }
   uint64_t ipc_blobs_received() const { return ipc_recv_.load(); }
 
+  // same-host shared memory (connect-type=SHM): announce that this end maps the
+  // peer's POSIX shared-memory segments (comm/shm.h).  The peer then sends a
+  // host blob that lies in one of its segments as a reference (segment, offset)
+  // instead of its bytes and holds the blob until this end releases it
+  bool send_shm_hello();
+  bool peer_shm() const { return peer_shm_.load(); }
+  uint64_t shm_blobs_sent() const { return shm_sent_.load(); }
+  uint64_t shm_blobs_received() const { return shm_recv_.load(); }
+
  private:
-  bool send_locked(const Message& m, const std::vector<uint64_t>* offsets);
+  bool send_locked(const Message& m, const std::vector<uint64_t>* offsets, bool shm = false);
   bool handle_control(const Message& m);  // IPC_* messages, consumed inside recv()
   void send_ack(uint64_t off, uint64_t bytes);
   std::weak_ptr<Connection> self_;  // for the ACK-on-release closures
   friend std::shared_ptr<Connection> make_connection(int fd, std::string peer);
-  std::atomic<bool> peer_ipc_{false}, hello_sent_{false};
+  std::atomic<bool> peer_ipc_{false}, hello_sent_{false}, peer_shm_{false};
+  std::atomic<uint64_t> shm_sent_{0}, shm_recv_{0};
+  std::mutex shm_mu_;
+  std::map<std::string, uint32_t> shm_ids_;              // sender: our segments announced to the peer
+  std::multimap<uint64_t, MemoryPtr> shm_held_;          // sender: blobs the peer still reads
+  std::map<uint32_t, std::shared_ptr<void>> shm_peer_;   // receiver: the peer's segments, mapped
   std::atomic<uint64_t> ipc_sent_{0}, ipc_recv_{0};
   size_t ring_bytes_ = 0;
   std::shared_ptr<IpcRing> ring_;      // ours (sending side)

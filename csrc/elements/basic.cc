@@ -11,6 +11,7 @@
 #include <fstream>
 #include <random>
 
+#include "comm/shm.h"
 #include "core/log.h"
 #include "elements/elements.h"
 #include "runtime/base.h"
@@ -562,6 +563,9 @@ class VideoTestSrc : public BaseSrc {
     prop_uint("foreground-color", &fg_, "Foreground color to use (big-endian ARGB)");
     prop_uint("background-color", &bg_, "Background color to use (big-endian ARGB)");
     prop_int("pool-size", &pool_size_, "Number of distinct pre-rendered frames cycled for animated patterns (nnsx)");
+    prop_string("pool-shm", &pool_shm_,
+                "nnsx: render the frame ring into this named POSIX shared-memory segment, so edgesink "
+                "connect-type=SHM hands frames to other processes by reference ('' = private pinned memory)");
   }
 
  protected:
@@ -589,7 +593,19 @@ class VideoTestSrc : public BaseSrc {
     // one pinned block holds the whole ring (a camera's mmap'ed capture ring):
     // consecutive frames are adjacent, so a batching consumer uploads a run of
     // them with one DMA copy
-    ring_ = Memory::alloc_pinned(static_cast<size_t>(n) * info_.size);
+    if (!pool_shm_.empty()) {
+      // the ring in shared memory: consumers in other processes map it and
+      // DMA their frames over their own GPU's link (comm/shm.h)
+      std::string err;
+      shm_ = comm::ShmSegment::create(pool_shm_, static_cast<size_t>(n) * info_.size, &err);
+      if (!shm_) {
+        post_error("videotestsrc: pool-shm: " + err);
+        return false;
+      }
+      ring_ = shm_->view(0, static_cast<size_t>(n) * info_.size);
+    } else {
+      ring_ = Memory::alloc_pinned(static_cast<size_t>(n) * info_.size);
+    }
     for (int64_t i = 0; i < n; ++i)
       frames_[static_cast<size_t>(i)] = Memory::view(ring_, static_cast<size_t>(i) * info_.size, info_.size);
     const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
@@ -722,6 +738,8 @@ class VideoTestSrc : public BaseSrc {
   int pattern_ = 0;
   unsigned fg_ = 0xffffffff, bg_ = 0xff000000;
   int64_t pool_size_ = 8;
+  std::string pool_shm_;
+  std::shared_ptr<comm::ShmSegment> shm_;
   VideoInfo info_;
   std::vector<MemoryPtr> frames_;
   MemoryPtr ring_;

@@ -40,9 +40,12 @@ namespace nnsx {
 
 namespace {
 
-const std::vector<std::string> kConnectTypes = {"TCP", "HYBRID", "MQTT", "AITT", "HIPIPC", "RCCL"};
+const std::vector<std::string> kConnectTypes = {"TCP", "HYBRID", "MQTT", "AITT", "HIPIPC", "RCCL", "SHM"};
 constexpr int kHipIpc = 4;
 constexpr int kRccl = 5;
+// same-host processes: TCP carries the headers, host frames that live in a
+// shared-memory segment (videotestsrc pool-shm) travel by reference (comm/shm.h)
+constexpr int kShm = 6;
 const std::vector<std::string> kRcclModes = {"broadcast", "scatter", "allgather"};
 constexpr int kRcclAllGather = 2;
 constexpr uint32_t kPktCaps = 1;  // packet carries only a caps string
@@ -56,9 +59,10 @@ bool via_broker(int type) { return type == kMqtt || type == kAitt; }
 
 bool check_connect_type(Element* e, int type, bool pubsub = false) {
   if (type == 0 || type == kHybrid || type == kHipIpc || type == kRccl) return true;
+  if (pubsub && type == kShm) return true;
   if (pubsub && via_broker(type)) return true;
   e->post_error("connect-type " + kConnectTypes[static_cast<size_t>(type)] + " is not supported by " + e->name() +
-                (pubsub ? " (nnsx implements TCP, HYBRID, MQTT, AITT, HIPIPC and RCCL)"
+                (pubsub ? " (nnsx implements TCP, HYBRID, MQTT, AITT, HIPIPC, RCCL and SHM)"
                         : " (nnsx implements TCP, HYBRID, HIPIPC and RCCL; MQTT / AITT are pub/sub: edgesink / edgesrc)"));
   return false;
 }
@@ -1202,6 +1206,8 @@ class EdgeSrc : public BaseSrc {
     prop_int("device", &device_, "nnsx: upload received tensors to this GPU (-1 = pinned host memory)");
     prop_readonly("ipc-blobs", [this] { return std::to_string(conn_ ? conn_->ipc_blobs_received() : 0); },
                   "nnsx: tensors received through the HIPIPC device ring");
+    prop_readonly("shm-blobs", [this] { return std::to_string(conn_ ? conn_->shm_blobs_received() : 0); },
+                  "nnsx: tensors received by reference into the publisher's shared memory (connect-type=SHM)");
     rp_.install([this](PropSpec p) -> PropSpec& { return add_prop(p); }, false);
     prop_enum("rccl-mode", &rccl_mode_, kRcclModes, "nnsx (connect-type=RCCL): must match the publishing edgesink");
     prop_readonly("comm-bytes", [this] { return std::to_string(g_ ? g_->bytes_received() : 0); },
@@ -1333,6 +1339,7 @@ class EdgeSrc : public BaseSrc {
         return false;
       }
       if (m.type == comm::MsgType::HELLO && connect_type_ == kHipIpc) conn_->send_ipc_hello();
+      if (m.type == comm::MsgType::HELLO && connect_type_ == kShm) conn_->send_shm_hello();
       if ((m.type == comm::MsgType::HELLO || m.type == comm::MsgType::CAPS) && !m.caps.empty()) caps_str_ = m.caps;
       if (m.type == comm::MsgType::EOS) return false;
     }

@@ -494,9 +494,14 @@ class TensorConverter : public Element {
     auto stg = stage_alloc(spacing * (ps.size() - 1) + sf, dev, s);
     char* sp = static_cast<char*>(stg->data());
     // (splitting the upload over 2-4 copy streams did not help: profiles/r4_upload_bench.txt)
+    // (a run never spans two allocations: frames of separate pinned blocks can
+    // be adjacent in virtual memory, and a copy across them fails HIP's bounds
+    // check on the source allocation)
     for (size_t i = 0; i < ps.size();) {
       size_t j = i + 1;
-      while (j < ps.size() && at(j) == at(i) + (j - i) * spacing) ++j;
+      while (j < ps.size() && at(j) == at(i) + (j - i) * spacing &&
+             ps[j]->mem->allocation() == ps[i]->mem->allocation())
+        ++j;
       hip::check(hipMemcpyAsync(sp + i * spacing, at(i), spacing * (j - i - 1) + sf, hipMemcpyHostToDevice, s),
                  "padded DMA");
       i = j;

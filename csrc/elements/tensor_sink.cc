@@ -9,6 +9,8 @@
 #include <mutex>
 #include <vector>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "elements/elements.h"
 #include "elements/tensor_common.h"
 #include "runtime/base.h"
@@ -29,6 +31,21 @@ class TensorSink : public BaseSink {
     prop_bool("sync-device", &sync_device_, "nnsx: wait until device-resident payloads are produced before signalling");
     prop_readonly("frames", [this] { return std::to_string(frames_.load()); }, "nnsx: number of rendered frames");
     prop_uint("stats-every", &stats_every_, "nnsx: record every N-th buffer's arrival time and latency (0 = off)");
+    PropSpec mk;
+    mk.name = "roctx-marks";
+    mk.blurb = "nnsx: comma-separated buffer counts at whose arrival a roctx mark 'nnsx:<name>:<count>' is emitted "
+               "(profilers window their kernel statistics to a timed region with them)";
+    mk.set = [this](const std::string& v) {
+      marks_.clear();
+      for (auto& t : split(v, ','))
+        if (!strip(t).empty()) marks_.push_back(std::stoll(strip(t)));
+    };
+    mk.get = [this] {
+      std::string r;
+      for (int64_t m : marks_) r += (r.empty() ? "" : ",") + std::to_string(m);
+      return r;
+    };
+    add_prop(mk);
     prop_readonly(
         "stats",
         [this] {
@@ -63,6 +80,8 @@ class TensorSink : public BaseSink {
     if (sync_device_)
       for (auto& m : buf->mems) m->sync_ready();
     const int64_t n = ++frames_;
+    for (int64_t m : marks_)
+      if (m == n) roctxMarkA(strfmt("nnsx:", name(), ":", n).c_str());
     if (stats_every_ > 0 && n % stats_every_ == 0) {
       const int64_t lat = buf->pts >= 0 ? running_time() - buf->pts : -1;
       std::lock_guard<std::mutex> lk(stats_mu_);
@@ -89,6 +108,7 @@ class TensorSink : public BaseSink {
   int64_t last_emit_ = -1;
   std::atomic<int64_t> frames_{0};
   unsigned stats_every_ = 0;
+  std::vector<int64_t> marks_;  // roctx-marks
   std::mutex stats_mu_;
   std::vector<std::pair<int64_t, int64_t>> stats_;
   Caps caps_;

@@ -47,6 +47,10 @@
 
 namespace nnsx {
 
+namespace ops {
+void x3_retire_flush();  // ops/torch_ops.cc
+}  // namespace ops
+
 namespace {
 
 std::vector<int64_t> torch_sizes(const TensorInfo& ti, int rank_override) {
@@ -856,6 +860,7 @@ class TorchInstance : public FilterInstance {
   std::set<std::string> warmed_;                   // input shapes run eagerly before a capture
   void clear_graphs() {
     graphs_.clear();
+    ops::x3_retire_flush();  // (x3 weight parts the dropped graphs baked in: ops/torch_ops.cc)
     for (Lane& l : lanes_) l.pool = {0, 0};  // a pool goes with its last graph
     in_place_count_.clear();
     warmed_.clear();  // a reloaded module runs eagerly again before its first capture

@@ -32,19 +32,26 @@
 // fp64 is gated by tests/test_gpu_x3.py.
 #include "kernels/irw_common.h"
 
+#include <atomic>
+#include <cstdlib>
+
 namespace nnsx {
 namespace kernels {
 
 namespace {
 
 constexpr int kIrpH = 14;           // map size handled (S = 1)
-constexpr int kIrpWaves = 7;        // two image rows per wave
-constexpr int kIrpNT = 64 * kIrpWaves;
 constexpr int kIrpRow = 16;         // hidden grid row pitch (cells): 14 + 2 border
 constexpr int kIrpCells = 16 * kIrpRow + 16;  // + one scratch row for the padding lanes
 
-template <int CIN, int COUT>
+// TPW = 16-pixel MFMA tiles per wave: 2 -> 7 waves, a wave owns a row pair and
+// its lanes hold horizontal pixel pairs (the depthwise reads one 3 x 4 window
+// for both); 1 -> 14 waves, a wave owns one column parity of a row pair (half
+// the input fragments and accumulators per wave: the 96-channel blocks fit
+// four waves per SIMD without spilling)
+template <int CIN, int COUT, int TPW, bool XL = false>
 struct IrpGeom {
+  static constexpr int NW = 14 / TPW, NT = 64 * NW;
   static constexpr int NK32 = CIN / 32;        // expand k-steps
   static constexpr int NO16 = COUT / 16;       // project output tiles
   static constexpr int WEP = CIN / 8 + 1;      // expand weight row pitch (16-B chunks): odd -> conflict-free
@@ -54,38 +61,47 @@ struct IrpGeom {
   static constexpr size_t wp_b = static_cast<size_t>(3) * COUT * WPP * 16;      // [part][cout row][chunk]
   static constexpr size_t wd_b = static_cast<size_t>(10) * 32 * 4;              // [tap | bias][ch] f32
   static constexpr size_t be_b = static_cast<size_t>(32) * 4;
-  static constexpr size_t lds = hid_b + we_b + wp_b + wd_b + be_b;
+  // XL: the input image in LDS, fp32, pixel rows padded to CIN + 4 floats (a
+  // 16-lane fragment read then hits 16 distinct bank quads), read and split per
+  // step instead of held split in registers (the 96-channel blocks' registers)
+  static constexpr int XP = CIN + 4;
+  static constexpr size_t x_b = XL ? static_cast<size_t>(kIrpH * kIrpH) * XP * 4 : 0;
+  static constexpr size_t lds = hid_b + we_b + wp_b + wd_b + be_b + x_b;
   // 16-B chunks staged per step
   static constexpr int WE_CH = 3 * 32 * (CIN / 8) + 8;   // + expand bias (32 f32)
   static constexpr int WP_CH = 3 * COUT * 4 + 80;         // + depthwise taps and bias (10 x 32 f32)
-  static constexpr int WE_IT = (WE_CH + kIrpNT - 1) / kIrpNT;
-  static constexpr int WP_IT = (WP_CH + kIrpNT - 1) / kIrpNT;
+  static constexpr int WE_IT = (WE_CH + NT - 1) / NT;
+  static constexpr int WP_IT = (WP_CH + NT - 1) / NT;
+  static constexpr int MINW = TPW == 2 ? 2 : 4;  // waves per SIMD the registers are sized for
 };
 
-template <int CIN, int COUT>
-__global__ void __launch_bounds__(kIrpNT, 2) irp_x3_kernel(IrBlockF32Args a) {
-  using G = IrpGeom<CIN, COUT>;
-  constexpr int NK32 = G::NK32, NO16 = G::NO16, WEP = G::WEP, WPP = G::WPP;
+template <int CIN, int COUT, int TPW, bool XL>
+__global__ void __launch_bounds__((IrpGeom<CIN, COUT, TPW, XL>::NT), (IrpGeom<CIN, COUT, TPW, XL>::MINW))
+    irp_x3_kernel(IrBlockF32Args a) {
+  using G = IrpGeom<CIN, COUT, TPW, XL>;
+  constexpr int NK32 = G::NK32, NO16 = G::NO16, WEP = G::WEP, WPP = G::WPP, NT = G::NT;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   f32x4_t* hb = reinterpret_cast<f32x4_t*>(smem);                                   // [8][kIrpCells]
   char* wel = reinterpret_cast<char*>(smem) + G::hid_b;                              // expand weights
   char* wpl = wel + G::we_b;                                                         // project weights
   float* wdl = reinterpret_cast<float*>(wpl + G::wp_b);                              // [10][32]
   float* bel = wdl + 320;                                                            // [32]
+  float* xl = bel + 32;                                                              // XL: [196][XP]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, g = lane >> 4;
   const int b = blockIdx.x;
   const int hid = a.hid, nsteps = hid / 32;
-  const int r0 = 2 * wave;
-  // this lane's pixel slot (both tiles: columns x0 and x0 + 1 of row y)
+  const int r0 = 2 * (TPW == 2 ? wave : wave >> 1);
+  const int par = TPW == 2 ? 0 : (wave & 1);  // column parity of tile 0
+  // this lane's pixel slot: row y, columns x0 + par + t (t < TPW)
   const bool real = li < 14;
   const int y = r0 + (li >= 7 ? 1 : 0);
   const int x0 = 2 * (li >= 7 ? li - 7 : li);
   const int ys = real ? y : r0, x0s = real ? x0 : 0;  // (padding lanes read a valid window)
 
   // ---- zero the hidden image (its border is the depthwise padding) ----
-  for (int v = tid; v < 8 * kIrpCells; v += kIrpNT) hb[v] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (int v = tid; v < 8 * kIrpCells; v += NT) hb[v] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   // ---- weight staging (16-B chunks through registers) ----
   const int64_t wes = static_cast<int64_t>(hid) * CIN;     // we3 part stride (elements)
@@ -94,7 +110,7 @@ __global__ void __launch_bounds__(kIrpNT, 2) irp_x3_kernel(IrBlockF32Args a) {
   auto we_load = [&](int s) {
 #pragma unroll
     for (int it = 0; it < G::WE_IT; ++it) {
-      const int v = tid + it * kIrpNT;
+      const int v = tid + it * NT;
       if (v >= G::WE_CH) break;
       if (v < G::WE_CH - 8) {
         const int p = v / (32 * (CIN / 8)), r = v - p * 32 * (CIN / 8);
@@ -108,7 +124,7 @@ __global__ void __launch_bounds__(kIrpNT, 2) irp_x3_kernel(IrBlockF32Args a) {
   auto we_store = [&]() {
 #pragma unroll
     for (int it = 0; it < G::WE_IT; ++it) {
-      const int v = tid + it * kIrpNT;
+      const int v = tid + it * NT;
       if (v >= G::WE_CH) break;
       if (v < G::WE_CH - 8) {
         const int p = v / (32 * (CIN / 8)), r = v - p * 32 * (CIN / 8);
@@ -122,7 +138,7 @@ __global__ void __launch_bounds__(kIrpNT, 2) irp_x3_kernel(IrBlockF32Args a) {
   auto wp_load = [&](int s) {
 #pragma unroll
     for (int it = 0; it < G::WP_IT; ++it) {
-      const int v = tid + it * kIrpNT;
+      const int v = tid + it * NT;
       if (v >= G::WP_CH) break;
       if (v < G::WP_CH - 80) {
         const int p = v / (COUT * 4), r = v - p * COUT * 4;
@@ -137,7 +153,7 @@ __global__ void __launch_bounds__(kIrpNT, 2) irp_x3_kernel(IrBlockF32Args a) {
   auto wp_store = [&]() {
 #pragma unroll
     for (int it = 0; it < G::WP_IT; ++it) {
-      const int v = tid + it * kIrpNT;
+      const int v = tid + it * NT;
       if (v >= G::WP_CH) break;
       if (v < G::WP_CH - 80) {
         const int p = v / (COUT * 4), r = v - p * COUT * 4;
@@ -153,12 +169,18 @@ __global__ void __launch_bounds__(kIrpNT, 2) irp_x3_kernel(IrBlockF32Args a) {
   wp_load(0);
 
   // ---- the wave's input pixels, split once: B fragments of every expand ----
-  X3Frag xin[2][NK32];
-  {
-    const float* xb = a.x + static_cast<int64_t>(b) * kIrpH * kIrpH * CIN;
+  X3Frag xin[XL ? 1 : TPW][XL ? 1 : NK32];
+  const float* xb = a.x + static_cast<int64_t>(b) * kIrpH * kIrpH * CIN;
+  if constexpr (XL) {
+    // the image into LDS (16-B chunks; rows padded to XP floats)
+    for (int v = tid; v < kIrpH * kIrpH * (CIN / 4); v += NT) {
+      const int px = v / (CIN / 4), q = v - px * (CIN / 4);
+      *reinterpret_cast<f32x4_t*>(xl + px * G::XP + 4 * q) = *reinterpret_cast<const f32x4_t*>(xb + px * CIN + 4 * q);
+    }
+  } else {
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int64_t off = (static_cast<int64_t>(ys) * kIrpH + x0s + t) * CIN + 8 * g;
+    for (int t = 0; t < TPW; ++t) {
+      const int64_t off = (static_cast<int64_t>(ys) * kIrpH + x0s + par + t) * CIN + 8 * g;
 #pragma unroll
       for (int c = 0; c < NK32; ++c) {
         f32x4_t lo = *reinterpret_cast<const f32x4_t*>(xb + off + 32 * c);
@@ -168,21 +190,34 @@ __global__ void __launch_bounds__(kIrpNT, 2) irp_x3_kernel(IrBlockF32Args a) {
       }
     }
   }
+  // XL: this lane's fragment rows in the LDS image (tile t), zeros for the padding lanes
+  auto xfrag = [&](int t, int c) -> X3Frag {
+    if constexpr (XL) {
+      const float* r = xl + (ys * kIrpH + x0s + par + t) * G::XP + 32 * c + 8 * g;
+      f32x4_t lo = *reinterpret_cast<const f32x4_t*>(r);
+      f32x4_t hi = *reinterpret_cast<const f32x4_t*>(r + 4);
+      if (!real) lo = hi = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      return split_x3(lo, hi);
+    } else {
+      return xin[t][c];
+    }
+  };
   we_store();
   wp_store();
   __syncthreads();  // zeroed hidden image, step-0 weights
 
-  f32x4_t acc[2][NO16];
+  f32x4_t acc[TPW][NO16];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < TPW; ++t)
 #pragma unroll
     for (int o = 0; o < NO16; ++o) acc[t][o] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  // expand output cells of this lane (tile t: column x0 + t); padding lanes -> scratch row
-  const int ecell0 = real ? (y + 1) * kIrpRow + x0 + 1 : 16 * kIrpRow + li;
-  const int ecell1 = real ? ecell0 + 1 : 16 * kIrpRow + li;
-  // depthwise window origin: cell (ys - 1, x0s - 1) of the bordered grid = (ys) * row + x0s
-  const int wcell = ys * kIrpRow + x0s;
+  // expand output cell of this lane for tile t (column x0 + par + t); padding lanes -> scratch row
+  int ecell[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) ecell[t] = real ? (y + 1) * kIrpRow + x0 + par + t + 1 : 16 * kIrpRow + li;
+  // depthwise window origin: cell (ys - 1, x0s + par - 1) of the bordered grid
+  const int wcell = ys * kIrpRow + x0s + par;
 
   // Two barriers per step, single weight buffers: the project / depthwise
   // weights of step s are loaded at the start of its expand phase and stored at
@@ -193,60 +228,69 @@ __global__ void __launch_bounds__(kIrpNT, 2) irp_x3_kernel(IrBlockF32Args a) {
   for (int s = 0; s < nsteps; ++s) {
     if (s > 0) wp_load(s);
     // ================= expand (A: weights of hidden rows 16 ht + li) =================
-    f32x4_t e[2][2];
+    f32x4_t e[2][TPW];
 #pragma unroll
-    for (int ht = 0; ht < 2; ++ht) {
+    for (int ht = 0; ht < 2; ++ht)
 #pragma unroll
-      for (int t = 0; t < 2; ++t) e[ht][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int t = 0; t < TPW; ++t) e[ht][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int c = 0; c < NK32; ++c) {
+    for (int c = 0; c < NK32; ++c) {
+      X3Frag xf[TPW];
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) xf[t] = xfrag(t, c);
+#pragma unroll
+      for (int ht = 0; ht < 2; ++ht) {
         X3Frag wa;
         const char* wr = wel + ((ht * 16 + li) * WEP + 4 * c + g) * 16;
         wa.h = *reinterpret_cast<const bf16x8_t*>(wr);
         wa.m = *reinterpret_cast<const bf16x8_t*>(wr + 32 * WEP * 16);
         wa.l = *reinterpret_cast<const bf16x8_t*>(wr + 2 * 32 * WEP * 16);
 #pragma unroll
-        for (int t = 0; t < 2; ++t) e[ht][t] += mfma_x3(wa, xin[t][c]);
+        for (int t = 0; t < TPW; ++t) e[ht][t] += mfma_x3(wa, xf[t]);
       }
+      // (the 14-wave forms: one k-step's operands live at a time, else the
+      // scheduler hoists every step's LDS reads and spills past 128 VGPRs)
+      if constexpr (TPW == 1) __builtin_amdgcn_sched_barrier(0);
     }
     // bias + ReLU6 -> the shared hidden image (lane: pixel slot li, channels 16 ht + 4 g .. + 3)
 #pragma unroll
     for (int ht = 0; ht < 2; ++ht) {
       const f32x4_t be4 = *reinterpret_cast<const f32x4_t*>(bel + ht * 16 + 4 * g);
-      hb[(ht * 4 + g) * kIrpCells + ecell0] = relu6x4(e[ht][0] + be4);
-      hb[(ht * 4 + g) * kIrpCells + ecell1] = relu6x4(e[ht][1] + be4);
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) hb[(ht * 4 + g) * kIrpCells + ecell[t]] = relu6x4(e[ht][t] + be4);
     }
     if (s > 0) wp_store();
     __syncthreads();  // B1: hidden image and this step's project weights complete; wel free
     if (s + 1 < nsteps) we_load(s + 1);
 
-    // ================= depthwise 3 x 3 (+ bias, ReLU6): 2 pixels x 8 channels =================
-    f32x4_t d[2][2];  // [quad 2g + qq][pixel t]
+    // ================= depthwise 3 x 3 (+ bias, ReLU6): TPW pixels x 8 channels =================
+    f32x4_t d[2][TPW];  // [quad 2g + qq][pixel t]
 #pragma unroll
     for (int qq = 0; qq < 2; ++qq) {
       const int q = 2 * g + qq;
       const f32x4_t bd4 = *reinterpret_cast<const f32x4_t*>(wdl + 9 * 32 + 4 * q);
-      f32x4_t o0 = bd4, o1 = bd4;
+      f32x4_t o[TPW];
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) o[t] = bd4;
       const f32x4_t* hp = hb + q * kIrpCells + wcell;
 #pragma unroll
       for (int dy = 0; dy < 3; ++dy) {
-        const f32x4_t c0 = hp[dy * kIrpRow], c1 = hp[dy * kIrpRow + 1], c2 = hp[dy * kIrpRow + 2],
-                      c3 = hp[dy * kIrpRow + 3];
-        const f32x4_t w0 = *reinterpret_cast<const f32x4_t*>(wdl + (3 * dy) * 32 + 4 * q);
-        const f32x4_t w1 = *reinterpret_cast<const f32x4_t*>(wdl + (3 * dy + 1) * 32 + 4 * q);
-        const f32x4_t w2 = *reinterpret_cast<const f32x4_t*>(wdl + (3 * dy + 2) * 32 + 4 * q);
-        o0 = __builtin_elementwise_fma(c0, w0, o0);
-        o0 = __builtin_elementwise_fma(c1, w1, o0);
-        o0 = __builtin_elementwise_fma(c2, w2, o0);
-        o1 = __builtin_elementwise_fma(c1, w0, o1);
-        o1 = __builtin_elementwise_fma(c2, w1, o1);
-        o1 = __builtin_elementwise_fma(c3, w2, o1);
+        f32x4_t cc[TPW + 2];
+#pragma unroll
+        for (int j = 0; j < TPW + 2; ++j) cc[j] = hp[dy * kIrpRow + j];
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          const f32x4_t w = *reinterpret_cast<const f32x4_t*>(wdl + (3 * dy + dx) * 32 + 4 * q);
+#pragma unroll
+          for (int t = 0; t < TPW; ++t) o[t] = __builtin_elementwise_fma(cc[t + dx], w, o[t]);
+        }
       }
-      d[qq][0] = relu6x4(o0);
-      d[qq][1] = relu6x4(o1);
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) d[qq][t] = relu6x4(o[t]);
     }
-    const X3Frag bf0 = split_x3(d[0][0], d[1][0]);
-    const X3Frag bf1 = split_x3(d[0][1], d[1][1]);
+    X3Frag bf[TPW];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) bf[t] = split_x3(d[0][t], d[1][t]);
     // ================= project (A: weights of output rows 16 o + li, k = this step's 32) =================
 #pragma unroll
     for (int o = 0; o < NO16; ++o) {
@@ -255,8 +299,8 @@ __global__ void __launch_bounds__(kIrpNT, 2) irp_x3_kernel(IrBlockF32Args a) {
       wa.h = *reinterpret_cast<const bf16x8_t*>(wr);
       wa.m = *reinterpret_cast<const bf16x8_t*>(wr + COUT * WPP * 16);
       wa.l = *reinterpret_cast<const bf16x8_t*>(wr + 2 * COUT * WPP * 16);
-      acc[0][o] += mfma_x3(wa, bf0);
-      acc[1][o] += mfma_x3(wa, bf1);
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) acc[t][o] += mfma_x3(wa, bf[t]);
     }
     if (s + 1 < nsteps) we_store();
     __syncthreads();  // B2: the next expand weights complete; hb, wpl and wdl free
@@ -265,8 +309,280 @@ __global__ void __launch_bounds__(kIrpNT, 2) irp_x3_kernel(IrBlockF32Args a) {
   // ---- epilogue: + bias (+ residual) -> NHWC ----
   if (!real) return;
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int64_t pix = (static_cast<int64_t>(b) * kIrpH + y) * kIrpH + x0 + t;
+  for (int t = 0; t < TPW; ++t) {
+    const int64_t pix = (static_cast<int64_t>(b) * kIrpH + y) * kIrpH + x0 + par + t;
+#pragma unroll
+    for (int o = 0; o < NO16; ++o) {
+      const int co = o * 16 + 4 * g;
+      f32x4_t v = acc[t][o] + *reinterpret_cast<const f32x4_t*>(a.bp + co);
+      if (a.residual) {
+        if constexpr (XL)
+          v += *reinterpret_cast<const f32x4_t*>(xl + ((y * kIrpH) + x0 + par + t) * G::XP + co);
+        else
+          v += *reinterpret_cast<const f32x4_t*>(a.x + pix * CIN + co);
+      }
+      *reinterpret_cast<f32x4_t*>(a.y + pix * COUT + co) = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// irpp: the same block, software-pipelined over the hidden steps.  A 7-wave
+// workgroup at 200+ VGPRs (or a 14-wave one at 128) is ONE workgroup per CU,
+// so the LDS the second workgroup would have used is free: the hidden image
+// and both weight stages are double-buffered, and step s runs the expand of
+// step s + 1 (into hidden buffer (s + 1) & 1) next to the depthwise + project
+// of step s (from buffer s & 1) -- ONE barrier per step instead of two, and
+// half the waves (a.irp_order: wave bit 2) take the two phases in the other
+// order, so a SIMD's waves overlap one's MFMA expand with another's VALU / LDS
+// depthwise instead of the whole CU alternating between them.
+template <int CIN, int COUT, int TPW>
+struct IrppGeom {
+  static constexpr int NW = 14 / TPW, NT = 64 * NW;
+  static constexpr int NK32 = CIN / 32, NO16 = COUT / 16;
+  static constexpr int WEP = CIN / 8 + 1, WPP = 32 / 8 + 1;
+  static constexpr size_t hid1 = static_cast<size_t>(8) * kIrpCells * 16;
+  static constexpr size_t we_w = static_cast<size_t>(3) * 32 * WEP * 16;     // expand weights of a stage
+  static constexpr size_t we1 = we_w + 32 * 4;                               // + expand bias
+  static constexpr size_t wp_w = static_cast<size_t>(3) * COUT * WPP * 16;   // project weights of a stage
+  static constexpr size_t wp1 = wp_w + 10 * 32 * 4;                          // + depthwise taps and bias
+  static constexpr size_t lds = 2 * (hid1 + we1 + wp1);
+  static_assert(lds <= 160 * 1024, "irpp: LDS");
+  static constexpr int WE_CH = 3 * 32 * (CIN / 8) + 8;
+  static constexpr int WP_CH = 3 * COUT * 4 + 80;
+  static constexpr int WE_IT = (WE_CH + NT - 1) / NT;
+  static constexpr int WP_IT = (WP_CH + NT - 1) / NT;
+  static constexpr int MINW = TPW == 2 ? 2 : 4;
+};
+
+template <int CIN, int COUT, int TPW>
+__global__ void __launch_bounds__((IrppGeom<CIN, COUT, TPW>::NT), (IrppGeom<CIN, COUT, TPW>::MINW))
+    irpp_x3_kernel(IrBlockF32Args a) {
+  using G = IrppGeom<CIN, COUT, TPW>;
+  constexpr int NK32 = G::NK32, NO16 = G::NO16, WEP = G::WEP, WPP = G::WPP, NT = G::NT;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char* const base = reinterpret_cast<char*>(smem);
+  // [hidden 0][hidden 1][expand stage 0][expand stage 1][project stage 0][project stage 1]
+  auto hbuf = [&](int i) { return reinterpret_cast<f32x4_t*>(base + i * G::hid1); };
+  auto webuf = [&](int i) { return base + 2 * G::hid1 + i * G::we1; };
+  auto wpbuf = [&](int i) { return base + 2 * G::hid1 + 2 * G::we1 + i * G::wp1; };
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int b = blockIdx.x;
+  const int hid = a.hid, nsteps = hid / 32;
+  const int r0 = 2 * (TPW == 2 ? wave : wave >> 1);
+  const int par = TPW == 2 ? 0 : (wave & 1);
+  const bool real = li < 14;
+  const int y = r0 + (li >= 7 ? 1 : 0);
+  const int x0 = 2 * (li >= 7 ? li - 7 : li);
+  const int ys = real ? y : r0, x0s = real ? x0 : 0;
+  // phase order of this wave: 0 = expand first, 1 = depthwise + project first
+  const int late_e = a.irp_order == 0 ? 0 : (a.irp_order == 2 ? (wave & 1) : ((wave >> 2) & 1));
+
+  for (int v = tid; v < 2 * 8 * kIrpCells; v += NT) hbuf(0)[v] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t wes = static_cast<int64_t>(hid) * CIN;
+  const int64_t wps = static_cast<int64_t>(COUT) * hid;
+  u32x4_t we_st[G::WE_IT], wp_st[G::WP_IT];
+  auto we_load = [&](int s) {
+#pragma unroll
+    for (int it = 0; it < G::WE_IT; ++it) {
+      const int v = tid + it * NT;
+      if (v >= G::WE_CH) break;
+      if (v < G::WE_CH - 8) {
+        const int p = v / (32 * (CIN / 8)), r = v - p * 32 * (CIN / 8);
+        const int h = r / (CIN / 8), kc = r - h * (CIN / 8);
+        we_st[it] = *reinterpret_cast<const u32x4_t*>(a.we3 + p * wes + static_cast<int64_t>(32 * s + h) * CIN + kc * 8);
+      } else {
+        we_st[it] = *reinterpret_cast<const u32x4_t*>(a.be + 32 * s + 4 * (v - (G::WE_CH - 8)));
+      }
+    }
+  };
+  auto we_store = [&](int i) {
+    char* wel = webuf(i);
+#pragma unroll
+    for (int it = 0; it < G::WE_IT; ++it) {
+      const int v = tid + it * NT;
+      if (v >= G::WE_CH) break;
+      if (v < G::WE_CH - 8) {
+        const int p = v / (32 * (CIN / 8)), r = v - p * 32 * (CIN / 8);
+        const int h = r / (CIN / 8), kc = r - h * (CIN / 8);
+        *reinterpret_cast<u32x4_t*>(wel + ((p * 32 + h) * WEP + kc) * 16) = we_st[it];
+      } else {
+        *reinterpret_cast<u32x4_t*>(wel + G::we_w + 16 * (v - (G::WE_CH - 8))) = we_st[it];
+      }
+    }
+  };
+  auto wp_load = [&](int s) {
+#pragma unroll
+    for (int it = 0; it < G::WP_IT; ++it) {
+      const int v = tid + it * NT;
+      if (v >= G::WP_CH) break;
+      if (v < G::WP_CH - 80) {
+        const int p = v / (COUT * 4), r = v - p * COUT * 4;
+        const int co = r >> 2, kc = r & 3;
+        wp_st[it] = *reinterpret_cast<const u32x4_t*>(a.wp3 + p * wps + static_cast<int64_t>(co) * hid + 32 * s + kc * 8);
+      } else {
+        const int q = v - (G::WP_CH - 80), t = q >> 3, c4 = q & 7;
+        wp_st[it] = *reinterpret_cast<const u32x4_t*>((t < 9 ? a.wd + t * hid : a.bd) + 32 * s + 4 * c4);
+      }
+    }
+  };
+  auto wp_store = [&](int i) {
+    char* wpl = wpbuf(i);
+#pragma unroll
+    for (int it = 0; it < G::WP_IT; ++it) {
+      const int v = tid + it * NT;
+      if (v >= G::WP_CH) break;
+      if (v < G::WP_CH - 80) {
+        const int p = v / (COUT * 4), r = v - p * COUT * 4;
+        const int co = r >> 2, kc = r & 3;
+        *reinterpret_cast<u32x4_t*>(wpl + ((p * COUT + co) * WPP + kc) * 16) = wp_st[it];
+      } else {
+        *reinterpret_cast<u32x4_t*>(wpl + G::wp_w + 16 * (v - (G::WP_CH - 80))) = wp_st[it];
+      }
+    }
+  };
+
+  X3Frag xin[TPW][NK32];
+  const float* xb = a.x + static_cast<int64_t>(b) * kIrpH * kIrpH * CIN;
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int64_t off = (static_cast<int64_t>(ys) * kIrpH + x0s + par + t) * CIN + 8 * g;
+#pragma unroll
+    for (int c = 0; c < NK32; ++c) {
+      f32x4_t lo = *reinterpret_cast<const f32x4_t*>(xb + off + 32 * c);
+      f32x4_t hi = *reinterpret_cast<const f32x4_t*>(xb + off + 32 * c + 4);
+      if (!real) lo = hi = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      xin[t][c] = split_x3(lo, hi);
+    }
+  }
+  int ecell[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) ecell[t] = real ? (y + 1) * kIrpRow + x0 + par + t + 1 : 16 * kIrpRow + li;
+  const int wcell = ys * kIrpRow + x0s + par;
+
+  // expand of hidden step s: weights of stage s & 1 -> hidden buffer s & 1
+  auto expand = [&](int s) {
+    const char* wel = webuf(s & 1);
+    f32x4_t* hb = hbuf(s & 1);
+    f32x4_t e[2][TPW];
+#pragma unroll
+    for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) e[ht][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NK32; ++c) {
+#pragma unroll
+      for (int ht = 0; ht < 2; ++ht) {
+        X3Frag wa;
+        const char* wr = wel + ((ht * 16 + li) * WEP + 4 * c + g) * 16;
+        wa.h = *reinterpret_cast<const bf16x8_t*>(wr);
+        wa.m = *reinterpret_cast<const bf16x8_t*>(wr + 32 * WEP * 16);
+        wa.l = *reinterpret_cast<const bf16x8_t*>(wr + 2 * 32 * WEP * 16);
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) e[ht][t] += mfma_x3(wa, xin[t][c]);
+      }
+      if constexpr (TPW == 1) __builtin_amdgcn_sched_barrier(0);
+    }
+    const float* bel = reinterpret_cast<const float*>(wel + G::we_w);
+#pragma unroll
+    for (int ht = 0; ht < 2; ++ht) {
+      const f32x4_t be4 = *reinterpret_cast<const f32x4_t*>(bel + ht * 16 + 4 * g);
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) hb[(ht * 4 + g) * kIrpCells + ecell[t]] = relu6x4(e[ht][t] + be4);
+    }
+  };
+
+  f32x4_t acc[TPW][NO16];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t)
+#pragma unroll
+    for (int o = 0; o < NO16; ++o) acc[t][o] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // depthwise + project of hidden step s: hidden buffer s & 1, weights of stage s & 1
+  auto dwproj = [&](int s) {
+    const f32x4_t* hb = hbuf(s & 1);
+    const char* wpl = wpbuf(s & 1);
+    const float* wdl = reinterpret_cast<const float*>(wpl + G::wp_w);
+    f32x4_t d[2][TPW];
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      const int q = 2 * g + qq;
+      const f32x4_t bd4 = *reinterpret_cast<const f32x4_t*>(wdl + 9 * 32 + 4 * q);
+      f32x4_t o[TPW];
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) o[t] = bd4;
+      const f32x4_t* hp = hb + q * kIrpCells + wcell;
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy) {
+        f32x4_t cc[TPW + 2];
+#pragma unroll
+        for (int j = 0; j < TPW + 2; ++j) cc[j] = hp[dy * kIrpRow + j];
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          const f32x4_t w = *reinterpret_cast<const f32x4_t*>(wdl + (3 * dy + dx) * 32 + 4 * q);
+#pragma unroll
+          for (int t = 0; t < TPW; ++t) o[t] = __builtin_elementwise_fma(cc[t + dx], w, o[t]);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) d[qq][t] = relu6x4(o[t]);
+    }
+    X3Frag bf[TPW];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) bf[t] = split_x3(d[0][t], d[1][t]);
+#pragma unroll
+    for (int o = 0; o < NO16; ++o) {
+      X3Frag wa;
+      const char* wr = wpl + ((o * 16 + li) * WPP + g) * 16;
+      wa.h = *reinterpret_cast<const bf16x8_t*>(wr);
+      wa.m = *reinterpret_cast<const bf16x8_t*>(wr + COUT * WPP * 16);
+      wa.l = *reinterpret_cast<const bf16x8_t*>(wr + 2 * COUT * WPP * 16);
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) acc[t][o] += mfma_x3(wa, bf[t]);
+    }
+  };
+
+  // prologue: stage 0 (expand + project) and stage 1 (expand), the expand of step 0
+  we_load(0);
+  wp_load(0);
+  we_store(0);
+  wp_store(0);
+  if (nsteps > 1) {
+    we_load(1);
+    we_store(1);
+  }
+  __syncthreads();
+  expand(0);
+  __syncthreads();
+
+  // Step s: E(s + 1) -> hidden (s + 1) & 1 and D/P(s) <- hidden s & 1, in this
+  // wave's order; the stages loaded now (project s + 1, expand s + 2) go to
+  // buffers whose readers (D/P(s - 1), E(s)) finished before the last barrier,
+  // as did the readers of hidden (s + 1) & 1 (D/P(s - 1)).  One barrier.
+  for (int s = 0; s < nsteps; ++s) {
+    const bool more = s + 1 < nsteps, more2 = s + 2 < nsteps;
+    if (more) wp_load(s + 1);
+    if (more2) we_load(s + 2);
+#pragma nounroll
+    for (int ph = 0; ph < 2; ++ph) {
+      if (ph == late_e) {
+        if (more) expand(s + 1);
+      } else {
+        dwproj(s);
+      }
+    }
+    if (more) wp_store((s + 1) & 1);
+    if (more2) we_store(s & 1);
+    __syncthreads();
+  }
+
+  if (!real) return;
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int64_t pix = (static_cast<int64_t>(b) * kIrpH + y) * kIrpH + x0 + par + t;
 #pragma unroll
     for (int o = 0; o < NO16; ++o) {
       const int co = o * 16 + 4 * g;
@@ -278,20 +594,57 @@ __global__ void __launch_bounds__(kIrpNT, 2) irp_x3_kernel(IrBlockF32Args a) {
 }
 
 struct IrpCfg {
-  int cin, cout;
+  int cin, cout, tpw;
   void (*kernel)(IrBlockF32Args);
   size_t lds;
+  int threads;
+  bool xl, pipe;
 };
-#define NNSX_IRP(CI, CO) IrpCfg{CI, CO, &irp_x3_kernel<CI, CO>, IrpGeom<CI, CO>::lds}
-const IrpCfg kIrpCfgs[] = {NNSX_IRP(64, 64), NNSX_IRP(64, 96), NNSX_IRP(96, 96)};
+#define NNSX_IRP(CI, CO, T, XL) \
+  IrpCfg { CI, CO, T, &irp_x3_kernel<CI, CO, T, XL>, IrpGeom<CI, CO, T, XL>::lds, IrpGeom<CI, CO, T, XL>::NT, XL, false }
+#define NNSX_IRPP(CI, CO, T) \
+  IrpCfg { CI, CO, T, &irpp_x3_kernel<CI, CO, T>, IrppGeom<CI, CO, T>::lds, IrppGeom<CI, CO, T>::NT, false, true }
+// (first match per shape is the default; NNSX_IRP_TPW=1|2 picks that variant)
+// (batch 512, per block: 64 -> 384 -> 64 112.8 / 115.7 us with 2 / 1 tiles per
+// wave, 64 -> 384 -> 96 126.5 / 143.2, 96 -> 576 -> 96 309.2 / 264.8; the wave-split
+// kernels 145.0 / 188.0 / 318.4: profiles/r6_irp_layers_b512.txt)
+const IrpCfg kIrpCfgs[] = {NNSX_IRP(64, 64, 2, false),  NNSX_IRP(64, 96, 2, false),  NNSX_IRP(96, 96, 1, true),
+                           NNSX_IRP(96, 96, 1, false),  NNSX_IRP(64, 64, 1, false),  NNSX_IRP(64, 96, 1, false),
+                           NNSX_IRPP(64, 64, 2),        NNSX_IRPP(64, 96, 2),        NNSX_IRPP(96, 96, 2),
+                           NNSX_IRPP(64, 64, 1),        NNSX_IRPP(64, 96, 1),        NNSX_IRPP(96, 96, 1)};
 #undef NNSX_IRP
+#undef NNSX_IRPP
+
+std::atomic<int> g_irp_min_b{[] {
+  const char* e = std::getenv("NNSX_IRP_MIN_B");
+  return e && *e ? std::atoi(e) : 128;
+}()};
 
 const IrpCfg* find_irp(const IrBlockF32Args& a) {
+  // one workgroup per image: only batches that fill the chip (small batches keep
+  // the wave-split kernels, which spread an image's hidden channels over CUs)
+  const int min_b = g_irp_min_b.load(std::memory_order_relaxed);
   if (a.stride != 1 || a.dil != 1 || !a.has_expand || a.H != kIrpH || a.W != kIrpH || a.hid % 32 || !a.we3 ||
-      !a.wp3)
+      !a.wp3 || a.B < min_b)
     return nullptr;
+  // A/B: NNSX_IRP_TPW=1|2 picks that tile count, NNSX_IRP_XL=0|1 the input's place
+  static const int tpw = [] {
+    const char* e = std::getenv("NNSX_IRP_TPW");
+    return e && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : 0;
+  }();
+  static const int xl = [] {
+    const char* e = std::getenv("NNSX_IRP_XL");
+    return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
+  }();
+  // NNSX_IRP_PIPE=0|1: the two-barrier kernel / the pipelined one (irpp)
+  static const int pipe = [] {
+    const char* e = std::getenv("NNSX_IRP_PIPE");
+    return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
+  }();
   for (const IrpCfg& c : kIrpCfgs)
-    if (c.cin == a.cin && c.cout == a.cout) return &c;
+    if (c.cin == a.cin && c.cout == a.cout && (tpw == 0 || c.tpw == tpw) && (xl < 0 || c.xl == (xl == 1)) &&
+        (pipe < 0 || c.pipe == (pipe == 1)))
+      return &c;
   return nullptr;
 }
 
@@ -308,13 +661,23 @@ static bool irp_enabled() {
 
 bool irp_x3_supported(const IrBlockF32Args& a) { return irp_enabled() && find_irp(a) != nullptr; }
 
-bool irp_x3(const IrBlockF32Args& a, hipStream_t s) {
-  const IrpCfg* c = irp_enabled() ? find_irp(a) : nullptr;
+int irp_x3_set_min_batch(int b) { return g_irp_min_b.exchange(b); }
+
+bool irp_x3(const IrBlockF32Args& args, hipStream_t s) {
+  const IrpCfg* c = irp_enabled() ? find_irp(args) : nullptr;
   if (!c) return false;
+  IrBlockF32Args a = args;
+  // irpp phase order (NNSX_IRP_ORDER: 0 = every wave expand first, 1 = waves with
+  // bit 2 set depthwise + project first, 2 = odd waves)
+  static const int order = [] {
+    const char* e = std::getenv("NNSX_IRP_ORDER");
+    return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 1;
+  }();
+  a.irp_order = order;
   if (c->lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(c->kernel),
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
     return false;
-  hipLaunchKernelGGL(c->kernel, dim3(static_cast<unsigned>(a.B)), dim3(kIrpNT), c->lds, s, a);
+  hipLaunchKernelGGL(c->kernel, dim3(static_cast<unsigned>(a.B)), dim3(c->threads), c->lds, s, a);
   return true;
 }
 

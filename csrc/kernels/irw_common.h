@@ -40,6 +40,8 @@ const std::vector<IrwCfg>& x3_irw_cfgs();
 // needs a.we3 / a.wp3.  false: not this shape (or NNSX_IRP=0)
 bool irp_x3_supported(const IrBlockF32Args& a);
 bool irp_x3(const IrBlockF32Args& a, hipStream_t s);
+// smallest batch the image-per-workgroup kernels take (default 128, NNSX_IRP_MIN_B); returns the old value
+int irp_x3_set_min_batch(int b);
 
 namespace {
 

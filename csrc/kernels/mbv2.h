@@ -195,6 +195,7 @@ struct IrBlockF32Args {
   // the method x3: the irw_x3 kernel of the same geometry, when there is one
   const uint16_t* we3 = nullptr;
   const uint16_t* wp3 = nullptr;
+  int irp_order = 1;  // irpp_x3 phase order (kernels/irp_x3.hip)
 };
 // Launches enqueued by this thread while a SharedDeviceScope is alive may run
 // concurrently with other kernels of the same process (a filter's replay
@@ -253,6 +254,8 @@ bool ir_block_f32(const IrBlockF32Args& a, hipStream_t s);
 // which product method ir_block_f32 uses for this shape under the current
 // F32Math with x3 weights given: "x3", "fp32", or "" (unsupported)
 const char* ir_block_f32_method(int stride, int H, int W, int cin, int hid, int cout, int B, int dil = 1);
+// the 14 x 14 image-per-workgroup kernels' smallest batch (kernels/irp_x3.hip); returns the old value
+int irp_x3_set_min_batch(int b);
 
 }  // namespace kernels
 }  // namespace nnsx

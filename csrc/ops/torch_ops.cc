@@ -3,6 +3,7 @@
 // and hipGraph capture records them like any other kernel.  CPU
 // implementations are the fp32 numerics reference.
 #include <algorithm>
+#include <deque>
 #include <mutex>
 #include <unordered_map>
 #include <ATen/ATen.h>
@@ -39,6 +40,14 @@ struct X3Cached {
 std::mutex g_x3_mu;
 std::unordered_map<const void*, X3Cached> g_x3;
 bool g_x3_cache_on = true;
+// parts of replaced / evicted entries: a graph captured on a cache hit baked
+// in their address, so they stay alive until the graphs are cleared
+// (tensor_filter's clear_graphs -> x3_retire_flush; bounded for direct users)
+std::deque<at::Tensor> g_x3_retired;
+void x3_retire(at::Tensor parts) {
+  g_x3_retired.push_back(std::move(parts));
+  while (g_x3_retired.size() > 256) g_x3_retired.pop_front();
+}
 
 // tests: off = every x3 GEMM splits its weights per tile (the capture fallback)
 bool x3_weight_cache(bool on) {
@@ -62,7 +71,18 @@ nnsx::kernels::X3W x3_weights(const at::Tensor& wt) {
   hipStream_t s = cur_stream();
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return {};  // (per-tile split)
-  for (auto e = g_x3.begin(); e != g_x3.end();) e = e->second.src.use_count() == 1 ? g_x3.erase(e) : std::next(e);
+  if (it != g_x3.end()) {  // (in-place updated weights: their old parts)
+    x3_retire(std::move(it->second.parts));
+    g_x3.erase(it);
+  }
+  for (auto e = g_x3.begin(); e != g_x3.end();) {
+    if (e->second.src.use_count() == 1) {
+      x3_retire(std::move(e->second.parts));
+      e = g_x3.erase(e);
+    } else {
+      ++e;
+    }
+  }
   const int64_t rows = wt.size(0), cols = wt.size(1), stages = (cols + 31) / 32;
   X3Cached c;
   c.src = wt;
@@ -871,6 +891,17 @@ std::string set_f32_math(const std::string& m) {
 
 }  // namespace
 
+namespace nnsx {
+namespace ops {
+// tensor_filter (filter/pytorch.cc clear_graphs): no captured graph refers to
+// retired x3 weight parts any more
+void x3_retire_flush() {
+  std::lock_guard<std::mutex> lk(g_x3_mu);
+  g_x3_retired.clear();
+}
+}  // namespace ops
+}  // namespace nnsx
+
 TORCH_LIBRARY(nnsx, m) {
   m.def("f32_math() -> str", f32_math);
   m.def("set_device_shared(bool on) -> bool", set_device_shared);
@@ -878,6 +909,9 @@ TORCH_LIBRARY(nnsx, m) {
   m.def("ir_method_f32(int stride, int H, int W, int cin, int hid, int cout, int B, int dilation=1) -> str",
         ir_method_f32);
   m.def("set_f32_math(str method) -> str", set_f32_math);
+  m.def("irp_min_batch(int b) -> int", [](int64_t b) -> int64_t {
+    return nnsx::kernels::irp_x3_set_min_batch(static_cast<int>(b));
+  });
   m.def("pw_conv(Tensor x, Tensor wt, Tensor bias, Tensor? res, int N, int act, bool out_f32) -> Tensor");
   m.def("pw_conv_into(Tensor x, Tensor wt, Tensor bias, Tensor(a!) out, int row0, int n, int act) -> ()");
   m.def("pw_conv_rowbias(Tensor x, Tensor wt, Tensor bias, int N, int act) -> Tensor");

@@ -1,5 +1,6 @@
 #include "runtime/memory.h"
 
+#include <atomic>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -42,13 +43,29 @@ class DeferredRelease {
     void* data;
     size_t size;
     MemPlace place;
+    std::function<void()> fn;  // instead of a free: a wrapped memory's release (set_deferred_release)
   };
+  // backpressure: past this many queued blocks / bytes (the GPU has fallen
+  // behind its copies) the releasing thread frees the block itself, after the
+  // copies' events -- the pinned pool cannot grow without bound
+  static constexpr size_t kMaxItems = 256;
+  static constexpr size_t kMaxBytes = size_t{1} << 30;
   static DeferredRelease& get() {
-    static DeferredRelease* d = new DeferredRelease();  // (never destroyed: process-lifetime thread)
+    static DeferredRelease* d = [] {
+      auto* r = new DeferredRelease();  // (never destroyed: process-lifetime thread)
+      std::atexit([] { get().shutdown(); });
+      return r;
+    }();
     return *d;
   }
   void push(Item it) {
-    std::lock_guard<std::mutex> lk(mu_);
+    std::unique_lock<std::mutex> lk(mu_);
+    if (stopping_ || q_.size() >= kMaxItems || bytes_ + it.size > kMaxBytes) {
+      lk.unlock();
+      release(it);
+      return;
+    }
+    bytes_ += it.size;
     q_.push_back(std::move(it));
     ++queued_;
     cv_.notify_all();
@@ -58,10 +75,34 @@ class DeferredRelease {
     const uint64_t target = queued_;
     done_cv_.wait(lk, [&] { return done_ >= target; });
   }
+  // process exit (atexit, before the HIP runtime's own teardown): the queue is
+  // worked off -- bounded, the copies it waits for are already issued -- and
+  // later releases are done in place
+  void shutdown() {
+    std::unique_lock<std::mutex> lk(mu_);
+    stopping_ = true;
+    const uint64_t target = queued_;
+    done_cv_.wait_for(lk, std::chrono::seconds(5), [&] { return done_ >= target; });
+  }
 
  private:
   DeferredRelease() {
     std::thread([this] { run(); }).detach();
+  }
+  static void release(Item& it) {
+    for (auto& e : it.events) {
+      (void)hipEventSynchronize(e.second);
+      hip::event_put(e.first, e.second);
+    }
+    if (it.fn) {
+      it.fn();
+      return;
+    }
+    if (Memory::check_enabled() && it.size) poison_host(it.data, it.size);
+    if (it.place == MemPlace::PINNED)
+      hip::pinned_free(it.data, it.size);
+    else
+      hip::host_free(it.data);
   }
   void run() {
     for (;;) {
@@ -72,16 +113,9 @@ class DeferredRelease {
         it = std::move(q_.front());
         q_.pop_front();
       }
-      for (auto& e : it.events) {
-        (void)hipEventSynchronize(e.second);
-        hip::event_put(e.first, e.second);
-      }
-      if (Memory::check_enabled() && it.size) poison_host(it.data, it.size);
-      if (it.place == MemPlace::PINNED)
-        hip::pinned_free(it.data, it.size);
-      else
-        hip::host_free(it.data);
+      release(it);
       std::lock_guard<std::mutex> lk(mu_);
+      bytes_ -= it.size;
       ++done_;
       done_cv_.notify_all();
     }
@@ -90,6 +124,8 @@ class DeferredRelease {
   std::condition_variable cv_, done_cv_;
   std::deque<Item> q_;
   uint64_t queued_ = 0, done_ = 0;
+  size_t bytes_ = 0;
+  bool stopping_ = false;
 };
 
 }  // namespace
@@ -97,6 +133,13 @@ class DeferredRelease {
 void Memory::drain_deferred() {
   if (hip::available()) DeferredRelease::get().drain();
 }
+
+// lifetime self-test support (runtime/selftest.cc): undo one fix at run time so
+// the test that pins it can be shown to fail without it
+namespace {
+std::atomic<int> g_mutation{0};
+}  // namespace
+int Memory::set_test_mutation(int m) { return g_mutation.exchange(m); }
 
 Memory::Memory(void* data, size_t size, MemPlace place, int device, Release release)
     : data_(data), size_(size), place_(place), device_(device), release_(std::move(release)) {}
@@ -127,9 +170,19 @@ Memory::~Memory() {
     }
   } else {
     // other host memory (wrapped buffers with their own release) read by an
-    // asynchronous H2D copy: released only after that copy ran
-    if (place_ != MemPlace::DEVICE && !uses_.empty()) sync_uses();
-    if (release_) release_(this);
+    // asynchronous H2D copy: released only after that copy ran -- by the
+    // deferred-release thread when the release does not need this object
+    // (set_deferred_release: shared-memory frames handed back to their producer)
+    if (place_ != MemPlace::DEVICE && !uses_.empty() && defer_wrap_ && release_) {
+      std::vector<std::pair<int, hipEvent_t>> evs;
+      for (auto& u : uses_) evs.emplace_back(u.dev, u.event);
+      uses_.clear();
+      Release rel = std::move(release_);
+      DeferredRelease::get().push({std::move(evs), nullptr, 0, place_, [rel] { rel(nullptr); }});
+    } else {
+      if (place_ != MemPlace::DEVICE && !uses_.empty()) sync_uses();
+      if (release_) release_(this);
+    }
   }
   if (ready_) hip::event_put(ready_dev_, ready_);
   for (auto& u : uses_) hip::event_put(u.dev, u.event);
@@ -422,7 +475,7 @@ void Memory::record_use(hipStream_t stream, int dev) {
     auto it = dev_mirror_.find(dev);
     if (it != dev_mirror_.end()) mirror = it->second;
   }
-  if (mirror) mirror->record_use(stream, dev);
+  if (mirror && g_mutation.load() != kMutMirrorNotHeld) mirror->record_use(stream, dev);
   record_use_self(stream, dev);
 }
 
@@ -497,7 +550,7 @@ const void* Memory::map_device(int dev, hipStream_t stream) {
     // runtime's own staging): it must not be freed / recycled before the copy ran
     // (a pageable frame freed at once came back from malloc holding the next
     // frame, and the queued copy read that: test_hipgraph_static_outputs_...)
-    if (size_) record_use_self(stream, dev);
+    if (size_ && g_mutation.load() != kMutHostFreedEarly) record_use_self(stream, dev);
   }
   mirror->mark_ready(stream);
   dev_mirror_[dev] = mirror;

@@ -92,6 +92,18 @@ class Memory : public std::enable_shared_from_this<Memory> {
 
   Memory* root() { return parent_ ? parent_->root() : this; }
   const Memory* root() const { return parent_ ? parent_->root() : this; }
+  // the allocation this memory lies in (one copy may span several memories of
+  // the same allocation -- e.g. the frames of one capture ring): the root's
+  // own block unless set_allocation named a larger one (a shared segment)
+  const void* allocation() const {
+    const Memory* r = root();
+    return r->alloc_ ? r->alloc_ : r->data_;
+  }
+  void set_allocation(const void* a) { alloc_ = a; }
+  // wrapped memory whose release callback does not touch the Memory (it gets
+  // nullptr): after pending readers it runs on the deferred-release thread
+  // instead of blocking the thread that drops the last reference
+  void set_deferred_release() { defer_wrap_ = true; }
 
   // the device mirror of this memory on `dev` (map_device), if any
   MemoryPtr device_mirror(int dev);
@@ -104,6 +116,13 @@ class Memory : public std::enable_shared_from_this<Memory> {
   // destruction has begun throws.  Stale reads of a recycled block then read
   // NaNs (0x7FBADBAD as fp32) instead of plausible old data.
   static bool check_enabled();
+  // lifetime self-tests only: 0 none, kMutHostFreedEarly = a host source's
+  // async H2D is not recorded as a use (pageable: the fix of 7ba8684 undone;
+  // pinned: the rule it extended to pageable sources),
+  // kMutMirrorNotHeld = a reader of a host memory does not hold its device
+  // mirror (ee80b24 undone); returns the previous mutation
+  static constexpr int kMutHostFreedEarly = 1, kMutMirrorNotHeld = 2;
+  static int set_test_mutation(int m);
   static constexpr uint32_t kPoison = 0x7FBADBADu;
   // Wait until every deferred host / pinned release queued so far has run (tests).
   static void drain_deferred();
@@ -120,6 +139,8 @@ class Memory : public std::enable_shared_from_this<Memory> {
   MemPlace place_;
   int device_;
   Release release_;
+  const void* alloc_ = nullptr;  // set_allocation
+  bool defer_wrap_ = false;      // set_deferred_release
   MemoryPtr parent_;  // for views
   hipEvent_t ready_ = nullptr;
   int ready_dev_ = 0;

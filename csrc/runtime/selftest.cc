@@ -17,6 +17,9 @@
 //                      ordered only on the mapping stream)
 //   device_reader      a device block read on another stream while released
 //                      (the release waits for every recorded reader)
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -48,29 +51,48 @@ std::vector<uint8_t> d2h(const void* p, size_t n, hipStream_t s) {
 }
 
 // host frame (pageable or pinned) -> H2D on s behind a spin; the frame is
-// released at once, its storage reused for another frame; the mirror must hold
-// the first frame's bytes
-std::string host_h2d(int dev, bool pinned) {
+// released at once, its storage reused for other frames; the mirror must hold
+// the first frame's bytes.  Several sizes: malloc hands a freed small block
+// (below its mmap threshold) back at once, a large one through mmap; the HIP
+// runtime stages pageable copies differently by size.  NNSX_SELFTEST_VERBOSE=1
+// prints how long each map_device call blocked the host (a copy the runtime
+// completes inside the call cannot read a recycled frame).
+std::string host_h2d_one(int dev, bool pinned, size_t bytes) {
   hip::DeviceGuard g(dev);
   hipStream_t s = nullptr;
   hip::check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "selftest stream");
-  MemoryPtr h = pinned ? Memory::alloc_pinned(kBytes) : Memory::alloc_host(kBytes);
-  std::memset(h->data(), 0x11, kBytes);
+  MemoryPtr h = pinned ? Memory::alloc_pinned(bytes) : Memory::alloc_host(bytes);
+  std::memset(h->data(), 0x11, bytes);
   kernels::spin_us(s, kSpinUs);
+  const auto t0 = std::chrono::steady_clock::now();
   (void)h->map_device(dev, s);  // queued behind the spin
+  const double blocked_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   MemoryPtr mirror = h->device_mirror(dev);
   h.reset();  // the last reference: the copy has not run yet
   // the next frames take the freed storage (malloc / the pinned pool hand it out again)
   std::vector<MemoryPtr> next;
   for (int i = 0; i < 4; ++i) {
-    next.push_back(pinned ? Memory::alloc_pinned(kBytes) : Memory::alloc_host(kBytes));
-    std::memset(next.back()->data(), 0x22, kBytes);
+    next.push_back(pinned ? Memory::alloc_pinned(bytes) : Memory::alloc_host(bytes));
+    std::memset(next.back()->data(), 0x22, bytes);
   }
-  std::string r = check_bytes(d2h(mirror->data(), kBytes, s), 0x11, pinned ? "pinned_h2d" : "pageable_h2d");
+  const std::string what = std::string(pinned ? "pinned_h2d" : "pageable_h2d") + "[" + std::to_string(bytes) + " B]";
+  std::string r = check_bytes(d2h(mirror->data(), bytes, s), 0x11, what.c_str());
+  if (const char* v = std::getenv("NNSX_SELFTEST_VERBOSE"); v && v[0] == '1')
+    std::fprintf(stderr, "%s: map_device blocked the host %.3f ms (spin %d ms): %s\n", what.c_str(), blocked_ms,
+                 kSpinUs / 1000, r.empty() ? "bytes intact" : r.c_str());
   mirror.reset();
   next.clear();
   hip::check(hipStreamSynchronize(s), "selftest sync");
   (void)hipStreamDestroy(s);
+  return r;
+}
+
+std::string host_h2d(int dev, bool pinned) {
+  std::string r;
+  for (size_t bytes : {size_t(4) << 10, size_t(64) << 10, size_t(1) << 20, kBytes}) {
+    std::string e = host_h2d_one(dev, pinned, bytes);
+    if (!e.empty()) r += (r.empty() ? "" : "; ") + e;
+  }
   return r;
 }
 

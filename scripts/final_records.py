@@ -40,7 +40,7 @@ def kernel_stats(prof, title):
 shutil.copy(os.path.join(SRC, "bench_default.json"), os.path.join(DST, "r5_bench_mbv2_b512_fp32_1gpu.json"))
 # configs
 lines = [f"# configs 3-5 (and the multi-rank configs at N=1) at the target batches and at 512, HEAD {head} defaults, "
-         "1 x MI355X, fp32 (x3 products), bench.py --steps 100 --warmup 20 (scripts/gpu_r5_final.sh)"]
+         "1 x MI355X, fp32 (x3 products), bench.py --steps 100 --warmup 20 (scripts/gpu_drivers.sh gpu_r5_final)"]
 recs = []
 for f in sorted(glob.glob(os.path.join(SRC, "cfg_*.json"))):
     j = last_json(f)
@@ -63,6 +63,6 @@ for c in ("ssd_b64", "posenet_b64", "deeplab_b8"):
 shutil.copy(os.path.join(SRC, "layers_b512.txt"), os.path.join(DST, "r5_fp32_layers_b512.txt"))
 suite = [l for l in open(os.path.join(SRC, "gpu_suite.txt")).read().splitlines() if "amdgpu.ids" not in l]
 open(os.path.join(DST, f"r5_gpu_suite_{head}.txt"), "w").write(
-    f"# python -m pytest tests -m gpu -q --timeout 300 -x at HEAD {head}, 1 x MI355X (scripts/gpu_r5_final.sh)\n"
+    f"# python -m pytest tests -m gpu -q --timeout 300 -x at HEAD {head}, 1 x MI355X (scripts/gpu_drivers.sh gpu_r5_final)\n"
     + "\n".join(suite[-40:]) + "\n")
 print("records written for", head)

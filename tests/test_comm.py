@@ -145,3 +145,61 @@ def test_edge_pubsub_two_subscribers(nns):
         s.stop()
         assert [float(x[0]) for x in o] == [float(i) for i in range(6)]
     pub.stop()
+
+
+def test_edge_shm_frames_by_reference_across_processes(nns, tmp_path):
+    """connect-type=SHM: the publisher's camera ring lives in a POSIX shared
+    segment (videotestsrc pool-shm); frames reach a subscriber in ANOTHER
+    process as references into that segment (zero-copy: shm-blobs counts them),
+    byte-identical to the camera's, and every frame is handed back (the
+    publisher's pipeline finishes).  On a GPU the subscriber's mapping is
+    hipHostRegister'ed, so its own tensor_converter DMAs the frames over its
+    GPU's link (tests/test_gpu_shm_ingest.py).  Reference fan-out this
+    replaces across processes: gsttensor_demux.c:469-556 (buffers by reference)."""
+    import os
+
+    name = f"nnsx-test-{os.getpid()}"
+    script = tmp_path / "pub.py"
+    script.write_text(textwrap.dedent(f"""
+        import sys, time
+        sys.path.insert(0, {ROOT!r})
+        import nnstreamer_amd as nns
+        p = nns.parse_launch("videotestsrc num-buffers=24 pattern=snow pool-size=6 pool-shm={name} "
+                             "! video/x-raw,format=RGB,width=64,height=48,framerate=0/1 "
+                             "! edgesink name=es port=0 connect-type=SHM wait-connection=1")
+        p.set_state("playing")
+        while int(p.get_by_name("es").get_property("port")) == 0:
+            time.sleep(0.01)
+        print(p.get_by_name("es").get_property("port"), flush=True)
+        msg = p.wait(60)
+        print(msg[0] if msg else "timeout", flush=True)
+        sys.stdin.readline()
+        p.stop()
+    """))
+    proc = subprocess.Popen([sys.executable, str(script)], stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+    try:
+        port = int(proc.stdout.readline())
+        s = nns.parse_launch(f"edgesrc name=src dest-host=127.0.0.1 dest-port={port} connect-type=SHM "
+                             "! tensor_converter ! tensor_sink name=sink")
+        out = []
+        s.get_by_name("sink").connect("new-data", lambda b: out.append(b.memory(0).numpy("uint8").copy()))
+        s.set_state("playing")
+        msg = s.wait(60)
+        assert msg and msg[0] == "eos", s.messages()
+        shm_blobs = int(s.get_by_name("src").get_property("shm-blobs"))
+        s.stop()
+        assert proc.stdout.readline().strip() == "eos"
+    finally:
+        proc.stdin.write("\n")
+        proc.stdin.flush()
+        proc.wait(timeout=30)
+    assert len(out) == 24 and shm_blobs == 24, (len(out), shm_blobs)
+    # the camera's snow frames, in ring order (pool of 6 distinct frames)
+    ref = nns.parse_launch("videotestsrc num-buffers=6 pattern=snow pool-size=6 "
+                           "! video/x-raw,format=RGB,width=64,height=48,framerate=0/1 ! tensor_converter "
+                           "! tensor_sink name=sink")
+    want = []
+    ref.get_by_name("sink").connect("new-data", lambda b: want.append(b.memory(0).numpy("uint8").copy()))
+    ref.run(timeout=30)
+    for i, fr in enumerate(out):
+        np.testing.assert_array_equal(fr.ravel(), want[i % 6].ravel())

@@ -29,6 +29,53 @@ def test_memory_lifetime_selftest(nns, case):
     assert msg == "", msg
 
 
+@pytest.mark.parametrize("case,mutation", [("pinned_h2d", 1), ("mirror_other_stream", 2)])
+def test_memory_selftest_fails_without_its_fix(nns, case, mutation, monkeypatch):
+    """each lifetime case must catch the bug its fix removed.
+    The fix is undone at run time (Memory::set_test_mutation: 1 = a host
+    source's H2D copy is not recorded as a use -- the rule 7ba8684 extended from
+    pinned to pageable sources; 2 = a reader of a host memory does not hold its
+    device mirror, before ee80b24) and the case must then fail; with the fix in
+    place it passes again.  Output: profiles/r6_lifetime_fail_on_parent.txt."""
+    from nnstreamer_amd import _C
+
+    monkeypatch.setenv("NNSX_SELFTEST_VERBOSE", "1")  # (per size: how long map_device blocked)
+    prev = _C.memory_test_mutation(mutation)
+    try:
+        broken = _C.memory_selftest(case, 0)
+    finally:
+        _C.memory_test_mutation(prev)
+    torch.cuda.synchronize()
+    print(f"{case} with fix undone ({mutation}): {broken!r}")
+    assert broken != "", f"{case} did not notice the undone fix"
+    assert _C.memory_selftest(case, 0) == ""
+
+
+def test_pageable_h2d_without_its_fix_on_this_runtime(nns, monkeypatch, capfd):
+    """The pageable half of 7ba8684 on this HIP runtime (ROCm 7.2): measured, a
+    pageable H2D of <= 1 MB returns at once with the source already staged (the
+    frame can be recycled without harm) and an 8 MB one blocks the host until
+    the copy ran -- so with the fix undone the case still passes here.  The
+    test pins that measurement (each size either intact with the host blocked
+    for the spin, or intact after an immediate return) so that a runtime which
+    starts reading pageable sources late shows up as a failure of
+    pageable_h2d, where the fix then matters."""
+    from nnstreamer_amd import _C
+
+    monkeypatch.setenv("NNSX_SELFTEST_VERBOSE", "1")
+    prev = _C.memory_test_mutation(1)
+    try:
+        broken = _C.memory_selftest("pageable_h2d", 0)
+    finally:
+        _C.memory_test_mutation(prev)
+    err = capfd.readouterr().err
+    print(err)
+    lines = [x for x in err.splitlines() if x.startswith("pageable_h2d[")]
+    assert len(lines) == 4, err
+    assert broken == "" and all("bytes intact" in x for x in lines), err
+    assert _C.memory_selftest("pageable_h2d", 0) == ""
+
+
 @pytest.mark.parametrize("H,cin,hid,cout,stride,B", [(7, 160, 960, 160, 1, 8), (14, 96, 576, 160, 2, 2),
                                                      (14, 64, 384, 64, 1, 1)])
 def test_shared_device_scope_ignores_tickets(nns, H, cin, hid, cout, stride, B):
