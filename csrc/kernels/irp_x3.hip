@@ -333,7 +333,7 @@ __global__ void __launch_bounds__((IrpGeom<CIN, COUT, TPW, XL>::NT), (IrpGeom<CI
 // and both weight stages are double-buffered, and step s runs the expand of
 // step s + 1 (into hidden buffer (s + 1) & 1) next to the depthwise + project
 // of step s (from buffer s & 1) -- ONE barrier per step instead of two, and
-// half the waves (a.irp_order: wave bit 2) take the two phases in the other
+// half the waves (a.irp_order: the odd ones by default) take the two phases in the other
 // order, so a SIMD's waves overlap one's MFMA expand with another's VALU / LDS
 // depthwise instead of the whole CU alternating between them.
 template <int CIN, int COUT, int TPW>
@@ -604,13 +604,16 @@ struct IrpCfg {
   IrpCfg { CI, CO, T, &irp_x3_kernel<CI, CO, T, XL>, IrpGeom<CI, CO, T, XL>::lds, IrpGeom<CI, CO, T, XL>::NT, XL, false }
 #define NNSX_IRPP(CI, CO, T) \
   IrpCfg { CI, CO, T, &irpp_x3_kernel<CI, CO, T>, IrppGeom<CI, CO, T>::lds, IrppGeom<CI, CO, T>::NT, false, true }
-// (first match per shape is the default; NNSX_IRP_TPW=1|2 picks that variant)
-// (batch 512, per block: 64 -> 384 -> 64 112.8 / 115.7 us with 2 / 1 tiles per
-// wave, 64 -> 384 -> 96 126.5 / 143.2, 96 -> 576 -> 96 309.2 / 264.8; the wave-split
-// kernels 145.0 / 188.0 / 318.4: profiles/r6_irp_layers_b512.txt)
-const IrpCfg kIrpCfgs[] = {NNSX_IRP(64, 64, 2, false),  NNSX_IRP(64, 96, 2, false),  NNSX_IRP(96, 96, 1, true),
-                           NNSX_IRP(96, 96, 1, false),  NNSX_IRP(64, 64, 1, false),  NNSX_IRP(64, 96, 1, false),
-                           NNSX_IRPP(64, 64, 2),        NNSX_IRPP(64, 96, 2),        NNSX_IRPP(96, 96, 2),
+// (first match per shape is the default; NNSX_IRP_TPW=1|2, NNSX_IRP_XL=0|1 and
+// NNSX_IRP_PIPE=0|1 pick a variant).  Batch 512, us per block
+// (profiles/r6_irp_layers_b512.txt), wave-split irw_x3 / irp TPW 2 / irp TPW 1 /
+// irp TPW 1 XL / irpp TPW 2 (phase order 2):
+//   64 -> 384 -> 64   143.9 / 111.0 / 115.7 /   -   / 110.2
+//   64 -> 384 -> 96   187.1 / 125.5 / 143.2 /   -   / 131.9
+//   96 -> 576 -> 96   315.6 / 309.2 / 279.0 / 248.6 / 223.4
+const IrpCfg kIrpCfgs[] = {NNSX_IRP(64, 64, 2, false),  NNSX_IRP(64, 96, 2, false),  NNSX_IRPP(96, 96, 2),
+                           NNSX_IRP(96, 96, 1, true),   NNSX_IRP(96, 96, 1, false),  NNSX_IRP(64, 64, 1, false),
+                           NNSX_IRP(64, 96, 1, false),  NNSX_IRPP(64, 64, 2),        NNSX_IRPP(64, 96, 2),
                            NNSX_IRPP(64, 64, 1),        NNSX_IRPP(64, 96, 1),        NNSX_IRPP(96, 96, 1)};
 #undef NNSX_IRP
 #undef NNSX_IRPP
@@ -668,10 +671,11 @@ bool irp_x3(const IrBlockF32Args& args, hipStream_t s) {
   if (!c) return false;
   IrBlockF32Args a = args;
   // irpp phase order (NNSX_IRP_ORDER: 0 = every wave expand first, 1 = waves with
-  // bit 2 set depthwise + project first, 2 = odd waves)
+  // bit 2 set depthwise + project first, 2 = odd waves -- the fastest: 223.4 /
+  // 227.4 / 227.8 us on 96 -> 576 -> 96, profiles/r6_irp_layers_b512.txt)
   static const int order = [] {
     const char* e = std::getenv("NNSX_IRP_ORDER");
-    return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 1;
+    return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 2;
   }();
   a.irp_order = order;
   if (c->lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(c->kernel),

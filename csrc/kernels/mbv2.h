@@ -195,7 +195,7 @@ struct IrBlockF32Args {
   // the method x3: the irw_x3 kernel of the same geometry, when there is one
   const uint16_t* we3 = nullptr;
   const uint16_t* wp3 = nullptr;
-  int irp_order = 1;  // irpp_x3 phase order (kernels/irp_x3.hip)
+  int irp_order = 2;  // irpp_x3 phase order (kernels/irp_x3.hip)
 };
 // Launches enqueued by this thread while a SharedDeviceScope is alive may run
 // concurrently with other kernels of the same process (a filter's replay
