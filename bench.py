@@ -114,6 +114,10 @@ def parse_args(argv=None):
                     help="N > 1: rank 0 broadcasts the model bytes to every rank at load over this data plane")
     ap.add_argument("--comm-backend", default="auto", choices=["auto", "rccl", "tcp"],
                     help="posenet_multi: tensor_allgather data plane")
+    ap.add_argument("--fan-transport", default=os.environ.get("NNSX_BENCH_FAN", "shm"), choices=["shm", "rccl"],
+                    help="deeplab_fan: shm = rank 0's cameras render into shared rings and every worker's "
+                         "tensor_converter DMAs its own camera over its own GPU's link (edgesink/edgesrc "
+                         "connect-type=SHM); rccl = rank 0 uploads all cameras, tensor_demux + RCCL scatter")
     ap.add_argument("--config", default=os.environ.get("NNSX_BENCH_CONFIG", "mbv2"),
                     choices=sorted(CONFIGS), help="BASELINE.json config (default: the headline MobileNetV2 pipeline)")
     return ap.parse_args(argv)
@@ -122,6 +126,8 @@ def parse_args(argv=None):
 # best CPU reference path for the MobileNetV2 pipeline
 # (identical pipeline, host elements + fp32 PyTorch CPU, 8 vCPU).
 CPU_BASELINE_FPS = 254.1
+
+_FAN_RUN = 0  # deeplab_fan passes so far (each gets fresh shared-ring names and ports)
 
 # BASELINE.json configs that run on one GPU per rank.  Each: input size, model,
 # normalisation, decoder string and whether the decoder emits one buffer per frame.
@@ -286,8 +292,32 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
                     f"world-size={world} device={dev} comm-backend={a.comm_backend}")
         branch = (f"! tensor_transform name=norm mode=arithmetic option={cfg['norm']} ! {filt}"
                   f"! queue max-size-buffers={a.queue} ! {cfg['decoder'].format(**files)} ! tensor_sink name=sink")
-        if rank == 0:  # the N cameras: upload, mux, demux -> own branch + one RCCL edge per other rank
-            cam_pool = max(2 * B, min(pool, -(-128 * 2**20 // frame_bytes)))
+        cam_pool = max(2 * B, min(pool, -(-128 * 2**20 // frame_bytes)))
+        if a.fan_transport == "shm":
+            # same host: camera r's ring lives in a named shared segment on rank 0
+            # (videotestsrc pool-shm); rank r subscribes (edgesrc connect-type=SHM),
+            # gets its frames as references into its hipHostRegister'ed mapping and
+            # its own tensor_converter DMAs them over ITS GPU's host link -- the
+            # ingest scales with the ranks instead of funnelling through GPU 0
+            # (profiles/r6_shared_ring_ingest.txt); rank 0 runs camera 0's branch
+            global _FAN_RUN
+            _FAN_RUN += 1
+            mport = int(os.environ.get("MASTER_PORT", "29500"))
+            port = lambda r: 20000 + (mport * 37 + _FAN_RUN * 16 + r) % 40000  # noqa: E731
+            tag = f"{mport}-{_FAN_RUN}"
+            conv = f"! tensor_converter frames-per-tensor={B} device={dev} ! queue max-size-buffers=2 "
+            shm_pool = max(2 * B, min(cam_pool, -(-64 * 2**20 // frame_bytes)))  # (64 MiB of /dev/shm per camera)
+            cam = (f"videotestsrc num-buffers={frames} pattern=snow pool-size={shm_pool} {{shm}}"
+                   f"! video/x-raw,format=RGB,width={S},height={S},framerate=0/1 ")
+            if rank == 0:
+                desc = (cam.format(shm="") + conv + branch + " "
+                        + " ".join(cam.format(shm=f"pool-shm=nnsx-fan-{tag}-{r} ")
+                                   + f"! edgesink name=fan{r} port={port(r)} connect-type=SHM wait-connection=1"
+                                   for r in range(1, world)))
+            else:
+                desc = (f"edgesrc name=fan dest-host=127.0.0.1 dest-port={port(rank)} connect-type=SHM "
+                        + conv + branch)
+        elif rank == 0:  # the N cameras: upload, mux, demux -> own branch + one RCCL edge per other rank
             desc = ("".join(f"videotestsrc num-buffers={frames} pattern=snow pool-size={cam_pool} "
                             f"! video/x-raw,format=RGB,width={S},height={S},framerate=0/1 "
                             f"! tensor_converter frames-per-tensor={B} device={dev} ! queue max-size-buffers=2 "
@@ -615,7 +645,8 @@ def headline_record(a, cfg, runs, results, lat_b1, sweep, per_rank, world, use_g
             "model": cfg["desc"],
             "global_batch": B * world,
             "seq_len": 1,
-            "parallelism": (f"tensor_demux fan-out 1->{world} (RCCL p2p)" if fan else
+            "parallelism": ((f"shared-ring fan-out 1->{world} (per-rank ingest)" if a.fan_transport == "shm" else
+                             f"tensor_demux fan-out 1->{world} (RCCL p2p)") if fan else
                             f"branch-dp{world} + edge all-gather" if cfg.get("gather") else f"branch-dp{world}"),
             "pipeline": head["desc"],
         },
@@ -724,6 +755,8 @@ def run_aux(a, nns, cfg, files, rank, world, dev, use_gpu, dist, workdir, out, t
                         "rccl_world": max([int(v.split(":")[1]) for v in r["groups"].values()
                                            if v.startswith("rccl:")] or [0]),
                         "groups_rank0": r["groups"]}
+            if name == "deeplab_fan":
+                xs[name]["transport"] = a.fan_transport
         out["extra_configs"] = xs
 
 

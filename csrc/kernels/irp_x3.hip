@@ -573,9 +573,12 @@ __global__ void __launch_bounds__((IrppGeom<CIN, COUT, TPW>::NT), (IrppGeom<CIN,
       } else {
         dwproj(s);
       }
+      // (stored between the phases: the staging registers live across one phase)
+      if (ph == 0) {
+        if (more) wp_store((s + 1) & 1);
+        if (more2) we_store(s & 1);
+      }
     }
-    if (more) wp_store((s + 1) & 1);
-    if (more2) we_store(s & 1);
     __syncthreads();
   }
 
@@ -590,6 +593,505 @@ __global__ void __launch_bounds__((IrppGeom<CIN, COUT, TPW>::NT), (IrppGeom<CIN,
       if (a.residual) v += *reinterpret_cast<const f32x4_t*>(a.x + pix * CIN + co);
       *reinterpret_cast<f32x4_t*>(a.y + pix * COUT + co) = v;
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// irps: the stride-2 14 x 14 -> 7 x 7 block (96 -> 576 -> 160), one image per
+// workgroup, pipelined like irpp.  8 waves:
+//   * expand: the 196 input pixels as 13 dense 16-pixel tiles (waves 0-4 two,
+//     waves 5-7 one), inputs split once and held in registers;
+//   * depthwise (stride 2) + project: the 49 outputs as 4 16-pixel tiles;
+//     wave w takes tile w / 2 and half of the 10 output-channel tiles;
+//   * the stages loaded at a step's start are stored between its two phases
+//     (their buffers' readers finished before the step began), so the staging
+//     registers live across one phase only;
+//   * LDS: a 15 x 15 bordered hidden grid (the stride-2 windows never reach row
+//     or column 15), expand stages with an odd chunk pitch, project stages
+//     unpadded with the chunk index XOR-swizzled by row (16 lanes reading 16
+//     rows hit 16 distinct 16-byte bank groups); double-buffered: 158 KB.
+constexpr int kIrpsG = 15;                    // hidden grid (bordered): cell (y + 1, x + 1)
+constexpr int kIrpsCells = kIrpsG * kIrpsG;   // 225
+
+template <int CIN, int COUT>
+struct IrpsGeom {
+  static constexpr int NW = 8, NT = 64 * NW;
+  static constexpr int NK32 = CIN / 32, NO16 = COUT / 16, NOH = NO16 / 2;
+  static constexpr int WEP = CIN / 8 + 1;
+  static constexpr size_t hid1 = static_cast<size_t>(8) * kIrpsCells * 16;
+  static constexpr size_t we_w = static_cast<size_t>(3) * 32 * WEP * 16;
+  static constexpr size_t we1 = we_w + 32 * 4;
+  static constexpr size_t wp_w = static_cast<size_t>(3) * COUT * 4 * 16;
+  static constexpr size_t wp1 = wp_w + 10 * 32 * 4;
+  static constexpr size_t lds = 2 * (hid1 + we1 + wp1);
+  static_assert(lds <= 160 * 1024, "irps: LDS");
+  static_assert(NO16 % 2 == 0, "irps: output tiles split in halves");
+  static constexpr int WE_CH = 3 * 32 * (CIN / 8) + 8;
+  static constexpr int WP_CH = 3 * COUT * 4 + 80;
+  static constexpr int WE_IT = (WE_CH + NT - 1) / NT;
+  static constexpr int WP_IT = (WP_CH + NT - 1) / NT;
+};
+
+// (TERMS: bit 0 = eight-product project, bit 1 = eight-product expand, bit 2 =
+// compensated project accumulation (add_comp); A/B of the numerics)
+template <int CIN, int COUT, int TERMS = 0>
+__global__ void __launch_bounds__(512, 2) irps_x3_kernel(IrBlockF32Args a) {
+  using G = IrpsGeom<CIN, COUT>;
+  constexpr int NK32 = G::NK32, NO16 = G::NO16, NOH = G::NOH, WEP = G::WEP, NT = G::NT;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char* const base = reinterpret_cast<char*>(smem);
+  auto hbuf = [&](int i) { return reinterpret_cast<f32x4_t*>(base + i * G::hid1); };
+  auto webuf = [&](int i) { return base + 2 * G::hid1 + i * G::we1; };
+  auto wpbuf = [&](int i) { return base + 2 * G::hid1 + 2 * G::we1 + i * G::wp1; };
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int b = blockIdx.x;
+  const int hid = a.hid, nsteps = hid / 32;
+  const int late_e = a.irp_order == 0 ? 0 : (a.irp_order == 2 ? (wave & 1) : ((wave >> 2) & 1));
+  // expand tiles of this wave: 2 w, 2 w + 1 (waves 5-7: w + 5 only)
+  const bool two = wave < 5;
+  const int et0 = two ? 2 * wave : wave + 5;
+  // depthwise + project: output tile and the first of its output-channel tiles
+  const int dt = wave >> 1;
+  const int o0 = (wave & 1) * NOH;
+  const int q = 16 * dt + li;  // output pixel of this lane
+  const bool qreal = q < 49;
+  const int oy = qreal ? q / 7 : 6, ox = qreal ? q - 7 * (q / 7) : 6;
+
+  for (int v = tid; v < 2 * 8 * kIrpsCells; v += NT) hbuf(0)[v] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t wes = static_cast<int64_t>(hid) * CIN;
+  const int64_t wps = static_cast<int64_t>(COUT) * hid;
+  u32x4_t we_st[G::WE_IT], wp_st[G::WP_IT];
+  auto we_load = [&](int s) {
+#pragma unroll
+    for (int it = 0; it < G::WE_IT; ++it) {
+      const int v = tid + it * NT;
+      if (v >= G::WE_CH) break;
+      if (v < G::WE_CH - 8) {
+        const int p = v / (32 * (CIN / 8)), r = v - p * 32 * (CIN / 8);
+        const int h = r / (CIN / 8), kc = r - h * (CIN / 8);
+        we_st[it] = *reinterpret_cast<const u32x4_t*>(a.we3 + p * wes + static_cast<int64_t>(32 * s + h) * CIN + kc * 8);
+      } else {
+        we_st[it] = *reinterpret_cast<const u32x4_t*>(a.be + 32 * s + 4 * (v - (G::WE_CH - 8)));
+      }
+    }
+  };
+  auto we_store = [&](int i) {
+    char* wel = webuf(i);
+#pragma unroll
+    for (int it = 0; it < G::WE_IT; ++it) {
+      const int v = tid + it * NT;
+      if (v >= G::WE_CH) break;
+      if (v < G::WE_CH - 8) {
+        const int p = v / (32 * (CIN / 8)), r = v - p * 32 * (CIN / 8);
+        const int h = r / (CIN / 8), kc = r - h * (CIN / 8);
+        *reinterpret_cast<u32x4_t*>(wel + ((p * 32 + h) * WEP + kc) * 16) = we_st[it];
+      } else {
+        *reinterpret_cast<u32x4_t*>(wel + G::we_w + 16 * (v - (G::WE_CH - 8))) = we_st[it];
+      }
+    }
+  };
+  auto wp_load = [&](int s) {
+#pragma unroll
+    for (int it = 0; it < G::WP_IT; ++it) {
+      const int v = tid + it * NT;
+      if (v >= G::WP_CH) break;
+      if (v < G::WP_CH - 80) {
+        const int p = v / (COUT * 4), r = v - p * COUT * 4;
+        const int co = r >> 2, kc = r & 3;
+        wp_st[it] = *reinterpret_cast<const u32x4_t*>(a.wp3 + p * wps + static_cast<int64_t>(co) * hid + 32 * s + kc * 8);
+      } else {
+        const int qq = v - (G::WP_CH - 80), t = qq >> 3, c4 = qq & 7;
+        wp_st[it] = *reinterpret_cast<const u32x4_t*>((t < 9 ? a.wd + t * hid : a.bd) + 32 * s + 4 * c4);
+      }
+    }
+  };
+  // project stage: [part][row][chunk ^ ((row >> 2) & 3)]
+  auto wp_store = [&](int i) {
+    char* wpl = wpbuf(i);
+#pragma unroll
+    for (int it = 0; it < G::WP_IT; ++it) {
+      const int v = tid + it * NT;
+      if (v >= G::WP_CH) break;
+      if (v < G::WP_CH - 80) {
+        const int p = v / (COUT * 4), r = v - p * COUT * 4;
+        const int co = r >> 2, kc = r & 3;
+        *reinterpret_cast<u32x4_t*>(wpl + ((p * COUT + co) * 4 + (kc ^ ((co >> 2) & 3))) * 16) = wp_st[it];
+      } else {
+        *reinterpret_cast<u32x4_t*>(wpl + G::wp_w + 16 * (v - (G::WP_CH - 80))) = wp_st[it];
+      }
+    }
+  };
+
+  // the wave's input pixels, split once (tile et0 + t; pixel 16 e + li)
+  X3Frag xin[2][NK32];
+  int ecell[2];
+  const float* xb = a.x + static_cast<int64_t>(b) * kIrpH * kIrpH * CIN;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int p = 16 * (et0 + t) + li;
+    const bool real = p < 196 && (t == 0 || two);
+    const int ps = real ? p : 0;
+    const int py = ps / 14, px = ps - 14 * (ps / 14);
+    ecell[t] = real ? (py + 1) * kIrpsG + px + 1 : -1;
+    const int64_t off = static_cast<int64_t>(ps) * CIN + 8 * g;
+#pragma unroll
+    for (int c = 0; c < NK32; ++c) {
+      f32x4_t lo = *reinterpret_cast<const f32x4_t*>(xb + off + 32 * c);
+      f32x4_t hi = *reinterpret_cast<const f32x4_t*>(xb + off + 32 * c + 4);
+      if (!real) lo = hi = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      xin[t][c] = split_x3(lo, hi);
+    }
+  }
+  const int wcell = 2 * oy * kIrpsG + 2 * ox;  // window origin: input (2 oy - 1, 2 ox - 1)
+
+  auto expand = [&](int s) {
+    const char* wel = webuf(s & 1);
+    f32x4_t* hb = hbuf(s & 1);
+    f32x4_t e[2][2];
+#pragma unroll
+    for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) e[ht][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NK32; ++c) {
+#pragma unroll
+      for (int ht = 0; ht < 2; ++ht) {
+        X3Frag wa;
+        const char* wr = wel + ((ht * 16 + li) * WEP + 4 * c + g) * 16;
+        wa.h = *reinterpret_cast<const bf16x8_t*>(wr);
+        wa.m = *reinterpret_cast<const bf16x8_t*>(wr + 32 * WEP * 16);
+        wa.l = *reinterpret_cast<const bf16x8_t*>(wr + 2 * 32 * WEP * 16);
+        if constexpr (TERMS & 2) {
+          e[ht][0] += mfma_x3e(wa, xin[0][c]);
+          if (two) e[ht][1] += mfma_x3e(wa, xin[1][c]);
+        } else {
+          e[ht][0] += mfma_x3(wa, xin[0][c]);
+          if (two) e[ht][1] += mfma_x3(wa, xin[1][c]);
+        }
+      }
+    }
+    const float* bel = reinterpret_cast<const float*>(wel + G::we_w);
+#pragma unroll
+    for (int ht = 0; ht < 2; ++ht) {
+      const f32x4_t be4 = *reinterpret_cast<const f32x4_t*>(bel + ht * 16 + 4 * g);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        if (ecell[t] >= 0) hb[(ht * 4 + g) * kIrpsCells + ecell[t]] = relu6x4(e[ht][t] + be4);
+    }
+  };
+
+  f32x4_t acc[NOH], cmp[(TERMS & 4) ? NOH : 1];
+#pragma unroll
+  for (int o = 0; o < NOH; ++o) acc[o] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int o = 0; o < ((TERMS & 4) ? NOH : 1); ++o) cmp[o] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto dwproj = [&](int s) {
+    const f32x4_t* hb = hbuf(s & 1);
+    const char* wpl = wpbuf(s & 1);
+    const float* wdl = reinterpret_cast<const float*>(wpl + G::wp_w);
+    f32x4_t d[2];
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      const int qd = 2 * g + qq;
+      f32x4_t o = *reinterpret_cast<const f32x4_t*>(wdl + 9 * 32 + 4 * qd);
+      const f32x4_t* hp = hb + qd * kIrpsCells + wcell;
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+          o = __builtin_elementwise_fma(hp[dy * kIrpsG + dx],
+                                        *reinterpret_cast<const f32x4_t*>(wdl + (3 * dy + dx) * 32 + 4 * qd), o);
+      d[qq] = relu6x4(o);
+    }
+    const X3Frag bf = split_x3(d[0], d[1]);
+#pragma unroll
+    for (int oi = 0; oi < NOH; ++oi) {
+      const int row = (o0 + oi) * 16 + li;
+      const char* wr = wpl + (row * 4 + (g ^ ((row >> 2) & 3))) * 16;
+      X3Frag wa;
+      wa.h = *reinterpret_cast<const bf16x8_t*>(wr);
+      wa.m = *reinterpret_cast<const bf16x8_t*>(wr + COUT * 64);
+      wa.l = *reinterpret_cast<const bf16x8_t*>(wr + 2 * COUT * 64);
+      const f32x4_t tt = (TERMS & 1) ? mfma_x3e(wa, bf) : mfma_x3(wa, bf);
+      if constexpr ((TERMS & 4) != 0)
+        add_comp(acc[oi], cmp[(TERMS & 4) ? oi : 0], tt);
+      else
+        acc[oi] += tt;
+    }
+  };
+
+  we_load(0);
+  wp_load(0);
+  we_store(0);
+  wp_store(0);
+  if (nsteps > 1) {
+    we_load(1);
+    we_store(1);
+  }
+  __syncthreads();
+  expand(0);
+  __syncthreads();
+  // one barrier per step (irpp_x3_kernel's hazard argument, same buffers);
+  // the stages go to LDS between the phases
+  for (int s = 0; s < nsteps; ++s) {
+    const bool more = s + 1 < nsteps, more2 = s + 2 < nsteps;
+    if (more) wp_load(s + 1);
+    if (more2) we_load(s + 2);
+#pragma nounroll
+    for (int ph = 0; ph < 2; ++ph) {
+      if (ph == late_e) {
+        if (more) expand(s + 1);
+      } else {
+        dwproj(s);
+      }
+      if (ph == 0) {
+        if (more) wp_store((s + 1) & 1);
+        if (more2) we_store(s & 1);
+      }
+    }
+    __syncthreads();
+  }
+
+  if (!qreal) return;
+  float* yo = a.y + (static_cast<int64_t>(b) * 49 + q) * COUT;
+#pragma unroll
+  for (int oi = 0; oi < NOH; ++oi) {
+    const int co = (o0 + oi) * 16 + 4 * g;
+    f32x4_t v = acc[oi];
+    if constexpr ((TERMS & 4) != 0) v += cmp[(TERMS & 4) ? oi : 0];
+    *reinterpret_cast<f32x4_t*>(yo + co) = v + *reinterpret_cast<const f32x4_t*>(a.bp + co);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// irp7: the 7 x 7 block (160 -> 960 -> 160, residual), one image per
+// workgroup, pipelined like irpp.  The 49 pixels are 4 16-pixel tiles; 8 waves,
+// wave w owns tile w & 3 and half w >> 2 of the work on it: the expand's 16
+// hidden channels of that half (of the step's 32) and the project's output
+// tiles of that half -- every wave runs 60 split-bf16 MFMAs per step in 5 + 5
+// independent chains, its 16 input pixels split once and held in registers
+// (5 k-chunks of 160 channels).  LDS: 9 x 9 bordered hidden grid, expand stages
+// with an odd chunk pitch, project stages XOR-swizzled (irps), double-buffered.
+constexpr int kIrp7G = 9;                          // hidden grid (bordered)
+constexpr int kIrp7Cells = kIrp7G * kIrp7G + 16;   // + scratch cells for the padding lanes
+
+template <int CIN, int COUT>
+struct Irp7Geom {
+  static constexpr int NW = 8, NT = 64 * NW;
+  static constexpr int NK32 = CIN / 32, NO16 = COUT / 16, NOH = NO16 / 2;
+  static constexpr int WEP = CIN / 8 + 1;
+  static constexpr size_t hid1 = static_cast<size_t>(8) * kIrp7Cells * 16;
+  static constexpr size_t we_w = static_cast<size_t>(3) * 32 * WEP * 16;
+  static constexpr size_t we1 = we_w + 32 * 4;
+  static constexpr size_t wp_w = static_cast<size_t>(3) * COUT * 4 * 16;
+  static constexpr size_t wp1 = wp_w + 10 * 32 * 4;
+  static constexpr size_t lds = 2 * (hid1 + we1 + wp1);
+  static_assert(lds <= 160 * 1024, "irp7: LDS");
+  static_assert(NO16 % 2 == 0, "irp7: output tiles split in halves");
+  static constexpr int WE_CH = 3 * 32 * (CIN / 8) + 8;
+  static constexpr int WP_CH = 3 * COUT * 4 + 80;
+  static constexpr int WE_IT = (WE_CH + NT - 1) / NT;
+  static constexpr int WP_IT = (WP_CH + NT - 1) / NT;
+};
+
+template <int CIN, int COUT>
+__global__ void __launch_bounds__(512, 2) irp7_x3_kernel(IrBlockF32Args a) {
+  using G = Irp7Geom<CIN, COUT>;
+  constexpr int NK32 = G::NK32, NOH = G::NOH, WEP = G::WEP, NT = G::NT;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char* const base = reinterpret_cast<char*>(smem);
+  auto hbuf = [&](int i) { return reinterpret_cast<f32x4_t*>(base + i * G::hid1); };
+  auto webuf = [&](int i) { return base + 2 * G::hid1 + i * G::we1; };
+  auto wpbuf = [&](int i) { return base + 2 * G::hid1 + 2 * G::we1 + i * G::wp1; };
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int b = blockIdx.x;
+  const int hid = a.hid, nsteps = hid / 32;
+  const int late_e = a.irp_order == 0 ? 0 : (a.irp_order == 2 ? (wave & 1) : ((wave >> 2) & 1));
+  const int t = wave & 3, half = wave >> 2;
+  const int p = 16 * t + li;  // this lane's pixel
+  const bool real = p < 49;
+  const int py = real ? p / 7 : 0, px = real ? p - 7 * (p / 7) : 0;
+  const int ecell = real ? (py + 1) * kIrp7G + px + 1 : kIrp7G * kIrp7G + li;
+  const int wcell = py * kIrp7G + px;  // window origin (bordered grid)
+  const int o0 = half * NOH;
+
+  for (int v = tid; v < 2 * 8 * kIrp7Cells; v += NT) hbuf(0)[v] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t wes = static_cast<int64_t>(hid) * CIN;
+  const int64_t wps = static_cast<int64_t>(COUT) * hid;
+  u32x4_t we_st[G::WE_IT], wp_st[G::WP_IT];
+  auto we_load = [&](int s) {
+#pragma unroll
+    for (int it = 0; it < G::WE_IT; ++it) {
+      const int v = tid + it * NT;
+      if (v >= G::WE_CH) break;
+      if (v < G::WE_CH - 8) {
+        const int pp = v / (32 * (CIN / 8)), r = v - pp * 32 * (CIN / 8);
+        const int h = r / (CIN / 8), kc = r - h * (CIN / 8);
+        we_st[it] = *reinterpret_cast<const u32x4_t*>(a.we3 + pp * wes + static_cast<int64_t>(32 * s + h) * CIN + kc * 8);
+      } else {
+        we_st[it] = *reinterpret_cast<const u32x4_t*>(a.be + 32 * s + 4 * (v - (G::WE_CH - 8)));
+      }
+    }
+  };
+  auto we_store = [&](int i) {
+    char* wel = webuf(i);
+#pragma unroll
+    for (int it = 0; it < G::WE_IT; ++it) {
+      const int v = tid + it * NT;
+      if (v >= G::WE_CH) break;
+      if (v < G::WE_CH - 8) {
+        const int pp = v / (32 * (CIN / 8)), r = v - pp * 32 * (CIN / 8);
+        const int h = r / (CIN / 8), kc = r - h * (CIN / 8);
+        *reinterpret_cast<u32x4_t*>(wel + ((pp * 32 + h) * WEP + kc) * 16) = we_st[it];
+      } else {
+        *reinterpret_cast<u32x4_t*>(wel + G::we_w + 16 * (v - (G::WE_CH - 8))) = we_st[it];
+      }
+    }
+  };
+  auto wp_load = [&](int s) {
+#pragma unroll
+    for (int it = 0; it < G::WP_IT; ++it) {
+      const int v = tid + it * NT;
+      if (v >= G::WP_CH) break;
+      if (v < G::WP_CH - 80) {
+        const int pp = v / (COUT * 4), r = v - pp * COUT * 4;
+        const int co = r >> 2, kc = r & 3;
+        wp_st[it] = *reinterpret_cast<const u32x4_t*>(a.wp3 + pp * wps + static_cast<int64_t>(co) * hid + 32 * s + kc * 8);
+      } else {
+        const int qq = v - (G::WP_CH - 80), tt = qq >> 3, c4 = qq & 7;
+        wp_st[it] = *reinterpret_cast<const u32x4_t*>((tt < 9 ? a.wd + tt * hid : a.bd) + 32 * s + 4 * c4);
+      }
+    }
+  };
+  auto wp_store = [&](int i) {
+    char* wpl = wpbuf(i);
+#pragma unroll
+    for (int it = 0; it < G::WP_IT; ++it) {
+      const int v = tid + it * NT;
+      if (v >= G::WP_CH) break;
+      if (v < G::WP_CH - 80) {
+        const int pp = v / (COUT * 4), r = v - pp * COUT * 4;
+        const int co = r >> 2, kc = r & 3;
+        *reinterpret_cast<u32x4_t*>(wpl + ((pp * COUT + co) * 4 + (kc ^ ((co >> 2) & 3))) * 16) = wp_st[it];
+      } else {
+        *reinterpret_cast<u32x4_t*>(wpl + G::wp_w + 16 * (v - (G::WP_CH - 80))) = wp_st[it];
+      }
+    }
+  };
+
+  X3Frag xin[NK32];
+  const float* xb = a.x + static_cast<int64_t>(b) * 49 * CIN;
+  {
+    const int64_t off = static_cast<int64_t>(real ? p : 0) * CIN + 8 * g;
+#pragma unroll
+    for (int c = 0; c < NK32; ++c) {
+      f32x4_t lo = *reinterpret_cast<const f32x4_t*>(xb + off + 32 * c);
+      f32x4_t hi = *reinterpret_cast<const f32x4_t*>(xb + off + 32 * c + 4);
+      if (!real) lo = hi = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      xin[c] = split_x3(lo, hi);
+    }
+  }
+
+  // expand: the wave's 16 hidden channels (half) of step s for its tile
+  auto expand = [&](int s) {
+    const char* wel = webuf(s & 1);
+    f32x4_t* hb = hbuf(s & 1);
+    f32x4_t e = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NK32; ++c) {
+      X3Frag wa;
+      const char* wr = wel + ((half * 16 + li) * WEP + 4 * c + g) * 16;
+      wa.h = *reinterpret_cast<const bf16x8_t*>(wr);
+      wa.m = *reinterpret_cast<const bf16x8_t*>(wr + 32 * WEP * 16);
+      wa.l = *reinterpret_cast<const bf16x8_t*>(wr + 2 * 32 * WEP * 16);
+      e += mfma_x3(wa, xin[c]);
+    }
+    const float* bel = reinterpret_cast<const float*>(wel + G::we_w);
+    const f32x4_t be4 = *reinterpret_cast<const f32x4_t*>(bel + half * 16 + 4 * g);
+    hb[(half * 4 + g) * kIrp7Cells + ecell] = relu6x4(e + be4);
+  };
+
+  f32x4_t acc[NOH];
+#pragma unroll
+  for (int o = 0; o < NOH; ++o) acc[o] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto dwproj = [&](int s) {
+    const f32x4_t* hb = hbuf(s & 1);
+    const char* wpl = wpbuf(s & 1);
+    const float* wdl = reinterpret_cast<const float*>(wpl + G::wp_w);
+    f32x4_t d[2];
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      const int qd = 2 * g + qq;
+      f32x4_t o = *reinterpret_cast<const f32x4_t*>(wdl + 9 * 32 + 4 * qd);
+      const f32x4_t* hp = hb + qd * kIrp7Cells + wcell;
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+          o = __builtin_elementwise_fma(hp[dy * kIrp7G + dx],
+                                        *reinterpret_cast<const f32x4_t*>(wdl + (3 * dy + dx) * 32 + 4 * qd), o);
+      d[qq] = relu6x4(o);
+    }
+    const X3Frag bf = split_x3(d[0], d[1]);
+#pragma unroll
+    for (int oi = 0; oi < NOH; ++oi) {
+      const int row = (o0 + oi) * 16 + li;
+      const char* wr = wpl + (row * 4 + (g ^ ((row >> 2) & 3))) * 16;
+      X3Frag wa;
+      wa.h = *reinterpret_cast<const bf16x8_t*>(wr);
+      wa.m = *reinterpret_cast<const bf16x8_t*>(wr + COUT * 64);
+      wa.l = *reinterpret_cast<const bf16x8_t*>(wr + 2 * COUT * 64);
+      acc[oi] += mfma_x3(wa, bf);
+    }
+  };
+
+  we_load(0);
+  wp_load(0);
+  we_store(0);
+  wp_store(0);
+  if (nsteps > 1) {
+    we_load(1);
+    we_store(1);
+  }
+  __syncthreads();
+  expand(0);
+  __syncthreads();
+  // one barrier per step (irpp_x3_kernel's hazard argument, same buffers)
+  for (int s = 0; s < nsteps; ++s) {
+    const bool more = s + 1 < nsteps, more2 = s + 2 < nsteps;
+    if (more) wp_load(s + 1);
+    if (more2) we_load(s + 2);
+#pragma nounroll
+    for (int ph = 0; ph < 2; ++ph) {
+      if (ph == late_e) {
+        if (more) expand(s + 1);
+      } else {
+        dwproj(s);
+      }
+      if (ph == 0) {
+        if (more) wp_store((s + 1) & 1);
+        if (more2) we_store(s & 1);
+      }
+    }
+    __syncthreads();
+  }
+
+  if (!real) return;
+  float* yo = a.y + (static_cast<int64_t>(b) * 49 + p) * COUT;
+#pragma unroll
+  for (int oi = 0; oi < NOH; ++oi) {
+    const int co = (o0 + oi) * 16 + 4 * g;
+    f32x4_t v = acc[oi] + *reinterpret_cast<const f32x4_t*>(a.bp + co);
+    if (a.residual) v += *reinterpret_cast<const f32x4_t*>(xb + static_cast<int64_t>(p) * CIN + co);
+    *reinterpret_cast<f32x4_t*>(yo + co) = v;
   }
 }
 
@@ -662,11 +1164,67 @@ static bool irp_enabled() {
   return on;
 }
 
-bool irp_x3_supported(const IrBlockF32Args& a) { return irp_enabled() && find_irp(a) != nullptr; }
+// the stride-2 14 -> 7 block (irps); NNSX_IRPS=0 turns it off (A/B)
+static bool irps_match(const IrBlockF32Args& a) {
+  static const bool on = [] {
+    const char* e = std::getenv("NNSX_IRPS");
+    return !(e && e[0] == '0');
+  }();
+  return on && a.stride == 2 && a.dil == 1 && a.has_expand && a.H == kIrpH && a.W == kIrpH && a.cin == 96 &&
+         a.cout == 160 && a.hid % 32 == 0 && a.hid >= 64 && a.we3 && a.wp3 && !a.residual &&
+         a.B >= g_irp_min_b.load(std::memory_order_relaxed);
+}
+
+// the 7 x 7 160 -> 960 -> 160 block (irp7); NNSX_IRP7=0 turns it off (A/B)
+static bool irp7_match(const IrBlockF32Args& a) {
+  static const bool on = [] {
+    const char* e = std::getenv("NNSX_IRP7");
+    return !(e && e[0] == '0');
+  }();
+  return on && a.stride == 1 && a.dil == 1 && a.has_expand && a.H == 7 && a.W == 7 && a.cin == 160 &&
+         a.cout == 160 && a.hid % 32 == 0 && a.hid >= 64 && a.we3 && a.wp3 &&
+         a.B >= g_irp_min_b.load(std::memory_order_relaxed);
+}
+
+bool irp_x3_supported(const IrBlockF32Args& a) {
+  return irp_enabled() && (irps_match(a) || irp7_match(a) || find_irp(a) != nullptr);
+}
 
 int irp_x3_set_min_batch(int b) { return g_irp_min_b.exchange(b); }
 
 bool irp_x3(const IrBlockF32Args& args, hipStream_t s) {
+  if (irp_enabled() && irps_match(args)) {
+    using G = IrpsGeom<96, 160>;
+    IrBlockF32Args a = args;
+    a.irp_order = 2;
+    // NNSX_IRPS_TERMS=0..7: product terms of the project (bit 0) / expand (bit 1),
+    // compensated project accumulation (bit 2)
+    static const int terms = [] {
+      const char* e = std::getenv("NNSX_IRPS_TERMS");
+      return e && e[0] >= '0' && e[0] <= '7' ? e[0] - '0' : 0;
+    }();
+    void (*k)(IrBlockF32Args) = terms == 1   ? &irps_x3_kernel<96, 160, 1>
+                                : terms == 2 ? &irps_x3_kernel<96, 160, 2>
+                                : terms == 3 ? &irps_x3_kernel<96, 160, 3>
+                                : terms == 4 ? &irps_x3_kernel<96, 160, 4>
+                                : terms == 5 ? &irps_x3_kernel<96, 160, 5>
+                                             : &irps_x3_kernel<96, 160, 0>;
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024) != hipSuccess)
+      return false;
+    hipLaunchKernelGGL(k, dim3(static_cast<unsigned>(a.B)), dim3(G::NT), G::lds, s, a);
+    return true;
+  }
+  if (irp_enabled() && irp7_match(args)) {
+    using G = Irp7Geom<160, 160>;
+    IrBlockF32Args a = args;
+    a.irp_order = 2;
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&irp7_x3_kernel<160, 160>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+      return false;
+    hipLaunchKernelGGL((irp7_x3_kernel<160, 160>), dim3(static_cast<unsigned>(a.B)), dim3(G::NT), G::lds, s, a);
+    return true;
+  }
   const IrpCfg* c = irp_enabled() ? find_irp(args) : nullptr;
   if (!c) return false;
   IrBlockF32Args a = args;

@@ -72,6 +72,29 @@ __device__ __forceinline__ f32x4_t mfma_x3(const X3Frag& a, const X3Frag& b) {
   return mfma_bf16(a.h, b.h, t);
 }
 
+// the same with the two mid x low products too (eight MFMAs): every product
+// term above 2^-32 relative kept
+__device__ __forceinline__ f32x4_t mfma_x3e(const X3Frag& a, const X3Frag& b) {
+  f32x4_t t = mfma_bf16(a.l, b.m, f32x4_t{0.f, 0.f, 0.f, 0.f});
+  t = mfma_bf16(a.m, b.l, t);
+  t = mfma_bf16(a.l, b.h, t);
+  t = mfma_bf16(a.h, b.l, t);
+  t = mfma_bf16(a.m, b.m, t);
+  t = mfma_bf16(a.m, b.h, t);
+  t = mfma_bf16(a.h, b.m, t);
+  return mfma_bf16(a.h, b.h, t);
+}
+
+// acc += t with the rounding error of the add carried in c (Knuth's TwoSum:
+// exact for any magnitudes); acc + c at the end is the sum of the partials to
+// within one final rounding, whatever the number of k-steps
+__device__ __forceinline__ void add_comp(f32x4_t& acc, f32x4_t& c, f32x4_t t) {
+  const f32x4_t s = acc + t;
+  const f32x4_t bb = s - acc;
+  c += (acc - (s - bb)) + (t - bb);
+  acc = s;
+}
+
 // 32 x 32 x 16 form (project phases whose k-step is one 16-channel subtile):
 // lane l holds k = 8 (l >> 5) + j of row / column l & 31; the result lane l
 // holds column l & 31, rows (r & 3) + 8 (r >> 2) + 4 (l >> 5)

@@ -5,6 +5,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -36,17 +38,20 @@ def test_bench_refuses_world_mismatch():
     assert "WORLD_SIZE=1" in (r.stderr + r.stdout)
 
 
-def test_bench_three_ranks_selfcheck_and_extra_configs():
+@pytest.mark.parametrize("fan", ["shm", "rccl"])
+def test_bench_three_ranks_selfcheck_and_extra_configs(fan):
     """WORLD_SIZE > 1 (the driver's scaling run): after the headline every
     comm::Group operation is checked on every rank (rccl_selfcheck; tcp data
     plane on CPU, RCCL on GPUs) and short passes of the multi-rank configs 4
     and 5 report their frames/s and groups -- all outside the timed region,
-    well inside a minute."""
+    well inside a minute.  Config 4 with both fan-out transports: shared frame
+    rings (each worker ingests its own camera, the default) and tensor_demux +
+    scatter over the rank group."""
     import time
 
     t0 = time.time()
     r = _run(["--cpu", "--gpus", "3", "--steps", "2", "--warmup", "1", "--batch", "1", "--latency-frames", "0",
-              "--sweep", ""])
+              "--sweep", "", "--fan-transport", fan])
     assert r.returncode == 0, r.stderr[-3000:]
     assert time.time() - t0 < 120
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
@@ -58,7 +63,9 @@ def test_bench_three_ranks_selfcheck_and_extra_configs():
     xs = out["extra_configs"]
     assert set(xs) == {"deeplab_fan", "posenet_multi"}
     assert all(v["frames_per_s"] and v["frames_per_s"] > 0 for v in xs.values()), xs
-    assert "edge_fan1" in xs["deeplab_fan"]["groups_rank0"] and "edge_allgather" in xs["posenet_multi"]["groups_rank0"]
+    assert xs["deeplab_fan"]["transport"] == fan
+    assert ("edge_fan1" in xs["deeplab_fan"]["groups_rank0"]) == (fan == "rccl")
+    assert "edge_allgather" in xs["posenet_multi"]["groups_rank0"]
     assert out["fp32_method"] in ("x3", "fp32")
     assert out["value"] > 0 and out["n_gpus"] == 0
 

@@ -82,3 +82,34 @@ def test_irp_matches_wave_split_kernel(nns, method, monkeypatch):
         os.unlink(path)
     assert not torch.equal(outs[0], outs[1])
     assert (outs[0] - outs[1]).abs().max().item() < 1e-4
+
+
+@pytest.mark.parametrize("H,cin,hid,cout,stride", [(14, 96, 576, 160, 2), (7, 160, 960, 160, 1)])
+@pytest.mark.parametrize("B", [1, 3, 128, 512])
+@pytest.mark.parametrize("dist", ["normal", "relu6"])
+def test_irp_other_maps_no_worse_than_native(nns, method, H, cin, hid, cout, stride, B, dist):
+    """the stride-2 14 x 14 -> 7 x 7 block (96 -> 576 -> 160, irps_x3_kernel) and
+    the 7 x 7 160 -> 960 -> 160 residual block (irp7_x3_kernel): same gate as
+    the 14 x 14 stride-1 shapes"""
+    we, be, wd, bd, wp, bp, we3, wp3 = _ir_weights(cin, hid, cout, 7 + B + H)
+    x = torch.randn(B, H, H, cin, device="cuda")
+    if dist == "relu6":
+        x = (x * 2).clamp(0, 6)
+    res = stride == 1 and cin == cout
+    ref = _ir_ref64(x, we, be, wd, bd, wp, bp, stride, cout, True, res)
+
+    def run():
+        return torch.ops.nnsx.ir_block(x, we, be, wd, bd, wp, bp, stride, cout, True, res, 1, None, we3, wp3)
+
+    method("fp32")
+    y_nat = run()
+    method("x3")
+    assert torch.ops.nnsx.ir_method_f32(stride, H, H, cin, hid, cout, B, 1) == "x3"
+    y = run()
+    Ho = (H - 1) // stride + 1
+    assert y.shape == (B, Ho, Ho, cout)
+    assert not torch.equal(y, y_nat), "the x3 kernel did not run"
+    (nat_max, nat_mean), (x3_max, x3_mean) = _errs(y_nat, ref), _errs(y, ref)
+    slack = 1.0 if B >= 128 else 1.1
+    assert x3_max <= nat_max * slack and x3_mean <= nat_mean, (nat_max, x3_max, nat_mean, x3_mean)
+    assert torch.equal(y, run())
