@@ -2036,6 +2036,24 @@ void avgpool_f32(const float* x, float* y, int B, int HW, int C, hipStream_t s) 
 bool ir_block_f32_supported(int stride, int H, int W, int cin, int hid, int cout, bool has_expand, int dil, int B) {
   if (stride != 1 && stride != 2) return false;
   if (cin % 8 || cout % 4 || hid % 16) return false;
+  if (f32_math() == F32Math::kX3 && B > 0) {
+    // the image-per-workgroup x3 kernels (kernels/irp_x3.hip) cover some blocks
+    // no fp32 kernel does (7 x 7 160 -> 960 -> 320); the callers pass the split weights
+    IrBlockF32Args q;
+    q.stride = stride;
+    q.H = H;
+    q.W = W;
+    q.cin = cin;
+    q.hid = hid;
+    q.cout = cout;
+    q.B = B;
+    q.dil = dil;
+    q.has_expand = has_expand;
+    q.residual = stride == 1 && cin == cout;
+    static const uint16_t dummy[8] = {};
+    q.we3 = q.wp3 = dummy;
+    if (irp_x3_supported(q)) return true;
+  }
   if (dil != 1) return find_irw(stride, H, W, cin, hid, cout, has_expand, dil, B) != nullptr;
   return find_irw(stride, H, W, cin, hid, cout, has_expand) != nullptr ||
          find_cfg(stride, H, W, cin, hid, cout, has_expand) != nullptr;

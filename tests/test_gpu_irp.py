@@ -84,13 +84,15 @@ def test_irp_matches_wave_split_kernel(nns, method, monkeypatch):
     assert (outs[0] - outs[1]).abs().max().item() < 1e-4
 
 
-@pytest.mark.parametrize("H,cin,hid,cout,stride", [(14, 96, 576, 160, 2), (7, 160, 960, 160, 1)])
+@pytest.mark.parametrize("H,cin,hid,cout,stride", [(14, 96, 576, 160, 2), (28, 32, 192, 32, 1),
+                                                    (28, 32, 192, 64, 2)])
 @pytest.mark.parametrize("B", [1, 3, 128, 512])
 @pytest.mark.parametrize("dist", ["normal", "relu6"])
 def test_irp_other_maps_no_worse_than_native(nns, method, H, cin, hid, cout, stride, B, dist):
     """the stride-2 14 x 14 -> 7 x 7 block (96 -> 576 -> 160, irps_x3_kernel) and
-    the 7 x 7 160 -> 960 -> 160 residual block (irp7_x3_kernel): same gate as
-    the 14 x 14 stride-1 shapes"""
+    the 28 x 28 32 -> 192 -> 32 and 28 -> 14 32 -> 192 -> 64 blocks (half an
+    image per workgroup, irh_x3_kernel): same gate as the 14 x 14 stride-1
+    shapes"""
     we, be, wd, bd, wp, bp, we3, wp3 = _ir_weights(cin, hid, cout, 7 + B + H)
     x = torch.randn(B, H, H, cin, device="cuda")
     if dist == "relu6":
