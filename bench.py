@@ -403,6 +403,9 @@ def run_pipeline(a, nns, cfg, model_name, model_path, files, B, steps, warmup, r
         # last warmup end to the last timed end)
         rec["gpu_elapsed"] = (max(d[0] for d in ds[:warmup + steps]) - max(d[0] for d in ds[:warmup])) / 1e9
         rec["gpu_busy_ms"] = float(np.median([d[1] for d in ds[warmup:warmup + steps]])) / 1e6
+        if os.environ.get("NNSX_BENCH_SERIES") == "1":  # (diagnostics: every invoke's device ms, warm-up included)
+            print(f"rank {rank}: device ms per invoke " + " ".join(f"{d[1] / 1e6:.3f}" for d in ds[:warmup + steps]),
+                  file=sys.stderr, flush=True)
     return rec
 
 

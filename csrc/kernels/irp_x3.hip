@@ -1232,18 +1232,25 @@ static bool irps_match(const IrBlockF32Args& a) {
 }
 
 // the 28 x 28 32 -> 192 -> 32 block and the 28 -> 14 32 -> 192 -> 64 one, half
-// an image per workgroup (irh); NNSX_IRH=0 turns both off, NNSX_IRH=1 the
-// stride-2 one only (A/B)
+// an image per workgroup (irh).  Off by default: faster per block in isolation
+// (157.5 vs 188 / 109 vs 138 us at batch 512) but the sustained pipeline ran
+// 0.04 ms per invoke SLOWER with it on two boxes (3.986 / 4.023 vs 3.951 / 3.976
+// ms, 200- and 600-step runs: profiles/r6_power_throttle.txt).  Mode 2 = both,
+// 1 = the stride-2 one, 0 = off (NNSX_IRH, or irh_mode() at run time)
+std::atomic<int> g_irh_mode{[] {
+  const char* e = std::getenv("NNSX_IRH");
+  return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 0;
+}()};
+
 static bool irh_match(const IrBlockF32Args& a) {
-  static const int on = [] {
-    const char* e = std::getenv("NNSX_IRH");
-    return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : 2;
-  }();
+  const int on = g_irh_mode.load(std::memory_order_relaxed);
   const bool s1 = a.stride == 1 && a.cout == 32 && on >= 2;
   const bool s2 = a.stride == 2 && a.cout == 64 && !a.residual && on >= 1;
   return (s1 || s2) && a.dil == 1 && a.has_expand && a.H == kIrhW && a.W == kIrhW && a.cin == 32 &&
          a.hid % 32 == 0 && a.hid >= 64 && a.we3 && a.wp3 && a.B >= g_irp_min_b.load(std::memory_order_relaxed);
 }
+
+int irh_set_mode(int m) { return g_irh_mode.exchange(m); }
 
 bool irp_x3_supported(const IrBlockF32Args& a) {
   return irp_enabled() && (irps_match(a) || irh_match(a) || find_irp(a) != nullptr);

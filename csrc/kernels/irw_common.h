@@ -42,6 +42,8 @@ bool irp_x3_supported(const IrBlockF32Args& a);
 bool irp_x3(const IrBlockF32Args& a, hipStream_t s);
 // smallest batch the image-per-workgroup kernels take (default 128, NNSX_IRP_MIN_B); returns the old value
 int irp_x3_set_min_batch(int b);
+// the 28 x 28 half-image kernels (kernels/irp_x3.hip): 0 off, 1 stride 2, 2 both; returns the old mode
+int irh_set_mode(int m);
 
 namespace {
 

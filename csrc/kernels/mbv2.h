@@ -256,6 +256,8 @@ bool ir_block_f32(const IrBlockF32Args& a, hipStream_t s);
 const char* ir_block_f32_method(int stride, int H, int W, int cin, int hid, int cout, int B, int dil = 1);
 // the 14 x 14 image-per-workgroup kernels' smallest batch (kernels/irp_x3.hip); returns the old value
 int irp_x3_set_min_batch(int b);
+// the 28 x 28 half-image kernels (kernels/irp_x3.hip): 0 off, 1 stride 2, 2 both; returns the old mode
+int irh_set_mode(int m);
 
 }  // namespace kernels
 }  // namespace nnsx

@@ -912,6 +912,9 @@ TORCH_LIBRARY(nnsx, m) {
   m.def("irp_min_batch(int b) -> int", [](int64_t b) -> int64_t {
     return nnsx::kernels::irp_x3_set_min_batch(static_cast<int>(b));
   });
+  m.def("irh_mode(int m) -> int", [](int64_t m) -> int64_t {
+    return nnsx::kernels::irh_set_mode(static_cast<int>(m));
+  });
   m.def("pw_conv(Tensor x, Tensor wt, Tensor bias, Tensor? res, int N, int act, bool out_f32) -> Tensor");
   m.def("pw_conv_into(Tensor x, Tensor wt, Tensor bias, Tensor(a!) out, int row0, int n, int act) -> ()");
   m.def("pw_conv_rowbias(Tensor x, Tensor wt, Tensor bias, int N, int act) -> Tensor");

@@ -26,9 +26,11 @@ IRP_SHAPES = [(64, 384, 64), (64, 384, 96), (96, 576, 96)]
 def method():
     prev = torch.ops.nnsx.f32_math()
     prev_b = torch.ops.nnsx.irp_min_batch(1)  # (small test batches take the kernel too)
+    prev_h = torch.ops.nnsx.irh_mode(2)  # (the 28 x 28 half-image kernels: off by default)
     yield lambda m: torch.ops.nnsx.set_f32_math(m)
     torch.ops.nnsx.set_f32_math(prev)
     torch.ops.nnsx.irp_min_batch(prev_b)
+    torch.ops.nnsx.irh_mode(prev_h)
 
 
 @pytest.mark.parametrize("cin,hid,cout", IRP_SHAPES)
