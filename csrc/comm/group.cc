@@ -613,6 +613,7 @@ bool Group::init(const GroupSpec& in, std::string* err) {
   unconsumed_.assign(static_cast<size_t>(n), 0);
   allowed_.assign(static_cast<size_t>(n), kWindow);
   granted_.assign(static_cast<size_t>(n), kWindow);
+  recvd_since_grant_.assign(static_cast<size_t>(n), 0);
   active_.assign(static_cast<size_t>(n), 1);
   listed_upto_.assign(static_cast<size_t>(n), 0);
   engine_ = n > 1 || rccl();
@@ -824,8 +825,32 @@ void Group::progress() {
   cv_.notify_all();
 }
 
+bool Group::pending_out() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!failed_.empty()) return false;
+  for (int d = 0; d < size(); ++d)
+    if (d != grank_ && active_[static_cast<size_t>(d)] && !outbox_[static_cast<size_t>(d)].empty()) return true;
+  return false;
+}
+
 bool Group::wait_trigger() {
-  while (!stop_.load()) {
+  while (true) {
+    if (stop_.load()) {
+      // an orderly close flushes what send() accepted: rounds go on while a
+      // queued message has a member to go to (members that leave are dropped
+      // with theirs), for at most min(timeout, 10 s); a cancel does not wait
+      if (cancelled_.load() || !mesh_ || !pending_out()) return false;
+      const int64_t now = now_ns();
+      if (drain_deadline_ == 0)
+        drain_deadline_ = now + static_cast<int64_t>(std::min(spec_.timeout_ms, 10000)) * 1000000;
+      if (now > drain_deadline_) {
+        NNSX_LOGW("comm", "group ", spec_.name, " (member ", grank_, "): closing with undelivered messages");
+        return false;
+      }
+      // (a receiver that does not consume grants nothing: do not spin)
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+      return true;
+    }
     if (work_.load()) return true;
     if (mesh_) {
       const int st = mesh_->wait_tag(round_ + 1, [this] { return work_.load() || stop_.load(); }, 100);
@@ -934,6 +959,7 @@ bool Group::run_round(std::string* err) {
       if (d != grank_) {
         grant[static_cast<size_t>(d)] = static_cast<uint32_t>(std::max(0, kWindow - unconsumed_[static_cast<size_t>(d)]));
         granted_[static_cast<size_t>(d)] = static_cast<int>(grant[static_cast<size_t>(d)]);
+        recvd_since_grant_[static_cast<size_t>(d)] = 0;  // (this round's messages count against it)
       }
     }
   }
@@ -1041,7 +1067,10 @@ bool Group::run_round(std::string* err) {
       colls_.clear();
     }
     for (auto& p : got) {
-      if (p.src != grank_) ++unconsumed_[static_cast<size_t>(p.src)];
+      if (p.src != grank_) {
+        ++unconsumed_[static_cast<size_t>(p.src)];
+        ++recvd_since_grant_[static_cast<size_t>(p.src)];
+      }
       inbox_.push_back(std::move(p));
     }
     for (int d = 0; d < n; ++d) {
@@ -1540,8 +1569,12 @@ bool Group::recv(Packet* p, int timeout_ms, bool* timed_out, std::string* err) {
   const int s = p->src;
   if (engine_ && s != grank_ && s >= 0 && s < size()) {
     --unconsumed_[static_cast<size_t>(s)];
-    // the sender may be held back by the last grant: advertise the room
-    wake = granted_[static_cast<size_t>(s)] < kWindow;
+    // the sender may be held back by the last grant: advertise the room.  A
+    // partial grant can grow now; a full one the sender has used up (its credit
+    // is the grant minus what arrived since) leaves it unable to send until
+    // some member runs a round -- this one must
+    const size_t si = static_cast<size_t>(s);
+    wake = granted_[si] < kWindow || granted_[si] - recvd_since_grant_[si] <= 0;
   }
   lk.unlock();
   if (wake) {

@@ -297,6 +297,10 @@ class Group {
   bool collective(const std::shared_ptr<CollOp>& op, std::string* err);
   void progress();
   bool wait_trigger();
+  // stopping (not cancelled): messages still queued for a member that is in
+  // the group -- the engine runs rounds until they are out (bounded), so an
+  // orderly close never drops what send() accepted
+  bool pending_out();
   bool run_round(std::string* err);
   Message manifest_for(int d, uint32_t grant, const std::vector<std::shared_ptr<CollOp>>& colls,
                        const std::vector<Packet>& sends);
@@ -325,6 +329,8 @@ class Group {
   int op_timeout_ms_ = 60000;   // device completion deadline of an issued round
   std::thread thr_;
   std::atomic<bool> work_{false}, stop_{false}, cancelled_{false}, aborted_{false};
+  int64_t drain_deadline_ = 0;  // stopping with queued sends: the flush rounds end by then
+  std::vector<int> recvd_since_grant_;  // per sender: messages received since this member's last grant
   mutable std::mutex mu_;       // everything below, shared by callers and the progress thread
   std::condition_variable cv_;  // collective completion, inbox, outbox room
   std::string failed_;          // fatal error ("" while healthy)

@@ -103,6 +103,32 @@ def main():
 
     g = nns.Group("test/collectives", rank, world, f"127.0.0.1:{port}", dev, backend, 60000)
     res = {"rank": rank, "backend": g.backend, "size": g.size}
+    if mode in ("flush", "credit"):
+        # member 1 queues 20 messages for member 0 (2.5 credit windows); member 0
+        # starts receiving a second later.  flush: member 1 closes the group at
+        # once -- the orderly close must deliver all of them; credit: member 1
+        # stays (waits for an ack) -- member 0's receives must refresh the credit
+        # member 1 used up
+        import time
+
+        if rank == 1:
+            for k in range(20):
+                g.send(0, nns.Packet([arr(np.full(4, k, np.float32))], pts=k))
+            if mode == "credit":
+                ack = g.recv(60000)
+                res["ack"] = None if ack is None else ack.pts
+        elif rank == 0:
+            time.sleep(1.0)
+            got = []
+            for _ in range(20):
+                p = g.recv(30000)
+                got.append(None if p is None else [p.src, p.pts, float(p.blobs[0].numpy("float32")[0])])
+            res["flush"] = got
+            if mode == "credit":
+                g.send(1, nns.Packet([arr(np.zeros(1, np.float32))], pts=99))
+        del g
+        print(json.dumps(res), flush=True)
+        return
     if mode == "big":
         big(g, rank, world, arr, res)
         res["bytes_sent"] = g.bytes_sent

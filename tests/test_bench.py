@@ -79,7 +79,7 @@ def test_bench_selfcheck_fault_never_blocks_headline():
 
     t0 = time.time()
     r = _run(["--cpu", "--gpus", "3", "--steps", "2", "--warmup", "1", "--batch", "1", "--latency-frames", "0",
-              "--sweep", "", "--extra-configs", "", "--selfcheck-timeout-ms", "4000"],
+              "--sweep", "", "--extra-configs", "", "--selfcheck-timeout-ms", "10000"],
              env={"NNSX_SELFCHECK_FAULT": "1:broadcast"})
     assert r.returncode == 0, r.stderr[-3000:]
     assert time.time() - t0 < 150

@@ -197,20 +197,29 @@ def test_bench_posenet_multi_two_ranks_cpu():
     assert d["mux_sets_rank0"] == 3  # warmup + steps batches, every one a full 2-camera set
 
 
-def test_bench_deeplab_fan_three_ranks_cpu():
-    """BASELINE.json config 4 through bench.py: rank 0 holds the three cameras,
-    tensor_mux -> tensor_demux; pad 0 feeds its own DeepLab branch, pads 1 and 2
-    go to ranks 1 and 2 through edgesink connect-type=RCCL (two-member groups)."""
+@pytest.mark.parametrize("fan", ["rccl", "shm"])
+def test_bench_deeplab_fan_three_ranks_cpu(fan):
+    """BASELINE.json config 4 through bench.py, both fan-out transports.  rccl:
+    rank 0 holds the three cameras, tensor_mux -> tensor_demux; pad 0 feeds its
+    own DeepLab branch, pads 1 and 2 go to ranks 1 and 2 through edgesink
+    connect-type=RCCL (two-member groups).  shm (the default): rank 0 renders
+    cameras 1 and 2 into shared rings and publishes them with edgesink
+    connect-type=SHM; ranks 1 and 2 subscribe and ingest their own camera."""
     import json
     port = _free_port()
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-                        "--gpus", "3", "--cpu", "--config", "deeplab_fan", "--batch", "1", "--steps", "2", "--warmup", "1"],
+                        "--gpus", "3", "--cpu", "--config", "deeplab_fan", "--batch", "1", "--steps", "2", "--warmup", "1",
+                        "--fan-transport", fan],
                        capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
-    assert d["config"]["parallelism"].startswith("tensor_demux fan-out 1->3") and d["value"] > 0
-    assert "tensor_demux name=d" in d["config"]["pipeline"]
+    if fan == "rccl":
+        assert d["config"]["parallelism"].startswith("tensor_demux fan-out 1->3") and d["value"] > 0
+        assert "tensor_demux name=d" in d["config"]["pipeline"]
+    else:
+        assert d["config"]["parallelism"].startswith("shared-ring fan-out 1->3") and d["value"] > 0
+        assert "pool-shm=" in d["config"]["pipeline"] and "connect-type=SHM" in d["config"]["pipeline"]
 
 
 def test_ini_rccl_and_hip_sections(tmp_path):
