@@ -107,8 +107,10 @@ def parse_args(argv=None):
                          "printed with aux_timeout and every rank exits 0")
     ap.add_argument("--cpu", action="store_true", help="CPU reference path (device=-1, torch CPU)")
     # (depth 1 / 1: same frames/s as 4 / 2 at batch 512, p50 23 vs 37 ms: profiles/r4_mbv2_ab_b512.txt q11)
-    ap.add_argument("--queue", type=int, default=1, help="queue depth between filter and decoder")
-    ap.add_argument("--queue-in", type=int, default=1, help="queue depth between converter and filter")
+    ap.add_argument("--queue", type=int, default=int(os.environ.get("NNSX_BENCH_QUEUE", "1")),
+                    help="queue depth between filter and decoder")
+    ap.add_argument("--queue-in", type=int, default=int(os.environ.get("NNSX_BENCH_QUEUE_IN", "1")),
+                    help="queue depth between converter and filter")
     ap.add_argument("--model-broadcast", default=os.environ.get("NNSX_BENCH_BCAST", "auto"),
                     choices=["off", "tcp", "rccl", "auto"],
                     help="N > 1: rank 0 broadcasts the model bytes to every rank at load over this data plane")

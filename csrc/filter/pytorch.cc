@@ -116,6 +116,7 @@ class TorchInstance : public FilterInstance {
   }
   ~TorchInstance() override {
     if (device_ >= 0 && device_ < 64) g_device_instances[device_].fetch_sub(1);
+    print_trace_wait();
     clear_graphs();
     for (Lane& l : lanes_) {
       hip::DeviceGuard g(l.dev);
@@ -559,6 +560,14 @@ class TorchInstance : public FilterInstance {
       sg = std::make_unique<c10::hip::HIPStreamGuardMasqueradingAsCUDA>(
           c10::hip::getStreamFromExternalMasqueradingAsCUDA(s, static_cast<c10::DeviceIndex>(dev_idx)));
     }
+    // NNSX_TRACE_WAIT=1 (diagnostics): events at the invoke's start on the
+    // stream, before the replay and after it -- printed at teardown as the
+    // device time spent waiting for the inputs and in the graph, per invoke
+    hipEvent_t tw_a = nullptr, tw_b = nullptr, tw_c = nullptr;
+    if (trace_wait() && dev_idx >= 0) {
+      for (hipEvent_t* e : {&tw_a, &tw_b, &tw_c}) hip::check(hipEventCreate(e), "trace event");
+      hip::check(hipEventRecord(tw_a, s), "trace event");
+    }
     std::vector<at::Tensor> inputs;
     for (size_t i = 0; i < in.size(); ++i) {
       TensorInfo ti = i < info.num_tensors ? info.at(static_cast<unsigned>(i)) : TensorInfo();
@@ -634,7 +643,13 @@ class TorchInstance : public FilterInstance {
       // (shared-tensor-filter-key) each bring their own stream, so a replay on a
       // new stream first waits for the last one
       if (ln.last_ev && ln.last_stream != s) hip::check(hipStreamWaitEvent(s, ln.last_ev, 0), "replay order wait");
+      if (tw_b) hip::check(hipEventRecord(tw_b, s), "trace event");
       hip::check(hipGraphLaunch(gs->graph->raw_cuda_graph_exec(), s), "hipGraphLaunch");
+      if (tw_c) {
+        hip::check(hipEventRecord(tw_c, s), "trace event");
+        trace_.push_back({tw_a, tw_b, tw_c});
+        tw_a = tw_b = tw_c = nullptr;
+      }
       if (copy_out_ || gs->copy_out) {  // private copies of the outputs: the instance is free again
         for (size_t k = 0; k < gs->static_out.size(); ++k) {
           const at::Tensor& t = gs->static_out[k];
@@ -684,6 +699,8 @@ class TorchInstance : public FilterInstance {
       if (dev_idx < 0 && t.is_cuda()) t = t.cpu();
       out->push_back(wrap_output(t, dev_idx, s, held));
     }
+    for (hipEvent_t e : {tw_a, tw_b, tw_c})  // (an eager invoke: not traced)
+      if (e) (void)hipEventDestroy(e);
     return 0;
   }
 
@@ -877,6 +894,36 @@ class TorchInstance : public FilterInstance {
     hipStream_t last_stream = nullptr;
   };
   std::vector<Lane> lanes_ = std::vector<Lane>(kMaxLanes);
+  static bool trace_wait() {
+    static const bool on = [] {
+      const char* e = std::getenv("NNSX_TRACE_WAIT");
+      return e && e[0] == '1';
+    }();
+    return on;
+  }
+  struct TraceWait {
+    hipEvent_t a, b, c;
+  };
+  std::vector<TraceWait> trace_;  // NNSX_TRACE_WAIT: (invoke start, replay start, replay end) per replay
+  void print_trace_wait() {
+    if (trace_.empty()) return;
+    std::string w = "input-wait ms", g = "graph ms", gap = "start-after-prev-end ms";
+    for (size_t i = 0; i < trace_.size(); ++i) {
+      auto& t = trace_[i];
+      if (hipEventSynchronize(t.c) != hipSuccess) break;
+      float x = 0.f, y = 0.f, z = 0.f;
+      (void)hipEventElapsedTime(&x, t.a, t.b);
+      (void)hipEventElapsedTime(&y, t.b, t.c);
+      if (i > 0) (void)hipEventElapsedTime(&z, trace_[i - 1].c, t.b);
+      w += strfmt(" ", static_cast<int>(x * 1000));
+      g += strfmt(" ", static_cast<int>(y * 1000));
+      gap += strfmt(" ", static_cast<int>(z * 1000));
+    }
+    std::fprintf(stderr, "pytorch filter (us per replay)\n%s\n%s\n%s\n", w.c_str(), g.c_str(), gap.c_str());
+    for (auto& t : trace_)
+      for (hipEvent_t e : {t.a, t.b, t.c}) (void)hipEventDestroy(e);
+    trace_.clear();
+  }
   int lanes_opt_ = 0;  // custom=lanes:<n>; 0 = auto
   bool graphs_shared_ = false;  // graphs_ were captured under kernels::SharedDeviceScope
   uint64_t invokes_ = 0;
