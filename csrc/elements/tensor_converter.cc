@@ -398,10 +398,19 @@ class TensorConverter : public Element {
                    "ring upload");
         done += r.second;
       }
+      // one use record per source allocation: the frames of a ring are views
+      // of one block, whose use event is re-recorded by every record_use on the
+      // same stream (Memory::record_use_self) -- 512 per batch cost ~2.5-4 ms of
+      // converter-thread time in hipEventRecord, the sustained headline's
+      // bottleneck on slower hosts (profiles/r6_host_bound_converter.txt)
+      const Memory* last_root = nullptr;
       for (size_t left = size; left > 0;) {
         Piece& p = adapter_.front();
         const size_t n = std::min(left, p.size() - p.off);
-        p.mem->record_use(s, dev);
+        if (p.mem->root() != last_root) {
+          p.mem->record_use(s, dev);
+          last_root = p.mem->root();
+        }
         p.off += n;
         left -= n;
         if (p.off == p.size()) adapter_.pop_front();
@@ -509,8 +518,12 @@ class TensorConverter : public Element {
     kernels::unpad_rows(sp, out->data(), static_cast<uint32_t>(ps.size()), static_cast<uint32_t>(row),
                         static_cast<uint32_t>(stride), static_cast<uint32_t>(rows), spacing, s);
     stg->record_use(s, dev);
+    const Memory* last_root = nullptr;  // (one use record per source allocation, as above)
     for (size_t i = 0; i < ps.size(); ++i) {
-      adapter_.front().mem->record_use(s, dev);
+      if (adapter_.front().mem->root() != last_root) {
+        adapter_.front().mem->record_use(s, dev);
+        last_root = adapter_.front().mem->root();
+      }
       adapter_.pop_front();
     }
     return true;

@@ -1232,14 +1232,14 @@ static bool irps_match(const IrBlockF32Args& a) {
 }
 
 // the 28 x 28 32 -> 192 -> 32 block and the 28 -> 14 32 -> 192 -> 64 one, half
-// an image per workgroup (irh).  Off by default: faster per block in isolation
-// (157.5 vs 188 / 109 vs 138 us at batch 512) but the sustained pipeline ran
-// 0.04 ms per invoke SLOWER with it on two boxes (3.986 / 4.023 vs 3.951 / 3.976
-// ms, 200- and 600-step runs: profiles/r6_power_throttle.txt).  Mode 2 = both,
-// 1 = the stride-2 one, 0 = off (NNSX_IRH, or irh_mode() at run time)
+// an image per workgroup (irh): 157.5 vs 188 / 109 vs 138 us at batch 512, and
+// the sustained pipeline 3.753 vs 3.866 ms per invoke on the same box
+// (profiles/r6_host_bound_converter.txt; an earlier A/B that had it slower was
+// bound by the converter's per-frame event records, not the GPU).  Mode 2 =
+// both (default), 1 = the stride-2 one, 0 = off (NNSX_IRH, or irh_mode() at run time)
 std::atomic<int> g_irh_mode{[] {
   const char* e = std::getenv("NNSX_IRH");
-  return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 0;
+  return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 2;
 }()};
 
 static bool irh_match(const IrBlockF32Args& a) {
