@@ -191,6 +191,8 @@ class ImageSegment : public DecoderInstance {
     out->at(0).dim = make_dims({4, rs ? out_w_ : w, rs ? out_h_ : h, batch});
     return true;
   }
+  // the depth mode reduces through ws_; the label modes write only `out`
+  bool stage_lane_safe() const override { return mode_ != SNPE_DEPTH; }
   bool stage_enqueue(const std::vector<const void*>& in, const std::vector<void*>& out, hipStream_t s) override {
     if (in.empty() || out.size() != 1) return false;
     enqueue_device(static_cast<const float*>(in[0]), st_w_, st_h_, st_batch_, static_cast<uint32_t*>(out[0]), s);

@@ -46,6 +46,7 @@ class InstanceStage : public DecodeStage {
     return inst_->stage_enqueue(in, out, static_cast<hipStream_t>(stream));
   }
   bool stale() const override { return stale_.load(); }
+  bool lane_safe() const override { return inst_->stage_lane_safe(); }
   void revoke() { stale_.store(true); }
 
  private:

@@ -932,11 +932,11 @@ class TorchInstance : public FilterInstance {
       const char* e = std::getenv("NNSX_TORCH_LANES");
       return e ? std::max(0, std::min(kMaxLanes, std::atoi(e))) : 0;
     }();
-    // an absorbed decoder stage keeps its scratch (candidate lists, keypoint and
-    // label buffers) in the stage object, and every lane's graph would capture
-    // the same buffers: concurrent replays on two lanes would share them.  One
-    // lane then, whatever custom=lanes asks for.
-    if (stage_) return 1;
+    // an absorbed decoder stage with scratch of its own (candidate lists,
+    // keypoint buffers) would have every lane's graph capture the same buffers:
+    // concurrent replays on two lanes would share them.  One lane then, whatever
+    // custom=lanes asks for; stages that write only their outputs may have lanes.
+    if (stage_ && !stage_->lane_safe()) return 1;
     if (forced > 0) return forced;
     if (lanes_opt_ > 0) return lanes_opt_;
     if (inputs.empty() || inputs[0].dim() < 1) return 1;

@@ -86,6 +86,10 @@ class DecodeStage {
   // prepared: graphs captured with it run the old post-processing.  The filter
   // checks it before every invoke and re-takes a fresh stage (re-capturing).
   virtual bool stale() const { return false; }
+  // true when enqueue() touches no buffer of the stage's own (only `in` and
+  // `out`): graphs captured with it on several replay lanes may then run
+  // concurrently.  Stages with scratch (candidate lists, keypoints) say false.
+  virtual bool lane_safe() const { return false; }
 };
 
 class DecodeStageConsumer {  // implemented by tensor_decoder

@@ -221,6 +221,9 @@ class DecoderInstance {
     (void)s;
     return false;
   }
+  // stage_enqueue writes only its `out` buffers (no scratch of the instance):
+  // the stage may be replayed on several lanes at once (DecodeStage::lane_safe)
+  virtual bool stage_lane_safe() const { return false; }
   virtual bool accept_argmax_input(uint32_t classes) {
     (void)classes;
     return false;

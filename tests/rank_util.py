@@ -11,11 +11,29 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """A MASTER_PORT P such that P and P + 17 are both free: comm::Group derives
+    its control-plane store from MASTER_PORT + 17 (group.cc), and when that port
+    is taken -- e.g. the local end of an unrelated outgoing connection -- the
+    first member takes it for another member's store and the group fails."""
+    for _ in range(64):
+        socks = []
+        try:
+            s = socket.socket()
+            s.bind(("127.0.0.1", 0))
+            socks.append(s)
+            p = s.getsockname()[1]
+            if p + 17 > 65535:
+                continue
+            t = socket.socket()
+            socks.append(t)
+            t.bind(("127.0.0.1", p + 17))
+            return p
+        except OSError:
+            continue
+        finally:
+            for x in socks:
+                x.close()
+    raise RuntimeError("no free port pair")
 
 
 def run_ranks(world, devices, backend, timeout=240, mode="small"):

@@ -72,11 +72,14 @@ def test_decoder_stage_in_graph_matches_own_kernels(nns, workdir, case, B, graph
         assert any(any(x) for x in got[:4])  # something was drawn
 
 
-@pytest.mark.parametrize("case", ["ssd", "posenet"])
+@pytest.mark.parametrize("case", ["ssd", "posenet", "deeplab"])
 def test_decoder_stage_with_replay_lanes_asked(nns, workdir, case):
-    """custom=lanes:3 with a decoder stage absorbed: the stage's scratch lives in
-    the stage object, so the filter replays on one lane (lane_count); the frames
-    equal, byte for byte, the decoder running its own kernels"""
+    """custom=lanes:3 with a decoder stage absorbed.  SSD's and PoseNet's stages
+    keep scratch in the stage object, so the filter replays on one lane
+    (lane_count); DeepLab's (resize + argmax + colour map) writes only its output
+    frames (DecodeStage::lane_safe), so its graphs replay on three lanes at once.
+    Either way the frames equal, byte for byte, the decoder running its own
+    kernels"""
     got, info = _run(nns, workdir, case, 4, True, True, True, lanes=3)
     ref, _ = _run(nns, workdir, case, 4, False, True, True, lanes=3)
     assert info == ("dec", "f"), info

@@ -5,7 +5,6 @@ though each rank's model= points at a different file.  Two processes launched
 like torchrun (RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT)."""
 import json
 import os
-import socket
 import subprocess
 import sys
 import textwrap
@@ -23,7 +22,7 @@ RANK_SCRIPT = textwrap.dedent(r'''
     path = os.path.join(sys.argv[2], f"m{rank}.pt")
     torch.jit.script(m).save(path)
     caps = "other/tensors,format=static,num_tensors=1,dimensions=4,types=float32,framerate=0/1"
-    p = nns.parse_launch(f"appsrc name=src caps={caps} ! tensor_filter framework=pytorch model={path} "
+    p = nns.parse_launch(f"appsrc name=src caps={caps} ! tensor_filter name=f framework=pytorch model={path} "
                          "accelerator=false custom=broadcast:0,broadcast-backend:tcp,broadcast-name:t "
                          "! tensor_sink name=sink")
     out = []
@@ -32,18 +31,17 @@ RANK_SCRIPT = textwrap.dedent(r'''
     p.get_by_name("src").push_buffer(np.arange(4, dtype=np.float32), pts=0)
     p.get_by_name("src").end_of_stream()
     assert p.wait(60)[0] == "eos", p.messages()
+    group = p.get_by_name("f").get_property("model-broadcast")
     p.stop()
     own = m(torch.arange(4, dtype=torch.float32)).tolist()
-    print(json.dumps({"rank": rank, "out": out[0], "own": own}), flush=True)
+    print(json.dumps({"rank": rank, "out": out[0], "own": own, "group": group}), flush=True)
 ''')
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    from rank_util import free_port
+
+    return free_port()
 
 
 def test_model_broadcast_two_ranks(tmp_path):
@@ -63,6 +61,7 @@ def test_model_broadcast_two_ranks(tmp_path):
         d = json.loads([line for line in out.splitlines() if line.startswith("{")][-1])
         res[d["rank"]] = d
     # both ranks computed with rank 0's weights
+    assert not res[1]["group"].startswith("failed"), (res, err[-3000:])
     assert res[0]["out"] == res[1]["out"]
     assert max(abs(a - b) for a, b in zip(res[0]["out"], res[0]["own"])) < 1e-6
     assert max(abs(a - b) for a, b in zip(res[1]["out"], res[1]["own"])) > 1e-3  # rank 1's own file differs

@@ -9,7 +9,6 @@ MASTER_ADDR / MASTER_PORT).  The RCCL data plane is covered by
 tests/test_gpu_comm.py (one GPU: single-member groups) and by the
 multi-GPU bench."""
 import os
-import socket
 import subprocess
 import sys
 import textwrap
@@ -22,11 +21,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    from rank_util import free_port
+
+    return free_port()
 
 
 def _rank(k, n, store, extra=""):
