@@ -41,8 +41,30 @@ namespace kernels {
 namespace {
 
 constexpr int kIrpH = 14;           // map size handled (S = 1)
-constexpr int kIrpRow = 16;         // hidden grid row pitch (cells): 14 + 2 border
-constexpr int kIrpCells = 16 * kIrpRow + 16;  // + one scratch row for the padding lanes
+// hidden grid row pitch (cells): 14 + 2 border + 1 pad.  The depthwise reads
+// (ds_read_b128, lane = pixel pair li of rows r0 / r0 + 1, quad 2 g + qq) put
+// lanes li and li + 7 -- same columns, adjacent rows -- on the same bank slot
+// at a 16-cell pitch (2-way in every lane group); at 17 the next row moves one
+// 16-B slot over and all 16 lanes of a group land on distinct slots.
+constexpr int kIrpRow = 17;
+constexpr int kIrpCells = 16 * kIrpRow + 16;  // + one scratch row for the padding lanes (a multiple of 16 slots)
+
+// Physical 16-B chunk of chunk `ch` of weight row `row` in a stage of NCH
+// chunks per row (rows unpadded).  An MFMA A-fragment read has lane (li, g)
+// read row 16 t + li, chunk 4 c + g; ds_read_b128 serves a wave in four 16-lane
+// groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}, + 32) on 64 banks = 16 slots,
+// so a plain or odd-padded pitch leaves two lanes per slot (2-way).  The XOR
+// below gives every group 16 distinct slots for NCH = 4, 8, 12 (checked for
+// every row / k-step by scripts/lds_banks.py) and keeps the chunk inside its
+// row (a bijection of 0..NCH-1).
+template <int NCH>
+__device__ __forceinline__ int wsw(int row, int ch) {
+  static_assert(NCH == 4 || NCH == 8 || NCH == 12, "wsw: chunks per row");
+  if constexpr (NCH == 8)
+    return ch ^ (2 * ((row >> 1) & 3));
+  else
+    return ch ^ ((0x1320 >> (4 * ((row >> 2) & 3))) & 3);  // {0, 2, 3, 1}[(row >> 2) & 3]
+}
 
 // TPW = 16-pixel MFMA tiles per wave: 2 -> 7 waves, a wave owns a row pair and
 // its lanes hold horizontal pixel pairs (the depthwise reads one 3 x 4 window
@@ -54,8 +76,8 @@ struct IrpGeom {
   static constexpr int NW = 14 / TPW, NT = 64 * NW;
   static constexpr int NK32 = CIN / 32;        // expand k-steps
   static constexpr int NO16 = COUT / 16;       // project output tiles
-  static constexpr int WEP = CIN / 8 + 1;      // expand weight row pitch (16-B chunks): odd -> conflict-free
-  static constexpr int WPP = 32 / 8 + 1;       // project weight row pitch (chunks)
+  static constexpr int WEP = CIN / 8;          // expand weight row pitch (16-B chunks, swizzled: wsw)
+  static constexpr int WPP = 32 / 8;           // project weight row pitch (chunks, swizzled)
   static constexpr size_t hid_b = static_cast<size_t>(8) * kIrpCells * 16;      // [quad][cell] f32x4
   static constexpr size_t we_b = static_cast<size_t>(3) * 32 * WEP * 16;        // [part][hid row][chunk]
   static constexpr size_t wp_b = static_cast<size_t>(3) * COUT * WPP * 16;      // [part][cout row][chunk]
@@ -129,7 +151,7 @@ __global__ void __launch_bounds__((IrpGeom<CIN, COUT, TPW, XL>::NT), (IrpGeom<CI
       if (v < G::WE_CH - 8) {
         const int p = v / (32 * (CIN / 8)), r = v - p * 32 * (CIN / 8);
         const int h = r / (CIN / 8), kc = r - h * (CIN / 8);
-        *reinterpret_cast<u32x4_t*>(wel + ((p * 32 + h) * WEP + kc) * 16) = we_st[it];
+        *reinterpret_cast<u32x4_t*>(wel + ((p * 32 + h) * WEP + wsw<WEP>(h, kc)) * 16) = we_st[it];
       } else {
         *reinterpret_cast<u32x4_t*>(bel + 4 * (v - (G::WE_CH - 8))) = we_st[it];
       }
@@ -158,7 +180,7 @@ __global__ void __launch_bounds__((IrpGeom<CIN, COUT, TPW, XL>::NT), (IrpGeom<CI
       if (v < G::WP_CH - 80) {
         const int p = v / (COUT * 4), r = v - p * COUT * 4;
         const int co = r >> 2, kc = r & 3;
-        *reinterpret_cast<u32x4_t*>(wpl + ((p * COUT + co) * WPP + kc) * 16) = wp_st[it];
+        *reinterpret_cast<u32x4_t*>(wpl + ((p * COUT + co) * WPP + wsw<WPP>(co, kc)) * 16) = wp_st[it];
       } else {
         const int q = v - (G::WP_CH - 80);
         *reinterpret_cast<u32x4_t*>(wdl + 4 * q) = wp_st[it];
@@ -241,7 +263,7 @@ __global__ void __launch_bounds__((IrpGeom<CIN, COUT, TPW, XL>::NT), (IrpGeom<CI
 #pragma unroll
       for (int ht = 0; ht < 2; ++ht) {
         X3Frag wa;
-        const char* wr = wel + ((ht * 16 + li) * WEP + 4 * c + g) * 16;
+        const char* wr = wel + ((ht * 16 + li) * WEP + wsw<WEP>(li, 4 * c + g)) * 16;
         wa.h = *reinterpret_cast<const bf16x8_t*>(wr);
         wa.m = *reinterpret_cast<const bf16x8_t*>(wr + 32 * WEP * 16);
         wa.l = *reinterpret_cast<const bf16x8_t*>(wr + 2 * 32 * WEP * 16);
@@ -295,7 +317,7 @@ __global__ void __launch_bounds__((IrpGeom<CIN, COUT, TPW, XL>::NT), (IrpGeom<CI
 #pragma unroll
     for (int o = 0; o < NO16; ++o) {
       X3Frag wa;
-      const char* wr = wpl + ((o * 16 + li) * WPP + g) * 16;
+      const char* wr = wpl + ((o * 16 + li) * WPP + wsw<WPP>(li, g)) * 16;
       wa.h = *reinterpret_cast<const bf16x8_t*>(wr);
       wa.m = *reinterpret_cast<const bf16x8_t*>(wr + COUT * WPP * 16);
       wa.l = *reinterpret_cast<const bf16x8_t*>(wr + 2 * COUT * WPP * 16);
@@ -340,7 +362,7 @@ template <int CIN, int COUT, int TPW>
 struct IrppGeom {
   static constexpr int NW = 14 / TPW, NT = 64 * NW;
   static constexpr int NK32 = CIN / 32, NO16 = COUT / 16;
-  static constexpr int WEP = CIN / 8 + 1, WPP = 32 / 8 + 1;
+  static constexpr int WEP = CIN / 8, WPP = 32 / 8;  // swizzled rows (wsw)
   static constexpr size_t hid1 = static_cast<size_t>(8) * kIrpCells * 16;
   static constexpr size_t we_w = static_cast<size_t>(3) * 32 * WEP * 16;     // expand weights of a stage
   static constexpr size_t we1 = we_w + 32 * 4;                               // + expand bias
@@ -408,7 +430,7 @@ __global__ void __launch_bounds__((IrppGeom<CIN, COUT, TPW>::NT), (IrppGeom<CIN,
       if (v < G::WE_CH - 8) {
         const int p = v / (32 * (CIN / 8)), r = v - p * 32 * (CIN / 8);
         const int h = r / (CIN / 8), kc = r - h * (CIN / 8);
-        *reinterpret_cast<u32x4_t*>(wel + ((p * 32 + h) * WEP + kc) * 16) = we_st[it];
+        *reinterpret_cast<u32x4_t*>(wel + ((p * 32 + h) * WEP + wsw<WEP>(h, kc)) * 16) = we_st[it];
       } else {
         *reinterpret_cast<u32x4_t*>(wel + G::we_w + 16 * (v - (G::WE_CH - 8))) = we_st[it];
       }
@@ -438,7 +460,7 @@ __global__ void __launch_bounds__((IrppGeom<CIN, COUT, TPW>::NT), (IrppGeom<CIN,
       if (v < G::WP_CH - 80) {
         const int p = v / (COUT * 4), r = v - p * COUT * 4;
         const int co = r >> 2, kc = r & 3;
-        *reinterpret_cast<u32x4_t*>(wpl + ((p * COUT + co) * WPP + kc) * 16) = wp_st[it];
+        *reinterpret_cast<u32x4_t*>(wpl + ((p * COUT + co) * WPP + wsw<WPP>(co, kc)) * 16) = wp_st[it];
       } else {
         *reinterpret_cast<u32x4_t*>(wpl + G::wp_w + 16 * (v - (G::WP_CH - 80))) = wp_st[it];
       }
@@ -477,7 +499,7 @@ __global__ void __launch_bounds__((IrppGeom<CIN, COUT, TPW>::NT), (IrppGeom<CIN,
 #pragma unroll
       for (int ht = 0; ht < 2; ++ht) {
         X3Frag wa;
-        const char* wr = wel + ((ht * 16 + li) * WEP + 4 * c + g) * 16;
+        const char* wr = wel + ((ht * 16 + li) * WEP + wsw<WEP>(li, 4 * c + g)) * 16;
         wa.h = *reinterpret_cast<const bf16x8_t*>(wr);
         wa.m = *reinterpret_cast<const bf16x8_t*>(wr + 32 * WEP * 16);
         wa.l = *reinterpret_cast<const bf16x8_t*>(wr + 2 * 32 * WEP * 16);
@@ -536,7 +558,7 @@ __global__ void __launch_bounds__((IrppGeom<CIN, COUT, TPW>::NT), (IrppGeom<CIN,
 #pragma unroll
     for (int o = 0; o < NO16; ++o) {
       X3Frag wa;
-      const char* wr = wpl + ((o * 16 + li) * WPP + g) * 16;
+      const char* wr = wpl + ((o * 16 + li) * WPP + wsw<WPP>(li, g)) * 16;
       wa.h = *reinterpret_cast<const bf16x8_t*>(wr);
       wa.m = *reinterpret_cast<const bf16x8_t*>(wr + COUT * WPP * 16);
       wa.l = *reinterpret_cast<const bf16x8_t*>(wr + 2 * COUT * WPP * 16);
@@ -607,9 +629,9 @@ __global__ void __launch_bounds__((IrppGeom<CIN, COUT, TPW>::NT), (IrppGeom<CIN,
 //     (their buffers' readers finished before the step began), so the staging
 //     registers live across one phase only;
 //   * LDS: a 15 x 15 bordered hidden grid (the stride-2 windows never reach row
-//     or column 15), expand stages with an odd chunk pitch, project stages
-//     unpadded with the chunk index XOR-swizzled by row (16 lanes reading 16
-//     rows hit 16 distinct 16-byte bank groups); double-buffered: 158 KB.
+//     or column 15), expand and project stages unpadded with the chunk index
+//     XOR-swizzled by row (wsw: every ds_read_b128 lane group on 16 distinct
+//     16-byte bank slots); double-buffered: 155 KB.
 constexpr int kIrpsG = 15;                    // hidden grid (bordered): cell (y + 1, x + 1)
 constexpr int kIrpsCells = kIrpsG * kIrpsG;   // 225
 
@@ -617,7 +639,7 @@ template <int CIN, int COUT>
 struct IrpsGeom {
   static constexpr int NW = 8, NT = 64 * NW;
   static constexpr int NK32 = CIN / 32, NO16 = COUT / 16, NOH = NO16 / 2;
-  static constexpr int WEP = CIN / 8 + 1;
+  static constexpr int WEP = CIN / 8;  // expand weight row pitch (16-B chunks, swizzled: wsw)
   static constexpr size_t hid1 = static_cast<size_t>(8) * kIrpsCells * 16;
   static constexpr size_t we_w = static_cast<size_t>(3) * 32 * WEP * 16;
   static constexpr size_t we1 = we_w + 32 * 4;
@@ -687,7 +709,7 @@ __global__ void __launch_bounds__(512, 2) irps_x3_kernel(IrBlockF32Args a) {
       if (v < G::WE_CH - 8) {
         const int p = v / (32 * (CIN / 8)), r = v - p * 32 * (CIN / 8);
         const int h = r / (CIN / 8), kc = r - h * (CIN / 8);
-        *reinterpret_cast<u32x4_t*>(wel + ((p * 32 + h) * WEP + kc) * 16) = we_st[it];
+        *reinterpret_cast<u32x4_t*>(wel + ((p * 32 + h) * WEP + wsw<WEP>(h, kc)) * 16) = we_st[it];
       } else {
         *reinterpret_cast<u32x4_t*>(wel + G::we_w + 16 * (v - (G::WE_CH - 8))) = we_st[it];
       }
@@ -708,7 +730,7 @@ __global__ void __launch_bounds__(512, 2) irps_x3_kernel(IrBlockF32Args a) {
       }
     }
   };
-  // project stage: [part][row][chunk ^ ((row >> 2) & 3)]
+  // project stage: [part][row][wsw<4>(row, chunk)]
   auto wp_store = [&](int i) {
     char* wpl = wpbuf(i);
 #pragma unroll
@@ -718,7 +740,7 @@ __global__ void __launch_bounds__(512, 2) irps_x3_kernel(IrBlockF32Args a) {
       if (v < G::WP_CH - 80) {
         const int p = v / (COUT * 4), r = v - p * COUT * 4;
         const int co = r >> 2, kc = r & 3;
-        *reinterpret_cast<u32x4_t*>(wpl + ((p * COUT + co) * 4 + (kc ^ ((co >> 2) & 3))) * 16) = wp_st[it];
+        *reinterpret_cast<u32x4_t*>(wpl + ((p * COUT + co) * 4 + wsw<4>(co, kc)) * 16) = wp_st[it];
       } else {
         *reinterpret_cast<u32x4_t*>(wpl + G::wp_w + 16 * (v - (G::WP_CH - 80))) = wp_st[it];
       }
@@ -760,7 +782,7 @@ __global__ void __launch_bounds__(512, 2) irps_x3_kernel(IrBlockF32Args a) {
 #pragma unroll
       for (int ht = 0; ht < 2; ++ht) {
         X3Frag wa;
-        const char* wr = wel + ((ht * 16 + li) * WEP + 4 * c + g) * 16;
+        const char* wr = wel + ((ht * 16 + li) * WEP + wsw<WEP>(li, 4 * c + g)) * 16;
         wa.h = *reinterpret_cast<const bf16x8_t*>(wr);
         wa.m = *reinterpret_cast<const bf16x8_t*>(wr + 32 * WEP * 16);
         wa.l = *reinterpret_cast<const bf16x8_t*>(wr + 2 * 32 * WEP * 16);
@@ -811,7 +833,7 @@ __global__ void __launch_bounds__(512, 2) irps_x3_kernel(IrBlockF32Args a) {
 #pragma unroll
     for (int oi = 0; oi < NOH; ++oi) {
       const int row = (o0 + oi) * 16 + li;
-      const char* wr = wpl + (row * 4 + (g ^ ((row >> 2) & 3))) * 16;
+      const char* wr = wpl + (row * 4 + wsw<4>(row, g)) * 16;
       X3Frag wa;
       wa.h = *reinterpret_cast<const bf16x8_t*>(wr);
       wa.m = *reinterpret_cast<const bf16x8_t*>(wr + COUT * 64);
@@ -892,7 +914,7 @@ struct IrhGeom {
   // hidden grid rows: S = 1 16 (15 expand rows + a border row); S = 2 15 (the
   // windows never reach the last expand row of the top half)
   static constexpr int GH = S == 1 ? 16 : 15, CELLS = kIrhGW * GH;
-  static constexpr int WEP = CIN / 8 + 1;
+  static constexpr int WEP = CIN / 8;  // expand weight row pitch (16-B chunks, swizzled: wsw)
   static constexpr size_t hid1 = static_cast<size_t>(8) * CELLS * 16;
   static constexpr size_t we_w = static_cast<size_t>(3) * 32 * WEP * 16;
   static constexpr size_t we1 = we_w + 32 * 4;
@@ -960,7 +982,7 @@ __global__ void __launch_bounds__(1024, 1) irh_x3_kernel(IrBlockF32Args a) {
       if (v < G::WE_CH - 8) {
         const int pp = v / (32 * (CIN / 8)), r = v - pp * 32 * (CIN / 8);
         const int h = r / (CIN / 8), kc = r - h * (CIN / 8);
-        *reinterpret_cast<u32x4_t*>(wel + ((pp * 32 + h) * WEP + kc) * 16) = we_st[it];
+        *reinterpret_cast<u32x4_t*>(wel + ((pp * 32 + h) * WEP + wsw<WEP>(h, kc)) * 16) = we_st[it];
       } else {
         *reinterpret_cast<u32x4_t*>(wel + G::we_w + 16 * (v - (G::WE_CH - 8))) = we_st[it];
       }
@@ -990,7 +1012,7 @@ __global__ void __launch_bounds__(1024, 1) irh_x3_kernel(IrBlockF32Args a) {
       if (v < G::WP_CH - 80) {
         const int pp = v / (COUT * 4), r = v - pp * COUT * 4;
         const int co = r >> 2, kc = r & 3;
-        *reinterpret_cast<u32x4_t*>(wpl + ((pp * COUT + co) * 4 + (kc ^ ((co >> 2) & 3))) * 16) = wp_st[it];
+        *reinterpret_cast<u32x4_t*>(wpl + ((pp * COUT + co) * 4 + wsw<4>(co, kc)) * 16) = wp_st[it];
       } else {
         *reinterpret_cast<u32x4_t*>(wpl + G::wp_w + 16 * (v - (G::WP_CH - 80))) = wp_st[it];
       }
@@ -1043,7 +1065,7 @@ __global__ void __launch_bounds__(1024, 1) irh_x3_kernel(IrBlockF32Args a) {
 #pragma unroll
       for (int ht = 0; ht < 2; ++ht) {
         X3Frag wa;
-        const char* wr = wel + ((ht * 16 + li) * WEP + 4 * k + g) * 16;
+        const char* wr = wel + ((ht * 16 + li) * WEP + wsw<WEP>(li, 4 * k + g)) * 16;
         wa.h = *reinterpret_cast<const bf16x8_t*>(wr);
         wa.m = *reinterpret_cast<const bf16x8_t*>(wr + 32 * WEP * 16);
         wa.l = *reinterpret_cast<const bf16x8_t*>(wr + 2 * 32 * WEP * 16);
@@ -1094,7 +1116,7 @@ __global__ void __launch_bounds__(1024, 1) irh_x3_kernel(IrBlockF32Args a) {
 #pragma unroll
       for (int o = 0; o < NOW; ++o) {
         const int row = (o0 + o) * 16 + li;
-        const char* wr = wpl + (row * 4 + (g ^ ((row >> 2) & 3))) * 16;
+        const char* wr = wpl + (row * 4 + wsw<4>(row, g)) * 16;
         X3Frag wa;
         wa.h = *reinterpret_cast<const bf16x8_t*>(wr);
         wa.m = *reinterpret_cast<const bf16x8_t*>(wr + COUT * 64);

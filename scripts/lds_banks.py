@@ -1,0 +1,100 @@
+"""LDS bank model of the image-per-workgroup kernels' hot reads (csrc/kernels/irp_x3.hip).
+
+ds_read_b128 serves a wave64 in four 16-lane groups, one LDS cycle per group when the
+group's 16 addresses sit on distinct 16-byte slots of the 256-byte bank row
+(bank = (a / 4) mod 64; MI355X_MICROARCH.md section LDS); every extra distinct address on
+a slot adds a cycle.  This prints the cycles per wave-instruction (ideal 4) of:
+
+  * the MFMA A-fragment reads of the weight stages (lane (li, g): row 16 t + li, chunk
+    4 c + g) for the old odd-pitch rows and for the wsw() XOR swizzle;
+  * the depthwise window reads of irp / irpp (lane: pixel pair li of rows r0 / r0 + 1,
+    quad 2 g + qq) at hidden row pitch 16 (old) and 17 (kIrpRow);
+  * the stride-2 depthwise reads of irps and irh S = 2 (reported only).
+
+    python scripts/lds_banks.py        (asserts the swizzles are bijective and conflict-free)
+"""
+GROUPS = [[0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27],
+          [4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31]]
+GROUPS += [[lane + 32 for lane in grp] for grp in GROUPS]
+
+
+def cycles(slot_of_lane):
+    """Cycles of one ds_read_b128 whose lane l reads 16-B slot index slot_of_lane(l)."""
+    total = 0
+    for grp in GROUPS:
+        by = {}
+        for lane in grp:
+            a = slot_of_lane(lane)
+            by.setdefault(a % 16, set()).add(a)
+        total += max(len(v) for v in by.values())
+    return total
+
+
+def wsw(nch, row, ch):
+    """csrc/kernels/irp_x3.hip wsw<NCH>."""
+    if nch == 8:
+        return ch ^ (2 * ((row >> 1) & 3))
+    return ch ^ ((0x1320 >> (4 * ((row >> 2) & 3))) & 3)
+
+
+def weight_read(nch, pitch, swz, c, t=0):
+    def slot(lane):
+        li, g = lane & 15, lane >> 4
+        row = 16 * t + li
+        ch = 4 * c + g
+        return row * pitch + (wsw(nch, row, ch) if swz else ch)
+    return cycles(slot)
+
+
+def irp_dw(row_pitch, qq, dy, j):
+    quad_cells = 16 * row_pitch + 16
+
+    def slot(lane):
+        li, g = lane & 15, lane >> 4
+        real = li < 14
+        y = (1 if li >= 7 else 0) if real else 0
+        x0 = 2 * (li - 7 if li >= 7 else li) if real else 0
+        return (2 * g + qq) * quad_cells + (y + dy) * row_pitch + x0 + j
+    return cycles(slot)
+
+
+def irps_dw(qq, dy, dx, dt):
+    def slot(lane):
+        li, g = lane & 15, lane >> 4
+        q = 16 * dt + li
+        oy, ox = (q // 7, q % 7) if q < 49 else (6, 6)
+        return (2 * g + qq) * 225 + (2 * oy + dy) * 15 + 2 * ox + dx
+    return cycles(slot)
+
+
+def irh2_dw(qq, dy, dx, dt):
+    def slot(lane):
+        li, g = lane & 15, lane >> 4
+        pd = 16 * dt + li
+        r, c = (pd // 14, pd % 14) if pd < 98 else (0, 0)
+        return (2 * g + qq) * 450 + (2 * r + dy) * 30 + 2 * c + dx
+    return cycles(slot)
+
+
+def main():
+    for nch in (4, 8, 12):
+        for row in range(64):
+            assert sorted(wsw(nch, row, c) for c in range(nch)) == list(range(nch)), (nch, row)
+    print("weight A-fragment reads, cycles per ds_read_b128 (ideal 4):")
+    for nch, name in ((4, "project stages / irh expand (32 k)"), (8, "expand, cin 64"), (12, "expand, cin 96")):
+        old = [weight_read(nch, nch + 1, False, c, t) for c in range(nch // 4) for t in range(2)]
+        new = [weight_read(nch, nch, True, c, t) for c in range(nch // 4) for t in range(2)]
+        assert max(new) == 4, (nch, new)
+        print(f"  {name:36s} pitch {nch + 1} unswizzled: {sum(old) / len(old):.1f}   wsw: {sum(new) / len(new):.1f}")
+    old = [irp_dw(16, qq, dy, j) for qq in range(2) for dy in range(3) for j in range(4)]
+    new = [irp_dw(17, qq, dy, j) for qq in range(2) for dy in range(3) for j in range(4)]
+    assert max(new) == 4, new
+    print(f"irp / irpp depthwise window reads: row pitch 16: {sum(old) / len(old):.1f}   17: {sum(new) / len(new):.1f}")
+    s2 = [irps_dw(qq, dy, dx, dt) for qq in range(2) for dy in range(3) for dx in range(3) for dt in range(4)]
+    h2 = [irh2_dw(qq, dy, dx, dt) for qq in range(2) for dy in range(3) for dx in range(3) for dt in range(7)]
+    print(f"stride-2 depthwise reads (columns 2 ox + dx: one slot parity per group): irps {sum(s2) / len(s2):.1f}, "
+          f"irh S=2 {sum(h2) / len(h2):.1f}")
+
+
+if __name__ == "__main__":
+    main()
