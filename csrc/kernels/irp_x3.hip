@@ -635,12 +635,22 @@ __global__ void __launch_bounds__((IrppGeom<CIN, COUT, TPW>::NT), (IrppGeom<CIN,
 constexpr int kIrpsG = 15;                    // hidden grid (bordered): cell (y + 1, x + 1)
 constexpr int kIrpsCells = kIrpsG * kIrpsG;   // 225
 
+// First cell of hidden channel quad cq's plane in the stride-2 kernels (irps,
+// irh S = 2).  A stride-2 window read (lane: output pixel li, quads 2 g + qq)
+// reads columns 2 ox + dx, so all of a lane group's addresses have one slot
+// parity -- 16 lanes on 8 bank slots, 2-way.  Shifting plane cq by cq / 2
+// cells (g = cq / 2) puts a group's two g values on opposite parities:
+// conflict-free for irps, 8 -> 4.6 cycles for irh S = 2 (scripts/lds_banks.py).
+// The shift only grows with cq, so the planes stay disjoint: 3 cells past the
+// 8 planes.
+__device__ __forceinline__ int s2_plane(int cq, int cells) { return cq * cells + (cq >> 1); }
+
 template <int CIN, int COUT>
 struct IrpsGeom {
   static constexpr int NW = 8, NT = 64 * NW;
   static constexpr int NK32 = CIN / 32, NO16 = COUT / 16, NOH = NO16 / 2;
   static constexpr int WEP = CIN / 8;  // expand weight row pitch (16-B chunks, swizzled: wsw)
-  static constexpr size_t hid1 = static_cast<size_t>(8) * kIrpsCells * 16;
+  static constexpr size_t hid1 = static_cast<size_t>(8 * kIrpsCells + 3) * 16;  // (+3: s2_plane)
   static constexpr size_t we_w = static_cast<size_t>(3) * 32 * WEP * 16;
   static constexpr size_t we1 = we_w + 32 * 4;
   static constexpr size_t wp_w = static_cast<size_t>(3) * COUT * 4 * 16;
@@ -681,7 +691,7 @@ __global__ void __launch_bounds__(512, 2) irps_x3_kernel(IrBlockF32Args a) {
   const bool qreal = q < 49;
   const int oy = qreal ? q / 7 : 6, ox = qreal ? q - 7 * (q / 7) : 6;
 
-  for (int v = tid; v < 2 * 8 * kIrpsCells; v += NT) hbuf(0)[v] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (int v = tid; v < static_cast<int>(2 * G::hid1 / 16); v += NT) hbuf(0)[v] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int64_t wes = static_cast<int64_t>(hid) * CIN;
   const int64_t wps = static_cast<int64_t>(COUT) * hid;
@@ -801,7 +811,7 @@ __global__ void __launch_bounds__(512, 2) irps_x3_kernel(IrBlockF32Args a) {
       const f32x4_t be4 = *reinterpret_cast<const f32x4_t*>(bel + ht * 16 + 4 * g);
 #pragma unroll
       for (int t = 0; t < 2; ++t)
-        if (ecell[t] >= 0) hb[(ht * 4 + g) * kIrpsCells + ecell[t]] = relu6x4(e[ht][t] + be4);
+        if (ecell[t] >= 0) hb[s2_plane(ht * 4 + g, kIrpsCells) + ecell[t]] = relu6x4(e[ht][t] + be4);
     }
   };
 
@@ -820,7 +830,7 @@ __global__ void __launch_bounds__(512, 2) irps_x3_kernel(IrBlockF32Args a) {
     for (int qq = 0; qq < 2; ++qq) {
       const int qd = 2 * g + qq;
       f32x4_t o = *reinterpret_cast<const f32x4_t*>(wdl + 9 * 32 + 4 * qd);
-      const f32x4_t* hp = hb + qd * kIrpsCells + wcell;
+      const f32x4_t* hp = hb + s2_plane(qd, kIrpsCells) + wcell;
 #pragma unroll
       for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
@@ -915,7 +925,7 @@ struct IrhGeom {
   // windows never reach the last expand row of the top half)
   static constexpr int GH = S == 1 ? 16 : 15, CELLS = kIrhGW * GH;
   static constexpr int WEP = CIN / 8;  // expand weight row pitch (16-B chunks, swizzled: wsw)
-  static constexpr size_t hid1 = static_cast<size_t>(8) * CELLS * 16;
+  static constexpr size_t hid1 = static_cast<size_t>(8 * CELLS + (S == 2 ? 3 : 0)) * 16;  // (S = 2: s2_plane)
   static constexpr size_t we_w = static_cast<size_t>(3) * 32 * WEP * 16;
   static constexpr size_t we1 = we_w + 32 * 4;
   static constexpr size_t wp_w = static_cast<size_t>(3) * COUT * 4 * 16;
@@ -954,7 +964,10 @@ __global__ void __launch_bounds__(1024, 1) irh_x3_kernel(IrBlockF32Args a) {
   const int er0 = hh ? 13 : 0;      // first image row of the expand
   const int gro = hh ? 0 : 1;       // grid row of expand row er0
 
-  for (int v = tid; v < 2 * 8 * kIrhCells; v += NT) hbuf(0)[v] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (int v = tid; v < static_cast<int>(2 * G::hid1 / 16); v += NT) hbuf(0)[v] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // plane of channel quad cq (S = 2: shifted by cq / 2 cells, s2_plane; S = 1
+  // reads consecutive pixels, where the shift would cost: 5.9 -> 8 cycles)
+  auto plane = [](int cq) { return S == 2 ? s2_plane(cq, kIrhCells) : cq * kIrhCells; };
 
   const int64_t wes = static_cast<int64_t>(hid) * CIN;
   const int64_t wps = static_cast<int64_t>(COUT) * hid;
@@ -1080,7 +1093,7 @@ __global__ void __launch_bounds__(1024, 1) irh_x3_kernel(IrBlockF32Args a) {
       const f32x4_t be4 = *reinterpret_cast<const f32x4_t*>(bel + ht * 16 + 4 * g);
 #pragma unroll
       for (int t = 0; t < 2; ++t)
-        if (ecell[t] >= 0) hb[(ht * 4 + g) * kIrhCells + ecell[t]] = relu6x4(e[ht][t] + be4);
+        if (ecell[t] >= 0) hb[plane(ht * 4 + g) + ecell[t]] = relu6x4(e[ht][t] + be4);
     }
   };
 
@@ -1103,7 +1116,7 @@ __global__ void __launch_bounds__(1024, 1) irh_x3_kernel(IrBlockF32Args a) {
       for (int qq = 0; qq < 2; ++qq) {
         const int qd = 2 * g + qq;
         f32x4_t o = *reinterpret_cast<const f32x4_t*>(wdl + 9 * 32 + 4 * qd);
-        const f32x4_t* hp = hb + qd * kIrhCells + wcell[t];
+        const f32x4_t* hp = hb + plane(qd) + wcell[t];
 #pragma unroll
         for (int dy = 0; dy < 3; ++dy)
 #pragma unroll

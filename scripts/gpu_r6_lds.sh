@@ -11,7 +11,9 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_irp.py -q --timeout 200 --t
 tail -1 $O/irp_tests.txt
 timeout -k 10 300 python -u scripts/bench_ir_f32.py 512 > $O/layers_b512.txt 2>&1
 grep -E "H=14|H=28|TOTAL" $O/layers_b512.txt
-for spec in "14,64,384,64,1 irp_x3" "14,96,576,96,1 irpp_x3" "28,32,192,32,1 irh_x3"; do
+# PMC blocks: "H,cin,hid,cout,s kernel" pairs separated by ';' (default: the three stride-1 kernels)
+IFS=';' read -ra SPECS <<< "${PMC_SPECS:-14,64,384,64,1 irp_x3;14,96,576,96,1 irpp_x3;28,32,192,32,1 irh_x3}"
+for spec in "${SPECS[@]}"; do
   set -- $spec
   tag=$(echo "$1_$2" | tr ',' '_')
   OUT=$O/$tag SHAPE=$1 B=512 KERNEL=$2 bash scripts/pmc_f32.sh > $O/$tag.txt 2>&1

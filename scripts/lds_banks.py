@@ -9,7 +9,8 @@ a slot adds a cycle.  This prints the cycles per wave-instruction (ideal 4) of:
     4 c + g) for the old odd-pitch rows and for the wsw() XOR swizzle;
   * the depthwise window reads of irp / irpp (lane: pixel pair li of rows r0 / r0 + 1,
     quad 2 g + qq) at hidden row pitch 16 (old) and 17 (kIrpRow);
-  * the stride-2 depthwise reads of irps and irh S = 2 (reported only).
+  * the stride-2 depthwise reads of irps and irh S = 2 (columns 2 ox + dx: one slot parity
+    per lane group) with plain quad planes and with s2_plane's shift (plane cq moved by cq / 2 cells).
 
     python scripts/lds_banks.py        (asserts the swizzles are bijective and conflict-free)
 """
@@ -58,21 +59,26 @@ def irp_dw(row_pitch, qq, dy, j):
     return cycles(slot)
 
 
-def irps_dw(qq, dy, dx, dt):
+def s2_plane(cq, cells, shift):
+    """irp_x3.hip s2_plane (shift) or the plain cq * cells."""
+    return cq * cells + ((cq >> 1) if shift else 0)
+
+
+def irps_dw(qq, dy, dx, dt, shift):
     def slot(lane):
         li, g = lane & 15, lane >> 4
         q = 16 * dt + li
         oy, ox = (q // 7, q % 7) if q < 49 else (6, 6)
-        return (2 * g + qq) * 225 + (2 * oy + dy) * 15 + 2 * ox + dx
+        return s2_plane(2 * g + qq, 225, shift) + (2 * oy + dy) * 15 + 2 * ox + dx
     return cycles(slot)
 
 
-def irh2_dw(qq, dy, dx, dt):
+def irh2_dw(qq, dy, dx, dt, shift):
     def slot(lane):
         li, g = lane & 15, lane >> 4
         pd = 16 * dt + li
         r, c = (pd // 14, pd % 14) if pd < 98 else (0, 0)
-        return (2 * g + qq) * 450 + (2 * r + dy) * 30 + 2 * c + dx
+        return s2_plane(2 * g + qq, 450, shift) + (2 * r + dy) * 30 + 2 * c + dx
     return cycles(slot)
 
 
@@ -90,10 +96,17 @@ def main():
     new = [irp_dw(17, qq, dy, j) for qq in range(2) for dy in range(3) for j in range(4)]
     assert max(new) == 4, new
     print(f"irp / irpp depthwise window reads: row pitch 16: {sum(old) / len(old):.1f}   17: {sum(new) / len(new):.1f}")
-    s2 = [irps_dw(qq, dy, dx, dt) for qq in range(2) for dy in range(3) for dx in range(3) for dt in range(4)]
-    h2 = [irh2_dw(qq, dy, dx, dt) for qq in range(2) for dy in range(3) for dx in range(3) for dt in range(7)]
-    print(f"stride-2 depthwise reads (columns 2 ox + dx: one slot parity per group): irps {sum(s2) / len(s2):.1f}, "
-          f"irh S=2 {sum(h2) / len(h2):.1f}")
+    for shift in (False, True):
+        s2 = [irps_dw(qq, dy, dx, dt, shift) for qq in range(2) for dy in range(3) for dx in range(3) for dt in range(4)]
+        h2 = [irh2_dw(qq, dy, dx, dt, shift) for qq in range(2) for dy in range(3) for dx in range(3) for dt in range(7)]
+        print(f"stride-2 depthwise reads, {'planes shifted by cq / 2 (s2_plane)' if shift else 'plain planes':38s}: "
+              f"irps {sum(s2) / len(s2):.1f}, irh S=2 {sum(h2) / len(h2):.1f}")
+        if shift:
+            assert max(s2) == 4, s2
+    # the shifted planes must stay disjoint (the 15 x 15 grid's last cell holds data)
+    for cells in (225, 450):
+        for cq in range(7):
+            assert s2_plane(cq, cells, True) + cells <= s2_plane(cq + 1, cells, True)
 
 
 if __name__ == "__main__":
