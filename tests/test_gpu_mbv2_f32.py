@@ -22,7 +22,7 @@ def _close(y, ref, tol=2e-5):
 
 @pytest.mark.parametrize("M,K,N", [(1000, 16, 96), (777, 24, 144), (4096, 144, 24), (6272, 320, 1280),
                                    (128, 1280, 1000), (130, 960, 160), (64, 32, 16), (6272, 160, 960),
-                                   (6272, 960, 320)])
+                                   (6272, 960, 320), (8712, 960, 160)])
 @pytest.mark.parametrize("act,use_res", [(1, False), (0, True), (0, False)])
 def test_pw_conv_f32(nns, M, K, N, act, use_res):
     torch.manual_seed(M + K + N)
