@@ -746,6 +746,90 @@ for V in ${VARIANTS:-2 1}; do
 done
 )
 ;;
-list) echo blaslt_probe gpu_ab_variant gpu_b1_combine_ab gpu_b1_lat_ab gpu_b1_prof gpu_b1_upload_ab gpu_config_traces gpu_final_check gpu_host_argmax_ab gpu_pipe_ab gpu_pmc_early gpu_r3_hiptrace gpu_r4_b512cfg gpu_r4_cfgprof gpu_r4_configs gpu_r4_dllanes gpu_r4_dwdil gpu_r4_dwnew gpu_r4_dwsweep gpu_r4_final gpu_r4_heads gpu_r4_lanes512 gpu_r4_mbv2_ab gpu_r4_pmc gpu_r4_posehead gpu_r4_prof gpu_r4_small gpu_r4_ssd5 gpu_r4_stage gpu_r4_stem gpu_r5_final gpu_r5_pmc_early gpu_r5_pmc_gemm gpu_r6_check gpu_session stem_ab ;;
-*) echo "usage: $0 <name> [args]; names: blaslt_probe gpu_ab_variant gpu_b1_combine_ab gpu_b1_lat_ab gpu_b1_prof gpu_b1_upload_ab gpu_config_traces gpu_final_check gpu_host_argmax_ab gpu_pipe_ab gpu_pmc_early gpu_r3_hiptrace gpu_r4_b512cfg gpu_r4_cfgprof gpu_r4_configs gpu_r4_dllanes gpu_r4_dwdil gpu_r4_dwnew gpu_r4_dwsweep gpu_r4_final gpu_r4_heads gpu_r4_lanes512 gpu_r4_mbv2_ab gpu_r4_pmc gpu_r4_posehead gpu_r4_prof gpu_r4_small gpu_r4_ssd5 gpu_r4_stage gpu_r4_stem gpu_r5_final gpu_r5_pmc_early gpu_r5_pmc_gemm gpu_r6_check gpu_session stem_ab" >&2; exit 2 ;;
+gpu_r6_irw2)
+(
+# irw_f32 stride-2 tiles with per-quad hidden planes one cell apart (GSH): fp32 block numerics, per-block times at
+# batch 512, LDS counters of the 56 -> 28 and 112 -> 56 blocks, the headline bench.
+#   scripts/gpu_r6_irw2.sh [outdir]
+set -eo pipefail
+O=${1:-gpurun_out/r6irw2}
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_gpu_mbv2_f32.py tests/test_gpu_x3.py tests/test_gpu_models_f32.py -q -x --timeout 300 --timeout-method thread > $O/tests.txt 2>&1
+tail -1 $O/tests.txt
+timeout -k 10 300 python -u scripts/bench_ir_f32.py 512 > $O/layers_b512.txt 2>&1
+grep -E "H=112|H=56|TOTAL" $O/layers_b512.txt
+for spec in "56,24,144,32,2 irw_f32" "112,16,96,24,2 irw_f32"; do
+  set -- $spec
+  tag=$(echo "$1_$2" | tr ',' '_')
+  OUT=$O/$tag SHAPE=$1 B=512 KERNEL=$2 bash scripts/pmc_f32.sh > $O/$tag.txt 2>&1
+  echo "== $1 $2"; tail -2 $O/$tag.txt
+done
+timeout -k 10 400 python bench.py > $O/bench_default.json 2> $O/bench_default.err
+tail -1 $O/bench_default.json | cut -c1-300; echo
+)
+;;
+gpu_r6_midsplit)
+(
+# Split-K for mid-size GEMM grids (NNSX_GEMM_MIDSPLIT=1: 128-511 tiles in two k-slices, residual added by the reduce):
+# fp32 numerics under the switch, then each config with it off / on (DeepLab b8's 8712 x 960 -> 160 projects).
+#   scripts/gpu_r6_midsplit.sh [outdir]
+set -eo pipefail
+O=${1:-gpurun_out/r6mid}
+mkdir -p $O
+export TMPDIR=/tmp
+NNSX_GEMM_MIDSPLIT=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_mbv2_f32.py tests/test_gpu_x3.py tests/test_gpu_models_f32.py tests/test_gpu_decode_stage.py -q -x --timeout 300 --timeout-method thread > $O/tests_mid.txt 2>&1
+tail -1 $O/tests_mid.txt
+for rep in 1 2; do
+  for c in "deeplab 8" "ssd 64" "posenet 64"; do
+    set -- $c
+    for m in 0 1; do
+      NNSX_GEMM_MIDSPLIT=$m timeout -k 10 300 python bench.py --config $1 --batch $2 --steps 200 --warmup 30 --sweep "" > $O/${1}_m${m}_r${rep}.json 2> $O/${1}_m${m}_r${rep}.err
+      echo "$1 b$2 mid=$m rep $rep $(grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*' $O/${1}_m${m}_r${rep}.json | tr '\n' ' ')"
+    done
+  done
+done
+)
+;;
+gpu_r6_parts)
+(
+# Hidden-channel parts of the wave-split kernels on 128-255 tiles (NNSX_IRW_PARTS_MID=2 default / 3 / 4): DeepLab b8's 33x33
+# blocks (200 tiles, 400 workgroups at 2 parts).  Numerics under 4 parts first.
+#   scripts/gpu_r6_parts.sh [outdir]
+set -eo pipefail
+O=${1:-gpurun_out/r6parts}
+mkdir -p $O
+export TMPDIR=/tmp
+NNSX_IRW_PARTS_MID=4 timeout -k 10 600 python -u -m pytest tests/test_gpu_mbv2_f32.py tests/test_gpu_models_f32.py tests/test_gpu_decode_stage.py -q -x --timeout 300 --timeout-method thread > $O/tests_p4.txt 2>&1
+tail -1 $O/tests_p4.txt
+for rep in 1 2; do
+  for p in 2 4 3; do
+    NNSX_IRW_PARTS_MID=$p timeout -k 10 300 python bench.py --config deeplab --batch 8 --steps 200 --warmup 30 --sweep "" > $O/dl_p${p}_r${rep}.json 2> $O/dl_p${p}_r${rep}.err
+    echo "deeplab b8 parts=$p rep $rep $(grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*' $O/dl_p${p}_r${rep}.json | tr '\n' ' ')"
+  done
+done
+)
+;;
+gpu_r6_lanes)
+(
+# DeepLab b8 with its absorbed segmentation stage on 1 / 2 / 3 replay lanes (the stage writes only its output
+# frames: DecodeStage::lane_safe), byte-exact check of the lanes against the decoder's own kernels first.
+#   scripts/gpu_r6_lanes.sh [outdir]
+set -eo pipefail
+O=${1:-gpurun_out/r6lanes}
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_gpu_decode_stage.py -q --timeout 200 --timeout-method thread > $O/decode_stage.txt 2>&1
+tail -1 $O/decode_stage.txt
+for rep in 1 2; do
+  for l in 1 2 3; do
+    NNSX_TORCH_LANES=$l timeout -k 10 300 python bench.py --config deeplab --batch 8 --steps 200 --warmup 30 --sweep "" \
+      > $O/deeplab_b8_l${l}_$rep.json 2> $O/deeplab_b8_l${l}_$rep.err
+    echo "lanes $l rep $rep $(grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*' $O/deeplab_b8_l${l}_$rep.json | tr '\n' ' ')"
+  done
+done
+)
+;;
+list) echo blaslt_probe gpu_ab_variant gpu_b1_combine_ab gpu_b1_lat_ab gpu_b1_prof gpu_b1_upload_ab gpu_config_traces gpu_final_check gpu_host_argmax_ab gpu_pipe_ab gpu_pmc_early gpu_r3_hiptrace gpu_r4_b512cfg gpu_r4_cfgprof gpu_r4_configs gpu_r4_dllanes gpu_r4_dwdil gpu_r4_dwnew gpu_r4_dwsweep gpu_r4_final gpu_r4_heads gpu_r4_lanes512 gpu_r4_mbv2_ab gpu_r4_pmc gpu_r4_posehead gpu_r4_prof gpu_r4_small gpu_r4_ssd5 gpu_r4_stage gpu_r4_stem gpu_r5_final gpu_r5_pmc_early gpu_r5_pmc_gemm gpu_r6_check gpu_r6_irw2 gpu_r6_lanes gpu_r6_midsplit gpu_r6_parts gpu_session stem_ab ;;
+*) echo "usage: $0 <name> [args]; names: blaslt_probe gpu_ab_variant gpu_b1_combine_ab gpu_b1_lat_ab gpu_b1_prof gpu_b1_upload_ab gpu_config_traces gpu_final_check gpu_host_argmax_ab gpu_pipe_ab gpu_pmc_early gpu_r3_hiptrace gpu_r4_b512cfg gpu_r4_cfgprof gpu_r4_configs gpu_r4_dllanes gpu_r4_dwdil gpu_r4_dwnew gpu_r4_dwsweep gpu_r4_final gpu_r4_heads gpu_r4_lanes512 gpu_r4_mbv2_ab gpu_r4_pmc gpu_r4_posehead gpu_r4_prof gpu_r4_small gpu_r4_ssd5 gpu_r4_stage gpu_r4_stem gpu_r5_final gpu_r5_pmc_early gpu_r5_pmc_gemm gpu_r6_check gpu_r6_irw2 gpu_r6_lanes gpu_r6_midsplit gpu_r6_parts gpu_session stem_ab" >&2; exit 2 ;;
 esac
