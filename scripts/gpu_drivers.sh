@@ -750,7 +750,7 @@ gpu_r6_irw2)
 (
 # irw_f32 stride-2 tiles with per-quad hidden planes one cell apart (GSH): fp32 block numerics, per-block times at
 # batch 512, LDS counters of the 56 -> 28 and 112 -> 56 blocks, the headline bench.
-#   scripts/gpu_r6_irw2.sh [outdir]
+#   scripts/gpu_drivers.sh gpu_r6_irw2 [outdir]
 set -eo pipefail
 O=${1:-gpurun_out/r6irw2}
 mkdir -p $O
@@ -773,7 +773,7 @@ gpu_r6_midsplit)
 (
 # Split-K for mid-size GEMM grids (NNSX_GEMM_MIDSPLIT=1: 128-511 tiles in two k-slices, residual added by the reduce):
 # fp32 numerics under the switch, then each config with it off / on (DeepLab b8's 8712 x 960 -> 160 projects).
-#   scripts/gpu_r6_midsplit.sh [outdir]
+#   scripts/gpu_drivers.sh gpu_r6_midsplit [outdir]
 set -eo pipefail
 O=${1:-gpurun_out/r6mid}
 mkdir -p $O
@@ -795,7 +795,7 @@ gpu_r6_parts)
 (
 # Hidden-channel parts of the wave-split kernels on 128-255 tiles (NNSX_IRW_PARTS_MID=2 default / 3 / 4): DeepLab b8's 33x33
 # blocks (200 tiles, 400 workgroups at 2 parts).  Numerics under 4 parts first.
-#   scripts/gpu_r6_parts.sh [outdir]
+#   scripts/gpu_drivers.sh gpu_r6_parts [outdir]
 set -eo pipefail
 O=${1:-gpurun_out/r6parts}
 mkdir -p $O
@@ -814,7 +814,7 @@ gpu_r6_lanes)
 (
 # DeepLab b8 with its absorbed segmentation stage on 1 / 2 / 3 replay lanes (the stage writes only its output
 # frames: DecodeStage::lane_safe), byte-exact check of the lanes against the decoder's own kernels first.
-#   scripts/gpu_r6_lanes.sh [outdir]
+#   scripts/gpu_drivers.sh gpu_r6_lanes [outdir]
 set -eo pipefail
 O=${1:-gpurun_out/r6lanes}
 mkdir -p $O
