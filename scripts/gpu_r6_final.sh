@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-6 records in one call: GPU suite, default bench (100 + 20), the other configs at their target batches,
-# windowed headline kernel stats, per-layer split, x3 error table, lowered-engine bench.
+# windowed headline kernel stats, per-layer split (x3 defaults and native fp32), x3 error table, lowered-engine bench.
 #   scripts/gpu_r6_final.sh [outdir]
 set -eo pipefail
 cd "$(dirname "$0")/.."
@@ -26,5 +26,6 @@ echo "lowered $(grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*\|"lowered": "[
 python3 scripts/kstats.py $O/prof --window --per-step 20 > $O/kstats_window.txt
 head -4 $O/kstats_window.txt
 timeout -k 10 300 python -u scripts/bench_ir_f32.py 512 > $O/layers_b512.txt 2>&1
+NNSX_F32_MATH=fp32 timeout -k 10 300 python -u scripts/bench_ir_f32.py 512 > $O/layers_b512_native.txt 2>&1
 timeout -k 10 300 python -u scripts/x3_error_table.py --batch 512 > $O/x3_error_table.txt 2>&1
 tail -1 $O/x3_error_table.txt
