@@ -830,6 +830,21 @@ for rep in 1 2; do
 done
 )
 ;;
-list) echo blaslt_probe gpu_ab_variant gpu_b1_combine_ab gpu_b1_lat_ab gpu_b1_prof gpu_b1_upload_ab gpu_config_traces gpu_final_check gpu_host_argmax_ab gpu_pipe_ab gpu_pmc_early gpu_r3_hiptrace gpu_r4_b512cfg gpu_r4_cfgprof gpu_r4_configs gpu_r4_dllanes gpu_r4_dwdil gpu_r4_dwnew gpu_r4_dwsweep gpu_r4_final gpu_r4_heads gpu_r4_lanes512 gpu_r4_mbv2_ab gpu_r4_pmc gpu_r4_posehead gpu_r4_prof gpu_r4_small gpu_r4_ssd5 gpu_r4_stage gpu_r4_stem gpu_r5_final gpu_r5_pmc_early gpu_r5_pmc_gemm gpu_r6_check gpu_r6_irw2 gpu_r6_lanes gpu_r6_midsplit gpu_r6_parts gpu_session stem_ab ;;
-*) echo "usage: $0 <name> [args]; names: blaslt_probe gpu_ab_variant gpu_b1_combine_ab gpu_b1_lat_ab gpu_b1_prof gpu_b1_upload_ab gpu_config_traces gpu_final_check gpu_host_argmax_ab gpu_pipe_ab gpu_pmc_early gpu_r3_hiptrace gpu_r4_b512cfg gpu_r4_cfgprof gpu_r4_configs gpu_r4_dllanes gpu_r4_dwdil gpu_r4_dwnew gpu_r4_dwsweep gpu_r4_final gpu_r4_heads gpu_r4_lanes512 gpu_r4_mbv2_ab gpu_r4_pmc gpu_r4_posehead gpu_r4_prof gpu_r4_small gpu_r4_ssd5 gpu_r4_stage gpu_r4_stem gpu_r5_final gpu_r5_pmc_early gpu_r5_pmc_gemm gpu_r6_check gpu_r6_irw2 gpu_r6_lanes gpu_r6_midsplit gpu_r6_parts gpu_session stem_ab" >&2; exit 2 ;;
+gpu_r6_irw7)
+(
+# irw_x3 7 x 7 tiles with the kIrw7Px / kIrw7Dc pixel assignment: x3 numerics, per-block times, LDS counters, headline.
+set -eo pipefail
+O=gpurun_out/r6irw7; mkdir -p $O; export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_gpu_x3.py tests/test_gpu_models_f32.py tests/test_gpu_mbv2_f32.py -q -x --timeout 300 --timeout-method thread > $O/tests.txt 2>&1
+tail -1 $O/tests.txt
+timeout -k 10 300 python -u scripts/bench_ir_f32.py 512 > $O/layers_b512.txt 2>&1
+grep -E "H=7 |TOTAL" $O/layers_b512.txt
+OUT=$O/p7 SHAPE=7,160,960,160,1 B=512 KERNEL=irw_x3 bash scripts/pmc_f32.sh > $O/p7.txt 2>&1
+tail -2 $O/p7.txt
+timeout -k 10 400 python bench.py > $O/bench_default.json 2> $O/bench_default.err
+tail -1 $O/bench_default.json | cut -c1-200; echo
+)
+;;
+list) echo blaslt_probe gpu_ab_variant gpu_b1_combine_ab gpu_b1_lat_ab gpu_b1_prof gpu_b1_upload_ab gpu_config_traces gpu_final_check gpu_host_argmax_ab gpu_pipe_ab gpu_pmc_early gpu_r3_hiptrace gpu_r4_b512cfg gpu_r4_cfgprof gpu_r4_configs gpu_r4_dllanes gpu_r4_dwdil gpu_r4_dwnew gpu_r4_dwsweep gpu_r4_final gpu_r4_heads gpu_r4_lanes512 gpu_r4_mbv2_ab gpu_r4_pmc gpu_r4_posehead gpu_r4_prof gpu_r4_small gpu_r4_ssd5 gpu_r4_stage gpu_r4_stem gpu_r5_final gpu_r5_pmc_early gpu_r5_pmc_gemm gpu_r6_check gpu_r6_irw2 gpu_r6_irw7 gpu_r6_lanes gpu_r6_midsplit gpu_r6_parts gpu_session stem_ab ;;
+*) echo "usage: $0 <name> [args]; names: blaslt_probe gpu_ab_variant gpu_b1_combine_ab gpu_b1_lat_ab gpu_b1_prof gpu_b1_upload_ab gpu_config_traces gpu_final_check gpu_host_argmax_ab gpu_pipe_ab gpu_pmc_early gpu_r3_hiptrace gpu_r4_b512cfg gpu_r4_cfgprof gpu_r4_configs gpu_r4_dllanes gpu_r4_dwdil gpu_r4_dwnew gpu_r4_dwsweep gpu_r4_final gpu_r4_heads gpu_r4_lanes512 gpu_r4_mbv2_ab gpu_r4_pmc gpu_r4_posehead gpu_r4_prof gpu_r4_small gpu_r4_ssd5 gpu_r4_stage gpu_r4_stem gpu_r5_final gpu_r5_pmc_early gpu_r5_pmc_gemm gpu_r6_check gpu_r6_irw2 gpu_r6_irw7 gpu_r6_lanes gpu_r6_midsplit gpu_r6_parts gpu_session stem_ab" >&2; exit 2 ;;
 esac
