@@ -2,8 +2,10 @@
 tests/nnstreamer_{protobuf,flatbuf,flexbuf}/runTest.sh: tensors -> wire format
 -> tensors must reproduce the raw frames).  Protobuf parity is pinned against
 the Python protobuf runtime with the reference schema (nnstreamer.proto)
-built at test time; flatbuf / flexbuf parity is round-trip only (no
-flatbuffers library in this image: parity unpinned)."""
+built at test time; flatbuf against a reader / writer written from the
+FlatBuffers format rules for nnstreamer.fbs (tests/fbspec.py: no flatbuffers
+library in this image, so not flatc's exact layout); flexbuf is round-trip
+only (parity unpinned)."""
 import numpy as np
 import pytest
 
@@ -120,3 +122,51 @@ def test_malformed_input_errors(nns, mode, caps):
     msg = p.wait(20)
     p.stop()
     assert msg and msg[0] == "error"
+
+
+def test_flatbuf_bytes_read_by_spec_reader(nns):
+    """tensor_decoder mode=flatbuf output read by a FlatBuffers reader written from
+    the format rules (tests/fbspec.py), field by field against nnstreamer.fbs
+    (tensordec-flatbuf.cc:57-121 writes num_tensor, fr, tensor[name, type,
+    dimension, data], format)"""
+    from fbspec import Reader
+
+    src = "videotestsrc num-buffers=1 pattern=snow ! video/x-raw,format=RGB,width=6,height=5,framerate=5/1 ! tensor_converter"
+    raw = _collect(nns, f"{src} ! tensor_sink name=sink")[0][0]
+    blob = _collect(nns, f"{src} ! tensor_decoder mode=flatbuf ! tensor_sink name=sink")[0][0]
+    m = Reader(blob).tensors()
+    assert m["num_tensor"] == 1 and m["fr"] == (5, 1) and m["format"] == 0
+    t = m["tensor"][0]
+    assert t["type"] == 5  # NNS_UINT8
+    # NNS_TENSOR_RANK_LIMIT entries; the ranks past the caps' dimension string are 1, as
+    # gst_tensor_parse_dimension fills them (nnstreamer_plugin_api_util_impl.c:949-950)
+    assert t["dims"] == [3, 6, 5, 1, 1, 1, 1, 1]
+    assert t["data"] == bytes(raw)
+
+
+@pytest.mark.parametrize("shared_vtable", [True, False])
+def test_flatbuf_spec_writer_layouts_convert(nns, shared_vtable):
+    """tensor_converter on flatbuffers laid out unlike our encoder: vtables after
+    their tables (negative soffset) or shared by every Tensor table, inline fields
+    out of schema order, children in another order, and an unknown trailing field
+    (a newer schema's) -- every valid layout must decode to the same tensors"""
+    from fbspec import Writer
+
+    a = np.arange(12, dtype=np.float32) * 0.5
+    b = np.arange(6, dtype=np.int64) - 3
+    blob = Writer().build([dict(name="a", type=7, dims=[4, 3, 1, 1], data=a.tobytes()),
+                           dict(name="bee", type=8, dims=[6, 1, 1, 1], data=b.tobytes())],
+                          fr=(30, 1), shared_vtable=shared_vtable)
+    p = nns.parse_launch("appsrc name=src caps=other/flatbuf-tensor,framerate=30/1 ! tensor_converter "
+                         "! tensor_sink name=sink")
+    got = []
+    p.get_by_name("sink").connect("new-data", lambda buf: got.append(buf))
+    p.set_state("playing")
+    p.get_by_name("src").push_buffer(blob, pts=0)
+    p.get_by_name("src").end_of_stream()
+    assert p.wait(20)[0] == "eos", p.messages()
+    caps = str(p.get_by_name("sink").pad_caps("sink"))
+    p.stop()
+    np.testing.assert_array_equal(got[0].memory(0).numpy("float32"), a)
+    np.testing.assert_array_equal(got[0].memory(1).numpy("int64"), b)
+    assert "float32,int64" in caps and "4:3" in caps and "framerate=(fraction)30/1" in caps, caps
