@@ -4,8 +4,9 @@ tests/nnstreamer_{protobuf,flatbuf,flexbuf}/runTest.sh: tensors -> wire format
 the Python protobuf runtime with the reference schema (nnstreamer.proto)
 built at test time; flatbuf against a reader / writer written from the
 FlatBuffers format rules for nnstreamer.fbs (tests/fbspec.py: no flatbuffers
-library in this image, so not flatc's exact layout); flexbuf is round-trip
-only (parity unpinned)."""
+library in this image, so not flatc's exact layout); flexbuf likewise
+against tests/fxspec.py, whose writer uses the builder's narrowest slot
+widths."""
 import numpy as np
 import pytest
 
@@ -170,3 +171,43 @@ def test_flatbuf_spec_writer_layouts_convert(nns, shared_vtable):
     np.testing.assert_array_equal(got[0].memory(0).numpy("float32"), a)
     np.testing.assert_array_equal(got[0].memory(1).numpy("int64"), b)
     assert "float32,int64" in caps and "4:3" in caps and "framerate=(fraction)30/1" in caps, caps
+
+
+def test_flexbuf_bytes_read_by_spec_reader(nns):
+    """tensor_decoder mode=flexbuf output read by a FlexBuffers reader written from
+    the format rules (tests/fxspec.py): the map tensordec-flexbuf.cc:120-160 builds"""
+    from fxspec import Reader
+
+    src = "videotestsrc num-buffers=1 pattern=snow ! video/x-raw,format=RGB,width=6,height=5,framerate=5/1 ! tensor_converter"
+    raw = _collect(nns, f"{src} ! tensor_sink name=sink")[0][0]
+    blob = _collect(nns, f"{src} ! tensor_decoder mode=flexbuf ! tensor_sink name=sink")[0][0]
+    m = Reader(blob).root()
+    assert sorted(m) == ["format", "num_tensors", "rate_d", "rate_n", "tensor_0"]
+    assert (m["num_tensors"], m["rate_n"], m["rate_d"], m["format"]) == (1, 5, 1, 0)
+    name, typ, dims, data = m["tensor_0"]
+    assert name == "" and typ == 5 and dims == [3, 6, 5, 1, 1, 1, 1, 1] and data == bytes(raw)
+
+
+@pytest.mark.parametrize("n", [12, 40000])
+def test_flexbuf_narrow_widths_convert(nns, n):
+    """tensor_converter on FlexBuffers with the builder's narrowest slot widths
+    (1-byte maps and vectors for small tensors, wider ones past 255 / 65535) --
+    what the reference's decoder emits -- where our encoder writes 8-byte slots"""
+    from fxspec import Writer
+
+    a = np.arange(n, dtype=np.float32) * 0.25
+    b = (np.arange(6, dtype=np.int64) - 3) * 1000
+    blob = Writer().build([dict(name="a", type=7, dims=[n, 1, 1, 1, 1, 1, 1, 1], data=a.tobytes()),
+                           dict(name="b", type=8, dims=[6, 1, 1, 1, 1, 1, 1, 1], data=b.tobytes())], rate=(30, 1))
+    p = nns.parse_launch("appsrc name=src caps=other/flexbuf,framerate=30/1 ! tensor_converter ! tensor_sink name=sink")
+    got = []
+    p.get_by_name("sink").connect("new-data", lambda buf: got.append(buf))
+    p.set_state("playing")
+    p.get_by_name("src").push_buffer(blob, pts=0)
+    p.get_by_name("src").end_of_stream()
+    assert p.wait(20)[0] == "eos", p.messages()
+    caps = str(p.get_by_name("sink").pad_caps("sink"))
+    p.stop()
+    np.testing.assert_array_equal(got[0].memory(0).numpy("float32"), a)
+    np.testing.assert_array_equal(got[0].memory(1).numpy("int64"), b)
+    assert "float32,int64" in caps and "framerate=(fraction)30/1" in caps, caps
