@@ -845,6 +845,25 @@ timeout -k 10 400 python bench.py > $O/bench_default.json 2> $O/bench_default.er
 tail -1 $O/bench_default.json | cut -c1-200; echo
 )
 ;;
-list) echo blaslt_probe gpu_ab_variant gpu_b1_combine_ab gpu_b1_lat_ab gpu_b1_prof gpu_b1_upload_ab gpu_config_traces gpu_final_check gpu_host_argmax_ab gpu_pipe_ab gpu_pmc_early gpu_r3_hiptrace gpu_r4_b512cfg gpu_r4_cfgprof gpu_r4_configs gpu_r4_dllanes gpu_r4_dwdil gpu_r4_dwnew gpu_r4_dwsweep gpu_r4_final gpu_r4_heads gpu_r4_lanes512 gpu_r4_mbv2_ab gpu_r4_pmc gpu_r4_posehead gpu_r4_prof gpu_r4_small gpu_r4_ssd5 gpu_r4_stage gpu_r4_stem gpu_r5_final gpu_r5_pmc_early gpu_r5_pmc_gemm gpu_r6_check gpu_r6_irw2 gpu_r6_irw7 gpu_r6_lanes gpu_r6_midsplit gpu_r6_parts gpu_session stem_ab ;;
-*) echo "usage: $0 <name> [args]; names: blaslt_probe gpu_ab_variant gpu_b1_combine_ab gpu_b1_lat_ab gpu_b1_prof gpu_b1_upload_ab gpu_config_traces gpu_final_check gpu_host_argmax_ab gpu_pipe_ab gpu_pmc_early gpu_r3_hiptrace gpu_r4_b512cfg gpu_r4_cfgprof gpu_r4_configs gpu_r4_dllanes gpu_r4_dwdil gpu_r4_dwnew gpu_r4_dwsweep gpu_r4_final gpu_r4_heads gpu_r4_lanes512 gpu_r4_mbv2_ab gpu_r4_pmc gpu_r4_posehead gpu_r4_prof gpu_r4_small gpu_r4_ssd5 gpu_r4_stage gpu_r4_stem gpu_r5_final gpu_r5_pmc_early gpu_r5_pmc_gemm gpu_r6_check gpu_r6_irw2 gpu_r6_irw7 gpu_r6_lanes gpu_r6_midsplit gpu_r6_parts gpu_session stem_ab" >&2; exit 2 ;;
+gpu_r6_ab2)
+(
+# After the LDS layouts: irp variants per 14x14 block again (pipelined / tiles per wave), and a sustained
+# 1000-step headline with every invoke's device time (NNSX_BENCH_SERIES=1).
+set -eo pipefail
+O=${1:-gpurun_out/r6ab2}
+mkdir -p $O
+export TMPDIR=/tmp
+for v in "NNSX_NONE=1" "NNSX_IRP_PIPE=1" "NNSX_IRP_PIPE=0" "NNSX_IRP_TPW=1" "NNSX_IRP_PIPE=1 NNSX_IRP_TPW=1"; do
+  tag=$(echo "$v" | tr ' =' '__')
+  env $v NNSX_IR_ONLY=14,64,384,64,1 timeout -k 10 120 python -u scripts/bench_ir_f32.py 512 > $O/l_a_$tag.txt 2>&1
+  env $v NNSX_IR_ONLY=14,64,384,96,1 timeout -k 10 120 python -u scripts/bench_ir_f32.py 512 > $O/l_b_$tag.txt 2>&1
+  env $v NNSX_IR_ONLY=14,96,576,96,1 timeout -k 10 120 python -u scripts/bench_ir_f32.py 512 > $O/l_c_$tag.txt 2>&1
+  echo "$v | $(grep -h 'fused' $O/l_a_$tag.txt $O/l_b_$tag.txt $O/l_c_$tag.txt | awk '{print $2, $3, $4}' | tr '\n' ' ')"
+done
+NNSX_BENCH_SERIES=1 timeout -k 10 400 python bench.py --steps 1000 --warmup 20 --sweep "" --latency-frames 0 > $O/bench_1000.json 2> $O/bench_1000.err
+tail -1 $O/bench_1000.json | grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*\|"gpu_invoke_ms_median": [0-9.]*' | tr '\n' ' '; echo
+)
+;;
+list) echo blaslt_probe gpu_ab_variant gpu_b1_combine_ab gpu_b1_lat_ab gpu_b1_prof gpu_b1_upload_ab gpu_config_traces gpu_final_check gpu_host_argmax_ab gpu_pipe_ab gpu_pmc_early gpu_r3_hiptrace gpu_r4_b512cfg gpu_r4_cfgprof gpu_r4_configs gpu_r4_dllanes gpu_r4_dwdil gpu_r4_dwnew gpu_r4_dwsweep gpu_r4_final gpu_r4_heads gpu_r4_lanes512 gpu_r4_mbv2_ab gpu_r4_pmc gpu_r4_posehead gpu_r4_prof gpu_r4_small gpu_r4_ssd5 gpu_r4_stage gpu_r4_stem gpu_r5_final gpu_r5_pmc_early gpu_r5_pmc_gemm gpu_r6_ab2 gpu_r6_check gpu_r6_irw2 gpu_r6_irw7 gpu_r6_lanes gpu_r6_midsplit gpu_r6_parts gpu_session stem_ab ;;
+*) echo "usage: $0 <name> [args]; names: blaslt_probe gpu_ab_variant gpu_b1_combine_ab gpu_b1_lat_ab gpu_b1_prof gpu_b1_upload_ab gpu_config_traces gpu_final_check gpu_host_argmax_ab gpu_pipe_ab gpu_pmc_early gpu_r3_hiptrace gpu_r4_b512cfg gpu_r4_cfgprof gpu_r4_configs gpu_r4_dllanes gpu_r4_dwdil gpu_r4_dwnew gpu_r4_dwsweep gpu_r4_final gpu_r4_heads gpu_r4_lanes512 gpu_r4_mbv2_ab gpu_r4_pmc gpu_r4_posehead gpu_r4_prof gpu_r4_small gpu_r4_ssd5 gpu_r4_stage gpu_r4_stem gpu_r5_final gpu_r5_pmc_early gpu_r5_pmc_gemm gpu_r6_ab2 gpu_r6_check gpu_r6_irw2 gpu_r6_irw7 gpu_r6_lanes gpu_r6_midsplit gpu_r6_parts gpu_session stem_ab" >&2; exit 2 ;;
 esac
