@@ -632,17 +632,21 @@ class TorchInstance : public FilterInstance {
       // an instance whose static outputs no downstream element holds: the replay
       // rewrites them and hands them out as they are (no copy); they return to
       // the instance when their last reader is done
+      // every graph of this instance shares one memory pool (capture) and a
+      // copy-out instance is handed back at once: replays must not overlap, nor
+      // a replay the previous one's copy-out.  Elements sharing the instance
+      // (shared-tensor-filter-key), or invokes from another thread, bring another
+      // stream, so work on a new stream first waits for the last replay -- before
+      // the static inputs are rewritten below: issued ahead of this wait, the
+      // copy could overwrite an instance's inputs while its previous replay on
+      // the old stream had not read them yet (that frame's outputs then carried
+      // the next frame's result: test_gpu_filter_graph.py, static outputs, appsrc)
+      if (ln.last_ev && ln.last_stream != s) hip::check(hipStreamWaitEvent(s, ln.last_ev, 0), "replay order wait");
       if (!gs->in_place)
         for (size_t i = 0; i < gs->static_in.size(); ++i) gs->static_in[i].copy_(inputs[i], /*non_blocking=*/true);
       // the captured executable on the element's stream (CUDAGraph::replay would
       // first refresh RNG offsets with two fill kernels: the models here draw no
       // random numbers)
-      // every graph of this instance shares one memory pool (capture) and a
-      // copy-out instance is handed back at once: replays must not overlap, nor
-      // a replay the previous one's copy-out.  Elements sharing the instance
-      // (shared-tensor-filter-key) each bring their own stream, so a replay on a
-      // new stream first waits for the last one
-      if (ln.last_ev && ln.last_stream != s) hip::check(hipStreamWaitEvent(s, ln.last_ev, 0), "replay order wait");
       if (tw_b) hip::check(hipEventRecord(tw_b, s), "trace event");
       hip::check(hipGraphLaunch(gs->graph->raw_cuda_graph_exec(), s), "hipGraphLaunch");
       if (tw_c) {
@@ -790,6 +794,11 @@ class TorchInstance : public FilterInstance {
     hip::check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "capture event");
     hip::check(hipEventRecord(ev, s), "capture event record");  // inputs were produced on s
     hip::check(hipStreamWaitEvent(cap_stream_, ev, 0), "capture stream wait");
+    // and after the lane's last replay, wherever it ran: the warm-up and the
+    // capture allocate from the lane's graph pool, whose activations that replay
+    // may still be using (an invoke on another stream than the last one)
+    if (lanes_[static_cast<size_t>(lane)].last_ev)
+      hip::check(hipStreamWaitEvent(cap_stream_, lanes_[static_cast<size_t>(lane)].last_ev, 0), "capture order wait");
     auto gs = std::make_unique<GraphState>();
     {
       c10::hip::HIPStreamGuardMasqueradingAsCUDA cg(

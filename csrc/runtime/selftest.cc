@@ -120,10 +120,15 @@ std::string mirror_other_stream(int dev) {
   mirror.reset();
   h.reset();  // mirror released: ordered on the release stream after its recorded readers
   hipStream_t rs = hip::release_stream(dev);
+  // allocate on the release stream until the pool hands out the mirror's block
+  // (after earlier tests the pool holds other free blocks of this size, and
+  // four allocations did not always reach it: the case then passed with the
+  // fix undone), each written at once; at most 64 blocks (512 MB)
   std::vector<MemoryPtr> again;
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < 64; ++i) {
     again.push_back(Memory::alloc_device(kBytes, dev, rs));
     hip::check(hipMemsetAsync(again.back()->data(), 0x44, kBytes, rs), "selftest memset");
+    if (again.back()->data() == mp) break;
   }
   std::string r = check_bytes(d2h(out->data(), kBytes, s2), 0x33, "mirror_other_stream");
   again.clear();
@@ -149,12 +154,14 @@ std::string device_reader(int dev) {
   d->wait_ready(s2);
   hip::check(hipMemcpyAsync(out->data(), d->data(), kBytes, hipMemcpyDeviceToDevice, s2), "selftest D2D");
   d->record_use(s2, dev);
+  const void* dp = d->data();
   d.reset();
   hipStream_t rs = hip::release_stream(dev);
-  std::vector<MemoryPtr> again;
-  for (int i = 0; i < 4; ++i) {
+  std::vector<MemoryPtr> again;  // (until the released block comes back: mirror_other_stream)
+  for (int i = 0; i < 64; ++i) {
     again.push_back(Memory::alloc_device(kBytes, dev, rs));
     hip::check(hipMemsetAsync(again.back()->data(), 0x66, kBytes, rs), "selftest memset");
+    if (again.back()->data() == dp) break;
   }
   std::string r = check_bytes(d2h(out->data(), kBytes, s2), 0x55, "device_reader");
   again.clear();
