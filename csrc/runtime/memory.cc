@@ -223,7 +223,7 @@ MemoryPtr Memory::alloc_device(size_t size, int dev, hipStream_t stream) {
     m->wait_uses(rs);
     if (check_enabled() && m->size() >= 4) {
       hip::DeviceGuard g(dev);
-      (void)hipMemsetD32Async(m->data(), static_cast<int>(kPoison), m->size() / 4, rs);
+      (void)hipMemsetD32Async(m->data(), static_cast<int>(kPoisonDevice), m->size() / 4, rs);
     }
     hip::device_free(dev, m->data(), rs);
   });

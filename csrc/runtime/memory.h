@@ -124,6 +124,9 @@ class Memory : public std::enable_shared_from_this<Memory> {
   static constexpr int kMutHostFreedEarly = 1, kMutMirrorNotHeld = 2;
   static int set_test_mutation(int m);
   static constexpr uint32_t kPoison = 0x7FBADBADu;
+  // released alloc_device blocks (not pooled ones) get their own NaN pattern, so a
+  // stale read tells a released device block from a released host one
+  static constexpr uint32_t kPoisonDevice = 0x7FDE7ADEu;
   // Wait until every deferred host / pinned release queued so far has run (tests).
   static void drain_deferred();
 
