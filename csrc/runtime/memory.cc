@@ -6,6 +6,7 @@
 #include <cstring>
 #include <deque>
 #include <iterator>
+#include <set>
 #include <thread>
 
 #include "core/log.h"
@@ -44,6 +45,7 @@ class DeferredRelease {
     size_t size;
     MemPlace place;
     std::function<void()> fn;  // instead of a free: a wrapped memory's release (set_deferred_release)
+    uint64_t seq = 0;          // (queue order)
   };
   // backpressure: past this many queued blocks / bytes (the GPU has fallen
   // behind its copies) the releasing thread frees the block itself, after the
@@ -66,14 +68,15 @@ class DeferredRelease {
       return;
     }
     bytes_ += it.size;
+    it.seq = ++queued_;
+    pending_.insert(it.seq);
     q_.push_back(std::move(it));
-    ++queued_;
     cv_.notify_all();
   }
   void drain() {
     std::unique_lock<std::mutex> lk(mu_);
     const uint64_t target = queued_;
-    done_cv_.wait(lk, [&] { return done_ >= target; });
+    done_cv_.wait(lk, [&] { return pending_.empty() || *pending_.begin() > target; });
   }
   // process exit (atexit, before the HIP runtime's own teardown): the queue is
   // worked off -- bounded, the copies it waits for are already issued -- and
@@ -82,7 +85,7 @@ class DeferredRelease {
     std::unique_lock<std::mutex> lk(mu_);
     stopping_ = true;
     const uint64_t target = queued_;
-    done_cv_.wait_for(lk, std::chrono::seconds(5), [&] { return done_ >= target; });
+    done_cv_.wait_for(lk, std::chrono::seconds(5), [&] { return pending_.empty() || *pending_.begin() > target; });
   }
 
  private:
@@ -105,25 +108,47 @@ class DeferredRelease {
       hip::host_free(it.data);
   }
   void run() {
+    // Out of order: the first queued item whose events have all completed goes
+    // first, so one block read by a long job (a frame ring a slow consumer
+    // holds) does not hold back the frees queued behind it; while nothing is
+    // complete the thread polls every 50 us (only while items are pending).
     for (;;) {
       Item it;
+      bool found = false;
       {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return !q_.empty(); });
-        it = std::move(q_.front());
-        q_.pop_front();
+        for (auto i = q_.begin(); i != q_.end(); ++i) {
+          bool done = true;
+          for (auto& e : i->events)
+            if (hipEventQuery(e.second) != hipSuccess) {
+              done = false;
+              break;
+            }
+          if (done) {
+            it = std::move(*i);
+            q_.erase(i);
+            found = true;
+            break;
+          }
+        }
+        if (!found) {
+          cv_.wait_for(lk, std::chrono::microseconds(50));
+          continue;
+        }
       }
       release(it);
       std::lock_guard<std::mutex> lk(mu_);
       bytes_ -= it.size;
-      ++done_;
+      pending_.erase(it.seq);
       done_cv_.notify_all();
     }
   }
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
   std::deque<Item> q_;
-  uint64_t queued_ = 0, done_ = 0;
+  std::set<uint64_t> pending_;  // queued, not yet released (drain / shutdown)
+  uint64_t queued_ = 0;
   size_t bytes_ = 0;
   bool stopping_ = false;
 };
@@ -221,11 +246,32 @@ MemoryPtr Memory::alloc_device(size_t size, int dev, hipStream_t stream) {
     hipStream_t rs = hip::release_stream(dev);
     m->wait_ready(rs);
     m->wait_uses(rs);
-    if (check_enabled() && m->size() >= 4) {
-      hip::DeviceGuard g(dev);
+    hip::DeviceGuard g(dev);
+    if (check_enabled() && m->size() >= 4)
       (void)hipMemsetD32Async(m->data(), static_cast<int>(kPoisonDevice), m->size() / 4, rs);
+    // The pool hands a block freed on rs to an allocation on another stream
+    // before rs has reached the free (measured: a filter input's device mirror,
+    // freed on rs behind the wait for the filter's replay, came back at the same
+    // address for the next frame's mirror on the filter's stream while the wait
+    // and the poison were still pending -- profiles/r6_memcheck_mirror_open.txt;
+    // with the pool's cross-stream reuse switched off too).  So the free is
+    // issued only once rs has passed the waits: by the deferred-release thread,
+    // after an event recorded here.
+    // (NNSX_DEVICE_FREE=direct: the free straight on rs, as before -- A/B only)
+    static const bool direct = [] {
+      const char* v = std::getenv("NNSX_DEVICE_FREE");
+      return v && std::string(v) == "direct";
+    }();
+    void* p = m->data();
+    if (direct) {
+      hip::device_free(dev, p, rs);
+      return;
     }
-    hip::device_free(dev, m->data(), rs);
+    hipEvent_t e = hip::event_get(dev);
+    hip::check(hipEventRecord(e, rs), "hipEventRecord(release)");
+    DeferredRelease::get().push({{{dev, e}}, nullptr, 0, MemPlace::DEVICE, [dev, p] {
+      hip::device_free(dev, p, hip::release_stream(dev));
+    }});
   });
 }
 
@@ -744,3 +790,4 @@ std::vector<MemoryPtr> unpack_extra(const std::vector<MemoryPtr>& mems, TensorsI
 }
 
 }  // namespace nnsx
+

@@ -22,6 +22,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "kernels/kernels.h"
@@ -120,17 +121,28 @@ std::string mirror_other_stream(int dev) {
   mirror.reset();
   h.reset();  // mirror released: ordered on the release stream after its recorded readers
   hipStream_t rs = hip::release_stream(dev);
+  // device frees are issued by the deferred-release thread once their waits have
+  // passed (memory.cc alloc_device): give the mirror's free time to be issued --
+  // within microseconds when nothing holds the mirror (the fix undone), only
+  // after the reader's 20 ms spin otherwise
+  std::this_thread::sleep_for(std::chrono::milliseconds(3));
   // allocate on the release stream until the pool hands out the mirror's block
-  // (after earlier tests the pool holds other free blocks of this size, and
-  // four allocations did not always reach it: the case then passed with the
-  // fix undone), each written at once; at most 64 blocks (512 MB)
+  // (after earlier tests the pool holds other free blocks of this size), each
+  // written at once; at most 64 blocks (512 MB).  Getting the block back while
+  // the reader has not run is itself the failure.
   std::vector<MemoryPtr> again;
+  bool early = false;
   for (int i = 0; i < 64; ++i) {
     again.push_back(Memory::alloc_device(kBytes, dev, rs));
     hip::check(hipMemsetAsync(again.back()->data(), 0x44, kBytes, rs), "selftest memset");
-    if (again.back()->data() == mp) break;
+    if (again.back()->data() == mp) {
+      early = hipStreamQuery(s2) != hipSuccess;
+      break;
+    }
   }
   std::string r = check_bytes(d2h(out->data(), kBytes, s2), 0x33, "mirror_other_stream");
+  if (r.empty() && early)
+    r = "mirror_other_stream: the mirror's block was handed out again while its reader on another stream had not run";
   again.clear();
   out.reset();
   hip::check(hipDeviceSynchronize(), "selftest sync");
@@ -157,13 +169,19 @@ std::string device_reader(int dev) {
   const void* dp = d->data();
   d.reset();
   hipStream_t rs = hip::release_stream(dev);
-  std::vector<MemoryPtr> again;  // (until the released block comes back: mirror_other_stream)
+  std::this_thread::sleep_for(std::chrono::milliseconds(3));  // (as in mirror_other_stream)
+  std::vector<MemoryPtr> again;
+  bool early = false;
   for (int i = 0; i < 64; ++i) {
     again.push_back(Memory::alloc_device(kBytes, dev, rs));
     hip::check(hipMemsetAsync(again.back()->data(), 0x66, kBytes, rs), "selftest memset");
-    if (again.back()->data() == dp) break;
+    if (again.back()->data() == dp) {
+      early = hipStreamQuery(s2) != hipSuccess;
+      break;
+    }
   }
   std::string r = check_bytes(d2h(out->data(), kBytes, s2), 0x55, "device_reader");
+  if (r.empty() && early) r = "device_reader: the block was handed out again while its reader had not run";
   again.clear();
   out.reset();
   hip::check(hipDeviceSynchronize(), "selftest sync");
