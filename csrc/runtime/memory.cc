@@ -163,8 +163,15 @@ void Memory::drain_deferred() {
 // the test that pins it can be shown to fail without it
 namespace {
 std::atomic<int> g_mutation{0};
+std::atomic<const void*> g_watch{nullptr};  // test_watch_free: the block whose free is watched
+std::atomic<bool> g_watch_freed{false};
 }  // namespace
 int Memory::set_test_mutation(int m) { return g_mutation.exchange(m); }
+void Memory::test_watch_free(const void* p) {
+  g_watch_freed.store(false);
+  g_watch.store(p);
+}
+bool Memory::test_watched_freed() { return g_watch_freed.load(); }
 
 Memory::Memory(void* data, size_t size, MemPlace place, int device, Release release)
     : data_(data), size_(size), place_(place), device_(device), release_(std::move(release)) {}
@@ -271,6 +278,7 @@ MemoryPtr Memory::alloc_device(size_t size, int dev, hipStream_t stream) {
     hip::check(hipEventRecord(e, rs), "hipEventRecord(release)");
     DeferredRelease::get().push({{{dev, e}}, nullptr, 0, MemPlace::DEVICE, [dev, p] {
       hip::device_free(dev, p, hip::release_stream(dev));
+      if (p == g_watch.load()) g_watch_freed.store(true);
     }});
   });
 }

@@ -123,6 +123,9 @@ class Memory : public std::enable_shared_from_this<Memory> {
   // mirror (ee80b24 undone); returns the previous mutation
   static constexpr int kMutHostFreedEarly = 1, kMutMirrorNotHeld = 2;
   static int set_test_mutation(int m);
+  // lifetime self-tests: watch one device block's free (issued by the deferred-release thread)
+  static void test_watch_free(const void* p);
+  static bool test_watched_freed();
   static constexpr uint32_t kPoison = 0x7FBADBADu;
   // released alloc_device blocks (not pooled ones) get their own NaN pattern, so a
   // stale read tells a released device block from a released host one

@@ -103,6 +103,11 @@ std::string host_h2d(int dev, bool pinned) {
 // same size, written on the release stream, must not reach the reader
 std::string mirror_other_stream(int dev) {
   hip::DeviceGuard g(dev);
+  // start from an idle release stream and an empty deferred queue: earlier
+  // releases (other cases' 20 ms spins) queued there would delay this case's
+  // free past the reader and hide the undone fix
+  Memory::drain_deferred();
+  hip::check(hipStreamSynchronize(hip::release_stream(dev)), "selftest sync");
   hipStream_t s1 = nullptr, s2 = nullptr;
   hip::check(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking), "selftest stream");
   hip::check(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking), "selftest stream");
@@ -118,6 +123,7 @@ std::string mirror_other_stream(int dev) {
   mirror->wait_ready(s2);
   hip::check(hipMemcpyAsync(out->data(), mp, kBytes, hipMemcpyDeviceToDevice, s2), "selftest D2D");
   h->record_use(s2, dev);  // the reader holds the host memory (and, through it, the mirror)
+  Memory::test_watch_free(mp);
   mirror.reset();
   h.reset();  // mirror released: ordered on the release stream after its recorded readers
   hipStream_t rs = hip::release_stream(dev);
@@ -125,7 +131,11 @@ std::string mirror_other_stream(int dev) {
   // passed (memory.cc alloc_device): give the mirror's free time to be issued --
   // within microseconds when nothing holds the mirror (the fix undone), only
   // after the reader's 20 ms spin otherwise
-  std::this_thread::sleep_for(std::chrono::milliseconds(3));
+  std::this_thread::sleep_for(std::chrono::milliseconds(5));
+  // the free issued while the reader has not run: the failure, whichever block
+  // the pool hands out next (after other tests it may split a larger free block)
+  const bool freed_early = Memory::test_watched_freed() && hipStreamQuery(s2) != hipSuccess;
+  Memory::test_watch_free(nullptr);
   // allocate on the release stream until the pool hands out the mirror's block
   // (after earlier tests the pool holds other free blocks of this size), each
   // written at once; at most 64 blocks (512 MB).  Getting the block back while
@@ -143,6 +153,8 @@ std::string mirror_other_stream(int dev) {
   std::string r = check_bytes(d2h(out->data(), kBytes, s2), 0x33, "mirror_other_stream");
   if (r.empty() && early)
     r = "mirror_other_stream: the mirror's block was handed out again while its reader on another stream had not run";
+  if (r.empty() && freed_early)
+    r = "mirror_other_stream: the mirror's free was issued while its reader on another stream had not run";
   again.clear();
   out.reset();
   hip::check(hipDeviceSynchronize(), "selftest sync");
